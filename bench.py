@@ -1,0 +1,197 @@
+"""bench.py -- headline benchmark: point-plane inlier tests/s of the MI355X RANSAC plane path.
+
+Workload (BASELINE.json configs[2], the 10M-point cloud the metric is quoted on): per GPU a 10M-
+point synthetic cloud with 20 planes (+10 % outliers, BASELINE.md §3 generator), sequential
+extract-and-remove RANSAC: each round scores 4096 hypotheses (max_iterations 4095, probability 1.0
+-> k = inf, exactly 4096 PCL iterations) over the remaining points, refits (fast double mode),
+selects and compacts the inliers; stop after 20 planes or when a plane has < 500 inliers.
+One step = one full extraction from the pristine cloud (inputs resident in HBM).
+
+Multi-GPU (weak scaling, torchrun one process per GPU): rank r holds its own 10M-point shard of
+one global cloud (same 20 planes); every round all ranks score the same hypotheses on their
+shards with one RCCL allreduce of the int32[4096] counts.
+
+value = useful point-plane tests (PCL iterations x global active points, summed over rounds) / s,
+whole job.  Roofline: the scoring kernel k_score, VALU-bound (7 f32 VALU ops per test), timed with
+HIP events on the library's stream.  cpu_baseline: the PCL-1.8 restatement (oracle, 1 thread) on
+a bounded sample of the same workload, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "G point–plane inlier tests/sec + %HBM-roofline, 10M-pt cloud, 1/2/4/8 GPU"
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # f32 VALU lane-ops/s (no FMA): 78.6 T
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--points", type=int, default=10_000_000, help="points per GPU")
+    ap.add_argument("--planes", type=int, default=20)
+    ap.add_argument("--hyps", type=int, default=4096)
+    ap.add_argument("--threshold", type=float, default=0.02)
+    ap.add_argument("--min-inliers", type=int, default=500)
+    ap.add_argument("--refit", choices=["fast", "pcl"], default="fast")
+    ap.add_argument("--cpu-hyps", type=int, default=256, help="hypotheses in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--torch-dist", action="store_true",
+                    help="rendezvous through torch.distributed even at N=1 (runtime check)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_torch = world > 1 or a.torch_dist
+    dist = None
+    if use_torch:
+        # torch first (its HIP runtime then serves libdialog_amd.so too: one runtime per process);
+        # gloo on the CPU only carries the RCCL unique id.  The data path is RCCL inside the lib.
+        import torch.distributed as dist  # noqa: F811
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    import dialog_amd as D
+    from dialog_amd.synth import SEED_BASE, plane_cloud
+
+    if world > 1:
+        uid = D.Context.unique_id() if rank == 0 else None
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        ctx = D.Context.distributed(local, rank, world, box[0])
+    else:
+        ctx = D.Context(local)
+    ctx.set_profiling(True)
+
+    seed = SEED_BASE + 3
+    t0 = time.time()
+    pts, _, _ = plane_cloud(a.points, a.planes, seed=seed, shard=rank)
+    gen_s = time.time() - t0
+    cloud = D.Cloud(ctx, pts, id_base=rank * a.points)
+    prm = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
+                        refit_mode=D.DLG_REFIT_FAST if a.refit == "fast" else D.DLG_REFIT_PCL,
+                        hypotheses_per_launch=a.hyps, gather_inliers=False)
+
+    def step():
+        cloud.reset()
+        return D.extract_planes(cloud, prm, max_planes=a.planes, min_inliers=a.min_inliers,
+                                capacity=a.points)
+
+    for _ in range(a.warmup):
+        step()
+    ctx.barrier()
+    ctx.synchronize()
+    tests = scored = launches = 0
+    score_ms = select_ms = 0.0
+    planes = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        e = step()
+        s = e["stats"]
+        tests += s["tests"]
+        scored += s["tests_scored"]
+        launches += s["score_launches"]
+        score_ms += s["score_ms"]
+        select_ms += s["select_ms"]
+        planes.append(e["n_planes"])
+    ctx.synchronize()
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = ctx.allreduce_max(elapsed)
+    score_ms_max = ctx.allreduce_max(score_ms)
+
+    value = tests / elapsed / 1e9  # G tests/s, whole job (tests counted over the global cloud)
+    ms_per_step = elapsed / a.steps * 1e3
+    # dominant kernel: k_score (this rank's launches; tests per rank = scored / world)
+    per_rank_tests = scored / world
+    avg_launch_ms = score_ms / max(launches, 1)
+    ktests_per_s = per_rank_tests / (score_ms / 1e3) if score_ms > 0 else 0.0
+    achieved = 7.0 * ktests_per_s / 1e12
+    roofline = {
+        "kernel": "k_score (countWithinDistance, 4096 hypotheses/launch)",
+        "bound": "valu",
+        "achieved": round(achieved, 3),
+        "peak": round(VALU_PEAK_TOPS, 2),
+        "unit": "TFLOP/s",
+        "frac": round(achieved / VALU_PEAK_TOPS, 4),
+        "traffic": None,
+        "avg_launch_ms": round(avg_launch_ms, 4),
+        "launches": launches,
+        "tests_per_s_in_kernel": ktests_per_s,
+        "ops_per_test": 7,
+        "hbm_view": {"algorithmic_GBps": round(12.0 * (per_rank_tests / max(a.hyps, 1)) /
+                                              (score_ms / 1e3) / 1e9, 2) if score_ms else None,
+                     "peak_GBps": HBM_PEAK_GBS},
+        "note": "1 op = one f32 VALU lane-op (3 mul + 3 add + 1 cmp per test, no FMA for PCL "
+                "bit-parity); peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz",
+    }
+    traffic_file = os.path.join(ROOT, "profiles", "score_traffic.json")
+    if os.path.exists(traffic_file):
+        try:
+            tj = json.load(open(traffic_file))
+            roofline["traffic"] = tj.get("hbm_bytes_per_launch")
+            roofline["traffic_source"] = tj.get("source")
+        except Exception:
+            pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O
+        t0 = time.perf_counter()
+        r = O.sac_segment(pts, a.threshold, max_iterations=a.cpu_hyps - 1, probability=1.0)
+        cdt = time.perf_counter() - t0
+        cpu = {"value": round(r["iterations"] * pts.shape[0] / cdt / 1e9, 4),
+               "unit": "G point-plane tests/s", "cores": 1, "kind": "port",
+               "sample": f"one PCL SACSegmentation::segment (first extraction round) on the same "
+                         f"{pts.shape[0]}-pt cloud with {a.cpu_hyps} hypotheses + refit + select, "
+                         f"oracle/pcl_oracle.c single thread, {cdt:.1f} s",
+               "host_cpu": platform.processor() or platform.machine(),
+               "host_nproc": os.cpu_count()}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "G point-plane tests/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "C3: sequential extract-and-remove RANSAC, 10M-pt 20-plane "
+                                   "synthetic cloud per GPU (BASELINE.json configs[2]; C4 shape "
+                                   "when N>1: shards of one cloud, RCCL allreduce of counts)",
+                       "points_per_gpu": a.points, "global_points": a.points * world,
+                       "planes": a.planes, "hypotheses_per_round": a.hyps,
+                       "threshold": a.threshold, "min_inliers": a.min_inliers,
+                       "refit": a.refit, "planes_extracted": planes[-1] if planes else 0,
+                       "parallelism": f"point-sharded x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "tests_per_step": tests // max(a.steps, 1),
+            "tests_scored_per_step": scored // max(a.steps, 1),
+            "score_ms_per_step_max_rank": round(score_ms_max / a.steps, 3),
+            "select_ms_per_step": round(select_ms / a.steps, 3),
+            "gen_s": round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    cloud.close()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

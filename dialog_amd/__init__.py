@@ -1,0 +1,14 @@
+"""dialog_amd -- MI355X-native RANSAC plane segmentation for the czh55/Dialog plane stage.
+
+The product path is libdialog_amd.so (hand-written gfx950 HIP kernels + C++ host driver behind the
+C ABI in include/dialog_ransac.h).  This package holds the ctypes binding, a Python mirror of
+PCL's SACSegmentation interface, the synthetic-cloud generator and PCD I/O.  There is no CPU
+fallback: without the library or a gfx950 device every compute call raises.
+"""
+from .sac import (SAC_RANSAC, SACMODEL_NORMAL_PLANE, SACMODEL_PLANE, Cloud, Context,  # noqa: F401
+                  DialogError, SACSegmentation, extract_planes, make_params, segment_cloud)
+from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, LIB_PATH  # noqa: F401
+
+__all__ = ["Context", "Cloud", "SACSegmentation", "extract_planes", "segment_cloud", "make_params",
+           "SACMODEL_PLANE", "SACMODEL_NORMAL_PLANE", "SAC_RANSAC", "DLG_REFIT_PCL",
+           "DLG_REFIT_FAST", "DialogError", "LIB_PATH"]

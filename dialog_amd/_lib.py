@@ -1,0 +1,117 @@
+"""ctypes binding of include/dialog_ransac.h (libdialog_amd.so, built in-tree for gfx950).
+
+No fallback: if the library is missing or no gfx950 device is visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdialog_amd.so")
+
+DLG_OK = 0
+DLG_ERR_CAPACITY = 5
+DLG_SACMODEL_PLANE = 0
+DLG_SACMODEL_NORMAL_PLANE = 11
+DLG_REFIT_PCL = 0
+DLG_REFIT_FAST = 1
+
+SYMBOLS = [
+    "dlg_abi_version", "dlg_status_string", "dlg_sac_params_default", "dlg_ctx_create",
+    "dlg_get_unique_id", "dlg_ctx_create_dist", "dlg_ctx_create_loopback_group", "dlg_ctx_destroy",
+    "dlg_last_error", "dlg_ctx_info", "dlg_cloud_upload", "dlg_cloud_destroy", "dlg_cloud_reset",
+    "dlg_cloud_active", "dlg_sac_segment", "dlg_sac_segment_host", "dlg_extract_planes",
+    "dlg_set_profiling", "dlg_synchronize", "dlg_allreduce_max_f64", "dlg_barrier",
+]
+
+
+class Points(C.Structure):
+    _fields_ = [("xyz", C.POINTER(C.c_float)), ("n", C.c_int64), ("stride_bytes", C.c_int64)]
+
+
+class SacParams(C.Structure):
+    _fields_ = [("threshold", C.c_double), ("max_iterations", C.c_int), ("probability", C.c_double),
+                ("optimize", C.c_int), ("seed", C.c_uint32), ("model", C.c_int),
+                ("normal_distance_weight", C.c_double), ("refit_mode", C.c_int),
+                ("hypotheses_per_launch", C.c_int), ("gather_inliers", C.c_int)]
+
+
+class SacStats(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("skipped", C.c_int), ("has_model", C.c_int),
+                ("launches", C.c_int), ("draws", C.c_int64), ("best_sample", C.c_int32 * 3),
+                ("coeff_unrefined", C.c_float * 4), ("n_unrefined", C.c_int64),
+                ("n_active", C.c_int64), ("tests", C.c_int64), ("tests_scored", C.c_int64),
+                ("score_ms", C.c_double)]
+
+
+class ExtractStats(C.Structure):
+    _fields_ = [("rounds", C.c_int), ("tests", C.c_int64), ("tests_scored", C.c_int64),
+                ("score_launches", C.c_int), ("score_ms", C.c_double), ("select_ms", C.c_double),
+                ("wall_ms", C.c_double)]
+
+
+_lib = None
+
+
+def load():
+    """Load libdialog_amd.so (building it first if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        from . import build as _b
+        _b.build()
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    pp = C.POINTER(C.c_void_p)
+    i32p = C.POINTER(C.c_int32)
+    i64p = C.POINTER(C.c_int64)
+    fp = C.POINTER(C.c_float)
+    L.dlg_abi_version.restype = C.c_int
+    L.dlg_status_string.restype = C.c_char_p
+    L.dlg_status_string.argtypes = [C.c_int]
+    L.dlg_sac_params_default.argtypes = [C.POINTER(SacParams)]
+    L.dlg_sac_params_default.restype = None
+    L.dlg_ctx_create.argtypes = [pp, C.c_int]
+    L.dlg_get_unique_id.argtypes = [vp]
+    L.dlg_ctx_create_dist.argtypes = [pp, C.c_int, C.c_int, C.c_int, vp]
+    L.dlg_ctx_create_loopback_group.argtypes = [pp, C.c_int, C.c_int]
+    L.dlg_ctx_destroy.argtypes = [vp]
+    L.dlg_last_error.argtypes = [vp]
+    L.dlg_last_error.restype = C.c_char_p
+    L.dlg_ctx_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.dlg_cloud_upload.argtypes = [vp, C.POINTER(Points), i32p, C.c_int64, C.c_int32, pp]
+    L.dlg_cloud_destroy.argtypes = [vp]
+    L.dlg_cloud_reset.argtypes = [vp]
+    L.dlg_cloud_active.argtypes = [vp, i64p]
+    L.dlg_sac_segment.argtypes = [vp, vp, C.POINTER(SacParams), fp, i32p, C.c_int64, i64p,
+                                  C.POINTER(SacStats)]
+    L.dlg_sac_segment_host.argtypes = [vp, C.POINTER(Points), i32p, C.c_int64,
+                                       C.POINTER(SacParams), fp, i32p, C.c_int64, i64p,
+                                       C.POINTER(SacStats)]
+    L.dlg_extract_planes.argtypes = [vp, vp, C.POINTER(SacParams), C.c_int, C.c_int64, fp, i64p,
+                                     i32p, C.c_int64, C.POINTER(C.c_int), C.POINTER(ExtractStats)]
+    L.dlg_set_profiling.argtypes = [vp, C.c_int]
+    L.dlg_synchronize.argtypes = [vp]
+    L.dlg_allreduce_max_f64.argtypes = [vp, C.POINTER(C.c_double)]
+    L.dlg_barrier.argtypes = [vp]
+    for s in SYMBOLS:
+        if s not in ("dlg_abi_version", "dlg_status_string", "dlg_sac_params_default",
+                     "dlg_last_error"):
+            getattr(L, s).restype = C.c_int
+    _lib = L
+    return L
+
+
+class DialogError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"dialog_amd error {status}: {msg}")
+        self.status = status
+
+
+def check(status, ctx=None):
+    if status != DLG_OK:
+        L = load()
+        detail = L.dlg_last_error(ctx).decode(errors="replace")
+        raise DialogError(status, f"{L.dlg_status_string(status).decode()}: {detail}")

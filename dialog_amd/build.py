@@ -1,0 +1,57 @@
+"""Build the in-tree HIP library dialog_amd/libdialog_amd.so for gfx950 (hipcc, no cmake).
+
+Flags that matter for parity with PCL: -ffp-contract=off (no fused multiply-adds except the explicit
+ones), -fhip-fp32-correctly-rounded-divide-sqrt (IEEE f32 / and sqrt), -fno-slp-vectorize (keeps
+the scoring loop in single-issue f32 ops instead of v_pk_* pairs).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libdialog_amd.so")
+SOURCES = ["kernels.hip", "comm.cpp", "driver.cpp"]
+HEADERS = ["kernels.hpp", "comm.hpp", "host_math.hpp"]
+ARCH = os.environ.get("DLG_OFFLOAD_ARCH", "gfx950")
+
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
+            "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps.append(os.path.join(HERE, "..", "include", "dialog_ransac.h"))
+    deps.append(os.path.abspath(__file__))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", *CXXFLAGS, "-shared",
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp", "-ldl", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,830 @@
+// driver.cpp -- host driver of the MI355X RANSAC plane path and its C ABI (include/dialog_ransac.h).
+//
+// One RANSAC segment() (PCL 1.8 SACSegmentation<PointXYZ>::segment, SACMODEL_PLANE, SAC_RANSAC;
+// reference call pattern Dialog/SimplifyVerticesSize.cpp:62-67) runs as:
+//
+//   host   : replay SampleConsensusModel::drawIndexSample over list *positions* for a batch of D
+//            draws (mt19937(seed) >> 1, swaps kept in a sparse overlay of the shuffled list; the
+//            positions do not depend on the data, only on N_active)
+//   device : k_gather_samples (positions -> points, per shard) [+ allreduce over ranks]
+//            k_build_hyps     (isSampleGood + computeModelCoefficients, PCL op order)
+//            k_score          (countWithinDistance for all D draws)    [+ allreduce of counts]
+//   host   : replay RandomSampleConsensus::computeModel over the D counts in draw order
+//            (strict '>' keeps the first best, k = log(1-p)/log(1-w^3), iteration cap, 1000-bad-
+//            draw getSamples limit); next batch only if the loop has not terminated
+//   device : refit (PCL float parity mode on the host from the gathered inlier xyz, or fast
+//            double moments on the device) and the final selectWithinDistance, which in
+//            extract-and-remove mode also compacts the survivors into the ping-pong buffers.
+//
+// The data-independent part of getSamples (which list positions are swapped) is what lets the
+// whole hypothesis batch be scored in one launch while still reproducing PCL's sequential RNG
+// use bit-for-bit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/dialog_ransac.h"
+#include "comm.hpp"
+#include "host_math.hpp"
+#include "kernels.hpp"
+
+namespace dlg {
+
+struct DlgError : std::runtime_error {
+  DlgError(dlg_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+  dlg_status code;
+};
+
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      throw DlgError(DLG_ERR_HIP, std::string(#expr) + " -> " + hipGetErrorString(e_));       \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 16);
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T)));
+    cap = want;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+template <typename T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) HIPCHK(hipHostFree(p));
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 16);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault));
+    cap = want;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// sparse overlay of SampleConsensusModel::shuffled_indices_ over list positions: pos -> pos'
+class Overlay {
+ public:
+  void reset(size_t expect) {
+    size_t cap = 64;
+    while (cap < expect * 2) cap <<= 1;
+    keys_.assign(cap, -1);
+    vals_.assign(cap, 0);
+    mask_ = cap - 1;
+    size_ = 0;
+  }
+  int32_t get(int32_t k) const {
+    size_t h = hash(k) & mask_;
+    while (keys_[h] != -1) {
+      if (keys_[h] == k) return vals_[h];
+      h = (h + 1) & mask_;
+    }
+    return k;
+  }
+  void set(int32_t k, int32_t v) {
+    if ((size_ + 1) * 2 > keys_.size()) grow();
+    size_t h = hash(k) & mask_;
+    while (keys_[h] != -1 && keys_[h] != k) h = (h + 1) & mask_;
+    if (keys_[h] == -1) {
+      keys_[h] = k;
+      ++size_;
+    }
+    vals_[h] = v;
+  }
+  void swap_pos(int32_t i, int32_t j) {
+    if (i == j) return;
+    int32_t vi = get(i), vj = get(j);
+    set(i, vj);
+    set(j, vi);
+  }
+
+ private:
+  static size_t hash(int32_t k) { return (size_t)((uint32_t)k * 2654435761u); }
+  void grow() {
+    std::vector<int32_t> ok = std::move(keys_), ov = std::move(vals_);
+    keys_.assign(ok.size() * 2, -1);
+    vals_.assign(ok.size() * 2, 0);
+    mask_ = keys_.size() - 1;
+    size_ = 0;
+    for (size_t t = 0; t < ok.size(); ++t)
+      if (ok[t] != -1) set(ok[t], ov[t]);
+  }
+  std::vector<int32_t> keys_, vals_;
+  size_t mask_ = 0, size_ = 0;
+};
+
+struct SoA {
+  DevBuf<float> x, y, z;
+  DevBuf<int32_t> gid;
+  void ensure(size_t n) { x.ensure(n); y.ensure(n); z.ensure(n); gid.ensure(n); }
+  void release() { x.release(); y.release(); z.release(); gid.release(); }
+  PointsView view(int64_t n) const { return PointsView{x.p, y.p, z.p, gid.p, n}; }
+  PointsOut out() { return PointsOut{x.p, y.p, z.p, gid.p}; }
+};
+
+}  // namespace dlg
+
+using namespace dlg;
+
+struct dlg_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  std::unique_ptr<Comm> comm;
+  std::string err;
+  bool profiling = false;
+  // scratch
+  DevBuf<int32_t> pos;
+  DevBuf<SampleRec> samples;
+  DevBuf<HypRec> hyps;
+  DevBuf<int32_t> res;  // counts[D] | good[D]
+  DevBuf<int32_t> tile_in, tile_off_in, tile_off_out, totals;
+  DevBuf<double> partials, moments;
+  DevBuf<int32_t> inl_gid;
+  DevBuf<float> inl_xyz;
+  DevBuf<int64_t> gath64;
+  DevBuf<int32_t> gath32;
+  PinBuf<int32_t> h_pos, h_res, h_tot;
+  PinBuf<double> h_mom;
+  PinBuf<int64_t> h_g64;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<int32_t> h_inl;
+  std::vector<float> h_xyz;
+};
+
+struct dlg_cloud {
+  dlg_ctx* ctx = nullptr;
+  int64_t n_total = 0;
+  int64_t n_active = 0;
+  int cur = -1;  // -1 pristine, 0 = A, 1 = B
+  SoA pristine, buf[2];
+  float amax[3] = {0, 0, 0};
+  PointsView view() const {
+    const SoA& s = cur < 0 ? pristine : buf[cur];
+    return s.view(n_active);
+  }
+  int spare() const { return cur == 0 ? 1 : 0; }
+};
+
+namespace {
+
+void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
+
+void sync(dlg_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); }
+
+int64_t allgather_i64(dlg_ctx* c, int64_t v, std::vector<int64_t>* all) {
+  const int W = c->comm->world();
+  all->assign(W, 0);
+  if (W == 1) {
+    (*all)[0] = v;
+    return v;
+  }
+  c->gath64.ensure(W + 1);
+  c->h_g64.ensure(W + 1);
+  c->h_g64.p[0] = v;
+  HIPCHK(hipMemcpyAsync(c->gath64.p + W, c->h_g64.p, 8, hipMemcpyHostToDevice, c->stream));
+  c->comm->allgather(c->gath64.p + W, c->gath64.p, 1, DType::I64, c->stream);
+  HIPCHK(hipMemcpyAsync(c->h_g64.p, c->gath64.p, 8 * W, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  int64_t s = 0;
+  for (int r = 0; r < W; ++r) {
+    (*all)[r] = c->h_g64.p[r];
+    s += c->h_g64.p[r];
+  }
+  return s;
+}
+
+// gather every rank's device list (count_r items of `width` int32 each) into host `out`, rank order
+void gather_lists(dlg_ctx* c, const int32_t* dev_local, int64_t n_local, int width,
+                  std::vector<int32_t>* out) {
+  const int W = c->comm->world();
+  std::vector<int64_t> cnt;
+  int64_t total = allgather_i64(c, n_local, &cnt);
+  out->resize((size_t)(total * width));
+  if (W == 1) {
+    if (total)
+      HIPCHK(hipMemcpyAsync(out->data(), dev_local, (size_t)total * width * 4, hipMemcpyDeviceToHost,
+                            c->stream));
+    sync(c);
+    return;
+  }
+  int64_t mx = *std::max_element(cnt.begin(), cnt.end());
+  if (mx == 0) return;
+  const size_t per = (size_t)mx * width;
+  c->gath32.ensure(per * (W + 1));
+  int32_t* send = c->gath32.p + per * W;
+  if (n_local)
+    HIPCHK(hipMemcpyAsync(send, dev_local, (size_t)n_local * width * 4, hipMemcpyDeviceToDevice,
+                          c->stream));
+  c->comm->allgather(send, c->gath32.p, per, DType::I32, c->stream);
+  std::vector<int32_t> tmp(per * W);
+  HIPCHK(hipMemcpyAsync(tmp.data(), c->gath32.p, per * W * 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  size_t w = 0;
+  for (int r = 0; r < W; ++r) {
+    std::memcpy(out->data() + w, tmp.data() + per * r, (size_t)cnt[r] * width * 4);
+    w += (size_t)cnt[r] * width;
+  }
+}
+
+float event_ms(dlg_ctx* c, int a, int b) {
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev[a], c->ev[b]));
+  return ms;
+}
+
+struct SegOut {
+  bool has_model = false;
+  float coeff[4] = {0, 0, 0, 0};
+  int64_t n_in_local = 0;   // refined inliers on this rank (ids in ctx->inl_gid)
+  int64_t n_out_local = 0;  // survivors on this rank (compacted into the spare buffer if remove)
+  int64_t n_in_global = 0;
+};
+
+// one SACSegmentation::segment() over the cloud's active list (all ranks)
+SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool compact,
+                    dlg_sac_stats* st, dlg_extract_stats* xs) {
+  SegOut out;
+  std::memset(st, 0, sizeof(*st));
+  if (prm.model != DLG_SACMODEL_PLANE)
+    throw DlgError(DLG_ERR_INVALID, "only SACMODEL_PLANE is implemented");
+  if (!(prm.threshold == prm.threshold)) throw DlgError(DLG_ERR_INVALID, "threshold is NaN");
+  const int cap_h = prm.hypotheses_per_launch > 0
+                        ? std::min(prm.hypotheses_per_launch, kMaxHypPerLaunch)
+                        : kMaxHypPerLaunch;
+  std::vector<int64_t> per_rank;
+  const int64_t N = allgather_i64(c, cl->n_active, &per_rank);
+  int64_t offset = 0;
+  for (int r = 0; r < c->comm->rank(); ++r) offset += per_rank[r];
+  st->n_active = N;
+  if (N > INT32_MAX) throw DlgError(DLG_ERR_INVALID, "more than 2^31-1 active points");
+  if (prm.threshold == DBL_MAX) return out;  // PCL: "No threshold set!" -> computeModel false
+  if (N < 3) return out;                      // getSamples: cannot select 3 unique points
+
+  const PointsView src = cl->view();
+  const float cthr = thr_ceil(prm.threshold);
+  Mt19937 rng(prm.seed);
+  Overlay ov;
+  ov.reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h) + 16);
+
+  // RandomSampleConsensus::computeModel state
+  int iterations = 0;
+  int best = -INT_MAX;
+  double k = 1.0;
+  const double log_probability = std::log(1.0 - prm.probability);
+  const double one_over_indices = 1.0 / (double)N;
+  int consec_bad = 0;
+  bool done = false, have = false;
+  HypRec best_h{};
+  SampleRec best_s[3]{};
+  int launches = 0;
+
+  while (!done) {
+    // batch size: the hypotheses PCL can still evaluate (+ a little slack for bad draws)
+    // (first batch: k is still 1.0 -- size it by the iteration cap; PCL's k is only known once
+    // the first hypothesis has been counted)
+    int64_t remaining = (int64_t)prm.max_iterations + 1 - iterations;
+    if (have && std::isfinite(k) && k < 1e18)
+      remaining = std::min<int64_t>(remaining, (int64_t)std::ceil(k) - iterations);
+    remaining = std::max<int64_t>(remaining, 1);
+    const int D = (int)std::min<int64_t>(cap_h, remaining + (iterations ? 8 : 0));
+
+    // ---- host: drawIndexSample over positions
+    c->h_pos.ensure(3 * (size_t)D);
+    int32_t* hp = c->h_pos.p;
+    for (int d = 0; d < D; ++d) {
+      for (int i = 0; i < 3; ++i) {
+        int64_t j = i + (int64_t)((uint64_t)(uint32_t)rng.rnd() % (uint64_t)(N - i));
+        ov.swap_pos(i, (int32_t)j);
+      }
+      hp[3 * d] = ov.get(0);
+      hp[3 * d + 1] = ov.get(1);
+      hp[3 * d + 2] = ov.get(2);
+    }
+    // ---- device: gather, build, score
+    c->pos.ensure(3 * (size_t)D);
+    c->samples.ensure(3 * (size_t)D);
+    c->hyps.ensure(D);
+    c->res.ensure(2 * (size_t)D);
+    HIPCHK(hipMemcpyAsync(c->pos.p, hp, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
+    launch_gather_samples(c->pos.p, 3 * D, offset, src, c->samples.p, c->stream);
+    if (c->comm->world() > 1) c->comm->allreduce_sum(c->samples.p, 12 * (size_t)D, DType::I32, c->stream);
+    launch_build_hyps(c->samples.p, D, cthr, cl->amax[0], cl->amax[1], cl->amax[2], c->hyps.p,
+                      c->res.p + D, c->stream);
+    HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)D, c->stream));
+    if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    launch_score(src, c->hyps.p, D, cthr, c->res.p, kScoreExact, c->num_cus, c->stream);
+    HIPCHK(hipGetLastError());
+    if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
+    c->h_res.ensure(2 * (size_t)D);
+    HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 8 * (size_t)D, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    ++launches;
+    st->tests_scored += (int64_t)D * N;
+    if (c->profiling) st->score_ms += event_ms(c, 0, 1);
+
+    // ---- host: computeModel replay over the batch
+    const int32_t* cnt = c->h_res.p;
+    const int32_t* good = c->h_res.p + D;
+    int best_d = -1;
+    for (int d = 0; d < D && !done; ++d) {
+      st->draws++;
+      if (!good[d]) {
+        if (++consec_bad >= 1000) done = true;  // getSamples: no valid sample in 1000 tries
+        continue;
+      }
+      consec_bad = 0;
+      const int n = cnt[d];
+      if (n > best) {
+        best = n;
+        best_d = d;
+        have = true;
+        const double w = (double)best * one_over_indices;
+        double p_no_outliers = 1.0 - std::pow(w, 3.0);
+        p_no_outliers = std::max(std::numeric_limits<double>::epsilon(), p_no_outliers);
+        p_no_outliers = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no_outliers);
+        k = log_probability / std::log(p_no_outliers);
+      }
+      ++iterations;
+      st->tests += N;
+      if (iterations > prm.max_iterations) done = true;
+      else if (!(iterations < k)) done = true;
+    }
+    if (best_d >= 0) {
+      HIPCHK(hipMemcpyAsync(&best_h, c->hyps.p + best_d, sizeof(HypRec), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(best_s, c->samples.p + 3 * best_d, 3 * sizeof(SampleRec),
+                            hipMemcpyDeviceToHost, c->stream));
+      sync(c);
+    }
+  }
+  st->iterations = iterations;
+  st->launches = launches;
+  if (xs) {
+    xs->tests += st->tests;
+    xs->tests_scored += st->tests_scored;
+    xs->score_launches += launches;
+    xs->score_ms += st->score_ms;
+  }
+  if (!have) return out;
+
+  st->has_model = 1;
+  st->n_unrefined = best;
+  const float bc[4] = {best_h.a, best_h.b, best_h.c, best_h.d};
+  std::memcpy(st->coeff_unrefined, bc, sizeof(bc));
+  for (int i = 0; i < 3; ++i) st->best_sample[i] = best_s[i].gid;
+
+  const int nt = select_tiles(src.n);
+  c->tile_in.ensure(nt + 1);
+  c->tile_off_in.ensure(nt + 1);
+  c->tile_off_out.ensure(nt + 1);
+  c->totals.ensure(2);
+  c->h_tot.ensure(2);
+  c->inl_gid.ensure((size_t)std::max<int64_t>(src.n, 1));
+  float rc[4];
+  if (c->profiling) HIPCHK(hipEventRecord(c->ev[2], c->stream));
+  if (!prm.optimize) {
+    std::memcpy(rc, bc, sizeof(rc));
+  } else if (prm.refit_mode == DLG_REFIT_FAST) {
+    const int nb = moments_blocks(src.n);
+    c->partials.ensure((size_t)nb * kMomentK);
+    c->moments.ensure(kMomentK);
+    c->h_mom.ensure(kMomentK);
+    const double shift[3] = {best_s[0].x, best_s[0].y, best_s[0].z};
+    launch_moments(src, make_float4(bc[0], bc[1], bc[2], bc[3]), cthr,
+                   make_double3(shift[0], shift[1], shift[2]), c->partials.p, nb, c->moments.p,
+                   c->stream);
+    if (c->comm->world() > 1) c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
+    HIPCHK(hipMemcpyAsync(c->h_mom.p, c->moments.p, kMomentK * 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    refit_from_moments(c->h_mom.p, shift, bc, rc);
+  } else {
+    // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
+    c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
+    launch_select(src, make_float4(bc[0], bc[1], bc[2], bc[3]), cthr, c->tile_in.p, c->tile_off_in.p,
+                  c->tile_off_out.p, c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
+    HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    std::vector<int32_t> xyz_bits;
+    gather_lists(c, reinterpret_cast<const int32_t*>(c->inl_xyz.p), c->h_tot.p[0], 3, &xyz_bits);
+    refit_pcl_float(reinterpret_cast<const float*>(xyz_bits.data()), (int64_t)xyz_bits.size() / 3,
+                    bc, rc);
+  }
+  std::memcpy(out.coeff, rc, sizeof(rc));
+  out.has_model = true;
+
+  // final selectWithinDistance with the refined model (+ compaction of the survivors)
+  PointsOut dst{};
+  if (compact) {
+    SoA& sp = cl->buf[cl->spare()];
+    sp.ensure((size_t)std::max<int64_t>(src.n, 1));
+    dst = sp.out();
+  }
+  launch_select(src, make_float4(rc[0], rc[1], rc[2], rc[3]), cthr, c->tile_in.p, c->tile_off_in.p,
+                c->tile_off_out.p, c->totals.p, c->inl_gid.p, nullptr, compact ? &dst : nullptr,
+                c->stream);
+  HIPCHK(hipGetLastError());
+  if (c->profiling) HIPCHK(hipEventRecord(c->ev[3], c->stream));
+  HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  if (c->profiling && xs) xs->select_ms += event_ms(c, 2, 3);
+  out.n_in_local = c->h_tot.p[0];
+  out.n_out_local = src.n == 0 ? 0 : c->h_tot.p[1];
+  return out;
+}
+
+// copy this rank's (or every rank's) refined inliers to the caller buffer
+int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, int64_t cap,
+                     int64_t* global_count) {
+  if (gather && c->comm->world() > 1) {
+    gather_lists(c, c->inl_gid.p, so.n_in_local, 1, &c->h_inl);
+    int64_t n = (int64_t)c->h_inl.size();
+    *global_count = n;
+    if (n > cap) throw DlgError(DLG_ERR_CAPACITY, "inlier buffer too small: need " + std::to_string(n));
+    if (n) std::memcpy(dst, c->h_inl.data(), (size_t)n * 4);
+    return n;
+  }
+  std::vector<int64_t> all;
+  *global_count = allgather_i64(c, so.n_in_local, &all);
+  if (so.n_in_local > cap)
+    throw DlgError(DLG_ERR_CAPACITY, "inlier buffer too small: need " + std::to_string(so.n_in_local));
+  if (so.n_in_local) {
+    HIPCHK(hipMemcpyAsync(dst, c->inl_gid.p, (size_t)so.n_in_local * 4, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+  }
+  return so.n_in_local;
+}
+
+dlg_status fail(dlg_ctx* c, dlg_status code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+template <typename F>
+dlg_status guarded(dlg_ctx* c, F&& f) {
+  try {
+    if (c) set_device(c);
+    f();
+    if (c) c->err.clear();
+    return DLG_OK;
+  } catch (const DlgError& e) {
+    return fail(c, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(c, DLG_ERR_INTERNAL, e.what());
+  } catch (...) {
+    return fail(c, DLG_ERR_INTERNAL, "unknown error");
+  }
+}
+
+std::string g_last_create_error;
+
+dlg_status init_ctx(dlg_ctx* c, int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0)
+    return fail(c, DLG_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
+  if (device < 0 || device >= n) return fail(c, DLG_ERR_NO_DEVICE, "device index out of range");
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) != hipSuccess)
+    return fail(c, DLG_ERR_NO_DEVICE, "hipGetDeviceProperties failed");
+  if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+    return fail(c, DLG_ERR_NO_DEVICE, std::string("built for gfx950, device is ") + p.gcnArchName);
+  c->device = device;
+  c->num_cus = p.multiProcessorCount;
+  return guarded(c, [&] {
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
+  });
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+int dlg_abi_version(void) { return DLG_ABI_VERSION; }
+
+const char* dlg_status_string(dlg_status s) {
+  switch (s) {
+    case DLG_OK: return "ok";
+    case DLG_ERR_INVALID: return "invalid argument";
+    case DLG_ERR_HIP: return "HIP error";
+    case DLG_ERR_NO_DEVICE: return "no usable gfx950 device";
+    case DLG_ERR_COMM: return "communicator error";
+    case DLG_ERR_CAPACITY: return "output buffer too small";
+    case DLG_ERR_INTERNAL: return "internal error";
+  }
+  return "unknown status";
+}
+
+void dlg_sac_params_default(dlg_sac_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->threshold = 0.0;  // SACSegmentation::threshold_ default
+  p->max_iterations = 50;
+  p->probability = 0.99;
+  p->optimize = 1;
+  p->seed = 12345u;
+  p->model = DLG_SACMODEL_PLANE;
+  p->normal_distance_weight = 0.1;
+  p->refit_mode = DLG_REFIT_PCL;
+  p->hypotheses_per_launch = 0;
+  p->gather_inliers = 1;
+}
+
+dlg_status dlg_ctx_create(dlg_ctx** out, int device) {
+  if (!out) return DLG_ERR_INVALID;
+  *out = nullptr;
+  auto c = std::make_unique<dlg_ctx>();
+  dlg_status s = init_ctx(c.get(), device);
+  if (s != DLG_OK) {
+    g_last_create_error = c->err;
+    return s;
+  }
+  c->comm = make_single_comm();
+  *out = c.release();
+  return DLG_OK;
+}
+
+dlg_status dlg_get_unique_id(void* uid) {
+  if (!uid) return DLG_ERR_INVALID;
+  std::string err;
+  if (!rccl_get_unique_id(uid, &err)) {
+    g_last_create_error = err;
+    return DLG_ERR_COMM;
+  }
+  return DLG_OK;
+}
+
+dlg_status dlg_ctx_create_dist(dlg_ctx** out, int device, int rank, int world, const void* uid) {
+  if (!out || world < 1 || rank < 0 || rank >= world || (world > 1 && !uid)) return DLG_ERR_INVALID;
+  *out = nullptr;
+  auto c = std::make_unique<dlg_ctx>();
+  dlg_status s = init_ctx(c.get(), device);
+  if (s != DLG_OK) {
+    g_last_create_error = c->err;
+    return s;
+  }
+  if (world == 1) {
+    c->comm = make_single_comm();
+  } else {
+    std::string err;
+    (void)hipSetDevice(device);
+    c->comm = make_rccl_comm(rank, world, uid, &err);
+    if (!c->comm) {
+      g_last_create_error = err;
+      return DLG_ERR_COMM;
+    }
+  }
+  *out = c.release();
+  return DLG_OK;
+}
+
+dlg_status dlg_ctx_create_loopback_group(dlg_ctx** out_array, int world, int device) {
+  if (!out_array || world < 1) return DLG_ERR_INVALID;
+  auto g = make_loopback_group(world);
+  std::vector<dlg_ctx*> made;
+  for (int r = 0; r < world; ++r) {
+    auto c = std::make_unique<dlg_ctx>();
+    dlg_status s = init_ctx(c.get(), device);
+    if (s != DLG_OK) {
+      g_last_create_error = c->err;
+      for (auto* m : made) dlg_ctx_destroy(m);
+      return s;
+    }
+    c->comm = make_loopback_comm(g, r);
+    made.push_back(c.release());
+  }
+  for (int r = 0; r < world; ++r) out_array[r] = made[r];
+  return DLG_OK;
+}
+
+dlg_status dlg_ctx_destroy(dlg_ctx* c) {
+  if (!c) return DLG_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->comm.reset();
+  c->pos.release(); c->samples.release(); c->hyps.release(); c->res.release();
+  c->tile_in.release(); c->tile_off_in.release(); c->tile_off_out.release(); c->totals.release();
+  c->partials.release(); c->moments.release(); c->inl_gid.release(); c->inl_xyz.release();
+  c->gath64.release(); c->gath32.release();
+  c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
+  for (auto& ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return DLG_OK;
+}
+
+const char* dlg_last_error(const dlg_ctx* c) {
+  return c ? c->err.c_str() : g_last_create_error.c_str();
+}
+
+dlg_status dlg_ctx_info(const dlg_ctx* c, int* rank, int* world, int* device) {
+  if (!c) return DLG_ERR_INVALID;
+  if (rank) *rank = c->comm->rank();
+  if (world) *world = c->comm->world();
+  if (device) *device = c->device;
+  return DLG_OK;
+}
+
+dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* indices,
+                            int64_t n_indices, int32_t id_base, dlg_cloud** out) {
+  if (!c || !pts || !out || (pts->n > 0 && !pts->xyz) || pts->n < 0) return DLG_ERR_INVALID;
+  if (pts->stride_bytes < 12 || pts->stride_bytes % 4) return fail(c, DLG_ERR_INVALID, "stride_bytes must be >= 12 and a multiple of 4");
+  if (indices && n_indices < 0) return fail(c, DLG_ERR_INVALID, "negative n_indices");
+  *out = nullptr;
+  auto cl = std::make_unique<dlg_cloud>();
+  dlg_status s = guarded(c, [&] {
+    const int64_t n = indices ? n_indices : pts->n;
+    if (n > INT32_MAX) throw DlgError(DLG_ERR_INVALID, "more than 2^31-1 points");
+    const int64_t sf = pts->stride_bytes / 4;
+    std::vector<float> x(n), y(n), z(n);
+    std::vector<int32_t> g(n);
+    for (int64_t i = 0; i < n; ++i) {
+      int64_t k = indices ? indices[i] : i;
+      if (k < 0 || k >= pts->n) throw DlgError(DLG_ERR_INVALID, "index out of range");
+      const float* p = pts->xyz + k * sf;
+      x[i] = p[0]; y[i] = p[1]; z[i] = p[2];
+      g[i] = (int32_t)(id_base + k);
+    }
+    cl->ctx = c;
+    cl->n_total = n;
+    cl->n_active = n;
+    cl->pristine.ensure((size_t)std::max<int64_t>(n, 1));
+    if (n) {
+      HIPCHK(hipMemcpyAsync(cl->pristine.x.p, x.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(cl->pristine.y.p, y.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(cl->pristine.z.p, z.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(cl->pristine.gid.p, g.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+    }
+    c->totals.ensure(4);
+    launch_absmax(cl->pristine.view(n), reinterpret_cast<uint32_t*>(c->totals.p), c->stream);
+    uint32_t bits[3];
+    HIPCHK(hipMemcpyAsync(bits, c->totals.p, 12, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    for (int k = 0; k < 3; ++k) std::memcpy(&cl->amax[k], &bits[k], 4);
+  });
+  if (s != DLG_OK) {
+    cl->pristine.release();
+    return s;
+  }
+  *out = cl.release();
+  return DLG_OK;
+}
+
+dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
+  if (!cl) return DLG_OK;
+  if (cl->ctx) (void)hipSetDevice(cl->ctx->device);
+  if (cl->ctx && cl->ctx->stream) (void)hipStreamSynchronize(cl->ctx->stream);
+  cl->pristine.release();
+  cl->buf[0].release();
+  cl->buf[1].release();
+  delete cl;
+  return DLG_OK;
+}
+
+dlg_status dlg_cloud_reset(dlg_cloud* cl) {
+  if (!cl) return DLG_ERR_INVALID;
+  cl->cur = -1;
+  cl->n_active = cl->n_total;
+  return DLG_OK;
+}
+
+dlg_status dlg_cloud_active(const dlg_cloud* cl, int64_t* n) {
+  if (!cl || !n) return DLG_ERR_INVALID;
+  *n = cl->n_active;
+  return DLG_OK;
+}
+
+dlg_status dlg_sac_segment(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* prm, float coeff_out[4],
+                           int32_t* inliers_out, int64_t cap, int64_t* n_inliers,
+                           dlg_sac_stats* stats) {
+  if (!c || !cl || !prm || !coeff_out || !n_inliers || cl->ctx != c) return DLG_ERR_INVALID;
+  if (!inliers_out && cap > 0) return DLG_ERR_INVALID;
+  dlg_sac_stats local;
+  dlg_sac_stats* st = stats ? stats : &local;
+  return guarded(c, [&] {
+    std::memset(coeff_out, 0, 4 * sizeof(float));
+    *n_inliers = 0;
+    SegOut so = segment_impl(c, cl, *prm, false, st, nullptr);
+    if (!so.has_model) return;
+    std::memcpy(coeff_out, so.coeff, sizeof(so.coeff));
+    int64_t g = 0;
+    *n_inliers = emit_inliers(c, so, prm->gather_inliers != 0, inliers_out, cap, &g);
+  });
+}
+
+dlg_status dlg_sac_segment_host(dlg_ctx* c, const dlg_points* pts, const int32_t* indices,
+                                int64_t n_indices, const dlg_sac_params* prm, float coeff_out[4],
+                                int32_t* inliers_out, int64_t cap, int64_t* n_inliers,
+                                dlg_sac_stats* stats) {
+  dlg_cloud* cl = nullptr;
+  dlg_status s = dlg_cloud_upload(c, pts, indices, n_indices, 0, &cl);
+  if (s != DLG_OK) return s;
+  s = dlg_sac_segment(c, cl, prm, coeff_out, inliers_out, cap, n_inliers, stats);
+  dlg_cloud_destroy(cl);
+  return s;
+}
+
+dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* prm, int max_planes,
+                              int64_t min_inliers, float* coeffs_out, int64_t* offsets_out,
+                              int32_t* inliers_out, int64_t cap, int* n_planes,
+                              dlg_extract_stats* stats) {
+  if (!c || !cl || !prm || max_planes < 0 || !n_planes || cl->ctx != c) return DLG_ERR_INVALID;
+  if (max_planes > 0 && (!coeffs_out || !offsets_out)) return DLG_ERR_INVALID;
+  if (!inliers_out && cap > 0) return DLG_ERR_INVALID;
+  dlg_extract_stats local;
+  dlg_extract_stats* xs = stats ? stats : &local;
+  std::memset(xs, 0, sizeof(*xs));
+  auto t0 = std::chrono::steady_clock::now();
+  dlg_status s = guarded(c, [&] {
+    *n_planes = 0;
+    if (max_planes > 0) offsets_out[0] = 0;
+    int64_t written = 0;
+    const int64_t floor_n = std::max<int64_t>(3, min_inliers);
+    for (int p = 0; p < max_planes; ++p) {
+      std::vector<int64_t> all;
+      const int64_t N = allgather_i64(c, cl->n_active, &all);
+      if (N < floor_n) break;
+      dlg_sac_stats st;
+      SegOut so = segment_impl(c, cl, *prm, true, &st, xs);
+      xs->rounds++;
+      if (!so.has_model) break;
+      std::vector<int64_t> tot;
+      const int64_t n_in = allgather_i64(c, so.n_in_local, &tot);
+      if (n_in == 0 || n_in < min_inliers) break;  // plane rejected: active list unchanged
+      int64_t g = 0;
+      int64_t n = emit_inliers(c, so, prm->gather_inliers != 0, inliers_out + written,
+                               cap - written, &g);
+      std::memcpy(coeffs_out + 4 * p, so.coeff, sizeof(so.coeff));
+      written += n;
+      offsets_out[p + 1] = written;
+      *n_planes = p + 1;
+      cl->cur = cl->spare();  // commit the removal
+      cl->n_active = so.n_out_local;
+    }
+  });
+  xs->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return s;
+}
+
+dlg_status dlg_set_profiling(dlg_ctx* c, int enable) {
+  if (!c) return DLG_ERR_INVALID;
+  c->profiling = enable != 0;
+  return DLG_OK;
+}
+
+dlg_status dlg_synchronize(dlg_ctx* c) {
+  if (!c) return DLG_ERR_INVALID;
+  return guarded(c, [&] { HIPCHK(hipDeviceSynchronize()); });
+}
+
+dlg_status dlg_allreduce_max_f64(dlg_ctx* c, double* v) {
+  if (!c || !v) return DLG_ERR_INVALID;
+  if (c->comm->world() == 1) return DLG_OK;
+  return guarded(c, [&] {
+    c->moments.ensure(kMomentK);
+    HIPCHK(hipMemcpyAsync(c->moments.p, v, 8, hipMemcpyHostToDevice, c->stream));
+    c->comm->allreduce_max_f64(c->moments.p, 1, c->stream);
+    HIPCHK(hipMemcpyAsync(v, c->moments.p, 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+  });
+}
+
+dlg_status dlg_barrier(dlg_ctx* c) {
+  double v = 0.0;
+  return dlg_allreduce_max_f64(c, &v);
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+// kernels.hpp -- device kernels of the RANSAC plane path (gfx950 / CDNA4) and their launchers.
+//
+// Layout in HBM (per rank, per cloud): structure-of-arrays float x[], y[], z[] plus int32 gid[]
+// (global point id), active prefix [0, n_active).  Extract-and-remove compacts the survivors
+// into a ping-pong set of the same arrays, so every scoring pass streams exactly 12 B per active
+// point and the active order stays the PCL "remaining indices" order.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dlg {
+
+// one sampled point of a hypothesis (gathered by list position; zero on ranks not holding it)
+struct alignas(16) SampleRec {
+  int32_t gid;
+  float x, y, z;
+};
+
+// plane hypothesis: PCL coefficients + the prefilter band [tlo, thi) around the exact threshold
+struct alignas(16) HypRec {
+  float a, b, c, d;
+  float tlo, thi;
+  int32_t good;  // SampleConsensusModelPlane::isSampleGood
+  int32_t pad;
+};
+
+struct PointsView {
+  const float* x;
+  const float* y;
+  const float* z;
+  const int32_t* gid;
+  int64_t n;
+};
+
+struct PointsOut {
+  float* x;
+  float* y;
+  float* z;
+  int32_t* gid;
+};
+
+constexpr int kMaxHypPerLaunch = 4096;  // LDS count array of the scoring kernel
+constexpr int kSelTile = 4096;          // points per select/compact workgroup
+constexpr int kMomentK = 10;            // n, sx, sy, sz, sxx, sxy, sxz, syy, syz, szz
+
+// Scoring kernel variants (bench/profiling A/B; product default = kScoreExact)
+enum ScoreVariant { kScoreExact = 0, kScoreFmaBand = 1 };
+
+void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
+                           hipStream_t s);
+// writes hyps[D] and good[D] (int32 flags next to the counts for one D2H copy)
+void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,
+                       HypRec* hyps, int32_t* good, hipStream_t s);
+// counts[D] = #{i < n : |plane_h . (x_i, y_i, z_i, 1)| < cthr}, PCL (Eigen SSE) op order.
+// counts must be zeroed by the caller (memset on the same stream).
+void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
+                  int variant, int num_cus, hipStream_t s);
+// moments (count + 9 sums, double, coordinates shifted by `shift`) of the inliers of coef;
+// partials [nblocks][10] -> out[10] (fixed-order reduction: deterministic)
+int moments_blocks(int64_t n);
+void launch_moments(PointsView src, float4 coef, float cthr, double3 shift, double* partials,
+                    int nblocks, double* out, hipStream_t s);
+// select: inliers of coef in list order; optional inlier xyz (AoS, 3 floats); optional
+// compaction of the outliers into dst.  tile_in/out: [ntiles] scratch; totals[2] = {in, out}.
+int select_tiles(int64_t n);
+void launch_select(PointsView src, float4 coef, float cthr, int32_t* tile_in, int32_t* tile_off_in,
+                   int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid, float* inl_xyz,
+                   const PointsOut* dst, hipStream_t s);
+// max |x|, |y|, |z| over the cloud (prefilter error bound); out: 3 floats (as uint bits)
+void launch_absmax(PointsView src, uint32_t* out3, hipStream_t s);
+
+}  // namespace dlg

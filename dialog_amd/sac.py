@@ -1,0 +1,292 @@
+"""Host-side mirror of PCL's SACSegmentation interface over the MI355X C ABI.
+
+`SACSegmentation` keeps the PCL 1.8 names, argument meanings and failure behaviour of
+pcl::SACSegmentation<pcl::PointXYZ> as the reference calls it (Dialog/SimplifyVerticesSize.cpp:
+62-67, 86-87): setModelType / setMethodType / setDistanceThreshold / setMaxIterations /
+setProbability / setOptimizeCoefficients / setInputCloud / setIndices / segment().  segment()
+returns (inliers, coefficients); "no model" is an empty inlier list and empty coefficients, as in
+PCL.  `extract_planes` is the sequential extract-and-remove loop that fills the reference's
+plane_clouds slot (Dialog/PlaneDetect.h:100, :667-1355).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import _lib
+from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, DLG_SACMODEL_PLANE, DialogError  # noqa: F401
+
+SACMODEL_PLANE = 0
+SACMODEL_NORMAL_PLANE = 11
+SAC_RANSAC = 0
+
+
+def _f32p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _i32p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def _points(xyz):
+    """float32 [N,3] or [N,4] (pcl::PointXYZ layout) -> (keepalive array, Points struct)."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] not in (3, 4):
+        raise ValueError("points must be float32 [N,3] or [N,4]")
+    return a, _lib.Points(_f32p(a), a.shape[0], 4 * a.shape[1])
+
+
+class Context:
+    """One HIP device (+ optional rank communicator).  Not thread-safe: one per host thread."""
+
+    def __init__(self, device: int = 0, _handle=None):
+        self._L = _lib.load()
+        if _handle is not None:
+            self.h = _handle
+        else:
+            h = C.c_void_p()
+            _lib.check(self._L.dlg_ctx_create(C.byref(h), int(device)), None)
+            self.h = h
+        r, w, d = C.c_int(), C.c_int(), C.c_int()
+        _lib.check(self._L.dlg_ctx_info(self.h, C.byref(r), C.byref(w), C.byref(d)), self.h)
+        self.rank, self.world, self.device = r.value, w.value, d.value
+
+    @classmethod
+    def distributed(cls, device, rank, world, unique_id: bytes):
+        L = _lib.load()
+        h = C.c_void_p()
+        buf = C.create_string_buffer(bytes(unique_id), 128)
+        _lib.check(L.dlg_ctx_create_dist(C.byref(h), int(device), int(rank), int(world), buf), None)
+        return cls(_handle=h)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = _lib.load()
+        buf = C.create_string_buffer(128)
+        _lib.check(L.dlg_get_unique_id(buf), None)
+        return buf.raw
+
+    @classmethod
+    def loopback_group(cls, world: int, device: int = 0):
+        L = _lib.load()
+        arr = (C.c_void_p * world)()
+        _lib.check(L.dlg_ctx_create_loopback_group(arr, int(world), int(device)), None)
+        return [cls(_handle=C.c_void_p(arr[r])) for r in range(world)]
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self._L.dlg_ctx_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, status):
+        _lib.check(status, self.h)
+
+    def set_profiling(self, on=True):
+        self.check(self._L.dlg_set_profiling(self.h, int(bool(on))))
+
+    def synchronize(self):
+        self.check(self._L.dlg_synchronize(self.h))
+
+    def barrier(self):
+        self.check(self._L.dlg_barrier(self.h))
+
+    def allreduce_max(self, v: float) -> float:
+        x = C.c_double(float(v))
+        self.check(self._L.dlg_allreduce_max_f64(self.h, C.byref(x)))
+        return x.value
+
+
+class Cloud:
+    """Device-resident active point list (this rank's shard)."""
+
+    def __init__(self, ctx: Context, xyz, indices=None, id_base: int = 0):
+        self.ctx = ctx
+        arr, pts = _points(xyz)
+        h = C.c_void_p()
+        if indices is not None:
+            idx = np.ascontiguousarray(indices, dtype=np.int32)
+            ctx.check(ctx._L.dlg_cloud_upload(ctx.h, C.byref(pts), _i32p(idx), idx.shape[0],
+                                              int(id_base), C.byref(h)))
+            self.n = idx.shape[0]
+        else:
+            ctx.check(ctx._L.dlg_cloud_upload(ctx.h, C.byref(pts), None, 0, int(id_base),
+                                              C.byref(h)))
+            self.n = arr.shape[0]
+        self.h = h
+
+    def reset(self):
+        self.ctx.check(self.ctx._L.dlg_cloud_reset(self.h))
+
+    @property
+    def n_active(self):
+        v = C.c_int64()
+        self.ctx.check(self.ctx._L.dlg_cloud_active(self.h, C.byref(v)))
+        return v.value
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.ctx._L.dlg_cloud_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_params(threshold=0.0, max_iterations=50, probability=0.99, optimize=True, seed=12345,
+                refit_mode=DLG_REFIT_PCL, hypotheses_per_launch=0, gather_inliers=True,
+                model=SACMODEL_PLANE):
+    L = _lib.load()
+    p = _lib.SacParams()
+    L.dlg_sac_params_default(C.byref(p))
+    p.threshold = float(threshold)
+    p.max_iterations = int(max_iterations)
+    p.probability = float(probability)
+    p.optimize = int(bool(optimize))
+    p.seed = int(seed)
+    p.refit_mode = int(refit_mode)
+    p.hypotheses_per_launch = int(hypotheses_per_launch)
+    p.gather_inliers = int(bool(gather_inliers))
+    p.model = int(model)
+    return p
+
+
+def _stats_dict(st):
+    return dict(iterations=st.iterations, skipped=st.skipped, has_model=bool(st.has_model),
+                launches=st.launches, draws=st.draws,
+                best_sample=np.array(st.best_sample[:], np.int32),
+                coeff_unrefined=np.array(st.coeff_unrefined[:], np.float32),
+                n_unrefined=st.n_unrefined, n_active=st.n_active, tests=st.tests,
+                tests_scored=st.tests_scored, score_ms=st.score_ms)
+
+
+def segment_cloud(cloud: Cloud, params, capacity=None):
+    """One SACSegmentation::segment over the cloud's active list -> (inliers, coeff, stats)."""
+    ctx = cloud.ctx
+    cap = int(capacity if capacity is not None else max(cloud.n_active * max(ctx.world, 1), 1))
+    inl = np.empty(max(cap, 1), np.int32)
+    coeff = np.zeros(4, np.float32)
+    n = C.c_int64()
+    st = _lib.SacStats()
+    ctx.check(ctx._L.dlg_sac_segment(ctx.h, cloud.h, C.byref(params), _f32p(coeff), _i32p(inl),
+                                     cap, C.byref(n), C.byref(st)))
+    return inl[:n.value].copy(), coeff, _stats_dict(st)
+
+
+def extract_planes(cloud: Cloud, params, max_planes=20, min_inliers=0, capacity=None):
+    """Sequential extract-and-remove -> dict(coeffs [P,4], offsets [P+1], inliers, stats)."""
+    ctx = cloud.ctx
+    cap = int(capacity if capacity is not None else max(cloud.n_active * max(ctx.world, 1), 1))
+    coeffs = np.zeros((max(max_planes, 1), 4), np.float32)
+    offs = np.zeros(max_planes + 1, np.int64)
+    inl = np.empty(max(cap, 1), np.int32)
+    npl = C.c_int()
+    xs = _lib.ExtractStats()
+    ctx.check(ctx._L.dlg_extract_planes(ctx.h, cloud.h, C.byref(params), int(max_planes),
+                                        int(min_inliers), _f32p(coeffs),
+                                        offs.ctypes.data_as(C.POINTER(C.c_int64)), _i32p(inl), cap,
+                                        C.byref(npl), C.byref(xs)))
+    k = npl.value
+    stats = dict(rounds=xs.rounds, tests=xs.tests, tests_scored=xs.tests_scored,
+                 score_launches=xs.score_launches, score_ms=xs.score_ms, select_ms=xs.select_ms,
+                 wall_ms=xs.wall_ms)
+    return dict(coeffs=coeffs[:k].copy(), offsets=offs[:k + 1].copy(),
+                inliers=inl[:offs[k]].copy(), n_planes=k, stats=stats)
+
+
+_default_ctx = threading.local()
+
+
+def default_context() -> Context:
+    c = getattr(_default_ctx, "ctx", None)
+    if c is None:
+        c = Context(0)
+        _default_ctx.ctx = c
+    return c
+
+
+class SACSegmentation:
+    """pcl::SACSegmentation<pcl::PointXYZ> (SACMODEL_PLANE, SAC_RANSAC) on the GPU."""
+
+    def __init__(self, ctx: Context | None = None):
+        self.ctx = ctx
+        self.model_type = -1
+        self.method_type = -1
+        self.threshold = 0.0
+        self.max_iterations = 50
+        self.probability = 0.99
+        self.optimize = True
+        self.refit_mode = DLG_REFIT_PCL
+        self.input = None
+        self.indices = None
+        self.last_stats = None
+
+    # PCL setters (camelCase as in the reference's call sites) ------------------------------
+    def setModelType(self, m):
+        self.model_type = int(m)
+
+    def setMethodType(self, m):
+        self.method_type = int(m)
+
+    def setDistanceThreshold(self, t):
+        self.threshold = float(t)
+
+    def setMaxIterations(self, n):
+        self.max_iterations = int(n)
+
+    def setProbability(self, p):
+        self.probability = float(p)
+
+    def setOptimizeCoefficients(self, b):
+        self.optimize = bool(b)
+
+    def setInputCloud(self, xyz):
+        self.input = np.ascontiguousarray(xyz, dtype=np.float32)
+
+    def setIndices(self, idx):
+        self.indices = None if idx is None else np.ascontiguousarray(idx, dtype=np.int32)
+
+    def setRefitMode(self, mode):
+        self.refit_mode = int(mode)
+
+    def segment(self):
+        """-> (inliers int32[], coefficients float32[4] or [] when no model was found)."""
+        if self.input is None:
+            raise ValueError("setInputCloud() first")
+        if self.model_type != SACMODEL_PLANE:
+            raise ValueError("only SACMODEL_PLANE is supported (PCL: initSACModel fails)")
+        if self.method_type not in (SAC_RANSAC,):
+            raise ValueError("only SAC_RANSAC is supported")
+        ctx = self.ctx or default_context()
+        params = make_params(self.threshold, self.max_iterations, self.probability, self.optimize,
+                             refit_mode=self.refit_mode)
+        cloud = Cloud(ctx, self.input, indices=self.indices)
+        try:
+            inl, coeff, st = segment_cloud(cloud, params)
+        finally:
+            cloud.close()
+        self.last_stats = st
+        if not st["has_model"]:
+            return np.zeros(0, np.int32), np.zeros(0, np.float32)
+        return inl, coeff
+
+    # snake_case aliases
+    set_model_type = setModelType
+    set_method_type = setMethodType
+    set_distance_threshold = setDistanceThreshold
+    set_max_iterations = setMaxIterations
+    set_probability = setProbability
+    set_optimize_coefficients = setOptimizeCoefficients
+    set_input_cloud = setInputCloud
+    set_indices = setIndices

@@ -1,0 +1,169 @@
+/*
+ * dialog_ransac.h -- C ABI of the MI355X-native RANSAC plane-segmentation path.
+ *
+ * Drop-in boundary for czh55/Dialog's plane stage.  The reference has no FFI of its own: its
+ * plane stage is a header "module" of free functions over globals (Dialog/PlaneDetect.h:143-211,
+ * source_cloud :104, source_normal :107, plane_clouds :100) that calls PCL.  These entry points
+ * replace the PCL calls that sit under PlaneDetect.h's functions:
+ *
+ *   dlg_sac_segment      <- pcl::SACSegmentation<PointXYZ>::segment(PointIndices&, ModelCoefficients&)
+ *                           with SACMODEL_PLANE / SAC_RANSAC (reference call pattern
+ *                           Dialog/SimplifyVerticesSize.cpp:62-67, :86-87)
+ *   dlg_extract_planes   <- the segmentation slot Dialog/PlaneDetect.h:667-1355 (createPS ..
+ *                           mergePlanes) re-filled by sequential extract-and-remove RANSAC, the
+ *                           analogue of the re-run loop PCLViewer.cpp:1120-1177 /
+ *                           PlaneDetect.h:1500-1573; output feeds plane_clouds (PlaneDetect.h:100)
+ *   dlg_estimate_normals <- estimateNormal(), Dialog/PlaneDetect.h:515-545
+ *                           (pcl::NormalEstimationOMP, radius r_for_estimate_normal)
+ *   dlg_regulate_normals <- regulateNormal(), Dialog/PlaneDetect.h:547-665
+ *
+ * Conventions: inputs are borrowed for the duration of a call; outputs go to caller buffers
+ * (capacity given; DLG_ERR_CAPACITY + required size when too small).  No exceptions cross the
+ * ABI.  "No model" is DLG_OK with *n_inliers == 0 and a zeroed coefficient vector (the C++ shim
+ * maps it to PCL's empty indices/values).  One context per host thread; calls block until the
+ * device work of the call has finished.  Every compute entry point runs on the GPU: there is no
+ * CPU fallback, and creating a context without a usable HIP device fails with DLG_ERR_NO_DEVICE.
+ */
+#ifndef DIALOG_RANSAC_H
+#define DIALOG_RANSAC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLG_ABI_VERSION 1
+
+typedef enum {
+  DLG_OK = 0,
+  DLG_ERR_INVALID = 1,    /* bad argument */
+  DLG_ERR_HIP = 2,        /* HIP runtime error */
+  DLG_ERR_NO_DEVICE = 3,  /* no usable gfx950 device */
+  DLG_ERR_COMM = 4,       /* RCCL / communicator error */
+  DLG_ERR_CAPACITY = 5,   /* output buffer too small; required size reported */
+  DLG_ERR_INTERNAL = 6
+} dlg_status;
+
+/* pcl::SacModel values (pcl/sample_consensus/model_types.h) */
+enum { DLG_SACMODEL_PLANE = 0, DLG_SACMODEL_NORMAL_PLANE = 11 };
+/* refit of the winning model (SampleConsensusModelPlane::optimizeModelCoefficients) */
+enum {
+  DLG_REFIT_PCL = 0,   /* PCL float, single pass, index order: bit-exact with PCL (host-sequential) */
+  DLG_REFIT_FAST = 1   /* on-device double moments + double eigen33: within 1e-5 of the exact LS plane */
+};
+
+typedef struct dlg_ctx dlg_ctx;
+typedef struct dlg_cloud dlg_cloud;
+
+/* Host points, borrowed.  stride_bytes 16 = pcl::PointXYZ (x, y, z, pad), 12 = packed xyz. */
+typedef struct {
+  const float* xyz;
+  int64_t n;
+  int64_t stride_bytes;
+} dlg_points;
+
+typedef struct {
+  double threshold;            /* setDistanceThreshold */
+  int max_iterations;          /* setMaxIterations (PCL default 50) */
+  double probability;          /* setProbability (PCL default 0.99) */
+  int optimize;                /* setOptimizeCoefficients (PCL default 1) */
+  uint32_t seed;               /* 12345u = PCL's non-random seed */
+  int model;                   /* DLG_SACMODEL_PLANE */
+  double normal_distance_weight;
+  int refit_mode;              /* DLG_REFIT_PCL (default) | DLG_REFIT_FAST */
+  int hypotheses_per_launch;   /* upper bound of one scoring launch; 0 = 4096 */
+  int gather_inliers;          /* multi-rank: 1 = every rank receives the global inlier list */
+} dlg_sac_params;
+
+typedef struct {
+  int iterations;              /* RandomSampleConsensus iterations_ at exit */
+  int skipped;
+  int has_model;
+  int launches;                /* scoring launches */
+  int64_t draws;               /* drawIndexSample calls */
+  int32_t best_sample[3];      /* global indices of the winning triple */
+  float coeff_unrefined[4];
+  int64_t n_unrefined;         /* inliers of the unrefined model */
+  int64_t n_active;            /* points the model was fitted on (all ranks) */
+  int64_t tests;               /* point-plane tests PCL's loop evaluates (iterations x n_active) */
+  int64_t tests_scored;        /* point-plane tests the GPU scored (>= tests: batch tail) */
+  double score_ms;             /* device time of the scoring launches (HIP events) */
+} dlg_sac_stats;
+
+typedef struct {
+  int rounds;                  /* segment() calls */
+  int64_t tests;
+  int64_t tests_scored;
+  int score_launches;
+  double score_ms;             /* sum of scoring-kernel device time */
+  double select_ms;            /* sum of select/compact/moments device time */
+  double wall_ms;              /* host wall time of the call */
+} dlg_extract_stats;
+
+void dlg_sac_params_default(dlg_sac_params* p);   /* PCL SACSegmentation defaults */
+const char* dlg_status_string(dlg_status s);
+int dlg_abi_version(void);
+
+/* ---- contexts ------------------------------------------------------------------------------ */
+dlg_status dlg_ctx_create(dlg_ctx** out, int device);
+/* one process per GPU: rank/world over RCCL (xGMI).  unique_id: 128 bytes from dlg_get_unique_id
+ * on rank 0, distributed out of band (e.g. torch.distributed gloo). */
+dlg_status dlg_get_unique_id(void* unique_id_128);
+dlg_status dlg_ctx_create_dist(dlg_ctx** out, int device, int rank, int world,
+                               const void* unique_id_128);
+/* in-process group of `world` ranks sharing one device, one host thread per rank (test and
+ * rehearsal of the sharded path on a single GPU); the group's contexts must be driven
+ * concurrently, rank r from its own thread. */
+dlg_status dlg_ctx_create_loopback_group(dlg_ctx** out_array, int world, int device);
+dlg_status dlg_ctx_destroy(dlg_ctx* ctx);
+const char* dlg_last_error(const dlg_ctx* ctx);
+dlg_status dlg_ctx_info(const dlg_ctx* ctx, int* rank, int* world, int* device);
+
+/* ---- device-resident clouds (this rank's contiguous shard of the global index order) -------- */
+/* The active list starts as point xyz[k] for k = indices[i] (pcl setIndices(); any order,
+ * duplicates allowed) or k = 0..n-1 when indices is NULL; its global id is id_base + k.
+ * Multi-rank: each rank uploads its contiguous shard with id_base = the shard's first global id;
+ * the global active list is the concatenation of the ranks' lists in rank order. */
+dlg_status dlg_cloud_upload(dlg_ctx* ctx, const dlg_points* pts, const int32_t* indices,
+                            int64_t n_indices, int32_t id_base, dlg_cloud** out);
+dlg_status dlg_cloud_destroy(dlg_cloud* cloud);
+/* re-activate every point of the cloud (undo extract-and-remove) */
+dlg_status dlg_cloud_reset(dlg_cloud* cloud);
+dlg_status dlg_cloud_active(const dlg_cloud* cloud, int64_t* n_active_local);
+
+/* ---- RANSAC ----------------------------------------------------------------------------------- */
+/* SACSegmentation::segment on the cloud's active points (not removed).  inliers_out receives
+ * global ids in active-list order (this rank's part, or all ranks' if gather_inliers). */
+dlg_status dlg_sac_segment(dlg_ctx* ctx, dlg_cloud* cloud, const dlg_sac_params* prm,
+                           float coeff_out[4], int32_t* inliers_out, int64_t cap,
+                           int64_t* n_inliers, dlg_sac_stats* stats);
+
+/* Host-buffer convenience: upload, segment, free (PCL setInputCloud + setIndices + segment). */
+dlg_status dlg_sac_segment_host(dlg_ctx* ctx, const dlg_points* pts, const int32_t* indices,
+                                int64_t n_indices, const dlg_sac_params* prm, float coeff_out[4],
+                                int32_t* inliers_out, int64_t cap, int64_t* n_inliers,
+                                dlg_sac_stats* stats);
+
+/* Sequential extract-and-remove: round r runs segment() on the remaining points (RNG reseeded,
+ * shuffled list = remaining list), records the plane and removes its inliers.  Stops when fewer
+ * than max(3, min_inliers) points remain, when no model is found, or when a plane has fewer than
+ * min_inliers inliers (not recorded).  coeffs_out: 4*max_planes floats; offsets_out:
+ * max_planes+1 (offsets into inliers_out); inliers_out capacity `cap` ids. */
+dlg_status dlg_extract_planes(dlg_ctx* ctx, dlg_cloud* cloud, const dlg_sac_params* prm,
+                              int max_planes, int64_t min_inliers, float* coeffs_out,
+                              int64_t* offsets_out, int32_t* inliers_out, int64_t cap,
+                              int* n_planes, dlg_extract_stats* stats);
+
+/* ---- profiling ------------------------------------------------------------------------------ */
+/* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
+dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);
+dlg_status dlg_synchronize(dlg_ctx* ctx);
+/* max over ranks of a host double (bench timing) and a barrier; no-ops for world == 1 */
+dlg_status dlg_allreduce_max_f64(dlg_ctx* ctx, double* value);
+dlg_status dlg_barrier(dlg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIALOG_RANSAC_H */

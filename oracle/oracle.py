@@ -1,0 +1,210 @@
+"""ctypes wrapper for the C oracle (liborc.so) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+It is the checker, never the thing measured or shipped (see pcl_oracle.h for provenance and
+pinning status: RNG pinned, PCL arithmetic "parity unpinned" -- restated from PCL 1.8).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liborc.so")
+    src = os.path.join(_HERE, "pcl_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return path
+
+
+class SacParams(C.Structure):
+    _fields_ = [("threshold", C.c_double), ("max_iterations", C.c_int),
+                ("probability", C.c_double), ("optimize", C.c_int),
+                ("seed", C.c_uint32), ("refit_double", C.c_int)]
+
+
+class SacStats(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("skipped", C.c_int), ("draws", C.c_int64),
+                ("best_sample", C.c_int32 * 3), ("coeff_unrefined", C.c_float * 4),
+                ("n_unrefined", C.c_int64), ("has_model", C.c_int)]
+
+
+class MT(C.Structure):
+    _fields_ = [("mt", C.c_uint32 * 624), ("idx", C.c_int)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        L = C.CDLL(build())
+        fp = C.POINTER(C.c_float)
+        i32p = C.POINTER(C.c_int32)
+        i64p = C.POINTER(C.c_int64)
+        L.orc_mt_seed.argtypes = [C.POINTER(MT), C.c_uint32]
+        L.orc_mt_next.argtypes = [C.POINTER(MT)]
+        L.orc_mt_next.restype = C.c_uint32
+        L.orc_rnd.argtypes = [C.POINTER(MT)]
+        L.orc_rnd.restype = C.c_int
+        L.orc_plane_coefficients.argtypes = [fp, fp, fp, fp]
+        L.orc_plane_sample_good.argtypes = [fp, fp, fp]
+        L.orc_thr_ceil.argtypes = [C.c_double]
+        L.orc_thr_ceil.restype = C.c_float
+        L.orc_sac_segment.argtypes = [fp, C.c_int64, C.c_int64, i32p, C.c_int64,
+                                      C.POINTER(SacParams), fp, i32p, i64p, C.POINTER(SacStats)]
+        L.orc_extract_planes.argtypes = [fp, C.c_int64, C.c_int64, C.POINTER(SacParams), C.c_int,
+                                         C.c_int64, fp, i64p, i32p, C.POINTER(C.c_int)]
+        L.orc_count_within.argtypes = [fp, C.c_int64, i32p, C.c_int64, fp, C.c_double]
+        L.orc_count_within.restype = C.c_int64
+        L.orc_mean_cov.argtypes = [fp, C.c_int64, i32p, C.c_int64, fp, fp]
+        L.orc_eigen33.argtypes = [fp, fp, fp]
+        L.orc_refit_double.argtypes = [fp, C.c_int64, i32p, C.c_int64, fp, fp]
+        L.orc_estimate_normals.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, fp, fp]
+        L.orc_regulate_normals.argtypes = [fp, C.c_int64, C.c_int64, fp, C.c_int64, C.c_int,
+                                           C.c_float, C.POINTER(C.c_uint8)]
+        L.orc_regulate_normals.restype = C.c_int64
+        _LIB = L
+    return _LIB
+
+
+def _f(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _i32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def _xyz(points):
+    p = np.ascontiguousarray(points, dtype=np.float32)
+    assert p.ndim == 2 and p.shape[1] in (3, 4)
+    return p, p.shape[1]
+
+
+def rnd_stream(n, seed=12345):
+    g = MT()
+    lib().orc_mt_seed(C.byref(g), seed)
+    return np.array([lib().orc_rnd(C.byref(g)) for _ in range(n)], dtype=np.int64)
+
+
+def mt_stream(n, seed=12345):
+    g = MT()
+    lib().orc_mt_seed(C.byref(g), seed)
+    return np.array([lib().orc_mt_next(C.byref(g)) for _ in range(n)], dtype=np.uint64)
+
+
+def params(threshold, max_iterations=50, probability=0.99, optimize=True, seed=12345,
+           refit_double=False):
+    return SacParams(float(threshold), int(max_iterations), float(probability), int(bool(optimize)),
+                     int(seed), int(bool(refit_double)))
+
+
+def sac_segment(points, threshold, indices=None, **kw):
+    """PCL SACSegmentation(PLANE, RANSAC).segment -> dict(coeff, inliers, stats...)."""
+    p, stride = _xyz(points)
+    n = p.shape[0]
+    prm = params(threshold, **kw)
+    if indices is not None:
+        idx = np.ascontiguousarray(indices, dtype=np.int32)
+        nidx = idx.shape[0]
+        idxp = _i32(idx)
+    else:
+        idx, nidx, idxp = None, n, None
+    coeff = np.zeros(4, np.float32)
+    inl = np.zeros(max(nidx, 1), np.int32)
+    nin = C.c_int64(0)
+    st = SacStats()
+    ok = lib().orc_sac_segment(_f(p), n, stride, idxp, nidx, C.byref(prm), _f(coeff), _i32(inl),
+                               C.byref(nin), C.byref(st))
+    return dict(ok=bool(ok), coeff=coeff, inliers=inl[:nin.value].copy(),
+                iterations=st.iterations, skipped=st.skipped, draws=st.draws,
+                best_sample=np.array(st.best_sample[:], np.int32),
+                coeff_unrefined=np.array(st.coeff_unrefined[:], np.float32),
+                n_unrefined=st.n_unrefined)
+
+
+def extract_planes(points, threshold, max_planes=20, min_inliers=0, **kw):
+    p, stride = _xyz(points)
+    n = p.shape[0]
+    prm = params(threshold, **kw)
+    coeffs = np.zeros((max_planes, 4), np.float32)
+    offs = np.zeros(max_planes + 1, np.int64)
+    inl = np.zeros(max(n, 1), np.int32)
+    npl = C.c_int(0)
+    lib().orc_extract_planes(_f(p), n, stride, C.byref(prm), max_planes, int(min_inliers),
+                             _f(coeffs), offs.ctypes.data_as(C.POINTER(C.c_int64)), _i32(inl),
+                             C.byref(npl))
+    k = npl.value
+    return dict(coeffs=coeffs[:k].copy(), offsets=offs[:k + 1].copy(),
+                inliers=inl[:offs[k]].copy(), n_planes=k)
+
+
+def count_within(points, coeff, threshold, indices=None):
+    p, stride = _xyz(points)
+    c = np.ascontiguousarray(coeff, np.float32)
+    if indices is None:
+        return lib().orc_count_within(_f(p), stride, None, p.shape[0], _f(c), float(threshold))
+    idx = np.ascontiguousarray(indices, np.int32)
+    return lib().orc_count_within(_f(p), stride, _i32(idx), idx.shape[0], _f(c), float(threshold))
+
+
+def plane_coefficients(p0, p1, p2):
+    a = [np.ascontiguousarray(v, np.float32) for v in (p0, p1, p2)]
+    c = np.zeros(4, np.float32)
+    ok = lib().orc_plane_coefficients(_f(a[0]), _f(a[1]), _f(a[2]), _f(c))
+    return bool(ok), c
+
+
+def eigen33(cov):
+    m = np.ascontiguousarray(cov, np.float32).reshape(9)
+    ev = np.zeros(1, np.float32)
+    v = np.zeros(3, np.float32)
+    lib().orc_eigen33(_f(m), _f(ev), _f(v))
+    return ev[0], v
+
+
+def mean_cov(points, indices):
+    p, stride = _xyz(points)
+    idx = np.ascontiguousarray(indices, np.int32)
+    cov = np.zeros(9, np.float32)
+    cen = np.zeros(4, np.float32)
+    lib().orc_mean_cov(_f(p), stride, _i32(idx), idx.shape[0], _f(cov), _f(cen))
+    return cov, cen
+
+
+def refit_double(points, indices, coeff_in):
+    p, stride = _xyz(points)
+    idx = np.ascontiguousarray(indices, np.int32)
+    ci = np.ascontiguousarray(coeff_in, np.float32)
+    co = np.zeros(4, np.float32)
+    lib().orc_refit_double(_f(p), stride, _i32(idx), idx.shape[0], _f(ci), _f(co))
+    return co
+
+
+def thr_ceil(thr):
+    return np.float32(lib().orc_thr_ceil(float(thr)))
+
+
+def estimate_normals(points, radius, viewpoint=(0.0, 0.0, 0.0)):
+    p, stride = _xyz(points)
+    out = np.zeros((p.shape[0], 4), np.float32)
+    vp = np.array(viewpoint, np.float32)
+    lib().orc_estimate_normals(_f(p), p.shape[0], stride, float(radius), _f(vp), _f(out))
+    return out
+
+
+def regulate_normals(points, normals, seed_idx, seed_is_outward, radius):
+    p, stride = _xyz(points)
+    nrm = np.ascontiguousarray(normals, np.float32).copy()
+    assert nrm.shape == (p.shape[0], 4)
+    proc = np.zeros(p.shape[0], np.uint8)
+    cnt = lib().orc_regulate_normals(_f(p), p.shape[0], stride, _f(nrm), int(seed_idx),
+                                     int(bool(seed_is_outward)), float(radius),
+                                     proc.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return nrm, proc.astype(bool), int(cnt)

@@ -1,0 +1,625 @@
+/*
+ * pcl_oracle.c -- TEST INFRASTRUCTURE ONLY (see pcl_oracle.h for provenance and the
+ * pinning status).  Scalar C restatement of PCL 1.8 / Eigen 3.3 / Boost 1.64 semantics.
+ *
+ * Build: gcc -O2 -std=c11 -ffp-contract=off -fno-fast-math (x86-64 SSE scalar math, no FMA),
+ * which matches MSVC x64 /fp:precise code generation for the PCL build used by the reference
+ * (Dialog/PropertySheet-success.props:5-10: PCL 1.8, MSVC v140).
+ *
+ * Citations are to third-party sources ([PCL-1.8 ext], not vendored) unless they name a
+ * Dialog/ file, which are the reference call sites.
+ */
+#include "pcl_oracle.h"
+
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* Boost mt19937 + variate_generator<mt19937&, uniform_int<>(0, INT_MAX)>                       */
+/* pcl/sample_consensus/sac_model.h: SampleConsensusModel ctor seeds rng_alg_ with 12345u and   */
+/* rnd() returns (*rng_gen_)().  generate_uniform_int: brange = 2^32-1 > range = 2^31-1,        */
+/* bucket_size = 2 (brange % (range+1) == range), result = eng()/2 <= range always.             */
+/* ------------------------------------------------------------------------------------------ */
+void orc_mt_seed(orc_mt19937* g, uint32_t seed) {
+  g->mt[0] = seed;
+  for (int i = 1; i < 624; ++i)
+    g->mt[i] = 1812433253u * (g->mt[i - 1] ^ (g->mt[i - 1] >> 30)) + (uint32_t)i;
+  g->idx = 624;
+}
+
+static void orc_mt_twist(orc_mt19937* g) {
+  for (int i = 0; i < 624; ++i) {
+    uint32_t y = (g->mt[i] & 0x80000000u) | (g->mt[(i + 1) % 624] & 0x7fffffffu);
+    g->mt[i] = g->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+  g->idx = 0;
+}
+
+uint32_t orc_mt_next(orc_mt19937* g) {
+  if (g->idx >= 624) orc_mt_twist(g);
+  uint32_t y = g->mt[g->idx++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+int orc_rnd(orc_mt19937* g) { return (int)(orc_mt_next(g) >> 1); }
+
+/* ------------------------------------------------------------------------------------------ */
+/* SampleConsensusModelPlane                                                                   */
+/* ------------------------------------------------------------------------------------------ */
+/* isSampleGood: dy1dy2 = (p1-p0)/(p2-p0) (Array4f, lanes 0..2 matter);
+ * good iff (d0 != d1) || (d2 != d1)  (IEEE: NaN makes it "good"). */
+int orc_plane_sample_good(const float p0[3], const float p1[3], const float p2[3]) {
+  float d0 = (p1[0] - p0[0]) / (p2[0] - p0[0]);
+  float d1 = (p1[1] - p0[1]) / (p2[1] - p0[1]);
+  float d2 = (p1[2] - p0[2]) / (p2[2] - p0[2]);
+  return (d0 != d1) || (d2 != d1);
+}
+
+/* computeModelCoefficients: cross product in source order, VectorXf::normalize() with the
+ * Eigen-3.3 guard (z > 0) and SSE predux order (c0^2 + c2^2) + (c1^2 + c3^2), then
+ * d = -1 * ((c0 x0 + c2 z0) + (c1 y0 + c3 * 1)) with c3 == 0. */
+int orc_plane_coefficients(const float p0[3], const float p1[3], const float p2[3], float c[4]) {
+  float a0 = p1[0] - p0[0], a1 = p1[1] - p0[1], a2 = p1[2] - p0[2];
+  float b0 = p2[0] - p0[0], b1 = p2[1] - p0[1], b2 = p2[2] - p0[2];
+  float r0 = a0 / b0, r1 = a1 / b1, r2 = a2 / b2;
+  if ((r0 == r1) && (r2 == r1)) return 0; /* collinear */
+  float c0 = a1 * b2 - a2 * b1;
+  float c1 = a2 * b0 - a0 * b2;
+  float c2 = a0 * b1 - a1 * b0;
+  float c3 = 0.0f;
+  float z = (c0 * c0 + c2 * c2) + (c1 * c1 + c3 * c3);
+  if (z > 0.0f) {
+    float s = sqrtf(z);
+    c0 = c0 / s; c1 = c1 / s; c2 = c2 / s; c3 = c3 / s;
+  }
+  float dot = (c0 * p0[0] + c2 * p0[2]) + (c1 * p0[1] + c3 * 1.0f);
+  c[0] = c0; c[1] = c1; c[2] = c2; c[3] = -1.0f * dot;
+  return 1;
+}
+
+/* countWithinDistance / selectWithinDistance: fabs(model_coefficients.dot(Vector4f(x,y,z,1)))
+ * with the VectorXf(4) SSE predux order (c0 x + c2 z) + (c1 y + c3 * 1). */
+float orc_plane_abs_dist(const float c[4], float x, float y, float z) {
+  float d = (c[0] * x + c[2] * z) + (c[1] * y + c[3] * 1.0f);
+  return fabsf(d);
+}
+
+float orc_thr_ceil(double thr) {
+  float f = (float)thr;                 /* round to nearest */
+  if ((double)f < thr) f = nextafterf(f, INFINITY);
+  return f;
+}
+
+int64_t orc_count_within(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
+                         const float c[4], double thr) {
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + (int64_t)(idx ? idx[i] : i) * stride;
+    if ((double)orc_plane_abs_dist(c, p[0], p[1], p[2]) < thr) ++cnt;
+  }
+  return cnt;
+}
+
+static int64_t orc_select_within(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
+                                 const float c[4], double thr, int32_t* out) {
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t g = idx[i];
+    const float* p = xyz + (int64_t)g * stride;
+    if ((double)orc_plane_abs_dist(c, p[0], p[1], p[2]) < thr) out[k++] = g;
+  }
+  return k;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* pcl::computeMeanAndCovarianceMatrix (common/impl/centroid.hpp, dense branch), float.        */
+/* ------------------------------------------------------------------------------------------ */
+unsigned orc_mean_cov(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
+                      float cov[9], float centroid[4]) {
+  float a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + (int64_t)idx[i] * stride;
+    float x = p[0], y = p[1], z = p[2];
+    a[0] += x * x; a[1] += x * y; a[2] += x * z;
+    a[3] += y * y; a[4] += y * z; a[5] += z * z;
+    a[6] += x;     a[7] += y;     a[8] += z;
+  }
+  float cntf = (float)(size_t)n;
+  for (int k = 0; k < 9; ++k) a[k] = a[k] / cntf;
+  centroid[0] = a[6]; centroid[1] = a[7]; centroid[2] = a[8]; centroid[3] = 1.0f;
+  cov[0] = a[0] - a[6] * a[6];
+  cov[1] = a[1] - a[6] * a[7];
+  cov[2] = a[2] - a[6] * a[8];
+  cov[4] = a[3] - a[7] * a[7];
+  cov[5] = a[4] - a[7] * a[8];
+  cov[8] = a[5] - a[8] * a[8];
+  cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+  return (unsigned)n;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* pcl::computeRoots2 / computeRoots / eigen33 (common/impl/eigen.hpp), float.                  */
+/* ------------------------------------------------------------------------------------------ */
+static void orc_compute_roots2(float b, float c, float roots[3]) {
+  roots[0] = 0.0f;
+  float d = (float)((double)(b * b) - 4.0 * (double)c); /* Scalar(b * b - 4.0 * c) */
+  if (d < 0.0f) d = 0.0f;
+  float sd = sqrtf(d);
+  roots[2] = 0.5f * (b + sd);
+  roots[1] = 0.5f * (b - sd);
+}
+
+#define M(r, c) m[(r) * 3 + (c)]
+void orc_compute_roots(const float m[9], float roots[3]) {
+  float c0 = M(0, 0) * M(1, 1) * M(2, 2) + 2.0f * M(0, 1) * M(0, 2) * M(1, 2) -
+             M(0, 0) * M(1, 2) * M(1, 2) - M(1, 1) * M(0, 2) * M(0, 2) -
+             M(2, 2) * M(0, 1) * M(0, 1);
+  float c1 = M(0, 0) * M(1, 1) - M(0, 1) * M(0, 1) + M(0, 0) * M(2, 2) - M(0, 2) * M(0, 2) +
+             M(1, 1) * M(2, 2) - M(1, 2) * M(1, 2);
+  float c2 = M(0, 0) + M(1, 1) + M(2, 2);
+  if (fabsf(c0) < FLT_EPSILON) {
+    orc_compute_roots2(c2, c1, roots);
+  } else {
+    const float s_inv3 = (float)(1.0 / 3.0);
+    const float s_sqrt3 = sqrtf(3.0f);
+    float c2_over_3 = c2 * s_inv3;
+    float a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
+    if (a_over_3 > 0.0f) a_over_3 = 0.0f;
+    float half_b = 0.5f * (c0 + c2_over_3 * (2.0f * c2_over_3 * c2_over_3 - c1));
+    float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
+    if (q > 0.0f) q = 0.0f;
+    float rho = sqrtf(-a_over_3);
+    float theta = atan2f(sqrtf(-q), half_b) * s_inv3;
+    float cos_theta = cosf(theta);
+    float sin_theta = sinf(theta);
+    roots[0] = c2_over_3 + 2.0f * rho * cos_theta;
+    roots[1] = c2_over_3 - rho * (cos_theta + s_sqrt3 * sin_theta);
+    roots[2] = c2_over_3 - rho * (cos_theta - s_sqrt3 * sin_theta);
+    float t;
+    if (roots[0] >= roots[1]) { t = roots[0]; roots[0] = roots[1]; roots[1] = t; }
+    if (roots[1] >= roots[2]) {
+      t = roots[1]; roots[1] = roots[2]; roots[2] = t;
+      if (roots[0] >= roots[1]) { t = roots[0]; roots[0] = roots[1]; roots[1] = t; }
+    }
+    if (roots[0] <= 0.0f) orc_compute_roots2(c2, c1, roots);
+  }
+}
+
+/* Vector3f::squaredNorm(): Eigen's non-vectorised unroller gives x^2 + (y^2 + z^2). */
+static float sqn3(const float v[3]) { return v[0] * v[0] + (v[1] * v[1] + v[2] * v[2]); }
+static void cross3(const float* a, const float* b, float* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+void orc_eigen33(const float mat[9], float* eval, float evec[3]) {
+  float scale = 0.0f;
+  for (int k = 0; k < 9; ++k) { float v = fabsf(mat[k]); if (v > scale) scale = v; }
+  if (scale <= FLT_MIN) scale = 1.0f;
+  float m[9];
+  for (int k = 0; k < 9; ++k) m[k] = mat[k] / scale;
+  float roots[3];
+  orc_compute_roots(m, roots);
+  *eval = roots[0] * scale;
+  M(0, 0) -= roots[0]; M(1, 1) -= roots[0]; M(2, 2) -= roots[0];
+  float v1[3], v2[3], v3[3];
+  cross3(&M(0, 0), &M(1, 0), v1);
+  cross3(&M(0, 0), &M(2, 0), v2);
+  cross3(&M(1, 0), &M(2, 0), v3);
+  float l1 = sqn3(v1), l2 = sqn3(v2), l3 = sqn3(v3);
+  const float* v; float l;
+  if (l1 >= l2 && l1 >= l3) { v = v1; l = l1; }
+  else if (l2 >= l1 && l2 >= l3) { v = v2; l = l2; }
+  else { v = v3; l = l3; }
+  float s = sqrtf(l);
+  evec[0] = v[0] / s; evec[1] = v[1] / s; evec[2] = v[2] / s;
+}
+#undef M
+
+/* ---- double twin (fast-mode reference) ---- */
+#define M(r, c) m[(r) * 3 + (c)]
+static void orc_compute_roots2_d(double b, double c, double roots[3]) {
+  roots[0] = 0.0;
+  double d = b * b - 4.0 * c;
+  if (d < 0.0) d = 0.0;
+  double sd = sqrt(d);
+  roots[2] = 0.5 * (b + sd);
+  roots[1] = 0.5 * (b - sd);
+}
+static void orc_compute_roots_d(const double m[9], double roots[3]) {
+  double c0 = M(0, 0) * M(1, 1) * M(2, 2) + 2.0 * M(0, 1) * M(0, 2) * M(1, 2) -
+              M(0, 0) * M(1, 2) * M(1, 2) - M(1, 1) * M(0, 2) * M(0, 2) -
+              M(2, 2) * M(0, 1) * M(0, 1);
+  double c1 = M(0, 0) * M(1, 1) - M(0, 1) * M(0, 1) + M(0, 0) * M(2, 2) - M(0, 2) * M(0, 2) +
+              M(1, 1) * M(2, 2) - M(1, 2) * M(1, 2);
+  double c2 = M(0, 0) + M(1, 1) + M(2, 2);
+  if (fabs(c0) < DBL_EPSILON) {
+    orc_compute_roots2_d(c2, c1, roots);
+  } else {
+    const double s_inv3 = 1.0 / 3.0, s_sqrt3 = sqrt(3.0);
+    double c2_over_3 = c2 * s_inv3;
+    double a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
+    if (a_over_3 > 0.0) a_over_3 = 0.0;
+    double half_b = 0.5 * (c0 + c2_over_3 * (2.0 * c2_over_3 * c2_over_3 - c1));
+    double q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
+    if (q > 0.0) q = 0.0;
+    double rho = sqrt(-a_over_3);
+    double theta = atan2(sqrt(-q), half_b) * s_inv3;
+    double ct = cos(theta), st = sin(theta);
+    roots[0] = c2_over_3 + 2.0 * rho * ct;
+    roots[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
+    roots[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
+    double t;
+    if (roots[0] >= roots[1]) { t = roots[0]; roots[0] = roots[1]; roots[1] = t; }
+    if (roots[1] >= roots[2]) {
+      t = roots[1]; roots[1] = roots[2]; roots[2] = t;
+      if (roots[0] >= roots[1]) { t = roots[0]; roots[0] = roots[1]; roots[1] = t; }
+    }
+    if (roots[0] <= 0.0) orc_compute_roots2_d(c2, c1, roots);
+  }
+}
+void orc_eigen33_d(const double mat[9], double* eval, double evec[3]) {
+  double scale = 0.0;
+  for (int k = 0; k < 9; ++k) { double v = fabs(mat[k]); if (v > scale) scale = v; }
+  if (scale <= DBL_MIN) scale = 1.0;
+  double m[9];
+  for (int k = 0; k < 9; ++k) m[k] = mat[k] / scale;
+  double roots[3];
+  orc_compute_roots_d(m, roots);
+  *eval = roots[0] * scale;
+  M(0, 0) -= roots[0]; M(1, 1) -= roots[0]; M(2, 2) -= roots[0];
+  double v[3][3];
+  const double* r0 = &M(0, 0); const double* r1 = &M(1, 0); const double* r2 = &M(2, 0);
+  v[0][0] = r0[1] * r1[2] - r0[2] * r1[1]; v[0][1] = r0[2] * r1[0] - r0[0] * r1[2]; v[0][2] = r0[0] * r1[1] - r0[1] * r1[0];
+  v[1][0] = r0[1] * r2[2] - r0[2] * r2[1]; v[1][1] = r0[2] * r2[0] - r0[0] * r2[2]; v[1][2] = r0[0] * r2[1] - r0[1] * r2[0];
+  v[2][0] = r1[1] * r2[2] - r1[2] * r2[1]; v[2][1] = r1[2] * r2[0] - r1[0] * r2[2]; v[2][2] = r1[0] * r2[1] - r1[1] * r2[0];
+  double l[3];
+  for (int k = 0; k < 3; ++k) l[k] = v[k][0] * v[k][0] + (v[k][1] * v[k][1] + v[k][2] * v[k][2]);
+  int b = (l[0] >= l[1] && l[0] >= l[2]) ? 0 : ((l[1] >= l[0] && l[1] >= l[2]) ? 1 : 2);
+  double s = sqrt(l[b]);
+  evec[0] = v[b][0] / s; evec[1] = v[b][1] / s; evec[2] = v[b][2] / s;
+}
+#undef M
+
+/* Least-squares plane in double: two-pass centroid and covariance, eigen33 in double.
+ * Same "< 4 inliers keeps the model" rule as optimizeModelCoefficients. */
+int orc_refit_double(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
+                     const float coeff_in[4], float coeff_out[4]) {
+  if (n < 4) { memcpy(coeff_out, coeff_in, 4 * sizeof(float)); return 0; }
+  double cx = 0, cy = 0, cz = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + (int64_t)idx[i] * stride;
+    cx += p[0]; cy += p[1]; cz += p[2];
+  }
+  cx /= (double)n; cy /= (double)n; cz /= (double)n;
+  double c[9] = {0};
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + (int64_t)idx[i] * stride;
+    double dx = p[0] - cx, dy = p[1] - cy, dz = p[2] - cz;
+    c[0] += dx * dx; c[1] += dx * dy; c[2] += dx * dz;
+    c[4] += dy * dy; c[5] += dy * dz; c[8] += dz * dz;
+  }
+  for (int k = 0; k < 9; ++k) c[k] /= (double)n;
+  c[3] = c[1]; c[6] = c[2]; c[7] = c[5];
+  double ev, v[3];
+  orc_eigen33_d(c, &ev, v);
+  double d = -(v[0] * cx + v[1] * cy + v[2] * cz);
+  coeff_out[0] = (float)v[0]; coeff_out[1] = (float)v[1]; coeff_out[2] = (float)v[2];
+  coeff_out[3] = (float)d;
+  return 1;
+}
+
+/* optimizeModelCoefficients (sac_model_plane.hpp): < 4 inliers keep the coefficients; else
+ * float mean/cov, eigen33, coeff = (v, 0), coeff[3] = -1 * coeff.dot(centroid). */
+static void orc_optimize_plane(const float* xyz, int64_t stride, const int32_t* inl, int64_t n,
+                               const float cin[4], float cout[4]) {
+  if (n < 4) { memcpy(cout, cin, 4 * sizeof(float)); return; }
+  float cov[9], cen[4], ev, v[3];
+  orc_mean_cov(xyz, stride, inl, n, cov, cen);
+  orc_eigen33(cov, &ev, v);
+  float c3 = 0.0f;
+  float dot = (v[0] * cen[0] + v[2] * cen[2]) + (v[1] * cen[1] + c3 * cen[3]);
+  cout[0] = v[0]; cout[1] = v[1]; cout[2] = v[2]; cout[3] = -1.0f * dot;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SACSegmentation::segment -> RandomSampleConsensus::computeModel (sac_segmentation.hpp,      */
+/* ransac.hpp), SampleConsensusModel::getSamples / drawIndexSample (sac_model.h/.hpp).          */
+/* ------------------------------------------------------------------------------------------ */
+int orc_sac_segment(const float* xyz, int64_t n_points, int64_t stride,
+                    const int32_t* indices, int64_t n_idx, const orc_sac_params* prm,
+                    float coeff[4], int32_t* inliers_out, int64_t* n_inliers, orc_sac_stats* st) {
+  orc_sac_stats dummy;
+  if (!st) st = &dummy;
+  memset(st, 0, sizeof(*st));
+  memset(coeff, 0, 4 * sizeof(float));
+  *n_inliers = 0;
+  if (!indices) n_idx = n_points;
+  int32_t* idx = (int32_t*)malloc((size_t)(n_idx > 0 ? n_idx : 1) * sizeof(int32_t));
+  int32_t* shuf = (int32_t*)malloc((size_t)(n_idx > 0 ? n_idx : 1) * sizeof(int32_t));
+  for (int64_t i = 0; i < n_idx; ++i) idx[i] = indices ? indices[i] : (int32_t)i;
+  memcpy(shuf, idx, (size_t)n_idx * sizeof(int32_t));
+
+  orc_mt19937 g;
+  orc_mt_seed(&g, prm->seed);
+  const double thr = prm->threshold;
+  int iterations = 0;
+  int best = -INT_MAX;
+  double k = 1.0;
+  double log_probability = log(1.0 - prm->probability);
+  double one_over_indices = 1.0 / (double)n_idx;
+  unsigned skipped = 0;
+  const unsigned max_skip = (unsigned)prm->max_iterations * 10u;
+  int have = 0;
+  float best_c[4] = {0, 0, 0, 0};
+  int32_t best_s[3] = {0, 0, 0};
+
+  if (thr == DBL_MAX) goto done; /* "No threshold set!" */
+  while (iterations < k && skipped < max_skip) {
+    int32_t s[3];
+    int found = 0;
+    if (n_idx < 3) { iterations = INT_MAX - 1; break; } /* getSamples: cannot select 3 points */
+    for (unsigned t = 0; t < 1000u; ++t) {                 /* max_sample_checks_ */
+      for (int i = 0; i < 3; ++i) {
+        size_t j = (size_t)i + ((size_t)orc_rnd(&g) % (size_t)(n_idx - i));
+        int32_t tmp = shuf[i]; shuf[i] = shuf[j]; shuf[j] = tmp;
+      }
+      st->draws++;
+      s[0] = shuf[0]; s[1] = shuf[1]; s[2] = shuf[2];
+      if (orc_plane_sample_good(xyz + (int64_t)s[0] * stride, xyz + (int64_t)s[1] * stride,
+                                xyz + (int64_t)s[2] * stride)) { found = 1; break; }
+    }
+    if (!found) break; /* "No samples could be selected!" */
+    float c[4];
+    if (!orc_plane_coefficients(xyz + (int64_t)s[0] * stride, xyz + (int64_t)s[1] * stride,
+                                xyz + (int64_t)s[2] * stride, c)) { ++skipped; continue; }
+    int n = (int)orc_count_within(xyz, stride, idx, n_idx, c, thr);
+    if (n > best) {
+      best = n;
+      have = 1;
+      memcpy(best_c, c, sizeof(best_c));
+      memcpy(best_s, s, sizeof(best_s));
+      double w = (double)best * one_over_indices;
+      double p_no_outliers = 1.0 - pow(w, 3.0);
+      if (p_no_outliers < DBL_EPSILON) p_no_outliers = DBL_EPSILON;
+      if (p_no_outliers > 1.0 - DBL_EPSILON) p_no_outliers = 1.0 - DBL_EPSILON;
+      k = log_probability / log(p_no_outliers);
+    }
+    ++iterations;
+    if (iterations > prm->max_iterations) break;
+  }
+done:
+  st->iterations = iterations;
+  st->skipped = (int)skipped;
+  if (have) {
+    st->has_model = 1;
+    memcpy(st->best_sample, best_s, sizeof(best_s));
+    memcpy(st->coeff_unrefined, best_c, sizeof(best_c));
+    int64_t nin = orc_select_within(xyz, stride, idx, n_idx, best_c, thr, inliers_out);
+    st->n_unrefined = nin;
+    if (prm->optimize) {
+      float rc[4];
+      if (prm->refit_double) orc_refit_double(xyz, stride, inliers_out, nin, best_c, rc);
+      else orc_optimize_plane(xyz, stride, inliers_out, nin, best_c, rc);
+      memcpy(coeff, rc, sizeof(rc));
+      nin = orc_select_within(xyz, stride, idx, n_idx, rc, thr, inliers_out);
+    } else {
+      memcpy(coeff, best_c, sizeof(best_c));
+    }
+    *n_inliers = nin;
+  }
+  free(idx);
+  free(shuf);
+  return have;
+}
+
+int orc_extract_planes(const float* xyz, int64_t n_points, int64_t stride,
+                       const orc_sac_params* prm, int max_planes, int64_t min_inliers,
+                       float* coeffs, int64_t* offsets, int32_t* inliers, int* n_planes) {
+  int32_t* rem = (int32_t*)malloc((size_t)(n_points > 0 ? n_points : 1) * sizeof(int32_t));
+  int32_t* buf = (int32_t*)malloc((size_t)(n_points > 0 ? n_points : 1) * sizeof(int32_t));
+  int64_t n_rem = n_points;
+  for (int64_t i = 0; i < n_points; ++i) rem[i] = (int32_t)i;
+  int64_t total = 0;
+  int np = 0;
+  offsets[0] = 0;
+  int64_t floor_n = min_inliers > 3 ? min_inliers : 3;
+  while (np < max_planes && n_rem >= floor_n) {
+    float c[4];
+    int64_t nin = 0;
+    int ok = orc_sac_segment(xyz, n_points, stride, rem, n_rem, prm, c, buf, &nin, NULL);
+    if (!ok || nin == 0 || nin < min_inliers) break;
+    memcpy(coeffs + 4 * np, c, sizeof(c));
+    memcpy(inliers + total, buf, (size_t)nin * sizeof(int32_t));
+    /* remove (both lists ascending) */
+    int64_t w = 0, j = 0;
+    for (int64_t i = 0; i < n_rem; ++i) {
+      if (j < nin && rem[i] == buf[j]) { ++j; continue; }
+      rem[w++] = rem[i];
+    }
+    n_rem = w;
+    total += nin;
+    ++np;
+    offsets[np] = total;
+  }
+  *n_planes = np;
+  free(rem);
+  free(buf);
+  return np;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Normals: NormalEstimation(OMP)::computeFeature with radius search (features/impl/normal_3d) */
+/* called at Dialog/PlaneDetect.h:529-535.  Neighbour search = KdTreeFLANN::radiusSearch:       */
+/* dist2 = ((0 + dx^2) + dy^2) + dz^2 with d = query - point, kept iff dist2 < (float)(r*r),     */
+/* results sorted by (dist2, index).  A uniform grid (cell = r) finds the same set exactly.     */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { float d; int32_t j; } orc_nb;
+static int orc_nb_cmp(const void* a, const void* b) {
+  const orc_nb* x = (const orc_nb*)a; const orc_nb* y = (const orc_nb*)b;
+  if (x->d < y->d) return -1;
+  if (x->d > y->d) return 1;
+  return (x->j > y->j) - (x->j < y->j);
+}
+
+typedef struct {
+  float minx, miny, minz, cell;
+  int64_t gx, gy, gz;
+  int64_t* start;   /* gx*gy*gz + 1 */
+  int32_t* order;   /* point ids sorted by cell */
+} orc_grid;
+
+static int64_t orc_cell_of(const orc_grid* G, float v, float lo, int64_t gdim) {
+  int64_t c = (int64_t)floor(((double)v - (double)lo) / (double)G->cell);
+  if (c < 0) c = 0;
+  if (c >= gdim) c = gdim - 1;
+  return c;
+}
+
+static void orc_grid_build(orc_grid* G, const float* xyz, int64_t n, int64_t stride, float r) {
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) {
+      float v = xyz[i * stride + k];
+      if (v < mn[k]) mn[k] = v;
+      if (v > mx[k]) mx[k] = v;
+    }
+  G->minx = mn[0]; G->miny = mn[1]; G->minz = mn[2];
+  G->cell = r;
+  int64_t dims[3];
+  for (int k = 0; k < 3; ++k) {
+    double ext = n > 0 ? ((double)mx[k] - (double)mn[k]) / (double)r : 0.0;
+    dims[k] = (int64_t)floor(ext) + 1;
+    if (dims[k] < 1) dims[k] = 1;
+    if (dims[k] > 1024) dims[k] = 1024;
+  }
+  /* clamp total cells */
+  while (dims[0] * dims[1] * dims[2] > (int64_t)1 << 24) {
+    G->cell *= 2.0f;
+    for (int k = 0; k < 3; ++k) dims[k] = (dims[k] + 1) / 2;
+  }
+  G->gx = dims[0]; G->gy = dims[1]; G->gz = dims[2];
+  int64_t nc = G->gx * G->gy * G->gz;
+  G->start = (int64_t*)calloc((size_t)nc + 1, sizeof(int64_t));
+  G->order = (int32_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
+  int64_t* cid = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + i * stride;
+    int64_t cx = orc_cell_of(G, p[0], G->minx, G->gx), cy = orc_cell_of(G, p[1], G->miny, G->gy),
+            cz = orc_cell_of(G, p[2], G->minz, G->gz);
+    cid[i] = (cz * G->gy + cy) * G->gx + cx;
+    G->start[cid[i] + 1]++;
+  }
+  for (int64_t c = 0; c < nc; ++c) G->start[c + 1] += G->start[c];
+  int64_t* fill = (int64_t*)malloc((size_t)nc * sizeof(int64_t));
+  memcpy(fill, G->start, (size_t)nc * sizeof(int64_t));
+  for (int64_t i = 0; i < n; ++i) G->order[fill[cid[i]]++] = (int32_t)i;
+  free(fill);
+  free(cid);
+}
+
+static void orc_grid_free(orc_grid* G) { free(G->start); free(G->order); }
+
+/* exact radius neighbours of query q, sorted by (dist2, index); returns count */
+static int64_t orc_radius(const orc_grid* G, const float* xyz, int64_t stride, const float q[3],
+                          float r2, orc_nb** buf, int64_t* cap) {
+  int64_t cx = orc_cell_of(G, q[0], G->minx, G->gx), cy = orc_cell_of(G, q[1], G->miny, G->gy),
+          cz = orc_cell_of(G, q[2], G->minz, G->gz);
+  int64_t k = 0;
+  /* cell >= r, so the 27-neighbourhood covers the ball except for points clamped into the
+   * border cells; clamping only merges cells, never drops a point within r. */
+  for (int64_t dz = -1; dz <= 1; ++dz)
+    for (int64_t dy = -1; dy <= 1; ++dy)
+      for (int64_t dx = -1; dx <= 1; ++dx) {
+        int64_t x = cx + dx, y = cy + dy, z = cz + dz;
+        if (x < 0 || y < 0 || z < 0 || x >= G->gx || y >= G->gy || z >= G->gz) continue;
+        int64_t c = (z * G->gy + y) * G->gx + x;
+        for (int64_t t = G->start[c]; t < G->start[c + 1]; ++t) {
+          int32_t j = G->order[t];
+          const float* p = xyz + (int64_t)j * stride;
+          float ex = q[0] - p[0], ey = q[1] - p[1], ez = q[2] - p[2];
+          float d = ((0.0f + ex * ex) + ey * ey) + ez * ez;
+          if (d < r2) {
+            if (k == *cap) { *cap = *cap * 2 + 64; *buf = (orc_nb*)realloc(*buf, (size_t)*cap * sizeof(orc_nb)); }
+            (*buf)[k].d = d; (*buf)[k].j = j; ++k;
+          }
+        }
+      }
+  qsort(*buf, (size_t)k, sizeof(orc_nb), orc_nb_cmp);
+  return k;
+}
+
+void orc_estimate_normals(const float* xyz, int64_t n, int64_t stride, float radius,
+                          const float vp[3], float* out) {
+  orc_grid G;
+  orc_grid_build(&G, xyz, n, stride, radius);
+  float r2 = (float)((double)radius * (double)radius);
+  orc_nb* nb = NULL; int64_t cap = 0;
+  int32_t* ids = NULL; int64_t idcap = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + i * stride;
+    int64_t k = orc_radius(&G, xyz, stride, p, r2, &nb, &cap);
+    float* o = out + 4 * i;
+    if (k < 3) { o[0] = o[1] = o[2] = o[3] = NAN; continue; }
+    if (k > idcap) { idcap = k; ids = (int32_t*)realloc(ids, (size_t)idcap * sizeof(int32_t)); }
+    for (int64_t t = 0; t < k; ++t) ids[t] = nb[t].j;
+    float cov[9], cen[4], ev, v[3];
+    orc_mean_cov(xyz, stride, ids, k, cov, cen);
+    orc_eigen33(cov, &ev, v);
+    float eig_sum = cov[0] + cov[4] + cov[8];
+    float curv = eig_sum != 0.0f ? fabsf(ev / eig_sum) : 0.0f;
+    float vx = vp[0] - p[0], vy = vp[1] - p[1], vz = vp[2] - p[2];
+    float cos_theta = vx * v[0] + vy * v[1] + vz * v[2];
+    if (cos_theta < 0.0f) { v[0] *= -1.0f; v[1] *= -1.0f; v[2] *= -1.0f; }
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = curv;
+  }
+  free(nb); free(ids);
+  orc_grid_free(&G);
+}
+
+/* Dialog/PlaneDetect.h:547-665 (first-round branch; the second-round 1-NN branch at :553-584
+ * is not part of this oracle). normals: 4 floats per point. Returns #processed points. */
+int64_t orc_regulate_normals(const float* xyz, int64_t n, int64_t stride, float* normals,
+                             int64_t seed_idx, int seed_is_outward, float radius,
+                             uint8_t* processed) {
+  if (seed_idx < 0 || seed_idx >= n) return 0;   /* "invalid point index" */
+  memset(processed, 0, (size_t)n);
+  orc_grid G;
+  orc_grid_build(&G, xyz, n, stride, radius);
+  float r2 = (float)((double)radius * (double)radius);
+  if (!seed_is_outward) {
+    float* s = normals + 4 * seed_idx;
+    s[0] *= -1.0f; s[1] *= -1.0f; s[2] *= -1.0f;
+  }
+  processed[seed_idx] = 1;
+  int32_t* Q = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+  int64_t qh = 0, qt = 0, cnt = 1;
+  Q[qt++] = (int32_t)seed_idx;
+  orc_nb* nb = NULL; int64_t cap = 0;
+  while (qh < qt) {
+    int32_t cur = Q[qh++];
+    int64_t k = orc_radius(&G, xyz, stride, xyz + (int64_t)cur * stride, r2, &nb, &cap);
+    for (int64_t t = 0; t < k; ++t) {
+      int32_t j = nb[t].j;
+      if (processed[j]) continue;
+      const float* pc = normals + 4 * (int64_t)cur;
+      float* pn = normals + 4 * (int64_t)j;
+      float dp = pc[0] * pn[0] + pc[1] * pn[1] + pc[2] * pn[2];
+      if (dp < 0.0f) { pn[0] *= -1.0f; pn[1] *= -1.0f; pn[2] *= -1.0f; }
+      processed[j] = 1;
+      ++cnt;
+      Q[qt++] = j;
+    }
+  }
+  free(Q); free(nb);
+  orc_grid_free(&G);
+  return cnt;
+}

@@ -1,0 +1,108 @@
+/*
+ * pcl_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the PCL-1.8 arithmetic behind the RANSAC plane path that
+ * the MI355X product (dialog_amd/) replaces.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this; the product never links it.
+ *
+ * Provenance / pinning status (see DESIGN.md "Oracle"):
+ *   - The reference (czh55/Dialog) has no RANSAC plane code and no tests; the
+ *     arithmetic lives in third-party PCL 1.8 (+ Eigen 3.3, Boost 1.64), which is
+ *     not vendored under /root/reference and cannot be built here.
+ *     Reference call sites: Dialog/SimplifyVerticesSize.cpp:62-67 (SACSegmentation),
+ *     Dialog/PlaneDetect.h:529-535 (NormalEstimationOMP), PlaneDetect.h:547-665
+ *     (regulateNormal).
+ *   - PINNED: the RNG stream (mt19937 seeded 12345u) against libstdc++
+ *     std::mt19937 and numpy's MT19937 (tests/golden/rng_kat.json).
+ *   - UNPINNED ("parity unpinned" for the PCL arithmetic): op order of Eigen's SSE
+ *     predux, PCL's RANSAC loop and eigen33 are restated from the published PCL
+ *     1.8 / Eigen 3.3 sources; no reference output exists to check them against.
+ *     A second, independent numpy restatement (oracle/numpy_twin.py) cross-checks
+ *     this C code bit-for-bit.
+ */
+#ifndef DIALOG_PCL_ORACLE_H
+#define DIALOG_PCL_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- Boost.Random mt19937 + uniform_int<>(0, INT_MAX) (SampleConsensusModel::rnd) ---- */
+typedef struct { uint32_t mt[624]; int idx; } orc_mt19937;
+void     orc_mt_seed(orc_mt19937* g, uint32_t seed);
+uint32_t orc_mt_next(orc_mt19937* g);
+int      orc_rnd(orc_mt19937* g);          /* == mt() >> 1 (bucket size 2, never rejects) */
+
+/* ---- SampleConsensusModelPlane primitives (pcl/sample_consensus/impl/sac_model_plane.hpp) ---- */
+int   orc_plane_sample_good(const float p0[3], const float p1[3], const float p2[3]);
+int   orc_plane_coefficients(const float p0[3], const float p1[3], const float p2[3], float c[4]);
+float orc_plane_abs_dist(const float c[4], float x, float y, float z);
+/* smallest float >= thr: (double)|d| < thr  <=>  |d| < orc_thr_ceil(thr) */
+float orc_thr_ceil(double thr);
+
+/* ---- pcl::computeMeanAndCovarianceMatrix (float, single pass, index order) + eigen33 ---- */
+unsigned orc_mean_cov(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
+                      float cov[9], float centroid[4]);
+void orc_compute_roots(const float m[9], float roots[3]);
+void orc_eigen33(const float m[9], float* eval, float evec[3]);
+/* double-precision twin (fast-mode reference): two-pass centroid + covariance, eigen33 in double */
+void orc_eigen33_d(const double m[9], double* eval, double evec[3]);
+int  orc_refit_double(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
+                      const float coeff_in[4], float coeff_out[4]);
+
+/* ---- SACSegmentation<PointXYZ>::segment with SACMODEL_PLANE / SAC_RANSAC ---- */
+typedef struct {
+  double   threshold;        /* setDistanceThreshold */
+  int      max_iterations;   /* setMaxIterations (PCL default 50) */
+  double   probability;      /* setProbability (default 0.99) */
+  int      optimize;         /* setOptimizeCoefficients (default true) */
+  uint32_t seed;             /* 12345u unless random_ */
+  int      refit_double;     /* 0: PCL float refit; 1: double-exact refit (fast-mode twin) */
+} orc_sac_params;
+
+typedef struct {
+  int     iterations;        /* RandomSampleConsensus::iterations_ at exit */
+  int     skipped;
+  int64_t draws;             /* drawIndexSample calls */
+  int32_t best_sample[3];    /* global indices of the winning triple */
+  float   coeff_unrefined[4];
+  int64_t n_unrefined;       /* inliers of the unrefined model */
+  int     has_model;
+} orc_sac_stats;
+
+/* returns 1 if a model was found (PCL: computeModel true). inliers_out needs capacity n_idx
+ * (or n_points when indices == NULL). "No model" leaves *n_inliers = 0 and coeff zeroed. */
+int orc_sac_segment(const float* xyz, int64_t n_points, int64_t stride,
+                    const int32_t* indices, int64_t n_idx, const orc_sac_params* prm,
+                    float coeff[4], int32_t* inliers_out, int64_t* n_inliers, orc_sac_stats* st);
+
+/* sequential extract-and-remove (analogue of the reference's re-run loop,
+ * PCLViewer.cpp:1120-1177 / PlaneDetect.h:1500-1573): round r segments the ascending
+ * remaining-index list (RNG reseeded each round), records the plane and removes its inliers.
+ * Stops when fewer than max(3, min_inliers) points remain, when no model is found or when a
+ * plane has fewer than min_inliers inliers (that plane is not recorded). */
+int orc_extract_planes(const float* xyz, int64_t n_points, int64_t stride,
+                       const orc_sac_params* prm, int max_planes, int64_t min_inliers,
+                       float* coeffs /* 4*max_planes */, int64_t* offsets /* max_planes+1 */,
+                       int32_t* inliers /* n_points */, int* n_planes);
+
+/* count within distance for an arbitrary list of hypotheses (CPU baseline leg) */
+int64_t orc_count_within(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
+                         const float c[4], double thr);
+
+/* ---- NormalEstimation (radius search) + flipNormalTowardsViewpoint; regulateNormal BFS ---- */
+/* normals_out: 4 floats per point (nx, ny, nz, curvature); NaN when < 3 neighbours.
+ * Neighbours: all j with dist2(i,j) < r*r (FLANN L2, ((dx^2+dy^2)+dz^2)), sorted by (dist2, j). */
+void orc_estimate_normals(const float* xyz, int64_t n, int64_t stride, float radius,
+                          const float vp[3], float* normals_out);
+/* PlaneDetect.h:547-665 first-round branch: seed flip, BFS over radius neighbours (sorted). */
+int64_t orc_regulate_normals(const float* xyz, int64_t n, int64_t stride, float* normals,
+                             int64_t seed_idx, int seed_is_outward, float radius,
+                             uint8_t* processed_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,38 @@
+// Smoke program for the C++ host shim (include/dialog/sac_segmentation.hpp), written the way the
+// reference calls PCL (Dialog/SimplifyVerticesSize.cpp:62-67).  Without a GPU it must fail loudly
+// (exit 3 = no device); with one it prints "coeff a b c d n_inliers".
+#include <dialog/sac_segmentation.hpp>
+
+#include <cmath>
+#include <cstdio>
+
+int main(int argc, char** argv) {
+  pcl::PointCloud<pcl::PointXYZ>::Ptr cloud(new pcl::PointCloud<pcl::PointXYZ>);
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 64; ++j) cloud->push_back(pcl::PointXYZ(0.1f * i, 0.1f * j, 0.01f * std::sin(0.3f * i * j)));
+  for (int k = 0; k < 500; ++k) cloud->push_back(pcl::PointXYZ(0.013f * k, 0.007f * k, 1.0f + 0.002f * k));
+  try {
+    dialog::SACSegmentation<pcl::PointXYZ> seg;
+    seg.setOptimizeCoefficients(true);
+    seg.setModelType(pcl::SACMODEL_PLANE);
+    seg.setMethodType(pcl::SAC_RANSAC);
+    seg.setDistanceThreshold(0.02);
+    seg.setInputCloud(cloud);
+    pcl::PointIndices inliers;
+    pcl::ModelCoefficients coeff;
+    seg.segment(inliers, coeff);
+    if (coeff.values.size() != 4) return 4;
+    std::printf("coeff %.9g %.9g %.9g %.9g %zu\n", coeff.values[0], coeff.values[1], coeff.values[2],
+                coeff.values[3], inliers.indices.size());
+    std::vector<dialog::PlaneResult> planes;
+    dialog::ExtractParams ep;
+    ep.threshold = 0.02;
+    ep.min_inliers = 100;
+    dialog::extractPlanes(*cloud, ep, planes);
+    std::printf("planes %zu\n", planes.size());
+    return 0;
+  } catch (const dialog::Error& e) {
+    std::fprintf(stderr, "dialog error: %s\n", e.what());
+    return (int)e.status;
+  }
+}
