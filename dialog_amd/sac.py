@@ -10,8 +10,10 @@ plane_clouds slot (Dialog/PlaneDetect.h:100, :667-1355).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import threading
+import weakref
 
 import numpy as np
 
@@ -21,6 +23,26 @@ from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, DLG_SACMODEL_PLANE, DialogError
 SACMODEL_PLANE = 0
 SACMODEL_NORMAL_PLANE = 11
 SAC_RANSAC = 0
+
+
+# Live device objects, closed at interpreter exit before the HIP runtime's own static destructors
+# run (a hipFree after runtime teardown crashes).  Clouds first, then contexts.
+_LIVE_CLOUDS: "weakref.WeakSet" = weakref.WeakSet()
+_LIVE_CTXS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    for obj in list(_LIVE_CLOUDS):
+        try:
+            obj.close()
+        except Exception:
+            pass
+    for obj in list(_LIVE_CTXS):
+        try:
+            obj.close()
+        except Exception:
+            pass
 
 
 def _f32p(a):
@@ -53,6 +75,7 @@ class Context:
         r, w, d = C.c_int(), C.c_int(), C.c_int()
         _lib.check(self._L.dlg_ctx_info(self.h, C.byref(r), C.byref(w), C.byref(d)), self.h)
         self.rank, self.world, self.device = r.value, w.value, d.value
+        _LIVE_CTXS.add(self)
 
     @classmethod
     def distributed(cls, device, rank, world, unique_id: bytes):
@@ -122,6 +145,7 @@ class Cloud:
                                               C.byref(h)))
             self.n = arr.shape[0]
         self.h = h
+        _LIVE_CLOUDS.add(self)
 
     def reset(self):
         self.ctx.check(self.ctx._L.dlg_cloud_reset(self.h))
@@ -134,7 +158,8 @@ class Cloud:
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
-            self.ctx._L.dlg_cloud_destroy(self.h)
+            if self.ctx.h.value:  # a closed context already released the device
+                self.ctx._L.dlg_cloud_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):
