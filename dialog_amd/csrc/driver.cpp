@@ -25,6 +25,8 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -178,6 +180,13 @@ struct dlg_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<int32_t> h_inl;
   std::vector<float> h_xyz;
+  // inlier ids of the previous extract round: D2H into pinned staging is enqueued behind the
+  // round's select, the memcpy into the caller's buffer runs while the next round's scoring
+  // kernel executes (the host would otherwise only wait for it)
+  PinBuf<int32_t> h_stage;
+  hipEvent_t ev_stage = nullptr;
+  int32_t* pending_dst = nullptr;
+  int64_t pending_n = 0;
 };
 
 struct dlg_cloud {
@@ -197,6 +206,18 @@ struct dlg_cloud {
 namespace {
 
 void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
+
+// DLG_TRACE=1: per-round host timing breakdown on stderr (diagnostics only)
+bool trace_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLG_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 void sync(dlg_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); }
 
@@ -261,6 +282,14 @@ float event_ms(dlg_ctx* c, int a, int b) {
   return ms;
 }
 
+void drain_pending(dlg_ctx* c) {
+  if (!c->pending_dst) return;
+  HIPCHK(hipEventSynchronize(c->ev_stage));
+  std::memcpy(c->pending_dst, c->h_stage.p, (size_t)c->pending_n * 4);
+  c->pending_dst = nullptr;
+  c->pending_n = 0;
+}
+
 struct SegOut {
   bool has_model = false;
   float coeff[4] = {0, 0, 0, 0};
@@ -318,6 +347,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     const int D = (int)std::min<int64_t>(cap_h, remaining + (iterations ? 8 : 0));
 
     // ---- host: drawIndexSample over positions
+    const double t_draw0 = trace_on() ? now_ms() : 0.0;
     c->h_pos.ensure(3 * (size_t)D);
     int32_t* hp = c->h_pos.p;
     for (int d = 0; d < D; ++d) {
@@ -329,32 +359,39 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       hp[3 * d + 1] = ov.get(1);
       hp[3 * d + 2] = ov.get(2);
     }
+    const double t_draw1 = trace_on() ? now_ms() : 0.0;
     // ---- device: gather, build, score
     c->pos.ensure(3 * (size_t)D);
     c->samples.ensure(3 * (size_t)D);
-    c->hyps.ensure(D);
-    c->res.ensure(2 * (size_t)D);
+    c->hyps.ensure(kHypScratchBytes / sizeof(HypRec) + 1);
+    c->res.ensure(2 * (size_t)kMaxHypPerLaunch + 64);
     HIPCHK(hipMemcpyAsync(c->pos.p, hp, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
     launch_gather_samples(c->pos.p, 3 * D, offset, src, c->samples.p, c->stream);
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->samples.p, 12 * (size_t)D, DType::I32, c->stream);
+    // res = counts[Dp] | good[D]  (Dp = D rounded up to the 64-hypothesis groups of k_score)
+    const int Dp = (D + 63) / 64 * 64;
     launch_build_hyps(c->samples.p, D, cthr, cl->amax[0], cl->amax[1], cl->amax[2], c->hyps.p,
-                      c->res.p + D, c->stream);
-    HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)D, c->stream));
+                      c->res.p + Dp, c->stream);
+    HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    launch_score(src, c->hyps.p, D, cthr, c->res.p, kScoreExact, c->num_cus, c->stream);
+    launch_score(src, c->hyps.p, D, cthr, c->res.p, kScoreDefault, c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
-    c->h_res.ensure(2 * (size_t)D);
-    HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 8 * (size_t)D, hipMemcpyDeviceToHost, c->stream));
+    c->h_res.ensure((size_t)Dp + D);
+    HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 4 * ((size_t)Dp + D), hipMemcpyDeviceToHost, c->stream));
     sync(c);
+    if (trace_on())
+      std::fprintf(stderr, "[dlg] N=%lld D=%d draw=%.3fms score+wait=%.3fms\n", (long long)N, D,
+                   t_draw1 - t_draw0, now_ms() - t_draw1);
     ++launches;
     st->tests_scored += (int64_t)D * N;
     if (c->profiling) st->score_ms += event_ms(c, 0, 1);
 
     // ---- host: computeModel replay over the batch
     const int32_t* cnt = c->h_res.p;
-    const int32_t* good = c->h_res.p + D;
+    const int32_t* good = c->h_res.p + Dp;
     int best_d = -1;
     for (int d = 0; d < D && !done; ++d) {
       st->draws++;
@@ -402,6 +439,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   std::memcpy(st->coeff_unrefined, bc, sizeof(bc));
   for (int i = 0; i < 3; ++i) st->best_sample[i] = best_s[i].gid;
 
+  const double t_ref0 = trace_on() ? now_ms() : 0.0;
   const int nt = select_tiles(src.n);
   c->tile_in.ensure(nt + 1);
   c->tile_off_in.ensure(nt + 1);
@@ -458,12 +496,15 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   if (c->profiling && xs) xs->select_ms += event_ms(c, 2, 3);
   out.n_in_local = c->h_tot.p[0];
   out.n_out_local = src.n == 0 ? 0 : c->h_tot.p[1];
+  if (trace_on())
+    std::fprintf(stderr, "[dlg] refit+select=%.3fms n_in=%lld\n", now_ms() - t_ref0,
+                 (long long)out.n_in_local);
   return out;
 }
 
 // copy this rank's (or every rank's) refined inliers to the caller buffer
 int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, int64_t cap,
-                     int64_t* global_count) {
+                     int64_t* global_count, bool deferred = false) {
   if (gather && c->comm->world() > 1) {
     gather_lists(c, c->inl_gid.p, so.n_in_local, 1, &c->h_inl);
     int64_t n = (int64_t)c->h_inl.size();
@@ -477,8 +518,20 @@ int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, in
   if (so.n_in_local > cap)
     throw DlgError(DLG_ERR_CAPACITY, "inlier buffer too small: need " + std::to_string(so.n_in_local));
   if (so.n_in_local) {
-    HIPCHK(hipMemcpyAsync(dst, c->inl_gid.p, (size_t)so.n_in_local * 4, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
+    if (deferred) {
+      drain_pending(c);
+      c->h_stage.ensure((size_t)so.n_in_local);
+      if (!c->ev_stage) HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+      HIPCHK(hipMemcpyAsync(c->h_stage.p, c->inl_gid.p, (size_t)so.n_in_local * 4,
+                            hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipEventRecord(c->ev_stage, c->stream));
+      c->pending_dst = dst;
+      c->pending_n = so.n_in_local;
+    } else {
+      HIPCHK(hipMemcpyAsync(dst, c->inl_gid.p, (size_t)so.n_in_local * 4, hipMemcpyDeviceToHost,
+                            c->stream));
+      sync(c);
+    }
   }
   return so.n_in_local;
 }
@@ -639,6 +692,8 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->partials.release(); c->moments.release(); c->inl_gid.release(); c->inl_xyz.release();
   c->gath64.release(); c->gath32.release();
   c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
+  c->h_stage.release();
+  if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -786,7 +841,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       if (n_in == 0 || n_in < min_inliers) break;  // plane rejected: active list unchanged
       int64_t g = 0;
       int64_t n = emit_inliers(c, so, prm->gather_inliers != 0, inliers_out + written,
-                               cap - written, &g);
+                               cap - written, &g, /*deferred=*/true);
       std::memcpy(coeffs_out + 4 * p, so.coeff, sizeof(so.coeff));
       written += n;
       offsets_out[p + 1] = written;
@@ -794,9 +849,49 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       cl->cur = cl->spare();  // commit the removal
       cl->n_active = so.n_out_local;
     }
+    drain_pending(c);
   });
+  c->pending_dst = nullptr;  // (error path: never write into the caller's buffer later)
+  c->pending_n = 0;
   xs->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return s;
+}
+
+dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, int reps,
+                               double threshold, double* ms_per_launch, int32_t* counts_out) {
+  if (!c || !cl || D < 1 || D > kMaxHypPerLaunch || reps < 1 || !ms_per_launch) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    const PointsView src = cl->view();
+    if (src.n < 3) throw DlgError(DLG_ERR_INVALID, "need >= 3 active points");
+    Mt19937 rng(777u);
+    c->h_pos.ensure(3 * (size_t)D);
+    for (int i = 0; i < 3 * D; ++i) c->h_pos.p[i] = (int32_t)((uint32_t)rng.rnd() % (uint64_t)src.n);
+    c->pos.ensure(3 * (size_t)D);
+    c->samples.ensure(3 * (size_t)D);
+    c->hyps.ensure(kHypScratchBytes / sizeof(HypRec) + 1);
+    c->res.ensure(2 * (size_t)kMaxHypPerLaunch + 64);
+    const float cthr = thr_ceil(threshold);
+    HIPCHK(hipMemcpyAsync(c->pos.p, c->h_pos.p, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
+    launch_gather_samples(c->pos.p, 3 * D, 0, src, c->samples.p, c->stream);
+    const int Dp = (D + 63) / 64 * 64;
+    launch_build_hyps(c->samples.p, D, cthr, cl->amax[0], cl->amax[1], cl->amax[2], c->hyps.p,
+                      c->res.p + Dp, c->stream);
+    double total = 0.0;
+    for (int r = 0; r < reps; ++r) {
+      HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
+      HIPCHK(hipEventRecord(c->ev[0], c->stream));
+      launch_score(src, c->hyps.p, D, cthr, c->res.p, variant, c->num_cus, c->stream);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(c->ev[1], c->stream));
+      sync(c);
+      total += event_ms(c, 0, 1);
+    }
+    *ms_per_launch = total / reps;
+    if (counts_out) {
+      HIPCHK(hipMemcpyAsync(counts_out, c->res.p, 4 * (size_t)D, hipMemcpyDeviceToHost, c->stream));
+      sync(c);
+    }
+  });
 }
 
 dlg_status dlg_set_profiling(dlg_ctx* c, int enable) {

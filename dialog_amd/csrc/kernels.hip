@@ -14,6 +14,7 @@
 //   computeMeanAndCovarianceMatrix (fast mode, double)  -> k_moments
 #include "kernels.hpp"
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -57,18 +58,26 @@ __global__ void k_gather_samples(const int32_t* __restrict__ pos, int m, int64_t
 }
 
 // isSampleGood + computeModelCoefficients (sac_model_plane.hpp), one thread per draw.
-__global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, float cthr, float ax,
+__global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, int Dp, float cthr, float ax,
                              float ay, float az, HypRec* __restrict__ hyps,
                              int32_t* __restrict__ good_out) {
   int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
+  if (d >= Dp) return;
+  if (d >= D) {  // padding up to the 64-plane groups of k_score: NaN planes count nothing
+    HypRec h;
+    h.a = h.b = h.c = h.d = __builtin_nanf("");
+    h.tlo = h.thi = h.w = 0.0f;
+    h.good = 0;
+    hyps[d] = h;
+    return;
+  }
   const SampleRec s0 = s[3 * d], s1 = s[3 * d + 1], s2 = s[3 * d + 2];
   float a0 = s1.x - s0.x, a1 = s1.y - s0.y, a2 = s1.z - s0.z;
   float b0 = s2.x - s0.x, b1 = s2.y - s0.y, b2 = s2.z - s0.z;
   float r0 = a0 / b0, r1 = a1 / b1, r2 = a2 / b2;
   bool good = (r0 != r1) || (r2 != r1);
   HypRec h;
-  h.pad = 0;
+  h.w = 0.0f;
   h.good = good ? 1 : 0;
   if (good) {
     float c0 = a1 * b2 - a2 * b1;
@@ -89,9 +98,11 @@ __global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, float cthr,
     double E = S * (7.0 * 5.9604644775390625e-08) * (1.0 + 1e-6) + 1e-37;
     h.tlo = __double2float_rd((double)cthr - E);
     h.thi = __double2float_ru((double)cthr + E);
+    // min3 variant: r = fl(|f| - cthr) carries <= 2^-24 |r| relative error on top of E
+    h.w = __double2float_ru(E * (1.0 + 1e-4));
   } else {
     h.a = h.b = h.c = h.d = __builtin_nanf("");
-    h.tlo = h.thi = 0.0f;
+    h.tlo = h.thi = h.w = 0.0f;
   }
   hyps[d] = h;
   good_out[d] = h.good;
@@ -100,26 +111,31 @@ __global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, float cthr,
 // ---------------------------------------------------------------------------------------------
 // k_score: counts[h] = #{active i : |pcl_dot(h, p_i)| < cthr}.
 //
-// One lane per point slot (kP points per lane, coalesced 4-B SoA loads), the hypothesis tile
+// One lane per point slot (P points per lane, coalesced 4-B SoA loads), the hypothesis tile
 // staged in LDS and read with a wave-uniform address (LDS broadcast), the per-hypothesis wave
 // count from ballot + popcount on the scalar unit, parked in lane (h mod 64) by v_writelane and
 // flushed every 64 hypotheses with one ds_add per lane; the workgroup adds its LDS counts to the
-// global counts once (one atomic per hypothesis per workgroup).  Grid-stride over 2048-point
-// chunks with the grid sized to the resident capacity.
-// VALU cost (exact variant): 3 v_mul + 3 v_add + 1 v_cmp per test -> VALU-bound at large D.
-constexpr int kScBS = 256;
-constexpr int kP = 8;
-constexpr int kChunk = kScBS * kP;
+// global counts once (one atomic per hypothesis per workgroup).  Grid-stride over chunks of
+// 256 * P points with the grid sized to the resident capacity.
+//
+// Prefilter variants (band, min3) evaluate f = fma(a, x, fma(b, y, fma(c, z, d))) and decide
+// only outside the band |f| in [cthr - E, cthr + E), E = 7 u S >= |f - pcl_dot| (k_build_hyps);
+// any wave with a point inside the band recomputes those points in PCL op order, so the counts
+// stay bit-identical to the exact variant.
+constexpr int kScBS = 512;  // 8 waves share one LDS copy of the hypotheses
 constexpr int kHT = 1024;
 
-template <int VARIANT>
+enum Kind { kExact = 0, kBand = 1, kMin3 = 2 };
+
+template <int KIND, int P>
 __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
                                                  const float* __restrict__ Y,
                                                  const float* __restrict__ Z, int n,
                                                  const HypRec* __restrict__ hyps, int D,
                                                  float cthr, int32_t* __restrict__ counts) {
-  __shared__ float4 s_coef[kHT];
-  __shared__ float2 s_band[VARIANT == kScoreFmaBand ? kHT : 1];
+  constexpr int kChunk = kScBS * P;
+  __shared__ float4 s_coef[kHT + 1];  // +1: the prefetch of the group's last plane reads past
+  __shared__ float2 s_band[KIND == kExact ? 1 : kHT + 1];
   __shared__ int s_cnt[kMaxHypPerLaunch];
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
@@ -127,9 +143,9 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
   const int nchunks = (n + kChunk - 1) / kChunk;
   const float qnan = __builtin_nanf("");
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    float px[kP], py[kP], pz[kP];
+    float px[P], py[P], pz[P];
 #pragma unroll
-    for (int j = 0; j < kP; ++j) {
+    for (int j = 0; j < P; ++j) {
       int e = ch * kChunk + j * kScBS + tid;
       bool ok = e < n;
       px[j] = ok ? X[e] : qnan;
@@ -142,29 +158,34 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
       for (int i = tid; i < nt; i += kScBS) {
         const HypRec hr = hyps[t0 + i];
         s_coef[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
-        if (VARIANT == kScoreFmaBand) s_band[i] = make_float2(hr.tlo, hr.thi);
+        if (KIND == kBand) s_band[i] = make_float2(hr.tlo, hr.thi);
+        if (KIND == kMin3) s_band[i] = make_float2(hr.w, 0.0f);
       }
       __syncthreads();
-      for (int g0 = 0; g0 < nt; g0 += kWave) {
-        const int ng = min(kWave, nt - g0);
+      for (int g0 = 0; g0 < nt; g0 += kWave) {  // nt is a multiple of 64 (D padded with NaN planes)
         int my = 0;
-        float4 cn = s_coef[g0];
-        for (int k = 0; k < ng; ++k) {
-          const int h = g0 + k;
-          const float4 c = cn;
-          if (k + 1 < ng) cn = s_coef[h + 1];  // prefetch the next hypothesis (LDS broadcast)
+        // software pipeline: the next hypothesis' LDS broadcast read is in flight while the
+        // current one is evaluated (the wait lands at the loop back-edge, not at first use)
+        float4 cnext = s_coef[g0];
+        float2 bnext = KIND == kExact ? make_float2(0.f, 0.f) : s_band[g0];
+#pragma unroll 8
+        for (int k = 0; k < kWave; ++k) {
+          const float4 c = cnext;
+          const float2 bcur = bnext;
+          cnext = s_coef[g0 + k + 1];
+          if (KIND != kExact) bnext = s_band[g0 + k + 1];
           int cnt = 0;
-          if (VARIANT == kScoreExact) {
+          if (KIND == kExact) {
 #pragma unroll
-            for (int j = 0; j < kP; ++j) {
+            for (int j = 0; j < P; ++j) {
               float dd = pcl_dot(c.x, c.y, c.z, c.w, px[j], py[j], pz[j]);
               cnt += __popcll(ballot(fabsf(dd) < cthr));
             }
-          } else {
-            const float2 band = s_band[h];
+          } else if (KIND == kBand) {
+            const float2 band = bcur;
             uint64_t border = 0;
 #pragma unroll
-            for (int j = 0; j < kP; ++j) {
+            for (int j = 0; j < P; ++j) {
               float f = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
               uint64_t lo = ballot(fabsf(f) < band.x);
               uint64_t hi = ballot(fabsf(f) < band.y);
@@ -173,9 +194,30 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
             }
             if (border) {  // rare: some lane is inside the rounding band -> exact PCL test there
 #pragma unroll
-              for (int j = 0; j < kP; ++j) {
+              for (int j = 0; j < P; ++j) {
                 float f = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
                 bool inb = (fabsf(f) >= band.x) && (fabsf(f) < band.y);
+                float dd = pcl_dot(c.x, c.y, c.z, c.w, px[j], py[j], pz[j]);
+                cnt += __popcll(ballot(inb && (fabsf(dd) < cthr)));
+              }
+            }
+          } else {  // kMin3
+            const float w = bcur.x;
+            float m = INFINITY;
+#pragma unroll
+            for (int j = 0; j < P; j += 2) {
+              float f0 = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
+              float f1 = __builtin_fmaf(c.x, px[j + 1], __builtin_fmaf(c.y, py[j + 1], __builtin_fmaf(c.z, pz[j + 1], c.w)));
+              float r0 = fabsf(f0) - cthr, r1 = fabsf(f1) - cthr;
+              cnt += __popcll(ballot(r0 < -w));
+              cnt += __popcll(ballot(r1 < -w));
+              m = fminf(fminf(m, fabsf(r0)), fabsf(r1));  // v_min3_f32 m, |r0|, |r1|
+            }
+            if (ballot(m < w)) {  // rare: a point of this wave is within the band -> exact there
+#pragma unroll
+              for (int j = 0; j < P; ++j) {
+                float f = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
+                bool inb = fabsf(fabsf(f) - cthr) < w;
                 float dd = pcl_dot(c.x, c.y, c.z, c.w, px[j], py[j], pz[j]);
                 cnt += __popcll(ballot(inb && (fabsf(dd) < cthr)));
               }
@@ -183,7 +225,7 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
           }
           my = writelane(my, cnt, k);
         }
-        if (lane < ng) atomicAdd(&s_cnt[t0 + g0 + lane], my);
+        atomicAdd(&s_cnt[t0 + g0 + lane], my);
       }
     }
   }
@@ -191,6 +233,426 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
   for (int i = tid; i < D; i += kScBS) {
     int v = s_cnt[i];
     if (v) atomicAdd(&counts[i], v);
+  }
+}
+
+// k_score_s: the same counts, hypothesis coefficients in SGPRs.  A wave walks the hypotheses in
+// groups of GH (fully unrolled): the group's GH plane vectors come in by scalar loads (s_load,
+// scalar cache; wave-uniform), every VALU op takes its coefficient as the SGPR operand, so the
+// loop holds no LDS reads and no VGPRs for coefficients.  coef4 is padded with NaN planes to a
+// multiple of 64 (Dp); counts must have room for Dp entries.
+template <int KIND, int P, int GH>
+__global__ __launch_bounds__(kScBS) void k_score_s(const float* __restrict__ X,
+                                                   const float* __restrict__ Y,
+                                                   const float* __restrict__ Z, int n,
+                                                   const float4* __restrict__ coef4,
+                                                   const float* __restrict__ wband, int Dp,
+                                                   float cthr, int32_t* __restrict__ counts) {
+  constexpr int kChunk = kScBS * P;
+  __shared__ int s_cnt[kMaxHypPerLaunch];
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  for (int i = tid; i < Dp; i += kScBS) s_cnt[i] = 0;
+  __syncthreads();
+  const int nchunks = (n + kChunk - 1) / kChunk;
+  const float qnan = __builtin_nanf("");
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    float px[P], py[P], pz[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      int e = ch * kChunk + j * kScBS + tid;
+      bool ok = e < n;
+      px[j] = ok ? X[e] : qnan;
+      py[j] = ok ? Y[e] : qnan;
+      pz[j] = ok ? Z[e] : qnan;
+    }
+    for (int g0 = 0; g0 < Dp; g0 += kWave) {
+      int my = 0;
+      for (int h0 = g0; h0 < g0 + kWave; h0 += GH) {
+        float4 c[GH];
+        float w[GH];
+#pragma unroll
+        for (int k = 0; k < GH; ++k) {
+          c[k] = coef4[h0 + k];
+          if (KIND == kMin3) w[k] = wband[h0 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < GH; ++k) {
+          int cnt = 0;
+          if (KIND == kExact) {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+              float dd = pcl_dot(c[k].x, c[k].y, c[k].z, c[k].w, px[j], py[j], pz[j]);
+              cnt += __popcll(ballot(fabsf(dd) < cthr));
+            }
+          } else {
+            float m = INFINITY;
+#pragma unroll
+            for (int j = 0; j < P; j += 2) {
+              float f0 = __builtin_fmaf(c[k].x, px[j], __builtin_fmaf(c[k].y, py[j], __builtin_fmaf(c[k].z, pz[j], c[k].w)));
+              float f1 = __builtin_fmaf(c[k].x, px[j + 1], __builtin_fmaf(c[k].y, py[j + 1], __builtin_fmaf(c[k].z, pz[j + 1], c[k].w)));
+              float r0 = fabsf(f0) - cthr, r1 = fabsf(f1) - cthr;
+              cnt += __popcll(ballot(r0 < -w[k]));
+              cnt += __popcll(ballot(r1 < -w[k]));
+              m = fminf(fminf(m, fabsf(r0)), fabsf(r1));
+            }
+            if (ballot(m < w[k])) {
+#pragma unroll
+              for (int j = 0; j < P; ++j) {
+                float f = __builtin_fmaf(c[k].x, px[j], __builtin_fmaf(c[k].y, py[j], __builtin_fmaf(c[k].z, pz[j], c[k].w)));
+                bool inb = fabsf(fabsf(f) - cthr) < w[k];
+                float dd = pcl_dot(c[k].x, c[k].y, c[k].z, c[k].w, px[j], py[j], pz[j]);
+                cnt += __popcll(ballot(inb && (fabsf(dd) < cthr)));
+              }
+            }
+          }
+          my = writelane(my, cnt, (h0 - g0) + k);
+        }
+      }
+      atomicAdd(&s_cnt[g0 + lane], my);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < Dp; i += kScBS) {
+    int v = s_cnt[i];
+    if (v) atomicAdd(&counts[i], v);
+  }
+}
+
+// k_score_mfma: the same counts with the FMA chains on the matrix pipe.
+// v_mfma_f32_16x16x4f32 computes D[i][j] = fma(1, d_j, fma(z_i, c_j, fma(y_i, b_j, fma(x_i, a_j, 0))))
+// for 16 points i x 16 planes j (bit-for-bit a k-ordered f32 fmaf chain; |D - pcl_dot| <= 7 u S
+// as for the VALU prefilter).  A operand = 16 points (lane l: coordinate l>>4 of point l&15,
+// lanes 48..63 hold the homogeneous 1), B operand = 16 planes (lane l: coefficient l>>4 of plane
+// l&15), D in 4 VGPRs (lane l: rows 4(l>>4)+r of column l&15).  The VALU then only does
+// r = |D| - cthr, in iff r < -w (per-lane counter via the carry), and tracks min |r| per MFMA;
+// an MFMA tile with a value inside the band |r| < w is re-evaluated in PCL op order for exactly
+// those elements (points and planes fetched by cross-lane reads), so counts stay bit-identical.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int PA>
+__global__ __launch_bounds__(kScBS) void k_score_mfma(const float* __restrict__ X,
+                                                      const float* __restrict__ Y,
+                                                      const float* __restrict__ Z, int n,
+                                                      const HypRec* __restrict__ hyps, int Dp,
+                                                      float cthr, int32_t* __restrict__ counts) {
+  constexpr int kWavePts = 16 * PA;                  // points held by one wave
+  constexpr int kChunk = (kScBS / kWave) * kWavePts;  // points per workgroup pass
+  __shared__ float s_b[kHT * 4];
+  __shared__ float s_w[kHT];
+  __shared__ int s_cnt[kMaxHypPerLaunch];
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wv = tid / kWave;
+  const int q = lane >> 4, r16 = lane & 15;
+  for (int i = tid; i < Dp; i += kScBS) s_cnt[i] = 0;
+  const int nchunks = (n + kChunk - 1) / kChunk;
+  const float qnan = __builtin_nanf("");
+  const float* base = q == 0 ? X : (q == 1 ? Y : Z);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    float A[PA];
+    const int p0 = ch * kChunk + wv * kWavePts;
+#pragma unroll
+    for (int p = 0; p < PA; ++p) {
+      const int e = p0 + p * 16 + r16;
+      A[p] = q == 3 ? 1.0f : (e < n ? base[e] : qnan);
+    }
+    for (int t0 = 0; t0 < Dp; t0 += kHT) {
+      const int nt = min(kHT, Dp - t0);
+      __syncthreads();
+      for (int i = tid; i < nt; i += kScBS) {
+        const HypRec hr = hyps[t0 + i];
+        reinterpret_cast<float4*>(s_b)[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
+        s_w[i] = hr.w;
+      }
+      __syncthreads();
+      for (int h0 = 0; h0 < nt; h0 += 16) {
+        const float bop = s_b[(h0 + r16) * 4 + q];  // conflict-free: 64 consecutive floats
+        const float w = s_w[h0 + r16];
+        int cnt = 0;
+        float m = INFINITY;
+        // branch-free main pass: MFMA p+1 overlaps the VALU work on the result of MFMA p
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+          const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(A[p], bop, zero, 0, 0, 0);
+          const float r0 = fabsf(d[0]) - cthr, r1 = fabsf(d[1]) - cthr;
+          const float r2 = fabsf(d[2]) - cthr, r3 = fabsf(d[3]) - cthr;
+          cnt += (r0 < -w) + (r1 < -w) + (r2 < -w) + (r3 < -w);
+          m = fminf(fminf(m, fabsf(r0)), fabsf(r1));
+          m = fminf(fminf(m, fabsf(r2)), fabsf(r3));
+        }
+        if (ballot(m < w)) {  // rare: an element of this tile lies in the band -> PCL order there
+          const float ca = __shfl(bop, r16), cb = __shfl(bop, 16 + r16);
+          const float cc = __shfl(bop, 32 + r16), cd = __shfl(bop, 48 + r16);
+          for (int p = 0; p < PA; ++p) {
+            const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(A[p], bop, zero, 0, 0, 0);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int i = 4 * q + rr;
+              const float px = __shfl(A[p], i), py = __shfl(A[p], 16 + i), pz = __shfl(A[p], 32 + i);
+              const bool band = fabsf(fabsf(d[rr]) - cthr) < w;
+              const float ex = pcl_dot(ca, cb, cc, cd, px, py, pz);
+              cnt += (band && fabsf(ex) < cthr) ? 1 : 0;
+            }
+          }
+        }
+        // lanes r16, r16 + 16, r16 + 32, r16 + 48 hold partial counts of plane h0 + r16
+        cnt += __shfl_xor(cnt, 16);
+        cnt += __shfl_xor(cnt, 32);
+        if (q == 0) atomicAdd(&s_cnt[t0 + h0 + r16], cnt);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < Dp; i += kScBS) {
+    int v = s_cnt[i];
+    if (v) atomicAdd(&counts[i], v);
+  }
+}
+
+// v_min_f32 m, m, |r| without the canonicalising v_max that fminf() brings along
+__device__ __forceinline__ float min_abs(float m, float r) {
+  float o;
+  asm("v_min_f32_e64 %0, %1, |%2|" : "=v"(o) : "v"(m), "v"(r));
+  return o;
+}
+
+// one block of points (wave-uniform) against this lane's hypothesis; NB = 16 -> full block,
+// NB = 0 -> tail of nb < 16 points (guarded).  Returns the lane's inlier count for the block.
+template <int KIND, int NB>
+__device__ __forceinline__ int score_block(const float* __restrict__ X, const float* __restrict__ Y,
+                                           const float* __restrict__ Z, int jb, int nb, float a,
+                                           float b, float c, float d, float tlo, float W2,
+                                           float cthr) {
+  float px[16], py[16], pz[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const bool ok = NB == 16 || k < nb;
+    px[k] = ok ? X[jb + k] : 0.f;
+    py[k] = ok ? Y[jb + k] : 0.f;
+    pz[k] = ok ? Z[jb + k] : 0.f;
+  }
+  int cnt = 0;
+  if (KIND == kExact) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (NB == 16 || k < nb) {
+        float dd = pcl_dot(a, b, c, d, px[k], py[k], pz[k]);
+        cnt += fabsf(dd) < cthr ? 1 : 0;
+      }
+    }
+    return cnt;
+  }
+  float m = INFINITY;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (NB == 16 || k < nb) {
+      float f = __builtin_fmaf(a, px[k], __builtin_fmaf(b, py[k], __builtin_fmaf(c, pz[k], d)));
+      float r = fabsf(f) - tlo;
+      cnt += r < 0.0f ? 1 : 0;
+      m = min_abs(m, r);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(m <= W2)) {  // rare: a point in some lane's band -> PCL order
+    int ex = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (NB == 16 || k < nb) {
+        float dd = pcl_dot(a, b, c, d, px[k], py[k], pz[k]);
+        ex += fabsf(dd) < cthr ? 1 : 0;
+      }
+    }
+    cnt = ex;
+  }
+  return cnt;
+}
+
+// k_score_h: lanes = hypotheses, points = wave-uniform scalars.
+// A wave owns 64 hypotheses (one per lane: a, b, c, d and its band in VGPRs) and streams one
+// partition of the points through the scalar cache (s_load_dwordx16 of X, Y, Z: 16 points per
+// block, the same addresses for every wave of the workgroup).  Each lane counts its own
+// hypothesis with v_cmp + v_addc -- no ballot/popcount on the scalar unit and no cross-lane
+// reduction; at the end one atomic per lane.  Every VALU op takes the point coordinate as its
+// one SGPR operand.
+//   kExact : PCL op order, 3 v_mul + 3 v_add + v_cmp + v_addc             8 VALU / test
+//   kMin3  : f = fma chain; r = |f| - tlo; in iff r < 0 (exact since |f| < tlo guarantees
+//            |pcl| < cthr); band iff |r| <= W2 = thi - tlo tracked by v_min3, re-evaluated in
+//            PCL order for the 16-point block                             6.5 VALU / test
+// X/Y/Z must be readable up to n rounded up to 16 (allocation slack); the tail block is
+// handled by a wave-uniform bound.
+template <int KIND>
+__global__ __launch_bounds__(kScBS) void k_score_h(const float* __restrict__ X,
+                                                   const float* __restrict__ Y,
+                                                   const float* __restrict__ Z, int n,
+                                                   const HypRec* __restrict__ hyps, int Dp,
+                                                   int part, float cthr,
+                                                   int32_t* __restrict__ counts) {
+  constexpr int kWpg = kScBS / kWave;                  // waves (hypothesis groups) per workgroup
+  const int ngroups = Dp / kWave;
+  const int gblocks = (ngroups + kWpg - 1) / kWpg;      // workgroups per point partition
+  const int wv = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int hg = (blockIdx.x % gblocks) * kWpg + wv;    // this wave's hypothesis group
+  const int pp = blockIdx.x / gblocks;                  // point partition
+  if (hg >= ngroups) return;
+  const int h = hg * kWave + lane;
+  const HypRec hr = hyps[h];
+  const float a = hr.a, b = hr.b, c = hr.c, d = hr.d;
+  const float tlo = hr.tlo;
+  const float W2 = (hr.thi - hr.tlo) * (1.0f + 1.0f / 4194304.0f);  // >= fl(thi - tlo)
+  const int j0 = pp * part;
+  const int j1 = min(n, j0 + part);
+  int cnt = 0;
+  // full 16-point blocks (no per-point guards: the loop body is straight-line VALU)
+  int jb = j0;
+  for (; jb + 16 <= j1; jb += 16) cnt += score_block<KIND, 16>(X, Y, Z, jb, 16, a, b, c, d, tlo, W2, cthr);
+  if (jb < j1) cnt += score_block<KIND, 0>(X, Y, Z, jb, j1 - jb, a, b, c, d, tlo, W2, cthr);
+  atomicAdd(&counts[h], cnt);
+}
+
+// k_score_hl: lanes = hypotheses (as k_score_h), points staged per workgroup in LDS.
+// The workgroup (8 waves = 8 groups of 64 hypotheses) walks its point partition in chunks of
+// kHlChunk points: coalesced float4 global loads of the next chunk are issued before the current
+// chunk is evaluated and written to the other LDS buffer afterwards (one barrier per chunk).
+// A wave reads 4 points at a time with wave-uniform ds_read_b128 (broadcast) and moves them to
+// SGPRs with v_readfirstlane, so each FMA / mul has one SGPR operand.
+constexpr int kHlChunk = 1024;
+
+__device__ __forceinline__ float sgpr(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+template <int KIND>
+__device__ __forceinline__ int hl_quad(const float4& xs, const float4& ys, const float4& zs, float a,
+                                       float b, float c, float d, float tlo, float cthr, float& m) {
+  const float px[4] = {sgpr(xs.x), sgpr(xs.y), sgpr(xs.z), sgpr(xs.w)};
+  const float py[4] = {sgpr(ys.x), sgpr(ys.y), sgpr(ys.z), sgpr(ys.w)};
+  const float pz[4] = {sgpr(zs.x), sgpr(zs.y), sgpr(zs.z), sgpr(zs.w)};
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (KIND == kExact) {
+      float dd = pcl_dot(a, b, c, d, px[k], py[k], pz[k]);
+      cnt += fabsf(dd) < cthr ? 1 : 0;
+    } else {
+      float f = __builtin_fmaf(a, px[k], __builtin_fmaf(b, py[k], __builtin_fmaf(c, pz[k], d)));
+      float r = fabsf(f) - tlo;
+      cnt += r < 0.0f ? 1 : 0;
+      m = min_abs(m, r);
+    }
+  }
+  return cnt;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kScBS) void k_score_hl(const float* __restrict__ X,
+                                                    const float* __restrict__ Y,
+                                                    const float* __restrict__ Z, int n,
+                                                    const HypRec* __restrict__ hyps, int Dp,
+                                                    int part, float cthr,
+                                                    int32_t* __restrict__ counts) {
+  constexpr int kWpg = kScBS / kWave;
+  __shared__ float4 s_pts[2][3][kHlChunk / 4];  // [buffer][x|y|z][chunk/4]: 24 KB
+  const int ngroups = Dp / kWave;
+  const int gblocks = (ngroups + kWpg - 1) / kWpg;
+  const int wv = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int hg = (blockIdx.x % gblocks) * kWpg + wv;
+  const int pp = blockIdx.x / gblocks;
+  const bool active = hg < ngroups;           // wave-uniform; idle waves still help stage
+  const int h = min(hg, ngroups - 1) * kWave + lane;
+  const HypRec hr = hyps[h];
+  const float a = hr.a, b = hr.b, c = hr.c, d = hr.d;
+  const float tlo = hr.tlo;
+  const float W2 = (hr.thi - hr.tlo) * (1.0f + 1.0f / 4194304.0f);
+  const int j0 = pp * part;
+  const int j1 = min(n, j0 + part);
+  const int nch = (j1 - j0 + kHlChunk - 1) / kHlChunk;
+  const float qnan = __builtin_nanf("");
+  // staging: thread t loads float4 #(t % 256) of array (t / 256) (two rounds cover x, y, z)
+  auto load_chunk = [&](int cj, float4 (&v)[2]) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int idx = threadIdx.x + r * kScBS;  // 0 .. 1023 (768 used)
+      const int arr = idx / (kHlChunk / 4), q4 = idx % (kHlChunk / 4);
+      float4 t = make_float4(qnan, qnan, qnan, qnan);
+      if (arr < 3) {
+        const float* P = arr == 0 ? X : (arr == 1 ? Y : Z);
+        const int e = cj + 4 * q4;
+        if (e + 3 < j1) {
+          t = *reinterpret_cast<const float4*>(P + e);  // partitions/chunks are 4-aligned
+        } else {
+          if (e < j1) t.x = P[e];
+          if (e + 1 < j1) t.y = P[e + 1];
+          if (e + 2 < j1) t.z = P[e + 2];
+        }
+      }
+      v[r] = t;
+    }
+  };
+  auto store_chunk = [&](int buf, const float4 (&v)[2]) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int idx = threadIdx.x + r * kScBS;
+      const int arr = idx / (kHlChunk / 4), q4 = idx % (kHlChunk / 4);
+      if (arr < 3) s_pts[buf][arr][q4] = v[r];
+    }
+  };
+  int cnt = 0;
+  float4 stage[2];
+  if (nch > 0) {
+    load_chunk(j0, stage);
+    store_chunk(0, stage);
+  }
+  __syncthreads();
+  for (int ci = 0; ci < nch; ++ci) {
+    const int buf = ci & 1;
+    const int cj = j0 + ci * kHlChunk;
+    if (ci + 1 < nch) load_chunk(cj + kHlChunk, stage);  // in flight during the compute below
+    if (active) {
+      const int npts = min(kHlChunk, j1 - cj);
+      for (int q = 0; q < npts; q += 16) {  // 16-point blocks: 4 quads, one band check
+        float m = INFINITY;
+        int blk = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int qi = (q >> 2) + t;
+          blk += hl_quad<KIND>(s_pts[buf][0][qi], s_pts[buf][1][qi], s_pts[buf][2][qi], a, b, c,
+                               d, tlo, cthr, m);
+        }
+        if (KIND != kExact && __builtin_amdgcn_ballot_w64(m <= W2)) {
+          float mm = INFINITY;
+          int ex = 0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int qi = (q >> 2) + t;
+            ex += hl_quad<kExact>(s_pts[buf][0][qi], s_pts[buf][1][qi], s_pts[buf][2][qi], a, b,
+                                  c, d, tlo, cthr, mm);
+          }
+          blk = ex;
+        }
+        cnt += blk;
+      }
+    }
+    if (ci + 1 < nch) store_chunk(buf ^ 1, stage);
+    __syncthreads();
+  }
+  if (active) atomicAdd(&counts[h], cnt);
+}
+
+__global__ void k_pack_coef(const HypRec* __restrict__ hyps, int D, int Dp, float4* __restrict__ coef4,
+                            float* __restrict__ wband) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Dp) return;
+  const float qnan = __builtin_nanf("");
+  if (i < D) {
+    const HypRec h = hyps[i];
+    coef4[i] = make_float4(h.a, h.b, h.c, h.d);
+    wband[i] = h.w;
+  } else {
+    coef4[i] = make_float4(qnan, qnan, qnan, qnan);
+    wband[i] = 0.0f;
   }
 }
 
@@ -239,20 +701,14 @@ __global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, float4 cf, fl
 
 __global__ void k_reduce_partials(const double* __restrict__ partials, int nb,
                                   double* __restrict__ out) {
-  // fixed order: thread k sums column k over blocks 0..nb-1 in 8 strided lanes, then in order
-  __shared__ double s[kMomentK][8];
-  const int k = threadIdx.x / 8, r = threadIdx.x % 8;
-  if (k < kMomentK) {
-    double v = 0.0;
-    for (int b = r; b < nb; b += 8) v += partials[(int64_t)b * kMomentK + k];
-    s[k][r] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < kMomentK) {
-    double v = 0.0;
-    for (int q = 0; q < 8; ++q) v += s[threadIdx.x][q];
-    out[threadIdx.x] = v;
-  }
+  // fixed order (deterministic): wave k sums column k, lane l takes blocks l, l+64, ...; then a
+  // fixed xor-butterfly across the wave
+  const int k = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  if (k >= kMomentK) return;
+  double v = 0.0;
+  for (int b = lane; b < nb; b += kWave) v += partials[(int64_t)b * kMomentK + k];
+  v = wave_sum_d(v);
+  if (lane == 0) out[k] = v;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -404,24 +860,113 @@ void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,
                        HypRec* hyps, int32_t* good, hipStream_t s) {
   if (D <= 0) return;
-  hipLaunchKernelGGL(k_build_hyps, dim3(cdiv(D, 256)), dim3(256), 0, s, samples, D, cthr, ax, ay,
-                     az, hyps, good);
+  const int Dp = (D + 63) / 64 * 64;
+  hipLaunchKernelGGL(k_build_hyps, dim3(cdiv(Dp, 256)), dim3(256), 0, s, samples, D, Dp, cthr, ax,
+                     ay, az, hyps, good);
+}
+
+int kScoreDefault = kScoreExactP4;  // fastest measured (tools/score_ab.py)
+
+template <int KIND, int P>
+static void launch_score_t(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
+                           int num_cus, hipStream_t s) {
+  constexpr int kChunk = kScBS * P;
+  D = (D + kWave - 1) / kWave * kWave;  // hyps[D..Dp) are NaN planes; counts has room
+  const int64_t nchunks = (src.n + kChunk - 1) / kChunk;
+  // resident capacity: <= 40 KB LDS per 8-wave workgroup -> 4 workgroups (32 waves) per CU
+  const int64_t cap = (int64_t)num_cus * 4;
+  const int64_t per = (nchunks + cap - 1) / cap;  // chunks per workgroup (balanced grid)
+  const unsigned grid = (unsigned)((nchunks + per - 1) / per);
+  hipLaunchKernelGGL((k_score<KIND, P>), dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
+                     (int)src.n, hyps, D, cthr, counts);
+}
+
+template <int KIND, int P, int GH>
+static void launch_score_s(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
+                           int num_cus, hipStream_t s) {
+  constexpr int kChunk = kScBS * P;
+  const int Dp = (D + kWave - 1) / kWave * kWave;
+  // packed plane vectors live behind the hypothesis records' scratch tail (see score_scratch)
+  float4* coef4 = reinterpret_cast<float4*>(const_cast<HypRec*>(hyps) + kMaxHypPerLaunch);
+  float* wband = reinterpret_cast<float*>(coef4 + kMaxHypPerLaunch);
+  hipLaunchKernelGGL(k_pack_coef, dim3((Dp + 255) / 256), dim3(256), 0, s, hyps, D, Dp, coef4, wband);
+  const int64_t nchunks = (src.n + kChunk - 1) / kChunk;
+  const int64_t cap = (int64_t)num_cus * 4;
+  const int64_t per = (nchunks + cap - 1) / cap;
+  const unsigned grid = (unsigned)((nchunks + per - 1) / per);
+  hipLaunchKernelGGL((k_score_s<KIND, P, GH>), dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
+                     (int)src.n, coef4, wband, Dp, cthr, counts);
+}
+
+template <int PA>
+static void launch_score_mfma(PointsView src, const HypRec* hyps, int D, float cthr,
+                              int32_t* counts, int num_cus, hipStream_t s) {
+  constexpr int kChunk = (kScBS / kWave) * 16 * PA;
+  const int Dp = (D + kWave - 1) / kWave * kWave;  // hyps[D..Dp) must be NaN planes (padded)
+  const int64_t nchunks = (src.n + kChunk - 1) / kChunk;
+  const int64_t cap = (int64_t)num_cus * 4;
+  const int64_t per = (nchunks + cap - 1) / cap;
+  const unsigned grid = (unsigned)((nchunks + per - 1) / per);
+  hipLaunchKernelGGL((k_score_mfma<PA>), dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
+                     (int)src.n, hyps, Dp, cthr, counts);
+}
+
+template <int KIND>
+static void launch_score_h(PointsView src, const HypRec* hyps, int D, float cthr,
+                           int32_t* counts, int num_cus, hipStream_t s) {
+  constexpr int kWpg = kScBS / kWave;
+  const int Dp = (D + kWave - 1) / kWave * kWave;  // hyps[D..Dp) are NaN planes
+  const int ngroups = Dp / kWave;
+  const int gblocks = (ngroups + kWpg - 1) / kWpg;
+  // enough partitions for ~8 resident waves per SIMD, partitions a multiple of 16 points
+  const int64_t want_waves = (int64_t)num_cus * 4 * 8;
+  int64_t nparts = (want_waves + ngroups - 1) / ngroups;
+  int64_t part = (src.n + nparts - 1) / nparts;
+  part = std::max<int64_t>(256, (part + 15) / 16 * 16);
+  nparts = (src.n + part - 1) / part;
+  hipLaunchKernelGGL((k_score_h<KIND>), dim3((unsigned)(nparts * gblocks)), dim3(kScBS), 0, s,
+                     src.x, src.y, src.z, (int)src.n, hyps, Dp, (int)part, cthr, counts);
+}
+
+template <int KIND>
+static void launch_score_hl(PointsView src, const HypRec* hyps, int D, float cthr,
+                            int32_t* counts, int num_cus, hipStream_t s) {
+  constexpr int kWpg = kScBS / kWave;
+  const int Dp = (D + kWave - 1) / kWave * kWave;
+  const int ngroups = Dp / kWave;
+  const int gblocks = (ngroups + kWpg - 1) / kWpg;
+  const int64_t want_blocks = (int64_t)num_cus * 4 * 2;  // 2 x (4 resident 8-wave blocks / CU)
+  int64_t nparts = std::max<int64_t>(1, (want_blocks + gblocks - 1) / gblocks);
+  int64_t part = (src.n + nparts - 1) / nparts;
+  part = std::max<int64_t>(kHlChunk, (part + kHlChunk - 1) / kHlChunk * kHlChunk);
+  nparts = (src.n + part - 1) / part;
+  hipLaunchKernelGGL((k_score_hl<KIND>), dim3((unsigned)(nparts * gblocks)), dim3(kScBS), 0, s,
+                     src.x, src.y, src.z, (int)src.n, hyps, Dp, (int)part, cthr, counts);
 }
 
 void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
                   int variant, int num_cus, hipStream_t s) {
   if (D <= 0 || src.n <= 0) return;
-  const int64_t nchunks = (src.n + kChunk - 1) / kChunk;
-  // resident capacity: LDS ~ 16 KB coef + 8 KB band + 16 KB counts -> 4 workgroups / CU
-  const int64_t cap = (int64_t)num_cus * 4;
-  const int64_t per = (nchunks + cap - 1) / cap;       // chunks per workgroup
-  const unsigned grid = (unsigned)((nchunks + per - 1) / per);
-  if (variant == kScoreFmaBand)
-    hipLaunchKernelGGL(k_score<kScoreFmaBand>, dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
-                       (int)src.n, hyps, D, cthr, counts);
-  else
-    hipLaunchKernelGGL(k_score<kScoreExact>, dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
-                       (int)src.n, hyps, D, cthr, counts);
+  switch (variant) {
+    case kScoreLdsExact: launch_score_hl<kExact>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreLdsMin3: launch_score_hl<kMin3>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreLanesExact: launch_score_h<kExact>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreLanesMin3: launch_score_h<kMin3>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreMfma32: launch_score_mfma<32>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreMfma16: launch_score_mfma<16>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreMfma8: launch_score_mfma<8>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreExactS8: launch_score_s<kExact, 8, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreMin3S8: launch_score_s<kMin3, 8, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreExactS4: launch_score_s<kExact, 4, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreExactS8G4: launch_score_s<kExact, 8, 4>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreBandP8: launch_score_t<kBand, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreMin3P8: launch_score_t<kMin3, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreExactP16: launch_score_t<kExact, 16>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreMin3P16: launch_score_t<kMin3, 16>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreExactP4: launch_score_t<kExact, 4>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreMin3P4: launch_score_t<kMin3, 4>(src, hyps, D, cthr, counts, num_cus, s); break;
+    default: launch_score_t<kExact, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
+  }
 }
 
 int moments_blocks(int64_t n) {
@@ -434,7 +979,7 @@ int moments_blocks(int64_t n) {
 void launch_moments(PointsView src, float4 coef, float cthr, double3 shift, double* partials,
                     int nblocks, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_moments, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, cthr, shift, partials);
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kMomentK * 8), 0, s, partials, nblocks, out);
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kMomentK * kWave), 0, s, partials, nblocks, out);
 }
 
 int select_tiles(int64_t n) { return (int)((n + kSelTile - 1) / kSelTile); }

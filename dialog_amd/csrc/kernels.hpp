@@ -23,7 +23,7 @@ struct alignas(16) HypRec {
   float a, b, c, d;
   float tlo, thi;
   int32_t good;  // SampleConsensusModelPlane::isSampleGood
-  int32_t pad;
+  float w;       // band half-width around cthr for the |fma(...)| - cthr test (variant 2)
 };
 
 struct PointsView {
@@ -45,8 +45,30 @@ constexpr int kMaxHypPerLaunch = 4096;  // LDS count array of the scoring kernel
 constexpr int kSelTile = 4096;          // points per select/compact workgroup
 constexpr int kMomentK = 10;            // n, sx, sy, sz, sxx, sxy, sxz, syy, syz, szz
 
-// Scoring kernel variants (bench/profiling A/B; product default = kScoreExact)
-enum ScoreVariant { kScoreExact = 0, kScoreFmaBand = 1 };
+// Scoring kernel variants (A/B via dlg_score_benchmark; the product uses kScoreDefault).
+//   exact : PCL op order (3 mul + 3 add) + compare                          7 VALU + 2 SALU / slot
+//   band  : FMA chain, two compares against [tlo, thi), exact recheck in band  5 VALU + 4 SALU
+//   min3  : FMA chain, r = |f| - cthr, in iff r < -w, band tracked by v_min3   5.5 VALU + 2 SALU
+// P = points per lane.
+enum ScoreVariant {
+  kScoreExactP8 = 0, kScoreBandP8 = 1, kScoreMin3P8 = 2, kScoreExactP16 = 3, kScoreMin3P16 = 4,
+  kScoreExactP4 = 5, kScoreMin3P4 = 6,
+  // coefficients in SGPRs (scalar loads), G hypotheses unrolled per group
+  kScoreExactS8 = 7, kScoreMin3S8 = 8, kScoreExactS4 = 9, kScoreExactS8G4 = 10,
+  // FMA chains on v_mfma_f32_16x16x4f32, band compare + counting on the VALU (PA x 16 points/wave)
+  kScoreMfma32 = 11, kScoreMfma16 = 12, kScoreMfma8 = 13,
+  // lanes = hypotheses, points as wave-uniform scalars (s_load), per-lane v_addc counting
+  kScoreLanesExact = 14, kScoreLanesMin3 = 15,
+  // lanes = hypotheses, points staged in LDS, broadcast-read and moved to SGPRs
+  kScoreLdsExact = 16, kScoreLdsMin3 = 17,
+  kScoreNumVariants = 18
+};
+// hyps buffer layout for launch_score: HypRec[kMaxHypPerLaunch] followed by the packed float4
+// plane vectors and float band widths (score_scratch_bytes); counts need room for D rounded up
+// to a multiple of 64.
+constexpr size_t kHypScratchBytes =
+    kMaxHypPerLaunch * (sizeof(HypRec) + sizeof(float4) + sizeof(float));
+extern int kScoreDefault;
 
 void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
                            hipStream_t s);

@@ -159,6 +159,12 @@ dlg_status dlg_extract_planes(dlg_ctx* ctx, dlg_cloud* cloud, const dlg_sac_para
 /* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);
 dlg_status dlg_synchronize(dlg_ctx* ctx);
+/* Scoring-kernel micro-benchmark (kernel A/B on the device): D random plane hypotheses through
+ * the same gather/build path, `variant` (0 = exact PCL op order, 1 = FMA prefilter + exact band
+ * recheck, ...) launched `reps` times on the cloud's active points; returns the mean device
+ * time per launch and (optional) the counts of the last launch. */
+dlg_status dlg_score_benchmark(dlg_ctx* ctx, dlg_cloud* cloud, int D, int variant, int reps,
+                               double threshold, double* ms_per_launch, int32_t* counts_out);
 /* max over ranks of a host double (bench timing) and a barrier; no-ops for world == 1 */
 dlg_status dlg_allreduce_max_f64(dlg_ctx* ctx, double* value);
 dlg_status dlg_barrier(dlg_ctx* ctx);
