@@ -648,7 +648,8 @@ dlg_status dlg_ctx_create_dist(dlg_ctx** out, int device, int rank, int world, c
     g_last_create_error = c->err;
     return s;
   }
-  if (world == 1) {
+  const char* force = std::getenv("DLG_FORCE_RCCL");  // 1-rank RCCL communicator (path test)
+  if (world == 1 && !(force && force[0] == '1' && uid)) {
     c->comm = make_single_comm();
   } else {
     std::string err;

@@ -235,3 +235,25 @@ def test_cpp_shim_runs_on_gpu(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.startswith("coeff ")
+
+
+def test_rccl_one_rank_path(monkeypatch, gpu_ctx):
+    """The RCCL communicator code (dlopen, ncclCommInitRank, in-place allreduce, allgather,
+    allreduce-max) on a real device with one rank: same planes as the plain context."""
+    monkeypatch.setenv("DLG_FORCE_RCCL", "1")
+    p, _, _ = plane_cloud(30000, 4, seed=5)
+    prm = D.make_params(0.02, max_iterations=255, probability=1.0)
+    c0 = D.Cloud(gpu_ctx, p)
+    ref = D.extract_planes(c0, prm, max_planes=4, min_inliers=100)
+    c0.close()
+    uid = D.Context.unique_id()
+    ctx = D.Context.distributed(0, 0, 1, uid)
+    assert ctx.world == 1
+    c1 = D.Cloud(ctx, p)
+    out = D.extract_planes(c1, prm, max_planes=4, min_inliers=100)
+    assert np.array_equal(out["inliers"], ref["inliers"])
+    assert np.array_equal(out["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
+    assert ctx.allreduce_max(3.5) == 3.5
+    ctx.barrier()
+    c1.close()
+    ctx.close()

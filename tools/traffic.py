@@ -1,0 +1,59 @@
+"""Per-launch HBM traffic of the dominant kernels from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+runs of `bench.py --steps 1 --warmup 0` (separate passes, as MI355X_MICROARCH.md prescribes).
+
+FETCH_SIZE/WRITE_SIZE are in KB (1024 B).  gfx950 counts exactly half of the bytes of a wide
+(16 B/lane) coalesced read; other widths are uncalibrated, so the factor for our 4-B/lane SoA
+reads is measured here on k_select_count, whose algorithmic read is known exactly
+(12 B per active point, read once).  Writes -> profiles/score_traffic.json.
+"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(path, counter):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        m = re.search(r"(k_\w+)", r["Kernel_Name"])
+        if not m:
+            continue
+        out[m.group(1)].append((int(r["Dispatch_Id"]), float(r["Counter_Value"]), int(r["Grid_Size"])))
+    return out
+
+
+def main():
+    fetch = load(sys.argv[1], "FETCH_SIZE")
+    write = load(sys.argv[2], "WRITE_SIZE") if len(sys.argv) > 2 else {}
+    bench = json.loads(open(sys.argv[3]).read()) if len(sys.argv) > 3 else None
+    res = {}
+    for k, rows in fetch.items():
+        vals = [v for _, v, _ in rows]
+        res[k] = {"launches": len(rows), "fetch_bytes_mean": 1024 * sum(vals) / len(vals)}
+        if k in write:
+            w = [v for _, v, _ in write[k]]
+            res[k]["write_bytes_mean"] = 1024 * sum(w) / len(w)
+    # calibration on k_select_count: grid = tiles * 256 threads, 4096 points per tile
+    sc = sorted(fetch.get("k_select_count", []))
+    cal = None
+    if sc:
+        # first launch of a step runs on the full cloud: 12 B per point
+        n = bench["config"]["points_per_gpu"] if bench else None
+        if n:
+            cal = (12.0 * n) / (1024 * sc[0][1])
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, bench.py --steps 1 --warmup 0",
+           "kernels": res, "read_calibration_dword_loads": cal}
+    if "k_score" in res and cal:
+        out["hbm_bytes_per_launch"] = res["k_score"]["fetch_bytes_mean"] * cal + res["k_score"].get("write_bytes_mean", 0.0)
+    json.dump(out, open(os.path.join(ROOT, "profiles", "score_traffic.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
