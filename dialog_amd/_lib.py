@@ -23,7 +23,7 @@ SYMBOLS = [
     "dlg_last_error", "dlg_ctx_info", "dlg_cloud_upload", "dlg_cloud_destroy", "dlg_cloud_reset",
     "dlg_cloud_active", "dlg_sac_segment", "dlg_sac_segment_host", "dlg_extract_planes",
     "dlg_set_profiling", "dlg_synchronize", "dlg_allreduce_max_f64", "dlg_barrier",
-    "dlg_score_benchmark",
+    "dlg_score_benchmark", "dlg_estimate_normals", "dlg_regulate_normals",
 ]
 
 
@@ -99,6 +99,9 @@ def load():
     L.dlg_barrier.argtypes = [vp]
     L.dlg_score_benchmark.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                       C.POINTER(C.c_double), i32p]
+    L.dlg_estimate_normals.argtypes = [vp, C.POINTER(Points), C.c_float, C.c_int, fp, fp, C.c_int64]
+    L.dlg_regulate_normals.argtypes = [vp, C.POINTER(Points), fp, C.c_int64, C.c_int64, C.c_int,
+                                       C.c_float, C.POINTER(C.c_uint8), i64p]
     for s in SYMBOLS:
         if s not in ("dlg_abi_version", "dlg_status_string", "dlg_sac_params_default",
                      "dlg_last_error"):

@@ -35,62 +35,11 @@
 
 #include "../../include/dialog_ransac.h"
 #include "comm.hpp"
+#include "driver.hpp"
 #include "host_math.hpp"
 #include "kernels.hpp"
 
 namespace dlg {
-
-struct DlgError : std::runtime_error {
-  DlgError(dlg_status c, const std::string& m) : std::runtime_error(m), code(c) {}
-  dlg_status code;
-};
-
-#define HIPCHK(expr)                                                                          \
-  do {                                                                                        \
-    hipError_t e_ = (expr);                                                                   \
-    if (e_ != hipSuccess)                                                                     \
-      throw DlgError(DLG_ERR_HIP, std::string(#expr) + " -> " + hipGetErrorString(e_));       \
-  } while (0)
-
-template <typename T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t cap = 0;
-  void ensure(size_t n) {
-    if (n <= cap) return;
-    if (p) HIPCHK(hipFree(p));
-    p = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(n, 16);
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T)));
-    cap = want;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-};
-
-template <typename T>
-struct PinBuf {
-  T* p = nullptr;
-  size_t cap = 0;
-  void ensure(size_t n) {
-    if (n <= cap) return;
-    if (p) HIPCHK(hipHostFree(p));
-    p = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(n, 16);
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault));
-    cap = want;
-  }
-  void release() {
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-};
 
 // sparse overlay of SampleConsensusModel::shuffled_indices_ over list positions: pos -> pos'
 class Overlay {
@@ -143,69 +92,11 @@ class Overlay {
   size_t mask_ = 0, size_ = 0;
 };
 
-struct SoA {
-  DevBuf<float> x, y, z;
-  DevBuf<int32_t> gid;
-  void ensure(size_t n) { x.ensure(n); y.ensure(n); z.ensure(n); gid.ensure(n); }
-  void release() { x.release(); y.release(); z.release(); gid.release(); }
-  PointsView view(int64_t n) const { return PointsView{x.p, y.p, z.p, gid.p, n}; }
-  PointsOut out() { return PointsOut{x.p, y.p, z.p, gid.p}; }
-};
-
 }  // namespace dlg
 
 using namespace dlg;
 
-struct dlg_ctx {
-  int device = 0;
-  int num_cus = 256;
-  hipStream_t stream = nullptr;
-  std::unique_ptr<Comm> comm;
-  std::string err;
-  bool profiling = false;
-  // scratch
-  DevBuf<int32_t> pos;
-  DevBuf<SampleRec> samples;
-  DevBuf<HypRec> hyps;
-  DevBuf<int32_t> res;  // counts[D] | good[D]
-  DevBuf<int32_t> tile_in, tile_off_in, tile_off_out, totals;
-  DevBuf<double> partials, moments;
-  DevBuf<int32_t> inl_gid;
-  DevBuf<float> inl_xyz;
-  DevBuf<int64_t> gath64;
-  DevBuf<int32_t> gath32;
-  PinBuf<int32_t> h_pos, h_res, h_tot;
-  PinBuf<double> h_mom;
-  PinBuf<int64_t> h_g64;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  std::vector<int32_t> h_inl;
-  std::vector<float> h_xyz;
-  // inlier ids of the previous extract round: D2H into pinned staging is enqueued behind the
-  // round's select, the memcpy into the caller's buffer runs while the next round's scoring
-  // kernel executes (the host would otherwise only wait for it)
-  PinBuf<int32_t> h_stage;
-  hipEvent_t ev_stage = nullptr;
-  int32_t* pending_dst = nullptr;
-  int64_t pending_n = 0;
-};
-
-struct dlg_cloud {
-  dlg_ctx* ctx = nullptr;
-  int64_t n_total = 0;
-  int64_t n_active = 0;
-  int cur = -1;  // -1 pristine, 0 = A, 1 = B
-  SoA pristine, buf[2];
-  float amax[3] = {0, 0, 0};
-  PointsView view() const {
-    const SoA& s = cur < 0 ? pristine : buf[cur];
-    return s.view(n_active);
-  }
-  int spare() const { return cur == 0 ? 1 : 0; }
-};
-
 namespace {
-
-void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
 
 // DLG_TRACE=1: per-round host timing breakdown on stderr (diagnostics only)
 bool trace_on() {
@@ -218,8 +109,6 @@ bool trace_on() {
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-
-void sync(dlg_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); }
 
 int64_t allgather_i64(dlg_ctx* c, int64_t v, std::vector<int64_t>* all) {
   const int W = c->comm->world();
@@ -536,27 +425,6 @@ int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, in
   return so.n_in_local;
 }
 
-dlg_status fail(dlg_ctx* c, dlg_status code, const std::string& msg) {
-  if (c) c->err = msg;
-  return code;
-}
-
-template <typename F>
-dlg_status guarded(dlg_ctx* c, F&& f) {
-  try {
-    if (c) set_device(c);
-    f();
-    if (c) c->err.clear();
-    return DLG_OK;
-  } catch (const DlgError& e) {
-    return fail(c, e.code, e.what());
-  } catch (const std::exception& e) {
-    return fail(c, DLG_ERR_INTERNAL, e.what());
-  } catch (...) {
-    return fail(c, DLG_ERR_INTERNAL, "unknown error");
-  }
-}
-
 std::string g_last_create_error;
 
 dlg_status init_ctx(dlg_ctx* c, int device) {
@@ -694,6 +562,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->gath64.release(); c->gath32.release();
   c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
   c->h_stage.release();
+  c->nw.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);

@@ -1,0 +1,192 @@
+// driver.hpp -- host-side state shared by the RANSAC driver (driver.cpp) and the normals driver
+// (normals_host.cpp): error type, device/pinned buffers, the context and cloud objects.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/dialog_ransac.h"
+#include "comm.hpp"
+#include "kernels.hpp"
+
+namespace dlg {
+
+struct DlgError : std::runtime_error {
+  DlgError(dlg_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+  dlg_status code;
+};
+
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      throw DlgError(DLG_ERR_HIP, std::string(#expr) + " -> " + hipGetErrorString(e_));       \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 16);
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T)));
+    cap = want;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+template <typename T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) HIPCHK(hipHostFree(p));
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 16);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault));
+    cap = want;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct SoA {
+  DevBuf<float> x, y, z;
+  DevBuf<int32_t> gid;
+  void ensure(size_t n) { x.ensure(n); y.ensure(n); z.ensure(n); gid.ensure(n); }
+  void release() { x.release(); y.release(); z.release(); gid.release(); }
+  PointsView view(int64_t n) const { return PointsView{x.p, y.p, z.p, gid.p, n}; }
+  PointsOut out() { return PointsOut{x.p, y.p, z.p, gid.p}; }
+};
+
+// one sorted grid of the normals path (normals.hip): points in cell order + occupied-cell table
+struct GridLevelBufs {
+  DevBuf<float> sx, sy, sz;
+  DevBuf<int32_t> idx;
+  DevBuf<uint32_t> tkeys;
+  DevBuf<int2> trange;
+  void release() {
+    sx.release(); sy.release(); sz.release(); idx.release(); tkeys.release(); trange.release();
+  }
+};
+
+// scratch of the normals / RegulateNormal path (normals_host.cpp)
+struct NormalsWork {
+  static constexpr int kLevels = 12;
+  GridLevelBufs lv[kLevels];
+  DevBuf<uint8_t> raw, out, processed, sort_tmp;
+  DevBuf<float> x, y, z, partial;
+  DevBuf<uint32_t> keys_in, keys_out, counters;
+  DevBuf<int32_t> idx_in, queue, cand, ids_alt;
+  DevBuf<float4> nrm;
+  DevBuf<unsigned long long> claim, keys64, keys_alt;
+  PinBuf<uint32_t> h_cnt;
+  void release() {
+    for (auto& l : lv) l.release();
+    raw.release(); out.release(); processed.release(); sort_tmp.release();
+    x.release(); y.release(); z.release(); partial.release();
+    keys_in.release(); keys_out.release(); counters.release();
+    idx_in.release(); queue.release(); cand.release(); ids_alt.release();
+    nrm.release(); claim.release(); keys64.release(); keys_alt.release(); h_cnt.release();
+  }
+};
+
+}  // namespace dlg
+
+using namespace dlg;
+
+struct dlg_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  std::unique_ptr<Comm> comm;
+  std::string err;
+  bool profiling = false;
+  // scratch
+  DevBuf<int32_t> pos;
+  DevBuf<SampleRec> samples;
+  DevBuf<HypRec> hyps;
+  DevBuf<int32_t> res;  // counts[D] | good[D]
+  DevBuf<int32_t> tile_in, tile_off_in, tile_off_out, totals;
+  DevBuf<double> partials, moments;
+  DevBuf<int32_t> inl_gid;
+  DevBuf<float> inl_xyz;
+  DevBuf<int64_t> gath64;
+  DevBuf<int32_t> gath32;
+  PinBuf<int32_t> h_pos, h_res, h_tot;
+  PinBuf<double> h_mom;
+  PinBuf<int64_t> h_g64;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<int32_t> h_inl;
+  std::vector<float> h_xyz;
+  // inlier ids of the previous extract round: D2H into pinned staging is enqueued behind the
+  // round's select, the memcpy into the caller's buffer runs while the next round's scoring
+  // kernel executes (the host would otherwise only wait for it)
+  PinBuf<int32_t> h_stage;
+  hipEvent_t ev_stage = nullptr;
+  int32_t* pending_dst = nullptr;
+  int64_t pending_n = 0;
+  NormalsWork nw;
+};
+
+struct dlg_cloud {
+  dlg_ctx* ctx = nullptr;
+  int64_t n_total = 0;
+  int64_t n_active = 0;
+  int cur = -1;  // -1 pristine, 0 = A, 1 = B
+  SoA pristine, buf[2];
+  float amax[3] = {0, 0, 0};
+  PointsView view() const {
+    const SoA& s = cur < 0 ? pristine : buf[cur];
+    return s.view(n_active);
+  }
+  int spare() const { return cur == 0 ? 1 : 0; }
+};
+
+namespace dlg {
+
+inline void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
+inline void sync(dlg_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); }
+
+inline dlg_status fail(dlg_ctx* c, dlg_status code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+// runs f with the context's device current; exceptions become status codes + dlg_last_error text
+template <typename F>
+dlg_status guarded(dlg_ctx* c, F&& f) {
+  try {
+    if (c) set_device(c);
+    f();
+    if (c) c->err.clear();
+    return DLG_OK;
+  } catch (const DlgError& e) {
+    return fail(c, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(c, DLG_ERR_INTERNAL, e.what());
+  } catch (...) {
+    return fail(c, DLG_ERR_INTERNAL, "unknown error");
+  }
+}
+
+}  // namespace dlg

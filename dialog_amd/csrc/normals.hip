@@ -1,0 +1,566 @@
+// normals.hip -- neighbour-search normal estimation and RegulateNormal BFS on gfx950.
+//
+// Replaces Dialog/PlaneDetect.h:515-545 estimateNormal() (pcl::NormalEstimationOMP with
+// setRadiusSearch(r_for_estimate_normal)), the k = 20 NormalEstimation of PCLViewer.cpp:507-522 /
+// TriangularMeshing.h:28-35, and the BFS of PlaneDetect.h:547-665 regulateNormal().
+//
+// Neighbour search: a uniform grid with cells >= r, points sorted by cell key (hipCUB radix sort,
+// stable, so deterministic), occupied cells in an open-addressing hash (key -> [begin, end) of the
+// sorted order).  A radius query visits the 27 cells around its own; the neighbour test is the
+// one KdTreeFLANN applies: d2 = ((0 + dx^2) + dy^2) + dz^2 in float with d = q - p, kept iff
+// d2 < (float)(r * r).  Every candidate sits in exactly one cell, so nothing is double counted.
+//
+// Normals: covariance of the neighbourhood accumulated in double on coordinates centred at the
+// query (PCL 1.8 sums raw float coordinates single-pass; that loses ~1e-3 relative accuracy away
+// from the origin -- the result here is the better-conditioned value of the same quantity),
+// pcl::eigen33 in double, curvature = |lambda0 / trace|, flipNormalTowardsViewpoint in float in
+// PCL's order.  Fewer than 3 neighbours or a non-finite query -> NaN normal and curvature.
+//
+// RegulateNormal: level-synchronous BFS that reproduces PCL's sequential queue exactly.  In the
+// sequential BFS a node is claimed by the first popped node (queue order) having it within
+// r_regulate; levels are contiguous in the queue, so a node is claimed by the smallest queue
+// position of the current level that reaches it (64-bit atomicMin), and the next level is ordered
+// as PCL pushes it: by parent position, then by the parent's neighbour-list order (d2, index).
+// A node flips iff dot(parent normal, node normal) < 0 in float, left to right (PlaneDetect.h:629).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+
+#include "normals.hpp"
+
+namespace dlg {
+
+namespace {
+
+constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr int kBS = 256;
+
+__device__ __forceinline__ uint32_t hash_key(uint32_t k) {
+  k ^= k >> 16;
+  k *= 0x7feb352du;
+  k ^= k >> 15;
+  k *= 0x846ca68bu;
+  k ^= k >> 16;
+  return k;
+}
+
+__device__ __forceinline__ bool finite3(float x, float y, float z) {
+  return isfinite(x) && isfinite(y) && isfinite(z);
+}
+
+__device__ __forceinline__ int cell_of(float v, float lo, float inv_cell, int g) {
+  int c = (int)floorf((v - lo) * inv_cell);
+  return c < 0 ? 0 : (c >= g ? g - 1 : c);
+}
+
+__device__ __forceinline__ uint32_t cell_key(const GridDesc& G, int x, int y, int z) {
+  return (uint32_t)((z * G.g[1] + y) * G.g[0] + x);
+}
+
+__device__ __forceinline__ float flann_d2(float qx, float qy, float qz, float px, float py, float pz) {
+  const float ex = qx - px, ey = qy - py, ez = qz - pz;
+  return ((0.0f + ex * ex) + ey * ey) + ez * ez;
+}
+
+// ---------------------------------------------------------------------------------------------
+// bounding box of the finite points
+__global__ __launch_bounds__(kBS) void k_bbox(const float* __restrict__ X, const float* __restrict__ Y,
+                                              const float* __restrict__ Z, int n,
+                                              float* __restrict__ partial) {
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = blockIdx.x * kBS + threadIdx.x; i < n; i += gridDim.x * kBS) {
+    const float x = X[i], y = Y[i], z = Z[i];
+    if (!finite3(x, y, z)) continue;
+    lo[0] = fminf(lo[0], x); lo[1] = fminf(lo[1], y); lo[2] = fminf(lo[2], z);
+    hi[0] = fmaxf(hi[0], x); hi[1] = fmaxf(hi[1], y); hi[2] = fmaxf(hi[2], z);
+  }
+  __shared__ float s[6][kBS / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int k = 0; k < 3; ++k) {
+    float a = lo[k], b = hi[k];
+    for (int o = 32; o > 0; o >>= 1) {
+      a = fminf(a, __shfl_xor(a, o, 64));
+      b = fmaxf(b, __shfl_xor(b, o, 64));
+    }
+    if (lane == 0) { s[k][w] = a; s[3 + k][w] = b; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int k = threadIdx.x;
+    float v = s[k][0];
+    for (int t = 1; t < kBS / 64; ++t) v = k < 3 ? fminf(v, s[k][t]) : fmaxf(v, s[k][t]);
+    partial[6 * blockIdx.x + k] = v;
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_cell_keys(const float* __restrict__ X,
+                                                   const float* __restrict__ Y,
+                                                   const float* __restrict__ Z, int n, GridDesc G,
+                                                   uint32_t* __restrict__ keys,
+                                                   int32_t* __restrict__ idx) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const float x = X[i], y = Y[i], z = Z[i];
+  uint32_t k = G.ncells;  // non-finite: sorted last, never inserted
+  if (finite3(x, y, z))
+    k = cell_key(G, cell_of(x, G.lo[0], G.inv_cell, G.g[0]), cell_of(y, G.lo[1], G.inv_cell, G.g[1]),
+                 cell_of(z, G.lo[2], G.inv_cell, G.g[2]));
+  keys[i] = k;
+  idx[i] = i;
+}
+
+// sorted keys -> cell table + coordinates in sorted order
+__global__ __launch_bounds__(kBS) void k_cells_build(
+    const uint32_t* __restrict__ skeys, const int32_t* __restrict__ sidx, int n, uint32_t ncells,
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    uint32_t* __restrict__ tkeys, int2* __restrict__ trange, uint32_t tmask,
+    float* __restrict__ sx, float* __restrict__ sy, float* __restrict__ sz,
+    uint32_t* __restrict__ n_occupied) {
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= n) return;
+  const int i = sidx[t];
+  sx[t] = X[i];
+  sy[t] = Y[i];
+  sz[t] = Z[i];
+  const uint32_t k = skeys[t];
+  if (k == ncells || (t > 0 && skeys[t - 1] == k)) return;
+  int e = t + 1;
+  while (e < n && skeys[e] == k) ++e;  // run length of one cell
+  uint32_t h = hash_key(k) & tmask;
+  while (true) {
+    const uint32_t prev = atomicCAS(&tkeys[h], kEmpty, k);
+    if (prev == kEmpty) break;
+    h = (h + 1) & tmask;
+  }
+  trange[h] = make_int2(t, e);
+  atomicAdd(n_occupied, 1u);
+}
+
+__device__ __forceinline__ int2 cell_range(const uint32_t* __restrict__ tkeys,
+                                           const int2* __restrict__ trange, uint32_t tmask,
+                                           uint32_t k) {
+  uint32_t h = hash_key(k) & tmask;
+  while (true) {
+    const uint32_t tk = tkeys[h];
+    if (tk == k) return trange[h];
+    if (tk == kEmpty) return make_int2(0, 0);
+    h = (h + 1) & tmask;
+  }
+}
+
+// ---- pcl::computeRoots / pcl::eigen33 (common/impl/eigen.hpp), in double ----
+__device__ void roots2_d(double b, double c, double r[3]) {
+  r[0] = 0.0;
+  double d = b * b - 4.0 * c;
+  if (d < 0.0) d = 0.0;
+  const double sd = sqrt(d);
+  r[2] = 0.5 * (b + sd);
+  r[1] = 0.5 * (b - sd);
+}
+
+__device__ void compute_roots_d(const double m[9], double r[3]) {
+  const double c0 = m[0] * m[4] * m[8] + 2.0 * m[1] * m[2] * m[5] - m[0] * m[5] * m[5] -
+                    m[4] * m[2] * m[2] - m[8] * m[1] * m[1];
+  const double c1 =
+      m[0] * m[4] - m[1] * m[1] + m[0] * m[8] - m[2] * m[2] + m[4] * m[8] - m[5] * m[5];
+  const double c2 = m[0] + m[4] + m[8];
+  if (fabs(c0) < DBL_EPSILON) {
+    roots2_d(c2, c1, r);
+    return;
+  }
+  const double s_inv3 = 1.0 / 3.0, s_sqrt3 = sqrt(3.0);
+  const double c2_over_3 = c2 * s_inv3;
+  double a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
+  if (a_over_3 > 0.0) a_over_3 = 0.0;
+  const double half_b = 0.5 * (c0 + c2_over_3 * (2.0 * c2_over_3 * c2_over_3 - c1));
+  double q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
+  if (q > 0.0) q = 0.0;
+  const double rho = sqrt(-a_over_3);
+  const double theta = atan2(sqrt(-q), half_b) * s_inv3;
+  const double ct = cos(theta), st = sin(theta);
+  r[0] = c2_over_3 + 2.0 * rho * ct;
+  r[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
+  r[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
+  double t;
+  if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+  if (r[1] >= r[2]) {
+    t = r[1]; r[1] = r[2]; r[2] = t;
+    if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+  }
+  if (r[0] <= 0.0) roots2_d(c2, c1, r);
+}
+
+// smallest eigenvalue / eigenvector of a symmetric 3x3 (row-major m)
+__device__ void eigen33_d(const double mat[9], double* eval, double v[3]) {
+  double scale = 0.0;
+  for (int k = 0; k < 9; ++k) scale = fmax(scale, fabs(mat[k]));
+  if (scale <= DBL_MIN) scale = 1.0;
+  double m[9];
+  for (int k = 0; k < 9; ++k) m[k] = mat[k] / scale;
+  double r[3];
+  compute_roots_d(m, r);
+  *eval = r[0] * scale;
+  m[0] -= r[0]; m[4] -= r[0]; m[8] -= r[0];
+  // row0 x row1, row0 x row2, row1 x row2
+  const double a0x = m[1] * m[5] - m[2] * m[4], a0y = m[2] * m[3] - m[0] * m[5], a0z = m[0] * m[4] - m[1] * m[3];
+  const double a1x = m[1] * m[8] - m[2] * m[7], a1y = m[2] * m[6] - m[0] * m[8], a1z = m[0] * m[7] - m[1] * m[6];
+  const double a2x = m[4] * m[8] - m[5] * m[7], a2y = m[5] * m[6] - m[3] * m[8], a2z = m[3] * m[7] - m[4] * m[6];
+  const double l0 = a0x * a0x + a0y * a0y + a0z * a0z;
+  const double l1 = a1x * a1x + a1y * a1y + a1z * a1z;
+  const double l2 = a2x * a2x + a2y * a2y + a2z * a2z;
+  double vx = a0x, vy = a0y, vz = a0z, l = l0;
+  if (l1 > l) { vx = a1x; vy = a1y; vz = a1z; l = l1; }
+  if (l2 > l) { vx = a2x; vy = a2y; vz = a2z; l = l2; }
+  const double s = sqrt(l);
+  v[0] = vx / s; v[1] = vy / s; v[2] = vz / s;
+}
+
+// centred double moments -> (normal, curvature), viewpoint flip in float (PCL order)
+struct Moments {
+  double s0 = 0, sx = 0, sy = 0, sz = 0, sxx = 0, sxy = 0, sxz = 0, syy = 0, syz = 0, szz = 0;
+  __device__ __forceinline__ void add(float px, float py, float pz, float qx, float qy, float qz) {
+    const double ax = (double)px - qx, ay = (double)py - qy, az = (double)pz - qz;
+    s0 += 1.0;
+    sx += ax; sy += ay; sz += az;
+    sxx += ax * ax; sxy += ax * ay; sxz += ax * az;
+    syy += ay * ay; syz += ay * az; szz += az * az;
+  }
+};
+
+__device__ float4 finish_normal(const Moments& M, float qx, float qy, float qz, float vpx,
+                                float vpy, float vpz) {
+  if (M.s0 < 3.0) {
+    const float qnan = __builtin_nanf("");
+    return make_float4(qnan, qnan, qnan, qnan);
+  }
+  const double inv = 1.0 / M.s0;
+  const double mx = M.sx * inv, my = M.sy * inv, mz = M.sz * inv;
+  double cov[9];
+  cov[0] = M.sxx * inv - mx * mx;
+  cov[1] = M.sxy * inv - mx * my;
+  cov[2] = M.sxz * inv - mx * mz;
+  cov[4] = M.syy * inv - my * my;
+  cov[5] = M.syz * inv - my * mz;
+  cov[8] = M.szz * inv - mz * mz;
+  cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+  double ev, v[3];
+  eigen33_d(cov, &ev, v);
+  const double tr = cov[0] + cov[4] + cov[8];
+  const float curv = tr != 0.0 ? (float)fabs(ev / tr) : 0.0f;
+  float nx = (float)v[0], ny = (float)v[1], nz = (float)v[2];
+  // pcl::flipNormalTowardsViewpoint: vp -= p; if (vp.dot(n) < 0) n *= -1
+  const float vx = vpx - qx, vy = vpy - qy, vz = vpz - qz;
+  const float cos_theta = vx * nx + vy * ny + vz * nz;
+  if (cos_theta < 0.0f) { nx *= -1.0f; ny *= -1.0f; nz *= -1.0f; }
+  return make_float4(nx, ny, nz, curv);
+}
+
+// one thread per query, queries taken in sorted-cell order so a wavefront shares its cells
+__global__ __launch_bounds__(kBS) void k_normals_radius(
+    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
+    const int32_t* __restrict__ sidx, int n, GridDesc G, const uint32_t* __restrict__ tkeys,
+    const int2* __restrict__ trange, uint32_t tmask, float r2, float vpx, float vpy, float vpz,
+    float4* __restrict__ normals) {
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= n) return;
+  const float qx = sx[t], qy = sy[t], qz = sz[t];
+  Moments M;
+  if (finite3(qx, qy, qz)) {
+    const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+    const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+    const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+    for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
+      for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
+        for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
+          const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+          for (int u = rg.x; u < rg.y; ++u) {
+            const float px = sx[u], py = sy[u], pz = sz[u];
+            if (flann_d2(qx, qy, qz, px, py, pz) < r2) M.add(px, py, pz, qx, qy, qz);
+          }
+        }
+  }
+  normals[sidx[t]] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+}
+
+// k nearest neighbours over a grid hierarchy (cell_l = 2^l * cell_0, the top level has <= 2 cells
+// per axis).  At level l the 27 cells around the query hold every point closer than cell_l, so if
+// at least K candidates have d2 < cell_l^2 their K smallest (d2, index) are exactly FLANN's kNN
+// set (anything unvisited is farther, ties included).  Otherwise the query moves up a level; at
+// the top level the 27 cells are the whole cloud and every candidate counts.  One launch per
+// level over the queries still open (compacted), so the few sparse outliers that climb do not
+// hold back the wavefronts of the surface points, which finish at level 0.
+__global__ __launch_bounds__(kBS) void k_normals_knn(
+    KnnLevels L, int l, const int32_t* __restrict__ qlist, int nq, const float* __restrict__ X,
+    const float* __restrict__ Y, const float* __restrict__ Z, int K, float vpx, float vpy,
+    float vpz, float4* __restrict__ normals, int32_t* __restrict__ next,
+    uint32_t* __restrict__ n_next) {
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= nq) return;
+  int qi;
+  float qx, qy, qz;
+  if (qlist) {
+    qi = qlist[t];
+    qx = X[qi]; qy = Y[qi]; qz = Z[qi];
+  } else {  // level 0: every query, in level-0 cell order (wavefronts share cells)
+    qi = L.idx[0][t];
+    qx = L.sx[0][t]; qy = L.sy[0][t]; qz = L.sz[0][t];
+  }
+  Moments M;
+  if (finite3(qx, qy, qz)) {
+    const GridDesc& G = L.G[l];
+    const bool top = l == L.levels - 1;
+    const float lim = top ? INFINITY : G.cell * G.cell;
+    const float* __restrict__ sx = L.sx[l];
+    const float* __restrict__ sy = L.sy[l];
+    const float* __restrict__ sz = L.sz[l];
+    const int32_t* __restrict__ sidx = L.idx[l];
+    float bd[kMaxKnn];
+    int bi[kMaxKnn];
+    int cnt = 0;
+    const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+    const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+    const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+    for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
+      for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
+        for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
+          const int2 rg = cell_range(L.tkeys[l], L.trange[l], L.tmask[l], cell_key(G, x, y, z));
+          for (int u = rg.x; u < rg.y; ++u) {
+            const float d2 = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
+            if (!(d2 < lim)) continue;
+            const int iu = sidx[u];
+            if (cnt == K) {
+              const float w = bd[K - 1];
+              if (d2 > w || (d2 == w && iu > bi[K - 1])) continue;
+            }
+            int p = cnt < K ? cnt++ : K - 1;
+            while (p > 0 && (bd[p - 1] > d2 || (bd[p - 1] == d2 && bi[p - 1] > iu))) {
+              bd[p] = bd[p - 1];
+              bi[p] = bi[p - 1];
+              --p;
+            }
+            bd[p] = d2;
+            bi[p] = iu;
+          }
+        }
+    if (cnt < K && !top) {
+      next[atomicAdd(n_next, 1u)] = qi;
+      return;
+    }
+    for (int j = 0; j < cnt; ++j) {
+      const int i = bi[j];
+      M.add(X[i], Y[i], Z[i], qx, qy, qz);
+    }
+  }
+  normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+}
+
+// ---------------------------------------------------------------------------------------------
+// RegulateNormal BFS, one level per (claim, settle, order)
+__global__ __launch_bounds__(kBS) void k_bfs_claim(
+    const int32_t* __restrict__ queue, int64_t fbase, int nf, const float* __restrict__ X,
+    const float* __restrict__ Y, const float* __restrict__ Z, const float* __restrict__ sx,
+    const float* __restrict__ sy, const float* __restrict__ sz, const int32_t* __restrict__ sidx,
+    GridDesc G, const uint32_t* __restrict__ tkeys, const int2* __restrict__ trange,
+    uint32_t tmask, float r2, const uint8_t* __restrict__ processed,
+    unsigned long long* __restrict__ claim, int32_t* __restrict__ cand,
+    uint32_t* __restrict__ ncand) {
+  const int f = blockIdx.x * kBS + threadIdx.x;
+  if (f >= nf) return;
+  const unsigned long long mypos = (unsigned long long)(fbase + f);
+  const int32_t cur = queue[mypos];
+  const float qx = X[cur], qy = Y[cur], qz = Z[cur];
+  if (!finite3(qx, qy, qz)) return;
+  const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+  const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+  const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+  for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
+    for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
+      for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
+        const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+        for (int u = rg.x; u < rg.y; ++u) {
+          const int32_t j = sidx[u];
+          if (processed[j]) continue;
+          if (flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2) {
+            if (atomicMin(&claim[j], mypos) == ~0ull) cand[atomicAdd(ncand, 1u)] = j;
+          }
+        }
+      }
+}
+
+__global__ __launch_bounds__(kBS) void k_bfs_settle(
+    const int32_t* __restrict__ queue, const int32_t* __restrict__ cand, int nc,
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    uint8_t* __restrict__ processed, const unsigned long long* __restrict__ claim,
+    float4* __restrict__ normals, unsigned long long* __restrict__ keys) {
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= nc) return;
+  const int32_t j = cand[t];
+  const unsigned long long ppos = claim[j];
+  const int32_t parent = queue[ppos];
+  const float4 pn = normals[parent];
+  float4 nn = normals[j];
+  const float dp = pn.x * nn.x + pn.y * nn.y + pn.z * nn.z;
+  if (dp < 0.0f) {
+    nn.x *= -1.0f; nn.y *= -1.0f; nn.z *= -1.0f;
+    normals[j] = nn;
+  }
+  processed[j] = 1;
+  // the parent's neighbour list is sorted by the d2 FLANN computes for query = parent
+  const float d2 = flann_d2(X[parent], Y[parent], Z[parent], X[j], Y[j], Z[j]);
+  keys[t] = (ppos << 32) | (unsigned long long)__float_as_uint(d2);
+}
+
+__global__ __launch_bounds__(kBS) void k_pack_normals(const float4* __restrict__ nrm, int n,
+                                                      float* __restrict__ out, int64_t stride,
+                                                      int curv_offset) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const float4 v = nrm[i];
+  float* o = out + (int64_t)i * stride;
+  o[0] = v.x; o[1] = v.y; o[2] = v.z;
+  if (curv_offset < 0) return;  // direction only: leave the caller's other fields alone
+  for (int f = 3; f < stride; ++f) o[f] = f == curv_offset ? v.w : 0.0f;
+}
+
+__global__ __launch_bounds__(kBS) void k_unpack_normals(const float* __restrict__ in, int n,
+                                                        int64_t stride, float4* __restrict__ nrm) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const float* p = in + (int64_t)i * stride;
+  nrm[i] = make_float4(p[0], p[1], p[2], 0.0f);
+}
+
+__global__ __launch_bounds__(kBS) void k_deinterleave(const float* __restrict__ raw, int n,
+                                                      int64_t stride, float* __restrict__ X,
+                                                      float* __restrict__ Y, float* __restrict__ Z) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const float* p = raw + (int64_t)i * stride;
+  X[i] = p[0];
+  Y[i] = p[1];
+  Z[i] = p[2];
+}
+
+inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+int bbox_blocks(int n) {
+  int b = (int)cdiv(n, kBS * 8);
+  return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+}
+
+void launch_bbox(const float* X, const float* Y, const float* Z, int n, float* partial,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(k_bbox, dim3(bbox_blocks(n)), dim3(kBS), 0, s, X, Y, Z, n, partial);
+}
+
+size_t sort_tmp_bytes(int n, int key_bits) {
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (int32_t*)nullptr, (int32_t*)nullptr, n, 0, key_bits);
+  return tmp;
+}
+
+hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, const GridDesc& G,
+                      GridBufs& B, uint32_t* n_occupied, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(B.tkeys, 0xff, (size_t)(B.tmask + 1) * 4, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(n_occupied, 0, 4, s);
+  if (e != hipSuccess || n <= 0) return e;
+  hipLaunchKernelGGL(k_cell_keys, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, X, Y, Z, n, G, B.keys_in,
+                     B.idx_in);
+  size_t tmp = B.sort_tmp_bytes;
+  e = hipcub::DeviceRadixSort::SortPairs(B.sort_tmp, tmp, B.keys_in, B.keys_out, B.idx_in,
+                                         B.idx_out, n, 0, G.key_bits, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_cells_build, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.keys_out, B.idx_out, n,
+                     G.ncells, X, Y, Z, B.tkeys, B.trange, B.tmask, B.sx, B.sy, B.sz, n_occupied);
+  return hipGetLastError();
+}
+
+void launch_normals_radius(const GridDesc& G, const GridBufs& B, int n, float r2, const float vp[3],
+                           float4* normals, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_normals_radius, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.sx, B.sy, B.sz,
+                     B.idx_out, n, G, B.tkeys, B.trange, B.tmask, r2, vp[0], vp[1], vp[2],
+                     normals);
+}
+
+void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qlist, int nq,
+                        const float* X, const float* Y, const float* Z, int k, const float vp[3],
+                        float4* normals, int32_t* next, uint32_t* n_next, hipStream_t s) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(k_normals_knn, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, L, level, qlist, nq, X, Y,
+                     Z, k, vp[0], vp[1], vp[2], normals, next, n_next);
+}
+
+void launch_bfs_claim(const int32_t* queue, int64_t fbase, int nf, const float* X, const float* Y,
+                      const float* Z, const GridDesc& G, const GridBufs& B, float r2,
+                      const uint8_t* processed, unsigned long long* claim, int32_t* cand,
+                      uint32_t* ncand, hipStream_t s) {
+  if (nf <= 0) return;
+  hipLaunchKernelGGL(k_bfs_claim, dim3(cdiv(nf, kBS)), dim3(kBS), 0, s, queue, fbase, nf, X, Y, Z,
+                     B.sx, B.sy, B.sz, B.idx_out, G, B.tkeys, B.trange, B.tmask, r2, processed,
+                     claim, cand, ncand);
+}
+
+void launch_bfs_settle(const int32_t* queue, const int32_t* cand, int nc, const float* X,
+                       const float* Y, const float* Z, uint8_t* processed,
+                       const unsigned long long* claim, float4* normals,
+                       unsigned long long* keys, hipStream_t s) {
+  if (nc <= 0) return;
+  hipLaunchKernelGGL(k_bfs_settle, dim3(cdiv(nc, kBS)), dim3(kBS), 0, s, queue, cand, nc, X, Y, Z,
+                     processed, claim, normals, keys);
+}
+
+size_t bfs_sort_tmp_bytes(int n) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (int32_t*)nullptr, (int32_t*)nullptr,
+                                           (unsigned long long*)nullptr,
+                                           (unsigned long long*)nullptr, n);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (unsigned long long*)nullptr,
+                                           (unsigned long long*)nullptr, (int32_t*)nullptr,
+                                           (int32_t*)nullptr, n);
+  return a > b ? a : b;
+}
+
+hipError_t bfs_order(void* tmp, size_t tmp_bytes, int32_t* cand, unsigned long long* keys,
+                     int32_t* ids_alt, unsigned long long* keys_alt, int32_t* out_ids, int nc,
+                     hipStream_t s) {
+  if (nc <= 0) return hipSuccess;
+  size_t t = tmp_bytes;
+  // ids ascending (the atomic append order is arbitrary), then stable by (parent pos, d2)
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, t, cand, ids_alt, keys, keys_alt, nc, 0,
+                                                    32, s);
+  if (e != hipSuccess) return e;
+  t = tmp_bytes;
+  return hipcub::DeviceRadixSort::SortPairs(tmp, t, keys_alt, keys, ids_alt, out_ids, nc, 0, 64, s);
+}
+
+void launch_pack_normals(const float4* nrm, int n, float* out, int64_t stride_floats,
+                         int curv_offset, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pack_normals, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, nrm, n, out,
+                     stride_floats, curv_offset);
+}
+
+void launch_deinterleave(const float* raw, int n, int64_t stride_floats, float* X, float* Y,
+                         float* Z, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_deinterleave, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, raw, n, stride_floats, X,
+                     Y, Z);
+}
+
+void launch_unpack_normals(const float* in, int n, int64_t stride_floats, float4* nrm,
+                           hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_unpack_normals, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, in, n, stride_floats,
+                     nrm);
+}
+
+}  // namespace dlg

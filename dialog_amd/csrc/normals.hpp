@@ -1,0 +1,102 @@
+// normals.hpp -- uniform-grid neighbour search, normal estimation and RegulateNormal BFS kernels
+// (normals.hip), driven by normals_host.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace dlg {
+
+// Uniform grid over the cloud's bounding box; cell edge >= the search radius so a radius query
+// touches at most the 27 cells around its own.  Cell key = (cz * gy + cy) * gx + cx < ncells
+// <= 2^30; key ncells marks a non-finite point (sorted last, never inserted).
+struct GridDesc {
+  float lo[3];
+  float cell;
+  float inv_cell;
+  int g[3];
+  uint32_t ncells;
+  int key_bits;
+};
+
+// Device buffers of one grid (owned by the caller).  Sorted order: position t holds point
+// idx_out[t] with coordinates (sx, sy, sz)[t]; the open-addressing cell table maps an occupied
+// cell's key to its [begin, end) range of sorted positions.
+struct GridBufs {
+  uint32_t* keys_in = nullptr;
+  uint32_t* keys_out = nullptr;
+  int32_t* idx_in = nullptr;
+  int32_t* idx_out = nullptr;
+  float* sx = nullptr;
+  float* sy = nullptr;
+  float* sz = nullptr;
+  uint32_t* tkeys = nullptr;
+  int2* trange = nullptr;
+  uint32_t tmask = 0;
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
+};
+
+// bounding box of the finite points: per-block partial (min xyz, max xyz) -> out[6 * blocks]
+int bbox_blocks(int n);
+void launch_bbox(const float* X, const float* Y, const float* Z, int n, float* partial,
+                 hipStream_t s);
+
+size_t sort_tmp_bytes(int n, int key_bits);
+// sort by cell, fill the cell table; *n_occupied (device) = number of occupied cells
+hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, const GridDesc& G,
+                      GridBufs& B, uint32_t* n_occupied, hipStream_t s);
+// strided host-layout xyz records (uploaded raw) -> SoA
+void launch_deinterleave(const float* raw, int n, int64_t stride_floats, float* X, float* Y,
+                         float* Z, hipStream_t s);
+
+// radius normals: out[i] = (nx, ny, nz, curvature) for original point i
+void launch_normals_radius(const GridDesc& G, const GridBufs& B, int n, float r2, const float vp[3],
+                           float4* normals, hipStream_t s);
+// k nearest neighbours (k <= kMaxKnn) over a grid hierarchy, FLANN order (d2, index)
+constexpr int kMaxKnn = 64;
+constexpr int kMaxLevels = 12;
+struct KnnLevels {
+  int levels;
+  GridDesc G[kMaxLevels];
+  const float* sx[kMaxLevels];
+  const float* sy[kMaxLevels];
+  const float* sz[kMaxLevels];
+  const int32_t* idx[kMaxLevels];
+  const uint32_t* tkeys[kMaxLevels];
+  const int2* trange[kMaxLevels];
+  uint32_t tmask[kMaxLevels];
+};
+// one level: queries qlist[0..nq) (nullptr at level 0: every point, level-0 order); queries with
+// fewer than k neighbours inside the level's guaranteed radius are appended to next[]
+void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qlist, int nq,
+                        const float* X, const float* Y, const float* Z, int k, const float vp[3],
+                        float4* normals, int32_t* next, uint32_t* n_next, hipStream_t s);
+
+// ---- RegulateNormal, level-synchronous BFS ----
+// queue[]: point ids in PCL queue order; the current level is queue[fbase, fbase + nf).
+// claim: min over claiming queue positions (init ~0); cand/ncand: first-claimed nodes.
+void launch_bfs_claim(const int32_t* queue, int64_t fbase, int nf, const float* X, const float* Y,
+                      const float* Z, const GridDesc& G, const GridBufs& B, float r2,
+                      const uint8_t* processed, unsigned long long* claim, int32_t* cand,
+                      uint32_t* ncand, hipStream_t s);
+// settle the claimed nodes: sign flip against the parent, processed = 1, (parent pos | d2) keys
+void launch_bfs_settle(const int32_t* queue, const int32_t* cand, int nc, const float* X,
+                       const float* Y, const float* Z, uint8_t* processed,
+                       const unsigned long long* claim, float4* normals,
+                       unsigned long long* keys, hipStream_t s);
+size_t bfs_sort_tmp_bytes(int n);
+// order the next level: stable sort by id, then stable sort by (parent pos, d2) -> out_ids
+hipError_t bfs_order(void* tmp, size_t tmp_bytes, int32_t* cand, unsigned long long* keys,
+                     int32_t* ids_alt, unsigned long long* keys_alt, int32_t* out_ids, int nc,
+                     hipStream_t s);
+
+// pcl::Normal scatter helpers
+void launch_pack_normals(const float4* nrm, int n, float* out, int64_t stride_floats,
+                         int curv_offset, hipStream_t s);
+void launch_unpack_normals(const float* in, int n, int64_t stride_floats, float4* nrm,
+                           hipStream_t s);
+
+}  // namespace dlg

@@ -1,0 +1,308 @@
+// normals_host.cpp -- host driver of the normals path: dlg_estimate_normals and
+// dlg_regulate_normals (include/dialog_ransac.h; Dialog/PlaneDetect.h:515-665).
+//
+// Both calls take host buffers (the reference keeps source_cloud / source_normal on the host,
+// PlaneDetect.h:104-107): the strided records are uploaded raw and de-interleaved on the device,
+// a uniform grid is built (normals.hip), the kernels run, and the results are packed into the
+// caller's record layout on the device before one D2H copy.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "driver.hpp"
+#include "normals.hpp"
+
+namespace dlg {
+namespace {
+
+struct BBox {
+  float lo[3], hi[3];
+  bool any;
+};
+
+// points -> device SoA (nw.x/y/z) + bounding box of the finite points
+BBox upload_points(dlg_ctx* c, const dlg_points* pts) {
+  NormalsWork& w = c->nw;
+  const int n = (int)pts->n;
+  const size_t bytes = (size_t)pts->n * (size_t)pts->stride_bytes;
+  w.raw.ensure(bytes);
+  w.x.ensure(n); w.y.ensure(n); w.z.ensure(n);
+  HIPCHK(hipMemcpyAsync(w.raw.p, pts->xyz, bytes, hipMemcpyHostToDevice, c->stream));
+  launch_deinterleave(reinterpret_cast<const float*>(w.raw.p), n, pts->stride_bytes / 4, w.x.p,
+                      w.y.p, w.z.p, c->stream);
+  const int nb = bbox_blocks(n);
+  w.partial.ensure(6 * nb);
+  launch_bbox(w.x.p, w.y.p, w.z.p, n, w.partial.p, c->stream);
+  std::vector<float> part(6 * nb);
+  HIPCHK(hipMemcpyAsync(part.data(), w.partial.p, part.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  BBox b;
+  for (int k = 0; k < 3; ++k) {
+    b.lo[k] = INFINITY;
+    b.hi[k] = -INFINITY;
+  }
+  for (int i = 0; i < nb; ++i)
+    for (int k = 0; k < 3; ++k) {
+      b.lo[k] = std::fmin(b.lo[k], part[6 * i + k]);
+      b.hi[k] = std::fmax(b.hi[k], part[6 * i + 3 + k]);
+    }
+  b.any = b.lo[0] <= b.hi[0];
+  return b;
+}
+
+// grid with cell edge `cell` (grown until the key space fits 2^30 cells)
+GridDesc make_grid(const BBox& b, double cell) {
+  GridDesc G;
+  for (;;) {
+    double tot = 1.0;
+    for (int k = 0; k < 3; ++k) {
+      const double ext = b.any ? (double)b.hi[k] - (double)b.lo[k] : 0.0;
+      const double gk = std::floor(ext / cell) + 1.0;
+      G.g[k] = (int)std::min(gk, 1e9);
+      tot *= gk;
+    }
+    if (tot <= (double)(1u << 30)) break;
+    cell *= 1.25;
+  }
+  for (int k = 0; k < 3; ++k) G.lo[k] = b.any ? b.lo[k] : 0.0f;
+  // cell_of() computes floor((v - lo) * inv_cell) in float; shrinking inv_cell by 1e-3 keeps the
+  // effective cell edge >= `cell` despite the rounding of (v - lo) and of the product (<= 1024
+  // cells per axis at float precision: ~1e-4 cell), so points within r stay in adjacent cells
+  G.inv_cell = (float)((1.0 / cell) * (1.0 - 1e-3));
+  G.cell = (float)(cell * (1.0 - 1e-6));  // guaranteed coverage radius of the 27 cells
+  G.ncells = (uint32_t)((uint64_t)G.g[0] * G.g[1] * G.g[2]);
+  int bits = 1;
+  while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)G.ncells) ++bits;
+  G.key_bits = bits;
+  return G;
+}
+
+// builds grid level `lv` over nw.x/y/z; returns the number of occupied cells
+uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B) {
+  NormalsWork& w = c->nw;
+  GridLevelBufs& L = w.lv[lv];
+  w.keys_in.ensure(n); w.keys_out.ensure(n); w.idx_in.ensure(n);
+  L.idx.ensure(n); L.sx.ensure(n); L.sy.ensure(n); L.sz.ensure(n);
+  const uint64_t occ_max = std::min<uint64_t>((uint64_t)n, G.ncells);
+  uint32_t tcap = 1024;
+  while (tcap < 2 * occ_max && tcap < (1u << 31)) tcap <<= 1;
+  L.tkeys.ensure(tcap);
+  L.trange.ensure(tcap);
+  const size_t tmp = sort_tmp_bytes(n, G.key_bits);
+  w.sort_tmp.ensure(tmp);
+  w.counters.ensure(4);
+  w.h_cnt.ensure(4);
+  B->keys_in = w.keys_in.p; B->keys_out = w.keys_out.p;
+  B->idx_in = w.idx_in.p; B->idx_out = L.idx.p;
+  B->sx = L.sx.p; B->sy = L.sy.p; B->sz = L.sz.p;
+  B->tkeys = L.tkeys.p; B->trange = L.trange.p; B->tmask = tcap - 1;
+  B->sort_tmp = w.sort_tmp.p; B->sort_tmp_bytes = w.sort_tmp.cap;
+  HIPCHK(grid_build(w.x.p, w.y.p, w.z.p, n, G, *B, w.counters.p, c->stream));
+  HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  return w.h_cnt.p[0];
+}
+
+void check_points(const dlg_points* pts) {
+  if (!pts || pts->n < 0 || (pts->n > 0 && !pts->xyz))
+    throw DlgError(DLG_ERR_INVALID, "points: null or negative size");
+  if (pts->stride_bytes < 12 || pts->stride_bytes % 4)
+    throw DlgError(DLG_ERR_INVALID, "stride_bytes must be >= 12 and a multiple of 4");
+  if (pts->n > INT32_MAX / 2) throw DlgError(DLG_ERR_INVALID, "more than 2^30 points");
+}
+
+void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn, const float* vp_in,
+                      float* out, int64_t out_stride) {
+  check_points(pts);
+  if (!out) throw DlgError(DLG_ERR_INVALID, "normals_out is null");
+  if (out_stride != 16 && out_stride < 32) throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be 16 or >= 32");
+  if (out_stride % 4) throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be a multiple of 4");
+  if (k_nn < 0 || k_nn > kMaxKnn) throw DlgError(DLG_ERR_INVALID, "k_nn must be in 0..64");
+  if (k_nn == 0 && !(radius > 0.0f && std::isfinite(radius)))
+    throw DlgError(DLG_ERR_INVALID, "neither radius nor k set");  // PCL initCompute error
+  const int n = (int)pts->n;
+  if (n == 0) return;
+  const float vp[3] = {vp_in ? vp_in[0] : 0.0f, vp_in ? vp_in[1] : 0.0f, vp_in ? vp_in[2] : 0.0f};
+  NormalsWork& w = c->nw;
+  const BBox b = upload_points(c, pts);
+  w.nrm.ensure(n);
+  GridBufs B;
+  if (k_nn == 0) {
+    const GridDesc G = make_grid(b, (double)radius);
+    build_grid(c, n, G, 0, &B);
+    const float r2 = (float)((double)radius * (double)radius);  // KdTreeFLANN: radius * radius
+    launch_normals_radius(G, B, n, r2, vp, w.nrm.p, c->stream);
+  } else {
+    // level-0 cell: guess from the bounding volume, then one resize from the measured occupancy
+    // so an occupied cell holds ~k/2 points (surface-like clouds: occupancy ~ cell^2); levels
+    // above grow 2x until one has <= 2 cells per axis (normals.hip, k_normals_knn)
+    double ext[3], maxe = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      ext[k] = b.any ? (double)b.hi[k] - (double)b.lo[k] : 0.0;
+      maxe = std::max(maxe, ext[k]);
+    }
+    if (maxe <= 0.0) maxe = 1.0;
+    double vol = 1.0;
+    for (int k = 0; k < 3; ++k) vol *= std::max(ext[k], maxe * 1e-3);
+    double cell = std::cbrt(vol * k_nn / n);
+    GridDesc G = make_grid(b, cell);
+    const uint32_t occ = build_grid(c, n, G, 0, &B);
+    const double target = std::max(2.0, k_nn / 2.0);
+    const double avg = occ ? (double)n / occ : target;
+    if (avg > 2.0 * target || avg < 0.5 * target) {
+      cell *= std::sqrt(target / avg);
+      G = make_grid(b, cell);
+      build_grid(c, n, G, 0, &B);
+    }
+    KnnLevels L;
+    L.levels = 0;
+    const double top_cell = maxe * 0.75;  // floor(ext / cell) + 1 <= 2 on every axis
+    // 2x per level, more when the hierarchy would not fit kMaxLevels
+    const double fac = std::max(2.0, std::pow(top_cell / cell, 1.0 / (kMaxLevels - 1)));
+    for (int l = 0; l < kMaxLevels; ++l) {
+      const bool last = cell >= top_cell || l == kMaxLevels - 1;
+      if (last) cell = std::max(cell, top_cell);
+      GridBufs BL;
+      if (l == 0) {
+        BL = B;
+      } else {
+        G = make_grid(b, cell);
+        build_grid(c, n, G, l, &BL);
+      }
+      L.G[l] = G;
+      L.sx[l] = BL.sx; L.sy[l] = BL.sy; L.sz[l] = BL.sz; L.idx[l] = BL.idx_out;
+      L.tkeys[l] = BL.tkeys; L.trange[l] = BL.trange; L.tmask[l] = BL.tmask;
+      L.levels = l + 1;
+      if (last) break;
+      cell *= fac;
+    }
+    w.queue.ensure(n);
+    w.cand.ensure(n);
+    int32_t* qin = nullptr;
+    int32_t* qout = w.queue.p;
+    int nq = n;
+    for (int l = 0; l < L.levels && nq > 0; ++l) {
+      HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
+      launch_normals_knn(L, l, qin, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, qout,
+                         w.counters.p, c->stream);
+      if (l == L.levels - 1) break;
+      HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+      sync(c);
+      nq = (int)w.h_cnt.p[0];
+      qin = qout;
+      qout = qout == w.queue.p ? w.cand.p : w.queue.p;
+    }
+  }
+  HIPCHK(hipGetLastError());
+  const size_t obytes = (size_t)n * (size_t)out_stride;
+  w.out.ensure(obytes);
+  launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), out_stride / 4,
+                      out_stride == 16 ? 3 : 4, c->stream);
+  HIPCHK(hipMemcpyAsync(out, w.out.p, obytes, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+}
+
+int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64_t stride,
+                         int64_t seed, int seed_is_outward, float radius, uint8_t* processed_out) {
+  check_points(pts);
+  if (!nrm_io) throw DlgError(DLG_ERR_INVALID, "normals_inout is null");
+  if (stride < 12 || stride % 4) throw DlgError(DLG_ERR_INVALID, "stride_bytes must be >= 12 and a multiple of 4");
+  if (!(radius > 0.0f && std::isfinite(radius))) throw DlgError(DLG_ERR_INVALID, "radius must be > 0");
+  const int n = (int)pts->n;
+  if (seed < 0) {  // PlaneDetect.h:592-596: "invalid point index", return
+    if (processed_out) std::memset(processed_out, 0, (size_t)n);
+    return 0;
+  }
+  if (seed >= n) throw DlgError(DLG_ERR_INVALID, "seed index out of range");
+  NormalsWork& w = c->nw;
+  const BBox b = upload_points(c, pts);
+  const GridDesc G = make_grid(b, (double)radius);
+  GridBufs B;
+  build_grid(c, n, G, 0, &B);
+  const float r2 = (float)((double)radius * (double)radius);
+
+  const size_t nbytes = (size_t)n * (size_t)stride;
+  w.out.ensure(nbytes);
+  w.nrm.ensure(n);
+  HIPCHK(hipMemcpyAsync(w.out.p, nrm_io, nbytes, hipMemcpyHostToDevice, c->stream));
+  launch_unpack_normals(reinterpret_cast<const float*>(w.out.p), n, stride / 4, w.nrm.p, c->stream);
+  if (!seed_is_outward) {  // PlaneDetect.h:600-605
+    const float* s = nrm_io + seed * (stride / 4);
+    static thread_local float4 flipped;
+    flipped = make_float4(s[0] * -1.0f, s[1] * -1.0f, s[2] * -1.0f, 0.0f);
+    HIPCHK(hipMemcpyAsync(w.nrm.p + seed, &flipped, 16, hipMemcpyHostToDevice, c->stream));
+  }
+  w.processed.ensure(n);
+  w.claim.ensure(n);
+  w.queue.ensure(n);
+  w.cand.ensure(n);
+  w.ids_alt.ensure(n);
+  w.keys64.ensure(n);
+  w.keys_alt.ensure(n);
+  const size_t stmp = bfs_sort_tmp_bytes(n);
+  w.sort_tmp.ensure(stmp);
+  w.counters.ensure(4);
+  w.h_cnt.ensure(4);
+  HIPCHK(hipMemsetAsync(w.processed.p, 0, n, c->stream));
+  HIPCHK(hipMemsetAsync(w.claim.p, 0xff, (size_t)n * 8, c->stream));
+  HIPCHK(hipMemsetAsync(w.processed.p + seed, 1, 1, c->stream));
+  const int32_t seed32 = (int32_t)seed;
+  HIPCHK(hipMemcpyAsync(w.queue.p, &seed32, 4, hipMemcpyHostToDevice, c->stream));
+  sync(c);  // the two small H2D copies above read host stack/thread-local memory
+  int64_t fbase = 0, qt = 1;
+  int nf = 1;
+  while (nf > 0) {
+    HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
+    launch_bfs_claim(w.queue.p, fbase, nf, w.x.p, w.y.p, w.z.p, G, B, r2, w.processed.p,
+                     w.claim.p, w.cand.p, w.counters.p, c->stream);
+    HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    const int nc = (int)w.h_cnt.p[0];
+    if (nc == 0) break;
+    if (qt + nc > n) throw DlgError(DLG_ERR_INTERNAL, "BFS queue overflow");
+    launch_bfs_settle(w.queue.p, w.cand.p, nc, w.x.p, w.y.p, w.z.p, w.processed.p, w.claim.p,
+                      w.nrm.p, w.keys64.p, c->stream);
+    HIPCHK(bfs_order(w.sort_tmp.p, w.sort_tmp.cap, w.cand.p, w.keys64.p, w.ids_alt.p,
+                     w.keys_alt.p, w.queue.p + qt, nc, c->stream));
+    fbase = qt;
+    qt += nc;
+    nf = nc;
+  }
+  launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), stride / 4, -1, c->stream);
+  HIPCHK(hipMemcpyAsync(nrm_io, w.out.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+  if (processed_out)
+    HIPCHK(hipMemcpyAsync(processed_out, w.processed.p, n, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  return qt;
+}
+
+}  // namespace
+}  // namespace dlg
+
+extern "C" {
+
+dlg_status dlg_estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
+                                const float viewpoint[3], float* normals_out,
+                                int64_t out_stride_bytes) {
+  if (!c) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    estimate_normals(c, pts, radius, k_nn, viewpoint, normals_out, out_stride_bytes);
+  });
+}
+
+dlg_status dlg_regulate_normals(dlg_ctx* c, const dlg_points* pts, float* normals_inout,
+                                int64_t stride_bytes, int64_t seed_idx, int seed_is_outward,
+                                float radius, uint8_t* processed_out, int64_t* n_processed) {
+  if (!c) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    const int64_t k = regulate_normals(c, pts, normals_inout, stride_bytes, seed_idx,
+                                       seed_is_outward, radius, processed_out);
+    if (n_processed) *n_processed = k;
+  });
+}
+
+}  // extern "C"

@@ -155,6 +155,29 @@ dlg_status dlg_extract_planes(dlg_ctx* ctx, dlg_cloud* cloud, const dlg_sac_para
                               int64_t* offsets_out, int32_t* inliers_out, int64_t cap,
                               int* n_planes, dlg_extract_stats* stats);
 
+/* ---- normals (Dialog/PlaneDetect.h:515-665) -------------------------------------------------- */
+/* pcl::NormalEstimation(OMP)::compute on every point of pts (estimateNormal(),
+ * PlaneDetect.h:515-545): neighbours = radius search (k_nn == 0, radius > 0; PCL's radius
+ * r_for_estimate_normal, config.txt:4) or the k_nn nearest (k_nn in 1..64; PCLViewer.cpp:507-522
+ * uses 20), as KdTreeFLANN returns them; normal = eigenvector of the smallest eigenvalue of the
+ * neighbourhood covariance, curvature = lambda0 / (lambda0 + lambda1 + lambda2), flipped towards
+ * viewpoint (NULL = origin).  < 3 neighbours or a non-finite point -> NaN normal and curvature.
+ * normals_out: n records of out_stride_bytes: 16 = (nx, ny, nz, curvature); >= 32 = pcl::Normal
+ * (normal_x/y/z at bytes 0-11, curvature at byte 16, other fields zeroed). */
+dlg_status dlg_estimate_normals(dlg_ctx* ctx, const dlg_points* pts, float radius, int k_nn,
+                                const float viewpoint[3], float* normals_out,
+                                int64_t out_stride_bytes);
+/* regulateNormal() first-round branch (PlaneDetect.h:586-646): flip the seed normal unless
+ * seed_is_outward (is_norm_direction_valid), then BFS over radius-`radius` neighbourhoods
+ * (r_for_regulate_normal, config.txt:9) in PCL's queue order, flipping each newly reached normal
+ * whose float dot with the normal of the point that reached it is < 0.  normals_inout: n records
+ * of stride_bytes (>= 12, multiple of 4); only normal_x/y/z are written.  processed_out
+ * (nullable): n bytes, 1 = reached (isProcessed).  seed_idx < 0 is PCL's "invalid point index":
+ * DLG_OK, nothing changed, *n_processed = 0. */
+dlg_status dlg_regulate_normals(dlg_ctx* ctx, const dlg_points* pts, float* normals_inout,
+                                int64_t stride_bytes, int64_t seed_idx, int seed_is_outward,
+                                float radius, uint8_t* processed_out, int64_t* n_processed);
+
 /* ---- profiling ------------------------------------------------------------------------------ */
 /* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);

@@ -66,6 +66,7 @@ def lib():
         L.orc_eigen33.argtypes = [fp, fp, fp]
         L.orc_refit_double.argtypes = [fp, C.c_int64, i32p, C.c_int64, fp, fp]
         L.orc_estimate_normals.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, fp, fp]
+        L.orc_estimate_normals_knn.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, fp, fp]
         L.orc_regulate_normals.argtypes = [fp, C.c_int64, C.c_int64, fp, C.c_int64, C.c_int,
                                            C.c_float, C.POINTER(C.c_uint8)]
         L.orc_regulate_normals.restype = C.c_int64
@@ -196,6 +197,14 @@ def estimate_normals(points, radius, viewpoint=(0.0, 0.0, 0.0)):
     out = np.zeros((p.shape[0], 4), np.float32)
     vp = np.array(viewpoint, np.float32)
     lib().orc_estimate_normals(_f(p), p.shape[0], stride, float(radius), _f(vp), _f(out))
+    return out
+
+
+def estimate_normals_knn(points, k, viewpoint=(0.0, 0.0, 0.0)):
+    p, stride = _xyz(points)
+    out = np.zeros((p.shape[0], 4), np.float32)
+    vp = np.array(viewpoint, np.float32)
+    lib().orc_estimate_normals_knn(_f(p), p.shape[0], stride, int(k), _f(vp), _f(out))
     return out
 
 

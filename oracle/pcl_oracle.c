@@ -585,6 +585,45 @@ void orc_estimate_normals(const float* xyz, int64_t n, int64_t stride, float rad
   orc_grid_free(&G);
 }
 
+/* k-nearest-neighbour variant: NormalEstimation with setKSearch(k) (PCLViewer.cpp:507-522,
+ * TriangularMeshing.h:28-35, k = 20).  Brute force over all points: neighbours = the k smallest
+ * (dist2, index) pairs, FLANN's sorted kNN result (the query itself has dist2 0).  O(n^2): for
+ * test-sized clouds only. */
+void orc_estimate_normals_knn(const float* xyz, int64_t n, int64_t stride, int k_nn,
+                              const float vp[3], float* out) {
+  orc_nb* all = (orc_nb*)malloc((size_t)(n > 0 ? n : 1) * sizeof(orc_nb));
+  int32_t* ids = (int32_t*)malloc((size_t)(k_nn > 0 ? k_nn : 1) * sizeof(int32_t));
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + i * stride;
+    float* o = out + 4 * i;
+    int64_t m = 0;
+    for (int64_t j = 0; j < n; ++j) {
+      const float* q = xyz + j * stride;
+      float ex = p[0] - q[0], ey = p[1] - q[1], ez = p[2] - q[2];
+      float d = ((0.0f + ex * ex) + ey * ey) + ez * ez;
+      if (d != d) continue;
+      all[m].d = d; all[m].j = (int32_t)j; ++m;
+    }
+    qsort(all, (size_t)m, sizeof(orc_nb), orc_nb_cmp);
+    int64_t k = m < k_nn ? m : k_nn;
+    if (k < 3 || !(p[0] == p[0] && p[1] == p[1] && p[2] == p[2])) {
+      o[0] = o[1] = o[2] = o[3] = NAN;
+      continue;
+    }
+    for (int64_t t = 0; t < k; ++t) ids[t] = all[t].j;
+    float cov[9], cen[4], ev, v[3];
+    orc_mean_cov(xyz, stride, ids, k, cov, cen);
+    orc_eigen33(cov, &ev, v);
+    float eig_sum = cov[0] + cov[4] + cov[8];
+    float curv = eig_sum != 0.0f ? fabsf(ev / eig_sum) : 0.0f;
+    float vx = vp[0] - p[0], vy = vp[1] - p[1], vz = vp[2] - p[2];
+    float cos_theta = vx * v[0] + vy * v[1] + vz * v[2];
+    if (cos_theta < 0.0f) { v[0] *= -1.0f; v[1] *= -1.0f; v[2] *= -1.0f; }
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = curv;
+  }
+  free(all); free(ids);
+}
+
 /* Dialog/PlaneDetect.h:547-665 (first-round branch; the second-round 1-NN branch at :553-584
  * is not part of this oracle). normals: 4 floats per point. Returns #processed points. */
 int64_t orc_regulate_normals(const float* xyz, int64_t n, int64_t stride, float* normals,

@@ -112,6 +112,15 @@ def main():
     np.savez_compressed(os.path.join(HERE, "synth_c3_small.npz"), points=p3, threshold=0.02,
                         max_iterations=1023, probability=1.0, min_inliers=200, max_planes=20,
                         coeffs=e["coeffs"], offsets=e["offsets"], inliers=e["inliers"])
+    # normals (SURVEY.md §8(c) fixture 4): radius + k = 20 on a small 3-plane cloud, and the
+    # RegulateNormal BFS from seed 0 with the seed flipped (is_norm_direction_valid = 0)
+    pn, _, _ = plane_cloud(2048, 3, outlier_frac=0.05, seed=SEED_BASE + 5, patch=1.0)
+    rn = O.estimate_normals(pn, 0.1)
+    kn = O.estimate_normals_knn(pn, 20)
+    reg, proc, _ = O.regulate_normals(pn, rn, 0, False, 0.08)
+    np.savez_compressed(os.path.join(HERE, "normals_small.npz"), points=pn, radius=0.1, k=20,
+                        radius_normals=rn, knn_normals=kn, seed_idx=0, r_regulate=0.08,
+                        regulated=reg, processed=proc)
     print("golden fixtures written to", HERE)
 
 
