@@ -26,6 +26,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cfloat>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(kBS) void k_cell_keys(const float* __restrict__ X,
   idx[i] = i;
 }
 
-// sorted keys -> cell table + coordinates in sorted order
+// sorted keys -> cell table (begin) + coordinates in sorted order
 __global__ __launch_bounds__(kBS) void k_cells_build(
     const uint32_t* __restrict__ skeys, const int32_t* __restrict__ sidx, int n, uint32_t ncells,
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
@@ -126,17 +127,31 @@ __global__ __launch_bounds__(kBS) void k_cells_build(
   sy[t] = Y[i];
   sz[t] = Z[i];
   const uint32_t k = skeys[t];
-  if (k == ncells || (t > 0 && skeys[t - 1] == k)) return;
-  int e = t + 1;
-  while (e < n && skeys[e] == k) ++e;  // run length of one cell
+  const bool first = k != ncells && (t == 0 || skeys[t - 1] != k);
+  // occupied-cell count: one atomic per wavefront, not per cell (a single hot address)
+  const unsigned long long b = __ballot(first);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_occupied, (uint32_t)__popcll(b));
+  if (!first) return;
   uint32_t h = hash_key(k) & tmask;
   while (true) {
     const uint32_t prev = atomicCAS(&tkeys[h], kEmpty, k);
     if (prev == kEmpty) break;
     h = (h + 1) & tmask;
   }
-  trange[h] = make_int2(t, e);
-  atomicAdd(n_occupied, 1u);
+  trange[h].x = t;
+}
+
+// the last point of each cell run writes the run's end (separate launch: the begin must exist)
+__global__ __launch_bounds__(kBS) void k_cells_end(const uint32_t* __restrict__ skeys, int n,
+                                                   uint32_t ncells, const uint32_t* __restrict__ tkeys,
+                                                   int2* __restrict__ trange, uint32_t tmask) {
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t k = skeys[t];
+  if (k == ncells || (t + 1 < n && skeys[t + 1] == k)) return;
+  uint32_t h = hash_key(k) & tmask;
+  while (tkeys[h] != k) h = (h + 1) & tmask;
+  trange[h].y = t + 1;
 }
 
 __device__ __forceinline__ int2 cell_range(const uint32_t* __restrict__ tkeys,
@@ -292,6 +307,7 @@ __global__ __launch_bounds__(kBS) void k_normals_radius(
 // the top level the 27 cells are the whole cloud and every candidate counts.  One launch per
 // level over the queries still open (compacted), so the few sparse outliers that climb do not
 // hold back the wavefronts of the surface points, which finish at level 0.
+template <int KP>
 __global__ __launch_bounds__(kBS) void k_normals_knn(
     KnnLevels L, int l, const int32_t* __restrict__ qlist, int nq, const float* __restrict__ X,
     const float* __restrict__ Y, const float* __restrict__ Z, int K, float vpx, float vpy,
@@ -317,9 +333,14 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     const float* __restrict__ sy = L.sy[l];
     const float* __restrict__ sz = L.sz[l];
     const int32_t* __restrict__ sidx = L.idx[l];
-    float bd[kMaxKnn];
-    int bi[kMaxKnn];
-    int cnt = 0;
+    // the KP smallest (d2, index) so far, ascending, in registers (fully unrolled network)
+    float bd[KP];
+    int bi[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) { bd[j] = INFINITY; bi[j] = INT_MAX; }
+    float kd = INFINITY;  // current K-th entry: the admission bound
+    int ki = INT_MAX;
+    int cnt = 0;          // candidates inside the level's guaranteed radius
     const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
     const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
     const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
@@ -330,87 +351,139 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
           for (int u = rg.x; u < rg.y; ++u) {
             const float d2 = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
             if (!(d2 < lim)) continue;
-            const int iu = sidx[u];
-            if (cnt == K) {
-              const float w = bd[K - 1];
-              if (d2 > w || (d2 == w && iu > bi[K - 1])) continue;
+            ++cnt;
+            if (d2 > kd) continue;
+            int ci = sidx[u];
+            if (d2 == kd && ci > ki) continue;
+            float cd = d2;
+#pragma unroll
+            for (int j = 0; j < KP; ++j) {
+              const bool lt = cd < bd[j] || (cd == bd[j] && ci < bi[j]);
+              const float od = bd[j];
+              const int oi = bi[j];
+              bd[j] = lt ? cd : od;
+              bi[j] = lt ? ci : oi;
+              cd = lt ? od : cd;
+              ci = lt ? oi : ci;
             }
-            int p = cnt < K ? cnt++ : K - 1;
-            while (p > 0 && (bd[p - 1] > d2 || (bd[p - 1] == d2 && bi[p - 1] > iu))) {
-              bd[p] = bd[p - 1];
-              bi[p] = bi[p - 1];
-              --p;
-            }
-            bd[p] = d2;
-            bi[p] = iu;
+#pragma unroll
+            for (int j = 0; j < KP; ++j)
+              if (j == K - 1) { kd = bd[j]; ki = bi[j]; }
           }
         }
     if (cnt < K && !top) {
       next[atomicAdd(n_next, 1u)] = qi;
       return;
     }
-    for (int j = 0; j < cnt; ++j) {
-      const int i = bi[j];
-      M.add(X[i], Y[i], Z[i], qx, qy, qz);
-    }
+    const int m = cnt < K ? cnt : K;
+#pragma unroll
+    for (int j = 0; j < KP; ++j)
+      if (j < m) {
+        const int i = bi[j];
+        M.add(X[i], Y[i], Z[i], qx, qy, qz);
+      }
   }
   normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
 }
 
 // ---------------------------------------------------------------------------------------------
 // RegulateNormal BFS, one level per (claim, settle, order)
-__global__ __launch_bounds__(kBS) void k_bfs_claim(
-    const int32_t* __restrict__ queue, int64_t fbase, int nf, const float* __restrict__ X,
-    const float* __restrict__ Y, const float* __restrict__ Z, const float* __restrict__ sx,
-    const float* __restrict__ sy, const float* __restrict__ sz, const int32_t* __restrict__ sidx,
-    GridDesc G, const uint32_t* __restrict__ tkeys, const int2* __restrict__ trange,
-    uint32_t tmask, float r2, const uint8_t* __restrict__ processed,
-    unsigned long long* __restrict__ claim, int32_t* __restrict__ cand,
-    uint32_t* __restrict__ ncand) {
-  const int f = blockIdx.x * kBS + threadIdx.x;
-  if (f >= nf) return;
-  const unsigned long long mypos = (unsigned long long)(fbase + f);
-  const int32_t cur = queue[mypos];
-  const float qx = X[cur], qy = Y[cur], qz = Z[cur];
-  if (!finite3(qx, qy, qz)) return;
-  const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
-  const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
-  const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
-  for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
-    for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
-      for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
-        const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
-        for (int u = rg.x; u < rg.y; ++u) {
-          const int32_t j = sidx[u];
-          if (processed[j]) continue;
-          if (flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2) {
-            if (atomicMin(&claim[j], mypos) == ~0ull) cand[atomicAdd(ncand, 1u)] = j;
-          }
-        }
-      }
+// The BFS state lives in the grid's sorted order (position u of point sidx[u]): processed[],
+// claim[] and the normals are read per cell run, i.e. coalesced, instead of at random point ids.
+// The queue holds point ids (PCL's order keys use them); pos_of[] maps id -> u.
+__global__ __launch_bounds__(kBS) void k_bfs_prepare(const int32_t* __restrict__ sidx, int n,
+                                                     const float4* __restrict__ nrm,
+                                                     float4* __restrict__ nrm_s,
+                                                     int32_t* __restrict__ pos_of) {
+  const int u = blockIdx.x * kBS + threadIdx.x;
+  if (u >= n) return;
+  const int j = sidx[u];
+  pos_of[j] = u;
+  nrm_s[u] = nrm[j];
 }
 
+// seed (PlaneDetect.h:600-607): flip unless outward, mark processed, queue[0] = seed
+__global__ void k_bfs_seed(int32_t seed, int flip, const int32_t* __restrict__ pos_of,
+                           float4* __restrict__ nrm_s, uint8_t* __restrict__ processed_s,
+                           int32_t* __restrict__ queue) {
+  const int u = pos_of[seed];
+  if (flip) {
+    float4 v = nrm_s[u];
+    v.x *= -1.0f; v.y *= -1.0f; v.z *= -1.0f;
+    nrm_s[u] = v;
+  }
+  processed_s[u] = 1;
+  queue[0] = seed;
+}
+
+// one thread per (frontier node, one of its 27 cells): short dependent chains, 27x the threads
+__global__ __launch_bounds__(kBS) void k_bfs_claim(
+    const int32_t* __restrict__ queue, int64_t fbase, int nf, const int32_t* __restrict__ pos_of,
+    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
+    GridDesc G, const uint32_t* __restrict__ tkeys, const int2* __restrict__ trange,
+    uint32_t tmask, float r2, const uint8_t* __restrict__ processed_s,
+    uint32_t* __restrict__ claim_s, int32_t* __restrict__ cand, uint32_t* __restrict__ ncand) {
+  const int64_t t = (int64_t)blockIdx.x * kBS + threadIdx.x;
+  if (t >= (int64_t)nf * 27) return;
+  const int f = (int)(t / 27), c = (int)(t % 27);
+  const uint32_t mypos = (uint32_t)(fbase + f);
+  const int cu = pos_of[queue[mypos]];
+  const float qx = sx[cu], qy = sy[cu], qz = sz[cu];
+  if (!finite3(qx, qy, qz)) return;
+  const int x = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]) + c % 3 - 1;
+  const int y = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]) + (c / 3) % 3 - 1;
+  const int z = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]) + c / 9 - 1;
+  if (x < 0 || y < 0 || z < 0 || x >= G.g[0] || y >= G.g[1] || z >= G.g[2]) return;
+  const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+  for (int u = rg.x; u < rg.y; ++u) {
+    if (processed_s[u]) continue;
+    if (flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2) {
+      // claims only decrease: a plain read filters most of the contended atomics
+      if (claim_s[u] <= mypos) continue;
+      if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) cand[atomicAdd(ncand, 1u)] = u;
+    }
+  }
+}
+
+// settle the newly reached nodes: flip against the claiming parent (PlaneDetect.h:624-636),
+// processed = 1, order key (parent queue position, d2 from the parent) + point id
 __global__ __launch_bounds__(kBS) void k_bfs_settle(
     const int32_t* __restrict__ queue, const int32_t* __restrict__ cand, int nc,
-    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    uint8_t* __restrict__ processed, const unsigned long long* __restrict__ claim,
-    float4* __restrict__ normals, unsigned long long* __restrict__ keys) {
+    const int32_t* __restrict__ pos_of, const int32_t* __restrict__ sidx,
+    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
+    uint8_t* __restrict__ processed_s, const uint32_t* __restrict__ claim_s,
+    float4* __restrict__ nrm_s, unsigned long long* __restrict__ keys,
+    int32_t* __restrict__ ids) {
   const int t = blockIdx.x * kBS + threadIdx.x;
   if (t >= nc) return;
-  const int32_t j = cand[t];
-  const unsigned long long ppos = claim[j];
-  const int32_t parent = queue[ppos];
-  const float4 pn = normals[parent];
-  float4 nn = normals[j];
+  const int u = cand[t];
+  const unsigned long long ppos = claim_s[u];
+  const int pu = pos_of[queue[ppos]];
+  const float4 pn = nrm_s[pu];
+  float4 nn = nrm_s[u];
   const float dp = pn.x * nn.x + pn.y * nn.y + pn.z * nn.z;
   if (dp < 0.0f) {
     nn.x *= -1.0f; nn.y *= -1.0f; nn.z *= -1.0f;
-    normals[j] = nn;
+    nrm_s[u] = nn;
   }
-  processed[j] = 1;
+  processed_s[u] = 1;
   // the parent's neighbour list is sorted by the d2 FLANN computes for query = parent
-  const float d2 = flann_d2(X[parent], Y[parent], Z[parent], X[j], Y[j], Z[j]);
+  const float d2 = flann_d2(sx[pu], sy[pu], sz[pu], sx[u], sy[u], sz[u]);
   keys[t] = (ppos << 32) | (unsigned long long)__float_as_uint(d2);
+  ids[t] = sidx[u];
+}
+
+// sorted order -> point order
+__global__ __launch_bounds__(kBS) void k_bfs_finish(const int32_t* __restrict__ sidx, int n,
+                                                    const float4* __restrict__ nrm_s,
+                                                    const uint8_t* __restrict__ processed_s,
+                                                    float4* __restrict__ nrm,
+                                                    uint8_t* __restrict__ processed) {
+  const int u = blockIdx.x * kBS + threadIdx.x;
+  if (u >= n) return;
+  const int j = sidx[u];
+  nrm[j] = nrm_s[u];
+  processed[j] = processed_s[u];
 }
 
 __global__ __launch_bounds__(kBS) void k_pack_normals(const float4* __restrict__ nrm, int n,
@@ -480,6 +553,8 @@ hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, con
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_cells_build, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.keys_out, B.idx_out, n,
                      G.ncells, X, Y, Z, B.tkeys, B.trange, B.tmask, B.sx, B.sy, B.sz, n_occupied);
+  hipLaunchKernelGGL(k_cells_end, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.keys_out, n, G.ncells,
+                     B.tkeys, B.trange, B.tmask);
   return hipGetLastError();
 }
 
@@ -495,27 +570,59 @@ void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qlist, int
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
                         float4* normals, int32_t* next, uint32_t* n_next, hipStream_t s) {
   if (nq <= 0) return;
-  hipLaunchKernelGGL(k_normals_knn, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, L, level, qlist, nq, X, Y,
-                     Z, k, vp[0], vp[1], vp[2], normals, next, n_next);
+  const dim3 g(cdiv(nq, kBS)), b(kBS);
+  if (k <= 8)
+    hipLaunchKernelGGL(k_normals_knn<8>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, next, n_next);
+  else if (k <= 16)
+    hipLaunchKernelGGL(k_normals_knn<16>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, next, n_next);
+  else if (k <= 24)
+    hipLaunchKernelGGL(k_normals_knn<24>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, next, n_next);
+  else if (k <= 32)
+    hipLaunchKernelGGL(k_normals_knn<32>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, next, n_next);
+  else
+    hipLaunchKernelGGL(k_normals_knn<64>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, next, n_next);
 }
 
-void launch_bfs_claim(const int32_t* queue, int64_t fbase, int nf, const float* X, const float* Y,
-                      const float* Z, const GridDesc& G, const GridBufs& B, float r2,
-                      const uint8_t* processed, unsigned long long* claim, int32_t* cand,
-                      uint32_t* ncand, hipStream_t s) {
+void launch_bfs_prepare(const GridBufs& B, int n, const float4* nrm, float4* nrm_s, int32_t* pos_of,
+                        hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_bfs_prepare, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.idx_out, n, nrm, nrm_s,
+                     pos_of);
+}
+
+void launch_bfs_seed(int32_t seed, int flip, const int32_t* pos_of, float4* nrm_s,
+                     uint8_t* processed_s, int32_t* queue, hipStream_t s) {
+  hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(1), 0, s, seed, flip, pos_of, nrm_s, processed_s,
+                     queue);
+}
+
+void launch_bfs_claim(const int32_t* queue, int64_t fbase, int nf, const int32_t* pos_of,
+                      const GridDesc& G, const GridBufs& B, float r2, const uint8_t* processed_s,
+                      uint32_t* claim_s, int32_t* cand, uint32_t* ncand, hipStream_t s) {
   if (nf <= 0) return;
-  hipLaunchKernelGGL(k_bfs_claim, dim3(cdiv(nf, kBS)), dim3(kBS), 0, s, queue, fbase, nf, X, Y, Z,
-                     B.sx, B.sy, B.sz, B.idx_out, G, B.tkeys, B.trange, B.tmask, r2, processed,
-                     claim, cand, ncand);
+  hipLaunchKernelGGL(k_bfs_claim, dim3(cdiv((int64_t)nf * 27, kBS)), dim3(kBS), 0, s, queue, fbase,
+                     nf, pos_of, B.sx, B.sy, B.sz, G, B.tkeys, B.trange, B.tmask, r2, processed_s,
+                     claim_s, cand, ncand);
 }
 
-void launch_bfs_settle(const int32_t* queue, const int32_t* cand, int nc, const float* X,
-                       const float* Y, const float* Z, uint8_t* processed,
-                       const unsigned long long* claim, float4* normals,
-                       unsigned long long* keys, hipStream_t s) {
+void launch_bfs_settle(const int32_t* queue, const int32_t* cand, int nc, const int32_t* pos_of,
+                       const GridBufs& B, uint8_t* processed_s, const uint32_t* claim_s,
+                       float4* nrm_s, unsigned long long* keys, int32_t* ids, hipStream_t s) {
   if (nc <= 0) return;
-  hipLaunchKernelGGL(k_bfs_settle, dim3(cdiv(nc, kBS)), dim3(kBS), 0, s, queue, cand, nc, X, Y, Z,
-                     processed, claim, normals, keys);
+  hipLaunchKernelGGL(k_bfs_settle, dim3(cdiv(nc, kBS)), dim3(kBS), 0, s, queue, cand, nc, pos_of,
+                     B.idx_out, B.sx, B.sy, B.sz, processed_s, claim_s, nrm_s, keys, ids);
+}
+
+void launch_bfs_finish(const GridBufs& B, int n, const float4* nrm_s, const uint8_t* processed_s,
+                       float4* nrm, uint8_t* processed, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_bfs_finish, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.idx_out, n, nrm_s,
+                     processed_s, nrm, processed);
 }
 
 size_t bfs_sort_tmp_bytes(int n) {
@@ -529,13 +636,13 @@ size_t bfs_sort_tmp_bytes(int n) {
   return a > b ? a : b;
 }
 
-hipError_t bfs_order(void* tmp, size_t tmp_bytes, int32_t* cand, unsigned long long* keys,
+hipError_t bfs_order(void* tmp, size_t tmp_bytes, int32_t* ids, unsigned long long* keys,
                      int32_t* ids_alt, unsigned long long* keys_alt, int32_t* out_ids, int nc,
                      hipStream_t s) {
   if (nc <= 0) return hipSuccess;
   size_t t = tmp_bytes;
   // ids ascending (the atomic append order is arbitrary), then stable by (parent pos, d2)
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, t, cand, ids_alt, keys, keys_alt, nc, 0,
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, t, ids, ids_alt, keys, keys_alt, nc, 0,
                                                     32, s);
   if (e != hipSuccess) return e;
   t = tmp_bytes;

@@ -230,16 +230,14 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   w.nrm.ensure(n);
   HIPCHK(hipMemcpyAsync(w.out.p, nrm_io, nbytes, hipMemcpyHostToDevice, c->stream));
   launch_unpack_normals(reinterpret_cast<const float*>(w.out.p), n, stride / 4, w.nrm.p, c->stream);
-  if (!seed_is_outward) {  // PlaneDetect.h:600-605
-    const float* s = nrm_io + seed * (stride / 4);
-    static thread_local float4 flipped;
-    flipped = make_float4(s[0] * -1.0f, s[1] * -1.0f, s[2] * -1.0f, 0.0f);
-    HIPCHK(hipMemcpyAsync(w.nrm.p + seed, &flipped, 16, hipMemcpyHostToDevice, c->stream));
-  }
+  w.nrm_s.ensure(n);
+  w.pos_of.ensure(n);
   w.processed.ensure(n);
+  w.processed_s.ensure(n);
   w.claim.ensure(n);
   w.queue.ensure(n);
   w.cand.ensure(n);
+  w.ids.ensure(n);
   w.ids_alt.ensure(n);
   w.keys64.ensure(n);
   w.keys_alt.ensure(n);
@@ -247,31 +245,32 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   w.sort_tmp.ensure(stmp);
   w.counters.ensure(4);
   w.h_cnt.ensure(4);
-  HIPCHK(hipMemsetAsync(w.processed.p, 0, n, c->stream));
-  HIPCHK(hipMemsetAsync(w.claim.p, 0xff, (size_t)n * 8, c->stream));
-  HIPCHK(hipMemsetAsync(w.processed.p + seed, 1, 1, c->stream));
-  const int32_t seed32 = (int32_t)seed;
-  HIPCHK(hipMemcpyAsync(w.queue.p, &seed32, 4, hipMemcpyHostToDevice, c->stream));
-  sync(c);  // the two small H2D copies above read host stack/thread-local memory
+  HIPCHK(hipMemsetAsync(w.processed_s.p, 0, n, c->stream));
+  HIPCHK(hipMemsetAsync(w.claim.p, 0xff, (size_t)n * 4, c->stream));
+  launch_bfs_prepare(B, n, w.nrm.p, w.nrm_s.p, w.pos_of.p, c->stream);
+  // PlaneDetect.h:600-607: seed flipped unless its direction was confirmed outward
+  launch_bfs_seed((int32_t)seed, seed_is_outward ? 0 : 1, w.pos_of.p, w.nrm_s.p, w.processed_s.p,
+                  w.queue.p, c->stream);
   int64_t fbase = 0, qt = 1;
   int nf = 1;
   while (nf > 0) {
     HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
-    launch_bfs_claim(w.queue.p, fbase, nf, w.x.p, w.y.p, w.z.p, G, B, r2, w.processed.p,
-                     w.claim.p, w.cand.p, w.counters.p, c->stream);
+    launch_bfs_claim(w.queue.p, fbase, nf, w.pos_of.p, G, B, r2, w.processed_s.p, w.claim.p,
+                     w.cand.p, w.counters.p, c->stream);
     HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
     sync(c);
     const int nc = (int)w.h_cnt.p[0];
     if (nc == 0) break;
     if (qt + nc > n) throw DlgError(DLG_ERR_INTERNAL, "BFS queue overflow");
-    launch_bfs_settle(w.queue.p, w.cand.p, nc, w.x.p, w.y.p, w.z.p, w.processed.p, w.claim.p,
-                      w.nrm.p, w.keys64.p, c->stream);
-    HIPCHK(bfs_order(w.sort_tmp.p, w.sort_tmp.cap, w.cand.p, w.keys64.p, w.ids_alt.p,
+    launch_bfs_settle(w.queue.p, w.cand.p, nc, w.pos_of.p, B, w.processed_s.p, w.claim.p,
+                      w.nrm_s.p, w.keys64.p, w.ids.p, c->stream);
+    HIPCHK(bfs_order(w.sort_tmp.p, w.sort_tmp.cap, w.ids.p, w.keys64.p, w.ids_alt.p,
                      w.keys_alt.p, w.queue.p + qt, nc, c->stream));
     fbase = qt;
     qt += nc;
     nf = nc;
   }
+  launch_bfs_finish(B, n, w.nrm_s.p, w.processed_s.p, w.nrm.p, w.processed.p, c->stream);
   launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), stride / 4, -1, c->stream);
   HIPCHK(hipMemcpyAsync(nrm_io, w.out.p, nbytes, hipMemcpyDeviceToHost, c->stream));
   if (processed_out)
