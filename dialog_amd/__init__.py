@@ -6,11 +6,12 @@ PCL's SACSegmentation interface, the synthetic-cloud generator and PCD I/O.  The
 fallback: without the library or a gfx950 device every compute call raises.
 """
 from .sac import (SAC_RANSAC, SACMODEL_NORMAL_PLANE, SACMODEL_PLANE, Cloud, Context,  # noqa: F401
-                  DialogError, SACSegmentation, extract_planes, make_params, segment_cloud)
+                  DialogError, SACSegmentation, SACSegmentationFromNormals, extract_planes,
+                  make_params, segment_cloud)
 from .normals import NormalEstimation, estimate_normals, regulate_normals  # noqa: F401
 from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, LIB_PATH  # noqa: F401
 
 __all__ = ["Context", "Cloud", "SACSegmentation", "extract_planes", "segment_cloud", "make_params",
            "SACMODEL_PLANE", "SACMODEL_NORMAL_PLANE", "SAC_RANSAC", "DLG_REFIT_PCL",
            "DLG_REFIT_FAST", "DialogError", "LIB_PATH", "NormalEstimation", "estimate_normals",
-           "regulate_normals"]
+           "regulate_normals", "SACSegmentationFromNormals"]

@@ -192,8 +192,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                     dlg_sac_stats* st, dlg_extract_stats* xs) {
   SegOut out;
   std::memset(st, 0, sizeof(*st));
-  if (prm.model != DLG_SACMODEL_PLANE)
-    throw DlgError(DLG_ERR_INVALID, "only SACMODEL_PLANE is implemented");
+  const bool np = prm.model == DLG_SACMODEL_NORMAL_PLANE;
+  if (prm.model != DLG_SACMODEL_PLANE && !np)
+    throw DlgError(DLG_ERR_INVALID, "model must be SACMODEL_PLANE or SACMODEL_NORMAL_PLANE");
+  if (np && !cl->has_normals)  // PCL: "No input dataset containing normals was given!"
+    throw DlgError(DLG_ERR_INVALID, "SACMODEL_NORMAL_PLANE needs normals (dlg_cloud_set_normals)");
   if (!(prm.threshold == prm.threshold)) throw DlgError(DLG_ERR_INVALID, "threshold is NaN");
   const int cap_h = prm.hypotheses_per_launch > 0
                         ? std::min(prm.hypotheses_per_launch, kMaxHypPerLaunch)
@@ -209,6 +212,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
 
   const PointsView src = cl->view();
   const float cthr = thr_ceil(prm.threshold);
+  ModelTest mt;
+  mt.cthr = cthr;
+  mt.normal_plane = np ? 1 : 0;
+  mt.thr = prm.threshold;
+  mt.lambda = prm.normal_distance_weight;
   Mt19937 rng(prm.seed);
   Overlay ov;
   ov.reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h) + 16);
@@ -263,7 +271,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                       c->res.p + Dp, c->stream);
     HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    launch_score(src, c->hyps.p, D, cthr, c->res.p, kScoreDefault, c->num_cus, c->stream);
+    if (np)
+      launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
+    else
+      launch_score(src, c->hyps.p, D, cthr, c->res.p, kScoreDefault, c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
@@ -346,7 +357,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     c->moments.ensure(kMomentK);
     c->h_mom.ensure(kMomentK);
     const double shift[3] = {best_s[0].x, best_s[0].y, best_s[0].z};
-    launch_moments(src, make_float4(bc[0], bc[1], bc[2], bc[3]), cthr,
+    launch_moments(src, make_float4(bc[0], bc[1], bc[2], bc[3]), mt,
                    make_double3(shift[0], shift[1], shift[2]), c->partials.p, nb, c->moments.p,
                    c->stream);
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
@@ -356,7 +367,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   } else {
     // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
     c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
-    launch_select(src, make_float4(bc[0], bc[1], bc[2], bc[3]), cthr, c->tile_in.p, c->tile_off_in.p,
+    launch_select(src, make_float4(bc[0], bc[1], bc[2], bc[3]), mt, c->tile_in.p, c->tile_off_in.p,
                   c->tile_off_out.p, c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
     HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
     sync(c);
@@ -373,9 +384,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   if (compact) {
     SoA& sp = cl->buf[cl->spare()];
     sp.ensure((size_t)std::max<int64_t>(src.n, 1));
+    if (src.nrm) sp.ensure_nrm((size_t)std::max<int64_t>(src.n, 1));
     dst = sp.out();
   }
-  launch_select(src, make_float4(rc[0], rc[1], rc[2], rc[3]), cthr, c->tile_in.p, c->tile_off_in.p,
+  launch_select(src, make_float4(rc[0], rc[1], rc[2], rc[3]), mt, c->tile_in.p, c->tile_off_in.p,
                 c->tile_off_out.p, c->totals.p, c->inl_gid.p, nullptr, compact ? &dst : nullptr,
                 c->stream);
   HIPCHK(hipGetLastError());
@@ -605,6 +617,8 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     }
     cl->ctx = c;
     cl->n_total = n;
+    cl->n_points = pts->n;
+    cl->id_base = id_base;
     cl->n_active = n;
     cl->pristine.ensure((size_t)std::max<int64_t>(n, 1));
     if (n) {
@@ -650,6 +664,32 @@ dlg_status dlg_cloud_active(const dlg_cloud* cl, int64_t* n) {
   if (!cl || !n) return DLG_ERR_INVALID;
   *n = cl->n_active;
   return DLG_OK;
+}
+
+dlg_status dlg_cloud_set_normals(dlg_ctx* c, dlg_cloud* cl, const float* normals, int64_t n,
+                                 int64_t stride_bytes) {
+  if (!c || !cl || cl->ctx != c || (n > 0 && !normals)) return DLG_ERR_INVALID;
+  if (n != cl->n_points)
+    return fail(c, DLG_ERR_INVALID, "normals must have one record per uploaded point");
+  if (stride_bytes != 16 && (stride_bytes < 32 || stride_bytes % 4))
+    return fail(c, DLG_ERR_INVALID, "stride_bytes must be 16 (nx, ny, nz, curvature) or >= 32 (pcl::Normal)");
+  return guarded(c, [&] {
+    cl->cur = -1;  // normals attach to the pristine list: the cloud is reset
+    cl->n_active = cl->n_total;
+    cl->pristine.ensure_nrm((size_t)std::max<int64_t>(cl->n_total, 1));
+    if (n > 0) {
+      DevBuf<uint8_t>& raw = c->nw.raw;  // scratch shared with the normals path
+      raw.ensure((size_t)n * (size_t)stride_bytes);
+      HIPCHK(hipMemcpyAsync(raw.p, normals, (size_t)n * (size_t)stride_bytes,
+                            hipMemcpyHostToDevice, c->stream));
+      launch_pack_point_normals(reinterpret_cast<const float*>(raw.p), stride_bytes / 4,
+                                stride_bytes == 16 ? 3 : 4, cl->pristine.view(cl->n_total),
+                                cl->id_base, cl->pristine.nrm.p, c->stream);
+      HIPCHK(hipGetLastError());
+      sync(c);
+    }
+    cl->has_normals = true;
+  });
 }
 
 dlg_status dlg_sac_segment(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* prm, float coeff_out[4],

@@ -72,10 +72,15 @@ struct PinBuf {
 struct SoA {
   DevBuf<float> x, y, z;
   DevBuf<int32_t> gid;
+  DevBuf<float4> nrm;  // SACMODEL_NORMAL_PLANE only (normalized normal, curvature)
+  bool with_nrm = false;
   void ensure(size_t n) { x.ensure(n); y.ensure(n); z.ensure(n); gid.ensure(n); }
-  void release() { x.release(); y.release(); z.release(); gid.release(); }
-  PointsView view(int64_t n) const { return PointsView{x.p, y.p, z.p, gid.p, n}; }
-  PointsOut out() { return PointsOut{x.p, y.p, z.p, gid.p}; }
+  void ensure_nrm(size_t n) { nrm.ensure(n); with_nrm = true; }
+  void release() { x.release(); y.release(); z.release(); gid.release(); nrm.release(); with_nrm = false; }
+  PointsView view(int64_t n) const {
+    return PointsView{x.p, y.p, z.p, gid.p, n, with_nrm ? nrm.p : nullptr};
+  }
+  PointsOut out() { return PointsOut{x.p, y.p, z.p, gid.p, with_nrm ? nrm.p : nullptr}; }
 };
 
 // one sorted grid of the normals path (normals.hip): points in cell order + occupied-cell table
@@ -151,6 +156,9 @@ struct dlg_ctx {
 
 struct dlg_cloud {
   dlg_ctx* ctx = nullptr;
+  int64_t n_points = 0;  // records of the uploaded dlg_points (normals must match)
+  int32_t id_base = 0;
+  bool has_normals = false;
   int64_t n_total = 0;
   int64_t n_active = 0;
   int cur = -1;  // -1 pristine, 0 = A, 1 = B

@@ -43,6 +43,50 @@ __device__ __forceinline__ float pcl_dot(float a, float b, float c, float d, flo
   return (a * x + c * z) + (b * y + d * 1.0f);
 }
 
+// Eigen Vector4f(v0, v1, v2, 0).normalized(): z = (v0^2 + v2^2) + (v1^2 + 0); z > 0 ? v / sqrt(z)
+__device__ __forceinline__ float4 eigen_normalized3(float v0, float v1, float v2, float w) {
+  const float z = (v0 * v0 + v2 * v2) + (v1 * v1 + 0.0f * 0.0f);
+  if (z > 0.0f) {
+    const float s = sqrtf(z);
+    return make_float4(v0 / s, v1 / s, v2 / s, w);
+  }
+  return make_float4(v0, v1, v2, w);
+}
+
+// SampleConsensusModelNormalPlane (PCL 1.8 sac_model_normal_plane.hpp), one point:
+//   d_euclid = fabs(coeff.dot(p) + c3), coeff = (c0, c1, c2, 0), p = (x, y, z, 0)  [float]
+//   d_normal = min(a, pi - a), a = acos(clamp(n.normalized() . coeff.normalized()))   [double]
+//   fabs(w d_normal + (1 - w) d_euclid) < thr,  w = lambda (1 - curvature)          [double]
+// cn = coeff.normalized(); nn = (n.normalized(), curvature); omw = 1 - w.  Prefilter: w >= 0 and
+// d_normal >= 0 give fl(w d_normal + b) >= b = (1 - w) d_euclid, so b >= thr rejects exactly and
+// the acos is only evaluated near the plane.
+__device__ __forceinline__ float np_deuclid(float4 c, float x, float y, float z) {
+  return fabsf(((c.x * x + c.z * z) + (c.y * y + 0.0f * 0.0f)) + c.w);
+}
+__device__ __forceinline__ bool np_full(float4 cn, float4 nn, double w, double b, double thr) {
+  double rad = (double)((nn.x * cn.x + nn.z * cn.z) + (nn.y * cn.y + 0.0f * 0.0f));
+  if (rad < -1.0) rad = -1.0;
+  else if (rad > 1.0) rad = 1.0;
+  double dn = fabs(acos(rad));
+  const double alt = 3.14159265358979323846 - dn;  // M_PI
+  if (alt < dn) dn = alt;                          // std::min(dn, M_PI - dn)
+  return fabs(w * dn + b) < thr;
+}
+__device__ __forceinline__ bool np_test(float4 c, float4 cn, float x, float y, float z, float4 nn,
+                                        double lambda, double thr) {
+  const double w = lambda * (1.0 - (double)nn.w);
+  const double b = (1.0 - w) * (double)np_deuclid(c, x, y, z);
+  if (w >= 0.0 && !(b < thr)) return false;
+  return np_full(cn, nn, w, b, thr);
+}
+
+template <bool NP>
+__device__ __forceinline__ bool model_in(const PointsView& src, int64_t e, float4 cf, float4 cn,
+                                         const ModelTest& mt, float x, float y, float z) {
+  if (NP) return np_test(cf, cn, x, y, z, src.nrm[e], mt.lambda, mt.thr);
+  return fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, x, y, z)) < mt.cthr;
+}
+
 // ---------------------------------------------------------------------------------------------
 __global__ void k_gather_samples(const int32_t* __restrict__ pos, int m, int64_t lo,
                                  PointsView src, SampleRec* __restrict__ out) {
@@ -667,16 +711,17 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, float4 cf, float cthr,
+template <bool NP>
+__global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, float4 cf, ModelTest mt,
                                                    double3 sh, double* __restrict__ partials) {
+  const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   double acc[kMomentK];
 #pragma unroll
   for (int k = 0; k < kMomentK; ++k) acc[k] = 0.0;
   const int64_t stride = (int64_t)gridDim.x * kMoBS;
   for (int64_t e = (int64_t)blockIdx.x * kMoBS + threadIdx.x; e < src.n; e += stride) {
     float x = src.x[e], y = src.y[e], z = src.z[e];
-    float dd = pcl_dot(cf.x, cf.y, cf.z, cf.w, x, y, z);
-    if (fabsf(dd) < cthr) {
+    if (model_in<NP>(src, e, cf, cn, mt, x, y, z)) {
       double dx = (double)x - sh.x, dy = (double)y - sh.y, dz = (double)z - sh.z;
       acc[0] += 1.0;
       acc[1] += dx; acc[2] += dy; acc[3] += dz;
@@ -716,8 +761,10 @@ __global__ void k_reduce_partials(const double* __restrict__ partials, int nb,
 constexpr int kSelBS = 256;
 constexpr int kSelIt = kSelTile / kSelBS;
 
-__global__ __launch_bounds__(kSelBS) void k_select_count(PointsView src, float4 cf, float cthr,
+template <bool NP>
+__global__ __launch_bounds__(kSelBS) void k_select_count(PointsView src, float4 cf, ModelTest mt,
                                                          int32_t* __restrict__ tile_in) {
+  const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   __shared__ int s_w[kSelBS / kWave];
   const int64_t base = (int64_t)blockIdx.x * kSelTile;
   int cnt = 0;
@@ -725,7 +772,7 @@ __global__ __launch_bounds__(kSelBS) void k_select_count(PointsView src, float4 
   for (int j = 0; j < kSelIt; ++j) {
     int64_t e = base + j * kSelBS + threadIdx.x;
     bool in = false;
-    if (e < src.n) in = fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, src.x[e], src.y[e], src.z[e])) < cthr;
+    if (e < src.n) in = model_in<NP>(src, e, cf, cn, mt, src.x[e], src.y[e], src.z[e]);
     cnt += __popcll(ballot(in));
   }
   if ((threadIdx.x & (kWave - 1)) == 0) s_w[threadIdx.x / kWave] = cnt;
@@ -778,13 +825,15 @@ __global__ __launch_bounds__(kScanBS) void k_scan_tiles(const int32_t* __restric
   }
 }
 
-__global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src, float4 cf, float cthr,
+template <bool NP>
+__global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src, float4 cf, ModelTest mt,
                                                            const int32_t* __restrict__ off_in,
                                                            const int32_t* __restrict__ off_out,
                                                            int32_t* __restrict__ inl_gid,
                                                            float* __restrict__ inl_xyz,
                                                            PointsOut dst, int compact) {
   __shared__ int s_w[2][2][kSelBS / kWave];  // [buffer][in/out][wave]
+  const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   const int64_t base = (int64_t)blockIdx.x * kSelTile;
   const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
   int run_in = off_in[blockIdx.x], run_out = off_out[blockIdx.x];
@@ -797,7 +846,7 @@ __global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src, float
     bool in = false;
     if (valid) {
       x = src.x[e]; y = src.y[e]; z = src.z[e]; g = src.gid[e];
-      in = fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, x, y, z)) < cthr;
+      in = model_in<NP>(src, e, cf, cn, mt, x, y, z);
     }
     uint64_t mi = ballot(in), mo = ballot(valid && !in);
     if (lane == 0) {
@@ -823,10 +872,98 @@ __global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src, float
     } else if (valid && compact) {
       int p = run_out + wo + lanes_below(mo);
       dst.x[p] = x; dst.y[p] = y; dst.z[p] = z; dst.gid[p] = g;
+      if (dst.nrm) dst.nrm[p] = src.nrm[e];
     }
     run_in += ti;
     run_out += to;
   }
+}
+
+// k_score_np: counts[h] for SACMODEL_NORMAL_PLANE.  Same tiling as k_score (hypotheses in LDS,
+// P points per lane, ballot counts parked by writelane); per point the weight w and 1 - w are
+// computed once per launch.  The exact prefilter rejects every point with (1 - w) d_euclid >=
+// thr using one float dot and one double multiply; the acos path runs only for waves that have a
+// point near the plane.
+constexpr int kNpP = 4;
+
+__global__ __launch_bounds__(kScBS) void k_score_np(PointsView src, const HypRec* __restrict__ hyps,
+                                                    int D, double lambda, double thr,
+                                                    int32_t* __restrict__ counts) {
+  constexpr int kChunk = kScBS * kNpP;
+  __shared__ float4 s_coef[kHT];
+  __shared__ float4 s_cn[kHT];
+  __shared__ int s_cnt[kMaxHypPerLaunch];
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  for (int i = tid; i < D; i += kScBS) s_cnt[i] = 0;
+  const int64_t n = src.n;
+  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+  const float qnan = __builtin_nanf("");
+  for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    float px[kNpP], py[kNpP], pz[kNpP];
+    float4 pn[kNpP];
+    double pw[kNpP], pomw[kNpP];
+#pragma unroll
+    for (int j = 0; j < kNpP; ++j) {
+      const int64_t e = ch * kChunk + j * kScBS + tid;
+      const bool ok = e < n;
+      px[j] = ok ? src.x[e] : qnan;
+      py[j] = ok ? src.y[e] : qnan;
+      pz[j] = ok ? src.z[e] : qnan;
+      pn[j] = ok ? src.nrm[e] : make_float4(0.f, 0.f, 0.f, 1.f);
+      pw[j] = ok ? lambda * (1.0 - (double)pn[j].w) : 0.0;
+      pomw[j] = 1.0 - pw[j];
+    }
+    for (int t0 = 0; t0 < D; t0 += kHT) {
+      const int nt = min(kHT, D - t0);
+      __syncthreads();
+      for (int i = tid; i < nt; i += kScBS) {
+        const HypRec hr = hyps[t0 + i];
+        s_coef[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
+        s_cn[i] = eigen_normalized3(hr.a, hr.b, hr.c, 0.0f);
+      }
+      __syncthreads();
+      for (int g0 = 0; g0 < nt; g0 += kWave) {  // nt is a multiple of 64 (NaN-padded)
+        int my = 0;
+        for (int k = 0; k < kWave; ++k) {
+          const float4 c = s_coef[g0 + k];
+          double b[kNpP];
+          bool near = false;
+#pragma unroll
+          for (int j = 0; j < kNpP; ++j) {
+            b[j] = pomw[j] * (double)np_deuclid(c, px[j], py[j], pz[j]);
+            near |= (b[j] < thr) || !(pw[j] >= 0.0);
+          }
+          int cnt = 0;
+          if (ballot(near)) {
+            const float4 cn = s_cn[g0 + k];
+#pragma unroll
+            for (int j = 0; j < kNpP; ++j) {
+              const bool cand = (b[j] < thr) || !(pw[j] >= 0.0);
+              bool in = false;
+              if (cand) in = np_full(cn, pn[j], pw[j], b[j], thr);
+              cnt += __popcll(ballot(in));
+            }
+          }
+          my = writelane(my, cnt, k);
+        }
+        atomicAdd(&s_cnt[t0 + g0 + lane], my);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < D; i += kScBS) {
+    const int v = s_cnt[i];
+    if (v) atomicAdd(&counts[i], v);
+  }
+}
+
+__global__ void k_pack_point_normals(const float* __restrict__ raw, int64_t stride_f, int curv_off,
+                                     PointsView src, int32_t id_base, float4* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= src.n) return;
+  const float* r = raw + (int64_t)(src.gid[e] - id_base) * stride_f;
+  out[e] = eigen_normalized3(r[0], r[1], r[2], r[curv_off]);
 }
 
 __global__ void k_absmax(PointsView src, uint32_t* __restrict__ out3) {
@@ -976,28 +1113,58 @@ int moments_blocks(int64_t n) {
   return (int)b;
 }
 
-void launch_moments(PointsView src, float4 coef, float cthr, double3 shift, double* partials,
-                    int nblocks, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_moments, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, cthr, shift, partials);
+void launch_moments(PointsView src, float4 coef, const ModelTest& mt, double3 shift,
+                    double* partials, int nblocks, double* out, hipStream_t s) {
+  if (mt.normal_plane)
+    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
+                       partials);
+  else
+    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
+                       partials);
   hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kMomentK * kWave), 0, s, partials, nblocks, out);
 }
 
 int select_tiles(int64_t n) { return (int)((n + kSelTile - 1) / kSelTile); }
 
-void launch_select(PointsView src, float4 coef, float cthr, int32_t* tile_in, int32_t* tile_off_in,
-                   int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid, float* inl_xyz,
-                   const PointsOut* dst, hipStream_t s) {
+void launch_select(PointsView src, float4 coef, const ModelTest& mt, int32_t* tile_in,
+                   int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid,
+                   float* inl_xyz, const PointsOut* dst, hipStream_t s) {
   const int nt = select_tiles(src.n);
   if (nt == 0) {
     (void)hipMemsetAsync(totals, 0, 2 * sizeof(int32_t), s);
     return;
   }
-  hipLaunchKernelGGL(k_select_count, dim3(nt), dim3(kSelBS), 0, s, src, coef, cthr, tile_in);
+  if (mt.normal_plane)
+    hipLaunchKernelGGL(k_select_count<true>, dim3(nt), dim3(kSelBS), 0, s, src, coef, mt, tile_in);
+  else
+    hipLaunchKernelGGL(k_select_count<false>, dim3(nt), dim3(kSelBS), 0, s, src, coef, mt, tile_in);
   hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanBS), 0, s, tile_in, nt, src.n, tile_off_in,
                      tile_off_out, totals);
-  PointsOut d = dst ? *dst : PointsOut{nullptr, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL(k_select_scatter, dim3(nt), dim3(kSelBS), 0, s, src, coef, cthr, tile_off_in,
-                     tile_off_out, inl_gid, inl_xyz, d, dst ? 1 : 0);
+  PointsOut d = dst ? *dst : PointsOut{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (mt.normal_plane)
+    hipLaunchKernelGGL(k_select_scatter<true>, dim3(nt), dim3(kSelBS), 0, s, src, coef, mt,
+                       tile_off_in, tile_off_out, inl_gid, inl_xyz, d, dst ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_select_scatter<false>, dim3(nt), dim3(kSelBS), 0, s, src, coef, mt,
+                       tile_off_in, tile_off_out, inl_gid, inl_xyz, d, dst ? 1 : 0);
+}
+
+void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest& mt,
+                     int32_t* counts, int num_cus, hipStream_t s) {
+  if (D <= 0 || src.n <= 0) return;
+  const int Dp = (D + kWave - 1) / kWave * kWave;
+  const int64_t chunks = (src.n + (int64_t)kScBS * kNpP - 1) / ((int64_t)kScBS * kNpP);
+  const int64_t cap = (int64_t)num_cus * 2;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(chunks, cap));
+  hipLaunchKernelGGL(k_score_np, dim3(grid), dim3(kScBS), 0, s, src, hyps, Dp, mt.lambda, mt.thr,
+                     counts);
+}
+
+void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,
+                               int32_t id_base, float4* out, hipStream_t s) {
+  if (src.n <= 0) return;
+  hipLaunchKernelGGL(k_pack_point_normals, dim3(cdiv(src.n, 256)), dim3(256), 0, s, raw, stride_f,
+                     curv_off, src, id_base, out);
 }
 
 void launch_absmax(PointsView src, uint32_t* out3, hipStream_t s) {

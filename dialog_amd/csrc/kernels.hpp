@@ -26,12 +26,15 @@ struct alignas(16) HypRec {
   float w;       // band half-width around cthr for the |fma(...)| - cthr test (variant 2)
 };
 
+// nrm (optional, SACMODEL_NORMAL_PLANE): per point (n.normalized() as Eigen computes it for
+// getAngle3D, curvature) -- normalised once at upload, bit-identical to normalising per test
 struct PointsView {
   const float* x;
   const float* y;
   const float* z;
   const int32_t* gid;
   int64_t n;
+  const float4* nrm;
 };
 
 struct PointsOut {
@@ -39,6 +42,17 @@ struct PointsOut {
   float* y;
   float* z;
   int32_t* gid;
+  float4* nrm;
+};
+
+// inlier test of the select / moments / scoring kernels
+//   SACMODEL_PLANE        : |pcl_dot(c, p)| < cthr            (cthr = smallest float >= threshold)
+//   SACMODEL_NORMAL_PLANE : |w d_normal + (1 - w) d_euclid| < thr, w = lambda (1 - curvature)
+struct ModelTest {
+  float cthr;
+  int normal_plane;
+  double thr;
+  double lambda;
 };
 
 constexpr int kMaxHypPerLaunch = 4096;  // LDS count array of the scoring kernel
@@ -79,17 +93,26 @@ void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, fl
 // counts must be zeroed by the caller (memset on the same stream).
 void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
                   int variant, int num_cus, hipStream_t s);
+// SampleConsensusModelNormalPlane::countWithinDistance for D hypotheses (src.nrm required);
+// counts need room for D rounded up to 64 and must be zeroed by the caller
+void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest& mt,
+                     int32_t* counts, int num_cus, hipStream_t s);
 // moments (count + 9 sums, double, coordinates shifted by `shift`) of the inliers of coef;
 // partials [nblocks][10] -> out[10] (fixed-order reduction: deterministic)
 int moments_blocks(int64_t n);
-void launch_moments(PointsView src, float4 coef, float cthr, double3 shift, double* partials,
-                    int nblocks, double* out, hipStream_t s);
+void launch_moments(PointsView src, float4 coef, const ModelTest& mt, double3 shift,
+                    double* partials, int nblocks, double* out, hipStream_t s);
 // select: inliers of coef in list order; optional inlier xyz (AoS, 3 floats); optional
-// compaction of the outliers into dst.  tile_in/out: [ntiles] scratch; totals[2] = {in, out}.
+// compaction of the outliers (and their normals) into dst.  tile_in/out: [ntiles] scratch;
+// totals[2] = {in, out}.
 int select_tiles(int64_t n);
-void launch_select(PointsView src, float4 coef, float cthr, int32_t* tile_in, int32_t* tile_off_in,
-                   int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid, float* inl_xyz,
-                   const PointsOut* dst, hipStream_t s);
+void launch_select(PointsView src, float4 coef, const ModelTest& mt, int32_t* tile_in,
+                   int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid,
+                   float* inl_xyz, const PointsOut* dst, hipStream_t s);
+// raw caller normals (n records of stride_f floats, curvature at curv_off) gathered by the
+// cloud's local point index (gid - id_base) -> (normalized normal, curvature)
+void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,
+                               int32_t id_base, float4* out, hipStream_t s);
 // max |x|, |y|, |z| over the cloud (prefilter error bound); out: 3 floats (as uint bits)
 void launch_absmax(PointsView src, uint32_t* out3, hipStream_t s);
 

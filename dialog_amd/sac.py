@@ -150,6 +150,15 @@ class Cloud:
     def reset(self):
         self.ctx.check(self.ctx._L.dlg_cloud_reset(self.h))
 
+    def set_normals(self, normals):
+        """setInputNormals: float32 [N,4] (nx, ny, nz, curvature) or [N,8] pcl::Normal records,
+        one per uploaded point.  Resets the cloud."""
+        a = np.ascontiguousarray(normals, dtype=np.float32)
+        if a.ndim != 2 or a.shape[1] not in (4, 8):
+            raise ValueError("normals must be float32 [N,4] or [N,8]")
+        self.ctx.check(self.ctx._L.dlg_cloud_set_normals(self.ctx.h, self.h, _f32p(a), a.shape[0],
+                                                         4 * a.shape[1]))
+
     @property
     def n_active(self):
         v = C.c_int64()
@@ -171,7 +180,7 @@ class Cloud:
 
 def make_params(threshold=0.0, max_iterations=50, probability=0.99, optimize=True, seed=12345,
                 refit_mode=DLG_REFIT_PCL, hypotheses_per_launch=0, gather_inliers=True,
-                model=SACMODEL_PLANE):
+                model=SACMODEL_PLANE, normal_distance_weight=0.1):
     L = _lib.load()
     p = _lib.SacParams()
     L.dlg_sac_params_default(C.byref(p))
@@ -184,6 +193,7 @@ def make_params(threshold=0.0, max_iterations=50, probability=0.99, optimize=Tru
     p.hypotheses_per_launch = int(hypotheses_per_launch)
     p.gather_inliers = int(bool(gather_inliers))
     p.model = int(model)
+    p.normal_distance_weight = float(normal_distance_weight)
     return p
 
 
@@ -257,6 +267,11 @@ class SACSegmentation:
         self.indices = None
         self.last_stats = None
 
+    _models = (SACMODEL_PLANE,)
+
+    def _attach(self, cloud):
+        pass
+
     # PCL setters (camelCase as in the reference's call sites) ------------------------------
     def setModelType(self, m):
         self.model_type = int(m)
@@ -289,15 +304,18 @@ class SACSegmentation:
         """-> (inliers int32[], coefficients float32[4] or [] when no model was found)."""
         if self.input is None:
             raise ValueError("setInputCloud() first")
-        if self.model_type != SACMODEL_PLANE:
-            raise ValueError("only SACMODEL_PLANE is supported (PCL: initSACModel fails)")
+        if self.model_type not in self._models:
+            raise ValueError(f"model type {self.model_type} not supported here "
+                             "(PCL: initSACModel fails)")
         if self.method_type not in (SAC_RANSAC,):
             raise ValueError("only SAC_RANSAC is supported")
         ctx = self.ctx or default_context()
         params = make_params(self.threshold, self.max_iterations, self.probability, self.optimize,
-                             refit_mode=self.refit_mode)
+                             refit_mode=self.refit_mode, model=self.model_type,
+                             normal_distance_weight=getattr(self, "normal_distance_weight", 0.1))
         cloud = Cloud(ctx, self.input, indices=self.indices)
         try:
+            self._attach(cloud)
             inl, coeff, st = segment_cloud(cloud, params)
         finally:
             cloud.close()
@@ -315,3 +333,29 @@ class SACSegmentation:
     set_optimize_coefficients = setOptimizeCoefficients
     set_input_cloud = setInputCloud
     set_indices = setIndices
+
+
+class SACSegmentationFromNormals(SACSegmentation):
+    """pcl::SACSegmentationFromNormals<PointXYZ, Normal> (SACMODEL_NORMAL_PLANE, SAC_RANSAC)."""
+
+    _models = (SACMODEL_PLANE, SACMODEL_NORMAL_PLANE)
+
+    def __init__(self, ctx: Context | None = None):
+        super().__init__(ctx)
+        self.normals = None
+        self.normal_distance_weight = 0.1
+
+    def setInputNormals(self, normals):
+        self.normals = np.ascontiguousarray(normals, dtype=np.float32)
+
+    def setNormalDistanceWeight(self, w):
+        self.normal_distance_weight = float(w)
+
+    def _attach(self, cloud):
+        if self.model_type == SACMODEL_NORMAL_PLANE:
+            if self.normals is None:
+                raise ValueError("setInputNormals() first (PCL: no input normals)")
+            cloud.set_normals(self.normals)
+
+    set_input_normals = setInputNormals
+    set_normal_distance_weight = setNormalDistanceWeight

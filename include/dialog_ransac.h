@@ -69,8 +69,8 @@ typedef struct {
   double probability;          /* setProbability (PCL default 0.99) */
   int optimize;                /* setOptimizeCoefficients (PCL default 1) */
   uint32_t seed;               /* 12345u = PCL's non-random seed */
-  int model;                   /* DLG_SACMODEL_PLANE */
-  double normal_distance_weight;
+  int model;                   /* DLG_SACMODEL_PLANE | DLG_SACMODEL_NORMAL_PLANE (needs normals) */
+  double normal_distance_weight; /* SACSegmentationFromNormals::setNormalDistanceWeight (0.1) */
   int refit_mode;              /* DLG_REFIT_PCL (default) | DLG_REFIT_FAST */
   int hypotheses_per_launch;   /* upper bound of one scoring launch; 0 = 4096 */
   int gather_inliers;          /* multi-rank: 1 = every rank receives the global inlier list */
@@ -131,6 +131,12 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cloud);
 /* re-activate every point of the cloud (undo extract-and-remove) */
 dlg_status dlg_cloud_reset(dlg_cloud* cloud);
 dlg_status dlg_cloud_active(const dlg_cloud* cloud, int64_t* n_active_local);
+/* SACSegmentationFromNormals::setInputNormals: one normal record per uploaded point (n = the
+ * dlg_points n of dlg_cloud_upload; the cloud's indices select from it like from the points).
+ * stride_bytes 16 = (nx, ny, nz, curvature), >= 32 = pcl::Normal (curvature at byte 16).
+ * Required by DLG_SACMODEL_NORMAL_PLANE; resets the cloud to all points active. */
+dlg_status dlg_cloud_set_normals(dlg_ctx* ctx, dlg_cloud* cloud, const float* normals, int64_t n,
+                                 int64_t stride_bytes);
 
 /* ---- RANSAC ----------------------------------------------------------------------------------- */
 /* SACSegmentation::segment on the cloud's active points (not removed).  inliers_out receives

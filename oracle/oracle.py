@@ -24,10 +24,15 @@ def build() -> str:
     return path
 
 
+SACMODEL_PLANE = 0
+SACMODEL_NORMAL_PLANE = 11
+
+
 class SacParams(C.Structure):
     _fields_ = [("threshold", C.c_double), ("max_iterations", C.c_int),
                 ("probability", C.c_double), ("optimize", C.c_int),
-                ("seed", C.c_uint32), ("refit_double", C.c_int)]
+                ("seed", C.c_uint32), ("refit_double", C.c_int), ("model", C.c_int),
+                ("normal_distance_weight", C.c_double), ("normals", C.POINTER(C.c_float))]
 
 
 class SacStats(C.Structure):
@@ -65,6 +70,11 @@ def lib():
         L.orc_mean_cov.argtypes = [fp, C.c_int64, i32p, C.c_int64, fp, fp]
         L.orc_eigen33.argtypes = [fp, fp, fp]
         L.orc_refit_double.argtypes = [fp, C.c_int64, i32p, C.c_int64, fp, fp]
+        L.orc_count_within_np.argtypes = [fp, C.c_int64, fp, i32p, C.c_int64, fp, C.c_double,
+                                          C.c_double]
+        L.orc_count_within_np.restype = C.c_int64
+        L.orc_normal_plane_dist.argtypes = [fp, fp, fp, C.c_double]
+        L.orc_normal_plane_dist.restype = C.c_double
         L.orc_estimate_normals.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, fp, fp]
         L.orc_estimate_normals_knn.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, fp, fp]
         L.orc_regulate_normals.argtypes = [fp, C.c_int64, C.c_int64, fp, C.c_int64, C.c_int,
@@ -101,15 +111,30 @@ def mt_stream(n, seed=12345):
 
 
 def params(threshold, max_iterations=50, probability=0.99, optimize=True, seed=12345,
-           refit_double=False):
-    return SacParams(float(threshold), int(max_iterations), float(probability), int(bool(optimize)),
-                     int(seed), int(bool(refit_double)))
+           refit_double=False, normals=None, normal_distance_weight=0.1):
+    """normals (float32 [N,4]: nx, ny, nz, curvature) selects SACMODEL_NORMAL_PLANE; the caller
+    keeps the array alive for the call (params_keep)."""
+    prm = SacParams(float(threshold), int(max_iterations), float(probability),
+                    int(bool(optimize)), int(seed), int(bool(refit_double)))
+    if normals is not None:
+        assert normals.dtype == np.float32 and normals.flags.c_contiguous and normals.shape[1] == 4
+        prm.model = SACMODEL_NORMAL_PLANE
+        prm.normal_distance_weight = float(normal_distance_weight)
+        prm.normals = _f(normals)
+    return prm
+
+
+def _normals_arg(kw):
+    if kw.get("normals") is not None:
+        kw["normals"] = np.ascontiguousarray(kw["normals"], np.float32)
+    return kw
 
 
 def sac_segment(points, threshold, indices=None, **kw):
     """PCL SACSegmentation(PLANE, RANSAC).segment -> dict(coeff, inliers, stats...)."""
     p, stride = _xyz(points)
     n = p.shape[0]
+    kw = _normals_arg(kw)
     prm = params(threshold, **kw)
     if indices is not None:
         idx = np.ascontiguousarray(indices, dtype=np.int32)
@@ -133,6 +158,7 @@ def sac_segment(points, threshold, indices=None, **kw):
 def extract_planes(points, threshold, max_planes=20, min_inliers=0, **kw):
     p, stride = _xyz(points)
     n = p.shape[0]
+    kw = _normals_arg(kw)
     prm = params(threshold, **kw)
     coeffs = np.zeros((max_planes, 4), np.float32)
     offs = np.zeros(max_planes + 1, np.int64)
@@ -144,6 +170,21 @@ def extract_planes(points, threshold, max_planes=20, min_inliers=0, **kw):
     k = npl.value
     return dict(coeffs=coeffs[:k].copy(), offsets=offs[:k + 1].copy(),
                 inliers=inl[:offs[k]].copy(), n_planes=k)
+
+
+def count_within_np(points, normals, coeff, threshold, lam=0.1):
+    p, stride = _xyz(points)
+    nrm = np.ascontiguousarray(normals, np.float32)
+    c = np.ascontiguousarray(coeff, np.float32)
+    return lib().orc_count_within_np(_f(p), stride, _f(nrm), None, p.shape[0], _f(c),
+                                     float(threshold), float(lam))
+
+
+def normal_plane_dist(coeff, point, normal, lam=0.1):
+    c = np.ascontiguousarray(coeff, np.float32)
+    p = np.ascontiguousarray(point, np.float32)
+    n = np.ascontiguousarray(normal, np.float32)
+    return lib().orc_normal_plane_dist(_f(c), _f(p), _f(n), float(lam))
 
 
 def count_within(points, coeff, threshold, indices=None):

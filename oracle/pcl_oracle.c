@@ -107,13 +107,78 @@ int64_t orc_count_within(const float* xyz, int64_t stride, const int32_t* idx, i
   return cnt;
 }
 
-static int64_t orc_select_within(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
-                                 const float c[4], double thr, int32_t* out) {
+/* ------------------------------------------------------------------------------------------ */
+/* SampleConsensusModelNormalPlane::countWithinDistance / selectWithinDistance (PCL 1.8         */
+/* sac_model_normal_plane.hpp; SACMODEL_NORMAL_PLANE, not used by the reference -- config C5):  */
+/*   coeff = model with coeff[3] = 0;  p = (x, y, z, 0);  n = (nx, ny, nz, 0)                    */
+/*   d_euclid = fabs(coeff.dot(p) + model[3])            float, predux (c0x + c2z) + (c1y + 0)   */
+/*   d_normal = getAngle3D(n, coeff) = acos(clamp(n.normalized().dot(coeff.normalized())))       */
+/*   d_normal = min(d_normal, M_PI - d_normal)                                                   */
+/*   weight   = normal_distance_weight * (1.0 - curvature)                                       */
+/*   inlier  <=> fabs(weight * d_normal + (1.0 - weight) * d_euclid) < threshold   (double)      */
+/* Eigen normalized(): z = squaredNorm (predux order); z > 0 ? v / sqrt(z) : v.                  */
+/* ------------------------------------------------------------------------------------------ */
+void orc_normalized4(const float v[3], float out[3]) {
+  float z = (v[0] * v[0] + v[2] * v[2]) + (v[1] * v[1] + 0.0f * 0.0f);
+  if (z > 0.0f) {
+    float s = sqrtf(z);
+    out[0] = v[0] / s; out[1] = v[1] / s; out[2] = v[2] / s;
+  } else {
+    out[0] = v[0]; out[1] = v[1]; out[2] = v[2];
+  }
+}
+
+double orc_normal_plane_dist(const float c[4], const float p[3], const float nrm[4],
+                             double lambda) {
+  float de_f = fabsf(((c[0] * p[0] + c[2] * p[2]) + (c[1] * p[1] + 0.0f * 0.0f)) + c[3]);
+  double d_euclid = (double)de_f;
+  float nn[3], cn[3];
+  orc_normalized4(nrm, nn);
+  orc_normalized4(c, cn);
+  float rad_f = (nn[0] * cn[0] + nn[2] * cn[2]) + (nn[1] * cn[1] + 0.0f * 0.0f);
+  double rad = (double)rad_f;
+  if (rad < -1.0) rad = -1.0;
+  else if (rad > 1.0) rad = 1.0;
+  double d_normal = fabs(acos(rad));
+  double alt = 3.14159265358979323846 - d_normal;  /* M_PI */
+  if (alt < d_normal) d_normal = alt;             /* std::min(a, b) = (b < a) ? b : a */
+  double weight = lambda * (1.0 - (double)nrm[3]);
+  return fabs(weight * d_normal + (1.0 - weight) * d_euclid);
+}
+
+static int orc_within(const orc_sac_params* prm, const float* xyz, int64_t stride, int32_t g,
+                      const float c[4], double thr) {
+  const float* p = xyz + (int64_t)g * stride;
+  if (prm && prm->model == ORC_SACMODEL_NORMAL_PLANE)
+    return orc_normal_plane_dist(c, p, prm->normals + (int64_t)g * 4, prm->normal_distance_weight) < thr;
+  return (double)orc_plane_abs_dist(c, p[0], p[1], p[2]) < thr;
+}
+
+static int64_t orc_count_model(const orc_sac_params* prm, const float* xyz, int64_t stride,
+                               const int32_t* idx, int64_t n, const float c[4], double thr) {
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < n; ++i) cnt += orc_within(prm, xyz, stride, idx ? idx[i] : (int32_t)i, c, thr);
+  return cnt;
+}
+
+int64_t orc_count_within_np(const float* xyz, int64_t stride, const float* normals,
+                            const int32_t* idx, int64_t n, const float c[4], double thr,
+                            double lambda) {
+  orc_sac_params prm;
+  memset(&prm, 0, sizeof(prm));
+  prm.model = ORC_SACMODEL_NORMAL_PLANE;
+  prm.normals = normals;
+  prm.normal_distance_weight = lambda;
+  return orc_count_model(&prm, xyz, stride, idx, n, c, thr);
+}
+
+static int64_t orc_select_within(const orc_sac_params* prm, const float* xyz, int64_t stride,
+                                 const int32_t* idx, int64_t n, const float c[4], double thr,
+                                 int32_t* out) {
   int64_t k = 0;
   for (int64_t i = 0; i < n; ++i) {
     int32_t g = idx[i];
-    const float* p = xyz + (int64_t)g * stride;
-    if ((double)orc_plane_abs_dist(c, p[0], p[1], p[2]) < thr) out[k++] = g;
+    if (orc_within(prm, xyz, stride, g, c, thr)) out[k++] = g;
   }
   return k;
 }
@@ -381,7 +446,7 @@ int orc_sac_segment(const float* xyz, int64_t n_points, int64_t stride,
     float c[4];
     if (!orc_plane_coefficients(xyz + (int64_t)s[0] * stride, xyz + (int64_t)s[1] * stride,
                                 xyz + (int64_t)s[2] * stride, c)) { ++skipped; continue; }
-    int n = (int)orc_count_within(xyz, stride, idx, n_idx, c, thr);
+    int n = (int)orc_count_model(prm, xyz, stride, idx, n_idx, c, thr);
     if (n > best) {
       best = n;
       have = 1;
@@ -403,14 +468,14 @@ done:
     st->has_model = 1;
     memcpy(st->best_sample, best_s, sizeof(best_s));
     memcpy(st->coeff_unrefined, best_c, sizeof(best_c));
-    int64_t nin = orc_select_within(xyz, stride, idx, n_idx, best_c, thr, inliers_out);
+    int64_t nin = orc_select_within(prm, xyz, stride, idx, n_idx, best_c, thr, inliers_out);
     st->n_unrefined = nin;
     if (prm->optimize) {
       float rc[4];
       if (prm->refit_double) orc_refit_double(xyz, stride, inliers_out, nin, best_c, rc);
       else orc_optimize_plane(xyz, stride, inliers_out, nin, best_c, rc);
       memcpy(coeff, rc, sizeof(rc));
-      nin = orc_select_within(xyz, stride, idx, n_idx, rc, thr, inliers_out);
+      nin = orc_select_within(prm, xyz, stride, idx, n_idx, rc, thr, inliers_out);
     } else {
       memcpy(coeff, best_c, sizeof(best_c));
     }

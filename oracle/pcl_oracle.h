@@ -52,7 +52,10 @@ void orc_eigen33_d(const double m[9], double* eval, double evec[3]);
 int  orc_refit_double(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
                       const float coeff_in[4], float coeff_out[4]);
 
-/* ---- SACSegmentation<PointXYZ>::segment with SACMODEL_PLANE / SAC_RANSAC ---- */
+/* ---- SACSegmentation<PointXYZ>::segment with SACMODEL_PLANE / SAC_RANSAC, and
+ *      SACSegmentationFromNormals with SACMODEL_NORMAL_PLANE ---- */
+#define ORC_SACMODEL_PLANE 0
+#define ORC_SACMODEL_NORMAL_PLANE 11
 typedef struct {
   double   threshold;        /* setDistanceThreshold */
   int      max_iterations;   /* setMaxIterations (PCL default 50) */
@@ -60,6 +63,9 @@ typedef struct {
   int      optimize;         /* setOptimizeCoefficients (default true) */
   uint32_t seed;             /* 12345u unless random_ */
   int      refit_double;     /* 0: PCL float refit; 1: double-exact refit (fast-mode twin) */
+  int      model;            /* ORC_SACMODEL_PLANE | ORC_SACMODEL_NORMAL_PLANE */
+  double   normal_distance_weight;  /* setNormalDistanceWeight (PCL default 0.1) */
+  const float* normals;      /* NORMAL_PLANE: 4 floats per point (nx, ny, nz, curvature) */
 } orc_sac_params;
 
 typedef struct {
@@ -87,6 +93,13 @@ int orc_extract_planes(const float* xyz, int64_t n_points, int64_t stride,
                        const orc_sac_params* prm, int max_planes, int64_t min_inliers,
                        float* coeffs /* 4*max_planes */, int64_t* offsets /* max_planes+1 */,
                        int32_t* inliers /* n_points */, int* n_planes);
+
+/* NORMAL_PLANE distance of one point (|w d_normal + (1 - w) d_euclid|), and its count */
+void orc_normalized4(const float v[3], float out[3]);
+double orc_normal_plane_dist(const float c[4], const float p[3], const float nrm[4], double lambda);
+int64_t orc_count_within_np(const float* xyz, int64_t stride, const float* normals,
+                            const int32_t* idx, int64_t n, const float c[4], double thr,
+                            double lambda);
 
 /* count within distance for an arbitrary list of hypotheses (CPU baseline leg) */
 int64_t orc_count_within(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,

@@ -121,6 +121,21 @@ def main():
     np.savez_compressed(os.path.join(HERE, "normals_small.npz"), points=pn, radius=0.1, k=20,
                         radius_normals=rn, knn_normals=kn, seed_idx=0, r_regulate=0.08,
                         regulated=reg, processed=proc)
+    # SACMODEL_NORMAL_PLANE (config C5 shape, small): radius normals from the oracle, one segment
+    # and one extract-and-remove run, PCL float refit
+    pp, _, _ = plane_cloud(8192, 3, outlier_frac=0.1, seed=SEED_BASE + 6, patch=2.0)
+    pnrm = O.estimate_normals(pp, 0.1)
+    sg = O.sac_segment(pp, 0.05, max_iterations=200, probability=0.99, normals=pnrm,
+                       normal_distance_weight=0.1)
+    ex = O.extract_planes(pp, 0.05, max_planes=6, min_inliers=200, max_iterations=255,
+                          probability=1.0, normals=pnrm, normal_distance_weight=0.3)
+    np.savez_compressed(os.path.join(HERE, "normal_plane_small.npz"), points=pp, normals=pnrm,
+                        seg_threshold=0.05, seg_lambda=0.1, seg_max_iterations=200,
+                        seg_probability=0.99, seg_coeff=sg["coeff"], seg_inliers=sg["inliers"],
+                        seg_iterations=sg["iterations"], seg_best_sample=sg["best_sample"],
+                        ex_threshold=0.05, ex_lambda=0.3, ex_max_iterations=255, ex_min_inliers=200,
+                        ex_max_planes=6, ex_coeffs=ex["coeffs"], ex_offsets=ex["offsets"],
+                        ex_inliers=ex["inliers"])
     print("golden fixtures written to", HERE)
 
 

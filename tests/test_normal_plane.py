@@ -1,0 +1,236 @@
+"""SACMODEL_NORMAL_PLANE (SACSegmentationFromNormals; BASELINE config C5).
+
+The reference does not call this model; PCL 1.8's SampleConsensusModelNormalPlane is restated in
+oracle/pcl_oracle.c (orc_normal_plane_dist) and cross-checked here by an independent numpy
+restatement.  "Parity unpinned" as the rest of the PCL arithmetic (no PCL build here), and the
+exact getAngle3D form (n.normalized().dot(coeff.normalized()), clamped, acos) is taken from the
+PCL 1.8 sources as published.  GPU results must equal the oracle bit-for-bit (PCL float refit):
+same iterations, same winning sample, same coefficients bits, same inlier lists.
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def np_twin_dist(c, p, nrm, lam):
+    """numpy restatement of the NORMAL_PLANE point distance (float32 ops in Eigen's order)."""
+    c = np.asarray(c, np.float32)
+    p = np.asarray(p, np.float32)
+    n = np.asarray(nrm, np.float32)
+    f = np.float32
+    de = np.abs(((c[0] * p[:, 0] + c[2] * p[:, 2]) + (c[1] * p[:, 1] + f(0) * f(0))) + c[3])
+
+    def normalized(v0, v1, v2):
+        z = (v0 * v0 + v2 * v2) + (v1 * v1 + f(0) * f(0))
+        s = np.sqrt(z)
+        ok = z > 0
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return (np.where(ok, v0 / s, v0), np.where(ok, v1 / s, v1), np.where(ok, v2 / s, v2))
+
+    nx, ny, nz = normalized(n[:, 0], n[:, 1], n[:, 2])
+    cx, cy, cz = normalized(np.full(1, c[0]), np.full(1, c[1]), np.full(1, c[2]))
+    rad = ((nx * cx + nz * cz) + (ny * cy + f(0) * f(0))).astype(np.float64)
+    rad = np.where(rad < -1.0, -1.0, np.where(rad > 1.0, 1.0, rad))
+    dn = np.abs(np.arccos(rad))
+    alt = np.pi - dn
+    dn = np.where(alt < dn, alt, dn)
+    w = lam * (1.0 - n[:, 3].astype(np.float64))
+    return np.abs(w * dn + (1.0 - w) * de.astype(np.float64))
+
+
+def cloud_with_normals(n=8192, seed=6, outliers=0.1):
+    from dialog_amd.synth import plane_cloud
+    p, lab, pl = plane_cloud(n, 3, outlier_frac=outliers, seed=seed, patch=2.0)
+    return p, O.estimate_normals(p, 0.1), lab, pl
+
+
+# ------------------------------------------------------------------------------------- CPU tests
+def test_oracle_np_distance_matches_numpy_twin():
+    p, nrm, _, _ = cloud_with_normals(3000, seed=2)
+    rng = np.random.default_rng(0)
+    for t in range(20):
+        i = rng.choice(len(p), 3, replace=False)
+        c = np.zeros(4, np.float32)
+        # a plane through three of the points
+        v1, v2 = p[i[1]] - p[i[0]], p[i[2]] - p[i[0]]
+        nn = np.cross(v1.astype(np.float64), v2.astype(np.float64))
+        nn /= np.linalg.norm(nn)
+        c[:3] = nn
+        c[3] = -np.dot(nn, p[i[0]])
+        lam = [0.0, 0.1, 0.5, 1.0][t % 4]
+        ok = ~np.isnan(nrm[:, 0])
+        twin = np_twin_dist(c, p[ok], nrm[ok], lam)
+        orc = np.array([O.normal_plane_dist(c, p[k], nrm[k], lam) for k in np.flatnonzero(ok)[:400]])
+        np.testing.assert_allclose(orc, twin[:400], rtol=1e-14, atol=1e-15)
+        for thr in (0.01, 0.05, 0.2):
+            assert O.count_within_np(p, nrm, c, thr, lam) == int((twin < thr).sum())
+
+
+def test_oracle_np_segment_properties():
+    p, nrm, lab, pl = cloud_with_normals()
+    r = O.sac_segment(p, 0.05, max_iterations=200, normals=nrm, normal_distance_weight=0.1)
+    assert r["ok"]
+    d = np_twin_dist(r["coeff"], p, nrm, 0.1)
+    ok = np.flatnonzero(d < 0.05)
+    assert np.array_equal(ok.astype(np.int32), r["inliers"])
+    # the plane found is one of the generator's planes
+    k = np.argmax(np.abs(pl[:, :3] @ r["coeff"][:3]))
+    assert abs(abs(pl[k, :3] @ r["coeff"][:3]) - 1) < 1e-3
+    # the RNG stream does not depend on the model: same draws as the plane model
+    r0 = O.sac_segment(p, 0.05, max_iterations=3, probability=1.0, normals=nrm)
+    rp = O.sac_segment(p, 0.05, max_iterations=3, probability=1.0)
+    assert r0["draws"] == rp["draws"]
+
+
+def test_oracle_np_fixture():
+    z = np.load(os.path.join(GOLDEN, "normal_plane_small.npz"))
+    r = O.sac_segment(z["points"], float(z["seg_threshold"]),
+                      max_iterations=int(z["seg_max_iterations"]),
+                      probability=float(z["seg_probability"]), normals=z["normals"],
+                      normal_distance_weight=float(z["seg_lambda"]))
+    assert r["iterations"] == int(z["seg_iterations"])
+    assert np.array_equal(r["coeff"].view(np.uint32), z["seg_coeff"].view(np.uint32))
+    assert np.array_equal(r["inliers"], z["seg_inliers"])
+
+
+# ------------------------------------------------------------------------------------- GPU tests
+@pytest.mark.gpu
+def test_gpu_np_segment_golden(gpu_ctx):
+    import dialog_amd as D
+    z = np.load(os.path.join(GOLDEN, "normal_plane_small.npz"))
+    cloud = D.Cloud(gpu_ctx, z["points"])
+    cloud.set_normals(z["normals"])
+    prm = D.make_params(float(z["seg_threshold"]), max_iterations=int(z["seg_max_iterations"]),
+                        probability=float(z["seg_probability"]), model=D.SACMODEL_NORMAL_PLANE,
+                        normal_distance_weight=float(z["seg_lambda"]))
+    inl, coeff, st = D.segment_cloud(cloud, prm)
+    assert st["iterations"] == int(z["seg_iterations"])
+    assert np.array_equal(st["best_sample"], z["seg_best_sample"])
+    assert np.array_equal(coeff.view(np.uint32), z["seg_coeff"].view(np.uint32))
+    assert np.array_equal(inl, z["seg_inliers"])
+    cloud.close()
+
+
+@pytest.mark.gpu
+def test_gpu_np_extract_golden(gpu_ctx):
+    import dialog_amd as D
+    z = np.load(os.path.join(GOLDEN, "normal_plane_small.npz"))
+    cloud = D.Cloud(gpu_ctx, z["points"])
+    # pcl::Normal records (stride 32) must give the same result as (n, curvature) float4
+    rec = np.zeros((z["normals"].shape[0], 8), np.float32)
+    rec[:, :3] = z["normals"][:, :3]
+    rec[:, 4] = z["normals"][:, 3]
+    cloud.set_normals(rec)
+    prm = D.make_params(float(z["ex_threshold"]), max_iterations=int(z["ex_max_iterations"]),
+                        probability=1.0, model=D.SACMODEL_NORMAL_PLANE,
+                        normal_distance_weight=float(z["ex_lambda"]))
+    e = D.extract_planes(cloud, prm, max_planes=int(z["ex_max_planes"]),
+                         min_inliers=int(z["ex_min_inliers"]))
+    assert np.array_equal(e["offsets"], z["ex_offsets"])
+    assert np.array_equal(e["coeffs"].view(np.uint32), z["ex_coeffs"].view(np.uint32))
+    assert np.array_equal(e["inliers"], z["ex_inliers"])
+    cloud.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,lam,thr", [(1, 0.1, 0.05), (2, 0.5, 0.1), (3, 0.0, 0.02),
+                                          (4, 1.0, 0.3), (5, 0.2, 0.05)])
+def test_gpu_np_random_vs_oracle(gpu_ctx, seed, lam, thr):
+    import dialog_amd as D
+    p, nrm, _, _ = cloud_with_normals(int(2000 + 3000 * seed), seed=seed, outliers=0.2)
+    if seed == 5:  # NaN normals (isolated points) and a zero normal
+        nrm[::97] = np.nan
+        nrm[5, :3] = 0.0
+    idx = None
+    if seed == 2:  # setIndices subset, unsorted
+        idx = np.random.default_rng(seed).permutation(len(p))[: len(p) // 2].astype(np.int32)
+    r = O.sac_segment(p, thr, indices=idx, max_iterations=300, normals=nrm,
+                      normal_distance_weight=lam)
+    cloud = D.Cloud(gpu_ctx, p, indices=idx)
+    cloud.set_normals(nrm)
+    prm = D.make_params(thr, max_iterations=300, model=D.SACMODEL_NORMAL_PLANE,
+                        normal_distance_weight=lam)
+    inl, coeff, st = D.segment_cloud(cloud, prm)
+    assert st["has_model"] == r["ok"]
+    assert st["iterations"] == r["iterations"]
+    assert np.array_equal(st["best_sample"], r["best_sample"])
+    assert np.array_equal(coeff.view(np.uint32), r["coeff"].view(np.uint32))
+    assert np.array_equal(inl, r["inliers"])
+    cloud.close()
+
+
+@pytest.mark.gpu
+def test_gpu_np_requires_normals_and_fast_refit(gpu_ctx):
+    import dialog_amd as D
+    p, nrm, _, _ = cloud_with_normals(6000, seed=9)
+    cloud = D.Cloud(gpu_ctx, p)
+    prm = D.make_params(0.05, max_iterations=100, model=D.SACMODEL_NORMAL_PLANE)
+    with pytest.raises(D.DialogError):
+        D.segment_cloud(cloud, prm)
+    with pytest.raises(D.DialogError):
+        cloud.set_normals(nrm[:-1])  # one record per point
+    cloud.set_normals(nrm)
+    prm_f = D.make_params(0.05, max_iterations=100, model=D.SACMODEL_NORMAL_PLANE,
+                          refit_mode=D.DLG_REFIT_FAST)
+    inl, coeff, st = D.segment_cloud(cloud, prm_f)
+    r = O.sac_segment(p, 0.05, max_iterations=100, normals=nrm, refit_double=True)
+    assert np.abs(coeff - r["coeff"]).max() < 1e-5
+    d = np_twin_dist(coeff, p, nrm, 0.1)
+    assert np.array_equal(inl, np.flatnonzero(d < 0.05).astype(np.int32))
+    # the PCL mirror
+    seg = D.SACSegmentationFromNormals(gpu_ctx)
+    seg.setModelType(D.SACMODEL_NORMAL_PLANE)
+    seg.setMethodType(D.SAC_RANSAC)
+    seg.setDistanceThreshold(0.05)
+    seg.setMaxIterations(100)
+    seg.setNormalDistanceWeight(0.1)
+    seg.setInputCloud(p)
+    seg.setInputNormals(nrm)
+    i2, c2 = seg.segment()
+    r2 = O.sac_segment(p, 0.05, max_iterations=100, normals=nrm)
+    assert np.array_equal(i2, r2["inliers"])
+    assert np.array_equal(c2.view(np.uint32), r2["coeff"].view(np.uint32))
+    cloud.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_np_loopback_sharded(gpu_ctx, world):
+    import dialog_amd as D
+    p, nrm, _, _ = cloud_with_normals(20000, seed=12)
+    prm = D.make_params(0.05, max_iterations=255, probability=1.0,
+                        model=D.SACMODEL_NORMAL_PLANE, normal_distance_weight=0.2)
+    cloud = D.Cloud(gpu_ctx, p)
+    cloud.set_normals(nrm)
+    ref = D.extract_planes(cloud, prm, max_planes=4, min_inliers=200)
+    cloud.close()
+    ctxs = D.Context.loopback_group(world, 0)
+    bounds = np.linspace(0, p.shape[0], world + 1).astype(np.int64)
+    out = [None] * world
+    errs = []
+
+    def run(r):
+        try:
+            c = D.Cloud(ctxs[r], p[bounds[r]:bounds[r + 1]], id_base=int(bounds[r]))
+            c.set_normals(nrm[bounds[r]:bounds[r + 1]])
+            out[r] = D.extract_planes(c, prm, max_planes=4, min_inliers=200, capacity=p.shape[0])
+            c.close()
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errs, errs
+    for r in range(world):
+        assert np.array_equal(out[r]["offsets"], ref["offsets"])
+        assert np.array_equal(out[r]["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
+        assert np.array_equal(out[r]["inliers"], ref["inliers"])
+    for c in ctxs:
+        c.close()
