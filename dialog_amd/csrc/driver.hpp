@@ -99,9 +99,9 @@ struct NormalsWork {
   static constexpr int kLevels = 12;
   GridLevelBufs lv[kLevels];
   DevBuf<uint8_t> raw, out, processed, processed_s, sort_tmp;
-  DevBuf<float> x, y, z, partial;
+  DevBuf<float> x, y, z, qx, qy, qz, partial;
   DevBuf<uint32_t> keys_in, keys_out, counters;
-  DevBuf<int32_t> idx_in, queue, cand, ids, ids_alt, pos_of;
+  DevBuf<int32_t> idx_in, queue, cand, ids, ids_alt, pos_of, nn;
   DevBuf<float4> nrm, nrm_s;
   DevBuf<uint32_t> claim;
   DevBuf<unsigned long long> keys64, keys_alt;
@@ -109,7 +109,8 @@ struct NormalsWork {
   void release() {
     for (auto& l : lv) l.release();
     raw.release(); out.release(); processed.release(); processed_s.release(); sort_tmp.release();
-    x.release(); y.release(); z.release(); partial.release();
+    x.release(); y.release(); z.release(); qx.release(); qy.release(); qz.release();
+    partial.release(); nn.release();
     keys_in.release(); keys_out.release(); counters.release();
     idx_in.release(); queue.release(); cand.release(); ids.release(); ids_alt.release();
     pos_of.release(); nrm.release(); nrm_s.release(); claim.release(); keys64.release(); keys_alt.release(); h_cnt.release();

@@ -386,6 +386,65 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
   normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
 }
 
+// nearest neighbour of external queries over the grid hierarchy (same level rule as
+// k_normals_knn with K = 1); a non-finite query gets nn = -1
+__global__ __launch_bounds__(kBS) void k_nn1(KnnLevels L, int l, const int32_t* __restrict__ qlist,
+                                             int nq, const float* __restrict__ QX,
+                                             const float* __restrict__ QY,
+                                             const float* __restrict__ QZ,
+                                             int32_t* __restrict__ nn, int32_t* __restrict__ next,
+                                             uint32_t* __restrict__ n_next) {
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= nq) return;
+  const int qi = qlist ? qlist[t] : t;
+  const float qx = QX[qi], qy = QY[qi], qz = QZ[qi];
+  if (!finite3(qx, qy, qz)) {
+    nn[qi] = -1;
+    return;
+  }
+  const GridDesc& G = L.G[l];
+  const bool top = l == L.levels - 1;
+  const float lim = top ? INFINITY : G.cell * G.cell;
+  float bd = INFINITY;
+  int bi = INT_MAX;
+  const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+  const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+  const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+  for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
+    for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
+      for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
+        const int2 rg = cell_range(L.tkeys[l], L.trange[l], L.tmask[l], cell_key(G, x, y, z));
+        for (int u = rg.x; u < rg.y; ++u) {
+          const float d2 = flann_d2(qx, qy, qz, L.sx[l][u], L.sy[l][u], L.sz[l][u]);
+          if (!(d2 < lim) || d2 > bd) continue;
+          const int iu = L.idx[l][u];
+          if (d2 < bd || iu < bi) { bd = d2; bi = iu; }
+        }
+      }
+  if (bi == INT_MAX && !top) {
+    next[atomicAdd(n_next, 1u)] = qi;
+    return;
+  }
+  nn[qi] = bi == INT_MAX ? -1 : bi;
+}
+
+// PlaneDetect.h:565-578: Eigen Vector3f dot (not vectorised: (a0 b0 + a1 b1) + a2 b2)
+__global__ __launch_bounds__(kBS) void k_flip_to_reference(float* __restrict__ nrm, int64_t stride,
+                                                           const float* __restrict__ ref,
+                                                           int64_t ref_stride,
+                                                           const int32_t* __restrict__ nn, int n) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const int j = nn[i];
+  if (j < 0) return;
+  float* a = nrm + (int64_t)i * stride;
+  const float* b = ref + (int64_t)j * ref_stride;
+  const float d = (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+  if (d < 0.0f) {
+    a[0] *= -1.0f; a[1] *= -1.0f; a[2] *= -1.0f;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // RegulateNormal BFS, one level per (claim, settle, order)
 // The BFS state lives in the grid's sorted order (position u of point sidx[u]): processed[],
@@ -586,6 +645,21 @@ void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qlist, int
   else
     hipLaunchKernelGGL(k_normals_knn<64>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
                        vp[2], normals, next, n_next);
+}
+
+void launch_nn1(const KnnLevels& L, int level, const int32_t* qlist, int nq, const float* qx,
+                const float* qy, const float* qz, int32_t* nn, int32_t* next, uint32_t* n_next,
+                hipStream_t s) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(k_nn1, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, L, level, qlist, nq, qx, qy, qz,
+                     nn, next, n_next);
+}
+
+void launch_flip_to_reference(float* nrm, int64_t stride_f, const float* ref, int64_t ref_stride_f,
+                              const int32_t* nn, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_flip_to_reference, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, nrm, stride_f, ref,
+                     ref_stride_f, nn, n);
 }
 
 void launch_bfs_prepare(const GridBufs& B, int n, const float4* nrm, float4* nrm_s, int32_t* pos_of,

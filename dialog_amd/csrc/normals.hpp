@@ -75,6 +75,15 @@ void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qlist, int
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
                         float4* normals, int32_t* next, uint32_t* n_next, hipStream_t s);
 
+// nearest neighbour (k = 1, ties -> lowest index) in the hierarchy's cloud of external queries
+// (qx, qy, qz)[qlist or 0..nq); unresolved queries go to next[] for the level above
+void launch_nn1(const KnnLevels& L, int level, const int32_t* qlist, int nq, const float* qx,
+                const float* qy, const float* qz, int32_t* nn, int32_t* next, uint32_t* n_next,
+                hipStream_t s);
+// nrm[i] *= -1 when Vector3f(nrm[i]).dot(Vector3f(ref[nn[i]])) < 0 (strided records)
+void launch_flip_to_reference(float* nrm, int64_t stride_f, const float* ref, int64_t ref_stride_f,
+                              const int32_t* nn, int n, hipStream_t s);
+
 // ---- RegulateNormal, level-synchronous BFS (state in the grid's sorted order) ----
 // queue[]: point ids in PCL queue order; the current level is queue[fbase, fbase + nf).
 // claim_s: min over claiming queue positions (init ~0); cand/ncand: first-claimed positions.

@@ -107,6 +107,55 @@ uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B) {
   return w.h_cnt.p[0];
 }
 
+// grid hierarchy over nw.x/y/z for k-nearest-neighbour queries (normals.hip, k_normals_knn):
+// level-0 cell guessed from the bounding volume, then resized once from the measured occupancy
+// so an occupied cell holds ~k/2 points (surface-like clouds: occupancy ~ cell^2); levels above
+// grow 2x until one has <= 2 cells per axis
+KnnLevels build_hierarchy(dlg_ctx* c, int n, const BBox& b, int k_nn) {
+  GridBufs B;
+  double ext[3], maxe = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    ext[k] = b.any ? (double)b.hi[k] - (double)b.lo[k] : 0.0;
+    maxe = std::max(maxe, ext[k]);
+  }
+  if (maxe <= 0.0) maxe = 1.0;
+  double vol = 1.0;
+  for (int k = 0; k < 3; ++k) vol *= std::max(ext[k], maxe * 1e-3);
+  double cell = std::cbrt(vol * k_nn / n);
+  GridDesc G = make_grid(b, cell);
+  const uint32_t occ = build_grid(c, n, G, 0, &B);
+  const double target = std::max(2.0, k_nn / 2.0);
+  const double avg = occ ? (double)n / occ : target;
+  if (avg > 2.0 * target || avg < 0.5 * target) {
+    cell *= std::sqrt(target / avg);
+    G = make_grid(b, cell);
+    build_grid(c, n, G, 0, &B);
+  }
+  KnnLevels L;
+  L.levels = 0;
+  const double top_cell = maxe * 0.75;  // floor(ext / cell) + 1 <= 2 on every axis
+  // 2x per level, more when the hierarchy would not fit kMaxLevels
+  const double fac = std::max(2.0, std::pow(top_cell / cell, 1.0 / (kMaxLevels - 1)));
+  for (int l = 0; l < kMaxLevels; ++l) {
+    const bool last = cell >= top_cell || l == kMaxLevels - 1;
+    if (last) cell = std::max(cell, top_cell);
+    GridBufs BL;
+    if (l == 0) {
+      BL = B;
+    } else {
+      G = make_grid(b, cell);
+      build_grid(c, n, G, l, &BL);
+    }
+    L.G[l] = G;
+    L.sx[l] = BL.sx; L.sy[l] = BL.sy; L.sz[l] = BL.sz; L.idx[l] = BL.idx_out;
+    L.tkeys[l] = BL.tkeys; L.trange[l] = BL.trange; L.tmask[l] = BL.tmask;
+    L.levels = l + 1;
+    if (last) break;
+    cell *= fac;
+  }
+  return L;
+}
+
 void check_points(const dlg_points* pts) {
   if (!pts || pts->n < 0 || (pts->n > 0 && !pts->xyz))
     throw DlgError(DLG_ERR_INVALID, "points: null or negative size");
@@ -137,49 +186,7 @@ void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
     const float r2 = (float)((double)radius * (double)radius);  // KdTreeFLANN: radius * radius
     launch_normals_radius(G, B, n, r2, vp, w.nrm.p, c->stream);
   } else {
-    // level-0 cell: guess from the bounding volume, then one resize from the measured occupancy
-    // so an occupied cell holds ~k/2 points (surface-like clouds: occupancy ~ cell^2); levels
-    // above grow 2x until one has <= 2 cells per axis (normals.hip, k_normals_knn)
-    double ext[3], maxe = 0.0;
-    for (int k = 0; k < 3; ++k) {
-      ext[k] = b.any ? (double)b.hi[k] - (double)b.lo[k] : 0.0;
-      maxe = std::max(maxe, ext[k]);
-    }
-    if (maxe <= 0.0) maxe = 1.0;
-    double vol = 1.0;
-    for (int k = 0; k < 3; ++k) vol *= std::max(ext[k], maxe * 1e-3);
-    double cell = std::cbrt(vol * k_nn / n);
-    GridDesc G = make_grid(b, cell);
-    const uint32_t occ = build_grid(c, n, G, 0, &B);
-    const double target = std::max(2.0, k_nn / 2.0);
-    const double avg = occ ? (double)n / occ : target;
-    if (avg > 2.0 * target || avg < 0.5 * target) {
-      cell *= std::sqrt(target / avg);
-      G = make_grid(b, cell);
-      build_grid(c, n, G, 0, &B);
-    }
-    KnnLevels L;
-    L.levels = 0;
-    const double top_cell = maxe * 0.75;  // floor(ext / cell) + 1 <= 2 on every axis
-    // 2x per level, more when the hierarchy would not fit kMaxLevels
-    const double fac = std::max(2.0, std::pow(top_cell / cell, 1.0 / (kMaxLevels - 1)));
-    for (int l = 0; l < kMaxLevels; ++l) {
-      const bool last = cell >= top_cell || l == kMaxLevels - 1;
-      if (last) cell = std::max(cell, top_cell);
-      GridBufs BL;
-      if (l == 0) {
-        BL = B;
-      } else {
-        G = make_grid(b, cell);
-        build_grid(c, n, G, l, &BL);
-      }
-      L.G[l] = G;
-      L.sx[l] = BL.sx; L.sy[l] = BL.sy; L.sz[l] = BL.sz; L.idx[l] = BL.idx_out;
-      L.tkeys[l] = BL.tkeys; L.trange[l] = BL.trange; L.tmask[l] = BL.tmask;
-      L.levels = l + 1;
-      if (last) break;
-      cell *= fac;
-    }
+    const KnnLevels L = build_hierarchy(c, n, b, k_nn);
     w.queue.ensure(n);
     w.cand.ensure(n);
     int32_t* qin = nullptr;
@@ -279,6 +286,61 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   return qt;
 }
 
+// regulateNormal() later-round branch (PlaneDetect.h:553-584): for every point of the current
+// cloud, its nearest neighbour in the backup cloud (KdTreeFLANN::nearestKSearch, k = 1); the
+// normal flips when Vector3f(n).dot(Vector3f(n_backup)) < 0
+void orient_normals_nn(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64_t stride,
+                       const dlg_points* ref, const float* ref_nrm, int64_t ref_stride) {
+  check_points(pts);
+  check_points(ref);
+  if (!nrm_io || (ref->n > 0 && !ref_nrm)) throw DlgError(DLG_ERR_INVALID, "normals are null");
+  if (stride < 12 || stride % 4 || ref_stride < 12 || ref_stride % 4)
+    throw DlgError(DLG_ERR_INVALID, "normal strides must be >= 12 and a multiple of 4");
+  const int n = (int)pts->n, m = (int)ref->n;
+  if (n == 0) return;
+  if (m == 0) throw DlgError(DLG_ERR_INVALID, "empty backup cloud");
+  NormalsWork& w = c->nw;
+  // queries: the current cloud (own buffers), grid: the backup cloud (nw.x/y/z)
+  w.qx.ensure(n); w.qy.ensure(n); w.qz.ensure(n);
+  {
+    const size_t bytes = (size_t)n * (size_t)pts->stride_bytes;
+    w.raw.ensure(bytes);
+    HIPCHK(hipMemcpyAsync(w.raw.p, pts->xyz, bytes, hipMemcpyHostToDevice, c->stream));
+    launch_deinterleave(reinterpret_cast<const float*>(w.raw.p), n, pts->stride_bytes / 4, w.qx.p,
+                        w.qy.p, w.qz.p, c->stream);
+  }
+  const BBox b = upload_points(c, ref);
+  const KnnLevels L = build_hierarchy(c, m, b, 1);
+  w.nn.ensure(n);
+  w.queue.ensure(n);
+  w.cand.ensure(n);
+  int32_t* qin = nullptr;
+  int32_t* qout = w.queue.p;
+  int nq = n;
+  for (int l = 0; l < L.levels && nq > 0; ++l) {
+    HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
+    launch_nn1(L, l, qin, nq, w.qx.p, w.qy.p, w.qz.p, w.nn.p, qout, w.counters.p, c->stream);
+    if (l == L.levels - 1) break;
+    HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    nq = (int)w.h_cnt.p[0];
+    qin = qout;
+    qout = qout == w.queue.p ? w.cand.p : w.queue.p;
+  }
+  // normals: current (in/out) and backup, raw strided records on the device
+  const size_t nbytes = (size_t)n * (size_t)stride, rbytes = (size_t)m * (size_t)ref_stride;
+  w.out.ensure(nbytes);
+  w.raw.ensure(rbytes);
+  HIPCHK(hipMemcpyAsync(w.out.p, nrm_io, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(w.raw.p, ref_nrm, rbytes, hipMemcpyHostToDevice, c->stream));
+  launch_flip_to_reference(reinterpret_cast<float*>(w.out.p), stride / 4,
+                           reinterpret_cast<const float*>(w.raw.p), ref_stride / 4, w.nn.p, n,
+                           c->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(nrm_io, w.out.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+}
+
 }  // namespace
 }  // namespace dlg
 
@@ -301,6 +363,15 @@ dlg_status dlg_regulate_normals(dlg_ctx* c, const dlg_points* pts, float* normal
     const int64_t k = regulate_normals(c, pts, normals_inout, stride_bytes, seed_idx,
                                        seed_is_outward, radius, processed_out);
     if (n_processed) *n_processed = k;
+  });
+}
+
+dlg_status dlg_orient_normals_nn(dlg_ctx* c, const dlg_points* pts, float* normals_inout,
+                                 int64_t stride_bytes, const dlg_points* ref_pts,
+                                 const float* ref_normals, int64_t ref_stride_bytes) {
+  if (!c) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    orient_normals_nn(c, pts, normals_inout, stride_bytes, ref_pts, ref_normals, ref_stride_bytes);
   });
 }
 

@@ -49,6 +49,23 @@ def regulate_normals(points, normals, seed_idx: int, seed_is_outward: bool, radi
     return nrm, proc.astype(bool), int(cnt.value)
 
 
+def orient_normals_nn(points, normals, ref_points, ref_normals, ctx: Context | None = None):
+    """regulateNormal() later-round branch (PlaneDetect.h:553-584): flip each normal to agree
+    with its nearest backup point's normal.  Returns a copy (columns 0..2 change)."""
+    ctx = ctx or default_context()
+    a, pts = _points(points)
+    r, rpts = _points(ref_points)
+    nrm = np.array(normals, dtype=np.float32, order="C", copy=True)
+    rn = np.ascontiguousarray(ref_normals, dtype=np.float32)
+    if nrm.ndim != 2 or nrm.shape[0] != a.shape[0] or nrm.shape[1] < 3:
+        raise ValueError("normals must be float32 [N, >=3] matching points")
+    if rn.ndim != 2 or rn.shape[0] != r.shape[0] or rn.shape[1] < 3:
+        raise ValueError("ref_normals must be float32 [M, >=3] matching ref_points")
+    ctx.check(_lib.load().dlg_orient_normals_nn(ctx.h, C.byref(pts), _f32p(nrm), 4 * nrm.shape[1],
+                                                C.byref(rpts), _f32p(rn), 4 * rn.shape[1]))
+    return nrm
+
+
 class NormalEstimation:
     """pcl::NormalEstimation(OMP)<PointXYZ, Normal> on the GPU."""
 

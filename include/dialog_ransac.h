@@ -184,6 +184,14 @@ dlg_status dlg_regulate_normals(dlg_ctx* ctx, const dlg_points* pts, float* norm
                                 int64_t stride_bytes, int64_t seed_idx, int seed_is_outward,
                                 float radius, uint8_t* processed_out, int64_t* n_processed);
 
+/* regulateNormal() later-round branch (PlaneDetect.h:553-584, !isFirstPostProcess): each point
+ * of pts takes the orientation of its nearest neighbour in the backup cloud ref_pts
+ * (KdTreeFLANN::nearestKSearch k = 1; equidistant neighbours -> lowest index): its normal flips
+ * when Vector3f(n).dot(Vector3f(n_ref)) < 0.  Only normal_x/y/z of normals_inout are written. */
+dlg_status dlg_orient_normals_nn(dlg_ctx* ctx, const dlg_points* pts, float* normals_inout,
+                                 int64_t stride_bytes, const dlg_points* ref_pts,
+                                 const float* ref_normals, int64_t ref_stride_bytes);
+
 /* ---- profiling ------------------------------------------------------------------------------ */
 /* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);

@@ -77,6 +77,8 @@ def lib():
         L.orc_normal_plane_dist.restype = C.c_double
         L.orc_estimate_normals.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, fp, fp]
         L.orc_estimate_normals_knn.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, fp, fp]
+        L.orc_orient_normals_nn.argtypes = [fp, C.c_int64, C.c_int64, fp, fp, C.c_int64,
+                                            C.c_int64, fp]
         L.orc_regulate_normals.argtypes = [fp, C.c_int64, C.c_int64, fp, C.c_int64, C.c_int,
                                            C.c_float, C.POINTER(C.c_uint8)]
         L.orc_regulate_normals.restype = C.c_int64
@@ -258,3 +260,15 @@ def regulate_normals(points, normals, seed_idx, seed_is_outward, radius):
                                      int(bool(seed_is_outward)), float(radius),
                                      proc.ctypes.data_as(C.POINTER(C.c_uint8)))
     return nrm, proc.astype(bool), int(cnt)
+
+
+def orient_normals_nn(points, normals, ref_points, ref_normals):
+    p, stride = _xyz(points)
+    r, rstride = _xyz(ref_points)
+    nrm = np.ascontiguousarray(normals, np.float32).copy()
+    rn = np.ascontiguousarray(ref_normals, np.float32)
+    assert nrm.shape == (p.shape[0], 4) and rn.shape == (r.shape[0], 4)
+    lib().orc_orient_normals_nn(_f(p), p.shape[0], stride, _f(nrm), _f(r), r.shape[0], rstride,
+                                _f(rn))
+    return nrm
+

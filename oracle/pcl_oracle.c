@@ -727,3 +727,28 @@ int64_t orc_regulate_normals(const float* xyz, int64_t n, int64_t stride, float*
   orc_grid_free(&G);
   return cnt;
 }
+
+/* Dialog/PlaneDetect.h:553-584 (later-round branch of regulateNormal): nearest neighbour of each
+ * point in the backup cloud (FLANN L2 dist2, k = 1; equidistant -> lowest index), flip when the
+ * Vector3f dot (a0 b0 + a1 b1) + a2 b2 is negative.  Brute force: test-sized clouds only. */
+void orc_orient_normals_nn(const float* xyz, int64_t n, int64_t stride, float* normals,
+                           const float* ref_xyz, int64_t m, int64_t ref_stride,
+                           const float* ref_normals) {
+  for (int64_t i = 0; i < n; ++i) {
+    const float* q = xyz + i * stride;
+    float bd = INFINITY;
+    int64_t bj = -1;
+    for (int64_t j = 0; j < m; ++j) {
+      const float* p = ref_xyz + j * ref_stride;
+      float ex = q[0] - p[0], ey = q[1] - p[1], ez = q[2] - p[2];
+      float d = ((0.0f + ex * ex) + ey * ey) + ez * ez;
+      if (d < bd) { bd = d; bj = j; }
+    }
+    if (bj < 0) continue;
+    float* a = normals + 4 * i;
+    const float* b = ref_normals + 4 * bj;
+    float dd = (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+    if (dd < 0.0f) { a[0] *= -1.0f; a[1] *= -1.0f; a[2] *= -1.0f; }
+  }
+}
+

@@ -117,6 +117,11 @@ int64_t orc_regulate_normals(const float* xyz, int64_t n, int64_t stride, float*
                              int64_t seed_idx, int seed_is_outward, float radius,
                              uint8_t* processed_out);
 
+/* PlaneDetect.h:553-584: orientation from the nearest backup point (normals: 4 floats/point) */
+void orc_orient_normals_nn(const float* xyz, int64_t n, int64_t stride, float* normals,
+                           const float* ref_xyz, int64_t m, int64_t ref_stride,
+                           const float* ref_normals);
+
 #ifdef __cplusplus
 }
 #endif

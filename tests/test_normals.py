@@ -286,3 +286,42 @@ def test_gpu_normals_large_cloud_properties(gpu_ctx):
         m = lab == k
         assert np.median(np.abs(gk[m, :3] @ planes[k, :3])) > 0.99
     print(json.dumps({"normals_1M_radius_s": round(dt, 3)}))
+
+
+def test_oracle_orient_nn_semantics():
+    """later-round branch: normal flips iff its dot with the nearest backup normal is < 0."""
+    p, _, _ = small_cloud(1500, seed=21)
+    nrm = O.estimate_normals(p, RADIUS)
+    ref = p[::3] + np.float32(1e-3)
+    rn = O.estimate_normals(ref, 0.2)
+    out = O.orient_normals_nn(p, nrm, ref, rn)
+    d2 = ((p[:, None, :].astype(np.float64) - ref[None, :, :]) ** 2).sum(-1)
+    j = d2.argmin(1)
+    dot = np.sum(nrm[:, :3] * rn[j, :3], axis=1)
+    flip = dot < 0
+    np.testing.assert_array_equal(out[flip, :3], -nrm[flip, :3])
+    np.testing.assert_array_equal(out[~flip], nrm[~flip])
+
+
+@pytest.mark.gpu
+def test_gpu_orient_nn_bit_exact(gpu_ctx, cloud):
+    import dialog_amd as D
+    p, _, _ = cloud
+    nrm = O.estimate_normals(p, RADIUS)
+    rng = np.random.default_rng(4)
+    nrm[:, :3] *= np.where(rng.random(len(p)) < 0.5, -1.0, 1.0).astype(np.float32)[:, None]
+    # backup: a perturbed, subsampled copy with its own normals (the previous round's cloud)
+    ref = (p[::2] + rng.normal(0, 0.003, size=(len(p[::2]), 3))).astype(np.float32)
+    rn = O.estimate_normals(ref, 0.15)
+    rn[np.isnan(rn)] = 0.0
+    o = O.orient_normals_nn(p, nrm, ref, rn)
+    g = D.orient_normals_nn(p, nrm, ref, rn, ctx=gpu_ctx)
+    np.testing.assert_array_equal(g, o)
+    # pcl::Normal stride (8 floats) in and out
+    n8 = np.zeros((len(p), 8), np.float32)
+    n8[:, :3] = nrm[:, :3]
+    n8[:, 4] = nrm[:, 3]
+    g8 = D.orient_normals_nn(np.c_[p, np.ones(len(p), np.float32)], n8, ref, rn, ctx=gpu_ctx)
+    np.testing.assert_array_equal(g8[:, :3], o[:, :3])
+    np.testing.assert_array_equal(g8[:, 4], nrm[:, 3])
+
