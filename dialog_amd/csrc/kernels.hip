@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 namespace dlg {
 
@@ -879,80 +880,125 @@ __global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src, float
   }
 }
 
-// k_score_np: counts[h] for SACMODEL_NORMAL_PLANE.  Same tiling as k_score (hypotheses in LDS,
-// P points per lane, ballot counts parked by writelane); per point the weight w and 1 - w are
-// computed once per launch.  The exact prefilter rejects every point with (1 - w) d_euclid >=
-// thr using one float dot and one double multiply; the acos path runs only for waves that have a
-// point near the plane.
-constexpr int kNpP = 4;
+// k_score_np: counts[h] for SACMODEL_NORMAL_PLANE.
+//
+// Per point the exact prefilter b = (1 - w) d_euclid < thr becomes one float compare: b is
+// fl(omw * de) with omw fixed per point, monotone in de, so b < thr <=> de < lim where lim is the
+// smallest float with fl(omw * lim) >= thr (found once per point per launch; lim = +inf when the
+// prefilter does not apply: w < 0 or NaN, or omw <= 0).  The per-test cost is then the plane
+// model's: 3 mul + 3 add + compare.  Points that pass go, with their b and the hypothesis, into a
+// per-wave LDS queue; every 64 queued pairs are evaluated with full lanes (normalised-normal dot,
+// clamp, acos, min(a, pi - a), weighted sum -- all in PCL's order) and counted with LDS atomics,
+// so the double-precision acos path never runs in a mostly idle wavefront.
+constexpr int kNpBS = 256;
+constexpr int kNpWaves = kNpBS / kWave;
+constexpr int kNpQ = 128;
 
-__global__ __launch_bounds__(kScBS) void k_score_np(PointsView src, const HypRec* __restrict__ hyps,
+__device__ float np_de_limit(double w, double thr) {
+  if (!(w >= 0.0)) return INFINITY;
+  const double omw = 1.0 - w;
+  if (!(omw > 0.0)) return INFINITY;
+  if (!(thr > 0.0)) return thr == thr ? 0.0f : __builtin_nanf("");
+  float x = (float)(thr / omw);
+  if (!(x == x)) return INFINITY;
+  while (!(omw * (double)x >= thr) && x < INFINITY) x = nextafterf(x, INFINITY);
+  while (x > 0.0f) {
+    const float y = nextafterf(x, -INFINITY);
+    if (omw * (double)y >= thr) x = y;
+    else break;
+  }
+  return x;
+}
+
+template <int kNpP, int kNpHT>
+__global__ __launch_bounds__(kNpBS) void k_score_np(PointsView src, const HypRec* __restrict__ hyps,
                                                     int D, double lambda, double thr,
                                                     int32_t* __restrict__ counts) {
-  constexpr int kChunk = kScBS * kNpP;
-  __shared__ float4 s_coef[kHT];
-  __shared__ float4 s_cn[kHT];
+  constexpr int kChunk = kNpBS * kNpP;
+  __shared__ float4 s_coef[kNpHT + 1];
+  __shared__ float4 s_cn[kNpHT];
   __shared__ int s_cnt[kMaxHypPerLaunch];
+  __shared__ float4 s_pts[kNpWaves][kNpP * kWave];  // (n.normalized(), curvature) of the chunk
+  __shared__ uint32_t s_qk[kNpWaves][kNpQ];         // point slot | tile-local hypothesis << 8
+  __shared__ double s_qb[kNpWaves][kNpQ];           // b = (1 - w) d_euclid
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
-  for (int i = tid; i < D; i += kScBS) s_cnt[i] = 0;
+  const int wv = tid / kWave;
+  for (int i = tid; i < D; i += kNpBS) s_cnt[i] = 0;
   const int64_t n = src.n;
   const int64_t nchunks = (n + kChunk - 1) / kChunk;
   const float qnan = __builtin_nanf("");
   for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    float px[kNpP], py[kNpP], pz[kNpP];
-    float4 pn[kNpP];
-    double pw[kNpP], pomw[kNpP];
+    float px[kNpP], py[kNpP], pz[kNpP], lim[kNpP];
+    double omw[kNpP];
 #pragma unroll
     for (int j = 0; j < kNpP; ++j) {
-      const int64_t e = ch * kChunk + j * kScBS + tid;
+      const int64_t e = ch * kChunk + (int64_t)wv * (kNpP * kWave) + j * kWave + lane;
       const bool ok = e < n;
       px[j] = ok ? src.x[e] : qnan;
       py[j] = ok ? src.y[e] : qnan;
       pz[j] = ok ? src.z[e] : qnan;
-      pn[j] = ok ? src.nrm[e] : make_float4(0.f, 0.f, 0.f, 1.f);
-      pw[j] = ok ? lambda * (1.0 - (double)pn[j].w) : 0.0;
-      pomw[j] = 1.0 - pw[j];
+      const float4 nn = ok ? src.nrm[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const double w = lambda * (1.0 - (double)nn.w);
+      omw[j] = 1.0 - w;
+      lim[j] = ok ? np_de_limit(w, thr) : 0.0f;
+      s_pts[wv][j * kWave + lane] = nn;
     }
-    for (int t0 = 0; t0 < D; t0 += kHT) {
-      const int nt = min(kHT, D - t0);
+    for (int t0 = 0; t0 < D; t0 += kNpHT) {
+      const int nt = min(kNpHT, D - t0);
       __syncthreads();
-      for (int i = tid; i < nt; i += kScBS) {
+      for (int i = tid; i < nt; i += kNpBS) {
         const HypRec hr = hyps[t0 + i];
         s_coef[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
         s_cn[i] = eigen_normalized3(hr.a, hr.b, hr.c, 0.0f);
       }
       __syncthreads();
-      for (int g0 = 0; g0 < nt; g0 += kWave) {  // nt is a multiple of 64 (NaN-padded)
-        int my = 0;
-        for (int k = 0; k < kWave; ++k) {
-          const float4 c = s_coef[g0 + k];
-          double b[kNpP];
-          bool near = false;
-#pragma unroll
-          for (int j = 0; j < kNpP; ++j) {
-            b[j] = pomw[j] * (double)np_deuclid(c, px[j], py[j], pz[j]);
-            near |= (b[j] < thr) || !(pw[j] >= 0.0);
-          }
-          int cnt = 0;
-          if (ballot(near)) {
-            const float4 cn = s_cn[g0 + k];
-#pragma unroll
-            for (int j = 0; j < kNpP; ++j) {
-              const bool cand = (b[j] < thr) || !(pw[j] >= 0.0);
-              bool in = false;
-              if (cand) in = np_full(cn, pn[j], pw[j], b[j], thr);
-              cnt += __popcll(ballot(in));
-            }
-          }
-          my = writelane(my, cnt, k);
+      int qn = 0;  // wave-uniform queue length
+      auto drain = [&](int m) {  // evaluate the first m queued pairs, keep the rest
+        __builtin_amdgcn_wave_barrier();  // queue writes of other lanes precede these reads
+        if (lane < m) {
+          const uint32_t e = s_qk[wv][lane];
+          const float4 nn = s_pts[wv][e & 255u];
+          const int kk = (int)(e >> 8);
+          const double w = lambda * (1.0 - (double)nn.w);
+          if (np_full(s_cn[kk], nn, w, s_qb[wv][lane], thr)) atomicAdd(&s_cnt[t0 + kk], 1);
         }
-        atomicAdd(&s_cnt[t0 + g0 + lane], my);
+        const int rest = qn - m;
+        uint32_t mk = 0;
+        double mb = 0.0;
+        if (lane < rest) {
+          mk = s_qk[wv][m + lane];
+          mb = s_qb[wv][m + lane];
+        }
+        if (lane < rest) {
+          s_qk[wv][lane] = mk;
+          s_qb[wv][lane] = mb;
+        }
+        qn = rest;
+      };
+      float4 cnext = s_coef[0];  // software pipeline: next plane's LDS read in flight
+      for (int k = 0; k < nt; ++k) {
+        const float4 c = cnext;
+        cnext = s_coef[k + 1];
+#pragma unroll
+        for (int j = 0; j < kNpP; ++j) {
+          const float de = np_deuclid(c, px[j], py[j], pz[j]);
+          const bool near = de < lim[j];
+          const uint64_t m = ballot(near);
+          if (near) {
+            const int pos = qn + lanes_below(m);
+            s_qk[wv][pos] = (uint32_t)(j * kWave + lane) | ((uint32_t)k << 8);
+            s_qb[wv][pos] = omw[j] * (double)de;
+          }
+          qn += __popcll(m);
+          if (qn >= kWave) drain(kWave);
+        }
       }
+      if (qn > 0) drain(qn);  // the tile's coefficients are replaced next
     }
   }
   __syncthreads();
-  for (int i = tid; i < D; i += kScBS) {
+  for (int i = tid; i < D; i += kNpBS) {
     const int v = s_cnt[i];
     if (v) atomicAdd(&counts[i], v);
   }
@@ -1153,11 +1199,31 @@ void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest&
                      int32_t* counts, int num_cus, hipStream_t s) {
   if (D <= 0 || src.n <= 0) return;
   const int Dp = (D + kWave - 1) / kWave * kWave;
-  const int64_t chunks = (src.n + (int64_t)kScBS * kNpP - 1) / ((int64_t)kScBS * kNpP);
-  const int64_t cap = (int64_t)num_cus * 2;
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(chunks, cap));
-  hipLaunchKernelGGL(k_score_np, dim3(grid), dim3(kScBS), 0, s, src, hyps, Dp, mt.lambda, mt.thr,
-                     counts);
+  static const int variant = [] {
+    const char* e = std::getenv("DLG_NP_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  auto go = [&](auto kern, int P, int per_cu) {
+    const int64_t chunks = (src.n + (int64_t)kNpBS * P - 1) / ((int64_t)kNpBS * P);
+    const int64_t cap = (int64_t)num_cus * per_cu;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(chunks, cap));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kNpBS), 0, s, src, hyps, Dp, mt.lambda, mt.thr,
+                       counts);
+  };
+  // LDS per block: 16 KB counts + 32 B x HT planes + 4 KB x P point normals + 6 KB queue.
+  // Measured on C5 (10M points, 4096 planes/launch; tools/bench_c5.py, DLG_NP_VARIANT):
+  // <2,256> x4/CU 2.55 T tests/s > <2,128> 2.50 > <2,64> 2.43 > <4,256> x3 2.40 > <1,256> 2.21 >
+  // <4,512>, <8,256>, <4,1024> x2 1.69-1.73 (occupancy-bound: 2 waves/SIMD)
+  switch (variant) {
+    case 1: go(k_score_np<4, 1024>, 4, 2); break;
+    case 2: go(k_score_np<8, 256>, 8, 2); break;
+    case 3: go(k_score_np<4, 512>, 4, 2); break;
+    case 4: go(k_score_np<4, 256>, 4, 3); break;
+    case 5: go(k_score_np<2, 128>, 2, 4); break;
+    case 6: go(k_score_np<1, 256>, 1, 4); break;
+    case 7: go(k_score_np<2, 64>, 2, 4); break;
+    default: go(k_score_np<2, 256>, 2, 4); break;
+  }
 }
 
 void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,
