@@ -26,6 +26,7 @@ for s in $STEPS; do
     normals) run normals_gpu 600 python3 -m pytest tests/test_normals.py -m gpu -x -q -rA ;;
     nbench) run nbench 600 python3 tools/bench_normals.py ;;
     c5)     run c5 600 python3 tools/bench_c5.py ;;
+    c5prof) run c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof -o run -- python3 tools/bench_c5.py 10000000 2 ;;
     nprof)  run nprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nprof -o run -- python3 tools/bench_normals.py 10000000 2 ;;
     trace)  DLG_TRACE=1 run trace 300 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     benchtorch) run bench_torch 600 python3 bench.py --torch-dist --no-cpu-baseline --steps 2 ;;
