@@ -7,7 +7,12 @@
 //     Dialog/SimplifyVerticesSize.cpp:62-67, :86-87 -> dialog::SACSegmentation<PointT>;
 //   * the plane-stage slot of Dialog/PlaneDetect.h:667-1355 that fills
 //     `plane_clouds` (PlaneDetect.h:100, struct Plane HeaderFile.h:81-88) ->
-//     dialog::extractPlanes(cloud, params, planes) (sequential extract-and-remove RANSAC).
+//     dialog::extractPlanes(cloud, params, planes) (sequential extract-and-remove RANSAC);
+//   * pcl::SACSegmentationFromNormals (SACMODEL_NORMAL_PLANE) -> dialog::SACSegmentationFromNormals;
+//   * estimateNormal() (PlaneDetect.h:515-545, pcl::NormalEstimationOMP with a radius; k = 20 at
+//     PCLViewer.cpp:507-522) -> dialog::NormalEstimation<PointT, pcl::Normal>;
+//   * regulateNormal() (PlaneDetect.h:547-665) -> dialog::regulateNormals (first round) and
+//     dialog::orientNormalsToBackup (later rounds).
 // With real PCL available define DIALOG_HAVE_PCL before including; otherwise minimal
 // layout-identical stand-ins for pcl::PointXYZ (16 B), pcl::Normal (32 B), pcl::PointCloud,
 // pcl::ModelCoefficients and pcl::PointIndices are declared here.
@@ -148,7 +153,7 @@ class SACSegmentation {
     coefficients.values.assign(coeff, coeff + 4);
   }
 
- private:
+ protected:
   Context* ctx_;
   dlg_sac_params prm_;
   dlg_sac_stats stats_{};
@@ -157,6 +162,137 @@ class SACSegmentation {
   bool has_idx_ = false;
   int model_ = -1, method_ = -1;
 };
+
+// pcl::SACSegmentationFromNormals<PointT, pcl::Normal>: SACMODEL_NORMAL_PLANE (or PLANE) with the
+// input normals (one pcl::Normal per input point; setIndices selects from both)
+template <typename PointT, typename PointNT = pcl::Normal>
+class SACSegmentationFromNormals : public SACSegmentation<PointT> {
+ public:
+  typedef typename pcl::PointCloud<PointNT>::ConstPtr NormalsConstPtr;
+  explicit SACSegmentationFromNormals(Context* ctx = nullptr) : SACSegmentation<PointT>(ctx) {}
+  void setInputNormals(const NormalsConstPtr& normals) { normals_ = normals; }
+  void setNormalDistanceWeight(double w) { weight_ = w; }
+
+  void segment(pcl::PointIndices& inliers, pcl::ModelCoefficients& coefficients) {
+    if (this->model_ != pcl::SACMODEL_NORMAL_PLANE) {
+      SACSegmentation<PointT>::segment(inliers, coefficients);
+      return;
+    }
+    inliers.indices.clear();
+    coefficients.values.clear();
+    if (!this->input_ || !normals_ || normals_->points.size() != this->input_->points.size()) {
+      std::fprintf(stderr, "[dialog::SACSegmentationFromNormals::segment] No input dataset containing normals was given!\n");
+      return;
+    }
+    if (this->method_ != pcl::SAC_RANSAC) {
+      std::fprintf(stderr, "[dialog::SACSegmentationFromNormals::segment] Error initializing the SAC model!\n");
+      return;
+    }
+    dlg_ctx* c = (this->ctx_ ? this->ctx_ : &Context::thread_default())->get();
+    dlg_points pts{this->input_->points.empty() ? nullptr : &this->input_->points[0].x,
+                   (int64_t)this->input_->points.size(), (int64_t)sizeof(PointT)};
+    std::vector<int32_t> idx32(this->indices_.begin(), this->indices_.end());
+    const int64_t n = this->has_idx_ ? (int64_t)idx32.size() : pts.n;
+    dlg_cloud* cl = nullptr;
+    check(dlg_cloud_upload(c, &pts, this->has_idx_ ? idx32.data() : nullptr, n, 0, &cl), c);
+    std::unique_ptr<dlg_cloud, dlg_status (*)(dlg_cloud*)> guard(cl, dlg_cloud_destroy);
+    check(dlg_cloud_set_normals(c, cl, normals_->points.empty() ? nullptr : &normals_->points[0].normal_x,
+                                (int64_t)normals_->points.size(), (int64_t)sizeof(PointNT)),
+          c);
+    dlg_sac_params prm = this->prm_;
+    prm.model = DLG_SACMODEL_NORMAL_PLANE;
+    prm.normal_distance_weight = weight_;
+    std::vector<int32_t> out((size_t)(n > 0 ? n : 1));
+    float coeff[4];
+    int64_t nin = 0;
+    check(dlg_sac_segment(c, cl, &prm, coeff, out.data(), (int64_t)out.size(), &nin, &this->stats_), c);
+    if (!this->stats_.has_model) {
+      std::fprintf(stderr, "[dialog::SACSegmentationFromNormals::segment] Error segmenting the model! No solution found.\n");
+      return;
+    }
+    inliers.indices.assign(out.begin(), out.begin() + nin);
+    coefficients.values.assign(coeff, coeff + 4);
+  }
+
+ private:
+  NormalsConstPtr normals_;
+  double weight_ = 0.1;  // PCL default distance_weight_
+};
+
+// pcl::NormalEstimation(OMP)<PointT, pcl::Normal> (estimateNormal(), PlaneDetect.h:515-545)
+template <typename PointT, typename PointNT = pcl::Normal>
+class NormalEstimation {
+ public:
+  typedef typename pcl::PointCloud<PointT>::ConstPtr PointCloudConstPtr;
+  explicit NormalEstimation(Context* ctx = nullptr) : ctx_(ctx) {}
+  void setInputCloud(const PointCloudConstPtr& cloud) { input_ = cloud; }
+  void setRadiusSearch(double r) { radius_ = r; k_ = 0; }
+  void setKSearch(int k) { k_ = k; radius_ = 0.0; }
+  void setViewPoint(float vx, float vy, float vz) { vp_[0] = vx; vp_[1] = vy; vp_[2] = vz; }
+  // output: one PointNT per input point (NaN normal/curvature where < 3 neighbours)
+  void compute(pcl::PointCloud<PointNT>& output) {
+    output.points.clear();
+    if (!input_) {
+      std::fprintf(stderr, "[dialog::NormalEstimation::compute] No input dataset given!\n");
+      return;
+    }
+    output.points.resize(input_->points.size());
+    output.width = (uint32_t)output.points.size();
+    output.height = 1;
+    if (output.points.empty()) return;
+    dlg_ctx* c = (ctx_ ? ctx_ : &Context::thread_default())->get();
+    dlg_points pts{&input_->points[0].x, (int64_t)input_->points.size(), (int64_t)sizeof(PointT)};
+    check(dlg_estimate_normals(c, &pts, (float)radius_, k_, vp_, &output.points[0].normal_x,
+                               (int64_t)sizeof(PointNT)),
+          c);
+  }
+
+ private:
+  Context* ctx_;
+  PointCloudConstPtr input_;
+  double radius_ = 0.0;
+  int k_ = 0;
+  float vp_[3] = {0.f, 0.f, 0.f};
+};
+
+// regulateNormal() first round (PlaneDetect.h:586-646): returns the number of points reached;
+// processed (optional) receives isProcessed[]
+template <typename PointT, typename PointNT>
+inline int64_t regulateNormals(const pcl::PointCloud<PointT>& cloud, pcl::PointCloud<PointNT>& normals,
+                               int64_t selected_point_index, bool is_norm_direction_valid,
+                               float r_for_regulate_normal, std::vector<uint8_t>* processed = nullptr,
+                               Context* ctx = nullptr) {
+  if (normals.points.size() != cloud.points.size()) throw Error(DLG_ERR_INVALID, "normals/cloud size mismatch");
+  if (cloud.points.empty()) return 0;
+  dlg_ctx* c = (ctx ? ctx : &Context::thread_default())->get();
+  dlg_points pts{&cloud.points[0].x, (int64_t)cloud.points.size(), (int64_t)sizeof(PointT)};
+  if (processed) processed->assign(cloud.points.size(), 0);
+  int64_t count = 0;
+  check(dlg_regulate_normals(c, &pts, &normals.points[0].normal_x, (int64_t)sizeof(PointNT),
+                             selected_point_index, is_norm_direction_valid ? 1 : 0,
+                             r_for_regulate_normal, processed ? processed->data() : nullptr, &count),
+        c);
+  return count;
+}
+
+// regulateNormal() later rounds (PlaneDetect.h:553-584): orientation from the nearest point of
+// the backup cloud
+template <typename PointT, typename PointNT>
+inline void orientNormalsToBackup(const pcl::PointCloud<PointT>& cloud, pcl::PointCloud<PointNT>& normals,
+                                  const pcl::PointCloud<PointT>& backup,
+                                  const pcl::PointCloud<PointNT>& backup_normals, Context* ctx = nullptr) {
+  if (normals.points.size() != cloud.points.size() || backup_normals.points.size() != backup.points.size())
+    throw Error(DLG_ERR_INVALID, "normals/cloud size mismatch");
+  if (cloud.points.empty()) return;
+  dlg_ctx* c = (ctx ? ctx : &Context::thread_default())->get();
+  dlg_points pts{&cloud.points[0].x, (int64_t)cloud.points.size(), (int64_t)sizeof(PointT)};
+  dlg_points ref{backup.points.empty() ? nullptr : &backup.points[0].x, (int64_t)backup.points.size(),
+                 (int64_t)sizeof(PointT)};
+  check(dlg_orient_normals_nn(c, &pts, &normals.points[0].normal_x, (int64_t)sizeof(PointNT), &ref,
+                              backup_normals.points.empty() ? nullptr : &backup_normals.points[0].normal_x,
+                              (int64_t)sizeof(PointNT)),
+        c);
+}
 
 // Result of the plane stage for one plane: coefficients (a, b, c, d) and inlier ids.  The
 // reference's struct Plane (HeaderFile.h:81-88) is filled from it by copying the inlier points
@@ -173,6 +309,9 @@ struct ExtractParams {
   int max_iterations = 1000;
   double probability = 0.99;
   int refit_mode = DLG_REFIT_PCL;
+  // SACMODEL_NORMAL_PLANE when set: one pcl::Normal per cloud point
+  const pcl::PointCloud<pcl::Normal>* normals = nullptr;
+  double normal_distance_weight = 0.1;
 };
 
 template <typename PointT>
@@ -187,6 +326,13 @@ inline dlg_extract_stats extractPlanes(const pcl::PointCloud<PointT>& cloud, con
   std::unique_ptr<dlg_cloud, dlg_status (*)(dlg_cloud*)> guard(cl, dlg_cloud_destroy);
   dlg_sac_params prm;
   dlg_sac_params_default(&prm);
+  if (ep.normals) {
+    check(dlg_cloud_set_normals(c, cl, ep.normals->points.empty() ? nullptr : &ep.normals->points[0].normal_x,
+                                (int64_t)ep.normals->points.size(), (int64_t)sizeof(pcl::Normal)),
+          c);
+    prm.model = DLG_SACMODEL_NORMAL_PLANE;
+    prm.normal_distance_weight = ep.normal_distance_weight;
+  }
   prm.threshold = ep.threshold;
   prm.max_iterations = ep.max_iterations;
   prm.probability = ep.probability;

@@ -30,6 +30,27 @@ int main(int argc, char** argv) {
     ep.min_inliers = 100;
     dialog::extractPlanes(*cloud, ep, planes);
     std::printf("planes %zu\n", planes.size());
+    // normals stage: estimateNormal() + regulateNormal(), then the normal-plane model
+    pcl::PointCloud<pcl::Normal>::Ptr normals(new pcl::PointCloud<pcl::Normal>);
+    dialog::NormalEstimation<pcl::PointXYZ, pcl::Normal> ne;
+    ne.setInputCloud(cloud);
+    ne.setRadiusSearch(0.25);
+    ne.compute(*normals);
+    std::vector<uint8_t> processed;
+    int64_t reached = dialog::regulateNormals(*cloud, *normals, 0, true, 0.25f, &processed);
+    dialog::orientNormalsToBackup(*cloud, *normals, *cloud, *normals);
+    dialog::SACSegmentationFromNormals<pcl::PointXYZ, pcl::Normal> segn;
+    segn.setModelType(pcl::SACMODEL_NORMAL_PLANE);
+    segn.setMethodType(pcl::SAC_RANSAC);
+    segn.setDistanceThreshold(0.05);
+    segn.setNormalDistanceWeight(0.1);
+    segn.setInputCloud(cloud);
+    segn.setInputNormals(normals);
+    pcl::PointIndices inl_n;
+    pcl::ModelCoefficients coeff_n;
+    segn.segment(inl_n, coeff_n);
+    std::printf("normals %zu reached %lld np_inliers %zu\n", normals->points.size(), (long long)reached,
+                inl_n.indices.size());
     return 0;
   } catch (const dialog::Error& e) {
     std::fprintf(stderr, "dialog error: %s\n", e.what());

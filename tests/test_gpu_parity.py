@@ -235,6 +235,9 @@ def test_cpp_shim_runs_on_gpu(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.startswith("coeff ")
+    lines = dict(ln.split(" ", 1) for ln in out.stdout.strip().splitlines())
+    nrm = lines["normals"].split()
+    assert int(nrm[0]) == 64 * 64 + 500 and int(nrm[2]) > 0 and int(nrm[4]) > 0
 
 
 def test_rccl_one_rank_path(monkeypatch, gpu_ctx):
