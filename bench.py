@@ -50,7 +50,56 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--torch-dist", action="store_true",
                     help="rendezvous through torch.distributed even at N=1 (runtime check)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the C5 (normals + NORMAL_PLANE) secondary measurement")
     return ap.parse_args()
+
+
+def c5_secondary(D, ctx, a):
+    """BASELINE.json configs[4] (C5), reported beside the headline (not `value`): 10M points,
+    k = 20 normals and radius normals on the GPU, then SACMODEL_NORMAL_PLANE extract-and-remove
+    (weight 0.1) with the C3 RANSAC settings; plus RegulateNormal over the same cloud."""
+    from dialog_amd.synth import SEED_BASE, plane_cloud
+    pts, _, _ = plane_cloud(a.points, a.planes, seed=SEED_BASE + 5)
+    out = {"workload": "C5: 10M-pt 20-plane cloud, k=20 normals, NORMAL_PLANE (w=0.1) extract",
+           "points": a.points}
+
+    def timed(f, reps=2):
+        f()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = f()
+        ctx.synchronize()
+        return r, (time.perf_counter() - t0) / reps * 1e3
+
+    nrm, out["normals_knn20_ms"] = timed(lambda: D.estimate_normals(pts, k=20, ctx=ctx))
+    rn, out["normals_radius0.1_ms"] = timed(lambda: D.estimate_normals(pts, radius=0.1, ctx=ctx))
+    reg, out["regulate_r0.1_ms"] = timed(lambda: D.regulate_normals(pts, rn, 0, True, 0.1, ctx=ctx), 1)
+    out["regulate_reached"] = reg[2]
+    cloud = D.Cloud(ctx, pts)
+    cloud.set_normals(nrm)
+    prm = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
+                        refit_mode=D.DLG_REFIT_FAST, hypotheses_per_launch=a.hyps,
+                        gather_inliers=False, model=D.SACMODEL_NORMAL_PLANE,
+                        normal_distance_weight=0.1)
+
+    def step():
+        cloud.reset()
+        return D.extract_planes(cloud, prm, max_planes=a.planes, min_inliers=a.min_inliers,
+                                capacity=a.points)
+
+    e, ms = timed(step)
+    st = e["stats"]
+    out.update({"np_extract_ms": round(ms, 2), "np_planes": e["n_planes"],
+                "np_value": round(st["tests"] / (ms / 1e3) / 1e9, 3),
+                "np_unit": "G point-plane tests/s",
+                "np_kernel_tests_per_s": round(st["tests_scored"] / (st["score_ms"] / 1e3) / 1e9, 3)
+                if st["score_ms"] else None})
+    for k in ("normals_knn20_ms", "normals_radius0.1_ms", "regulate_r0.1_ms"):
+        out[k] = round(out[k], 2)
+    cloud.close()
+    return out
 
 
 def main():
@@ -153,6 +202,10 @@ def main():
         except Exception:
             pass
 
+    secondary = None
+    if world == 1 and not a.no_secondary:
+        secondary = c5_secondary(D, ctx, a)
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O
@@ -183,6 +236,7 @@ def main():
                        "parallelism": f"point-sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "secondary": secondary,
             "tests_per_step": tests // max(a.steps, 1),
             "tests_scored_per_step": scored // max(a.steps, 1),
             "score_ms_per_step_max_rank": round(score_ms_max / a.steps, 3),

@@ -12,6 +12,7 @@
 
 constexpr int ITER = 2048;
 constexpr int NA = 16;
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void stamp(unsigned long long* clk, int which) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -42,6 +43,18 @@ __global__ __launch_bounds__(256) void k_body(const float* in, float* out, int* 
       if (OP == 4) {                                              // v_add + v_cmp(vcc) + v_addc
         a[k] = a[k] + b;
         cnt += fabsf(a[k]) < thr ? 1 : 0;
+      }
+    }
+    if (OP >= 5) {  // packed f32 on register pairs (a[2i], a[2i+1])
+#pragma unroll
+      for (int k = 0; k < NA; k += 2) {
+        v2f x = {a[k], a[k + 1]};
+        v2f y = {b, c};
+        if (OP == 5) asm volatile("v_pk_mul_f32 %0, %1, %2" : "=v"(x) : "v"(x), "v"(y));
+        if (OP == 6) asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(x) : "v"(x), "v"(y));
+        if (OP == 7) asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(x) : "v"(x), "v"(y), "v"(y));
+        a[k] = x.x;
+        a[k + 1] = x.y;
       }
     }
     asm volatile("" ::: "memory");
@@ -78,13 +91,14 @@ int main(int argc, char** argv) {
   const int maxb = cus * 8;
   CHECK(hipMalloc(&fo, (size_t)maxb * 256 * 4)); CHECK(hipMalloc(&io, (size_t)maxb * 256 * 4));
   CHECK(hipMalloc(&clk, 64));
-  const char* names[] = {"fma", "mul", "add", "add+cmp->sgpr+bcnt", "add+cmp->vcc+addc"};
+  const char* names[] = {"fma", "mul", "add", "add+cmp->sgpr+bcnt", "add+cmp->vcc+addc",
+                         "pk_mul (2 lanes-ops)", "pk_add (2 lane-ops)", "pk_fma (2 lane-ops)"};
   // VALU instructions per (iteration, accumulator), from the gfx950 asm of each body
-  const double valu[] = {1, 1, 1, 2, 3};
+  const double valu[] = {1, 1, 1, 2, 3, 0.5, 0.5, 0.5};
   for (int wps = 1; wps <= 8; wps *= 2) {
     const int blocks = cus * wps;  // 256-thread block = 4 waves = 1 wave per SIMD
     printf("== %d wave(s)/SIMD\n", wps);
-    for (int op = 0; op < 5; ++op) {
+    for (int op = 0; op < 8; ++op) {
       auto L = [&] {
         switch (op) {
           case 0: hipLaunchKernelGGL(k_body<0>, blocks, 256, 0, 0, in, fo, io, clk); break;
@@ -92,6 +106,9 @@ int main(int argc, char** argv) {
           case 2: hipLaunchKernelGGL(k_body<2>, blocks, 256, 0, 0, in, fo, io, clk); break;
           case 3: hipLaunchKernelGGL(k_body<3>, blocks, 256, 0, 0, in, fo, io, clk); break;
           case 4: hipLaunchKernelGGL(k_body<4>, blocks, 256, 0, 0, in, fo, io, clk); break;
+          case 5: hipLaunchKernelGGL(k_body<5>, blocks, 256, 0, 0, in, fo, io, clk); break;
+          case 6: hipLaunchKernelGGL(k_body<6>, blocks, 256, 0, 0, in, fo, io, clk); break;
+          case 7: hipLaunchKernelGGL(k_body<7>, blocks, 256, 0, 0, in, fo, io, clk); break;
         }
       };
       float ms = time_kernel(L, 5);
