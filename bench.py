@@ -77,6 +77,9 @@ def c5_secondary(D, ctx, a):
     rn, out["normals_radius0.1_ms"] = timed(lambda: D.estimate_normals(pts, radius=0.1, ctx=ctx))
     reg, out["regulate_r0.1_ms"] = timed(lambda: D.regulate_normals(pts, rn, 0, True, 0.1, ctx=ctx), 1)
     out["regulate_reached"] = reg[2]
+    # preProcess with the reference's default min_dist_between_points (Dialog/config.txt:3)
+    pp, out["preprocess_0.001_ms"] = timed(lambda: D.preprocess(pts, 0.001, ctx=ctx), 1)
+    out["preprocess_kept"] = int(len(pp[1]))
     cloud = D.Cloud(ctx, pts)
     cloud.set_normals(nrm)
     prm = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
@@ -96,7 +99,7 @@ def c5_secondary(D, ctx, a):
                 "np_unit": "G point-plane tests/s",
                 "np_kernel_tests_per_s": round(st["tests_scored"] / (st["score_ms"] / 1e3) / 1e9, 3)
                 if st["score_ms"] else None})
-    for k in ("normals_knn20_ms", "normals_radius0.1_ms", "regulate_r0.1_ms"):
+    for k in ("normals_knn20_ms", "normals_radius0.1_ms", "regulate_r0.1_ms", "preprocess_0.001_ms"):
         out[k] = round(out[k], 2)
     cloud.close()
     return out

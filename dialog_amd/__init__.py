@@ -10,9 +10,11 @@ from .sac import (SAC_RANSAC, SACMODEL_NORMAL_PLANE, SACMODEL_PLANE, Cloud, Cont
                   make_params, segment_cloud)
 from .normals import (NormalEstimation, estimate_normals, orient_normals_nn,  # noqa: F401
                       regulate_normals)
+from .preprocess import preprocess, remove_redundant_points  # noqa: F401
 from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, LIB_PATH  # noqa: F401
 
 __all__ = ["Context", "Cloud", "SACSegmentation", "extract_planes", "segment_cloud", "make_params",
            "SACMODEL_PLANE", "SACMODEL_NORMAL_PLANE", "SAC_RANSAC", "DLG_REFIT_PCL",
            "DLG_REFIT_FAST", "DialogError", "LIB_PATH", "NormalEstimation", "estimate_normals",
-           "regulate_normals", "SACSegmentationFromNormals", "orient_normals_nn"]
+           "regulate_normals", "SACSegmentationFromNormals", "orient_normals_nn",
+           "preprocess", "remove_redundant_points"]

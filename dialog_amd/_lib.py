@@ -24,7 +24,7 @@ SYMBOLS = [
     "dlg_cloud_active", "dlg_sac_segment", "dlg_sac_segment_host", "dlg_extract_planes",
     "dlg_set_profiling", "dlg_synchronize", "dlg_allreduce_max_f64", "dlg_barrier",
     "dlg_score_benchmark", "dlg_estimate_normals", "dlg_regulate_normals",
-    "dlg_cloud_set_normals", "dlg_orient_normals_nn",
+    "dlg_cloud_set_normals", "dlg_orient_normals_nn", "dlg_preprocess",
 ]
 
 
@@ -100,6 +100,8 @@ def load():
     L.dlg_barrier.argtypes = [vp]
     L.dlg_score_benchmark.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                       C.POINTER(C.c_double), i32p]
+    L.dlg_preprocess.argtypes = [vp, C.POINTER(Points), C.c_int, C.c_float, fp, C.c_int64, i32p,
+                                 C.c_int64, i64p, fp]
     L.dlg_orient_normals_nn.argtypes = [vp, C.POINTER(Points), fp, C.c_int64, C.POINTER(Points),
                                         fp, C.c_int64]
     L.dlg_cloud_set_normals.argtypes = [vp, vp, fp, C.c_int64, C.c_int64]

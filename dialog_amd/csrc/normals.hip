@@ -446,6 +446,134 @@ __global__ __launch_bounds__(kBS) void k_flip_to_reference(float* __restrict__ n
 }
 
 // ---------------------------------------------------------------------------------------------
+// preProcess() (PlaneDetect.h:448-512): NaN removal, translation to the centroid, and the greedy
+// redundancy removal -- keep i unless an already kept j < i lies within min_dist -- which is the
+// lexicographically-first maximal independent set of the radius graph in index order.
+
+__global__ __launch_bounds__(kBS) void k_finite_flags(const float* __restrict__ X,
+                                                      const float* __restrict__ Y,
+                                                      const float* __restrict__ Z, int n,
+                                                      uint8_t* __restrict__ flags) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i < n) flags[i] = finite3(X[i], Y[i], Z[i]) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kBS) void k_gather3(const int32_t* __restrict__ src, int n,
+                                                 const float* __restrict__ X,
+                                                 const float* __restrict__ Y,
+                                                 const float* __restrict__ Z,
+                                                 float* __restrict__ OX, float* __restrict__ OY,
+                                                 float* __restrict__ OZ) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const int j = src[i];
+  OX[i] = X[j];
+  OY[i] = Y[j];
+  OZ[i] = Z[j];
+}
+
+// the reference's centroid: sequential float sums in index order, then / float(n).  One block;
+// lanes 0, 1, 2 run the x, y, z chains over LDS-staged chunks (bit-exact with the serial loop).
+__global__ __launch_bounds__(256) void k_seq_centroid(const float* __restrict__ X,
+                                                      const float* __restrict__ Y,
+                                                      const float* __restrict__ Z, int n,
+                                                      float* __restrict__ out) {
+  __shared__ float s[2][3][256];
+  const int lane = threadIdx.x;
+  float acc = 0.0f;
+  int buf = 0;
+  if (lane < n) { s[0][0][lane] = X[lane]; s[0][1][lane] = Y[lane]; s[0][2][lane] = Z[lane]; }
+  for (int base = 0; base < n; base += 256) {
+    __syncthreads();
+    const int nb = base + 256;  // prefetch the next chunk while lanes 0-2 sum this one
+    if (nb + lane < n) {
+      s[buf ^ 1][0][lane] = X[nb + lane];
+      s[buf ^ 1][1][lane] = Y[nb + lane];
+      s[buf ^ 1][2][lane] = Z[nb + lane];
+    }
+    if (lane < 3) {
+      const int m = min(256, n - base);
+      for (int k = 0; k < m; ++k) acc += s[buf][lane][k];
+    }
+    buf ^= 1;
+  }
+  if (lane < 3) out[lane] = acc / (float)n;
+}
+
+__global__ __launch_bounds__(kBS) void k_translate(float* __restrict__ X, float* __restrict__ Y,
+                                                   float* __restrict__ Z, int n,
+                                                   const float* __restrict__ p) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  X[i] -= p[0];
+  Y[i] -= p[1];
+  Z[i] -= p[2];
+}
+
+// one round of the index-ordered MIS over the sorted positions still undecided (state 0):
+// kept (1) iff every lower-index neighbour is removed, removed (2) as soon as one is kept
+__global__ __launch_bounds__(kBS) void k_mis_round(
+    const int32_t* __restrict__ qlist, int nq, const float* __restrict__ sx,
+    const float* __restrict__ sy, const float* __restrict__ sz, const int32_t* __restrict__ sidx,
+    GridDesc G, const uint32_t* __restrict__ tkeys, const int2* __restrict__ trange,
+    uint32_t tmask, float r2, uint8_t* state, int32_t* __restrict__ next,
+    uint32_t* __restrict__ n_next) {
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= nq) return;
+  const int u = qlist ? qlist[t] : t;
+  const int j = sidx[u];
+  const float qx = sx[u], qy = sy[u], qz = sz[u];
+  bool kept_nb = false, all_removed = true;
+  const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+  const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+  const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+  for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1) && !kept_nb; ++z)
+    for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1) && !kept_nb; ++y)
+      for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1) && !kept_nb; ++x) {
+        const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+        for (int v = rg.x; v < rg.y; ++v) {
+          if (sidx[v] >= j) continue;
+          if (!(flann_d2(qx, qy, qz, sx[v], sy[v], sz[v]) < r2)) continue;
+          const uint8_t st = __hip_atomic_load(&state[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (st == 1) { kept_nb = true; break; }
+          if (st == 0) all_removed = false;
+        }
+      }
+  if (kept_nb) {
+    __hip_atomic_store(&state[u], (uint8_t)2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (all_removed) {
+    __hip_atomic_store(&state[u], (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    next[atomicAdd(n_next, 1u)] = u;
+  }
+}
+
+// kept[point] = state[sorted position] == 1
+__global__ __launch_bounds__(kBS) void k_mis_flags(const int32_t* __restrict__ sidx, int n,
+                                                   const uint8_t* __restrict__ state,
+                                                   uint8_t* __restrict__ kept) {
+  const int u = blockIdx.x * kBS + threadIdx.x;
+  if (u < n) kept[sidx[u]] = state[u] == 1 ? 1 : 0;
+}
+
+// output records: translated xyz (+ pad 1.0 in a 16-byte PointXYZ) and the source index
+__global__ __launch_bounds__(kBS) void k_emit_points(const int32_t* __restrict__ sel, int n,
+                                                     const float* __restrict__ X,
+                                                     const float* __restrict__ Y,
+                                                     const float* __restrict__ Z,
+                                                     const int32_t* __restrict__ src,
+                                                     float* __restrict__ out, int64_t stride,
+                                                     int32_t* __restrict__ out_idx) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const int k = sel[i];
+  float* o = out + (int64_t)i * stride;
+  o[0] = X[k]; o[1] = Y[k]; o[2] = Z[k];
+  for (int f = 3; f < stride; ++f) o[f] = f == 3 ? 1.0f : 0.0f;
+  out_idx[i] = src[k];
+}
+
+// ---------------------------------------------------------------------------------------------
 // RegulateNormal BFS, one level per (claim, settle, order)
 // The BFS state lives in the grid's sorted order (position u of point sidx[u]): processed[],
 // claim[] and the normals are read per cell run, i.e. coalesced, instead of at random point ids.
@@ -660,6 +788,65 @@ void launch_flip_to_reference(float* nrm, int64_t stride_f, const float* ref, in
   if (n <= 0) return;
   hipLaunchKernelGGL(k_flip_to_reference, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, nrm, stride_f, ref,
                      ref_stride_f, nn, n);
+}
+
+void launch_finite_flags(const float* X, const float* Y, const float* Z, int n, uint8_t* flags,
+                         hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_finite_flags, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, X, Y, Z, n, flags);
+}
+
+size_t select_tmp_bytes(int n) {
+  size_t t = 0;
+  (void)hipcub::DeviceSelect::Flagged(nullptr, t, hipcub::CountingInputIterator<int32_t>(0),
+                                      (const uint8_t*)nullptr, (int32_t*)nullptr,
+                                      (uint32_t*)nullptr, (int64_t)n);
+  return t;
+}
+
+hipError_t select_flagged(void* tmp, size_t tmp_bytes, const uint8_t* flags, int n, int32_t* out,
+                          uint32_t* n_out, hipStream_t s) {
+  size_t t = tmp_bytes;
+  return hipcub::DeviceSelect::Flagged(tmp, t, hipcub::CountingInputIterator<int32_t>(0), flags,
+                                       out, n_out, (int64_t)n, s);
+}
+
+void launch_gather3(const int32_t* src, int n, const float* X, const float* Y, const float* Z,
+                    float* OX, float* OY, float* OZ, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather3, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, src, n, X, Y, Z, OX, OY, OZ);
+}
+
+void launch_seq_centroid(const float* X, const float* Y, const float* Z, int n, float* out,
+                         hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_seq_centroid, dim3(1), dim3(256), 0, s, X, Y, Z, n, out);
+}
+
+void launch_translate(float* X, float* Y, float* Z, int n, const float* p, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_translate, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, X, Y, Z, n, p);
+}
+
+void launch_mis_round(const int32_t* qlist, int nq, const GridDesc& G, const GridBufs& B, float r2,
+                      uint8_t* state, int32_t* next, uint32_t* n_next, hipStream_t s) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(k_mis_round, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, qlist, nq, B.sx, B.sy,
+                     B.sz, B.idx_out, G, B.tkeys, B.trange, B.tmask, r2, state, next, n_next);
+}
+
+void launch_mis_flags(const GridBufs& B, int n, const uint8_t* state, uint8_t* kept,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_mis_flags, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.idx_out, n, state, kept);
+}
+
+void launch_emit_points(const int32_t* sel, int n, const float* X, const float* Y, const float* Z,
+                        const int32_t* src, float* out, int64_t stride_f, int32_t* out_idx,
+                        hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_emit_points, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, sel, n, X, Y, Z, src, out,
+                     stride_f, out_idx);
 }
 
 void launch_bfs_prepare(const GridBufs& B, int n, const float4* nrm, float4* nrm_s, int32_t* pos_of,

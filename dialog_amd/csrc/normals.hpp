@@ -84,6 +84,28 @@ void launch_nn1(const KnnLevels& L, int level, const int32_t* qlist, int nq, con
 void launch_flip_to_reference(float* nrm, int64_t stride_f, const float* ref, int64_t ref_stride_f,
                               const int32_t* nn, int n, hipStream_t s);
 
+// ---- preProcess (PlaneDetect.h:448-512) ----
+void launch_finite_flags(const float* X, const float* Y, const float* Z, int n, uint8_t* flags,
+                         hipStream_t s);
+size_t select_tmp_bytes(int n);
+// out = indices i (ascending) with flags[i] != 0; *n_out (device) = their number
+hipError_t select_flagged(void* tmp, size_t tmp_bytes, const uint8_t* flags, int n, int32_t* out,
+                          uint32_t* n_out, hipStream_t s);
+void launch_gather3(const int32_t* src, int n, const float* X, const float* Y, const float* Z,
+                    float* OX, float* OY, float* OZ, hipStream_t s);
+// out[0..2] = (sequential float sum of X, Y, Z) / float(n), exactly the reference's loop
+void launch_seq_centroid(const float* X, const float* Y, const float* Z, int n, float* out,
+                         hipStream_t s);
+void launch_translate(float* X, float* Y, float* Z, int n, const float* p, hipStream_t s);
+// index-ordered maximal independent set of the radius graph, one round over the undecided
+// sorted positions (qlist == nullptr: all); state: 0 undecided, 1 kept, 2 removed
+void launch_mis_round(const int32_t* qlist, int nq, const GridDesc& G, const GridBufs& B, float r2,
+                      uint8_t* state, int32_t* next, uint32_t* n_next, hipStream_t s);
+void launch_mis_flags(const GridBufs& B, int n, const uint8_t* state, uint8_t* kept, hipStream_t s);
+void launch_emit_points(const int32_t* sel, int n, const float* X, const float* Y, const float* Z,
+                        const int32_t* src, float* out, int64_t stride_f, int32_t* out_idx,
+                        hipStream_t s);
+
 // ---- RegulateNormal, level-synchronous BFS (state in the grid's sorted order) ----
 // queue[]: point ids in PCL queue order; the current level is queue[fbase, fbase + nf).
 // claim_s: min over claiming queue positions (init ~0); cand/ncand: first-claimed positions.

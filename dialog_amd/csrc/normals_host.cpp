@@ -24,19 +24,11 @@ struct BBox {
   bool any;
 };
 
-// points -> device SoA (nw.x/y/z) + bounding box of the finite points
-BBox upload_points(dlg_ctx* c, const dlg_points* pts) {
+BBox bbox_of(dlg_ctx* c, const float* X, const float* Y, const float* Z, int n) {
   NormalsWork& w = c->nw;
-  const int n = (int)pts->n;
-  const size_t bytes = (size_t)pts->n * (size_t)pts->stride_bytes;
-  w.raw.ensure(bytes);
-  w.x.ensure(n); w.y.ensure(n); w.z.ensure(n);
-  HIPCHK(hipMemcpyAsync(w.raw.p, pts->xyz, bytes, hipMemcpyHostToDevice, c->stream));
-  launch_deinterleave(reinterpret_cast<const float*>(w.raw.p), n, pts->stride_bytes / 4, w.x.p,
-                      w.y.p, w.z.p, c->stream);
   const int nb = bbox_blocks(n);
   w.partial.ensure(6 * nb);
-  launch_bbox(w.x.p, w.y.p, w.z.p, n, w.partial.p, c->stream);
+  launch_bbox(X, Y, Z, n, w.partial.p, c->stream);
   std::vector<float> part(6 * nb);
   HIPCHK(hipMemcpyAsync(part.data(), w.partial.p, part.size() * 4, hipMemcpyDeviceToHost, c->stream));
   sync(c);
@@ -52,6 +44,19 @@ BBox upload_points(dlg_ctx* c, const dlg_points* pts) {
     }
   b.any = b.lo[0] <= b.hi[0];
   return b;
+}
+
+// points -> device SoA (nw.x/y/z) + bounding box of the finite points
+BBox upload_points(dlg_ctx* c, const dlg_points* pts) {
+  NormalsWork& w = c->nw;
+  const int n = (int)pts->n;
+  const size_t bytes = (size_t)pts->n * (size_t)pts->stride_bytes;
+  w.raw.ensure(bytes);
+  w.x.ensure(n); w.y.ensure(n); w.z.ensure(n);
+  HIPCHK(hipMemcpyAsync(w.raw.p, pts->xyz, bytes, hipMemcpyHostToDevice, c->stream));
+  launch_deinterleave(reinterpret_cast<const float*>(w.raw.p), n, pts->stride_bytes / 4, w.x.p,
+                      w.y.p, w.z.p, c->stream);
+  return bbox_of(c, w.x.p, w.y.p, w.z.p, n);
 }
 
 // grid with cell edge `cell` (grown until the key space fits 2^30 cells)
@@ -81,8 +86,9 @@ GridDesc make_grid(const BBox& b, double cell) {
   return G;
 }
 
-// builds grid level `lv` over nw.x/y/z; returns the number of occupied cells
-uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B) {
+// builds grid level `lv` over (X, Y, Z) (default nw.x/y/z); returns the number of occupied cells
+uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B,
+                    const float* X = nullptr, const float* Y = nullptr, const float* Z = nullptr) {
   NormalsWork& w = c->nw;
   GridLevelBufs& L = w.lv[lv];
   w.keys_in.ensure(n); w.keys_out.ensure(n); w.idx_in.ensure(n);
@@ -101,7 +107,8 @@ uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B) {
   B->sx = L.sx.p; B->sy = L.sy.p; B->sz = L.sz.p;
   B->tkeys = L.tkeys.p; B->trange = L.trange.p; B->tmask = tcap - 1;
   B->sort_tmp = w.sort_tmp.p; B->sort_tmp_bytes = w.sort_tmp.cap;
-  HIPCHK(grid_build(w.x.p, w.y.p, w.z.p, n, G, *B, w.counters.p, c->stream));
+  HIPCHK(grid_build(X ? X : w.x.p, Y ? Y : w.y.p, Z ? Z : w.z.p, n, G, *B, w.counters.p,
+                    c->stream));
   HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
   sync(c);
   return w.h_cnt.p[0];
@@ -341,6 +348,93 @@ void orient_normals_nn(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64_t
   sync(c);
 }
 
+// preProcess() (PlaneDetect.h:448-512): removeNaNFromPointCloud, optional translation of the
+// cloud to its centroid (sequential float sums, as the reference), then the redundancy removal
+// with radius min_dist.  Output: kept points (translated) in input order and their input index.
+int64_t preprocess(dlg_ctx* c, const dlg_points* pts, int translate, float min_dist, float* out,
+                   int64_t out_stride, int32_t* out_idx, int64_t cap, float* translation,
+                   int64_t* n_needed) {
+  check_points(pts);
+  if (out_stride != 12 && out_stride < 16) throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be 12 or >= 16");
+  if (out_stride % 4) throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be a multiple of 4");
+  if (!(min_dist == min_dist)) throw DlgError(DLG_ERR_INVALID, "min_dist is NaN");
+  if (translation) translation[0] = translation[1] = translation[2] = 0.0f;
+  const int n0 = (int)pts->n;
+  if (n0 == 0) return 0;
+  NormalsWork& w = c->nw;
+  (void)upload_points(c, pts);  // nw.x/y/z
+  // 1. removeNaNFromPointCloud: ascending indices of the finite points
+  w.processed.ensure(n0);
+  w.ids.ensure(n0);
+  w.counters.ensure(4);
+  w.h_cnt.ensure(4);
+  w.sort_tmp.ensure(select_tmp_bytes(n0));
+  launch_finite_flags(w.x.p, w.y.p, w.z.p, n0, w.processed.p, c->stream);
+  HIPCHK(select_flagged(w.sort_tmp.p, w.sort_tmp.cap, w.processed.p, n0, w.ids.p, w.counters.p,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  const int n = (int)w.h_cnt.p[0];
+  if (n == 0) return 0;
+  w.qx.ensure(n); w.qy.ensure(n); w.qz.ensure(n);
+  launch_gather3(w.ids.p, n, w.x.p, w.y.p, w.z.p, w.qx.p, w.qy.p, w.qz.p, c->stream);
+  // 2. translation to the centroid (PlaneDetect.h:458-479)
+  if (translate) {
+    w.partial.ensure(6);
+    launch_seq_centroid(w.qx.p, w.qy.p, w.qz.p, n, w.partial.p, c->stream);
+    launch_translate(w.qx.p, w.qy.p, w.qz.p, n, w.partial.p, c->stream);
+    float p[3];
+    HIPCHK(hipMemcpyAsync(p, w.partial.p, 12, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    if (translation) std::memcpy(translation, p, 12);
+  }
+  // 3. redundancy removal (PlaneDetect.h:482-508)
+  const BBox b = bbox_of(c, w.qx.p, w.qy.p, w.qz.p, n);
+  const double r = min_dist > 0.0f ? (double)min_dist : 0.0;
+  const GridDesc G = make_grid(b, r > 0.0 ? r : 1.0);
+  GridBufs B;
+  build_grid(c, n, G, 0, &B, w.qx.p, w.qy.p, w.qz.p);
+  const float r2 = (float)(r * r);  // radiusSearch(point, float radius): (float)(r * r)
+  w.processed_s.ensure(n);
+  w.queue.ensure(n);
+  w.cand.ensure(n);
+  HIPCHK(hipMemsetAsync(w.processed_s.p, 0, n, c->stream));
+  int32_t* qin = nullptr;
+  int32_t* qout = w.queue.p;
+  int nq = n;
+  while (nq > 0) {
+    HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
+    launch_mis_round(qin, nq, G, B, r2, w.processed_s.p, qout, w.counters.p, c->stream);
+    HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    const int left = (int)w.h_cnt.p[0];
+    if (left >= nq) throw DlgError(DLG_ERR_INTERNAL, "redundancy removal made no progress");
+    nq = left;
+    qin = qout;
+    qout = qout == w.queue.p ? w.cand.p : w.queue.p;
+  }
+  launch_mis_flags(B, n, w.processed_s.p, w.processed.p, c->stream);
+  HIPCHK(select_flagged(w.sort_tmp.p, w.sort_tmp.cap, w.processed.p, n, w.cand.p, w.counters.p,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  const int64_t kept = w.h_cnt.p[0];
+  *n_needed = kept;
+  if (kept > cap) throw DlgError(DLG_ERR_CAPACITY, "output too small: need " + std::to_string(kept));
+  if (!out || !out_idx) throw DlgError(DLG_ERR_INVALID, "output buffers are null");
+  const size_t obytes = (size_t)kept * (size_t)out_stride;
+  w.out.ensure(obytes + 4 * (size_t)kept);
+  float* dout = reinterpret_cast<float*>(w.out.p);
+  int32_t* didx = reinterpret_cast<int32_t*>(w.out.p + obytes);
+  launch_emit_points(w.cand.p, (int)kept, w.qx.p, w.qy.p, w.qz.p, w.ids.p, dout, out_stride / 4,
+                     didx, c->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, dout, obytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out_idx, didx, 4 * (size_t)kept, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  return kept;
+}
+
 }  // namespace
 }  // namespace dlg
 
@@ -375,4 +469,16 @@ dlg_status dlg_orient_normals_nn(dlg_ctx* c, const dlg_points* pts, float* norma
   });
 }
 
+dlg_status dlg_preprocess(dlg_ctx* c, const dlg_points* pts, int translate, float min_dist,
+                          float* out_xyz, int64_t out_stride_bytes, int32_t* out_index,
+                          int64_t cap, int64_t* n_out, float translation[3]) {
+  if (!c || !n_out) return DLG_ERR_INVALID;
+  *n_out = 0;
+  return guarded(c, [&] {
+    preprocess(c, pts, translate, min_dist, out_xyz, out_stride_bytes, out_index, cap, translation,
+               n_out);  // *n_out = points kept, also when the output capacity is too small
+  });
+}
+
 }  // extern "C"
+

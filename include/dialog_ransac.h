@@ -192,6 +192,19 @@ dlg_status dlg_orient_normals_nn(dlg_ctx* ctx, const dlg_points* pts, float* nor
                                  int64_t stride_bytes, const dlg_points* ref_pts,
                                  const float* ref_normals, int64_t ref_stride_bytes);
 
+/* ---- preprocessing (Dialog/PlaneDetect.h:448-512, PCLViewer.cpp:781-805) -------------------- */
+/* preProcess(): pcl::removeNaNFromPointCloud, then (translate != 0) the translation of the cloud
+ * to its centroid (sequential float sums / float(n), as the reference; translation[3] receives
+ * it), then the redundancy removal: walking the points in order, a point is kept unless an
+ * already kept point lies within min_dist (KdTreeFLANN radius test), i.e. the index-ordered
+ * maximal independent set of the radius graph.  out_xyz: the kept (translated) points in input
+ * order, records of out_stride_bytes (12 = xyz, 16 = pcl::PointXYZ with pad 1.0); out_index: their
+ * input index.  *n_out = kept points (also on DLG_ERR_CAPACITY when cap is too small).  With
+ * translate = 0 this is on_removeRedundantPointsAction_triggered (PCLViewer.cpp:781-805). */
+dlg_status dlg_preprocess(dlg_ctx* ctx, const dlg_points* pts, int translate, float min_dist,
+                          float* out_xyz, int64_t out_stride_bytes, int32_t* out_index,
+                          int64_t cap, int64_t* n_out, float translation[3]);
+
 /* ---- profiling ------------------------------------------------------------------------------ */
 /* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);

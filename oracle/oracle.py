@@ -79,6 +79,8 @@ def lib():
         L.orc_estimate_normals_knn.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, fp, fp]
         L.orc_orient_normals_nn.argtypes = [fp, C.c_int64, C.c_int64, fp, fp, C.c_int64,
                                             C.c_int64, fp]
+        L.orc_preprocess.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, C.c_float, fp, i32p, fp]
+        L.orc_preprocess.restype = C.c_int64
         L.orc_regulate_normals.argtypes = [fp, C.c_int64, C.c_int64, fp, C.c_int64, C.c_int,
                                            C.c_float, C.POINTER(C.c_uint8)]
         L.orc_regulate_normals.restype = C.c_int64
@@ -271,4 +273,15 @@ def orient_normals_nn(points, normals, ref_points, ref_normals):
     lib().orc_orient_normals_nn(_f(p), p.shape[0], stride, _f(nrm), _f(r), r.shape[0], rstride,
                                 _f(rn))
     return nrm
+
+
+def preprocess(points, min_dist, translate=True):
+    p, stride = _xyz(points)
+    n = p.shape[0]
+    out = np.zeros((max(n, 1), 3), np.float32)
+    idx = np.zeros(max(n, 1), np.int32)
+    tr = np.zeros(3, np.float32)
+    k = lib().orc_preprocess(_f(p), n, stride, int(bool(translate)), float(min_dist), _f(out),
+                             _i32(idx), _f(tr))
+    return out[:k].copy(), idx[:k].copy(), tr
 

@@ -752,3 +752,53 @@ void orc_orient_normals_nn(const float* xyz, int64_t n, int64_t stride, float* n
   }
 }
 
+/* Dialog/PlaneDetect.h:448-512 preProcess(), restated literally: removeNaNFromPointCloud (drop
+ * points with a non-finite coordinate), optional translation to the centroid (pcl::PointXYZ p:
+ * float sums in index order, then /= float(n), then every point -= p), then the redundancy loop
+ * with radiusSearch results sorted by (dist2, index) and indices[0] skipped.  out_xyz: 3 floats
+ * per kept point; out_index: input index.  Returns the number kept. */
+int64_t orc_preprocess(const float* xyz, int64_t n, int64_t stride, int translate, float min_dist,
+                       float* out_xyz, int32_t* out_index, float translation[3]) {
+  float* pts = (float*)malloc((size_t)(n > 0 ? n : 1) * 3 * sizeof(float));
+  int32_t* src = (int32_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + i * stride;
+    if (!isfinite(p[0]) || !isfinite(p[1]) || !isfinite(p[2])) continue;
+    pts[3 * m] = p[0]; pts[3 * m + 1] = p[1]; pts[3 * m + 2] = p[2];
+    src[m++] = (int32_t)i;
+  }
+  translation[0] = translation[1] = translation[2] = 0.0f;
+  if (translate && m > 0) {
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    for (int64_t i = 0; i < m; ++i) { px += pts[3 * i]; py += pts[3 * i + 1]; pz += pts[3 * i + 2]; }
+    px /= (float)m; py /= (float)m; pz /= (float)m;
+    for (int64_t i = 0; i < m; ++i) { pts[3 * i] -= px; pts[3 * i + 1] -= py; pts[3 * i + 2] -= pz; }
+    translation[0] = px; translation[1] = py; translation[2] = pz;
+  }
+  int64_t kept = 0;
+  if (m > 0) {
+    uint8_t* processed = (uint8_t*)calloc((size_t)m, 1);
+    float radius = min_dist;
+    orc_grid G;
+    orc_grid_build(&G, pts, m, 3, radius > 0.0f ? radius : 1.0f);
+    float r2 = (float)((double)radius * (double)radius);
+    orc_nb* nb = NULL; int64_t cap = 0;
+    for (int64_t i = 0; i < m; ++i) {
+      if (processed[i]) continue;
+      processed[i] = 1;
+      out_xyz[3 * kept] = pts[3 * i]; out_xyz[3 * kept + 1] = pts[3 * i + 1];
+      out_xyz[3 * kept + 2] = pts[3 * i + 2];
+      out_index[kept++] = src[i];
+      int64_t k = radius > 0.0f ? orc_radius(&G, pts, 3, pts + 3 * i, r2, &nb, &cap) : 0;
+      for (int64_t j = 1; j < k; ++j) processed[nb[j].j] = 1;
+    }
+    free(nb);
+    orc_grid_free(&G);
+    free(processed);
+  }
+  free(pts);
+  free(src);
+  return kept;
+}
+

@@ -122,6 +122,10 @@ void orc_orient_normals_nn(const float* xyz, int64_t n, int64_t stride, float* n
                            const float* ref_xyz, int64_t m, int64_t ref_stride,
                            const float* ref_normals);
 
+/* PlaneDetect.h:448-512 preProcess(): NaN removal, centroid translation, redundancy removal */
+int64_t orc_preprocess(const float* xyz, int64_t n, int64_t stride, int translate, float min_dist,
+                       float* out_xyz, int32_t* out_index, float translation[3]);
+
 #ifdef __cplusplus
 }
 #endif
