@@ -55,12 +55,50 @@ def read_pcd(path: str) -> np.ndarray:
     return np.ascontiguousarray(np.stack([cols["x"], cols["y"], cols["z"]], axis=1))
 
 
-def write_pcd_ascii(path: str, xyz: np.ndarray) -> None:
-    xyz = np.asarray(xyz, np.float32)
+def read_pcd_fields(path: str, fields) -> np.ndarray:
+    """Named float fields (e.g. normal_x normal_y normal_z curvature) as float32 [N, len(fields)]."""
+    with open(path, "rb") as f:
+        header = {}
+        while True:
+            line = f.readline()
+            if not line:
+                raise ValueError(f"{path}: truncated PCD header")
+            s = line.decode("ascii", "replace").strip()
+            if not s or s.startswith("#"):
+                continue
+            key, _, rest = s.partition(" ")
+            header[key.upper()] = rest.split()
+            if key.upper() == "DATA":
+                break
+        body = f.read()
+    names = header["FIELDS"]
+    counts = [int(v) for v in header.get("COUNT", ["1"] * len(names))]
+    n = int(header["POINTS"][0])
+    if header["DATA"][0].lower() != "ascii":
+        raise ValueError(f"{path}: read_pcd_fields reads ASCII PCD only")
+    rows = [r.split() for r in body.decode("ascii", "replace").splitlines() if r.strip()][:n]
+    pos, col = {}, 0
+    for fld, cnt in zip(names, counts):
+        pos[fld] = col
+        col += cnt
+    out = np.empty((len(rows), len(fields)), np.float32)
+    for k, fld in enumerate(fields):
+        out[:, k] = [float(r[pos[fld]]) for r in rows]
+    return out
+
+
+def write_pcd_ascii(path: str, data: np.ndarray, fields=("x", "y", "z"), precision: int = 8) -> None:
+    """pcl::io::savePCDFileASCII: v0.7 header, one line per point, floats printed as an ostream
+    with precision(8) prints them (%g style; nan/inf as 'nan'/'inf')."""
+    data = np.asarray(data, np.float32).reshape(-1, len(fields))
+    n = data.shape[0]
+    k = len(fields)
     with open(path, "w") as f:
-        f.write("# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\nFIELDS x y z\n"
-                "SIZE 4 4 4\nTYPE F F F\nCOUNT 1 1 1\n")
-        f.write(f"WIDTH {xyz.shape[0]}\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\n")
-        f.write(f"POINTS {xyz.shape[0]}\nDATA ascii\n")
-        for p in xyz:
-            f.write("%.9g %.9g %.9g\n" % (float(p[0]), float(p[1]), float(p[2])))
+        f.write("# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\n")
+        f.write("FIELDS " + " ".join(fields) + "\n")
+        f.write("SIZE " + " ".join(["4"] * k) + "\nTYPE " + " ".join(["F"] * k) + "\n")
+        f.write("COUNT " + " ".join(["1"] * k) + "\n")
+        f.write(f"WIDTH {n}\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS {n}\nDATA ascii\n")
+        fmt = " ".join([f"%.{precision}g"] * k) + "\n"
+        for row in data:
+            f.write(fmt % tuple(float(v) for v in row))
