@@ -229,8 +229,12 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   const double one_over_indices = 1.0 / (double)N;
   int consec_bad = 0;
   bool done = false, have = false;
-  HypRec best_h{};
-  SampleRec best_s[3]{};
+  // device slots: winning HypRec (its first float4 is the plane), its 3 samples, refined plane
+  c->small.ensure(8);
+  HypRec* best_dev = reinterpret_cast<HypRec*>(c->small.p);
+  SampleRec* best_smp_dev = reinterpret_cast<SampleRec*>(c->small.p + 2);
+  float4* rc_dev = c->small.p + 5;
+  const float4* bc_dev = c->small.p;
   int launches = 0;
 
   while (!done) {
@@ -316,11 +320,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       if (iterations > prm.max_iterations) done = true;
       else if (!(iterations < k)) done = true;
     }
-    if (best_d >= 0) {
-      HIPCHK(hipMemcpyAsync(&best_h, c->hyps.p + best_d, sizeof(HypRec), hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipMemcpyAsync(best_s, c->samples.p + 3 * best_d, 3 * sizeof(SampleRec),
-                            hipMemcpyDeviceToHost, c->stream));
-      sync(c);
+    if (best_d >= 0) {  // keep the winner on the device (the next batch overwrites hyps)
+      HIPCHK(hipMemcpyAsync(best_dev, c->hyps.p + best_d, sizeof(HypRec), hipMemcpyDeviceToDevice,
+                            c->stream));
+      HIPCHK(hipMemcpyAsync(best_smp_dev, c->samples.p + 3 * best_d, 3 * sizeof(SampleRec),
+                            hipMemcpyDeviceToDevice, c->stream));
     }
   }
   st->iterations = iterations;
@@ -335,10 +339,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
 
   st->has_model = 1;
   st->n_unrefined = best;
-  const float bc[4] = {best_h.a, best_h.b, best_h.c, best_h.d};
-  std::memcpy(st->coeff_unrefined, bc, sizeof(bc));
-  for (int i = 0; i < 3; ++i) st->best_sample[i] = best_s[i].gid;
 
+  // Refit + final select.  Fast mode (and no optimisation) never leave the device: moments of
+  // the unrefined plane's inliers (k_moments, centred on the winning sample), the double eigen33
+  // refit in a one-thread kernel, then the select with the refined plane read from device memory;
+  // one D2H + sync at the end.  PCL mode needs the host's sequential float sums in between.
   const double t_ref0 = trace_on() ? now_ms() : 0.0;
   const int nt = select_tiles(src.n);
   c->tile_in.ensure(nt + 1);
@@ -346,40 +351,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   c->tile_off_out.ensure(nt + 1);
   c->totals.ensure(2);
   c->h_tot.ensure(2);
+  c->h_small.ensure(8);
   c->inl_gid.ensure((size_t)std::max<int64_t>(src.n, 1));
-  float rc[4];
-  if (c->profiling) HIPCHK(hipEventRecord(c->ev[2], c->stream));
-  if (!prm.optimize) {
-    std::memcpy(rc, bc, sizeof(rc));
-  } else if (prm.refit_mode == DLG_REFIT_FAST) {
-    const int nb = moments_blocks(src.n);
-    c->partials.ensure((size_t)nb * kMomentK);
-    c->moments.ensure(kMomentK);
-    c->h_mom.ensure(kMomentK);
-    const double shift[3] = {best_s[0].x, best_s[0].y, best_s[0].z};
-    launch_moments(src, make_float4(bc[0], bc[1], bc[2], bc[3]), mt,
-                   make_double3(shift[0], shift[1], shift[2]), c->partials.p, nb, c->moments.p,
-                   c->stream);
-    if (c->comm->world() > 1) c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
-    HIPCHK(hipMemcpyAsync(c->h_mom.p, c->moments.p, kMomentK * 8, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
-    refit_from_moments(c->h_mom.p, shift, bc, rc);
-  } else {
-    // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
-    c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
-    launch_select(src, make_float4(bc[0], bc[1], bc[2], bc[3]), mt, c->tile_in.p, c->tile_off_in.p,
-                  c->tile_off_out.p, c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
-    HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
-    std::vector<int32_t> xyz_bits;
-    gather_lists(c, reinterpret_cast<const int32_t*>(c->inl_xyz.p), c->h_tot.p[0], 3, &xyz_bits);
-    refit_pcl_float(reinterpret_cast<const float*>(xyz_bits.data()), (int64_t)xyz_bits.size() / 3,
-                    bc, rc);
-  }
-  std::memcpy(out.coeff, rc, sizeof(rc));
-  out.has_model = true;
-
-  // final selectWithinDistance with the refined model (+ compaction of the survivors)
+  c->moments.ensure(kMomentK);
   PointsOut dst{};
   if (compact) {
     SoA& sp = cl->buf[cl->spare()];
@@ -387,14 +361,55 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (src.nrm) sp.ensure_nrm((size_t)std::max<int64_t>(src.n, 1));
     dst = sp.out();
   }
-  launch_select(src, make_float4(rc[0], rc[1], rc[2], rc[3]), mt, c->tile_in.p, c->tile_off_in.p,
-                c->tile_off_out.p, c->totals.p, c->inl_gid.p, nullptr, compact ? &dst : nullptr,
-                c->stream);
+  if (c->profiling) HIPCHK(hipEventRecord(c->ev[2], c->stream));
+  const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
+  if (!pcl_refit) {
+    if (prm.optimize) {
+      const int nb = moments_blocks(src.n);
+      c->partials.ensure((size_t)nb * kMomentK);
+      launch_moments(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p, c->stream);
+      if (c->comm->world() > 1)
+        c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
+    }
+    launch_refit_moments(c->moments.p, best_smp_dev, bc_dev, prm.optimize, rc_dev, c->stream);
+  } else {
+    // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
+    c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
+    launch_select(src, bc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
+                  c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
+    HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 5 * sizeof(float4), hipMemcpyDeviceToHost,
+                          c->stream));
+    sync(c);
+    const HypRec* bh = reinterpret_cast<const HypRec*>(c->h_small.p);
+    const float bc[4] = {bh->a, bh->b, bh->c, bh->d};
+    std::vector<int32_t> xyz_bits;
+    gather_lists(c, reinterpret_cast<const int32_t*>(c->inl_xyz.p), c->h_tot.p[0], 3, &xyz_bits);
+    float rc[4];
+    refit_pcl_float(reinterpret_cast<const float*>(xyz_bits.data()), (int64_t)xyz_bits.size() / 3,
+                    bc, rc);
+    c->h_small.p[5] = make_float4(rc[0], rc[1], rc[2], rc[3]);
+    HIPCHK(hipMemcpyAsync(rc_dev, c->h_small.p + 5, sizeof(float4), hipMemcpyHostToDevice,
+                          c->stream));
+  }
+  // final selectWithinDistance with the refined model (+ compaction of the survivors)
+  launch_select(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
+                c->inl_gid.p, nullptr, compact ? &dst : nullptr, c->stream);
   HIPCHK(hipGetLastError());
   if (c->profiling) HIPCHK(hipEventRecord(c->ev[3], c->stream));
   HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 6 * sizeof(float4), hipMemcpyDeviceToHost,
+                        c->stream));
   sync(c);
   if (c->profiling && xs) xs->select_ms += event_ms(c, 2, 3);
+  const HypRec* bh = reinterpret_cast<const HypRec*>(c->h_small.p);
+  const SampleRec* bs = reinterpret_cast<const SampleRec*>(c->h_small.p + 2);
+  const float4 rc = c->h_small.p[5];
+  st->coeff_unrefined[0] = bh->a; st->coeff_unrefined[1] = bh->b;
+  st->coeff_unrefined[2] = bh->c; st->coeff_unrefined[3] = bh->d;
+  for (int i = 0; i < 3; ++i) st->best_sample[i] = bs[i].gid;
+  out.coeff[0] = rc.x; out.coeff[1] = rc.y; out.coeff[2] = rc.z; out.coeff[3] = rc.w;
+  out.has_model = true;
   out.n_in_local = c->h_tot.p[0];
   out.n_out_local = src.n == 0 ? 0 : c->h_tot.p[1];
   if (trace_on())
@@ -571,6 +586,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->pos.release(); c->samples.release(); c->hyps.release(); c->res.release();
   c->tile_in.release(); c->tile_off_in.release(); c->tile_off_out.release(); c->totals.release();
   c->partials.release(); c->moments.release(); c->inl_gid.release(); c->inl_xyz.release();
+  c->small.release(); c->h_small.release();
   c->gath64.release(); c->gath32.release();
   c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
   c->h_stage.release();

@@ -142,6 +142,8 @@ struct dlg_ctx {
   PinBuf<int32_t> h_pos, h_res, h_tot;
   PinBuf<double> h_mom;
   PinBuf<int64_t> h_g64;
+  DevBuf<float4> small;    // winning plane + samples + refined plane (segment_impl)
+  PinBuf<float4> h_small;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<int32_t> h_inl;
   std::vector<float> h_xyz;

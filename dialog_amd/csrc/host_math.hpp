@@ -9,13 +9,43 @@
 // -ffp-contract=off.  [PCL-1.8 ext] = third-party source, not vendored in the reference.
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <limits>
 #include <utility>
 
+#define DLG_HD __host__ __device__
+
 namespace dlg {
+
+template <typename S>
+DLG_HD inline S eps_of();
+template <>
+DLG_HD inline float eps_of<float>() { return FLT_EPSILON; }
+template <>
+DLG_HD inline double eps_of<double>() { return DBL_EPSILON; }
+template <typename S>
+DLG_HD inline S min_of();
+template <>
+DLG_HD inline float min_of<float>() { return FLT_MIN; }
+template <>
+DLG_HD inline double min_of<double>() { return DBL_MIN; }
+template <typename S>
+DLG_HD inline void swap_(S& a, S& b) { S t = a; a = b; b = t; }
+// float math stays float (sqrtf, atan2f, ...: what std:: overloads call for PCL's float eigen33)
+DLG_HD inline float m_sqrt(float x) { return sqrtf(x); }
+DLG_HD inline double m_sqrt(double x) { return sqrt(x); }
+DLG_HD inline float m_fabs(float x) { return fabsf(x); }
+DLG_HD inline double m_fabs(double x) { return fabs(x); }
+DLG_HD inline float m_atan2(float y, float x) { return atan2f(y, x); }
+DLG_HD inline double m_atan2(double y, double x) { return atan2(y, x); }
+DLG_HD inline float m_cos(float x) { return cosf(x); }
+DLG_HD inline double m_cos(double x) { return cos(x); }
+DLG_HD inline float m_sin(float x) { return sinf(x); }
+DLG_HD inline double m_sin(double x) { return sin(x); }
 
 class Mt19937 {
  public:
@@ -58,55 +88,55 @@ inline float thr_ceil(double thr) {
 
 // ---- pcl::computeRoots2 / computeRoots / eigen33 (common/impl/eigen.hpp) [PCL-1.8 ext] ----------
 template <typename S>
-inline void compute_roots2(S b, S c, S roots[3]) {
+DLG_HD inline void compute_roots2(S b, S c, S roots[3]) {
   roots[0] = S(0);
   S d = S((double)(b * b) - 4.0 * (double)c);  // Scalar(b * b - 4.0 * c): b*b in S, rest in double
   if (d < S(0)) d = S(0);
-  S sd = std::sqrt(d);
+  S sd = m_sqrt(d);
   roots[2] = S(0.5f) * (b + sd);
   roots[1] = S(0.5f) * (b - sd);
 }
 
 template <typename S>
-inline void compute_roots(const S m[9], S roots[3]) {
+DLG_HD inline void compute_roots(const S m[9], S roots[3]) {
   auto M = [&](int r, int c) { return m[r * 3 + c]; };
   S c0 = M(0, 0) * M(1, 1) * M(2, 2) + S(2) * M(0, 1) * M(0, 2) * M(1, 2) -
          M(0, 0) * M(1, 2) * M(1, 2) - M(1, 1) * M(0, 2) * M(0, 2) - M(2, 2) * M(0, 1) * M(0, 1);
   S c1 = M(0, 0) * M(1, 1) - M(0, 1) * M(0, 1) + M(0, 0) * M(2, 2) - M(0, 2) * M(0, 2) +
          M(1, 1) * M(2, 2) - M(1, 2) * M(1, 2);
   S c2 = M(0, 0) + M(1, 1) + M(2, 2);
-  const S eps = std::numeric_limits<S>::epsilon();
-  if (std::fabs(c0) < eps) {
+  const S eps = eps_of<S>();
+  if (m_fabs(c0) < eps) {
     compute_roots2(c2, c1, roots);
     return;
   }
   const S s_inv3 = S(1.0 / 3.0);
-  const S s_sqrt3 = std::sqrt(S(3.0));
+  const S s_sqrt3 = m_sqrt(S(3.0));
   S c2_over_3 = c2 * s_inv3;
   S a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
   if (a_over_3 > S(0)) a_over_3 = S(0);
   S half_b = S(0.5) * (c0 + c2_over_3 * (S(2) * c2_over_3 * c2_over_3 - c1));
   S q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
   if (q > S(0)) q = S(0);
-  S rho = std::sqrt(-a_over_3);
-  S theta = std::atan2(std::sqrt(-q), half_b) * s_inv3;
-  S ct = std::cos(theta), st = std::sin(theta);
+  S rho = m_sqrt(-a_over_3);
+  S theta = m_atan2(m_sqrt(-q), half_b) * s_inv3;
+  S ct = m_cos(theta), st = m_sin(theta);
   roots[0] = c2_over_3 + S(2) * rho * ct;
   roots[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
   roots[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
-  if (roots[0] >= roots[1]) std::swap(roots[0], roots[1]);
+  if (roots[0] >= roots[1]) swap_(roots[0], roots[1]);
   if (roots[1] >= roots[2]) {
-    std::swap(roots[1], roots[2]);
-    if (roots[0] >= roots[1]) std::swap(roots[0], roots[1]);
+    swap_(roots[1], roots[2]);
+    if (roots[0] >= roots[1]) swap_(roots[0], roots[1]);
   }
   if (roots[0] <= S(0)) compute_roots2(c2, c1, roots);
 }
 
 template <typename S>
-inline void eigen33(const S mat[9], S* eval, S evec[3]) {
+DLG_HD inline void eigen33(const S mat[9], S* eval, S evec[3]) {
   S scale = S(0);
-  for (int k = 0; k < 9; ++k) scale = std::fabs(mat[k]) > scale ? std::fabs(mat[k]) : scale;
-  if (scale <= std::numeric_limits<S>::min()) scale = S(1);
+  for (int k = 0; k < 9; ++k) scale = m_fabs(mat[k]) > scale ? m_fabs(mat[k]) : scale;
+  if (scale <= min_of<S>()) scale = S(1);
   S m[9];
   for (int k = 0; k < 9; ++k) m[k] = mat[k] / scale;
   S roots[3];
@@ -130,7 +160,7 @@ inline void eigen33(const S mat[9], S* eval, S evec[3]) {
   if (l1 >= l2 && l1 >= l3) { v = v1; l = l1; }
   else if (l2 >= l1 && l2 >= l3) { v = v2; l = l2; }
   else { v = v3; l = l3; }
-  S s = std::sqrt(l);
+  S s = m_sqrt(l);
   evec[0] = v[0] / s; evec[1] = v[1] / s; evec[2] = v[2] / s;
 }
 
@@ -167,8 +197,8 @@ inline void refit_pcl_float(const float* xyz, int64_t n, const float cin[4], flo
 }
 
 // fast mode: moments m[10] = {n, sx, sy, sz, sxx, sxy, sxz, syy, syz, szz} of (p - shift), double.
-inline void refit_from_moments(const double m[10], const double shift[3], const float cin[4],
-                               float cout[4]) {
+DLG_HD inline void refit_from_moments(const double m[10], const double shift[3], const float cin[4],
+                                      float cout[4]) {
   const double n = m[0];
   if (n < 4.0) {
     for (int k = 0; k < 4; ++k) cout[k] = cin[k];

@@ -13,6 +13,7 @@
 //   SampleConsensusModelPlane::isSampleGood + computeModelCoefficients -> k_build_hyps
 //   computeMeanAndCovarianceMatrix (fast mode, double)  -> k_moments
 #include "kernels.hpp"
+#include "host_math.hpp"
 
 #include <algorithm>
 #include <cfloat>
@@ -713,8 +714,11 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 template <bool NP>
-__global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, float4 cf, ModelTest mt,
-                                                   double3 sh, double* __restrict__ partials) {
+__global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, const float4* __restrict__ cfp,
+                                                   ModelTest mt, const SampleRec* __restrict__ shp,
+                                                   double* __restrict__ partials) {
+  const float4 cf = *cfp;
+  const double3 sh = make_double3((double)shp->x, (double)shp->y, (double)shp->z);
   const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   double acc[kMomentK];
 #pragma unroll
@@ -757,14 +761,34 @@ __global__ void k_reduce_partials(const double* __restrict__ partials, int nb,
   if (lane == 0) out[k] = v;
 }
 
+// fast refit on the device (one thread): moments -> double covariance -> pcl::eigen33 -> plane
+// through the centroid; < 4 inliers (or optimize off) keep the unrefined plane.  Keeps the
+// refined plane on the device for the final select (no host round trip between them).
+__global__ void k_refit_moments(const double* __restrict__ mom, const SampleRec* __restrict__ shp,
+                                const float4* __restrict__ cin, int optimize,
+                                float4* __restrict__ cout) {
+  if (threadIdx.x != 0) return;
+  const float4 c = *cin;
+  const float ci[4] = {c.x, c.y, c.z, c.w};
+  float co[4] = {c.x, c.y, c.z, c.w};
+  if (optimize) {
+    const double sh[3] = {(double)shp->x, (double)shp->y, (double)shp->z};
+    refit_from_moments(mom, sh, ci, co);
+  }
+  *cout = make_float4(co[0], co[1], co[2], co[3]);
+}
+
 // ---------------------------------------------------------------------------------------------
 // select / compact (selectWithinDistance + removal of the inliers from the active list)
 constexpr int kSelBS = 256;
 constexpr int kSelIt = kSelTile / kSelBS;
 
 template <bool NP>
-__global__ __launch_bounds__(kSelBS) void k_select_count(PointsView src, float4 cf, ModelTest mt,
+__global__ __launch_bounds__(kSelBS) void k_select_count(PointsView src,
+                                                         const float4* __restrict__ cfp,
+                                                         ModelTest mt,
                                                          int32_t* __restrict__ tile_in) {
+  const float4 cf = *cfp;
   const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   __shared__ int s_w[kSelBS / kWave];
   const int64_t base = (int64_t)blockIdx.x * kSelTile;
@@ -827,13 +851,16 @@ __global__ __launch_bounds__(kScanBS) void k_scan_tiles(const int32_t* __restric
 }
 
 template <bool NP>
-__global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src, float4 cf, ModelTest mt,
+__global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src,
+                                                           const float4* __restrict__ cfp,
+                                                           ModelTest mt,
                                                            const int32_t* __restrict__ off_in,
                                                            const int32_t* __restrict__ off_out,
                                                            int32_t* __restrict__ inl_gid,
                                                            float* __restrict__ inl_xyz,
                                                            PointsOut dst, int compact) {
   __shared__ int s_w[2][2][kSelBS / kWave];  // [buffer][in/out][wave]
+  const float4 cf = *cfp;
   const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   const int64_t base = (int64_t)blockIdx.x * kSelTile;
   const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
@@ -1159,8 +1186,14 @@ int moments_blocks(int64_t n) {
   return (int)b;
 }
 
-void launch_moments(PointsView src, float4 coef, const ModelTest& mt, double3 shift,
-                    double* partials, int nblocks, double* out, hipStream_t s) {
+void launch_refit_moments(const double* moments, const SampleRec* shift, const float4* cin,
+                          int optimize, float4* cout, hipStream_t s) {
+  hipLaunchKernelGGL(k_refit_moments, dim3(1), dim3(64), 0, s, moments, shift, cin, optimize, cout);
+}
+
+void launch_moments(PointsView src, const float4* coef, const ModelTest& mt,
+                    const SampleRec* shift, double* partials, int nblocks, double* out,
+                    hipStream_t s) {
   if (mt.normal_plane)
     hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
                        partials);
@@ -1172,7 +1205,7 @@ void launch_moments(PointsView src, float4 coef, const ModelTest& mt, double3 sh
 
 int select_tiles(int64_t n) { return (int)((n + kSelTile - 1) / kSelTile); }
 
-void launch_select(PointsView src, float4 coef, const ModelTest& mt, int32_t* tile_in,
+void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int32_t* tile_in,
                    int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid,
                    float* inl_xyz, const PointsOut* dst, hipStream_t s) {
   const int nt = select_tiles(src.n);

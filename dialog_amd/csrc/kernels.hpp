@@ -100,13 +100,19 @@ void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest&
 // moments (count + 9 sums, double, coordinates shifted by `shift`) of the inliers of coef;
 // partials [nblocks][10] -> out[10] (fixed-order reduction: deterministic)
 int moments_blocks(int64_t n);
-void launch_moments(PointsView src, float4 coef, const ModelTest& mt, double3 shift,
-                    double* partials, int nblocks, double* out, hipStream_t s);
+// coef: device float4 (a, b, c, d); shift: the device sample point the moments are centred on
+void launch_moments(PointsView src, const float4* coef, const ModelTest& mt,
+                    const SampleRec* shift, double* partials, int nblocks, double* out,
+                    hipStream_t s);
+// device fast refit: cout = plane of moments[10] (centred on shift), or cin when optimize == 0
+// or fewer than 4 inliers
+void launch_refit_moments(const double* moments, const SampleRec* shift, const float4* cin,
+                          int optimize, float4* cout, hipStream_t s);
 // select: inliers of coef in list order; optional inlier xyz (AoS, 3 floats); optional
 // compaction of the outliers (and their normals) into dst.  tile_in/out: [ntiles] scratch;
 // totals[2] = {in, out}.
 int select_tiles(int64_t n);
-void launch_select(PointsView src, float4 coef, const ModelTest& mt, int32_t* tile_in,
+void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int32_t* tile_in,
                    int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid,
                    float* inl_xyz, const PointsOut* dst, hipStream_t s);
 // raw caller normals (n records of stride_f floats, curvature at curv_off) gathered by the
