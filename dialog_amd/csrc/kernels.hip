@@ -178,14 +178,25 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
                                                  const float* __restrict__ Y,
                                                  const float* __restrict__ Z, int n,
                                                  const HypRec* __restrict__ hyps, int D,
-                                                 float cthr, int32_t* __restrict__ counts) {
+                                                 int slice_w, float cthr,
+                                                 int32_t* __restrict__ counts) {
   constexpr int kChunk = kScBS * P;
   __shared__ float4 s_coef[kHT + 1];  // +1: the prefetch of the group's last plane reads past
   __shared__ float2 s_band[KIND == kExact ? 1 : kHT + 1];
-  __shared__ int s_cnt[kMaxHypPerLaunch];
+  __shared__ int s_cnt[kHT];
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
-  for (int i = tid; i < D; i += kScBS) s_cnt[i] = 0;
+  // this workgroup's hypothesis slice [h0, h0 + nt): loaded once, kept in LDS for all chunks
+  const int h0 = blockIdx.y * slice_w;
+  const int nt = min(slice_w, D - h0);
+  for (int i = tid; i < nt; i += kScBS) {
+    s_cnt[i] = 0;
+    const HypRec hr = hyps[h0 + i];
+    s_coef[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
+    if (KIND == kBand) s_band[i] = make_float2(hr.tlo, hr.thi);
+    if (KIND == kMin3) s_band[i] = make_float2(hr.w, 0.0f);
+  }
+  __syncthreads();
   const int nchunks = (n + kChunk - 1) / kChunk;
   const float qnan = __builtin_nanf("");
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
@@ -198,16 +209,8 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
       py[j] = ok ? Y[e] : qnan;
       pz[j] = ok ? Z[e] : qnan;
     }
-    for (int t0 = 0; t0 < D; t0 += kHT) {
-      const int nt = min(kHT, D - t0);
-      __syncthreads();
-      for (int i = tid; i < nt; i += kScBS) {
-        const HypRec hr = hyps[t0 + i];
-        s_coef[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
-        if (KIND == kBand) s_band[i] = make_float2(hr.tlo, hr.thi);
-        if (KIND == kMin3) s_band[i] = make_float2(hr.w, 0.0f);
-      }
-      __syncthreads();
+    {
+      constexpr int t0 = 0;
       for (int g0 = 0; g0 < nt; g0 += kWave) {  // nt is a multiple of 64 (D padded with NaN planes)
         int my = 0;
         // software pipeline: the next hypothesis' LDS broadcast read is in flight while the
@@ -276,9 +279,9 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
     }
   }
   __syncthreads();
-  for (int i = tid; i < D; i += kScBS) {
+  for (int i = tid; i < nt; i += kScBS) {
     int v = s_cnt[i];
-    if (v) atomicAdd(&counts[i], v);
+    if (v) atomicAdd(&counts[h0 + i], v);
   }
 }
 
@@ -1083,12 +1086,21 @@ static void launch_score_t(PointsView src, const HypRec* hyps, int D, float cthr
   constexpr int kChunk = kScBS * P;
   D = (D + kWave - 1) / kWave * kWave;  // hyps[D..Dp) are NaN planes; counts has room
   const int64_t nchunks = (src.n + kChunk - 1) / kChunk;
-  // resident capacity: <= 40 KB LDS per 8-wave workgroup -> 4 workgroups (32 waves) per CU
+  // resident capacity: 4 workgroups (32 waves) per CU.  Work units = (point chunk, hypothesis
+  // slice): slices of <= 1024 planes (one LDS load per workgroup), narrowed while there are too
+  // few units to fill the chip several times over (small active lists in late extract rounds),
+  // and the workgroups of a slice stride over the chunks -- the tail of a launch is at most one
+  // chunk of one slice.
   const int64_t cap = (int64_t)num_cus * 4;
-  const int64_t per = (nchunks + cap - 1) / cap;  // chunks per workgroup (balanced grid)
-  const unsigned grid = (unsigned)((nchunks + per - 1) / per);
-  hipLaunchKernelGGL((k_score<KIND, P>), dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
-                     (int)src.n, hyps, D, cthr, counts);
+  int w = std::min(D, kHT);
+  while (w > kWave && nchunks * ((D + w - 1) / w) < 4 * cap) w = std::max(kWave, (w / 2) / kWave * kWave);
+  const int slices = (D + w - 1) / w;
+  int64_t bx = std::max<int64_t>(1, cap / slices);
+  bx = std::min<int64_t>(bx, nchunks);
+  const int64_t per = (nchunks + bx - 1) / bx;  // chunks per workgroup, balanced
+  bx = (nchunks + per - 1) / per;
+  hipLaunchKernelGGL((k_score<KIND, P>), dim3((unsigned)bx, (unsigned)slices), dim3(kScBS), 0, s,
+                     src.x, src.y, src.z, (int)src.n, hyps, D, w, cthr, counts);
 }
 
 template <int KIND, int P, int GH>
