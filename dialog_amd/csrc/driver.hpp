@@ -86,11 +86,12 @@ struct SoA {
 // one sorted grid of the normals path (normals.hip): points in cell order + occupied-cell table
 struct GridLevelBufs {
   DevBuf<float> sx, sy, sz;
-  DevBuf<int32_t> idx;
+  DevBuf<int32_t> idx, pos;
   DevBuf<uint32_t> tkeys;
   DevBuf<int2> trange;
   void release() {
-    sx.release(); sy.release(); sz.release(); idx.release(); tkeys.release(); trange.release();
+    sx.release(); sy.release(); sz.release(); idx.release(); pos.release(); tkeys.release();
+    trange.release();
   }
 };
 

@@ -48,6 +48,22 @@ __device__ __forceinline__ uint32_t hash_key(uint32_t k) {
   return k;
 }
 
+// append val to out[] for every lane with pred: one global atomic per wavefront (a single
+// hot counter serialises at the L2 when every lane hits it).  All lanes of the wave must call.
+__device__ __forceinline__ void wave_append(bool pred, int32_t val, int32_t* __restrict__ out,
+                                            uint32_t* __restrict__ counter) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (pred) out[base + below] = val;
+}
+
 __device__ __forceinline__ bool finite3(float x, float y, float z) {
   return isfinite(x) && isfinite(y) && isfinite(z);
 }
@@ -142,16 +158,26 @@ __global__ __launch_bounds__(kBS) void k_cells_build(
 }
 
 // the last point of each cell run writes the run's end (separate launch: the begin must exist)
+// ... and adds occupancy^2 of its cell to sumsq (sum over points of their cell's occupancy: the
+// point-weighted occupancy the k-NN cell size is tuned on; sparse outlier cells barely count)
 __global__ __launch_bounds__(kBS) void k_cells_end(const uint32_t* __restrict__ skeys, int n,
                                                    uint32_t ncells, const uint32_t* __restrict__ tkeys,
-                                                   int2* __restrict__ trange, uint32_t tmask) {
+                                                   int2* __restrict__ trange, uint32_t tmask,
+                                                   unsigned long long* __restrict__ sumsq) {
   const int t = blockIdx.x * kBS + threadIdx.x;
-  if (t >= n) return;
-  const uint32_t k = skeys[t];
-  if (k == ncells || (t + 1 < n && skeys[t + 1] == k)) return;
-  uint32_t h = hash_key(k) & tmask;
-  while (tkeys[h] != k) h = (h + 1) & tmask;
-  trange[h].y = t + 1;
+  unsigned long long sq = 0;
+  if (t < n) {
+    const uint32_t k = skeys[t];
+    if (k != ncells && !(t + 1 < n && skeys[t + 1] == k)) {
+      uint32_t h = hash_key(k) & tmask;
+      while (tkeys[h] != k) h = (h + 1) & tmask;
+      trange[h].y = t + 1;
+      const unsigned long long occ = (unsigned long long)(t + 1 - trange[h].x);
+      sq = occ * occ;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+  if ((threadIdx.x & 63) == 0 && sq) atomicAdd(sumsq, sq);
 }
 
 __device__ __forceinline__ int2 cell_range(const uint32_t* __restrict__ tkeys,
@@ -307,25 +333,23 @@ __global__ __launch_bounds__(kBS) void k_normals_radius(
 // the top level the 27 cells are the whole cloud and every candidate counts.  One launch per
 // level over the queries still open (compacted), so the few sparse outliers that climb do not
 // hold back the wavefronts of the surface points, which finish at level 0.
+// Queries are taken in the level's own cell order (qpos = sorted positions at level l; nullptr =
+// all), so the lanes of a wavefront scan the same cells; a deferred query is flagged at its
+// sorted position of level l + 1 and the next pass compacts the flags in that order.
 template <int KP>
 __global__ __launch_bounds__(kBS) void k_normals_knn(
-    KnnLevels L, int l, const int32_t* __restrict__ qlist, int nq, const float* __restrict__ X,
+    KnnLevels L, int l, const int32_t* __restrict__ qpos, int nq, const float* __restrict__ X,
     const float* __restrict__ Y, const float* __restrict__ Z, int K, float vpx, float vpy,
-    float vpz, float4* __restrict__ normals, int32_t* __restrict__ next,
-    uint32_t* __restrict__ n_next) {
+    float vpz, float4* __restrict__ normals, uint8_t* __restrict__ defer_next) {
   const int t = blockIdx.x * kBS + threadIdx.x;
   if (t >= nq) return;
-  int qi;
-  float qx, qy, qz;
-  if (qlist) {
-    qi = qlist[t];
-    qx = X[qi]; qy = Y[qi]; qz = Z[qi];
-  } else {  // level 0: every query, in level-0 cell order (wavefronts share cells)
-    qi = L.idx[0][t];
-    qx = L.sx[0][t]; qy = L.sy[0][t]; qz = L.sz[0][t];
-  }
+  const int uq = qpos ? qpos[t] : t;
+  const int qi = L.idx[l][uq];
+  const float qx = L.sx[l][uq], qy = L.sy[l][uq], qz = L.sz[l][uq];
+  const bool active = true;
   Moments M;
-  if (finite3(qx, qy, qz)) {
+  bool defer = false;
+  if (active && finite3(qx, qy, qz)) {
     const GridDesc& G = L.G[l];
     const bool top = l == L.levels - 1;
     const float lim = top ? INFINITY : G.cell * G.cell;
@@ -371,19 +395,25 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
               if (j == K - 1) { kd = bd[j]; ki = bi[j]; }
           }
         }
-    if (cnt < K && !top) {
-      next[atomicAdd(n_next, 1u)] = qi;
-      return;
-    }
-    const int m = cnt < K ? cnt : K;
+    defer = cnt < K && !top;
+    if (!defer) {
+      const int m = cnt < K ? cnt : K;
 #pragma unroll
-    for (int j = 0; j < KP; ++j)
-      if (j < m) {
-        const int i = bi[j];
-        M.add(X[i], Y[i], Z[i], qx, qy, qz);
-      }
+      for (int j = 0; j < KP; ++j)
+        if (j < m) {
+          const int i = bi[j];
+          M.add(X[i], Y[i], Z[i], qx, qy, qz);
+        }
+    }
   }
-  normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+  if (defer) defer_next[L.pos_of[l + 1][qi]] = 1;
+  else normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+}
+
+__global__ __launch_bounds__(kBS) void k_inverse_perm(const int32_t* __restrict__ idx, int n,
+                                                      int32_t* __restrict__ pos_of) {
+  const int u = blockIdx.x * kBS + threadIdx.x;
+  if (u < n) pos_of[idx[u]] = u;
 }
 
 // nearest neighbour of external queries over the grid hierarchy (same level rule as
@@ -395,13 +425,12 @@ __global__ __launch_bounds__(kBS) void k_nn1(KnnLevels L, int l, const int32_t* 
                                              int32_t* __restrict__ nn, int32_t* __restrict__ next,
                                              uint32_t* __restrict__ n_next) {
   const int t = blockIdx.x * kBS + threadIdx.x;
-  if (t >= nq) return;
-  const int qi = qlist ? qlist[t] : t;
-  const float qx = QX[qi], qy = QY[qi], qz = QZ[qi];
-  if (!finite3(qx, qy, qz)) {
-    nn[qi] = -1;
-    return;
-  }
+  const bool active = t < nq;
+  const int qi = active ? (qlist ? qlist[t] : t) : 0;
+  const float qx = active ? QX[qi] : 0.0f, qy = active ? QY[qi] : 0.0f,
+              qz = active ? QZ[qi] : 0.0f;
+  const bool ok = active && finite3(qx, qy, qz);
+  if (active && !ok) nn[qi] = -1;
   const GridDesc& G = L.G[l];
   const bool top = l == L.levels - 1;
   const float lim = top ? INFINITY : G.cell * G.cell;
@@ -410,6 +439,7 @@ __global__ __launch_bounds__(kBS) void k_nn1(KnnLevels L, int l, const int32_t* 
   const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
   const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
   const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+  if (ok)
   for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
     for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
       for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
@@ -421,11 +451,9 @@ __global__ __launch_bounds__(kBS) void k_nn1(KnnLevels L, int l, const int32_t* 
           if (d2 < bd || iu < bi) { bd = d2; bi = iu; }
         }
       }
-  if (bi == INT_MAX && !top) {
-    next[atomicAdd(n_next, 1u)] = qi;
-    return;
-  }
-  nn[qi] = bi == INT_MAX ? -1 : bi;
+  const bool defer = ok && bi == INT_MAX && !top;
+  wave_append(defer, qi, next, n_next);
+  if (ok && !defer) nn[qi] = bi == INT_MAX ? -1 : bi;
 }
 
 // PlaneDetect.h:565-578: Eigen Vector3f dot (not vectorised: (a0 b0 + a1 b1) + a2 b2)
@@ -519,11 +547,11 @@ __global__ __launch_bounds__(kBS) void k_mis_round(
     uint32_t tmask, float r2, uint8_t* state, int32_t* __restrict__ next,
     uint32_t* __restrict__ n_next) {
   const int t = blockIdx.x * kBS + threadIdx.x;
-  if (t >= nq) return;
-  const int u = qlist ? qlist[t] : t;
-  const int j = sidx[u];
-  const float qx = sx[u], qy = sy[u], qz = sz[u];
-  bool kept_nb = false, all_removed = true;
+  const bool active = t < nq;
+  const int u = active ? (qlist ? qlist[t] : t) : 0;
+  const int j = active ? sidx[u] : 0;
+  const float qx = active ? sx[u] : 0.0f, qy = active ? sy[u] : 0.0f, qz = active ? sz[u] : 0.0f;
+  bool kept_nb = !active, all_removed = true;
   const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
   const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
   const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
@@ -539,13 +567,12 @@ __global__ __launch_bounds__(kBS) void k_mis_round(
           if (st == 0) all_removed = false;
         }
       }
-  if (kept_nb) {
+  if (active && kept_nb) {
     __hip_atomic_store(&state[u], (uint8_t)2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (all_removed) {
+  } else if (active && all_removed) {
     __hip_atomic_store(&state[u], (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    next[atomicAdd(n_next, 1u)] = u;
   }
+  wave_append(active && !kept_nb && !all_removed, u, next, n_next);
 }
 
 // kept[point] = state[sorted position] == 1
@@ -610,26 +637,46 @@ __global__ __launch_bounds__(kBS) void k_bfs_claim(
     GridDesc G, const uint32_t* __restrict__ tkeys, const int2* __restrict__ trange,
     uint32_t tmask, float r2, const uint8_t* __restrict__ processed_s,
     uint32_t* __restrict__ claim_s, int32_t* __restrict__ cand, uint32_t* __restrict__ ncand) {
+  // first claims are staged in LDS and appended with one global atomic per workgroup
+  constexpr int kStage = 2048;
+  __shared__ uint32_t s_n, s_base;
+  __shared__ int32_t s_buf[kStage];
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * kBS + threadIdx.x;
-  if (t >= (int64_t)nf * 27) return;
-  const int f = (int)(t / 27), c = (int)(t % 27);
+  bool go = t < (int64_t)nf * 27;
+  const int f = go ? (int)(t / 27) : 0, c = go ? (int)(t % 27) : 0;
   const uint32_t mypos = (uint32_t)(fbase + f);
-  const int cu = pos_of[queue[mypos]];
-  const float qx = sx[cu], qy = sy[cu], qz = sz[cu];
-  if (!finite3(qx, qy, qz)) return;
+  float qx = 0.0f, qy = 0.0f, qz = 0.0f;
+  if (go) {
+    const int cu = pos_of[queue[mypos]];
+    qx = sx[cu]; qy = sy[cu]; qz = sz[cu];
+    go = finite3(qx, qy, qz);
+  }
   const int x = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]) + c % 3 - 1;
   const int y = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]) + (c / 3) % 3 - 1;
   const int z = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]) + c / 9 - 1;
-  if (x < 0 || y < 0 || z < 0 || x >= G.g[0] || y >= G.g[1] || z >= G.g[2]) return;
-  const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
-  for (int u = rg.x; u < rg.y; ++u) {
-    if (processed_s[u]) continue;
-    if (flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2) {
-      // claims only decrease: a plain read filters most of the contended atomics
-      if (claim_s[u] <= mypos) continue;
-      if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) cand[atomicAdd(ncand, 1u)] = u;
+  go = go && !(x < 0 || y < 0 || z < 0 || x >= G.g[0] || y >= G.g[1] || z >= G.g[2]);
+  if (go) {
+    const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+    for (int u = rg.x; u < rg.y; ++u) {
+      if (processed_s[u]) continue;
+      if (flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2) {
+        // claims only decrease: a plain read filters most of the contended atomics
+        if (claim_s[u] <= mypos) continue;
+        if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) {
+          const uint32_t p = atomicAdd(&s_n, 1u);
+          if (p < (uint32_t)kStage) s_buf[p] = u;
+          else cand[atomicAdd(ncand, 1u)] = u;  // overflow (rare): direct
+        }
+      }
     }
   }
+  __syncthreads();
+  const uint32_t m = min(s_n, (uint32_t)kStage);
+  if (threadIdx.x == 0 && m) s_base = atomicAdd(ncand, m);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += kBS) cand[s_base + i] = s_buf[i];
 }
 
 // settle the newly reached nodes: flip against the claiming parent (PlaneDetect.h:624-636),
@@ -730,7 +777,7 @@ hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, con
                       GridBufs& B, uint32_t* n_occupied, hipStream_t s) {
   hipError_t e = hipMemsetAsync(B.tkeys, 0xff, (size_t)(B.tmask + 1) * 4, s);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(n_occupied, 0, 4, s);
+  e = hipMemsetAsync(n_occupied, 0, 16, s);  // [0] occupied cells, [2..3] sum of occupancy^2
   if (e != hipSuccess || n <= 0) return e;
   hipLaunchKernelGGL(k_cell_keys, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, X, Y, Z, n, G, B.keys_in,
                      B.idx_in);
@@ -741,7 +788,8 @@ hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, con
   hipLaunchKernelGGL(k_cells_build, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.keys_out, B.idx_out, n,
                      G.ncells, X, Y, Z, B.tkeys, B.trange, B.tmask, B.sx, B.sy, B.sz, n_occupied);
   hipLaunchKernelGGL(k_cells_end, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.keys_out, n, G.ncells,
-                     B.tkeys, B.trange, B.tmask);
+                     B.tkeys, B.trange, B.tmask,
+                     reinterpret_cast<unsigned long long*>(n_occupied + 2));
   return hipGetLastError();
 }
 
@@ -753,26 +801,31 @@ void launch_normals_radius(const GridDesc& G, const GridBufs& B, int n, float r2
                      normals);
 }
 
-void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qlist, int nq,
+void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
-                        float4* normals, int32_t* next, uint32_t* n_next, hipStream_t s) {
+                        float4* normals, uint8_t* defer_next, hipStream_t s) {
   if (nq <= 0) return;
   const dim3 g(cdiv(nq, kBS)), b(kBS);
   if (k <= 8)
-    hipLaunchKernelGGL(k_normals_knn<8>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, next, n_next);
+    hipLaunchKernelGGL(k_normals_knn<8>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, defer_next);
   else if (k <= 16)
-    hipLaunchKernelGGL(k_normals_knn<16>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, next, n_next);
+    hipLaunchKernelGGL(k_normals_knn<16>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, defer_next);
   else if (k <= 24)
-    hipLaunchKernelGGL(k_normals_knn<24>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, next, n_next);
+    hipLaunchKernelGGL(k_normals_knn<24>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, defer_next);
   else if (k <= 32)
-    hipLaunchKernelGGL(k_normals_knn<32>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, next, n_next);
+    hipLaunchKernelGGL(k_normals_knn<32>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, defer_next);
   else
-    hipLaunchKernelGGL(k_normals_knn<64>, g, b, 0, s, L, level, qlist, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, next, n_next);
+    hipLaunchKernelGGL(k_normals_knn<64>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
+                       vp[2], normals, defer_next);
+}
+
+void launch_inverse_perm(const int32_t* idx, int n, int32_t* pos_of, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_inverse_perm, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, idx, n, pos_of);
 }
 
 void launch_nn1(const KnnLevels& L, int level, const int32_t* qlist, int nq, const float* qx,

@@ -45,7 +45,8 @@ void launch_bbox(const float* X, const float* Y, const float* Z, int n, float* p
                  hipStream_t s);
 
 size_t sort_tmp_bytes(int n, int key_bits);
-// sort by cell, fill the cell table; *n_occupied (device) = number of occupied cells
+// sort by cell, fill the cell table; n_occupied (device, 16 B): [0] = occupied cells,
+// [2..3] = uint64 sum over cells of occupancy^2
 hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, const GridDesc& G,
                       GridBufs& B, uint32_t* n_occupied, hipStream_t s);
 // strided host-layout xyz records (uploaded raw) -> SoA
@@ -65,15 +66,20 @@ struct KnnLevels {
   const float* sy[kMaxLevels];
   const float* sz[kMaxLevels];
   const int32_t* idx[kMaxLevels];
+  const int32_t* pos_of[kMaxLevels];  // inverse of idx: point -> sorted position
   const uint32_t* tkeys[kMaxLevels];
   const int2* trange[kMaxLevels];
   uint32_t tmask[kMaxLevels];
 };
 // one level: queries qlist[0..nq) (nullptr at level 0: every point, level-0 order); queries with
 // fewer than k neighbours inside the level's guaranteed radius are appended to next[]
-void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qlist, int nq,
+// one level: queries = sorted positions qpos[0..nq) of level `level` (nullptr: all of them);
+// a query with fewer than k neighbours inside the level's guaranteed radius sets
+// defer_next[its sorted position at level + 1]
+void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
-                        float4* normals, int32_t* next, uint32_t* n_next, hipStream_t s);
+                        float4* normals, uint8_t* defer_next, hipStream_t s);
+void launch_inverse_perm(const int32_t* idx, int n, int32_t* pos_of, hipStream_t s);
 
 // nearest neighbour (k = 1, ties -> lowest index) in the hierarchy's cloud of external queries
 // (qx, qy, qz)[qlist or 0..nq); unresolved queries go to next[] for the level above

@@ -87,8 +87,10 @@ GridDesc make_grid(const BBox& b, double cell) {
 }
 
 // builds grid level `lv` over (X, Y, Z) (default nw.x/y/z); returns the number of occupied cells
+// (and the point-weighted mean occupancy sum(occ^2) / n in *pw_occ)
 uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B,
-                    const float* X = nullptr, const float* Y = nullptr, const float* Z = nullptr) {
+                    const float* X = nullptr, const float* Y = nullptr, const float* Z = nullptr,
+                    double* pw_occ = nullptr) {
   NormalsWork& w = c->nw;
   GridLevelBufs& L = w.lv[lv];
   w.keys_in.ensure(n); w.keys_out.ensure(n); w.idx_in.ensure(n);
@@ -100,8 +102,8 @@ uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B,
   L.trange.ensure(tcap);
   const size_t tmp = sort_tmp_bytes(n, G.key_bits);
   w.sort_tmp.ensure(tmp);
-  w.counters.ensure(4);
-  w.h_cnt.ensure(4);
+  w.counters.ensure(8);
+  w.h_cnt.ensure(8);
   B->keys_in = w.keys_in.p; B->keys_out = w.keys_out.p;
   B->idx_in = w.idx_in.p; B->idx_out = L.idx.p;
   B->sx = L.sx.p; B->sy = L.sy.p; B->sz = L.sz.p;
@@ -109,8 +111,13 @@ uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B,
   B->sort_tmp = w.sort_tmp.p; B->sort_tmp_bytes = w.sort_tmp.cap;
   HIPCHK(grid_build(X ? X : w.x.p, Y ? Y : w.y.p, Z ? Z : w.z.p, n, G, *B, w.counters.p,
                     c->stream));
-  HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 16, hipMemcpyDeviceToHost, c->stream));
   sync(c);
+  if (pw_occ) {
+    unsigned long long sq;
+    std::memcpy(&sq, w.h_cnt.p + 2, 8);
+    *pw_occ = n > 0 ? (double)sq / (double)n : 0.0;
+  }
   return w.h_cnt.p[0];
 }
 
@@ -130,13 +137,15 @@ KnnLevels build_hierarchy(dlg_ctx* c, int n, const BBox& b, int k_nn) {
   for (int k = 0; k < 3; ++k) vol *= std::max(ext[k], maxe * 1e-3);
   double cell = std::cbrt(vol * k_nn / n);
   GridDesc G = make_grid(b, cell);
-  const uint32_t occ = build_grid(c, n, G, 0, &B);
+  // tune on the point-weighted occupancy (what a typical query sees; sparse outlier cells do
+  // not drag it down), assuming surface-like scaling occ ~ cell^2; two corrections at most
   const double target = std::max(2.0, k_nn / 2.0);
-  const double avg = occ ? (double)n / occ : target;
-  if (avg > 2.0 * target || avg < 0.5 * target) {
-    cell *= std::sqrt(target / avg);
+  for (int it = 0; it < 3; ++it) {
+    double pw = 0.0;
+    build_grid(c, n, G, 0, &B, nullptr, nullptr, nullptr, &pw);
+    if (it == 2 || pw <= 0.0 || (pw <= 2.0 * target && pw >= 0.5 * target)) break;
+    cell *= std::sqrt(target / pw);
     G = make_grid(b, cell);
-    build_grid(c, n, G, 0, &B);
   }
   KnnLevels L;
   L.levels = 0;
@@ -155,6 +164,9 @@ KnnLevels build_hierarchy(dlg_ctx* c, int n, const BBox& b, int k_nn) {
     }
     L.G[l] = G;
     L.sx[l] = BL.sx; L.sy[l] = BL.sy; L.sz[l] = BL.sz; L.idx[l] = BL.idx_out;
+    c->nw.lv[l].pos.ensure(n);
+    launch_inverse_perm(BL.idx_out, n, c->nw.lv[l].pos.p, c->stream);
+    L.pos_of[l] = c->nw.lv[l].pos.p;
     L.tkeys[l] = BL.tkeys; L.trange[l] = BL.trange; L.tmask[l] = BL.tmask;
     L.levels = l + 1;
     if (last) break;
@@ -195,20 +207,23 @@ void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
   } else {
     const KnnLevels L = build_hierarchy(c, n, b, k_nn);
     w.queue.ensure(n);
-    w.cand.ensure(n);
-    int32_t* qin = nullptr;
-    int32_t* qout = w.queue.p;
+    w.processed.ensure(n);
+    w.sort_tmp.ensure(select_tmp_bytes(n));
+    const int32_t* qpos = nullptr;  // level 0: every point
     int nq = n;
     for (int l = 0; l < L.levels && nq > 0; ++l) {
-      HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
-      launch_normals_knn(L, l, qin, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, qout,
-                         w.counters.p, c->stream);
-      if (l == L.levels - 1) break;
+      const bool top = l == L.levels - 1;
+      if (!top) HIPCHK(hipMemsetAsync(w.processed.p, 0, n, c->stream));
+      launch_normals_knn(L, l, qpos, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, w.processed.p,
+                         c->stream);
+      if (top) break;
+      // deferred queries in level l+1's cell order
+      HIPCHK(select_flagged(w.sort_tmp.p, w.sort_tmp.cap, w.processed.p, n, w.queue.p,
+                            w.counters.p, c->stream));
       HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
       sync(c);
       nq = (int)w.h_cnt.p[0];
-      qin = qout;
-      qout = qout == w.queue.p ? w.cand.p : w.queue.p;
+      qpos = w.queue.p;
     }
   }
   HIPCHK(hipGetLastError());
@@ -257,8 +272,8 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   w.keys_alt.ensure(n);
   const size_t stmp = bfs_sort_tmp_bytes(n);
   w.sort_tmp.ensure(stmp);
-  w.counters.ensure(4);
-  w.h_cnt.ensure(4);
+  w.counters.ensure(8);
+  w.h_cnt.ensure(8);
   HIPCHK(hipMemsetAsync(w.processed_s.p, 0, n, c->stream));
   HIPCHK(hipMemsetAsync(w.claim.p, 0xff, (size_t)n * 4, c->stream));
   launch_bfs_prepare(B, n, w.nrm.p, w.nrm_s.p, w.pos_of.p, c->stream);
@@ -366,8 +381,8 @@ int64_t preprocess(dlg_ctx* c, const dlg_points* pts, int translate, float min_d
   // 1. removeNaNFromPointCloud: ascending indices of the finite points
   w.processed.ensure(n0);
   w.ids.ensure(n0);
-  w.counters.ensure(4);
-  w.h_cnt.ensure(4);
+  w.counters.ensure(8);
+  w.h_cnt.ensure(8);
   w.sort_tmp.ensure(select_tmp_bytes(n0));
   launch_finite_flags(w.x.p, w.y.p, w.z.p, n0, w.processed.p, c->stream);
   HIPCHK(select_flagged(w.sort_tmp.p, w.sort_tmp.cap, w.processed.p, n0, w.ids.p, w.counters.p,
