@@ -30,15 +30,15 @@ for s in $STEPS; do
     nprof)  run nprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nprof -o run -- python3 tools/bench_normals.py 10000000 2 ;;
     trace)  DLG_TRACE=1 run trace 300 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     benchtorch) run bench_torch 600 python3 bench.py --torch-dist --no-cpu-baseline --steps 2 ;;
-    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --steps 3 ;;
-    pmc)    run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 ;;
+    pmc)    run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 1 --warmup 0 ;;
     ab)     run score_ab 600 python3 tools/score_ab.py ;;
     list)   run counters 120 rocprofv3 -L ;;
     sqpmc)  VARIANTS="${VARIANTS:-0,2}" run sqpmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \
             VARIANTS="${VARIANTS:-0,2}" run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM GRBM_COUNT --output-format csv -d gpurun_out/sqpmc2 -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
     mpmc)   VARIANTS="${VARIANTS:-5,12}" run mpmc1 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_SALU SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/mpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \
             VARIANTS="${VARIANTS:-5,12}" run mpmc2 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVES --output-format csv -d gpurun_out/mpmc2 -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
-    pmcw)   run pmcw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o run -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ;;
+    pmcw)   run pmcw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 1 --warmup 0 ;;
     *) echo "unknown step $s" ;;
   esac
 done
