@@ -1099,6 +1099,10 @@ static void launch_score_t(PointsView src, const HypRec* hyps, int D, float cthr
   bx = std::min<int64_t>(bx, nchunks);
   const int64_t per = (nchunks + bx - 1) / bx;  // chunks per workgroup, balanced
   bx = (nchunks + per - 1) / per;
+  // XCD-aware: workgroups are dealt round-robin to the 8 XCDs by linear id bx + by * gridDim.x,
+  // so with gridDim.x a multiple of 8 the slices of one chunk run on the same XCD at the same
+  // time and share its L2 (the chunk is fetched from HBM once, not once per slice)
+  if (slices > 1 && bx >= 8) bx = std::min<int64_t>((bx + 7) / 8 * 8, std::max<int64_t>(8, cap / slices / 8 * 8));
   hipLaunchKernelGGL((k_score<KIND, P>), dim3((unsigned)bx, (unsigned)slices), dim3(kScBS), 0, s,
                      src.x, src.y, src.z, (int)src.n, hyps, D, w, cthr, counts);
 }
