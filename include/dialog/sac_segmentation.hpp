@@ -12,7 +12,8 @@
 //   * estimateNormal() (PlaneDetect.h:515-545, pcl::NormalEstimationOMP with a radius; k = 20 at
 //     PCLViewer.cpp:507-522) -> dialog::NormalEstimation<PointT, pcl::Normal>;
 //   * regulateNormal() (PlaneDetect.h:547-665) -> dialog::regulateNormals (first round) and
-//     dialog::orientNormalsToBackup (later rounds).
+//     dialog::orientNormalsToBackup (later rounds);
+//   * preProcess() (PlaneDetect.h:448-512) -> dialog::preProcess.
 // With real PCL available define DIALOG_HAVE_PCL before including; otherwise minimal
 // layout-identical stand-ins for pcl::PointXYZ (16 B), pcl::Normal (32 B), pcl::PointCloud,
 // pcl::ModelCoefficients and pcl::PointIndices are declared here.
@@ -292,6 +293,33 @@ inline void orientNormalsToBackup(const pcl::PointCloud<PointT>& cloud, pcl::Poi
                               backup_normals.points.empty() ? nullptr : &backup_normals.points[0].normal_x,
                               (int64_t)sizeof(PointNT)),
         c);
+}
+
+// preProcess() (PlaneDetect.h:448-512) / removeRedundantPoints (PCLViewer.cpp:781-805): NaN
+// removal, optional translation to the centroid (returned in *translation), redundancy removal
+// with min_dist_between_points.  out: the kept points (translated); kept_index: their input index.
+template <typename PointT>
+inline void preProcess(const pcl::PointCloud<PointT>& cloud, bool translate, float min_dist,
+                       pcl::PointCloud<PointT>& out, std::vector<int>* kept_index = nullptr,
+                       float translation[3] = nullptr, Context* ctx = nullptr) {
+  static_assert(sizeof(PointT) == 16, "preProcess writes pcl::PointXYZ records");
+  out.points.clear();
+  if (kept_index) kept_index->clear();
+  if (cloud.points.empty()) return;
+  dlg_ctx* c = (ctx ? ctx : &Context::thread_default())->get();
+  dlg_points pts{&cloud.points[0].x, (int64_t)cloud.points.size(), (int64_t)sizeof(PointT)};
+  out.points.resize(cloud.points.size());
+  std::vector<int32_t> idx(cloud.points.size());
+  int64_t n = 0;
+  float tr[3];
+  check(dlg_preprocess(c, &pts, translate ? 1 : 0, min_dist, &out.points[0].x, (int64_t)sizeof(PointT),
+                       idx.data(), (int64_t)idx.size(), &n, tr),
+        c);
+  out.points.resize((size_t)n);
+  out.width = (uint32_t)n;
+  out.height = 1;
+  if (kept_index) kept_index->assign(idx.begin(), idx.begin() + n);
+  if (translation) { translation[0] = tr[0]; translation[1] = tr[1]; translation[2] = tr[2]; }
 }
 
 // Result of the plane stage for one plane: coefficients (a, b, c, d) and inlier ids.  The

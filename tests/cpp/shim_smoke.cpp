@@ -51,6 +51,11 @@ int main(int argc, char** argv) {
     segn.segment(inl_n, coeff_n);
     std::printf("normals %zu reached %lld np_inliers %zu\n", normals->points.size(), (long long)reached,
                 inl_n.indices.size());
+    pcl::PointCloud<pcl::PointXYZ> pre;
+    std::vector<int> kept;
+    float tr[3];
+    dialog::preProcess(*cloud, true, 0.15f, pre, &kept, tr);
+    std::printf("preprocess %zu %zu\n", pre.points.size(), kept.size());
     return 0;
   } catch (const dialog::Error& e) {
     std::fprintf(stderr, "dialog error: %s\n", e.what());

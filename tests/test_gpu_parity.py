@@ -238,6 +238,8 @@ def test_cpp_shim_runs_on_gpu(tmp_path):
     lines = dict(ln.split(" ", 1) for ln in out.stdout.strip().splitlines())
     nrm = lines["normals"].split()
     assert int(nrm[0]) == 64 * 64 + 500 and int(nrm[2]) > 0 and int(nrm[4]) > 0
+    pre = lines["preprocess"].split()
+    assert 0 < int(pre[0]) == int(pre[1]) < 64 * 64 + 500
 
 
 def test_rccl_one_rank_path(monkeypatch, gpu_ctx):
