@@ -104,7 +104,10 @@ struct NormalsWork {
   DevBuf<uint32_t> keys_in, keys_out, counters;
   DevBuf<int32_t> idx_in, queue, cand, ids, ids_alt, pos_of, nn;
   DevBuf<float4> nrm, nrm_s;
-  DevBuf<uint32_t> claim;
+  DevBuf<uint32_t> claim, ccnt, coffs, ccur, ctile, cslot;
+  DevBuf<float> sd2;
+  DevBuf<long long> bst;
+  PinBuf<long long> h_bst;
   DevBuf<unsigned long long> keys64, keys_alt;
   PinBuf<uint32_t> h_cnt;
   void release() {
@@ -114,7 +117,9 @@ struct NormalsWork {
     partial.release(); nn.release();
     keys_in.release(); keys_out.release(); counters.release();
     idx_in.release(); queue.release(); cand.release(); ids.release(); ids_alt.release();
-    pos_of.release(); nrm.release(); nrm_s.release(); claim.release(); keys64.release(); keys_alt.release(); h_cnt.release();
+    pos_of.release(); nrm.release(); nrm_s.release(); claim.release(); keys64.release();
+    keys_alt.release(); h_cnt.release(); ccnt.release(); coffs.release(); ccur.release();
+    sd2.release(); bst.release(); h_bst.release(); ctile.release(); cslot.release();
   }
 };
 

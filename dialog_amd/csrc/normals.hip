@@ -19,8 +19,10 @@
 // RegulateNormal: level-synchronous BFS that reproduces PCL's sequential queue exactly.  In the
 // sequential BFS a node is claimed by the first popped node (queue order) having it within
 // r_regulate; levels are contiguous in the queue, so a node is claimed by the smallest queue
-// position of the current level that reaches it (64-bit atomicMin), and the next level is ordered
-// as PCL pushes it: by parent position, then by the parent's neighbour-list order (d2, index).
+// position of the current level that reaches it (32-bit atomicMin), and the next level is
+// ordered as PCL pushes it: by parent position (counting sort: children per parent, scanned),
+// then by the parent's neighbour-list order (d2, index) (rank among the siblings).  All level
+// state stays on the device; the host only polls the level size every 16 levels.
 // A node flips iff dot(parent normal, node normal) < 0 in float, left to right (PlaneDetect.h:629).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -630,81 +632,201 @@ __global__ void k_bfs_seed(int32_t seed, int flip, const int32_t* __restrict__ p
   queue[0] = seed;
 }
 
-// one thread per (frontier node, one of its 27 cells): short dependent chains, 27x the threads
-__global__ __launch_bounds__(kBS) void k_bfs_claim(
-    const int32_t* __restrict__ queue, int64_t fbase, int nf, const int32_t* __restrict__ pos_of,
-    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
-    GridDesc G, const uint32_t* __restrict__ tkeys, const int2* __restrict__ trange,
-    uint32_t tmask, float r2, const uint8_t* __restrict__ processed_s,
-    uint32_t* __restrict__ claim_s, int32_t* __restrict__ cand, uint32_t* __restrict__ ncand) {
-  // first claims are staged in LDS and appended with one global atomic per workgroup
+// one thread per (frontier node, one of its 27 cells) in the claim pass: short dependent
+// chains, 27x the threads
+// ---- RegulateNormal without host round trips: every per-level quantity lives on the device.
+// st[0] = fbase (queue position of the level's first node), st[1] = nf (level size),
+// st[2] = ncand (nodes reached by this level), st[3] = qt (queue length).  Kernels stride over
+// device-side counts, so the host enqueues many levels and only checks nf now and then.  The
+// next level is ordered by a counting sort on the parent position (children per parent counted,
+// scanned, scattered) and a per-parent sort of the few children by (d2, index).
+__global__ __launch_bounds__(kBS) void k_bfs2_claim(
+    const int32_t* __restrict__ queue, const long long* __restrict__ st,
+    const int32_t* __restrict__ pos_of, const float* __restrict__ sx, const float* __restrict__ sy,
+    const float* __restrict__ sz, GridDesc G, const uint32_t* __restrict__ tkeys,
+    const int2* __restrict__ trange, uint32_t tmask, float r2,
+    const uint8_t* __restrict__ processed_s, uint32_t* __restrict__ claim_s,
+    int32_t* __restrict__ cand, long long* __restrict__ st_w, uint32_t* __restrict__ child_cnt,
+    uint32_t* __restrict__ cursor) {
   constexpr int kStage = 2048;
-  __shared__ uint32_t s_n, s_base;
+  __shared__ uint32_t s_n;
+  __shared__ long long s_base;
   __shared__ int32_t s_buf[kStage];
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
-  const int64_t t = (int64_t)blockIdx.x * kBS + threadIdx.x;
-  bool go = t < (int64_t)nf * 27;
-  const int f = go ? (int)(t / 27) : 0, c = go ? (int)(t % 27) : 0;
-  const uint32_t mypos = (uint32_t)(fbase + f);
-  float qx = 0.0f, qy = 0.0f, qz = 0.0f;
-  if (go) {
+  const long long fbase = st[0];
+  const long long nf = st[1];
+  const long long total = nf * 27;
+  for (long long t = (long long)blockIdx.x * kBS + threadIdx.x; t < total;
+       t += (long long)gridDim.x * kBS) {
+    const int f = (int)(t / 27), c = (int)(t % 27);
+    if (c == 0) { child_cnt[f] = 0; cursor[f] = 0; }
+    const uint32_t mypos = (uint32_t)(fbase + f);
     const int cu = pos_of[queue[mypos]];
-    qx = sx[cu]; qy = sy[cu]; qz = sz[cu];
-    go = finite3(qx, qy, qz);
-  }
-  const int x = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]) + c % 3 - 1;
-  const int y = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]) + (c / 3) % 3 - 1;
-  const int z = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]) + c / 9 - 1;
-  go = go && !(x < 0 || y < 0 || z < 0 || x >= G.g[0] || y >= G.g[1] || z >= G.g[2]);
-  if (go) {
+    const float qx = sx[cu], qy = sy[cu], qz = sz[cu];
+    if (!finite3(qx, qy, qz)) continue;
+    const int x = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]) + c % 3 - 1;
+    const int y = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]) + (c / 3) % 3 - 1;
+    const int z = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]) + c / 9 - 1;
+    if (x < 0 || y < 0 || z < 0 || x >= G.g[0] || y >= G.g[1] || z >= G.g[2]) continue;
     const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
     for (int u = rg.x; u < rg.y; ++u) {
       if (processed_s[u]) continue;
-      if (flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2) {
-        // claims only decrease: a plain read filters most of the contended atomics
-        if (claim_s[u] <= mypos) continue;
-        if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) {
-          const uint32_t p = atomicAdd(&s_n, 1u);
-          if (p < (uint32_t)kStage) s_buf[p] = u;
-          else cand[atomicAdd(ncand, 1u)] = u;  // overflow (rare): direct
-        }
+      if (!(flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2)) continue;
+      if (claim_s[u] <= mypos) continue;  // claims only decrease
+      if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) {
+        const uint32_t p = atomicAdd(&s_n, 1u);
+        if (p < (uint32_t)kStage) s_buf[p] = u;
+        else cand[atomicAdd((unsigned long long*)&st_w[2], 1ull)] = u;
       }
     }
   }
   __syncthreads();
   const uint32_t m = min(s_n, (uint32_t)kStage);
-  if (threadIdx.x == 0 && m) s_base = atomicAdd(ncand, m);
+  if (threadIdx.x == 0 && m)
+    s_base = (long long)atomicAdd((unsigned long long*)&st_w[2], (unsigned long long)m);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < m; i += kBS) cand[s_base + i] = s_buf[i];
 }
 
-// settle the newly reached nodes: flip against the claiming parent (PlaneDetect.h:624-636),
-// processed = 1, order key (parent queue position, d2 from the parent) + point id
-__global__ __launch_bounds__(kBS) void k_bfs_settle(
-    const int32_t* __restrict__ queue, const int32_t* __restrict__ cand, int nc,
-    const int32_t* __restrict__ pos_of, const int32_t* __restrict__ sidx,
-    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
+__global__ __launch_bounds__(kBS) void k_bfs2_settle(
+    const int32_t* __restrict__ queue, const int32_t* __restrict__ cand,
+    const long long* __restrict__ st, const int32_t* __restrict__ pos_of,
     uint8_t* __restrict__ processed_s, const uint32_t* __restrict__ claim_s,
-    float4* __restrict__ nrm_s, unsigned long long* __restrict__ keys,
-    int32_t* __restrict__ ids) {
-  const int t = blockIdx.x * kBS + threadIdx.x;
-  if (t >= nc) return;
-  const int u = cand[t];
-  const unsigned long long ppos = claim_s[u];
-  const int pu = pos_of[queue[ppos]];
-  const float4 pn = nrm_s[pu];
-  float4 nn = nrm_s[u];
-  const float dp = pn.x * nn.x + pn.y * nn.y + pn.z * nn.z;
-  if (dp < 0.0f) {
-    nn.x *= -1.0f; nn.y *= -1.0f; nn.z *= -1.0f;
-    nrm_s[u] = nn;
+    float4* __restrict__ nrm_s, uint32_t* __restrict__ child_cnt) {
+  const long long fbase = st[0], nc = st[2];
+  for (long long t = (long long)blockIdx.x * kBS + threadIdx.x; t < nc;
+       t += (long long)gridDim.x * kBS) {
+    const int u = cand[t];
+    const uint32_t ppos = claim_s[u];
+    const int pu = pos_of[queue[ppos]];
+    const float4 pn = nrm_s[pu];
+    float4 nn = nrm_s[u];
+    const float dp = pn.x * nn.x + pn.y * nn.y + pn.z * nn.z;  // PlaneDetect.h:629
+    if (dp < 0.0f) {
+      nn.x *= -1.0f; nn.y *= -1.0f; nn.z *= -1.0f;
+      nrm_s[u] = nn;
+    }
+    processed_s[u] = 1;
+    atomicAdd(&child_cnt[ppos - fbase], 1u);
   }
-  processed_s[u] = 1;
-  // the parent's neighbour list is sorted by the d2 FLANN computes for query = parent
-  const float d2 = flann_d2(sx[pu], sy[pu], sz[pu], sx[u], sy[u], sz[u]);
-  keys[t] = (ppos << 32) | (unsigned long long)__float_as_uint(d2);
-  ids[t] = sidx[u];
+}
+
+// exclusive scan of child_cnt[0..nf): tiles of 1024 scanned in LDS (offs = in-tile prefix,
+// tile_tot = tile sums), then one workgroup scans the tile sums (nf is one BFS level)
+__global__ __launch_bounds__(kBS) void k_bfs2_scan_tiles(const long long* __restrict__ st,
+                                                         const uint32_t* __restrict__ child_cnt,
+                                                         uint32_t* __restrict__ offs,
+                                                         uint32_t* __restrict__ tile_tot) {
+  __shared__ uint32_t s[1024];
+  const long long nf = st[1];
+  const long long ntiles = (nf + 1023) / 1024;
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long base = tile * 1024;
+    __syncthreads();
+    for (int k = threadIdx.x; k < 1024; k += kBS)
+      s[k] = base + k < nf ? child_cnt[base + k] : 0u;
+    __syncthreads();
+    // each thread scans 4 consecutive entries, then a block scan of the 256 partial sums
+    uint32_t v[4], sum = 0;
+    for (int k = 0; k < 4; ++k) { v[k] = s[threadIdx.x * 4 + k]; sum += v[k]; }
+    __syncthreads();
+    s[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < kBS; o <<= 1) {
+      const uint32_t add = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0u;
+      __syncthreads();
+      s[threadIdx.x] += add;
+      __syncthreads();
+    }
+    uint32_t run = s[threadIdx.x] - sum;
+    for (int k = 0; k < 4; ++k) {
+      const long long i = base + threadIdx.x * 4 + k;
+      if (i < nf) offs[i] = run;
+      run += v[k];
+    }
+    if (threadIdx.x == kBS - 1) tile_tot[tile] = s[kBS - 1];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_bfs2_scan_top(const long long* __restrict__ st,
+                                                        uint32_t* __restrict__ tile_tot) {
+  __shared__ uint32_t s[1024];
+  const long long ntiles = (st[1] + 1023) / 1024;
+  uint32_t carry = 0;
+  for (long long b = 0; b < ntiles; b += 1024) {
+    const long long i = b + threadIdx.x;
+    const uint32_t v = i < ntiles ? tile_tot[i] : 0u;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const uint32_t add = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0u;
+      __syncthreads();
+      s[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (i < ntiles) tile_tot[i] = carry + s[threadIdx.x] - v;  // exclusive
+    carry += s[1023];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_bfs2_scatter(
+    const int32_t* __restrict__ queue, const int32_t* __restrict__ cand,
+    const long long* __restrict__ st, const int32_t* __restrict__ pos_of,
+    const int32_t* __restrict__ sidx, const float* __restrict__ sx, const float* __restrict__ sy,
+    const float* __restrict__ sz, const uint32_t* __restrict__ claim_s,
+    const uint32_t* __restrict__ offs, const uint32_t* __restrict__ tile_tot,
+    uint32_t* __restrict__ cursor, float* __restrict__ slot_d2, int32_t* __restrict__ slot_id,
+    uint32_t* __restrict__ slot_of) {
+  const long long fbase = st[0], nc = st[2];
+  for (long long t = (long long)blockIdx.x * kBS + threadIdx.x; t < nc;
+       t += (long long)gridDim.x * kBS) {
+    const int u = cand[t];
+    const uint32_t ppos = claim_s[u];
+    const long long p = ppos - fbase;
+    const int pu = pos_of[queue[ppos]];
+    const uint32_t slot = tile_tot[p >> 10] + offs[p] + atomicAdd(&cursor[p], 1u);
+    // the parent's neighbour list is sorted by the d2 FLANN computes for query = parent
+    slot_d2[slot] = flann_d2(sx[pu], sy[pu], sz[pu], sx[u], sy[u], sz[u]);
+    slot_id[slot] = sidx[u];
+    slot_of[t] = slot;
+  }
+}
+
+// each child's rank among its siblings by (d2, index) -> its queue position
+__global__ __launch_bounds__(kBS) void k_bfs2_rank(const long long* __restrict__ st,
+                                                   const int32_t* __restrict__ cand,
+                                                   const uint32_t* __restrict__ claim_s,
+                                                   const uint32_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ tile_tot,
+                                                   const uint32_t* __restrict__ child_cnt,
+                                                   const uint32_t* __restrict__ slot_of,
+                                                   const float* __restrict__ slot_d2,
+                                                   const int32_t* __restrict__ slot_id,
+                                                   int32_t* __restrict__ queue) {
+  const long long fbase = st[0], nc = st[2], qt = st[3];
+  for (long long t = (long long)blockIdx.x * kBS + threadIdx.x; t < nc;
+       t += (long long)gridDim.x * kBS) {
+    const long long p = claim_s[cand[t]] - fbase;
+    const uint32_t o = tile_tot[p >> 10] + offs[p], m = child_cnt[p], me = slot_of[t];
+    const float d = slot_d2[me];
+    const int id = slot_id[me];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < m; ++j) {
+      const float dj = slot_d2[o + j];
+      r += (dj < d || (dj == d && slot_id[o + j] < id)) ? 1u : 0u;
+    }
+    queue[qt + o + r] = id;
+  }
+}
+
+__global__ void k_bfs2_advance(long long* __restrict__ st) {
+  const long long nf = st[1], nc = st[2];
+  st[0] += nf;
+  st[3] += nc;
+  st[1] = nc;
+  st[2] = 0;
 }
 
 // sorted order -> point order
@@ -915,21 +1037,23 @@ void launch_bfs_seed(int32_t seed, int flip, const int32_t* pos_of, float4* nrm_
                      queue);
 }
 
-void launch_bfs_claim(const int32_t* queue, int64_t fbase, int nf, const int32_t* pos_of,
-                      const GridDesc& G, const GridBufs& B, float r2, const uint8_t* processed_s,
-                      uint32_t* claim_s, int32_t* cand, uint32_t* ncand, hipStream_t s) {
-  if (nf <= 0) return;
-  hipLaunchKernelGGL(k_bfs_claim, dim3(cdiv((int64_t)nf * 27, kBS)), dim3(kBS), 0, s, queue, fbase,
-                     nf, pos_of, B.sx, B.sy, B.sz, G, B.tkeys, B.trange, B.tmask, r2, processed_s,
-                     claim_s, cand, ncand);
-}
-
-void launch_bfs_settle(const int32_t* queue, const int32_t* cand, int nc, const int32_t* pos_of,
-                       const GridBufs& B, uint8_t* processed_s, const uint32_t* claim_s,
-                       float4* nrm_s, unsigned long long* keys, int32_t* ids, hipStream_t s) {
-  if (nc <= 0) return;
-  hipLaunchKernelGGL(k_bfs_settle, dim3(cdiv(nc, kBS)), dim3(kBS), 0, s, queue, cand, nc, pos_of,
-                     B.idx_out, B.sx, B.sy, B.sz, processed_s, claim_s, nrm_s, keys, ids);
+void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, const GridDesc& G,
+                       const GridBufs& B, float r2, uint8_t* processed_s, uint32_t* claim_s,
+                       float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_bfs2_claim, dim3(grid), dim3(kBS), 0, s, queue, st, pos_of, B.sx, B.sy,
+                     B.sz, G, B.tkeys, B.trange, B.tmask, r2, processed_s, claim_s, cand, st,
+                     W.child_cnt, W.cursor);
+  hipLaunchKernelGGL(k_bfs2_settle, dim3(grid), dim3(kBS), 0, s, queue, cand, st, pos_of,
+                     processed_s, claim_s, nrm_s, W.child_cnt);
+  hipLaunchKernelGGL(k_bfs2_scan_tiles, dim3(grid), dim3(kBS), 0, s, st, W.child_cnt, W.offs,
+                     W.tile_tot);
+  hipLaunchKernelGGL(k_bfs2_scan_top, dim3(1), dim3(1024), 0, s, st, W.tile_tot);
+  hipLaunchKernelGGL(k_bfs2_scatter, dim3(grid), dim3(kBS), 0, s, queue, cand, st, pos_of,
+                     B.idx_out, B.sx, B.sy, B.sz, claim_s, W.offs, W.tile_tot, W.cursor,
+                     W.slot_d2, W.slot_id, W.slot_of);
+  hipLaunchKernelGGL(k_bfs2_rank, dim3(grid), dim3(kBS), 0, s, st, cand, claim_s, W.offs,
+                     W.tile_tot, W.child_cnt, W.slot_of, W.slot_d2, W.slot_id, queue);
+  hipLaunchKernelGGL(k_bfs2_advance, dim3(1), dim3(1), 0, s, st);
 }
 
 void launch_bfs_finish(const GridBufs& B, int n, const float4* nrm_s, const uint8_t* processed_s,
@@ -939,29 +1063,6 @@ void launch_bfs_finish(const GridBufs& B, int n, const float4* nrm_s, const uint
                      processed_s, nrm, processed);
 }
 
-size_t bfs_sort_tmp_bytes(int n) {
-  size_t a = 0, b = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (int32_t*)nullptr, (int32_t*)nullptr,
-                                           (unsigned long long*)nullptr,
-                                           (unsigned long long*)nullptr, n);
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (unsigned long long*)nullptr,
-                                           (unsigned long long*)nullptr, (int32_t*)nullptr,
-                                           (int32_t*)nullptr, n);
-  return a > b ? a : b;
-}
-
-hipError_t bfs_order(void* tmp, size_t tmp_bytes, int32_t* ids, unsigned long long* keys,
-                     int32_t* ids_alt, unsigned long long* keys_alt, int32_t* out_ids, int nc,
-                     hipStream_t s) {
-  if (nc <= 0) return hipSuccess;
-  size_t t = tmp_bytes;
-  // ids ascending (the atomic append order is arbitrary), then stable by (parent pos, d2)
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, t, ids, ids_alt, keys, keys_alt, nc, 0,
-                                                    32, s);
-  if (e != hipSuccess) return e;
-  t = tmp_bytes;
-  return hipcub::DeviceRadixSort::SortPairs(tmp, t, keys_alt, keys, ids_alt, out_ids, nc, 0, 64, s);
-}
 
 void launch_pack_normals(const float4* nrm, int n, float* out, int64_t stride_floats,
                          int curv_offset, hipStream_t s) {

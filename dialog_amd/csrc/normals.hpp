@@ -114,26 +114,27 @@ void launch_emit_points(const int32_t* sel, int n, const float* X, const float* 
 
 // ---- RegulateNormal, level-synchronous BFS (state in the grid's sorted order) ----
 // queue[]: point ids in PCL queue order; the current level is queue[fbase, fbase + nf).
-// claim_s: min over claiming queue positions (init ~0); cand/ncand: first-claimed positions.
+// claim_s: min over claiming queue positions (init ~0); cand: first-claimed positions.
 void launch_bfs_prepare(const GridBufs& B, int n, const float4* nrm, float4* nrm_s, int32_t* pos_of,
                         hipStream_t s);
 void launch_bfs_seed(int32_t seed, int flip, const int32_t* pos_of, float4* nrm_s,
                      uint8_t* processed_s, int32_t* queue, hipStream_t s);
-void launch_bfs_claim(const int32_t* queue, int64_t fbase, int nf, const int32_t* pos_of,
-                      const GridDesc& G, const GridBufs& B, float r2, const uint8_t* processed_s,
-                      uint32_t* claim_s, int32_t* cand, uint32_t* ncand, hipStream_t s);
-// settle the claimed nodes: sign flip against the parent, processed = 1, (parent pos | d2) keys
-// and point ids for the ordering sorts
-void launch_bfs_settle(const int32_t* queue, const int32_t* cand, int nc, const int32_t* pos_of,
-                       const GridBufs& B, uint8_t* processed_s, const uint32_t* claim_s,
-                       float4* nrm_s, unsigned long long* keys, int32_t* ids, hipStream_t s);
+// one BFS level entirely on the device (state st[4] = fbase, nf, ncand, qt; see normals.hip);
+// `grid` workgroups stride over the device-side counts.  Scratch: n entries each.
+struct Bfs2Bufs {
+  uint32_t* child_cnt;
+  uint32_t* cursor;
+  uint32_t* offs;
+  uint32_t* tile_tot;
+  uint32_t* slot_of;
+  float* slot_d2;
+  int32_t* slot_id;
+};
+void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, const GridDesc& G,
+                       const GridBufs& B, float r2, uint8_t* processed_s, uint32_t* claim_s,
+                       float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s);
 void launch_bfs_finish(const GridBufs& B, int n, const float4* nrm_s, const uint8_t* processed_s,
                        float4* nrm, uint8_t* processed, hipStream_t s);
-size_t bfs_sort_tmp_bytes(int n);
-// order the next level: stable sort by id, then stable sort by (parent pos, d2) -> out_ids
-hipError_t bfs_order(void* tmp, size_t tmp_bytes, int32_t* ids, unsigned long long* keys,
-                     int32_t* ids_alt, unsigned long long* keys_alt, int32_t* out_ids, int nc,
-                     hipStream_t s);
 
 // pcl::Normal scatter helpers
 void launch_pack_normals(const float4* nrm, int n, float* out, int64_t stride_floats,

@@ -267,11 +267,6 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   w.queue.ensure(n);
   w.cand.ensure(n);
   w.ids.ensure(n);
-  w.ids_alt.ensure(n);
-  w.keys64.ensure(n);
-  w.keys_alt.ensure(n);
-  const size_t stmp = bfs_sort_tmp_bytes(n);
-  w.sort_tmp.ensure(stmp);
   w.counters.ensure(8);
   w.h_cnt.ensure(8);
   HIPCHK(hipMemsetAsync(w.processed_s.p, 0, n, c->stream));
@@ -280,25 +275,27 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   // PlaneDetect.h:600-607: seed flipped unless its direction was confirmed outward
   launch_bfs_seed((int32_t)seed, seed_is_outward ? 0 : 1, w.pos_of.p, w.nrm_s.p, w.processed_s.p,
                   w.queue.p, c->stream);
-  int64_t fbase = 0, qt = 1;
-  int nf = 1;
-  while (nf > 0) {
-    HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
-    launch_bfs_claim(w.queue.p, fbase, nf, w.pos_of.p, G, B, r2, w.processed_s.p, w.claim.p,
-                     w.cand.p, w.counters.p, c->stream);
-    HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+  // levels run back to back on the device (state in w.bst); the host checks the level size every
+  // 16 levels -- levels enqueued after the frontier empties are no-ops
+  w.bst.ensure(4);
+  w.ccnt.ensure(n); w.coffs.ensure(n); w.ccur.ensure(n); w.sd2.ensure(n);
+  w.ctile.ensure(n / 1024 + 2); w.cslot.ensure(n);
+  const Bfs2Bufs W{w.ccnt.p, w.ccur.p, w.coffs.p, w.ctile.p, w.cslot.p, w.sd2.p, w.ids.p};
+  w.h_bst.ensure(4);
+  w.h_bst.p[0] = 0; w.h_bst.p[1] = 1; w.h_bst.p[2] = 0; w.h_bst.p[3] = 1;
+  HIPCHK(hipMemcpyAsync(w.bst.p, w.h_bst.p, 32, hipMemcpyHostToDevice, c->stream));
+  const int grid = c->num_cus * 4;
+  for (;;) {
+    for (int k = 0; k < 16; ++k)
+      launch_bfs2_level(w.queue.p, w.bst.p, w.pos_of.p, G, B, r2, w.processed_s.p, w.claim.p,
+                        w.nrm_s.p, w.cand.p, W, grid, c->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(w.h_bst.p, w.bst.p, 32, hipMemcpyDeviceToHost, c->stream));
     sync(c);
-    const int nc = (int)w.h_cnt.p[0];
-    if (nc == 0) break;
-    if (qt + nc > n) throw DlgError(DLG_ERR_INTERNAL, "BFS queue overflow");
-    launch_bfs_settle(w.queue.p, w.cand.p, nc, w.pos_of.p, B, w.processed_s.p, w.claim.p,
-                      w.nrm_s.p, w.keys64.p, w.ids.p, c->stream);
-    HIPCHK(bfs_order(w.sort_tmp.p, w.sort_tmp.cap, w.ids.p, w.keys64.p, w.ids_alt.p,
-                     w.keys_alt.p, w.queue.p + qt, nc, c->stream));
-    fbase = qt;
-    qt += nc;
-    nf = nc;
+    if (w.h_bst.p[3] > n) throw DlgError(DLG_ERR_INTERNAL, "BFS queue overflow");
+    if (w.h_bst.p[1] == 0) break;
   }
+  const int64_t qt = w.h_bst.p[3];
   launch_bfs_finish(B, n, w.nrm_s.p, w.processed_s.p, w.nrm.p, w.processed.p, c->stream);
   launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), stride / 4, -1, c->stream);
   HIPCHK(hipMemcpyAsync(nrm_io, w.out.p, nbytes, hipMemcpyDeviceToHost, c->stream));
