@@ -622,26 +622,45 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     const int64_t n = indices ? n_indices : pts->n;
     if (n > INT32_MAX) throw DlgError(DLG_ERR_INVALID, "more than 2^31-1 points");
     const int64_t sf = pts->stride_bytes / 4;
-    std::vector<float> x(n), y(n), z(n);
-    std::vector<int32_t> g(n);
-    for (int64_t i = 0; i < n; ++i) {
-      int64_t k = indices ? indices[i] : i;
-      if (k < 0 || k >= pts->n) throw DlgError(DLG_ERR_INVALID, "index out of range");
-      const float* p = pts->xyz + k * sf;
-      x[i] = p[0]; y[i] = p[1]; z[i] = p[2];
-      g[i] = (int32_t)(id_base + k);
-    }
     cl->ctx = c;
     cl->n_total = n;
     cl->n_points = pts->n;
     cl->id_base = id_base;
     cl->n_active = n;
     cl->pristine.ensure((size_t)std::max<int64_t>(n, 1));
-    if (n) {
+    if (indices)
+      for (int64_t i = 0; i < n; ++i)
+        if (indices[i] < 0 || indices[i] >= pts->n) throw DlgError(DLG_ERR_INVALID, "index out of range");
+    if (n && (!indices || 4 * n >= pts->n)) {
+      // the caller's records go up as they are (one DMA), the SoA split and ids on the device
+      DevBuf<uint8_t>& raw = c->nw.raw;
+      const size_t bytes = (size_t)pts->n * (size_t)pts->stride_bytes;
+      raw.ensure(bytes + (indices ? 4 * (size_t)n : 0));
+      HIPCHK(hipMemcpyAsync(raw.p, pts->xyz, bytes, hipMemcpyHostToDevice, c->stream));
+      const int32_t* didx = nullptr;
+      if (indices) {
+        HIPCHK(hipMemcpyAsync(raw.p + bytes, indices, 4 * (size_t)n, hipMemcpyHostToDevice,
+                              c->stream));
+        didx = reinterpret_cast<const int32_t*>(raw.p + bytes);
+      }
+      launch_upload_gather(reinterpret_cast<const float*>(raw.p), sf, didx, n, id_base,
+                           cl->pristine.out(), c->stream);
+      HIPCHK(hipGetLastError());
+    } else if (n) {
+      // a small subset of a large cloud: gather on the host
+      std::vector<float> x(n), y(n), z(n);
+      std::vector<int32_t> g(n);
+      for (int64_t i = 0; i < n; ++i) {
+        const int64_t k = indices[i];
+        const float* p = pts->xyz + k * sf;
+        x[i] = p[0]; y[i] = p[1]; z[i] = p[2];
+        g[i] = (int32_t)(id_base + k);
+      }
       HIPCHK(hipMemcpyAsync(cl->pristine.x.p, x.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
       HIPCHK(hipMemcpyAsync(cl->pristine.y.p, y.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
       HIPCHK(hipMemcpyAsync(cl->pristine.z.p, z.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
       HIPCHK(hipMemcpyAsync(cl->pristine.gid.p, g.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+      sync(c);  // the host vectors go out of scope
     }
     c->totals.ensure(4);
     launch_absmax(cl->pristine.view(n), reinterpret_cast<uint32_t*>(c->totals.p), c->stream);

@@ -1042,6 +1042,20 @@ __global__ void k_pack_point_normals(const float* __restrict__ raw, int64_t stri
   out[e] = eigen_normalized3(r[0], r[1], r[2], r[curv_off]);
 }
 
+// dlg_cloud_upload: caller records (stride_f floats, xyz first) -> SoA + global ids
+__global__ void k_upload_gather(const float* __restrict__ raw, int64_t stride_f,
+                                const int32_t* __restrict__ idx, int64_t n, int32_t id_base,
+                                PointsOut out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t k = idx ? idx[i] : i;
+  const float* p = raw + k * stride_f;
+  out.x[i] = p[0];
+  out.y[i] = p[1];
+  out.z[i] = p[2];
+  out.gid[i] = (int32_t)(id_base + k);
+}
+
 __global__ void k_absmax(PointsView src, uint32_t* __restrict__ out3) {
   float m[3] = {0.f, 0.f, 0.f};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1280,6 +1294,13 @@ void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off,
   if (src.n <= 0) return;
   hipLaunchKernelGGL(k_pack_point_normals, dim3(cdiv(src.n, 256)), dim3(256), 0, s, raw, stride_f,
                      curv_off, src, id_base, out);
+}
+
+void launch_upload_gather(const float* raw, int64_t stride_f, const int32_t* idx, int64_t n,
+                          int32_t id_base, PointsOut out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_upload_gather, dim3(cdiv(n, 256)), dim3(256), 0, s, raw, stride_f, idx, n,
+                     id_base, out);
 }
 
 void launch_absmax(PointsView src, uint32_t* out3, hipStream_t s) {

@@ -119,6 +119,9 @@ void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int3
 // cloud's local point index (gid - id_base) -> (normalized normal, curvature)
 void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,
                                int32_t id_base, float4* out, hipStream_t s);
+// cloud upload: records of stride_f floats (xyz first), optional index list -> SoA + ids
+void launch_upload_gather(const float* raw, int64_t stride_f, const int32_t* idx, int64_t n,
+                          int32_t id_base, PointsOut out, hipStream_t s);
 // max |x|, |y|, |z| over the cloud (prefilter error bound); out: 3 floats (as uint bits)
 void launch_absmax(PointsView src, uint32_t* out3, hipStream_t s);
 
