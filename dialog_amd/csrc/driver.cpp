@@ -281,10 +281,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       launch_score(src, c->hyps.p, D, cthr, c->res.p, kScoreDefault, c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
     c->h_res.ensure((size_t)Dp + D);
     HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 4 * ((size_t)Dp + D), hipMemcpyDeviceToHost, c->stream));
+    drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
     sync(c);
     if (trace_on())
       std::fprintf(stderr, "[dlg] N=%lld D=%d draw=%.3fms score+wait=%.3fms\n", (long long)N, D,
