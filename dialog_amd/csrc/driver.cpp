@@ -92,6 +92,31 @@ class Overlay {
   size_t mask_ = 0, size_ = 0;
 };
 
+// drawIndexSample's three swaps swap(shuf[i], shuf[i + rnd() % (N - i)]), i = 0, 1, 2, replayed
+// over list positions: positions 0..2 (touched by every draw) live in registers, the random
+// partners >= 3 in the sparse overlay -- one hash lookup and one insert per swap
+class ShuffleReplay {
+ public:
+  void reset(size_t expect) {
+    head_[0] = 0; head_[1] = 1; head_[2] = 2;
+    tail_.reset(expect);
+  }
+  void swap(int i, int64_t j) {
+    if (j < 3) {
+      std::swap(head_[i], head_[j]);
+      return;
+    }
+    const int32_t vj = tail_.get((int32_t)j);
+    tail_.set((int32_t)j, head_[i]);
+    head_[i] = vj;
+  }
+  int32_t at(int i) const { return head_[i]; }
+
+ private:
+  int32_t head_[3] = {0, 1, 2};
+  Overlay tail_;
+};
+
 }  // namespace dlg
 
 using namespace dlg;
@@ -218,7 +243,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   mt.thr = prm.threshold;
   mt.lambda = prm.normal_distance_weight;
   Mt19937 rng(prm.seed);
-  Overlay ov;
+  ShuffleReplay ov;
   ov.reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h) + 16);
 
   // RandomSampleConsensus::computeModel state
@@ -254,11 +279,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     for (int d = 0; d < D; ++d) {
       for (int i = 0; i < 3; ++i) {
         int64_t j = i + (int64_t)((uint64_t)(uint32_t)rng.rnd() % (uint64_t)(N - i));
-        ov.swap_pos(i, (int32_t)j);
+        ov.swap(i, j);
       }
-      hp[3 * d] = ov.get(0);
-      hp[3 * d + 1] = ov.get(1);
-      hp[3 * d + 2] = ov.get(2);
+      hp[3 * d] = ov.at(0);
+      hp[3 * d + 1] = ov.at(1);
+      hp[3 * d + 2] = ov.at(2);
     }
     const double t_draw1 = trace_on() ? now_ms() : 0.0;
     // ---- device: gather, build, score
