@@ -11,10 +11,13 @@ from .sac import (SAC_RANSAC, SACMODEL_NORMAL_PLANE, SACMODEL_PLANE, Cloud, Cont
 from .normals import (NormalEstimation, estimate_normals, orient_normals_nn,  # noqa: F401
                       regulate_normals)
 from .preprocess import preprocess, remove_redundant_points  # noqa: F401
+from .postprocess import (PostProcessParams, cluster_filter, post_process_planes,  # noqa: F401
+                          refit_planes)
 from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, LIB_PATH  # noqa: F401
 
 __all__ = ["Context", "Cloud", "SACSegmentation", "extract_planes", "segment_cloud", "make_params",
            "SACMODEL_PLANE", "SACMODEL_NORMAL_PLANE", "SAC_RANSAC", "DLG_REFIT_PCL",
            "DLG_REFIT_FAST", "DialogError", "LIB_PATH", "NormalEstimation", "estimate_normals",
            "regulate_normals", "SACSegmentationFromNormals", "orient_normals_nn",
-           "preprocess", "remove_redundant_points"]
+           "preprocess", "remove_redundant_points", "PostProcessParams", "post_process_planes",
+           "refit_planes", "cluster_filter"]

@@ -24,12 +24,26 @@ SYMBOLS = [
     "dlg_cloud_active", "dlg_sac_segment", "dlg_sac_segment_host", "dlg_extract_planes",
     "dlg_set_profiling", "dlg_synchronize", "dlg_allreduce_max_f64", "dlg_barrier",
     "dlg_score_benchmark", "dlg_estimate_normals", "dlg_regulate_normals",
-    "dlg_cloud_set_normals", "dlg_orient_normals_nn", "dlg_preprocess",
+    "dlg_cloud_set_normals", "dlg_orient_normals_nn", "dlg_preprocess", "dlg_refit_planes",
+    "dlg_post_process_planes", "dlg_cluster_filter",
 ]
 
 
 class Points(C.Structure):
     _fields_ = [("xyz", C.POINTER(C.c_float)), ("n", C.c_int64), ("stride_bytes", C.c_int64)]
+
+
+class Planes(C.Structure):
+    _fields_ = [("n_planes", C.c_int32), ("coeffs", C.POINTER(C.c_float)),
+                ("points", C.POINTER(C.c_float)), ("points_stride_bytes", C.c_int64),
+                ("point_offsets", C.POINTER(C.c_int64)), ("borders", C.POINTER(C.c_float)),
+                ("borders_stride_bytes", C.c_int64), ("border_offsets", C.POINTER(C.c_int64))]
+
+
+class PostProcessParams(C.Structure):
+    _fields_ = [("t_dist_point_plane", C.c_float), ("radius_local", C.c_float),
+                ("t_cluster_num", C.c_int32), ("plane_start_index", C.c_int32),
+                ("rand_seed", C.c_uint32)]
 
 
 class SacParams(C.Structure):
@@ -108,6 +122,12 @@ def load():
     L.dlg_estimate_normals.argtypes = [vp, C.POINTER(Points), C.c_float, C.c_int, fp, fp, C.c_int64]
     L.dlg_regulate_normals.argtypes = [vp, C.POINTER(Points), fp, C.c_int64, C.c_int64, C.c_int,
                                        C.c_float, C.POINTER(C.c_uint8), i64p]
+    L.dlg_refit_planes.argtypes = [C.POINTER(Planes), fp]
+    L.dlg_post_process_planes.argtypes = [vp, C.POINTER(Points), C.POINTER(Planes),
+                                          C.POINTER(PostProcessParams), fp, i64p, i32p, C.c_int64,
+                                          i32p, C.c_int64, i64p]
+    L.dlg_cluster_filter.argtypes = [vp, C.POINTER(Points), C.c_float, C.c_int32, i32p,
+                                     C.c_int64, i64p]
     for s in SYMBOLS:
         if s not in ("dlg_abi_version", "dlg_status_string", "dlg_sac_params_default",
                      "dlg_last_error"):

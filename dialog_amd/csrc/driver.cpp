@@ -616,6 +616,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
   c->h_stage.release();
   c->nw.release();
+  c->pw.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);

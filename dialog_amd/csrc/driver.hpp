@@ -14,6 +14,7 @@
 #include "../../include/dialog_ransac.h"
 #include "comm.hpp"
 #include "kernels.hpp"
+#include "postprocess.hpp"
 
 namespace dlg {
 
@@ -123,6 +124,24 @@ struct NormalsWork {
   }
 };
 
+// scratch of postProcessPlanes (postprocess_host.cpp)
+struct PostWork {
+  DevBuf<uint8_t> processed, flags, absorbed, keep;
+  DevBuf<uint32_t> counts, offs, cursor, abs_cnt, mask, csize;
+  DevBuf<int32_t> cand, ids, parent, sel, rids, out;
+  DevBuf<PipTask> tasks;
+  DevBuf<float4> planes, rays;
+  DevBuf<PipEdge> edges;
+  DevBuf<int64_t> edge_off;
+  void release() {
+    processed.release(); flags.release(); absorbed.release(); keep.release();
+    counts.release(); offs.release(); cursor.release(); abs_cnt.release(); mask.release();
+    csize.release(); cand.release(); ids.release(); parent.release(); sel.release();
+    rids.release(); out.release(); tasks.release(); planes.release(); rays.release();
+    edges.release(); edge_off.release();
+  }
+};
+
 }  // namespace dlg
 
 using namespace dlg;
@@ -161,6 +180,7 @@ struct dlg_ctx {
   int32_t* pending_dst = nullptr;
   int64_t pending_n = 0;
   NormalsWork nw;
+  PostWork pw;
 };
 
 struct dlg_cloud {

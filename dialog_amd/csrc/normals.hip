@@ -32,23 +32,17 @@
 #include <cmath>
 #include <cstdint>
 
+#include "grid_dev.hpp"
 #include "normals.hpp"
 
 namespace dlg {
 
 namespace {
 
-constexpr uint32_t kEmpty = 0xffffffffu;
+using namespace grid;
+
 constexpr int kBS = 256;
 
-__device__ __forceinline__ uint32_t hash_key(uint32_t k) {
-  k ^= k >> 16;
-  k *= 0x7feb352du;
-  k ^= k >> 15;
-  k *= 0x846ca68bu;
-  k ^= k >> 16;
-  return k;
-}
 
 // append val to out[] for every lane with pred: one global atomic per wavefront (a single
 // hot counter serialises at the L2 when every lane hits it).  All lanes of the wave must call.
@@ -70,19 +64,8 @@ __device__ __forceinline__ bool finite3(float x, float y, float z) {
   return isfinite(x) && isfinite(y) && isfinite(z);
 }
 
-__device__ __forceinline__ int cell_of(float v, float lo, float inv_cell, int g) {
-  int c = (int)floorf((v - lo) * inv_cell);
-  return c < 0 ? 0 : (c >= g ? g - 1 : c);
-}
 
-__device__ __forceinline__ uint32_t cell_key(const GridDesc& G, int x, int y, int z) {
-  return (uint32_t)((z * G.g[1] + y) * G.g[0] + x);
-}
 
-__device__ __forceinline__ float flann_d2(float qx, float qy, float qz, float px, float py, float pz) {
-  const float ex = qx - px, ey = qy - py, ez = qz - pz;
-  return ((0.0f + ex * ex) + ey * ey) + ez * ez;
-}
 
 // ---------------------------------------------------------------------------------------------
 // bounding box of the finite points
@@ -182,17 +165,6 @@ __global__ __launch_bounds__(kBS) void k_cells_end(const uint32_t* __restrict__ 
   if ((threadIdx.x & 63) == 0 && sq) atomicAdd(sumsq, sq);
 }
 
-__device__ __forceinline__ int2 cell_range(const uint32_t* __restrict__ tkeys,
-                                           const int2* __restrict__ trange, uint32_t tmask,
-                                           uint32_t k) {
-  uint32_t h = hash_key(k) & tmask;
-  while (true) {
-    const uint32_t tk = tkeys[h];
-    if (tk == k) return trange[h];
-    if (tk == kEmpty) return make_int2(0, 0);
-    h = (h + 1) & tmask;
-  }
-}
 
 // ---- pcl::computeRoots / pcl::eigen33 (common/impl/eigen.hpp), in double ----
 __device__ void roots2_d(double b, double c, double r[3]) {

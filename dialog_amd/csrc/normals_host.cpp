@@ -14,15 +14,10 @@
 #include <vector>
 
 #include "driver.hpp"
+#include "grid_host.hpp"
 #include "normals.hpp"
 
 namespace dlg {
-namespace {
-
-struct BBox {
-  float lo[3], hi[3];
-  bool any;
-};
 
 BBox bbox_of(dlg_ctx* c, const float* X, const float* Y, const float* Z, int n) {
   NormalsWork& w = c->nw;
@@ -88,9 +83,8 @@ GridDesc make_grid(const BBox& b, double cell) {
 
 // builds grid level `lv` over (X, Y, Z) (default nw.x/y/z); returns the number of occupied cells
 // (and the point-weighted mean occupancy sum(occ^2) / n in *pw_occ)
-uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B,
-                    const float* X = nullptr, const float* Y = nullptr, const float* Z = nullptr,
-                    double* pw_occ = nullptr) {
+uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B, const float* X,
+                    const float* Y, const float* Z, double* pw_occ) {
   NormalsWork& w = c->nw;
   GridLevelBufs& L = w.lv[lv];
   w.keys_in.ensure(n); w.keys_out.ensure(n); w.idx_in.ensure(n);
@@ -182,6 +176,8 @@ void check_points(const dlg_points* pts) {
     throw DlgError(DLG_ERR_INVALID, "stride_bytes must be >= 12 and a multiple of 4");
   if (pts->n > INT32_MAX / 2) throw DlgError(DLG_ERR_INVALID, "more than 2^30 points");
 }
+
+namespace {
 
 void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn, const float* vp_in,
                       float* out, int64_t out_stride) {

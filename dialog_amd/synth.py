@@ -76,3 +76,35 @@ def config_cloud(config_id: int, n_points: int | None = None, seed_offset: int =
     c = CONFIGS[config_id]
     return plane_cloud(n_points or c["n_points"], c["n_planes"], shares=c["shares"],
                        seed=SEED_BASE + config_id + seed_offset)
+
+
+def postprocess_scene(n_points: int, n_planes: int, keep_frac: float = 0.7, n_border: int = 40,
+                      seed: int = SEED_BASE + 6, outlier_frac: float = 0.1, sigma: float = 0.005):
+    """A cloud plus the plane list postProcessPlanes receives (Dialog/PlaneDetect.h:1454).
+
+    points_set of plane p = a random keep_frac of its points (the rest stays unclaimed in the
+    cloud); border = a concave star polygon (n_border vertices, radii alternating 4.6 / 3.2 around
+    the patch centre, counter-clockwise about the normal), lying on the plane; coeff = the plane
+    normal with a random sign (postProcessPlanes re-orients the refit normal by it).
+    Returns (cloud float32 [n, 3], planes: list of dict(coeff, points, border)).
+    """
+    pts, lab, planes = plane_cloud(n_points, n_planes, outlier_frac=outlier_frac, sigma=sigma,
+                                   seed=seed)
+    rng = np.random.default_rng((seed, 99))
+    out = []
+    for p in range(n_planes):
+        nrm = planes[p, :3].astype(np.float64)
+        a = np.array([1.0, 0.0, 0.0]) if abs(nrm[0]) < 0.9 else np.array([0.0, 1.0, 0.0])
+        u = np.cross(nrm, a)
+        u /= np.linalg.norm(u)
+        v = np.cross(nrm, u)
+        c = -float(planes[p, 3]) * nrm
+        th = np.arange(n_border) * (2.0 * np.pi / n_border)
+        r = np.where(np.arange(n_border) % 2 == 0, 4.6, 3.2)
+        border = (c + (r * np.cos(th))[:, None] * u + (r * np.sin(th))[:, None] * v)
+        ids = np.nonzero(lab == p)[0]
+        keep = np.sort(rng.choice(ids, size=int(round(keep_frac * ids.size)), replace=False))
+        sign = 1.0 if rng.random() < 0.5 else -1.0
+        out.append(dict(coeff=(sign * planes[p, :3]).astype(np.float32), points=pts[keep].copy(),
+                        border=border.astype(np.float32)))
+    return pts, out

@@ -205,6 +205,63 @@ dlg_status dlg_preprocess(dlg_ctx* ctx, const dlg_points* pts, int translate, fl
                           float* out_xyz, int64_t out_stride_bytes, int32_t* out_index,
                           int64_t cap, int64_t* n_out, float translation[3]);
 
+/* ---- postProcessPlanes (Dialog/PlaneDetect.h:1454-1579) ------------------------------------ */
+/* The final planes (plane_clouds_final, HeaderFile.h:98; struct Plane HeaderFile.h:81-88) as
+ * borrowed host arrays: plane k owns points[point_offsets[k] .. point_offsets[k + 1]) (its
+ * points_set) and border vertices [border_offsets[k] .. border_offsets[k + 1]) (its border, the
+ * ConcaveHull polygon of polyPlanes, PlaneDetect.h:1358-1436), records of *_stride_bytes (12 or
+ * >= 16, multiple of 4).  coeffs: 4 floats per plane (coeff.values; only [0..2], the outward
+ * normal, is read). */
+typedef struct {
+  int32_t n_planes;
+  const float* coeffs;
+  const float* points;
+  int64_t points_stride_bytes;
+  const int64_t* point_offsets;  /* n_planes + 1 */
+  const float* borders;
+  int64_t borders_stride_bytes;
+  const int64_t* border_offsets; /* n_planes + 1 */
+} dlg_planes;
+
+/* config.ini [PlaneDetect] values and the call's state (PlaneDetect.h:86-90, 1453) */
+typedef struct {
+  float t_dist_point_plane;  /* T_dist_point_plane: isPointInPoly's plane-distance gate */
+  float radius_local;        /* radius_local: clusterFilt neighbourhood radius (>= 0) */
+  int32_t t_cluster_num;     /* T_cluster_num: clusters of <= this many points are dropped */
+  int32_t plane_start_index; /* planes [plane_start_index, n_planes) may absorb points */
+  uint32_t rand_seed;        /* the srand(time(0)) value isPointInPoly reseeds rand() with */
+} dlg_postprocess_params;
+
+/* PlaneDetect.h:1477-1498: coeffs_out[4k..4k+3] = pcl::computePointNormal of plane k's points
+ * (float sums in list order, eigen33, d = -n.centroid; NaN with < 3 points), negated when its
+ * dot with the previous normal coeffs[4k..4k+2] is < 0.  Host arithmetic (sequential float sums
+ * are sequential by definition); no context needed. */
+dlg_status dlg_refit_planes(const dlg_planes* planes, float* coeffs_out);
+
+/* postProcessPlanes() minus its display/bookkeeping: (1) refit as dlg_refit_planes; (2) every
+ * plane point marks its nearest cloud point processed (KdTreeFLANN nearestKSearch k = 1, ties ->
+ * lowest index); (3) each unprocessed cloud point joins every plane k >= plane_start_index whose
+ * isPointInPoly (PlaneDetect.h:1891-1964, after srand(rand_seed)) accepts it; (4) clusterFilt
+ * (PlaneDetect.h:1582-1655) on the points still unprocessed.  Outputs: coeffs_out (4 per plane);
+ * absorbed_offsets[n_planes + 1] and absorbed_ids: per plane, the ascending cloud indices it
+ * absorbed (the shim appends those points to points_set); remaining_ids: ascending cloud indices
+ * that form the new source_cloud.  Sizes are reported (absorbed_offsets[n_planes],
+ * *n_remaining) also on DLG_ERR_CAPACITY.  A plane taking part in (3) must have >= 1 border
+ * vertex (the reference divides by the border size).  Exact duplicate points are assumed absent
+ * (preProcess removes them): clusterFilt's "skip the first neighbour" then skips the point
+ * itself, and its BFS clusters are the connected components computed here. */
+dlg_status dlg_post_process_planes(dlg_ctx* ctx, const dlg_points* cloud, const dlg_planes* planes,
+                                   const dlg_postprocess_params* params, float* coeffs_out,
+                                   int64_t* absorbed_offsets, int32_t* absorbed_ids,
+                                   int64_t absorbed_cap, int32_t* remaining_ids,
+                                   int64_t remaining_cap, int64_t* n_remaining);
+
+/* clusterFilt() alone (PlaneDetect.h:1582-1655): ascending indices of the points whose
+ * radius-`radius` connected component has more than t_cluster_num points. */
+dlg_status dlg_cluster_filter(dlg_ctx* ctx, const dlg_points* pts, float radius,
+                              int32_t t_cluster_num, int32_t* kept_ids, int64_t cap,
+                              int64_t* n_kept);
+
 /* ---- profiling ------------------------------------------------------------------------------ */
 /* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);

@@ -84,6 +84,17 @@ def lib():
         L.orc_regulate_normals.argtypes = [fp, C.c_int64, C.c_int64, fp, C.c_int64, C.c_int,
                                            C.c_float, C.POINTER(C.c_uint8)]
         L.orc_regulate_normals.restype = C.c_int64
+        u8p = C.POINTER(C.c_uint8)
+        L.orc_msvc_rand.argtypes = [C.POINTER(C.c_uint32)]
+        L.orc_msvc_rand.restype = C.c_uint32
+        L.orc_is_point_in_poly.argtypes = [fp, fp, fp, C.c_int64, C.c_int64, C.c_float,
+                                           C.c_uint32]
+        L.orc_compute_point_normal.argtypes = [fp, C.c_int64, C.c_int64, fp, fp]
+        L.orc_refit_planes.argtypes = [C.c_int, fp, fp, C.c_int64, i64p, fp]
+        L.orc_cluster_filter.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, C.c_int, u8p]
+        L.orc_post_process_planes.argtypes = [
+            fp, C.c_int64, C.c_int64, C.c_int, fp, fp, C.c_int64, i64p, fp, C.c_int64, i64p,
+            C.c_float, C.c_int, C.c_uint32, C.c_float, C.c_int, fp, u8p, u8p]
         _LIB = L
     return _LIB
 
@@ -285,3 +296,79 @@ def preprocess(points, min_dist, translate=True):
                              _i32(idx), _f(tr))
     return out[:k].copy(), idx[:k].copy(), tr
 
+
+
+# ---- postProcessPlanes (Dialog/PlaneDetect.h:1454-1579) ----
+def _u8(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def _i64(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def _concat(arrs):
+    off = np.zeros(len(arrs) + 1, np.int64)
+    for i, a in enumerate(arrs):
+        off[i + 1] = off[i] + len(a)
+    cat = (np.concatenate([np.asarray(a, np.float32).reshape(-1, 3) for a in arrs])
+           if off[-1] else np.zeros((1, 3), np.float32))
+    return np.ascontiguousarray(cat, np.float32), off
+
+
+def msvc_rand(n, seed):
+    st = C.c_uint32(seed)
+    return [lib().orc_msvc_rand(C.byref(st)) for _ in range(n)]
+
+
+def is_point_in_poly(p, coeff, border, t_dist, seed):
+    q = np.ascontiguousarray(p, np.float32)
+    c = np.ascontiguousarray(coeff, np.float32)
+    b = np.ascontiguousarray(border, np.float32).reshape(-1, 3)
+    return bool(lib().orc_is_point_in_poly(_f(q), _f(c), _f(b), b.shape[0], 3, float(t_dist),
+                                           int(seed) & 0xffffffff))
+
+
+def compute_point_normal(points):
+    p, stride = _xyz(points)
+    out = np.zeros(4, np.float32)
+    curv = np.zeros(1, np.float32)
+    lib().orc_compute_point_normal(_f(p), p.shape[0], stride, _f(out), _f(curv))
+    return out, float(curv[0])
+
+
+def refit_planes(coeffs, plane_points):
+    pts, off = _concat(plane_points)
+    c = np.ascontiguousarray(coeffs, np.float32).reshape(-1, 4)
+    out = np.zeros_like(c)
+    lib().orc_refit_planes(c.shape[0], _f(c), _f(pts), 3, _i64(off), _f(out))
+    return out
+
+
+def cluster_filter(points, radius, t_cluster_num):
+    p, stride = _xyz(points)
+    ok = np.zeros(max(p.shape[0], 1), np.uint8)
+    lib().orc_cluster_filter(_f(p), p.shape[0], stride, float(radius), int(t_cluster_num), _u8(ok))
+    return ok[:p.shape[0]].astype(bool)
+
+
+def post_process_planes(cloud, coeffs, plane_points, borders, t_dist, plane_start, seed,
+                        radius_local, t_cluster_num):
+    """Returns (coeffs_out (P,4), absorbed: list of ascending cloud ids per plane,
+    remaining: ascending cloud ids kept in source_cloud)."""
+    p, stride = _xyz(cloud)
+    n = p.shape[0]
+    c = np.ascontiguousarray(coeffs, np.float32).reshape(-1, 4)
+    P = c.shape[0]
+    pts, poff = _concat(plane_points)
+    bor, boff = _concat(borders)
+    out = np.zeros_like(c)
+    ab = np.zeros(max(P * n, 1), np.uint8)
+    rem = np.zeros(max(n, 1), np.uint8)
+    lib().orc_post_process_planes(_f(p), n, stride, P, _f(c), _f(pts), 3, _i64(poff), _f(bor), 3,
+                                  _i64(boff), float(t_dist), int(plane_start),
+                                  int(seed) & 0xffffffff, float(radius_local),
+                                  int(t_cluster_num), _f(out), _u8(ab), _u8(rem))
+    ab = ab[:P * n].reshape(P, n) if n else np.zeros((P, 0), np.uint8)
+    absorbed = [np.nonzero(ab[k])[0].astype(np.int32) for k in range(P)]
+    return out, absorbed, np.nonzero(rem[:n])[0].astype(np.int32)

@@ -802,3 +802,251 @@ int64_t orc_preprocess(const float* xyz, int64_t n, int64_t stride, int translat
   return kept;
 }
 
+
+/* ------------------------------------------------------------------------------------------ */
+/* postProcessPlanes (Dialog/PlaneDetect.h:1454-1579), isPointInPoly (:1891-1964) with its     */
+/* helpers isBothLineSegsIntersect (:1966-2015), getInfoBetPointAndPlane (:2018-2022),          */
+/* projPoint2Plane (:1437-1443), distP2P (:203-207), and clusterFilt (:1582-1655).             */
+/* Vector3f arithmetic as Eigen 3.3 evaluates it (no SSE for 3-vectors):                       */
+/*   dot / squaredNorm = a0*b0 + (a1*b1 + a2*b2); normalize: if (z > 0) v /= sqrt(z).          */
+/* pow(a, 0.5f) in distP2P is taken as the correctly rounded square root (sqrtf).              */
+/* rand(): MSVC CRT LCG; srand(time(0)) runs at every isPointInPoly call, so one call's ten    */
+/* edge draws depend on the seed only -- `seed` stands for that time(0) value.                 */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { float x, y, z; } orc_v3;
+
+static orc_v3 v3_at(const float* p) { orc_v3 v = {p[0], p[1], p[2]}; return v; }
+static orc_v3 v3_sub(orc_v3 a, orc_v3 b) { orc_v3 v = {a.x - b.x, a.y - b.y, a.z - b.z}; return v; }
+static float v3_dot(orc_v3 a, orc_v3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+static orc_v3 v3_normalized(orc_v3 v) {
+  float z = v.x * v.x + (v.y * v.y + v.z * v.z);
+  if (z > 0.0f) { float s = sqrtf(z); v.x /= s; v.y /= s; v.z /= s; }
+  return v;
+}
+static orc_v3 v3_cross(orc_v3 a, orc_v3 b) {
+  orc_v3 o = {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+  return o;
+}
+/* distP2P: pow(((dx*dx + dy*dy) + dz*dz), 0.5f) */
+static float orc_dist_p2p(orc_v3 a, orc_v3 b) {
+  float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+  return sqrtf((dx * dx + dy * dy) + dz * dz);
+}
+
+/* projPoint2Plane: lambda in float from 2.0 * (float expression), the update in double */
+static orc_v3 orc_proj_to_plane(orc_v3 p, const float c[4]) {
+  float lam = (float)(2.0 * (double)(((c[0] * p.x + c[1] * p.y) + c[2] * p.z) + c[3]));
+  orc_v3 o;
+  o.x = (float)((double)p.x - (double)lam / 2.0 * (double)c[0]);
+  o.y = (float)((double)p.y - (double)lam / 2.0 * (double)c[1]);
+  o.z = (float)((double)p.z - (double)lam / 2.0 * (double)c[2]);
+  return o;
+}
+
+static int orc_segs_intersect(orc_v3 pa, orc_v3 pb, orc_v3 pc, orc_v3 pd) {
+  orc_v3 nab = v3_normalized(v3_sub(pb, pa));
+  orc_v3 ncd = v3_normalized(v3_sub(pd, pc));
+  orc_v3 pa_pc = v3_sub(pc, pa);
+  float l1, l2;
+  float d = v3_dot(nab, ncd);
+  if (fabsf(d) <= 0.001f) {
+    l1 = v3_dot(nab, pa_pc);
+    l2 = -1.0f * v3_dot(ncd, pa_pc);
+  } else if (d >= 0.9999f) {
+    return 0;
+  } else {
+    float c1 = 1.0f - d * d;
+    float c2 = v3_dot(nab, pa_pc) * d - v3_dot(ncd, pa_pc);
+    l2 = c2 / c1;
+    l1 = (l2 + v3_dot(ncd, pa_pc)) / d;
+  }
+  orc_v3 p1 = {pa.x + l1 * nab.x, pa.y + l1 * nab.y, pa.z + l1 * nab.z};
+  orc_v3 p2 = {pc.x + l2 * ncd.x, pc.y + l2 * ncd.y, pc.z + l2 * ncd.z};
+  orc_v3 pi = {(p1.x + p2.x) / 2.0f, (p1.y + p2.y) / 2.0f, (p1.z + p2.z) / 2.0f};
+  float dpa = orc_dist_p2p(pi, pa), dpb = orc_dist_p2p(pi, pb), dab = orc_dist_p2p(pa, pb);
+  float dpc = orc_dist_p2p(pi, pc), dpd = orc_dist_p2p(pi, pd), dcd = orc_dist_p2p(pc, pd);
+  return fabsf(dpa + dpb - dab) < 0.001f && fabsf(dpc + dpd - dcd) < 0.001f;
+}
+
+uint32_t orc_msvc_rand(uint32_t* state) {
+  *state = *state * 214013u + 2531011u;
+  return (*state >> 16) & 0x7fffu;
+}
+
+int orc_is_point_in_poly(const float p[3], const float coeff[4], const float* border, int64_t nb,
+                         int64_t border_stride, float t_dist, uint32_t seed) {
+  orc_v3 q = v3_at(p);
+  orc_v3 pp = orc_proj_to_plane(q, coeff);
+  float dist = orc_dist_p2p(q, pp);
+  if (dist > t_dist) return 0;
+  if (nb <= 0) return 0;
+  uint32_t st = seed;
+  orc_v3 pn = {coeff[0], coeff[1], coeff[2]};
+  const float lambda = 10000.0f;
+  int odd = 0;
+  for (int i = 0; i < 10; ++i) {
+    int64_t index = (int64_t)((uint64_t)orc_msvc_rand(&st) % (uint64_t)nb);
+    orc_v3 s = v3_at(border + index * border_stride);
+    orc_v3 e = v3_at(border + (index == nb - 1 ? 0 : index + 1) * border_stride);
+    orc_v3 dir = v3_normalized(v3_sub(e, s));
+    orc_v3 dp = v3_normalized(v3_cross(dir, pn));
+    orc_v3 pl = {pp.x + lambda * dp.x, pp.y + lambda * dp.y, pp.z + lambda * dp.z};
+    int count = 0;
+    for (int64_t j = 0; j < nb; ++j) {
+      orc_v3 a = v3_at(border + j * border_stride);
+      orc_v3 b = v3_at(border + (j == nb - 1 ? 0 : j + 1) * border_stride);
+      if (orc_segs_intersect(a, b, pp, pl)) ++count;
+    }
+    odd += count % 2;
+  }
+  return odd >= 10 / 2;
+}
+
+int orc_compute_point_normal(const float* xyz, int64_t n, int64_t stride, float plane[4],
+                             float* curvature) {
+  if (n < 3) {
+    plane[0] = plane[1] = plane[2] = plane[3] = NAN;
+    *curvature = NAN;
+    return 0;
+  }
+  float a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + i * stride;
+    float x = p[0], y = p[1], z = p[2];
+    a[0] += x * x; a[1] += x * y; a[2] += x * z;
+    a[3] += y * y; a[4] += y * z; a[5] += z * z;
+    a[6] += x;     a[7] += y;     a[8] += z;
+  }
+  float cntf = (float)(size_t)n;
+  for (int k = 0; k < 9; ++k) a[k] = a[k] / cntf;
+  float cov[9];
+  cov[0] = a[0] - a[6] * a[6];
+  cov[1] = a[1] - a[6] * a[7];
+  cov[2] = a[2] - a[6] * a[8];
+  cov[4] = a[3] - a[7] * a[7];
+  cov[5] = a[4] - a[7] * a[8];
+  cov[8] = a[5] - a[8] * a[8];
+  cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+  float ev, v[3];
+  orc_eigen33(cov, &ev, v);
+  float eig_sum = cov[0] + cov[4] + cov[8];
+  *curvature = eig_sum != 0.0f ? fabsf(ev / eig_sum) : 0.0f;
+  plane[0] = v[0]; plane[1] = v[1]; plane[2] = v[2];
+  /* -1 * plane.dot(centroid), Vector4f SSE predux: (p0 c0 + p2 c2) + (p1 c1 + p3 c3), p3 = 0 */
+  plane[3] = -1.0f * ((v[0] * a[6] + v[2] * a[8]) + (v[1] * a[7] + 0.0f * 1.0f));
+  return 1;
+}
+
+/* PlaneDetect.h:1477-1498: refit + orientation by the previous coefficients' normal */
+void orc_refit_planes(int n_planes, const float* coeffs_in, const float* pts, int64_t stride,
+                      const int64_t* offs, float* coeffs_out) {
+  for (int i = 0; i < n_planes; ++i) {
+    float prm[4], curv;
+    orc_compute_point_normal(pts + offs[i] * stride, offs[i + 1] - offs[i], stride, prm, &curv);
+    const float* v = coeffs_in + 4 * i;
+    float d = (v[0] * prm[0] + v[2] * prm[2]) + (v[1] * prm[1] + 0.0f * prm[3]);
+    if (d < 0.0f)
+      for (int k = 0; k < 4; ++k) prm[k] = -1.0f * prm[k];
+    memcpy(coeffs_out + 4 * i, prm, sizeof(prm));
+  }
+}
+
+/* clusterFilt: BFS over radiusSearch(radius) results (sorted, first skipped); clusters with
+ * size <= t_cluster_num are dropped.  valid[i] = 1 for the points kept. */
+void orc_cluster_filter(const float* xyz, int64_t n, int64_t stride, float radius,
+                        int t_cluster_num, uint8_t* valid) {
+  if (n <= 0) return;
+  uint8_t* proc = (uint8_t*)calloc((size_t)n, 1);
+  int32_t* queue = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+  int32_t* members = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+  memset(valid, 1, (size_t)n);
+  orc_grid G;
+  orc_grid_build(&G, xyz, n, stride, radius > 0.0f ? radius : 1.0f);
+  float r2 = (float)((double)radius * (double)radius);
+  orc_nb* nb = NULL; int64_t cap = 0;
+  int64_t scan = 0;
+  for (;;) {
+    while (scan < n && proc[scan]) ++scan;  /* getSeedIndex: first unprocessed */
+    if (scan == n) break;
+    int64_t qh = 0, qt = 0, nm = 0;
+    queue[qt++] = (int32_t)scan;
+    members[nm++] = (int32_t)scan;
+    while (qh < qt) {
+      int32_t cur = queue[qh++];
+      proc[cur] = 1;
+      float q[3] = {xyz[cur * stride], xyz[cur * stride + 1], xyz[cur * stride + 2]};
+      int64_t k = radius > 0.0f ? orc_radius(&G, xyz, stride, q, r2, &nb, &cap) : 0;
+      for (int64_t j = 1; j < k; ++j) {
+        int32_t v = nb[j].j;
+        if (proc[v]) continue;
+        queue[qt++] = v;
+        members[nm++] = v;
+        proc[v] = 1;
+      }
+    }
+    if ((uint64_t)nm <= (uint64_t)(int64_t)t_cluster_num)
+      for (int64_t i = 0; i < nm; ++i) valid[members[i]] = 0;
+  }
+  free(nb);
+  orc_grid_free(&G);
+  free(members);
+  free(queue);
+  free(proc);
+}
+
+/* postProcessPlanes: refit (all planes), isProcessed from the 1-NN of every plane point in the
+ * cloud (ties -> lowest index), absorption of the unprocessed points into planes
+ * [plane_start, n_planes) (every plane whose polygon contains the point), clusterFilt of the
+ * rest.  absorbed: n_planes x n flags; remaining: n flags (1 = stays in source_cloud). */
+void orc_post_process_planes(const float* cloud, int64_t n, int64_t stride, int n_planes,
+                             const float* coeffs_in, const float* pts, int64_t pts_stride,
+                             const int64_t* pts_off, const float* border, int64_t border_stride,
+                             const int64_t* border_off, float t_dist, int plane_start,
+                             uint32_t seed, float radius_local, int t_cluster_num,
+                             float* coeffs_out, uint8_t* absorbed, uint8_t* remaining) {
+  orc_refit_planes(n_planes, coeffs_in, pts, pts_stride, pts_off, coeffs_out);
+  uint8_t* proc = (uint8_t*)calloc((size_t)(n > 0 ? n : 1), 1);
+  memset(absorbed, 0, (size_t)n_planes * (size_t)n);
+  if (n > 0)
+    for (int64_t t = 0; t < pts_off[n_planes]; ++t) {
+      const float* q = pts + t * pts_stride;
+      float bd = INFINITY;
+      int64_t bj = -1;
+      for (int64_t j = 0; j < n; ++j) {
+        const float* p = cloud + j * stride;
+        float ex = q[0] - p[0], ey = q[1] - p[1], ez = q[2] - p[2];
+        float d = ((0.0f + ex * ex) + ey * ey) + ez * ez;
+        if (d < bd) { bd = d; bj = j; }
+      }
+      if (bj >= 0) proc[bj] = 1;
+    }
+  for (int64_t i = 0; i < n; ++i) {
+    if (proc[i]) continue;
+    for (int ii = plane_start; ii < n_planes; ++ii) {
+      if (orc_is_point_in_poly(cloud + i * stride, coeffs_out + 4 * ii,
+                               border + border_off[ii] * border_stride,
+                               border_off[ii + 1] - border_off[ii], border_stride, t_dist, seed)) {
+        proc[i] = 1;
+        absorbed[(int64_t)ii * n + i] = 1;
+      }
+    }
+  }
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; ++i) m += !proc[i];
+  float* rest = (float*)malloc((size_t)(m > 0 ? m : 1) * 3 * sizeof(float));
+  int64_t* rid = (int64_t*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int64_t));
+  uint8_t* ok = (uint8_t*)malloc((size_t)(m > 0 ? m : 1));
+  m = 0;
+  for (int64_t i = 0; i < n; ++i)
+    if (!proc[i]) {
+      memcpy(rest + 3 * m, cloud + i * stride, 3 * sizeof(float));
+      rid[m++] = i;
+    }
+  memset(remaining, 0, (size_t)n);
+  orc_cluster_filter(rest, m, 3, radius_local, t_cluster_num, ok);
+  for (int64_t t = 0; t < m; ++t) remaining[rid[t]] = ok[t];
+  free(ok);
+  free(rid);
+  free(rest);
+  free(proc);
+}

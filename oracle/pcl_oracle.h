@@ -126,6 +126,26 @@ void orc_orient_normals_nn(const float* xyz, int64_t n, int64_t stride, float* n
 int64_t orc_preprocess(const float* xyz, int64_t n, int64_t stride, int translate, float min_dist,
                        float* out_xyz, int32_t* out_index, float translation[3]);
 
+/* ---- postProcessPlanes (PlaneDetect.h:1454-1579) and its parts ---- */
+uint32_t orc_msvc_rand(uint32_t* state);  /* MSVC CRT rand() on an explicit state */
+/* isPointInPoly (PlaneDetect.h:1891-1964) after srand(seed); border: nb vertices */
+int orc_is_point_in_poly(const float p[3], const float coeff[4], const float* border, int64_t nb,
+                         int64_t border_stride, float t_dist, uint32_t seed);
+/* pcl::computePointNormal over all n points (features/normal_3d.h) [PCL-1.8 ext] */
+int orc_compute_point_normal(const float* xyz, int64_t n, int64_t stride, float plane[4],
+                             float* curvature);
+void orc_refit_planes(int n_planes, const float* coeffs_in, const float* pts, int64_t stride,
+                      const int64_t* offs, float* coeffs_out);
+/* clusterFilt (PlaneDetect.h:1582-1655): valid[i] = 0 for clusters of <= t_cluster_num points */
+void orc_cluster_filter(const float* xyz, int64_t n, int64_t stride, float radius,
+                        int t_cluster_num, uint8_t* valid);
+void orc_post_process_planes(const float* cloud, int64_t n, int64_t stride, int n_planes,
+                             const float* coeffs_in, const float* pts, int64_t pts_stride,
+                             const int64_t* pts_off, const float* border, int64_t border_stride,
+                             const int64_t* border_off, float t_dist, int plane_start,
+                             uint32_t seed, float radius_local, int t_cluster_num,
+                             float* coeffs_out, uint8_t* absorbed, uint8_t* remaining);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,6 +24,7 @@ for s in $STEPS; do
     pytestfast) run pytest_gpu 600 python3 -m pytest tests -m "gpu and not slow" -x -q ;;
     bench)  run bench 600 python3 bench.py ;;
     normals) run normals_gpu 600 python3 -m pytest tests/test_normals.py -m gpu -x -q -rA ;;
+    post)   run post_gpu 600 python3 -m pytest tests/test_postprocess.py -m gpu -x -q -rA ;;
     nbench) run nbench 600 python3 tools/bench_normals.py ;;
     c5)     run c5 600 python3 tools/bench_c5.py ;;
     c5prof) run c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof -o run -- python3 tools/bench_c5.py 10000000 2 ;;
