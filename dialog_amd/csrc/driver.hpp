@@ -127,17 +127,17 @@ struct NormalsWork {
 // scratch of postProcessPlanes (postprocess_host.cpp)
 struct PostWork {
   DevBuf<uint8_t> processed, flags, absorbed, keep;
-  DevBuf<uint32_t> counts, offs, cursor, abs_cnt, mask, csize;
-  DevBuf<int32_t> cand, ids, parent, sel, rids, out;
+  DevBuf<uint32_t> bcnt, boff, offs, abs_cnt, mask, csize;
+  DevBuf<int32_t> cand, cand2, ids, parent, sel, rids, out, table, rest;
   DevBuf<PipTask> tasks;
   DevBuf<float4> planes, rays;
   DevBuf<PipEdge> edges;
   DevBuf<int64_t> edge_off;
   void release() {
     processed.release(); flags.release(); absorbed.release(); keep.release();
-    counts.release(); offs.release(); cursor.release(); abs_cnt.release(); mask.release();
-    csize.release(); cand.release(); ids.release(); parent.release(); sel.release();
-    rids.release(); out.release(); tasks.release(); planes.release(); rays.release();
+    bcnt.release(); boff.release(); offs.release(); abs_cnt.release(); mask.release();
+    csize.release(); cand.release(); cand2.release(); ids.release(); parent.release(); sel.release();
+    rids.release(); out.release(); table.release(); rest.release(); tasks.release(); planes.release(); rays.release();
     edges.release(); edge_off.release();
   }
 };

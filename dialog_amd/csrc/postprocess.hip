@@ -17,7 +17,9 @@
 // (union-find, hooking the larger root under the smaller with CAS); a component is dropped when
 // its size <= T_cluster_num.  The BFS of the reference finds the same components.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
+#include <cfloat>
 #include <cstdint>
 
 #include "grid_dev.hpp"
@@ -31,6 +33,8 @@ using namespace grid;
 
 constexpr int kBS = 256;
 
+inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
 __device__ __forceinline__ bool pip_candidate(V3 q, float4 c, float t_dist) {
   const V3 pp = proj_to_plane(q, c);
   // isPointInPoly returns false for dist > T; NaN distances (NaN plane or point) cannot pass
@@ -38,29 +42,91 @@ __device__ __forceinline__ bool pip_candidate(V3 q, float4 c, float t_dist) {
   return dist_p2p(q, pp) <= t_dist;
 }
 
-__global__ __launch_bounds__(kBS) void k_pip_candidates(
+// exclusive prefix of `pred` over the workgroup (ballot + LDS wave totals); returns the total
+__device__ __forceinline__ uint32_t block_prefix(bool pred, uint32_t* below) {
+  __shared__ uint32_t wtot[kBS / 64];
+  const uint64_t m = __ballot(pred);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t in_wave = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (lane == 0) wtot[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+  for (int k = 0; k < kBS / 64; ++k) {
+    before += k < w ? wtot[k] : 0u;
+    tot += wtot[k];
+  }
+  *below = before + in_wave;
+  return tot;
+}
+
+// pass 1: bcnt[p * nblk + block] = candidates of plane p (blockIdx.y) in the block's points
+__global__ __launch_bounds__(kBS) void k_pip_count(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
     const uint8_t* __restrict__ processed, const float4* __restrict__ planes, float t_dist,
-    uint32_t* __restrict__ counts, const uint32_t* __restrict__ offs, uint32_t* __restrict__ cursor,
-    int32_t* __restrict__ cand) {
+    uint32_t* __restrict__ bcnt) {
   const int p = blockIdx.y;
   const int i = blockIdx.x * kBS + threadIdx.x;
   bool c = false;
   if (i < n && !processed[i]) c = pip_candidate(V3{X[i], Y[i], Z[i]}, planes[p], t_dist);
-  const uint64_t m = __ballot(c);
-  if (m == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((unsigned long long)m) - 1;
-  if (!cand) {
-    if (lane == leader) atomicAdd(&counts[p], (uint32_t)__popcll(m));
-    return;
+  uint32_t below;
+  const uint32_t tot = block_prefix(c, &below);
+  if (threadIdx.x == 0) bcnt[(size_t)p * gridDim.x + blockIdx.x] = tot;
+}
+
+// pass 2: candidates of plane p in ascending point order at boff[p * nblk + block] + rank
+__global__ __launch_bounds__(kBS) void k_pip_fill(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
+    const uint8_t* __restrict__ processed, const float4* __restrict__ planes, float t_dist,
+    const uint32_t* __restrict__ boff, int32_t* __restrict__ cand) {
+  const int p = blockIdx.y;
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  bool c = false;
+  if (i < n && !processed[i]) c = pip_candidate(V3{X[i], Y[i], Z[i]}, planes[p], t_dist);
+  uint32_t below;
+  (void)block_prefix(c, &below);
+  if (c) cand[boff[(size_t)p * gridDim.x + blockIdx.x] + below] = i;
+}
+
+__device__ __forceinline__ uint64_t spread3_14(uint32_t v) {  // 14 bits -> every third bit
+  uint64_t x = v & 0x3fffu;
+  x = (x | (x << 16)) & 0x0000ff0000ffull;
+  x = (x | (x << 8)) & 0x00f00f00f00full;
+  x = (x | (x << 4)) & 0x0c30c30c30c3ull;
+  x = (x | (x << 2)) & 0x249249249249ull;
+  return x;
+}
+
+// sort key of a candidate: plane (major), then the 3-D Morton code of the point, so that the
+// lanes of a wave hold nearby points (their parallel rays meet the same few border edges, and
+// the early outs of segs_intersect agree across the wave)
+__global__ __launch_bounds__(kBS) void k_pip_keys(const int32_t* __restrict__ cand,
+                                                  const uint32_t* __restrict__ offs,
+                                                  const float* __restrict__ X,
+                                                  const float* __restrict__ Y,
+                                                  const float* __restrict__ Z, float4 lo_scale,
+                                                  uint64_t* __restrict__ keys) {
+  const int p = blockIdx.y;
+  const int t = blockIdx.x * kBS + threadIdx.x;
+  if (t >= (int)(offs[p + 1] - offs[p])) return;
+  const int ci = (int)offs[p] + t;
+  const int i = cand[ci];
+  const float sc = lo_scale.w;
+  const uint32_t qx = (uint32_t)fminf(fmaxf((X[i] - lo_scale.x) * sc, 0.0f), 16383.0f);
+  const uint32_t qy = (uint32_t)fminf(fmaxf((Y[i] - lo_scale.y) * sc, 0.0f), 16383.0f);
+  const uint32_t qz = (uint32_t)fminf(fmaxf((Z[i] - lo_scale.z) * sc, 0.0f), 16383.0f);
+  keys[ci] = ((uint64_t)p << 42) | spread3_14(qx) | (spread3_14(qy) << 1) | (spread3_14(qz) << 2);
+}
+
+// offs[p] = first candidate of plane p, offs[P] = total
+__global__ void k_pip_ranges(const uint32_t* __restrict__ bcnt, const uint32_t* __restrict__ boff,
+                             int nblk, int n_planes, uint32_t* __restrict__ offs) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_planes) offs[p] = boff[(size_t)p * nblk];
+  if (p == n_planes) {
+    const size_t last = (size_t)n_planes * nblk - 1;
+    offs[p] = boff[last] + bcnt[last];
   }
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(&cursor[p], (uint32_t)__popcll(m));
-  base = __shfl(base, leader, 64);
-  const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  if (c) cand[offs[p] + base + below] = i;
 }
 
 __global__ __launch_bounds__(kBS) void k_pip_test(
@@ -75,35 +141,35 @@ __global__ __launch_bounds__(kBS) void k_pip_test(
   const int ci = T.cbeg + (act ? t : 0);
   const int i = cand[ci];
   const V3 pc = proj_to_plane(V3{X[i], Y[i], Z[i]}, planes[T.plane]);
-  PipRay R[kPipRays];
-#pragma unroll
-  for (int k = 0; k < kPipRays; ++k) {
-    const float4 d = rays[T.plane * kPipRays + k];
-    R[k] = make_ray(pc, V3{d.x, d.y, d.z});
-  }
+  const float pc_l1 = (fabsf(pc.x) + fabsf(pc.y)) + fabsf(pc.z);
   const PipEdge* __restrict__ E = edges + edge_off[T.plane];
   uint32_t bits = 0;
-  for (int e = T.ebeg; e < T.eend; ++e) {
-    const PipEdge ed = E[e];
-    const V3 pa{ed.a_dab.x, ed.a_dab.y, ed.a_dab.z}, pb{ed.b.x, ed.b.y, ed.b.z};
-    const V3 nab{ed.nab.x, ed.nab.y, ed.nab.z};
-#pragma unroll
-    for (int k = 0; k < kPipRays; ++k)
-      if (segs_intersect(pa, pb, nab, ed.a_dab.w, pc, R[k])) bits ^= 1u << k;
+  // ray-outer, edge-inner: one ray in registers, the (wave-uniform) edge records in SGPRs
+#pragma unroll 1
+  for (int k = 0; k < kPipRays; ++k) {
+    const float4 d = rays[T.plane * kPipRays + k];
+    const PipRay R = make_ray(pc, V3{d.x, d.y, d.z});
+    uint32_t odd = 0;
+    for (int e = T.ebeg; e < T.eend; ++e) {
+      const PipEdge ed = E[e];
+      const V3 pa{ed.a_dab.x, ed.a_dab.y, ed.a_dab.z}, pb{ed.b.x, ed.b.y, ed.b.z};
+      const V3 nab{ed.nab.x, ed.nab.y, ed.nab.z};
+      odd ^= segs_intersect(pa, pb, nab, ed.a_dab.w, ed.b.w, pc, pc_l1, R) ? 1u : 0u;
+    }
+    bits |= odd << k;
   }
   if (act && bits) atomicXor(&mask[ci], bits);
 }
 
 __global__ __launch_bounds__(kBS) void k_pip_mark(
     const int32_t* __restrict__ cand, const uint32_t* __restrict__ mask,
-    const uint32_t* __restrict__ offs, const uint32_t* __restrict__ counts, int n,
-    uint8_t* __restrict__ absorbed, uint8_t* __restrict__ processed,
-    uint32_t* __restrict__ abs_cnt) {
+    const uint32_t* __restrict__ offs, int n, uint8_t* __restrict__ absorbed,
+    uint8_t* __restrict__ processed, uint32_t* __restrict__ abs_cnt) {
   const int p = blockIdx.y;
   const int t = blockIdx.x * kBS + threadIdx.x;
   bool in = false;
   int i = 0;
-  if (t < (int)counts[p]) {
+  if (t < (int)(offs[p + 1] - offs[p])) {
     const int ci = (int)offs[p] + t;
     i = cand[ci];
     in = __popc(mask[ci] & ((1u << kPipRays) - 1u)) >= kPipRays / 2;
@@ -134,6 +200,81 @@ __global__ __launch_bounds__(kBS) void k_gather_ids(const int32_t* __restrict__ 
                                                     int32_t* __restrict__ out) {
   const int i = blockIdx.x * kBS + threadIdx.x;
   if (i < n) out[i] = map[sel[i]];
+}
+
+// ---- 1-NN shortcut: a plane point equal to a cloud point has that point as nearest neighbour
+// (d2 = 0; equal points -> the lowest index).  Valid when every coordinate has |v| >= 2^-50:
+// any other float differs by >= 2^-73 there, whose square does not underflow, so d2 > 0 for
+// every point not equal to the query.  Other queries take the grid search.
+__device__ __forceinline__ uint32_t xyz_hash(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9e3779b1u ^ (b + 0x7f4a7c15u) * 0x85ebca77u ^ (c + 0x165667b1u) * 0xc2b2ae3du;
+  h ^= h >> 15;
+  h *= 0x2c1b3c6du;
+  h ^= h >> 12;
+  return h;
+}
+
+__device__ __forceinline__ bool same_bits(float a, float b) {
+  return __float_as_uint(a) == __float_as_uint(b);
+}
+
+__global__ __launch_bounds__(kBS) void k_xyz_insert(const float* __restrict__ X,
+                                                    const float* __restrict__ Y,
+                                                    const float* __restrict__ Z, int n,
+                                                    int32_t* table, uint32_t tmask) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= n) return;
+  const float x = X[i], y = Y[i], z = Z[i];
+  if (!(isfinite(x) && isfinite(y) && isfinite(z))) return;
+  uint32_t h = xyz_hash(__float_as_uint(x), __float_as_uint(y), __float_as_uint(z)) & tmask;
+  while (true) {
+    int32_t j = atomicCAS(&table[h], -1, i);
+    if (j == -1) return;
+    // occupied: every index stored in a slot has the coordinates of the slot's first writer
+    if (same_bits(X[j], x) && same_bits(Y[j], y) && same_bits(Z[j], z)) {
+      atomicMin(&table[h], i);
+      return;
+    }
+    h = (h + 1) & tmask;
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_xyz_lookup(
+    const float* __restrict__ qx, const float* __restrict__ qy, const float* __restrict__ qz, int m,
+    const int32_t* __restrict__ table, uint32_t tmask, const float* __restrict__ X,
+    const float* __restrict__ Y, const float* __restrict__ Z, int32_t* __restrict__ nn,
+    int32_t* __restrict__ rest, uint32_t* __restrict__ n_rest) {
+  const int q = blockIdx.x * kBS + threadIdx.x;
+  bool miss = false;
+  if (q < m) {
+    const float x = qx[q], y = qy[q], z = qz[q];
+    const float lim = 0x1p-50f;
+    miss = true;
+    if (fabsf(x) >= lim && fabsf(y) >= lim && fabsf(z) >= lim && fabsf(x) <= FLT_MAX &&
+        fabsf(y) <= FLT_MAX && fabsf(z) <= FLT_MAX) {
+      uint32_t h = xyz_hash(__float_as_uint(x), __float_as_uint(y), __float_as_uint(z)) & tmask;
+      while (true) {
+        const int32_t j = table[h];
+        if (j == -1) break;
+        if (same_bits(X[j], x) && same_bits(Y[j], y) && same_bits(Z[j], z)) {
+          nn[q] = j;
+          miss = false;
+          break;
+        }
+        h = (h + 1) & tmask;
+      }
+    }
+  }
+  const uint64_t mk = __ballot(miss);
+  if (mk == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)mk) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(n_rest, (uint32_t)__popcll(mk));
+  base = __shfl(base, leader, 64);
+  const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+  if (miss) rest[base + below] = q;
 }
 
 // ---- clusterFilt: union-find over sorted positions ----
@@ -200,11 +341,23 @@ __global__ __launch_bounds__(kBS) void k_cc_hook(const float* __restrict__ sx,
       }
 }
 
+// component sizes: lanes of a wave sharing a root (neighbours in cell order mostly do) add
+// with one atomic, so a large component does not serialise on its counter
 __global__ __launch_bounds__(kBS) void k_cc_count(int32_t* parent, int n,
                                                   uint32_t* __restrict__ size) {
   const int u = blockIdx.x * kBS + threadIdx.x;
-  if (u >= n) return;
-  atomicAdd(&size[uf_find(parent, u)], 1u);
+  const int r = u < n ? uf_find(parent, u) : -1;
+  bool todo = u < n;
+  const int lane = threadIdx.x & 63;
+  uint64_t act = __ballot(todo);
+  while (act) {
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const int rl = __shfl(r, leader, 64);
+    const uint64_t same = __ballot(todo && r == rl);
+    if (lane == leader) atomicAdd(&size[rl], (uint32_t)__popcll(same));
+    if (r == rl) todo = false;
+    act = __ballot(todo);
+  }
 }
 
 __global__ __launch_bounds__(kBS) void k_cc_keep(const int32_t* __restrict__ sidx,
@@ -219,17 +372,61 @@ __global__ __launch_bounds__(kBS) void k_cc_keep(const int32_t* __restrict__ sid
   keep[sidx[u]] = (uint64_t)size[r] > t_cluster_num ? 1 : 0;
 }
 
-inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
 }  // namespace
 
-void launch_pip_candidates(const float* X, const float* Y, const float* Z, int n,
-                           const uint8_t* processed, const float4* planes, int n_planes,
-                           float t_dist, uint32_t* counts, const uint32_t* offs, uint32_t* cursor,
-                           int32_t* cand, hipStream_t s) {
-  if (n <= 0 || n_planes <= 0) return;
-  hipLaunchKernelGGL(k_pip_candidates, dim3(cdiv(n, kBS), n_planes), dim3(kBS), 0, s, X, Y, Z, n,
-                     processed, planes, t_dist, counts, offs, cursor, cand);
+size_t pip_scan_tmp_bytes(size_t count) {
+  size_t t = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         count);
+  return t;
+}
+
+int pip_blocks(int n) { return (int)cdiv(n, kBS); }
+
+hipError_t launch_pip_candidates(const float* X, const float* Y, const float* Z, int n,
+                                 const uint8_t* processed, const float4* planes, int n_planes,
+                                 float t_dist, uint32_t* bcnt, uint32_t* boff, void* tmp,
+                                 size_t tmp_bytes, int32_t* cand, uint32_t* offs, hipStream_t s) {
+  if (n <= 0 || n_planes <= 0) return hipSuccess;
+  const int nblk = pip_blocks(n);
+  const dim3 g(nblk, n_planes);
+  if (!cand) {
+    hipLaunchKernelGGL(k_pip_count, g, dim3(kBS), 0, s, X, Y, Z, n, processed, planes, t_dist,
+                       bcnt);
+    size_t t = tmp_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, t, bcnt, boff,
+                                                    (size_t)n_planes * nblk, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pip_ranges, dim3(cdiv(n_planes + 1, 64)), dim3(64), 0, s, bcnt, boff,
+                       nblk, n_planes, offs);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_pip_fill, g, dim3(kBS), 0, s, X, Y, Z, n, processed, planes, t_dist, boff,
+                     cand);
+  return hipGetLastError();
+}
+
+size_t pip_sort_tmp_bytes(int count) {
+  size_t t = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const uint64_t*)nullptr,
+                                           (uint64_t*)nullptr, (const int32_t*)nullptr,
+                                           (int32_t*)nullptr, count);
+  return t;
+}
+
+hipError_t launch_pip_sort(const int32_t* cand, int count, const uint32_t* offs, int n_planes,
+                           int max_count, const float* X, const float* Y, const float* Z,
+                           float4 lo_scale, uint64_t* keys, uint64_t* keys_alt, int32_t* cand_out,
+                           void* tmp, size_t tmp_bytes, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pip_keys, dim3(cdiv(max_count, kBS), n_planes), dim3(kBS), 0, s, cand, offs,
+                     X, Y, Z, lo_scale, keys);
+  int end_bit = 42;
+  while (end_bit < 64 && ((uint64_t)1 << (end_bit - 42)) < (uint64_t)n_planes) ++end_bit;
+  size_t t = tmp_bytes;
+  return hipcub::DeviceRadixSort::SortPairs(tmp, t, keys, keys_alt, cand, cand_out, count, 0,
+                                            end_bit, s);
 }
 
 void launch_pip_test(const PipTask* tasks, int n_tasks, const int32_t* cand, const float* X,
@@ -242,11 +439,26 @@ void launch_pip_test(const PipTask* tasks, int n_tasks, const int32_t* cand, con
 }
 
 void launch_pip_mark(const int32_t* cand, const uint32_t* mask, const uint32_t* offs,
-                     const uint32_t* counts, int n_planes, int max_count, int n,
-                     uint8_t* absorbed, uint8_t* processed, uint32_t* abs_cnt, hipStream_t s) {
+                     int n_planes, int max_count, int n, uint8_t* absorbed, uint8_t* processed,
+                     uint32_t* abs_cnt, hipStream_t s) {
   if (max_count <= 0 || n_planes <= 0) return;
   hipLaunchKernelGGL(k_pip_mark, dim3(cdiv(max_count, kBS), n_planes), dim3(kBS), 0, s, cand, mask,
-                     offs, counts, n, absorbed, processed, abs_cnt);
+                     offs, n, absorbed, processed, abs_cnt);
+}
+
+void launch_xyz_insert(const float* X, const float* Y, const float* Z, int n, int32_t* table,
+                       uint32_t tmask, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_xyz_insert, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, X, Y, Z, n, table, tmask);
+}
+
+void launch_xyz_lookup(const float* qx, const float* qy, const float* qz, int m,
+                       const int32_t* table, uint32_t tmask, const float* X, const float* Y,
+                       const float* Z, int32_t* nn, int32_t* rest, uint32_t* n_rest,
+                       hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_xyz_lookup, dim3(cdiv(m, kBS)), dim3(kBS), 0, s, qx, qy, qz, m, table, tmask,
+                     X, Y, Z, nn, rest, n_rest);
 }
 
 void launch_mark_nn(const int32_t* nn, int m, uint8_t* processed, hipStream_t s) {

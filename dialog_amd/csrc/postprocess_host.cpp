@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <limits>
 #include <thread>
 #include <vector>
@@ -200,7 +201,8 @@ void plane_edges(const float* border, int64_t nb, int64_t sf, PipEdge* out) {
     const V3 pa{a[0], a[1], a[2]}, pb{b[0], b[1], b[2]};
     const V3 nab = v3_normalized(v3_sub(pb, pa));
     out[j].a_dab = make_float4(pa.x, pa.y, pa.z, dist_p2p(pa, pb));
-    out[j].b = make_float4(pb.x, pb.y, pb.z, 0.0f);
+    out[j].b = make_float4(pb.x, pb.y, pb.z,
+                           (std::fabs(pa.x) + std::fabs(pa.y)) + std::fabs(pa.z));
     out[j].nab = make_float4(nab.x, nab.y, nab.z, 0.0f);
   }
 }
@@ -208,6 +210,62 @@ void plane_edges(const float* border, int64_t nb, int64_t sf, PipEdge* out) {
 bool finite4(const float* c) {
   return std::isfinite(c[0]) && std::isfinite(c[1]) && std::isfinite(c[2]) && std::isfinite(c[3]);
 }
+
+// the nearest cloud point of every plane point (KdTreeFLANN nearestKSearch k = 1, ties -> lowest
+// index; PlaneDetect.h:1518-1526) -> processed.  Plane points that are cloud points (the usual
+// case: points_set holds copies) are found in an exact-coordinate table; the others take the
+// grid hierarchy search.  Cloud in nw.x/y/z, plane points in nw.qx/qy/qz.
+void mark_nearest(dlg_ctx* c, int n, const BBox& b, int m) {
+  NormalsWork& w = c->nw;
+  PostWork& pw = c->pw;
+  uint32_t tcap = 1024;
+  while (tcap < 2u * (uint32_t)n && tcap < (1u << 31)) tcap <<= 1;
+  pw.table.ensure(tcap);
+  pw.rest.ensure(m);
+  w.nn.ensure(m);
+  w.counters.ensure(8);
+  w.h_cnt.ensure(8);
+  HIPCHK(hipMemsetAsync(pw.table.p, 0xff, (size_t)tcap * 4, c->stream));
+  HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
+  launch_xyz_insert(w.x.p, w.y.p, w.z.p, n, pw.table.p, tcap - 1, c->stream);
+  launch_xyz_lookup(w.qx.p, w.qy.p, w.qz.p, m, pw.table.p, tcap - 1, w.x.p, w.y.p, w.z.p, w.nn.p,
+                    pw.rest.p, w.counters.p, c->stream);
+  HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  int nq = (int)w.h_cnt.p[0];
+  if (nq > 0) {
+    const KnnLevels L = build_hierarchy(c, n, b, 1);
+    w.queue.ensure(m);
+    w.cand.ensure(m);
+    int32_t* qin = pw.rest.p;
+    int32_t* qout = w.queue.p;
+    for (int l = 0; l < L.levels && nq > 0; ++l) {
+      HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
+      launch_nn1(L, l, qin, nq, w.qx.p, w.qy.p, w.qz.p, w.nn.p, qout, w.counters.p, c->stream);
+      if (l == L.levels - 1) break;
+      HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
+      sync(c);
+      nq = (int)w.h_cnt.p[0];
+      qin = qout;
+      qout = qout == w.queue.p ? w.cand.p : w.queue.p;
+    }
+  }
+  launch_mark_nn(w.nn.p, m, pw.processed.p, c->stream);
+  HIPCHK(hipGetLastError());
+}
+
+// the refit runs on host threads while the device does the nearest-neighbour marking
+struct RefitJob {
+  std::thread th;
+  std::exception_ptr err;
+  ~RefitJob() {
+    if (th.joinable()) th.join();
+  }
+  void wait() {
+    if (th.joinable()) th.join();
+    if (err) std::rethrow_exception(err);
+  }
+};
 
 void post_process(dlg_ctx* c, const dlg_points* cloud, const dlg_planes* P,
                   const dlg_postprocess_params* prm, float* coeffs_out, int64_t* abs_off,
@@ -219,50 +277,47 @@ void post_process(dlg_ctx* c, const dlg_points* cloud, const dlg_planes* P,
   check_radius(prm->radius_local);
   if (!abs_off || !n_rem) throw DlgError(DLG_ERR_INVALID, "absorbed_offsets / n_remaining are null");
   const int np = P->n_planes;
-  refit_planes(P, coeffs_out);
+  if (np > 0 && !coeffs_out) throw DlgError(DLG_ERR_INVALID, "coeffs_out is null");
+  const int start = std::max(0, prm->plane_start_index);
+  for (int k = start; k < np; ++k)
+    if (P->border_offsets[k + 1] == P->border_offsets[k])
+      throw DlgError(DLG_ERR_INVALID, "plane " + std::to_string(k) + " has an empty border");
   const int n = (int)cloud->n;
+  if ((int64_t)n * std::max(np - start, 0) > (int64_t)INT32_MAX)
+    throw DlgError(DLG_ERR_INVALID, "points x absorbing planes exceeds 2^31");
   for (int k = 0; k <= np; ++k) abs_off[k] = 0;
   *n_rem = 0;
-  if (n == 0) return;
+  RefitJob refit;
+  refit.th = std::thread([&] {
+    try {
+      refit_planes(P, coeffs_out);
+    } catch (...) {
+      refit.err = std::current_exception();
+    }
+  });
+  if (n == 0) {
+    refit.wait();
+    return;
+  }
   NormalsWork& w = c->nw;
   PostWork& pw = c->pw;
 
-  // (1) isProcessed: nearest cloud point of every plane point (kd-tree 1-NN, :1518-1526)
+  // (1) isProcessed from the plane points' nearest cloud points (:1518-1526)
   const BBox b = upload_points(c, cloud);  // nw.x/y/z
   pw.processed.ensure(n);
   HIPCHK(hipMemsetAsync(pw.processed.p, 0, n, c->stream));
   const int m = np > 0 ? (int)P->point_offsets[np] : 0;
   if (m > 0) {
-    const KnnLevels L = build_hierarchy(c, n, b, 1);
     w.qx.ensure(m); w.qy.ensure(m); w.qz.ensure(m);
     upload_records(c, P->points, m, P->points_stride_bytes, w.qx.p, w.qy.p, w.qz.p);
-    w.nn.ensure(m);
-    w.queue.ensure(m);
-    w.cand.ensure(m);
-    int32_t* qin = nullptr;
-    int32_t* qout = w.queue.p;
-    int nq = m;
-    for (int l = 0; l < L.levels && nq > 0; ++l) {
-      HIPCHK(hipMemsetAsync(w.counters.p, 0, 4, c->stream));
-      launch_nn1(L, l, qin, nq, w.qx.p, w.qy.p, w.qz.p, w.nn.p, qout, w.counters.p, c->stream);
-      if (l == L.levels - 1) break;
-      HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
-      sync(c);
-      nq = (int)w.h_cnt.p[0];
-      qin = qout;
-      qout = qout == w.queue.p ? w.cand.p : w.queue.p;
-    }
-    launch_mark_nn(w.nn.p, m, pw.processed.p, c->stream);
+    mark_nearest(c, n, b, m);
   }
+  refit.wait();
 
   // (2) absorption into planes [start, np) (:1530-1556)
-  const int start = std::max(0, prm->plane_start_index);
   std::vector<int> act;  // participating planes; a NaN plane accepts nothing (every test is NaN)
-  for (int k = start; k < np; ++k) {
-    if (P->border_offsets[k + 1] == P->border_offsets[k])
-      throw DlgError(DLG_ERR_INVALID, "plane " + std::to_string(k) + " has an empty border");
+  for (int k = start; k < np; ++k)
     if (finite4(coeffs_out + 4 * k)) act.push_back(k);
-  }
   const int na = (int)act.size();
   std::vector<int64_t> abs_cnt_h(np, 0);
   int64_t abs_total = 0;
@@ -288,47 +343,58 @@ void post_process(dlg_ctx* c, const dlg_points* cloud, const dlg_planes* P,
     pw.rays.ensure((size_t)na * kPipRays);
     pw.edges.ensure(h_edges.size());
     pw.edge_off.ensure(na + 1);
-    pw.counts.ensure(na); pw.offs.ensure(na); pw.cursor.ensure(na); pw.abs_cnt.ensure(na);
+    pw.offs.ensure(na + 1);
+    pw.abs_cnt.ensure(na);
+    const size_t nbk = (size_t)na * pip_blocks(n);
+    pw.bcnt.ensure(nbk);
+    pw.boff.ensure(nbk);
+    w.sort_tmp.ensure(pip_scan_tmp_bytes(nbk));
     HIPCHK(hipMemcpyAsync(pw.planes.p, h_planes.data(), na * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(pw.rays.p, h_rays.data(), h_rays.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(pw.edges.p, h_edges.data(), h_edges.size() * sizeof(PipEdge), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(pw.edge_off.p, h_eoff.data(), (na + 1) * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemsetAsync(pw.counts.p, 0, na * 4, c->stream));
-    launch_pip_candidates(w.x.p, w.y.p, w.z.p, n, pw.processed.p, pw.planes.p, na,
-                          prm->t_dist_point_plane, pw.counts.p, nullptr, nullptr, nullptr,
-                          c->stream);
-    std::vector<uint32_t> cnt(na), offs(na);
-    HIPCHK(hipMemcpyAsync(cnt.data(), pw.counts.p, na * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(launch_pip_candidates(w.x.p, w.y.p, w.z.p, n, pw.processed.p, pw.planes.p, na,
+                                 prm->t_dist_point_plane, pw.bcnt.p, pw.boff.p, w.sort_tmp.p,
+                                 w.sort_tmp.cap, nullptr, pw.offs.p, c->stream));
+    std::vector<uint32_t> offs(na + 1);
+    HIPCHK(hipMemcpyAsync(offs.data(), pw.offs.p, (na + 1) * 4, hipMemcpyDeviceToHost, c->stream));
     sync(c);
-    uint64_t total = 0;
+    const uint32_t total = offs[na];
     int max_cnt = 0;
-    for (int a = 0; a < na; ++a) {
-      offs[a] = (uint32_t)total;
-      total += cnt[a];
-      max_cnt = std::max(max_cnt, (int)cnt[a]);
-    }
-    if (total > (uint64_t)INT32_MAX) throw DlgError(DLG_ERR_INVALID, "too many (point, plane) candidates");
+    for (int a = 0; a < na; ++a) max_cnt = std::max(max_cnt, (int)(offs[a + 1] - offs[a]));
     if (total > 0) {
       pw.cand.ensure(total);
+      pw.cand2.ensure(total);
       pw.mask.ensure(total);
-      HIPCHK(hipMemcpyAsync(pw.offs.p, offs.data(), na * 4, hipMemcpyHostToDevice, c->stream));
-      HIPCHK(hipMemsetAsync(pw.cursor.p, 0, na * 4, c->stream));
-      HIPCHK(hipMemsetAsync(pw.mask.p, 0, total * 4, c->stream));
-      launch_pip_candidates(w.x.p, w.y.p, w.z.p, n, pw.processed.p, pw.planes.p, na,
-                            prm->t_dist_point_plane, pw.counts.p, pw.offs.p, pw.cursor.p,
-                            pw.cand.p, c->stream);
+      HIPCHK(hipMemsetAsync(pw.mask.p, 0, (size_t)total * 4, c->stream));
+      HIPCHK(launch_pip_candidates(w.x.p, w.y.p, w.z.p, n, pw.processed.p, pw.planes.p, na,
+                                   prm->t_dist_point_plane, pw.bcnt.p, pw.boff.p, nullptr, 0,
+                                   pw.cand2.p, pw.offs.p, c->stream));
+      {  // spatial order within each plane (Morton code over the cloud's bounding box)
+        float ext = 0.0f;
+        for (int k = 0; k < 3; ++k) ext = std::max(ext, b.hi[k] - b.lo[k]);
+        const float4 ls = make_float4(b.lo[0], b.lo[1], b.lo[2], ext > 0.0f ? 16383.0f / ext : 0.0f);
+        w.keys64.ensure(total);
+        w.keys_alt.ensure(total);
+        w.sort_tmp.ensure(pip_sort_tmp_bytes((int)total));
+        HIPCHK(launch_pip_sort(pw.cand2.p, (int)total, pw.offs.p, na, max_cnt, w.x.p, w.y.p, w.z.p,
+                               ls, reinterpret_cast<uint64_t*>(w.keys64.p),
+                               reinterpret_cast<uint64_t*>(w.keys_alt.p), pw.cand.p, w.sort_tmp.p,
+                               w.sort_tmp.cap, c->stream));
+      }
       // tasks: 256 candidates x a run of edges; edges split so the launch fills the chip
       int64_t cblocks = 0;
-      for (int a = 0; a < na; ++a) cblocks += (cnt[a] + 255) / 256;
+      for (int a = 0; a < na; ++a) cblocks += (offs[a + 1] - offs[a] + 255) / 256;
       const int64_t want = 8LL * 256;
       const int64_t split = std::max<int64_t>(1, (want + cblocks - 1) / std::max<int64_t>(cblocks, 1));
       std::vector<PipTask> tasks;
       for (int a = 0; a < na; ++a) {
         const int64_t nb = h_eoff[a + 1] - h_eoff[a];
         const int64_t chunk = std::max<int64_t>(16, (nb + split - 1) / split);
-        for (uint32_t cb = 0; cb < cnt[a]; cb += 256)
+        const uint32_t cnt = offs[a + 1] - offs[a];
+        for (uint32_t cb = 0; cb < cnt; cb += 256)
           for (int64_t e = 0; e < nb; e += chunk)
-            tasks.push_back(PipTask{a, (int32_t)(offs[a] + cb), (int32_t)std::min<uint32_t>(256, cnt[a] - cb),
+            tasks.push_back(PipTask{a, (int32_t)(offs[a] + cb), (int32_t)std::min<uint32_t>(256, cnt - cb),
                                     (int32_t)e, (int32_t)std::min(nb, e + chunk)});
       }
       pw.tasks.ensure(tasks.size());
@@ -339,8 +405,8 @@ void post_process(dlg_ctx* c, const dlg_points* cloud, const dlg_planes* P,
       pw.absorbed.ensure((size_t)na * n);
       HIPCHK(hipMemsetAsync(pw.absorbed.p, 0, (size_t)na * n, c->stream));
       HIPCHK(hipMemsetAsync(pw.abs_cnt.p, 0, na * 4, c->stream));
-      launch_pip_mark(pw.cand.p, pw.mask.p, pw.offs.p, pw.counts.p, na, max_cnt, n,
-                      pw.absorbed.p, pw.processed.p, pw.abs_cnt.p, c->stream);
+      launch_pip_mark(pw.cand.p, pw.mask.p, pw.offs.p, na, max_cnt, n, pw.absorbed.p,
+                      pw.processed.p, pw.abs_cnt.p, c->stream);
       HIPCHK(hipGetLastError());
       std::vector<uint32_t> ac(na);
       HIPCHK(hipMemcpyAsync(ac.data(), pw.abs_cnt.p, na * 4, hipMemcpyDeviceToHost, c->stream));

@@ -322,6 +322,74 @@ inline void preProcess(const pcl::PointCloud<PointT>& cloud, bool translate, flo
   if (translation) { translation[0] = tr[0]; translation[1] = tr[1]; translation[2] = tr[2]; }
 }
 
+// The fields of the reference's struct Plane (HeaderFile.h:81-88) that postProcessPlanes reads
+// and writes: points_set, coeff.values (3 = outward normal before the first post-process, 4
+// after) and border (the polyPlanes polygon, PlaneDetect.h:1358-1436).
+template <typename PointT>
+struct PlaneSet {
+  pcl::PointCloud<PointT> points_set;
+  std::vector<float> coeff;
+  pcl::PointCloud<PointT> border;
+};
+
+struct PostProcessParams {
+  float t_dist_point_plane = 0.1f;  // config.ini [PlaneDetect] T_dist_point_plane
+  float radius_local = 0.1f;        // radius_local (clusterFilt)
+  int t_cluster_num = 500;          // T_cluster_num
+  uint32_t rand_seed = 0;           // the time(0) value isPointInPoly seeds rand() with
+};
+
+// postProcessPlanes() (PlaneDetect.h:1454-1579) on the GPU: every plane's coeff becomes the
+// oriented computePointNormal refit (4 values); planes [plane_start_index, size) absorb the
+// cloud points inside their border polygon (appended to points_set in cloud order);
+// source_cloud is replaced by the points left after clusterFilt; plane_start_index advances to
+// planes.size() as in the reference (:1557-1558).
+template <typename PointT>
+inline void postProcessPlanes(pcl::PointCloud<PointT>& source_cloud,
+                              std::vector<PlaneSet<PointT>>& planes, int& plane_start_index,
+                              const PostProcessParams& pp, Context* ctx = nullptr) {
+  dlg_ctx* c = (ctx ? ctx : &Context::thread_default())->get();
+  const size_t np = planes.size();
+  std::vector<float> coeffs(4 * (np ? np : 1), 0.0f), out(4 * (np ? np : 1), 0.0f);
+  std::vector<PointT> pts, bor;
+  std::vector<int64_t> poff(np + 1, 0), boff(np + 1, 0);
+  for (size_t k = 0; k < np; ++k) {
+    for (size_t j = 0; j < planes[k].coeff.size() && j < 4; ++j) coeffs[4 * k + j] = planes[k].coeff[j];
+    pts.insert(pts.end(), planes[k].points_set.points.begin(), planes[k].points_set.points.end());
+    bor.insert(bor.end(), planes[k].border.points.begin(), planes[k].border.points.end());
+    poff[k + 1] = (int64_t)pts.size();
+    boff[k + 1] = (int64_t)bor.size();
+  }
+  dlg_planes P{(int32_t)np, coeffs.data(), pts.empty() ? nullptr : &pts[0].x, (int64_t)sizeof(PointT),
+               poff.data(), bor.empty() ? nullptr : &bor[0].x, (int64_t)sizeof(PointT), boff.data()};
+  dlg_postprocess_params prm{pp.t_dist_point_plane, pp.radius_local, (int32_t)pp.t_cluster_num,
+                             (int32_t)plane_start_index, pp.rand_seed};
+  dlg_points cl{source_cloud.points.empty() ? nullptr : &source_cloud.points[0].x,
+                (int64_t)source_cloud.points.size(), (int64_t)sizeof(PointT)};
+  std::vector<int64_t> aoff(np + 1, 0);
+  std::vector<int32_t> ids(source_cloud.points.size() ? source_cloud.points.size() : 1);
+  std::vector<int32_t> rem(source_cloud.points.size() ? source_cloud.points.size() : 1);
+  int64_t nrem = 0;
+  dlg_status st = dlg_post_process_planes(c, &cl, &P, &prm, out.data(), aoff.data(), ids.data(),
+                                          (int64_t)ids.size(), rem.data(), (int64_t)rem.size(), &nrem);
+  if (st == DLG_ERR_CAPACITY && aoff[np] > (int64_t)ids.size()) {  // a point joined several planes
+    ids.resize((size_t)aoff[np]);
+    st = dlg_post_process_planes(c, &cl, &P, &prm, out.data(), aoff.data(), ids.data(),
+                                 (int64_t)ids.size(), rem.data(), (int64_t)rem.size(), &nrem);
+  }
+  check(st, c);
+  for (size_t k = 0; k < np; ++k) {
+    planes[k].coeff.assign(out.begin() + 4 * k, out.begin() + 4 * k + 4);
+    for (int64_t t = aoff[k]; t < aoff[k + 1]; ++t) planes[k].points_set.push_back(source_cloud.points[ids[t]]);
+  }
+  pcl::PointCloud<PointT> kept;
+  kept.points.reserve((size_t)nrem);
+  for (int64_t t = 0; t < nrem; ++t) kept.points.push_back(source_cloud.points[rem[t]]);
+  kept.width = (uint32_t)kept.points.size();
+  source_cloud = std::move(kept);
+  plane_start_index = (int)np;
+}
+
 // Result of the plane stage for one plane: coefficients (a, b, c, d) and inlier ids.  The
 // reference's struct Plane (HeaderFile.h:81-88) is filled from it by copying the inlier points
 // into points_set and coeff.values (see INTEGRATION.md for the PlaneDetect.h adapter).

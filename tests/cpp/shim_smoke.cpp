@@ -56,6 +56,23 @@ int main(int argc, char** argv) {
     float tr[3];
     dialog::preProcess(*cloud, true, 0.15f, pre, &kept, tr);
     std::printf("preprocess %zu %zu\n", pre.points.size(), kept.size());
+    // postProcessPlanes: the 64x64 sheet as one plane holding every other point, its square
+    // border; the other half is absorbed, the 500-point line is one cluster of the rest
+    std::vector<dialog::PlaneSet<pcl::PointXYZ>> ps(1);
+    for (int i = 0; i < 64 * 64; i += 2) ps[0].points_set.push_back(cloud->points[i]);
+    ps[0].coeff = {0.0f, 0.0f, 1.0f};
+    ps[0].border.push_back(pcl::PointXYZ(-0.05f, -0.05f, 0.0f));
+    ps[0].border.push_back(pcl::PointXYZ(6.35f, -0.05f, 0.0f));
+    ps[0].border.push_back(pcl::PointXYZ(6.35f, 6.35f, 0.0f));
+    ps[0].border.push_back(pcl::PointXYZ(-0.05f, 6.35f, 0.0f));
+    pcl::PointCloud<pcl::PointXYZ> src = *cloud;
+    int start = 0;
+    dialog::PostProcessParams pp;
+    pp.radius_local = 0.05f;
+    pp.t_cluster_num = 10;
+    dialog::postProcessPlanes(src, ps, start, pp);
+    std::printf("postprocess %zu %zu %zu %d\n", ps[0].points_set.points.size(), src.points.size(),
+                ps[0].coeff.size(), start);
     return 0;
   } catch (const dialog::Error& e) {
     std::fprintf(stderr, "dialog error: %s\n", e.what());

@@ -240,6 +240,9 @@ def test_cpp_shim_runs_on_gpu(tmp_path):
     assert int(nrm[0]) == 64 * 64 + 500 and int(nrm[2]) > 0 and int(nrm[4]) > 0
     pre = lines["preprocess"].split()
     assert 0 < int(pre[0]) == int(pre[1]) < 64 * 64 + 500
+    post = [int(x) for x in lines["postprocess"].split()]
+    assert post[0] > 64 * 32 and post[2] == 4 and post[3] == 1
+    assert post[0] + post[1] <= 64 * 64 + 500
 
 
 def test_rccl_one_rank_path(monkeypatch, gpu_ctx):

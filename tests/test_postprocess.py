@@ -212,6 +212,23 @@ def test_gpu_post_process_edges(gpu_ctx):
 
 
 @pytest.mark.gpu
+def test_gpu_post_process_nearest_fallback(gpu_ctx):
+    """plane points that are not cloud points (nudged copies, points with a zero coordinate, a
+    point far away): their nearest cloud point comes from the grid search, not the exact table"""
+    cloud, planes = star_scene(12000, 3, seed=41)
+    rng = np.random.default_rng(2)
+    for pl in planes:
+        p = pl["points"].copy()
+        sel = rng.random(len(p)) < 0.5
+        p[sel] = np.nextafter(p[sel], np.float32(np.inf))
+        p[:3, 0] = 0.0
+        p[3] = [50.0, -50.0, 50.0]
+        pl["points"] = p
+    g = gpu_run(gpu_ctx, cloud, planes)
+    assert_same(g, oracle_run(cloud, planes))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,r,T", [(5000, 0.3, 10), (30000, 0.2, 3), (2000, 0.0, 0)])
 def test_gpu_cluster_filter_bit_exact(gpu_ctx, n, r, T):
     import dialog_amd as D

@@ -25,6 +25,8 @@ for s in $STEPS; do
     bench)  run bench 600 python3 bench.py ;;
     normals) run normals_gpu 600 python3 -m pytest tests/test_normals.py -m gpu -x -q -rA ;;
     post)   run post_gpu 600 python3 -m pytest tests/test_postprocess.py -m gpu -x -q -rA ;;
+    pbench) run pbench 600 python3 tools/bench_post.py ;;
+    pprof)  run pprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pprof -o run -- python3 tools/bench_post.py 10000000 2 ;;
     nbench) run nbench 600 python3 tools/bench_normals.py ;;
     c5)     run c5 600 python3 tools/bench_c5.py ;;
     c5prof) run c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof -o run -- python3 tools/bench_c5.py 10000000 2 ;;
