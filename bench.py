@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--torch-dist", action="store_true",
                     help="rendezvous through torch.distributed even at N=1 (runtime check)")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the C5 (normals + NORMAL_PLANE) secondary measurement")
+                    help="skip the C5 (normals + NORMAL_PLANE + post-process) secondary measurement")
     return ap.parse_args()
 
 
@@ -61,7 +61,8 @@ def c5_secondary(D, ctx, a):
     (weight 0.1) with the C3 RANSAC settings; plus RegulateNormal over the same cloud."""
     from dialog_amd.synth import SEED_BASE, plane_cloud
     pts, _, _ = plane_cloud(a.points, a.planes, seed=SEED_BASE + 5)
-    out = {"workload": "C5: 10M-pt 20-plane cloud, k=20 normals, NORMAL_PLANE (w=0.1) extract",
+    out = {"workload": "C5: 10M-pt 20-plane cloud, k=20 normals, NORMAL_PLANE (w=0.1) extract; "
+                       "postProcessPlanes on a 10M-pt 20-plane scene (1000-vertex borders)",
            "points": a.points}
 
     def timed(f, reps=2):
@@ -102,6 +103,16 @@ def c5_secondary(D, ctx, a):
     for k in ("normals_knn20_ms", "normals_radius0.1_ms", "regulate_r0.1_ms", "preprocess_0.001_ms"):
         out[k] = round(out[k], 2)
     cloud.close()
+    # postProcessPlanes on the same cloud size: 70% of each plane's points in its points_set,
+    # 1000-vertex concave borders, config.ini [PlaneDetect] T_dist 0.1 / radius_local 0.1 /
+    # T_cluster_num 500
+    from dialog_amd.synth import postprocess_scene
+    pc, planes = postprocess_scene(a.points, a.planes, n_border=1000, seed=SEED_BASE + 5)
+    pprm = D.PostProcessParams(0.1, 0.1, 500, 0, 12345)
+    po, out["post_process_ms"] = timed(lambda: D.post_process_planes(pc, planes, pprm, ctx=ctx))
+    out["post_process_ms"] = round(out["post_process_ms"], 2)
+    out["post_absorbed"] = int(sum(x.size for x in po[1]))
+    out["post_remaining"] = int(po[2].size)
     return out
 
 
