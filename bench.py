@@ -12,8 +12,8 @@ one global cloud (same 20 planes); every round all ranks score the same hypothes
 shards with one RCCL allreduce of the int32[4096] counts.
 
 value = useful point-plane tests (PCL iterations x global active points, summed over rounds) / s,
-whole job.  Roofline: the scoring kernel k_score, VALU-bound (7 f32 VALU ops per test), timed with
-HIP events on the library's stream.  cpu_baseline: the PCL-1.8 restatement (oracle, 1 thread) on
+whole job.  Roofline: the scoring kernel (k_score_bf16 by default), against the f32 VALU peak with
+SURVEY 8(d)'s algorithmic 7 ops per test, timed with HIP events on the library's stream.  cpu_baseline: the PCL-1.8 restatement (oracle, 1 thread) on
 a bounded sample of the same workload, rank 0 at N = 1 only.
 """
 from __future__ import annotations
@@ -189,8 +189,14 @@ def main():
     avg_launch_ms = score_ms / max(launches, 1)
     ktests_per_s = per_rank_tests / (score_ms / 1e3) if score_ms > 0 else 0.0
     achieved = 7.0 * ktests_per_s / 1e12
+    variant = int(os.environ.get("DLG_SCORE_VARIANT", "19"))
+    kname = {19: "k_score_bf16<8> (countWithinDistance: plane distances on the bf16 matrix cores, "
+                 "exact 3-way split operands; VALU sign count + rounding-band re-decision in PCL "
+                 "op order; 4096 hypotheses/launch)",
+             5: "k_score<exact,4> (countWithinDistance in PCL op order on the VALU, 4096 "
+                "hypotheses/launch)"}.get(variant, f"score variant {variant}")
     roofline = {
-        "kernel": "k_score (countWithinDistance, 4096 hypotheses/launch)",
+        "kernel": kname,
         "bound": "valu",
         "achieved": round(achieved, 3),
         "peak": round(VALU_PEAK_TOPS, 2),
@@ -204,8 +210,12 @@ def main():
         "hbm_view": {"algorithmic_GBps": round(12.0 * (per_rank_tests / max(a.hyps, 1)) /
                                               (score_ms / 1e3) / 1e9, 2) if score_ms else None,
                      "peak_GBps": HBM_PEAK_GBS},
-        "note": "1 op = one f32 VALU lane-op (3 mul + 3 add + 1 cmp per test, no FMA for PCL "
-                "bit-parity); peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz",
+        "note": "achieved = SURVEY 8(d) algorithmic work, 7 f32 ops per test (3 mul + 3 add + 1 "
+                "cmp, PCL op order) x tests / kernel time; peak = f32 VALU, 256 CU x 4 SIMD x 32 "
+                "lanes x 2.4 GHz.  The default kernel runs the multiply-adds on the bf16 matrix "
+                "cores (2 v_mfma_f32_32x32x16_bf16 per 1024 tests, ~29% of the MFMA pipe) and "
+                "~3.2 VALU lane-ops per test (rocprofv3 SQ_INSTS_VALU), so frac near or above 1 "
+                "means the work left the VALU, not that the VALU is saturated",
     }
     traffic_file = os.path.join(ROOT, "profiles", "score_traffic.json")
     if os.path.exists(traffic_file):

@@ -2,7 +2,8 @@
 
 Flags that matter for parity with PCL: -ffp-contract=off (no fused multiply-adds except the explicit
 ones), -fhip-fp32-correctly-rounded-divide-sqrt (IEEE f32 / and sqrt), -fno-slp-vectorize (keeps
-the scoring loop in single-issue f32 ops instead of v_pk_* pairs).
+the scoring loop in single-issue f32 ops instead of v_pk_* pairs), and
+-amdgpu-mfma-vgpr-form (bf16 scoring variant: MFMA accumulators in VGPRs).
 """
 from __future__ import annotations
 
@@ -21,7 +22,9 @@ HEADERS = ["kernels.hpp", "normals.hpp", "comm.hpp", "driver.hpp", "host_math.hp
 ARCH = os.environ.get("DLG_OFFLOAD_ARCH", "gfx950")
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
-            "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function"]
+            "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function",
+            # MFMA results in VGPRs (the VALU consumes every element; AGPR copies cost 1 op each)
+            "-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 
 def hipcc() -> str:

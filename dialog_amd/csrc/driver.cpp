@@ -303,7 +303,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (np)
       launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
     else
-      launch_score(src, c->hyps.p, D, cthr, c->res.p, kScoreDefault, c->num_cus, c->stream);
+      launch_score(src, c->hyps.p, D, cthr, c->res.p, score_variant(), c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);

@@ -460,6 +460,223 @@ __global__ __launch_bounds__(kScBS) void k_score_mfma(const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_score_bf16: the plane distance D = a x + b y + c z + d on the bf16 matrix cores.
+//
+// Every float is split exactly into three bf16 pieces v = v1 + v2 + v3 (truncations: v1 = top 8
+// significand bits, v2 = the next 8 of the remainder, v3 = the rest, <= 8 bits), so bf16 x bf16
+// products are exact in f32.  One 32-element dot product per (point, plane) keeps the products
+// v1 c1, v1 c2, v2 c1, v1 c3, v3 c1, v2 c2 of each coordinate (dropped: <= 2.1 u |v c|, u = 2^-24)
+// and d1 + d2 + d3 (point side 1, 1, 1):
+//   A row  (point):  x1 x1 x2 x1 x3 x2 | y1 y1 y2 y1 y3 y2 | z1 z1 z2 z1 z3 z2 | 1  1  1 | 0 x 11
+//   B col  (plane):  a1 a2 a1 a3 a1 a2 | b1 b2 b1 b3 b1 b2 | c1 c2 c1 c3 c1 c2 | d1 d2 d3 | 0 x 11
+// two v_mfma_f32_32x32x16_bf16 (K = 32) per 32 x 32 tile of (points, planes).
+// Error: the 21 exact products are summed with <= 20 f32 roundings (<= 40 u sum|p| even if the
+// hardware truncated), + dropped products 2.1 u S, + PCL's own rounding of pcl_dot <= 4 u S, so
+// |D - pcl_dot| <= e = 64 u S (S = |a| ax + |b| ay + |c| az + |d|, 1.4x margin), floored at 1e-7.
+// With r = |D| - cthr: |r| > w = 1.002 e decides exactly (r < 0: inlier).  The VALU per element:
+// r (1 op), the sign bits of four r gathered by two v_perm_b32 into bytes 0x00 / 0xFF and summed
+// by one v_sad_u8 (0.75 op), min |r| by v_min3 (0.5 op).  When some lane's min |r| <= w (an
+// element inside the rounding band, ~1e-5 of the elements) or the tile holds a missing /
+// non-finite point, the wave re-decides exactly those elements in PCL op order: the point comes
+// from its owner lane by ds_bpermute, the plane from LDS.
+//
+// C/D layout (32x32x16): lane l holds column (plane) l & 31, rows (reg & 3) + 8 (reg >> 2) +
+// 4 (l >> 5); A/B: lane l holds row/col l & 31, k = 8 (l >> 5) + j of each 16-wide K half.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBfBS = 256;  // 4 independent waves
+constexpr uint32_t kBf16One = 0x3F80u;
+
+struct Split3 {
+  uint32_t p1, p2, p3;  // bf16 bit patterns
+};
+
+__device__ __forceinline__ Split3 split3(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const float v1 = __uint_as_float(u & 0xFFFF0000u);
+  const float r1 = v - v1;  // exact (the low 16 significand bits)
+  const uint32_t u2 = __float_as_uint(r1) & 0xFFFF0000u;
+  const float r2 = r1 - __uint_as_float(u2);  // exact, <= 8 significant bits
+  return Split3{u >> 16, u2 >> 16, __float_as_uint(r2) >> 16};
+}
+
+__device__ __forceinline__ uint32_t pk(uint32_t lo, uint32_t hi) { return lo | (hi << 16); }
+
+__device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// per plane: B column (4 x uint4 = k 0-7, 8-15, 16-23, 24-31) and band half-width w
+__global__ void k_prep_bf16(const HypRec* __restrict__ hyps, int D, int Dp,
+                            uint4* __restrict__ bcol, float* __restrict__ band) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= Dp) return;
+  HypRec hr;
+  hr.good = 0;
+  if (h < D) hr = hyps[h];
+  const bool ok = hr.good && isfinite(hr.a) && isfinite(hr.b) && isfinite(hr.c) && isfinite(hr.d);
+  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+  // not a plane (bad sample, NaN coefficients: PCL counts nothing): B = 0 and d = 2 so D = 2,
+  // |r| >= 1.9 > w = 0 -- counts nothing, never re-decided
+  float w = 0.0f;
+  if (ok) {
+    const Split3 a = split3(hr.a), b = split3(hr.b), c = split3(hr.c), d = split3(hr.d);
+    q0 = make_uint4(pk(a.p1, a.p2), pk(a.p1, a.p3), pk(a.p1, a.p2), pk(b.p1, b.p2));
+    q1 = make_uint4(pk(b.p1, b.p3), pk(b.p1, b.p2), pk(c.p1, c.p2), pk(c.p1, c.p3));
+    q2 = make_uint4(pk(c.p1, c.p2), pk(d.p1, d.p2), pk(d.p3, 0u), 0u);
+    // hr.w >= 7 u S (k_build_hyps), so e = 64 u S <= hr.w * 64 / 7 (1% slack)
+    const double e = fmax((double)hr.w * (64.0 / 7.0) * 1.01, 1e-7);
+    // no finite bound (an infinite coordinate in the cloud): every element is re-decided
+    w = isfinite(hr.w) ? __double2float_ru(1.002 * e) : INFINITY;
+  } else {
+    q2 = make_uint4(0u, pk(0x4000u, 0u), 0u, 0u);  // d1 = 2.0
+  }
+  bcol[4 * h] = q0; bcol[4 * h + 1] = q1; bcol[4 * h + 2] = q2; bcol[4 * h + 3] = q3;
+  band[h] = w;
+}
+
+// sign bytes of r0..r3 (0xFF if negative) -> acc += 255 * #negative
+__device__ __forceinline__ uint32_t count4(float r0, float r1, float r2, float r3, uint32_t acc) {
+  // v_perm_b32 selectors: 9 = sign(S1) x 8, 11 = sign(S0) x 8, 12 = 0x00
+  const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(r0), __float_as_uint(r1), 0x0C0C0B09u);
+  const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(r2), __float_as_uint(r3), 0x0B090C0Cu);
+  return __builtin_amdgcn_sad_u8(lo, hi, acc);
+}
+
+__device__ __forceinline__ float min3_abs(float m, float a, float b) {
+  float o;
+  asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(o) : "v"(m), "v"(a), "v"(b));
+  return o;
+}
+
+template <int TH>
+__global__ __launch_bounds__(kBfBS) void k_score_bf16(const float* __restrict__ X,
+                                                      const float* __restrict__ Y,
+                                                      const float* __restrict__ Z, int n,
+                                                      const HypRec* __restrict__ hyps,
+                                                      const uint4* __restrict__ bcol,
+                                                      const float* __restrict__ band, int D,
+                                                      int ngroups, int part, float cthr,
+                                                      int32_t* __restrict__ counts) {
+  __shared__ float4 s_coef[kBfBS / kWave][TH * 32];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = threadIdx.x / kWave;
+  const int wid = blockIdx.x * (kBfBS / kWave) + wv;
+  const int g = wid % ngroups;  // this wave's planes: [g * 32 TH, (g + 1) * 32 TH)
+  const int pi = wid / ngroups;  // this wave's points: [pi * part, min(n, (pi + 1) * part))
+  const int p_beg = pi * part;
+  const int p_end = min(n, p_beg + part);
+  const int r32 = lane & 31, hh = lane >> 5;
+  for (int k = lane; k < TH * 32; k += kWave) {
+    const int h = g * TH * 32 + k;
+    const HypRec hr = hyps[min(h, max(D - 1, 0))];
+    s_coef[wv][k] = make_float4(hr.a, hr.b, hr.c, hr.d);
+  }
+  if (p_beg >= n) return;  // wave-uniform; no block-wide barrier below
+  u32x4 b1[TH], b2[TH];
+  float wb[TH];
+  uint32_t cnt[TH];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    const int h = (g * TH + t) * 32 + r32;
+    const uint4 q = bcol[4 * h + hh], q2 = bcol[4 * h + 2 + hh];
+    b1[t] = u32x4{q.x, q.y, q.z, q.w};
+    b2[t] = u32x4{q2.x, q2.y, q2.z, q2.w};
+    wb[t] = band[h];
+    cnt[t] = 0;
+  }
+  const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // point loads run two tiles ahead of their use
+  float x1 = 0.f, y1 = 0.f, z1 = 0.f, x2 = 0.f, y2 = 0.f, z2 = 0.f;
+  {
+    const int q1 = p_beg + r32, q2 = p_beg + 32 + r32;
+    if (q1 < p_end) { x1 = X[q1]; y1 = Y[q1]; z1 = Z[q1]; }
+    if (q2 < p_end) { x2 = X[q2]; y2 = Y[q2]; z2 = Z[q2]; }
+  }
+  for (int p0 = p_beg; p0 < p_end; p0 += 32) {
+    const bool valid = p0 + r32 < p_end;
+    const float x = x1, y = y1, z = z1;
+    x1 = x2; y1 = y2; z1 = z2;
+    {
+      const int q = p0 + 64 + r32;
+      x2 = 0.f; y2 = 0.f; z2 = 0.f;
+      if (q < p_end) { x2 = X[q]; y2 = Y[q]; z2 = Z[q]; }
+    }
+    // a tile with a missing or non-finite point is re-decided element by element
+    const bool bad = __builtin_amdgcn_ballot_w64(!valid || !(isfinite(x) && isfinite(y) && isfinite(z))) != 0;
+    const Split3 sx = split3(x), sy = split3(y), sz = split3(z);
+    u32x4 a1, a2;
+    if (hh == 0) {
+      a1 = u32x4{pk(sx.p1, sx.p1), pk(sx.p2, sx.p1), pk(sx.p3, sx.p2), pk(sy.p1, sy.p1)};
+      a2 = u32x4{pk(sz.p3, sz.p2), pk(kBf16One, kBf16One), pk(kBf16One, 0u), 0u};
+    } else {
+      a1 = u32x4{pk(sy.p2, sy.p1), pk(sy.p3, sy.p2), pk(sz.p1, sz.p1), pk(sz.p2, sz.p1)};
+      a2 = u32x4{0u, 0u, 0u, 0u};
+    }
+    const bf16x8 A1 = as_bf16x8(a1), A2 = as_bf16x8(a2);
+    uint32_t amask = 0;  // bit t: some element of plane tile t lies within its band
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      f32x16 Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, as_bf16x8(b1[t]), zero, 0, 0, 0);
+      Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, as_bf16x8(b2[t]), Dv, 0, 0, 0);
+      uint32_t acc = cnt[t];
+      float m = INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        const float r0 = fabsf(Dv[i]) - cthr, r1 = fabsf(Dv[i + 1]) - cthr;
+        const float r2 = fabsf(Dv[i + 2]) - cthr, r3 = fabsf(Dv[i + 3]) - cthr;
+        acc = count4(r0, r1, r2, r3, acc);
+        m = min3_abs(m, r0, r1);
+        m = min3_abs(m, r2, r3);
+      }
+      cnt[t] = acc;
+      amask |= m <= wb[t] ? (1u << t) : 0u;
+    }
+    // rare: re-decide the band elements in PCL op order (D recomputed on the matrix cores)
+    if (__builtin_amdgcn_ballot_w64(bad || amask != 0)) {
+#ifdef DLG_BF16_STATS
+      if (lane == 0) atomicAdd(&counts[0], 1);
+#endif
+#pragma unroll 1
+      for (int t = 0; t < TH; ++t) {
+        const bool need = bad || ((amask >> t) & 1u);
+        if (!__builtin_amdgcn_ballot_w64(need)) continue;
+        f32x16 Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, as_bf16x8(b1[t]), zero, 0, 0, 0);
+        Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, as_bf16x8(b2[t]), Dv, 0, 0, 0);
+        const float4 cf = s_coef[wv][t * 32 + r32];
+        const float w = wb[t];
+        uint32_t acc = cnt[t];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float ri = fabsf(Dv[i]) - cthr;
+          const bool inb = need && (bad || fabsf(ri) <= w);
+          if (__builtin_amdgcn_ballot_w64(inb)) {
+#ifdef DLG_BF16_STATS
+            if (lane == 0) atomicAdd(&counts[1], 1);
+#endif
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const float px = __shfl(x, row, kWave), py = __shfl(y, row, kWave);
+            const float pz = __shfl(z, row, kWave);
+            const bool ex = p0 + row < p_end &&
+                            fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, px, py, pz)) < cthr;
+            const uint32_t approx = __float_as_uint(ri) >> 31;  // what count4 counted
+            if (inb) acc = acc + (ex ? 255u : 0u) - 255u * approx;
+          }
+        }
+        cnt[t] = acc;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    uint32_t c = cnt[t] / 255u;
+    c += __shfl_xor(c, 32);  // lanes l and l + 32 hold the two row halves of column l & 31
+    const int h = (g * TH + t) * 32 + r32;
+    if (hh == 0 && c && h < D) atomicAdd(&counts[h], (int32_t)c);
+  }
+}
+
 // v_min_f32 m, m, |r| without the canonicalising v_max that fminf() brings along
 __device__ __forceinline__ float min_abs(float m, float r) {
   float o;
@@ -1092,7 +1309,18 @@ void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, fl
                      ay, az, hyps, good);
 }
 
-int kScoreDefault = kScoreExactP4;  // fastest measured (tools/score_ab.py)
+// fastest measured with bit-identical counts (tools/score_ab.py, tests/test_score_variants.py):
+// bf16 matrix-core distances + VALU band check 10.8 T tests/s vs 7.6 T for the exact VALU kernel
+int kScoreDefault = kScoreBf16T8;
+
+int score_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("DLG_SCORE_VARIANT");
+    const int x = e ? std::atoi(e) : -1;
+    return x >= 0 && x < kScoreNumVariants ? x : kScoreDefault;
+  }();
+  return v;
+}
 
 template <int KIND, int P>
 static void launch_score_t(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
@@ -1151,6 +1379,30 @@ static void launch_score_mfma(PointsView src, const HypRec* hyps, int D, float c
                      (int)src.n, hyps, Dp, cthr, counts);
 }
 
+template <int TH>
+static void launch_score_bf16(PointsView src, const HypRec* hyps, int D, float cthr,
+                              int32_t* counts, int num_cus, hipStream_t s) {
+  constexpr int kGroup = 32 * TH;
+  const int Dp = (D + kGroup - 1) / kGroup * kGroup;  // hyps[D..Dp): bad planes (count nothing)
+  if (Dp > kMaxHypPerLaunch) return;
+  uint4* bcol = reinterpret_cast<uint4*>(reinterpret_cast<float*>(
+      reinterpret_cast<float4*>(const_cast<HypRec*>(hyps) + kMaxHypPerLaunch) + kMaxHypPerLaunch) +
+      kMaxHypPerLaunch);
+  float* band = reinterpret_cast<float*>(bcol + 4 * kMaxHypPerLaunch);
+  hipLaunchKernelGGL(k_prep_bf16, dim3((Dp + 255) / 256), dim3(256), 0, s, hyps, D, Dp, bcol, band);
+  const int ngroups = Dp / kGroup;
+  // ~8 resident waves per SIMD; partitions a multiple of 32 points
+  const int64_t want_waves = (int64_t)num_cus * 4 * 8;
+  int64_t nparts = std::max<int64_t>(1, (want_waves + ngroups - 1) / ngroups);
+  int64_t part = (src.n + nparts - 1) / nparts;
+  part = std::max<int64_t>(32, (part + 31) / 32 * 32);
+  nparts = (src.n + part - 1) / part;
+  const int64_t waves = nparts * ngroups;
+  const unsigned grid = (unsigned)((waves + (kBfBS / kWave) - 1) / (kBfBS / kWave));
+  hipLaunchKernelGGL((k_score_bf16<TH>), dim3(grid), dim3(kBfBS), 0, s, src.x, src.y, src.z,
+                     (int)src.n, hyps, bcol, band, D, ngroups, (int)part, cthr, counts);
+}
+
 template <int KIND>
 static void launch_score_h(PointsView src, const HypRec* hyps, int D, float cthr,
                            int32_t* counts, int num_cus, hipStream_t s) {
@@ -1188,6 +1440,8 @@ void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t
                   int variant, int num_cus, hipStream_t s) {
   if (D <= 0 || src.n <= 0) return;
   switch (variant) {
+    case kScoreBf16T4: launch_score_bf16<4>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreBf16T8: launch_score_bf16<8>(src, hyps, D, cthr, counts, num_cus, s); break;
     case kScoreLdsExact: launch_score_hl<kExact>(src, hyps, D, cthr, counts, num_cus, s); break;
     case kScoreLdsMin3: launch_score_hl<kMin3>(src, hyps, D, cthr, counts, num_cus, s); break;
     case kScoreLanesExact: launch_score_h<kExact>(src, hyps, D, cthr, counts, num_cus, s); break;

@@ -75,14 +75,23 @@ enum ScoreVariant {
   kScoreLanesExact = 14, kScoreLanesMin3 = 15,
   // lanes = hypotheses, points staged in LDS, broadcast-read and moved to SGPRs
   kScoreLdsExact = 16, kScoreLdsMin3 = 17,
-  kScoreNumVariants = 18
+  // plane distances on the bf16 matrix cores (3-way split operands, products exact), counting +
+  // band tracking on the VALU (~2.25 ops / test), exact PCL recheck inside the rounding band;
+  // T = 32-plane tiles held per wave
+  kScoreBf16T4 = 18, kScoreBf16T8 = 19,
+  kScoreNumVariants = 20
 };
 // hyps buffer layout for launch_score: HypRec[kMaxHypPerLaunch] followed by the packed float4
 // plane vectors and float band widths (score_scratch_bytes); counts need room for D rounded up
 // to a multiple of 64.
+// For the bf16 variants the tail also holds each plane's B column (32 bf16 = 4 x uint4) and its
+// band (float2).
 constexpr size_t kHypScratchBytes =
-    kMaxHypPerLaunch * (sizeof(HypRec) + sizeof(float4) + sizeof(float));
+    kMaxHypPerLaunch * (sizeof(HypRec) + sizeof(float4) + sizeof(float) + 4 * sizeof(uint4) +
+                        sizeof(float2));
 extern int kScoreDefault;
+// kScoreDefault unless DLG_SCORE_VARIANT names another variant (A/B of the full pipeline)
+int score_variant();
 
 void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
                            hipStream_t s);

@@ -31,7 +31,10 @@ def load(path, counter):
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE") if len(sys.argv) > 2 else {}
-    bench = json.loads(open(sys.argv[3]).read()) if len(sys.argv) > 3 else None
+    bench = None
+    if len(sys.argv) > 3:  # the bench JSON line (possibly inside a log with other output)
+        lines = [ln for ln in open(sys.argv[3]).read().splitlines() if ln.startswith("{")]
+        bench = json.loads(lines[-1])
     res = {}
     for k, rows in fetch.items():
         vals = [v for _, v, _ in rows]
@@ -49,8 +52,10 @@ def main():
             cal = (12.0 * n) / (1024 * sc[0][1])
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, bench.py --steps 1 --warmup 0",
            "kernels": res, "read_calibration_dword_loads": cal}
-    if "k_score" in res and cal:
-        out["hbm_bytes_per_launch"] = res["k_score"]["fetch_bytes_mean"] * cal + res["k_score"].get("write_bytes_mean", 0.0)
+    key = "k_score_bf16" if "k_score_bf16" in res else "k_score"
+    if key in res and cal:
+        out["kernel"] = key
+        out["hbm_bytes_per_launch"] = res[key]["fetch_bytes_mean"] * cal + res[key].get("write_bytes_mean", 0.0)
     json.dump(out, open(os.path.join(ROOT, "profiles", "score_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
