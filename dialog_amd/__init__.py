@@ -6,6 +6,7 @@ PCL's SACSegmentation interface, the synthetic-cloud generator and PCD I/O.  The
 fallback: without the library or a gfx950 device every compute call raises.
 """
 from .sac import (SAC_RANSAC, SACMODEL_NORMAL_PLANE, SACMODEL_PLANE, Cloud, Context,  # noqa: F401
+                  RansacControl,
                   DialogError, SACSegmentation, SACSegmentationFromNormals, extract_planes,
                   make_params, segment_cloud)
 from .normals import (NormalEstimation, estimate_normals, orient_normals_nn,  # noqa: F401
@@ -20,4 +21,4 @@ __all__ = ["Context", "Cloud", "SACSegmentation", "extract_planes", "segment_clo
            "DLG_REFIT_FAST", "DialogError", "LIB_PATH", "NormalEstimation", "estimate_normals",
            "regulate_normals", "SACSegmentationFromNormals", "orient_normals_nn",
            "preprocess", "remove_redundant_points", "PostProcessParams", "post_process_planes",
-           "refit_planes", "cluster_filter"]
+           "refit_planes", "cluster_filter", "RansacControl"]

@@ -25,7 +25,9 @@ SYMBOLS = [
     "dlg_set_profiling", "dlg_synchronize", "dlg_allreduce_max_f64", "dlg_barrier",
     "dlg_score_benchmark", "dlg_estimate_normals", "dlg_regulate_normals",
     "dlg_cloud_set_normals", "dlg_orient_normals_nn", "dlg_preprocess", "dlg_refit_planes",
-    "dlg_post_process_planes", "dlg_cluster_filter",
+    "dlg_post_process_planes", "dlg_cluster_filter", "dlg_sac_control_create",
+    "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
+    "dlg_sac_control_result",
 ]
 
 
@@ -123,6 +125,12 @@ def load():
     L.dlg_regulate_normals.argtypes = [vp, C.POINTER(Points), fp, C.c_int64, C.c_int64, C.c_int,
                                        C.c_float, C.POINTER(C.c_uint8), i64p]
     L.dlg_refit_planes.argtypes = [C.POINTER(Planes), fp]
+    L.dlg_sac_control_create.argtypes = [pp, C.POINTER(SacParams), C.c_int64, C.c_int]
+    L.dlg_sac_control_destroy.argtypes = [vp]
+    L.dlg_sac_control_next.argtypes = [vp, i32p, C.c_int64, C.POINTER(C.c_int)]
+    L.dlg_sac_control_consume.argtypes = [vp, i32p, i32p, C.c_int, C.POINTER(C.c_int),
+                                          C.POINTER(C.c_int)]
+    L.dlg_sac_control_result.argtypes = [vp, C.POINTER(SacStats), i64p]
     L.dlg_post_process_planes.argtypes = [vp, C.POINTER(Points), C.POINTER(Planes),
                                           C.POINTER(PostProcessParams), fp, i64p, i32p, C.c_int64,
                                           i32p, C.c_int64, i64p]

@@ -38,84 +38,9 @@
 #include "driver.hpp"
 #include "host_math.hpp"
 #include "kernels.hpp"
+#include "sac_control.hpp"
 
 namespace dlg {
-
-// sparse overlay of SampleConsensusModel::shuffled_indices_ over list positions: pos -> pos'
-class Overlay {
- public:
-  void reset(size_t expect) {
-    size_t cap = 64;
-    while (cap < expect * 2) cap <<= 1;
-    keys_.assign(cap, -1);
-    vals_.assign(cap, 0);
-    mask_ = cap - 1;
-    size_ = 0;
-  }
-  int32_t get(int32_t k) const {
-    size_t h = hash(k) & mask_;
-    while (keys_[h] != -1) {
-      if (keys_[h] == k) return vals_[h];
-      h = (h + 1) & mask_;
-    }
-    return k;
-  }
-  void set(int32_t k, int32_t v) {
-    if ((size_ + 1) * 2 > keys_.size()) grow();
-    size_t h = hash(k) & mask_;
-    while (keys_[h] != -1 && keys_[h] != k) h = (h + 1) & mask_;
-    if (keys_[h] == -1) {
-      keys_[h] = k;
-      ++size_;
-    }
-    vals_[h] = v;
-  }
-  void swap_pos(int32_t i, int32_t j) {
-    if (i == j) return;
-    int32_t vi = get(i), vj = get(j);
-    set(i, vj);
-    set(j, vi);
-  }
-
- private:
-  static size_t hash(int32_t k) { return (size_t)((uint32_t)k * 2654435761u); }
-  void grow() {
-    std::vector<int32_t> ok = std::move(keys_), ov = std::move(vals_);
-    keys_.assign(ok.size() * 2, -1);
-    vals_.assign(ok.size() * 2, 0);
-    mask_ = keys_.size() - 1;
-    size_ = 0;
-    for (size_t t = 0; t < ok.size(); ++t)
-      if (ok[t] != -1) set(ok[t], ov[t]);
-  }
-  std::vector<int32_t> keys_, vals_;
-  size_t mask_ = 0, size_ = 0;
-};
-
-// drawIndexSample's three swaps swap(shuf[i], shuf[i + rnd() % (N - i)]), i = 0, 1, 2, replayed
-// over list positions: positions 0..2 (touched by every draw) live in registers, the random
-// partners >= 3 in the sparse overlay -- one hash lookup and one insert per swap
-class ShuffleReplay {
- public:
-  void reset(size_t expect) {
-    head_[0] = 0; head_[1] = 1; head_[2] = 2;
-    tail_.reset(expect);
-  }
-  void swap(int i, int64_t j) {
-    if (j < 3) {
-      std::swap(head_[i], head_[j]);
-      return;
-    }
-    const int32_t vj = tail_.get((int32_t)j);
-    tail_.set((int32_t)j, head_[i]);
-    head_[i] = vj;
-  }
-  int32_t at(int i) const { return head_[i]; }
-
- private:
-  int32_t head_[3] = {0, 1, 2};
-  Overlay tail_;
-};
 
 }  // namespace dlg
 
@@ -242,18 +167,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   mt.normal_plane = np ? 1 : 0;
   mt.thr = prm.threshold;
   mt.lambda = prm.normal_distance_weight;
-  Mt19937 rng(prm.seed);
-  ShuffleReplay ov;
-  ov.reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h) + 16);
-
-  // RandomSampleConsensus::computeModel state
-  int iterations = 0;
-  int best = -INT_MAX;
-  double k = 1.0;
-  const double log_probability = std::log(1.0 - prm.probability);
-  const double one_over_indices = 1.0 / (double)N;
-  int consec_bad = 0;
-  bool done = false, have = false;
+  RansacControl ctl(prm, N, cap_h);
   // device slots: winning HypRec (its first float4 is the plane), its 3 samples, refined plane
   c->small.ensure(8);
   HypRec* best_dev = reinterpret_cast<HypRec*>(c->small.p);
@@ -262,29 +176,13 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   const float4* bc_dev = c->small.p;
   int launches = 0;
 
-  while (!done) {
-    // batch size: the hypotheses PCL can still evaluate (+ a little slack for bad draws)
-    // (first batch: k is still 1.0 -- size it by the iteration cap; PCL's k is only known once
-    // the first hypothesis has been counted)
-    int64_t remaining = (int64_t)prm.max_iterations + 1 - iterations;
-    if (have && std::isfinite(k) && k < 1e18)
-      remaining = std::min<int64_t>(remaining, (int64_t)std::ceil(k) - iterations);
-    remaining = std::max<int64_t>(remaining, 1);
-    const int D = (int)std::min<int64_t>(cap_h, remaining + (iterations ? 8 : 0));
-
+  while (!ctl.done()) {
+    const int D = ctl.next_size();
     // ---- host: drawIndexSample over positions
     const double t_draw0 = trace_on() ? now_ms() : 0.0;
     c->h_pos.ensure(3 * (size_t)D);
     int32_t* hp = c->h_pos.p;
-    for (int d = 0; d < D; ++d) {
-      for (int i = 0; i < 3; ++i) {
-        int64_t j = i + (int64_t)((uint64_t)(uint32_t)rng.rnd() % (uint64_t)(N - i));
-        ov.swap(i, j);
-      }
-      hp[3 * d] = ov.at(0);
-      hp[3 * d + 1] = ov.at(1);
-      hp[3 * d + 2] = ov.at(2);
-    }
+    ctl.next_batch(hp);
     const double t_draw1 = trace_on() ? now_ms() : 0.0;
     // ---- device: gather, build, score
     c->pos.ensure(3 * (size_t)D);
@@ -319,32 +217,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (c->profiling) st->score_ms += event_ms(c, 0, 1);
 
     // ---- host: computeModel replay over the batch
-    const int32_t* cnt = c->h_res.p;
-    const int32_t* good = c->h_res.p + Dp;
-    int best_d = -1;
-    for (int d = 0; d < D && !done; ++d) {
-      st->draws++;
-      if (!good[d]) {
-        if (++consec_bad >= 1000) done = true;  // getSamples: no valid sample in 1000 tries
-        continue;
-      }
-      consec_bad = 0;
-      const int n = cnt[d];
-      if (n > best) {
-        best = n;
-        best_d = d;
-        have = true;
-        const double w = (double)best * one_over_indices;
-        double p_no_outliers = 1.0 - std::pow(w, 3.0);
-        p_no_outliers = std::max(std::numeric_limits<double>::epsilon(), p_no_outliers);
-        p_no_outliers = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no_outliers);
-        k = log_probability / std::log(p_no_outliers);
-      }
-      ++iterations;
-      st->tests += N;
-      if (iterations > prm.max_iterations) done = true;
-      else if (!(iterations < k)) done = true;
-    }
+    const int best_d = ctl.consume(c->h_res.p, c->h_res.p + Dp, D);
     if (best_d >= 0) {  // keep the winner on the device (the next batch overwrites hyps)
       HIPCHK(hipMemcpyAsync(best_dev, c->hyps.p + best_d, sizeof(HypRec), hipMemcpyDeviceToDevice,
                             c->stream));
@@ -352,6 +225,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                             hipMemcpyDeviceToDevice, c->stream));
     }
   }
+  const int iterations = ctl.iterations();
+  const bool have = ctl.have_model();
+  const int best = ctl.best_count();
+  st->draws = ctl.draws();
+  st->tests = ctl.tests();
   st->iterations = iterations;
   st->launches = launches;
   if (xs) {

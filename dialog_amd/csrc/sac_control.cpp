@@ -1,0 +1,165 @@
+// sac_control.cpp -- RansacControl (sac_control.hpp) and its C ABI (dlg_sac_control_*).
+// Restates RandomSampleConsensus<PointT>::computeModel and SampleConsensusModel::getSamples /
+// drawIndexSample of PCL 1.8 [PCL-1.8 ext; SURVEY.md §8(a) a6, a7]; reference call site
+// Dialog/SimplifyVerticesSize.cpp:62-67.
+#include "sac_control.hpp"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <limits>
+#include <new>
+
+namespace dlg {
+
+void Overlay::reset(size_t expect) {
+  size_t cap = 64;
+  while (cap < expect * 2) cap <<= 1;
+  keys_.assign(cap, -1);
+  vals_.assign(cap, 0);
+  mask_ = cap - 1;
+  size_ = 0;
+}
+
+void Overlay::grow() {
+  std::vector<int32_t> ok = std::move(keys_), ov = std::move(vals_);
+  keys_.assign(ok.size() * 2, -1);
+  vals_.assign(ok.size() * 2, 0);
+  mask_ = keys_.size() - 1;
+  size_ = 0;
+  for (size_t t = 0; t < ok.size(); ++t)
+    if (ok[t] != -1) set(ok[t], ov[t]);
+}
+
+RansacControl::RansacControl(const dlg_sac_params& prm, int64_t N, int cap_h)
+    : prm_(prm), N_(N), cap_h_(std::max(cap_h, 1)), rng_(prm.seed) {
+  log_probability_ = std::log(1.0 - prm.probability);
+  one_over_indices_ = 1.0 / (double)N;
+  // getSamples cannot select 3 unique points -> computeModel fails without an iteration
+  if (N < 3) done_ = true;
+  ov_.reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h_) + 16);
+}
+
+int RansacControl::next_size() const {
+  if (done_) return 0;
+  // the hypotheses PCL can still evaluate (+ a little slack for bad draws); before the first
+  // count k is still 1.0, so the first batch is sized by the iteration cap
+  int64_t remaining = (int64_t)prm_.max_iterations + 1 - iterations_;
+  if (have_ && std::isfinite(k_) && k_ < 1e18)
+    remaining = std::min<int64_t>(remaining, (int64_t)std::ceil(k_) - iterations_);
+  remaining = std::max<int64_t>(remaining, 1);
+  return (int)std::min<int64_t>(cap_h_, remaining + (iterations_ ? 8 : 0));
+}
+
+int RansacControl::next_batch(int32_t* pos) {
+  const int D = next_size();
+  for (int d = 0; d < D; ++d) {
+    for (int i = 0; i < 3; ++i) {
+      const int64_t j = i + (int64_t)((uint64_t)(uint32_t)rng_.rnd() % (uint64_t)(N_ - i));
+      ov_.swap(i, j);
+    }
+    pos[3 * d] = ov_.at(0);
+    pos[3 * d + 1] = ov_.at(1);
+    pos[3 * d + 2] = ov_.at(2);
+  }
+  batch_base_ = drawn_;
+  drawn_ += D;
+  pending_ = D;
+  return D;
+}
+
+int RansacControl::consume(const int32_t* cnt, const int32_t* good, int D) {
+  D = std::min(D, pending_);
+  pending_ = 0;
+  int best_d = -1;
+  for (int d = 0; d < D && !done_; ++d) {
+    ++draws_;
+    if (!good[d]) {
+      if (++consec_bad_ >= 1000) done_ = true;  // getSamples: no valid sample in 1000 tries
+      continue;
+    }
+    consec_bad_ = 0;
+    const int n = cnt[d];
+    if (n > best_) {
+      best_ = n;
+      best_d = d;
+      best_draw_ = batch_base_ + d;
+      have_ = true;
+      const double w = (double)best_ * one_over_indices_;
+      double p_no_outliers = 1.0 - std::pow(w, 3.0);
+      p_no_outliers = std::max(std::numeric_limits<double>::epsilon(), p_no_outliers);
+      p_no_outliers = std::min(1.0 - std::numeric_limits<double>::epsilon(), p_no_outliers);
+      k_ = log_probability_ / std::log(p_no_outliers);
+    }
+    ++iterations_;
+    tests_ += N_;
+    if (iterations_ > prm_.max_iterations) done_ = true;
+    else if (!(iterations_ < k_)) done_ = true;
+  }
+  return best_d;
+}
+
+}  // namespace dlg
+
+// ---- C ABI ------------------------------------------------------------------------------------
+
+struct dlg_sac_control {
+  dlg::RansacControl ctl;
+  dlg_sac_control(const dlg_sac_params& p, int64_t n, int cap) : ctl(p, n, cap) {}
+};
+
+extern "C" {
+
+dlg_status dlg_sac_control_create(dlg_sac_control** out, const dlg_sac_params* prm,
+                                  int64_t n_active_global, int max_batch) {
+  if (!out || !prm || n_active_global < 0 || n_active_global > INT32_MAX || max_batch < 0)
+    return DLG_ERR_INVALID;
+  *out = nullptr;
+  if (!(prm->probability == prm->probability)) return DLG_ERR_INVALID;
+  dlg_sac_control* c = new (std::nothrow) dlg_sac_control(*prm, n_active_global,
+                                                          max_batch > 0 ? max_batch : 4096);
+  if (!c) return DLG_ERR_INTERNAL;
+  *out = c;
+  return DLG_OK;
+}
+
+dlg_status dlg_sac_control_destroy(dlg_sac_control* c) {
+  delete c;
+  return DLG_OK;
+}
+
+dlg_status dlg_sac_control_next(dlg_sac_control* c, int32_t* positions_out, int64_t cap,
+                                int* n_draws) {
+  if (!c || !n_draws) return DLG_ERR_INVALID;
+  const int D = c->ctl.next_size();
+  *n_draws = D;
+  if (3 * (int64_t)D > cap) return DLG_ERR_CAPACITY;
+  if (D > 0 && !positions_out) return DLG_ERR_INVALID;
+  c->ctl.next_batch(positions_out);
+  return DLG_OK;
+}
+
+dlg_status dlg_sac_control_consume(dlg_sac_control* c, const int32_t* counts, const int32_t* good,
+                                   int n_draws, int* best_in_batch, int* finished) {
+  if (!c || (n_draws > 0 && (!counts || !good)) || n_draws < 0) return DLG_ERR_INVALID;
+  const int b = c->ctl.consume(counts, good, n_draws);
+  if (best_in_batch) *best_in_batch = b;
+  if (finished) *finished = c->ctl.done() ? 1 : 0;
+  return DLG_OK;
+}
+
+dlg_status dlg_sac_control_result(const dlg_sac_control* c, dlg_sac_stats* st,
+                                  int64_t* best_draw) {
+  if (!c || !st) return DLG_ERR_INVALID;
+  *st = dlg_sac_stats{};
+  st->iterations = c->ctl.iterations();
+  st->has_model = c->ctl.have_model() ? 1 : 0;
+  st->draws = c->ctl.draws();
+  st->n_unrefined = c->ctl.have_model() ? c->ctl.best_count() : 0;
+  st->tests = c->ctl.tests();
+  st->n_active = c->ctl.n();
+  if (best_draw) *best_draw = c->ctl.best_draw();
+  return DLG_OK;
+}
+
+}  // extern "C"

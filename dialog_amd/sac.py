@@ -240,6 +240,64 @@ def extract_planes(cloud: Cloud, params, max_planes=20, min_inliers=0, capacity=
                 inliers=inl[:offs[k]].copy(), n_planes=k, stats=stats)
 
 
+class RansacControl:
+    """The host half of RandomSampleConsensus::computeModel (dlg_sac_control_*; no device).
+
+    next() -> int32 [D, 3] global list positions of the next batch of draws (PCL's RNG and
+    drawIndexSample swaps); consume(counts, good) replays computeModel over the batch and returns
+    (batch index of a new best or -1, finished).  This is the replay dlg_sac_segment runs around
+    its scoring kernel; point-sharded ranks each run one on the global N and summed counts.
+    """
+
+    def __init__(self, params, n_active_global: int, max_batch: int = 0):
+        self._L = _lib.load()
+        h = C.c_void_p()
+        _lib.check(self._L.dlg_sac_control_create(C.byref(h), C.byref(params),
+                                                  int(n_active_global), int(max_batch)))
+        self.h = h
+        self.n = int(n_active_global)
+
+    def next(self) -> np.ndarray:
+        d = C.c_int()
+        st = self._L.dlg_sac_control_next(self.h, None, 0, C.byref(d))
+        if d.value == 0:
+            return np.zeros((0, 3), np.int32)
+        if st != _lib.DLG_ERR_CAPACITY:
+            _lib.check(st)
+        pos = np.empty(3 * d.value, np.int32)
+        _lib.check(self._L.dlg_sac_control_next(self.h, _i32p(pos), pos.size, C.byref(d)))
+        return pos.reshape(-1, 3)
+
+    def consume(self, counts, good):
+        c = np.ascontiguousarray(counts, np.int32)
+        g = np.ascontiguousarray(good, np.int32)
+        if c.shape != g.shape:
+            raise ValueError("counts and good differ in length")
+        b, f = C.c_int(), C.c_int()
+        _lib.check(self._L.dlg_sac_control_consume(self.h, _i32p(c), _i32p(g), c.shape[0],
+                                                   C.byref(b), C.byref(f)))
+        return b.value, bool(f.value)
+
+    def result(self):
+        st = _lib.SacStats()
+        bd = C.c_int64()
+        _lib.check(self._L.dlg_sac_control_result(self.h, C.byref(st), C.byref(bd)))
+        r = _stats_dict(st)
+        r["best_draw"] = bd.value
+        return r
+
+    def close(self):
+        if self.h:
+            self._L.dlg_sac_control_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 _default_ctx = threading.local()
 
 

@@ -262,6 +262,36 @@ dlg_status dlg_cluster_filter(dlg_ctx* ctx, const dlg_points* pts, float radius,
                               int32_t t_cluster_num, int32_t* kept_ids, int64_t cap,
                               int64_t* n_kept);
 
+/* ---- host-side RANSAC control (no device) ----------------------------------------------------
+ * The sequential half of RandomSampleConsensus::computeModel [PCL-1.8 ext] that dlg_sac_segment
+ * runs on the host, exported on its own so that a caller with another scorer -- and the
+ * multi-rank CPU tests -- drive exactly the replay the GPU path uses:
+ *   dlg_sac_control_next    <- SampleConsensusModel::getSamples/drawIndexSample (the RNG and the
+ *                              swaps on the persistent shuffled index copy) for the next batch:
+ *                              3 list positions per draw into the N_active-long global list;
+ *   dlg_sac_control_consume <- computeModel's loop over the batch's (isSampleGood, count) pairs:
+ *                              1000 bad draws in a row end it, strict '>' keeps the first best,
+ *                              k = log(1-p)/log(1-w^3), the max_iterations break.
+ * A batch must be consumed before the next one is drawn.  Point-sharded ranks each run one
+ * controller on the global N and the summed counts and so take identical decisions. */
+typedef struct dlg_sac_control dlg_sac_control;
+dlg_status dlg_sac_control_create(dlg_sac_control** out, const dlg_sac_params* prm,
+                                  int64_t n_active_global, int max_batch /* 0 = 4096 */);
+dlg_status dlg_sac_control_destroy(dlg_sac_control* ctl);
+/* *n_draws = size of the next batch (0 once the loop has ended); DLG_ERR_CAPACITY if
+ * cap < 3 * *n_draws (nothing is drawn) */
+dlg_status dlg_sac_control_next(dlg_sac_control* ctl, int32_t* positions_out, int64_t cap,
+                                int* n_draws);
+/* counts/good of the batch just drawn, in draw order; *best_in_batch = draw index of a new best
+ * (-1: unchanged), *finished = 1 once computeModel's loop has ended */
+dlg_status dlg_sac_control_consume(dlg_sac_control* ctl, const int32_t* counts,
+                                   const int32_t* good, int n_draws, int* best_in_batch,
+                                   int* finished);
+/* iterations, draws, has_model, n_unrefined (best count), n_active, tests; best_draw = global
+ * draw index (over all batches) of the winning hypothesis, -1 without a model */
+dlg_status dlg_sac_control_result(const dlg_sac_control* ctl, dlg_sac_stats* st,
+                                  int64_t* best_draw);
+
 /* ---- profiling ------------------------------------------------------------------------------ */
 /* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);

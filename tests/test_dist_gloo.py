@@ -1,0 +1,92 @@
+"""N > 1 on the CPU: the point-sharded RANSAC protocol over torch.distributed
+`gloo` with world_size 2 and 3, driven by the product's host controller (dlg_sac_control_*, the
+replay dlg_sac_segment runs between its kernels) -- see tests/dist_protocol.py.  Sharded extract-
+and-remove must reproduce the single-process PCL restatement bit for bit, and every rank must
+take the same decisions.  The GPU-side counterpart (same protocol through the library's own
+collectives, loopback ranks on one device) is tests/test_gpu_parity.py::test_sharded_*.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+from oracle import oracle as O  # noqa: E402
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _entry(rank, world, port, out_dir, kw):
+    import dist_protocol
+    dist_protocol.run(rank, world, port, out_dir, **kw)
+
+
+@pytest.mark.parametrize("world,sizes", [(2, None), (3, [1500, 4000, 500])],
+                         ids=["ws2-even", "ws3-ragged"])
+def test_sharded_extract_gloo(tmp_path, world, sizes):
+    n = 6000
+    if sizes is None:
+        sizes = [n // world] * world
+        sizes[-1] += n - sum(sizes)
+    kw = dict(n_points=n, n_planes=3, threshold=0.02, max_planes=4, min_inliers=50,
+              max_iterations=120, probability=0.99, batch=64, sizes=sizes)
+    mp.start_processes(_entry, args=(world, _port(), str(tmp_path), kw), nprocs=world,
+                       join=True, start_method="spawn")
+    outs = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    for o in outs[1:]:   # identical decisions and results on every rank
+        for k in ("coeffs", "inliers", "offsets", "decisions"):
+            assert np.array_equal(o[k], outs[0][k]), k
+    from dialog_amd.synth import plane_cloud
+    pts, _, _ = plane_cloud(n, 3, seed=913)
+    ref = O.extract_planes(pts, 0.02, max_planes=4, min_inliers=50, max_iterations=120,
+                           probability=0.99)
+    got = outs[0]
+    assert ref["n_planes"] >= 3 and got["coeffs"].shape[0] == ref["n_planes"]
+    assert np.array_equal(got["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
+    assert np.array_equal(got["offsets"], ref["offsets"])
+    assert np.array_equal(got["inliers"], ref["inliers"])
+
+
+def test_control_matches_oracle_single_rank():
+    """dlg_sac_control_* alone (no ranks): iterations, draws, best sample of PCL's loop."""
+    import dialog_amd as D
+    from dialog_amd.synth import plane_cloud
+    pts, _, _ = plane_cloud(4000, 3, seed=77)
+    for mi, p, batch in [(200, 0.99, 64), (50, 0.99, 4096), (300, 1.0, 100), (5, 0.5, 1)]:
+        prm = D.make_params(0.02, max_iterations=mi, probability=p)
+        ctl = D.RansacControl(prm, pts.shape[0], batch)
+        best = None
+        while True:
+            pos = ctl.next()
+            if pos.shape[0] == 0:
+                break
+            good = np.zeros(len(pos), np.int32)
+            cnt = np.zeros(len(pos), np.int32)
+            for i, (a, b, c) in enumerate(pos):
+                ok, co = O.plane_coefficients(pts[a], pts[b], pts[c])
+                good[i] = ok
+                cnt[i] = O.count_within(pts, co, 0.02) if ok else 0
+            bi, fin = ctl.consume(cnt, good)
+            if bi >= 0:
+                best = pos[bi].copy()
+            if fin:
+                break
+        r = ctl.result()
+        ref = O.sac_segment(pts, 0.02, max_iterations=mi, probability=p)
+        assert (r["iterations"], r["draws"], r["n_unrefined"]) == \
+            (ref["iterations"], ref["draws"], ref["n_unrefined"])
+        assert list(best) == list(ref["best_sample"])
+    ctl = D.RansacControl(D.make_params(0.02), 2)   # < 3 points: no draw, no model
+    assert ctl.next().shape[0] == 0 and not ctl.result()["has_model"]
