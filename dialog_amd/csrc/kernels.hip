@@ -13,6 +13,7 @@
 //   SampleConsensusModelPlane::isSampleGood + computeModelCoefficients -> k_build_hyps
 //   computeMeanAndCovarianceMatrix (fast mode, double)  -> k_moments
 #include "kernels.hpp"
+#include "dev_common.hpp"
 #include "host_math.hpp"
 
 #include <algorithm>
@@ -23,27 +24,6 @@
 namespace dlg {
 
 namespace {
-
-constexpr int kWave = 64;
-
-__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-
-// v_writelane_b32: lane `sel` of v takes the wave-uniform value s (no VALU compare/select)
-__device__ __forceinline__ int writelane(int v, int s, int sel) {
-  asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(s), "{m0}"(sel));
-  return v;
-}
-
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// Eigen VectorXf(4).dot(Vector4f(x, y, z, 1)) under SSE: predux((c0x, c1y, c2z, c3*1)) =
-// (c0 x + c2 z) + (c1 y + c3).  No contraction (-ffp-contract=off).
-__device__ __forceinline__ float pcl_dot(float a, float b, float c, float d, float x, float y,
-                                         float z) {
-  return (a * x + c * z) + (b * y + d * 1.0f);
-}
 
 // Eigen Vector4f(v0, v1, v2, 0).normalized(): z = (v0^2 + v2^2) + (v1^2 + 0); z > 0 ? v / sqrt(z)
 __device__ __forceinline__ float4 eigen_normalized3(float v0, float v1, float v2, float w) {
@@ -483,29 +463,7 @@ __global__ __launch_bounds__(kScBS) void k_score_mfma(const float* __restrict__ 
 //
 // C/D layout (32x32x16): lane l holds column (plane) l & 31, rows (reg & 3) + 8 (reg >> 2) +
 // 4 (l >> 5); A/B: lane l holds row/col l & 31, k = 8 (l >> 5) + j of each 16-wide K half.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
 constexpr int kBfBS = 256;  // 4 independent waves
-constexpr uint32_t kBf16One = 0x3F80u;
-
-struct Split3 {
-  uint32_t p1, p2, p3;  // bf16 bit patterns
-};
-
-__device__ __forceinline__ Split3 split3(float v) {
-  const uint32_t u = __float_as_uint(v);
-  const float v1 = __uint_as_float(u & 0xFFFF0000u);
-  const float r1 = v - v1;  // exact (the low 16 significand bits)
-  const uint32_t u2 = __float_as_uint(r1) & 0xFFFF0000u;
-  const float r2 = r1 - __uint_as_float(u2);  // exact, <= 8 significant bits
-  return Split3{u >> 16, u2 >> 16, __float_as_uint(r2) >> 16};
-}
-
-__device__ __forceinline__ uint32_t pk(uint32_t lo, uint32_t hi) { return lo | (hi << 16); }
-
-__device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 
 // per plane: B column (4 x uint4 = k 0-7, 8-15, 16-23, 24-31) and band half-width w
 __global__ void k_prep_bf16(const HypRec* __restrict__ hyps, int D, int Dp,
@@ -534,20 +492,6 @@ __global__ void k_prep_bf16(const HypRec* __restrict__ hyps, int D, int Dp,
   }
   bcol[4 * h] = q0; bcol[4 * h + 1] = q1; bcol[4 * h + 2] = q2; bcol[4 * h + 3] = q3;
   band[h] = w;
-}
-
-// sign bytes of r0..r3 (0xFF if negative) -> acc += 255 * #negative
-__device__ __forceinline__ uint32_t count4(float r0, float r1, float r2, float r3, uint32_t acc) {
-  // v_perm_b32 selectors: 9 = sign(S1) x 8, 11 = sign(S0) x 8, 12 = 0x00
-  const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(r0), __float_as_uint(r1), 0x0C0C0B09u);
-  const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(r2), __float_as_uint(r3), 0x0B090C0Cu);
-  return __builtin_amdgcn_sad_u8(lo, hi, acc);
-}
-
-__device__ __forceinline__ float min3_abs(float m, float a, float b) {
-  float o;
-  asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(o) : "v"(m), "v"(a), "v"(b));
-  return o;
 }
 
 template <int TH>
