@@ -188,34 +188,44 @@ def main():
     per_rank_tests = scored / world
     avg_launch_ms = score_ms / max(launches, 1)
     ktests_per_s = per_rank_tests / (score_ms / 1e3) if score_ms > 0 else 0.0
-    achieved = 7.0 * ktests_per_s / 1e12
     variant = int(os.environ.get("DLG_SCORE_VARIANT", "19"))
-    kname = {19: "k_score_bf16<8> (countWithinDistance: plane distances on the bf16 matrix cores, "
-                 "exact 3-way split operands; VALU sign count + rounding-band re-decision in PCL "
-                 "op order; 4096 hypotheses/launch)",
-             5: "k_score<exact,4> (countWithinDistance in PCL op order on the VALU, 4096 "
-                "hypotheses/launch)"}.get(variant, f"score variant {variant}")
+    pruned = variant == 19 and os.environ.get("DLG_PRUNE", "") != "0" and a.points >= 131072
+    if pruned:
+        kname = ("k_score_pruned (countWithinDistance over the Morton-ordered copy: super-tile and "
+                 "tile bounding spheres rule out (tile, plane) pairs with no possible PCL inlier; "
+                 "the rest as k_score_bf16's 32x32 bf16 matrix-core blocks + exact band "
+                 "re-decision; 4096 hypotheses/launch)")
+    else:
+        kname = {19: "k_score_bf16<8> (countWithinDistance: plane distances on the bf16 matrix "
+                     "cores, exact 3-way split operands; VALU sign count + rounding-band "
+                     "re-decision in PCL op order; 4096 hypotheses/launch)",
+                 5: "k_score<exact,4> (countWithinDistance in PCL op order on the VALU, 4096 "
+                    "hypotheses/launch)"}.get(variant, f"score variant {variant}")
+    # SURVEY 8(d) algorithmic bytes of a scoring launch: the active points once (12 B each) +
+    # the hypotheses (32 B plane record + 4 B count); sum over launches / kernel time
+    alg_bytes = 12.0 * per_rank_tests / max(a.hyps, 1) + 36.0 * a.hyps * launches
+    achieved = alg_bytes / (score_ms / 1e3) / 1e9 if score_ms else 0.0
     roofline = {
         "kernel": kname,
-        "bound": "valu",
-        "achieved": round(achieved, 3),
-        "peak": round(VALU_PEAK_TOPS, 2),
-        "unit": "TFLOP/s",
-        "frac": round(achieved / VALU_PEAK_TOPS, 4),
+        "bound": "hbm",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": None,
         "avg_launch_ms": round(avg_launch_ms, 4),
         "launches": launches,
         "tests_per_s_in_kernel": ktests_per_s,
-        "ops_per_test": 7,
-        "hbm_view": {"algorithmic_GBps": round(12.0 * (per_rank_tests / max(a.hyps, 1)) /
-                                              (score_ms / 1e3) / 1e9, 2) if score_ms else None,
-                     "peak_GBps": HBM_PEAK_GBS},
-        "note": "achieved = SURVEY 8(d) algorithmic work, 7 f32 ops per test (3 mul + 3 add + 1 "
-                "cmp, PCL op order) x tests / kernel time; peak = f32 VALU, 256 CU x 4 SIMD x 32 "
-                "lanes x 2.4 GHz.  The default kernel runs the multiply-adds on the bf16 matrix "
-                "cores (2 v_mfma_f32_32x32x16_bf16 per 1024 tests, ~29% of the MFMA pipe) and "
-                "~3.2 VALU lane-ops per test (rocprofv3 SQ_INSTS_VALU), so frac near or above 1 "
-                "means the work left the VALU, not that the VALU is saturated",
+        "hbm_roofline_tests_per_s": HBM_PEAK_GBS * 1e9 / 12.0 * a.hyps,
+        "valu_view": {"ops_per_test": 7, "pcl_equivalent_TFLOPs": round(7.0 * ktests_per_s / 1e12, 2),
+                      "valu_peak_TFLOPs": round(VALU_PEAK_TOPS, 2)},
+        "note": "north-star definition: tests/s against the HBM roofline of streaming each "
+                "active point (12 B) once per 4096-hypothesis launch, i.e. achieved = algorithmic "
+                "bytes (12 B x active points + 36 B x hypotheses per launch) / kernel time vs "
+                "8 TB/s; frac = tests/s / hbm_roofline_tests_per_s.  Kernel time from HIP events "
+                "on the library's stream.  valu_view restates the same tests as PCL's 7 f32 ops "
+                "each (the pruned kernel evaluates only the (tile, plane) pairs its bounding "
+                "spheres cannot rule out, so this exceeds the VALU peak)",
     }
     traffic_file = os.path.join(ROOT, "profiles", "score_traffic.json")
     if os.path.exists(traffic_file):

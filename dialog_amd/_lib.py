@@ -27,7 +27,7 @@ SYMBOLS = [
     "dlg_cloud_set_normals", "dlg_orient_normals_nn", "dlg_preprocess", "dlg_refit_planes",
     "dlg_post_process_planes", "dlg_cluster_filter", "dlg_sac_control_create",
     "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
-    "dlg_sac_control_result",
+    "dlg_sac_control_result", "dlg_cloud_build_spatial",
 ]
 
 
@@ -102,6 +102,7 @@ def load():
     L.dlg_cloud_upload.argtypes = [vp, C.POINTER(Points), i32p, C.c_int64, C.c_int32, pp]
     L.dlg_cloud_destroy.argtypes = [vp]
     L.dlg_cloud_reset.argtypes = [vp]
+    L.dlg_cloud_build_spatial.argtypes = [vp, vp]
     L.dlg_cloud_active.argtypes = [vp, i64p]
     L.dlg_sac_segment.argtypes = [vp, vp, C.POINTER(SacParams), fp, i32p, C.c_int64, i64p,
                                   C.POINTER(SacStats)]

@@ -15,9 +15,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdialog_amd.so")
-SOURCES = ["kernels.hip", "normals.hip", "postprocess.hip", "comm.cpp", "driver.cpp", "sac_control.cpp",
+SOURCES = ["kernels.hip", "spatial.hip", "normals.hip", "postprocess.hip", "comm.cpp", "driver.cpp", "sac_control.cpp",
            "normals_host.cpp", "postprocess_host.cpp"]
-HEADERS = ["kernels.hpp", "dev_common.hpp", "sac_control.hpp", "normals.hpp", "comm.hpp", "driver.hpp", "host_math.hpp", "grid_host.hpp",
+HEADERS = ["kernels.hpp", "spatial.hpp", "dev_common.hpp", "sac_control.hpp", "normals.hpp", "comm.hpp", "driver.hpp", "host_math.hpp", "grid_host.hpp",
            "pp_math.hpp", "postprocess.hpp", "grid_dev.hpp"]
 ARCH = os.environ.get("DLG_OFFLOAD_ARCH", "gfx950")
 

@@ -39,6 +39,7 @@
 #include "host_math.hpp"
 #include "kernels.hpp"
 #include "sac_control.hpp"
+#include "spatial.hpp"
 
 namespace dlg {
 
@@ -135,7 +136,65 @@ struct SegOut {
   int64_t n_in_local = 0;   // refined inliers on this rank (ids in ctx->inl_gid)
   int64_t n_out_local = 0;  // survivors on this rank (compacted into the spare buffer if remove)
   int64_t n_in_global = 0;
+  bool sp_compacted = false;  // the spatial copy's survivors are in its spare buffer
+  int64_t sp_n_out = 0;
 };
+
+// pruned scoring (spatial.hpp): DLG_PRUNE=0 disables it, DLG_PRUNE=1 also builds the spatial
+// copy for small clouds (tests); by default clouds of >= kPruneMinPoints points get one
+constexpr int64_t kPruneMinPoints = 131072;
+int prune_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("DLG_PRUNE");
+    return e ? std::atoi(e) : -1;
+  }();
+  return m;
+}
+
+// Morton-ordered copy of the pristine cloud's finite points + its bounding spheres
+void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
+  const int64_t n = cl->n_total;
+  DevBuf<uint32_t> k0, k1;
+  DevBuf<int32_t> i0, i1;
+  DevBuf<uint8_t> tmp;
+  try {
+    k0.ensure(n); k1.ensure(n); i0.ensure(n); i1.ensure(n);
+    const size_t tb = morton_sort_temp_bytes(n);
+    tmp.ensure(std::max<size_t>(tb, 16));
+    c->totals.ensure(4);
+    HIPCHK(hipMemsetAsync(c->totals.p, 0, 4, c->stream));
+    launch_morton_keys(cl->pristine.view(n), cl->amax[0], cl->amax[1], cl->amax[2], k0.p, i0.p,
+                       c->totals.p, c->stream);
+    HIPCHK(morton_sort(tmp.p, tb, k0.p, k1.p, i0.p, i1.p, n, c->stream));
+    int32_t nonfinite = 0;
+    HIPCHK(hipMemcpyAsync(&nonfinite, c->totals.p, 4, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    const int64_t m = n - nonfinite;
+    cl->sp_pristine.ensure((size_t)std::max<int64_t>(m, 1));
+    launch_gather_order(cl->pristine.view(n), i1.p, m, cl->sp_pristine.out(), c->stream);
+    cl->sp_tiles_pr.ensure((size_t)std::max<int64_t>(sp_tiles(m), 1));
+    cl->sp_supers_pr.ensure((size_t)std::max<int64_t>(sp_supers(m), 1));
+    launch_sphere_bounds(cl->sp_pristine.x.p, cl->sp_pristine.y.p, cl->sp_pristine.z.p, m,
+                         cl->sp_tiles_pr.p, cl->sp_supers_pr.p, c->stream);
+    HIPCHK(hipGetLastError());
+    sync(c);
+    cl->sp_n_pristine = cl->sp_n = m;
+    cl->sp_built = cl->sp_valid = true;
+    cl->sp_cur = -1;
+    cl->sp_dirty = false;
+  } catch (...) {
+    k0.release(); k1.release(); i0.release(); i1.release(); tmp.release();
+    throw;
+  }
+  k0.release(); k1.release(); i0.release(); i1.release(); tmp.release();
+}
+
+SpatialView spatial_view(const dlg_cloud* cl) {
+  const SoA& s = cl->sp_soa();
+  const bool pr = cl->sp_cur < 0;
+  return SpatialView{s.x.p, s.y.p, s.z.p, cl->sp_n, pr ? cl->sp_tiles_pr.p : cl->sp_tiles.p,
+                     pr ? cl->sp_supers_pr.p : cl->sp_supers.p};
+}
 
 // one SACSegmentation::segment() over the cloud's active list (all ranks)
 SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool compact,
@@ -168,6 +227,20 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   mt.thr = prm.threshold;
   mt.lambda = prm.normal_distance_weight;
   RansacControl ctl(prm, N, cap_h);
+  // pruned scoring over the spatial copy (plane model, default kernel, spatial copy in step)
+  const bool pruned = !np && cl->sp_valid && score_variant() == kScoreDefault && prune_mode() != 0;
+  const float pmargin = pruned ? prune_margin(cthr, cl->amax) : 0.0f;
+  if (pruned) {
+    c->work.ensure(1);
+    if (cl->sp_dirty && cl->sp_n > 0) {
+      cl->sp_tiles.ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+      cl->sp_supers.ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+      const SoA& s = cl->sp_soa();
+      launch_sphere_bounds(s.x.p, s.y.p, s.z.p, cl->sp_n, cl->sp_tiles.p, cl->sp_supers.p,
+                           c->stream);
+    }
+    cl->sp_dirty = false;
+  }
   // device slots: winning HypRec (its first float4 is the plane), its 3 samples, refined plane
   c->small.ensure(8);
   HypRec* best_dev = reinterpret_cast<HypRec*>(c->small.p);
@@ -200,7 +273,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     if (np)
       launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
-    else
+    else if (pruned) {
+      const uint4* bcol = nullptr;
+      const float* band = nullptr;
+      launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
+      HIPCHK(hipMemsetAsync(c->work.p, 0, 4, c->stream));
+      launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr, pmargin, c->res.p,
+                          c->work.p, c->num_cus, c->stream);
+    } else
       launch_score(src, c->hyps.p, D, cthr, c->res.p, score_variant(), c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
@@ -252,8 +332,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   c->tile_in.ensure(nt + 1);
   c->tile_off_in.ensure(nt + 1);
   c->tile_off_out.ensure(nt + 1);
-  c->totals.ensure(2);
-  c->h_tot.ensure(2);
+  c->totals.ensure(4);
+  c->h_tot.ensure(4);
   c->h_small.ensure(8);
   c->inl_gid.ensure((size_t)std::max<int64_t>(src.n, 1));
   c->moments.ensure(kMomentK);
@@ -298,9 +378,21 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // final selectWithinDistance with the refined model (+ compaction of the survivors)
   launch_select(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
                 c->inl_gid.p, nullptr, compact ? &dst : nullptr, c->stream);
+  // the spatial copy loses the same points (same predicate, same float inputs)
+  const bool sp_compact = compact && !np && cl->sp_valid;
+  if (sp_compact) {
+    SoA& sd = cl->sp_buf[cl->sp_spare()];
+    sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
+    const PointsOut spo = sd.out();
+    const SoA& ss = cl->sp_soa();
+    const PointsView spv{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n, nullptr};
+    launch_select(spv, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
+                  c->totals.p + 2, nullptr, nullptr, &spo, c->stream);
+  }
   HIPCHK(hipGetLastError());
   if (c->profiling) HIPCHK(hipEventRecord(c->ev[3], c->stream));
-  HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, sp_compact ? 16 : 8, hipMemcpyDeviceToHost,
+                        c->stream));
   HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 6 * sizeof(float4), hipMemcpyDeviceToHost,
                         c->stream));
   sync(c);
@@ -315,6 +407,13 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   out.has_model = true;
   out.n_in_local = c->h_tot.p[0];
   out.n_out_local = src.n == 0 ? 0 : c->h_tot.p[1];
+  if (sp_compact) {
+    out.sp_compacted = true;
+    out.sp_n_out = cl->sp_n == 0 ? 0 : c->h_tot.p[3];
+    // non-finite points are never inliers: both copies must lose exactly the same points
+    if ((cl->sp_n == 0 ? 0 : c->h_tot.p[2]) != out.n_in_local)
+      throw DlgError(DLG_ERR_INTERNAL, "spatial copy out of step with the active list");
+  }
   if (trace_on())
     std::fprintf(stderr, "[dlg] refit+select=%.3fms n_in=%lld\n", now_ms() - t_ref0,
                  (long long)out.n_in_local);
@@ -572,9 +671,14 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     HIPCHK(hipMemcpyAsync(bits, c->totals.p, 12, hipMemcpyDeviceToHost, c->stream));
     sync(c);
     for (int k = 0; k < 3; ++k) std::memcpy(&cl->amax[k], &bits[k], 4);
+    if (prune_mode() != 0 && n >= 3 && (n >= kPruneMinPoints || prune_mode() == 1))
+      build_spatial(c, cl.get());
   });
   if (s != DLG_OK) {
     cl->pristine.release();
+    cl->sp_pristine.release();
+    cl->sp_tiles_pr.release();
+    cl->sp_supers_pr.release();
     return s;
   }
   *out = cl.release();
@@ -588,14 +692,34 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
   cl->pristine.release();
   cl->buf[0].release();
   cl->buf[1].release();
+  cl->sp_pristine.release();
+  cl->sp_buf[0].release();
+  cl->sp_buf[1].release();
+  cl->sp_tiles_pr.release();
+  cl->sp_supers_pr.release();
+  cl->sp_tiles.release();
+  cl->sp_supers.release();
   delete cl;
   return DLG_OK;
+}
+
+dlg_status dlg_cloud_build_spatial(dlg_ctx* c, dlg_cloud* cl) {
+  if (!c || !cl || cl->ctx != c) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    if (cl->n_total < 3 || cl->sp_built) return;
+    if (cl->cur >= 0) throw DlgError(DLG_ERR_INVALID, "build the spatial copy before extracting (or after dlg_cloud_reset)");
+    build_spatial(c, cl);
+  });
 }
 
 dlg_status dlg_cloud_reset(dlg_cloud* cl) {
   if (!cl) return DLG_ERR_INVALID;
   cl->cur = -1;
   cl->n_active = cl->n_total;
+  cl->sp_cur = -1;
+  cl->sp_n = cl->sp_n_pristine;
+  cl->sp_valid = cl->sp_built;
+  cl->sp_dirty = false;
   return DLG_OK;
 }
 
@@ -697,6 +821,13 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       *n_planes = p + 1;
       cl->cur = cl->spare();  // commit the removal
       cl->n_active = so.n_out_local;
+      if (so.sp_compacted) {
+        cl->sp_cur = cl->sp_spare();
+        cl->sp_n = so.sp_n_out;
+        cl->sp_dirty = true;
+      } else {
+        cl->sp_valid = false;  // (SACMODEL_NORMAL_PLANE rounds do not carry the spatial copy)
+      }
     }
     drain_pending(c);
   });
@@ -720,6 +851,15 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
     c->hyps.ensure(kHypScratchBytes / sizeof(HypRec) + 1);
     c->res.ensure(2 * (size_t)kMaxHypPerLaunch + 64);
     const float cthr = thr_ceil(threshold);
+    c->work.ensure(1);
+    if (variant == kScorePruned && cl->sp_valid && cl->sp_dirty && cl->sp_n > 0) {
+      cl->sp_tiles.ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+      cl->sp_supers.ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+      const SoA& s = cl->sp_soa();
+      launch_sphere_bounds(s.x.p, s.y.p, s.z.p, cl->sp_n, cl->sp_tiles.p, cl->sp_supers.p,
+                           c->stream);
+      cl->sp_dirty = false;
+    }
     HIPCHK(hipMemcpyAsync(c->pos.p, c->h_pos.p, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
     launch_gather_samples(c->pos.p, 3 * D, 0, src, c->samples.p, c->stream);
     const int Dp = (D + 63) / 64 * 64;
@@ -729,7 +869,18 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
     for (int r = 0; r < reps; ++r) {
       HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
-      launch_score(src, c->hyps.p, D, cthr, c->res.p, variant, c->num_cus, c->stream);
+      if (variant == kScorePruned) {
+        if (!cl->sp_valid) throw DlgError(DLG_ERR_INVALID, "cloud has no spatial copy");
+        const uint4* bcol = nullptr;
+        const float* band = nullptr;
+        launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
+        HIPCHK(hipMemsetAsync(c->work.p, 0, 4, c->stream));
+        launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr,
+                            prune_margin(cthr, cl->amax), c->res.p, c->work.p, c->num_cus,
+                            c->stream);
+      } else {
+        launch_score(src, c->hyps.p, D, cthr, c->res.p, variant, c->num_cus, c->stream);
+      }
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev[1], c->stream));
       sync(c);

@@ -168,6 +168,7 @@ struct dlg_ctx {
   PinBuf<double> h_mom;
   PinBuf<int64_t> h_g64;
   DevBuf<float4> small;    // winning plane + samples + refined plane (segment_impl)
+  DevBuf<uint32_t> work;   // work queue counter of the pruned scoring kernel
   PinBuf<float4> h_small;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<int32_t> h_inl;
@@ -193,6 +194,17 @@ struct dlg_cloud {
   int cur = -1;  // -1 pristine, 0 = A, 1 = B
   SoA pristine, buf[2];
   float amax[3] = {0, 0, 0};
+  // Morton-ordered copy of the finite active points for the pruned scoring kernel (spatial.hpp):
+  // built at upload (large clouds), compacted with the list in every SACMODEL_PLANE extract round
+  bool sp_built = false;   // the pristine spatial copy exists
+  bool sp_valid = false;   // the current spatial copy holds exactly the finite active points
+  bool sp_dirty = false;   // sphere bounds of the working copy need recomputing
+  int sp_cur = -1;         // -1 pristine, 0 / 1 ping-pong
+  int64_t sp_n_pristine = 0, sp_n = 0;
+  SoA sp_pristine, sp_buf[2];
+  DevBuf<float4> sp_tiles_pr, sp_supers_pr, sp_tiles, sp_supers;
+  const SoA& sp_soa() const { return sp_cur < 0 ? sp_pristine : sp_buf[sp_cur]; }
+  int sp_spare() const { return sp_cur == 0 ? 1 : 0; }
   PointsView view() const {
     const SoA& s = cur < 0 ? pristine : buf[cur];
     return s.view(n_active);

@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src,
     }
     if (in) {
       int p = run_in + wi + lanes_below(mi);
-      inl_gid[p] = g;
+      if (inl_gid) inl_gid[p] = g;
       if (inl_xyz) {
         inl_xyz[3 * (int64_t)p] = x; inl_xyz[3 * (int64_t)p + 1] = y; inl_xyz[3 * (int64_t)p + 2] = z;
       }
@@ -1261,7 +1261,7 @@ int score_variant() {
   static const int v = [] {
     const char* e = std::getenv("DLG_SCORE_VARIANT");
     const int x = e ? std::atoi(e) : -1;
-    return x >= 0 && x < kScoreNumVariants ? x : kScoreDefault;
+    return x >= 0 && x < kScorePruned ? x : kScoreDefault;
   }();
   return v;
 }
@@ -1345,6 +1345,18 @@ static void launch_score_bf16(PointsView src, const HypRec* hyps, int D, float c
   const unsigned grid = (unsigned)((waves + (kBfBS / kWave) - 1) / (kBfBS / kWave));
   hipLaunchKernelGGL((k_score_bf16<TH>), dim3(grid), dim3(kBfBS), 0, s, src.x, src.y, src.z,
                      (int)src.n, hyps, bcol, band, D, ngroups, (int)part, cthr, counts);
+}
+
+void launch_prep_bf16(const HypRec* hyps, int D, const uint4** bcol_out, const float** band_out,
+                      hipStream_t s) {
+  const int Dp = (D + 31) / 32 * 32;
+  uint4* bcol = reinterpret_cast<uint4*>(reinterpret_cast<float*>(
+      reinterpret_cast<float4*>(const_cast<HypRec*>(hyps) + kMaxHypPerLaunch) + kMaxHypPerLaunch) +
+      kMaxHypPerLaunch);
+  float* band = reinterpret_cast<float*>(bcol + 4 * kMaxHypPerLaunch);
+  if (D > 0) hipLaunchKernelGGL(k_prep_bf16, dim3((Dp + 255) / 256), dim3(256), 0, s, hyps, D, Dp, bcol, band);
+  *bcol_out = bcol;
+  *band_out = band;
 }
 
 template <int KIND>

@@ -79,7 +79,11 @@ enum ScoreVariant {
   // band tracking on the VALU (~2.25 ops / test), exact PCL recheck inside the rounding band;
   // T = 32-plane tiles held per wave
   kScoreBf16T4 = 18, kScoreBf16T8 = 19,
-  kScoreNumVariants = 20
+  // k_score_bf16's 32 x 32 blocks only for (tile, plane) pairs the bounding spheres cannot rule
+  // out, over the cloud's Morton-ordered copy (spatial.hpp; dlg_score_benchmark only -- the
+  // product takes it whenever the cloud has a spatial copy)
+  kScorePruned = 20,
+  kScoreNumVariants = 21
 };
 // hyps buffer layout for launch_score: HypRec[kMaxHypPerLaunch] followed by the packed float4
 // plane vectors and float band widths (score_scratch_bytes); counts need room for D rounded up
@@ -102,6 +106,10 @@ void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, fl
 // counts must be zeroed by the caller (memset on the same stream).
 void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
                   int variant, int num_cus, hipStream_t s);
+// B columns (bf16 split plane coefficients) and band widths of D plane hypotheses for the bf16
+// matrix-core scoring kernels, written into the hyps scratch tail; returns pointers to them
+void launch_prep_bf16(const HypRec* hyps, int D, const uint4** bcol, const float** band,
+                      hipStream_t s);
 // SampleConsensusModelNormalPlane::countWithinDistance for D hypotheses (src.nrm required);
 // counts need room for D rounded up to 64 and must be zeroed by the caller
 void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest& mt,

@@ -1,0 +1,66 @@
+// spatial.hpp -- spatially ordered copy of a cloud's active points and the pruned scoring kernel.
+//
+// countWithinDistance (SampleConsensusModelPlane, PCL 1.8 [SURVEY.md §8(a) a9]) only needs the
+// number of inliers per hypothesis, which does not depend on the order the points are visited.
+// The cloud's finite active points are therefore also kept in Morton order (10 bits per axis),
+// cut into tiles of 32 consecutive points and super-tiles of 32 tiles, each with a bounding
+// sphere.  A plane whose computed distance to a sphere's centre exceeds
+//     cthr + radius + 2 e_max          (e_max = 64 u S_max >= every rounding error involved)
+// cannot have a single PCL inlier in that sphere, so its tests there are decided without being
+// evaluated; every other (tile, plane) pair is scored exactly as k_score_bf16 scores it (bf16
+// matrix cores + exact re-decision inside the rounding band).  Counts stay bit-identical to the
+// exhaustive kernels.
+//
+// The list-ordered SoA of kernels.hpp stays the source of truth for sampling positions, select
+// and the inlier lists; the spatial copy is compacted with the same refined-plane predicate in
+// every extract round, so it always holds exactly the finite active points.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace dlg {
+
+constexpr int kTileP = 32;       // points per tile (the 32 rows of one MFMA block)
+constexpr int kSuperTiles = 32;  // tiles per super-tile
+constexpr int kSuperP = kTileP * kSuperTiles;
+
+inline int64_t sp_tiles(int64_t n) { return (n + kTileP - 1) / kTileP; }
+inline int64_t sp_supers(int64_t n) { return (n + kSuperP - 1) / kSuperP; }
+
+struct SpatialView {
+  const float* x;
+  const float* y;
+  const float* z;
+  int64_t n;
+  const float4* tiles;   // [sp_tiles(n)]  (cx, cy, cz, r): every point of the tile within r of c
+  const float4* supers;  // [sp_supers(n)]
+};
+
+// Morton keys over [-amax, amax] per axis; non-finite points get key 0xFFFFFFFF (sorted last)
+// and are counted into *n_nonfinite (never inliers of any plane: PCL's distance is NaN or inf)
+void launch_morton_keys(PointsView src, float ax, float ay, float az, uint32_t* keys,
+                        int32_t* idx, int32_t* n_nonfinite, hipStream_t s);
+size_t morton_sort_temp_bytes(int64_t n);
+hipError_t morton_sort(void* tmp, size_t tmp_bytes, uint32_t* keys_in, uint32_t* keys_out,
+                       int32_t* idx_in, int32_t* idx_out, int64_t n, hipStream_t s);
+// dst[i] = src[order[i]], i < n
+void launch_gather_order(PointsView src, const int32_t* order, int64_t n, PointsOut dst,
+                         hipStream_t s);
+// tile and super-tile bounding spheres of n points
+void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_t n,
+                          float4* tiles, float4* supers, hipStream_t s);
+// margin = smallest float >= (cthr + 2 e_max)(1 + 2^-19), e_max = 64 u 2.0001 (ax + ay + az)
+float prune_margin(float cthr, const float amax[3]);
+// pruned countWithinDistance of D plane hypotheses over the spatial points.  hyps / bcol / band
+// as prepared for k_score_bf16 (launch_prep_bf16); counts[D] zeroed by the caller; work = one
+// uint32 zeroed by the caller (super-tile queue).
+void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
+                         const float* band, int D, float cthr, float margin, int32_t* counts,
+                         uint32_t* work, int num_cus, hipStream_t s);
+
+}  // namespace dlg

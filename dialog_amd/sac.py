@@ -147,6 +147,10 @@ class Cloud:
         self.h = h
         _LIVE_CLOUDS.add(self)
 
+    def build_spatial(self):
+        """Morton-ordered copy for the pruned scoring kernel (automatic for >= 131072 points)."""
+        self.ctx.check(self.ctx._L.dlg_cloud_build_spatial(self.ctx.h, self.h))
+
     def reset(self):
         self.ctx.check(self.ctx._L.dlg_cloud_reset(self.h))
 

@@ -130,6 +130,11 @@ dlg_status dlg_cloud_upload(dlg_ctx* ctx, const dlg_points* pts, const int32_t* 
 dlg_status dlg_cloud_destroy(dlg_cloud* cloud);
 /* re-activate every point of the cloud (undo extract-and-remove) */
 dlg_status dlg_cloud_reset(dlg_cloud* cloud);
+/* Morton-ordered copy of the cloud's finite points + tile bounding spheres for the pruned
+ * scoring kernel (same counts, fewer evaluated tests).  Built by dlg_cloud_upload for clouds of
+ * >= 131072 points (environment DLG_PRUNE=0: never, =1: always); this forces it for any cloud
+ * (call right after upload or dlg_cloud_reset).  Kept in step by SACMODEL_PLANE extraction. */
+dlg_status dlg_cloud_build_spatial(dlg_ctx* ctx, dlg_cloud* cloud);
 dlg_status dlg_cloud_active(const dlg_cloud* cloud, int64_t* n_active_local);
 /* SACSegmentationFromNormals::setInputNormals: one normal record per uploaded point (n = the
  * dlg_points n of dlg_cloud_upload; the cloud's indices select from it like from the points).

@@ -12,7 +12,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-VARIANTS = (5, 18, 19)  # exact (PCL op order), bf16 x 4 tiles, bf16 x 8 tiles
+VARIANTS = (5, 18, 19, 20)  # exact (PCL op order), bf16 x 4 / x 8 tiles, pruned (spatial copy)
 
 
 def counts(ctx, cloud, D, v, thr):
@@ -50,6 +50,7 @@ def test_score_variants_bit_identical(gpu_ctx, case):
     import dialog_amd as D
     p, thr = make(case)
     cloud = D.Cloud(gpu_ctx, p)
+    cloud.build_spatial()
     try:
         for nh in (1, 100, 257, 4096):
             ref = counts(gpu_ctx, cloud, nh, VARIANTS[0], thr)
