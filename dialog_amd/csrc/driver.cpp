@@ -231,7 +231,6 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   const bool pruned = !np && cl->sp_valid && score_variant() == kScoreDefault && prune_mode() != 0;
   const float pmargin = pruned ? prune_margin(cthr, cl->amax) : 0.0f;
   if (pruned) {
-    c->work.ensure(1);
     if (cl->sp_dirty && cl->sp_n > 0) {
       cl->sp_tiles.ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
       cl->sp_supers.ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
@@ -277,9 +276,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       const uint4* bcol = nullptr;
       const float* band = nullptr;
       launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
-      HIPCHK(hipMemsetAsync(c->work.p, 0, 4, c->stream));
+      c->lp.ensure((size_t)sp_supers(cl->sp_n) * D + 1);
+      c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
       launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr, pmargin, c->res.p,
-                          c->work.p, c->num_cus, c->stream);
+                          c->lp.p, c->lp_n.p, c->num_cus, c->stream);
     } else
       launch_score(src, c->hyps.p, D, cthr, c->res.p, score_variant(), c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
@@ -851,7 +851,6 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
     c->hyps.ensure(kHypScratchBytes / sizeof(HypRec) + 1);
     c->res.ensure(2 * (size_t)kMaxHypPerLaunch + 64);
     const float cthr = thr_ceil(threshold);
-    c->work.ensure(1);
     if (variant == kScorePruned && cl->sp_valid && cl->sp_dirty && cl->sp_n > 0) {
       cl->sp_tiles.ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
       cl->sp_supers.ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
@@ -874,10 +873,28 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
         const uint4* bcol = nullptr;
         const float* band = nullptr;
         launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
-        HIPCHK(hipMemsetAsync(c->work.p, 0, 4, c->stream));
+        c->lp.ensure((size_t)sp_supers(cl->sp_n) * D + 1);
+        c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
+        static const bool want_stats = std::getenv("DLG_PRUNE_STATS") != nullptr;
+        unsigned long long* stp = nullptr;
+        if (want_stats) {
+          c->gath64.ensure(8);
+          stp = reinterpret_cast<unsigned long long*>(c->gath64.p);
+          HIPCHK(hipMemsetAsync(stp, 0, 48, c->stream));
+        }
         launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr,
-                            prune_margin(cthr, cl->amax), c->res.p, c->work.p, c->num_cus,
-                            c->stream);
+                            prune_margin(cthr, cl->amax), c->res.p, c->lp.p, c->lp_n.p,
+                            c->num_cus, c->stream, stp);
+        if (want_stats) {
+          unsigned long long h[6];
+          HIPCHK(hipMemcpyAsync(h, stp, 48, hipMemcpyDeviceToHost, c->stream));
+          sync(c);
+          std::fprintf(stderr, "[prune] n=%lld D=%d mean_nlp=%.1f tiles=%llu "
+                       "groups=%llu pairs=%llu (%.4f of tile x plane) fill=%.3f recheck=%.4f\n",
+                       (long long)cl->sp_n, D, h[2] ? (double)h[1] / h[2] : 0.0, h[2], h[3],
+                       h[4], h[2] ? (double)h[4] / ((double)h[2] * D) : 0.0,
+                       h[3] ? (double)h[4] / (32.0 * h[3]) : 0.0, h[3] ? (double)h[5] / h[3] : 0.0);
+        }
       } else {
         launch_score(src, c->hyps.p, D, cthr, c->res.p, variant, c->num_cus, c->stream);
       }

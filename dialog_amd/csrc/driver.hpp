@@ -168,7 +168,8 @@ struct dlg_ctx {
   PinBuf<double> h_mom;
   PinBuf<int64_t> h_g64;
   DevBuf<float4> small;    // winning plane + samples + refined plane (segment_impl)
-  DevBuf<uint32_t> work;   // work queue counter of the pruned scoring kernel
+  DevBuf<uint16_t> lp;     // pruned scoring: per super-tile lists of near planes
+  DevBuf<int32_t> lp_n;
   PinBuf<float4> h_small;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<int32_t> h_inl;

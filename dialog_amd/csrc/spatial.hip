@@ -125,40 +125,83 @@ __global__ __launch_bounds__(kSbBS) void k_sphere_bounds(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_score_pruned: one 16-wave workgroup per CU (persistent), all D planes (a, b, c, d) in LDS.
-// Super-tiles are taken from a global queue.  Per super-tile:
-//   1. every plane is tested against the super sphere (FMA chain, 1 plane per thread per step);
-//      planes that may hold an inlier go to the LDS list Lp;
-//   2. the waves take the super-tile's tiles from an LDS queue; per tile the planes of Lp are
-//      tested against the tile sphere (64 per step, lanes = planes) and the near ones appended to
-//      the wave's ring; every 32 queued planes (and the remainder at the end of Lp) are scored
-//      against the tile's 32 points exactly as k_score_bf16 scores a 32 x 32 block: two
-//      v_mfma_f32_32x32x16_bf16 on the split operands, sign-byte count, min |r| band check and
-//      PCL-order re-decision of the band elements;
-//   3. per-plane counts accumulate in LDS and go to HBM once per workgroup.
-// A (tile, plane) pair is skipped only when fl(|h|) > (margin + r)(1 + 2^-20) (rounded
-// evaluation), i.e. the exact distance of the plane to the sphere centre exceeds
-// cthr + r + 2 e_max: no point of the sphere can then pass PCL's test (spatial.hpp).
+// Pruned countWithinDistance in two launches:
+//   k_prune_supers : every plane against every super-tile sphere (planes in LDS, 1024 threads =
+//                    4 planes per thread per super-tile); the planes that may hold an inlier go
+//                    to the super-tile's list lp[s * D ...], their number to lp_n[s];
+//   k_score_tiles  : waves walk the tiles independently (blocks of 4 consecutive tiles dealt
+//                    round-robin over all waves: no workgroup barrier inside the loop); per tile
+//                    the planes of its super-tile's list are tested against the tile sphere (64
+//                    per step, lanes = planes), the near ones appended to the wave's ring, and
+//                    every 32 queued planes (and the remainder) scored against the tile's 32
+//                    points as one 32 x 32 bf16 matrix-core block with exact band re-decision;
+//                    per-plane counts in LDS, flushed once per workgroup.
+// A (sphere, plane) pair is ruled out only when fl(|h|) > (margin + r)(1 + 2^-20), i.e. the
+// exact distance of the plane to the sphere centre exceeds cthr + r + 2 e_max: no point of the
+// sphere can then pass PCL's test (spatial.hpp).
+//
+// Block scoring relative to the tile centre c: A rows hold the split of p - c (|p - c| <= r),
+// the B column's d slots the split of h = n.c + d (double, rounded once to float).  The matrix
+// cores then add small terms, so |D - pcl_dot| is dominated by PCL's own rounding (4.1 u S)
+// and the re-decision band is ~15x narrower than k_score_bf16's 64 u S.
 constexpr int kPrBS = 1024;
 constexpr int kPrWaves = kPrBS / kWave;
 constexpr int kPrRing = 128;
+constexpr int kPrChunk = 4;  // consecutive tiles per work item of k_score_tiles
 
 __device__ __forceinline__ float prune_lim(float margin, float r) {
   return (margin + r) * (1.0f + 0x1p-20f);
 }
 
-__global__ __launch_bounds__(kPrBS) void k_score_pruned(
+__global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict__ supers,
+                                                        int nsup, const HypRec* __restrict__ hyps,
+                                                        int D, float margin,
+                                                        uint16_t* __restrict__ lp,
+                                                        int32_t* __restrict__ lp_n) {
+  __shared__ float4 s_cf[kMaxHypPerLaunch];
+  __shared__ int s_nlp;
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int j = threadIdx.x; j < D; j += kPrBS) {
+    const HypRec h = hyps[j];
+    s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
+  }
+  for (int sidx = blockIdx.x; sidx < nsup; sidx += gridDim.x) {
+    if (threadIdx.x == 0) s_nlp = 0;
+    __syncthreads();
+    const float4 sp = supers[sidx];
+    const float slim = prune_lim(margin, sp.w);
+    uint16_t* out = lp + (int64_t)sidx * D;
+    for (int b = 0; b < D; b += kPrBS) {  // block-uniform trip count
+      const int j = b + threadIdx.x;
+      bool near = false;
+      if (j < D) {
+        const float4 cf = s_cf[j];
+        const float h = __builtin_fmaf(cf.x, sp.x, __builtin_fmaf(cf.y, sp.y, __builtin_fmaf(cf.z, sp.z, cf.w)));
+        near = fabsf(h) <= slim;  // NaN planes: never near (PCL counts nothing for them)
+      }
+      const uint64_t m = ballot(near);
+      if (m) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_nlp, (int)__popcll(m));
+        base = __shfl(base, 0);
+        if (near) out[base + lanes_below(m)] = (uint16_t)j;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) lp_n[sidx] = s_nlp;
+  }
+}
+
+__global__ __launch_bounds__(kPrBS) void k_score_tiles(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    int n, const float4* __restrict__ tiles, const float4* __restrict__ supers,
-    const HypRec* __restrict__ hyps, const uint4* __restrict__ bcol,
-    const float* __restrict__ band, int D, float cthr, float margin,
-    int32_t* __restrict__ counts, uint32_t* __restrict__ work) {
+    int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp,
+    const int32_t* __restrict__ lp_n, const HypRec* __restrict__ hyps,
+    const uint4* __restrict__ bcol, const float* __restrict__ band, int D, float cthr,
+    float margin, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ int32_t s_cnt[kMaxHypPerLaunch];
-  __shared__ uint16_t s_lp[kMaxHypPerLaunch];
   __shared__ uint16_t s_ring[kPrWaves][kPrRing];
-  __shared__ float4 s_tile[kSuperTiles];
-  __shared__ int s_nlp, s_super, s_next;
+  __shared__ unsigned long long s_st[6];
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int r32 = lane & 31, hh = lane >> 5;
   for (int j = threadIdx.x; j < D; j += kPrBS) {
@@ -166,62 +209,58 @@ __global__ __launch_bounds__(kPrBS) void k_score_pruned(
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
     s_cnt[j] = 0;
   }
-  const int nsup = (n + kSuperP - 1) / kSuperP;
+  if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
+  __syncthreads();
   const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (;;) {
-    if (threadIdx.x == 0) {
-      s_super = (int)atomicAdd(work, 1u);
-      s_nlp = 0;
-      s_next = 0;
-    }
-    __syncthreads();
-    const int sidx = s_super;
-    if (sidx >= nsup) break;
-    const int ntile = min(kSuperTiles, (n - sidx * kSuperP + kTileP - 1) / kTileP);
-    if (threadIdx.x < ntile) s_tile[threadIdx.x] = tiles[(int64_t)sidx * kSuperTiles + threadIdx.x];
-    {
-      const float4 sp = supers[sidx];
-      const float slim = prune_lim(margin, sp.w);
-      for (int b = 0; b < D; b += kPrBS) {  // block-uniform trip count
-        const int j = b + threadIdx.x;
-        bool near = false;
-        if (j < D) {
-          const float4 cf = s_cf[j];
-          const float h = __builtin_fmaf(cf.x, sp.x, __builtin_fmaf(cf.y, sp.y, __builtin_fmaf(cf.z, sp.z, cf.w)));
-          near = fabsf(h) <= slim;  // NaN planes: never near (PCL counts nothing for them)
-        }
-        const uint64_t m = ballot(near);
-        if (m) {
-          int base = 0;
-          if (lane == 0) base = atomicAdd(&s_nlp, (int)__popcll(m));
-          base = __shfl(base, 0);
-          if (near) s_lp[base + lanes_below(m)] = (uint16_t)j;
-        }
-      }
-    }
-    __syncthreads();
-    const int nlp = s_nlp;
-    for (;;) {
-      int tl = 0;
-      if (lane == 0) tl = atomicAdd(&s_next, 1);
-      tl = __shfl(tl, 0);
-      if (tl >= ntile) break;
-      const float4 tb = s_tile[tl];
+  const int ntiles = (n + kTileP - 1) / kTileP;
+  const int nitems = (ntiles + kPrChunk - 1) / kPrChunk;
+  const int gw = blockIdx.x * kPrWaves + wv, nw = gridDim.x * kPrWaves;
+  for (int it = gw; it < nitems; it += nw) {
+    const int t_end = min(ntiles, (it + 1) * kPrChunk);
+    for (int t = it * kPrChunk; t < t_end; ++t) {
+      const int sidx = t / kSuperTiles;
+      const int nlp = lp_n[sidx];
+      const uint16_t* lps = lp + (int64_t)sidx * D;
+      const float4 tb = tiles[t];
       const float tlim = prune_lim(margin, tb.w);
-      const int64_t p0 = ((int64_t)sidx * kSuperTiles + tl) * kTileP;
-      bool have_a = false;
-      bool bad = false;
+      const int64_t p0 = (int64_t)t * kTileP;
+      if (stats && lane == 0) { atomicAdd(&s_st[2], 1ull); atomicAdd(&s_st[1], (unsigned long long)nlp); }
+      // the tile's points (A operand, relative to the tile centre) -- loaded up front
+      const bool valid = p0 + r32 < n;
       float x = 0.f, y = 0.f, z = 0.f;
+      if (valid) { x = X[p0 + r32]; y = Y[p0 + r32]; z = Z[p0 + r32]; }
+      bool a_ready = false, bad = false;
       u32x4 a1 = {0u, 0u, 0u, 0u}, a2 = {0u, 0u, 0u, 0u};
       int nq = 0, head = 0;
-      // score the ring entries [head, head + m) (m <= 32) against this tile
-      auto group = [&](int m) {
-        if (!have_a) {
-          have_a = true;
-          const bool valid = p0 + r32 < n;
-          if (valid) { x = X[p0 + r32]; y = Y[p0 + r32]; z = Z[p0 + r32]; }
+      // pending group: its loads are issued when it fills and it is scored at the next event,
+      // so the B-column / LDS latency overlaps the tile tests in between
+      bool pend = false;
+      int pj = 0;
+      bool pcol = false;
+      uint4 pq = make_uint4(0u, 0u, 0u, 0u), pq2 = pq;
+      float pband = 0.0f;
+      float4 pcf = make_float4(0.f, 0.f, 0.f, 0.f);
+      auto issue = [&](int m) {
+        pcol = r32 < m;
+        pj = pcol ? (int)s_ring[wv][(head + r32) & (kPrRing - 1)] : 0;
+        pcf = s_cf[pj];
+        if (pcol) {
+          pq = bcol[4 * pj + hh];
+          pq2 = bcol[4 * pj + 2 + hh];
+          pband = band[pj];
+        }
+        pend = true;
+        if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
+      };
+      auto compute = [&]() {
+        pend = false;
+        if (!a_ready) {
+          a_ready = true;
           bad = ballot(!valid || !(isfinite(x) && isfinite(y) && isfinite(z))) != 0;
-          const Split3 sx = split3(x), sy = split3(y), sz = split3(z);
+          // coordinates relative to the tile centre (|p - c| <= r)
+          const float dx = valid ? x - tb.x : 0.f, dy = valid ? y - tb.y : 0.f;
+          const float dz = valid ? z - tb.z : 0.f;
+          const Split3 sx = split3(dx), sy = split3(dy), sz = split3(dz);
           if (hh == 0) {
             a1 = u32x4{pk(sx.p1, sx.p1), pk(sx.p2, sx.p1), pk(sx.p3, sx.p2), pk(sy.p1, sy.p1)};
             a2 = u32x4{pk(sz.p3, sz.p2), pk(kBf16One, kBf16One), pk(kBf16One, 0u), 0u};
@@ -230,15 +269,29 @@ __global__ __launch_bounds__(kPrBS) void k_score_pruned(
             a2 = u32x4{0u, 0u, 0u, 0u};
           }
         }
-        const bool col = r32 < m;
-        const int j = col ? (int)s_ring[wv][(head + r32) & (kPrRing - 1)] : 0;
+        const int j = pj;
+        const bool col = pcol;
+        const float4 cf = pcf;
         u32x4 b1 = {0u, 0u, 0u, 0u}, b2 = {0u, 0u, 0u, 0u};
         float w = 0.0f;
         if (col) {
-          const uint4 q = bcol[4 * j + hh], q2 = bcol[4 * j + 2 + hh];
-          b1 = u32x4{q.x, q.y, q.z, q.w};
-          b2 = u32x4{q2.x, q2.y, q2.z, q2.w};
-          w = band[j];
+          b1 = u32x4{pq.x, pq.y, pq.z, pq.w};
+          b2 = u32x4{pq2.x, pq2.y, pq2.z, pq2.w};
+          // the plane's offset from the tile centre h = n.c + d: double (products exact), rounded
+          // once to float and split exactly into the d slots of the B column (k 18..20)
+          const double hd = __builtin_fma((double)cf.x, (double)tb.x,
+                                          __builtin_fma((double)cf.y, (double)tb.y,
+                                                        __builtin_fma((double)cf.z, (double)tb.z, (double)cf.w)));
+          const float hf = (float)hd;
+          if (hh == 0) {
+            const Split3 sh = split3(hf);
+            b2.y = pk(sh.p1, sh.p2);
+            b2.z = pk(sh.p3, 0u);
+          }
+          // |D - pcl_dot| <= 4.1 u S (PCL's rounding; band[j] >= 15.8 x that, k_prep_bf16)
+          //                + 44 u (|n|_1 r + |h|) (centring, dropped products, <= 20 roundings
+          //                  even if truncated) -- the constants carry >= 2 % slack
+          w = __builtin_fmaf(0.065f, pband, 3.0e-6f * __builtin_fmaf(1.8f, tb.w, fabsf(hf))) + 1e-9f;
         } else if (hh == 0) {
           b2 = u32x4{0u, pk(0x4000u, 0u), 0u, 0u};  // not a plane: D = 2, never counted
         }
@@ -256,7 +309,7 @@ __global__ __launch_bounds__(kPrBS) void k_score_pruned(
         }
         const bool need = bad || mn <= w;
         if (ballot(need)) {  // rare: re-decide the band elements in PCL op order
-          const float4 cf = s_cf[j];
+          if (stats && lane == 0) atomicAdd(&s_st[5], 1ull);
 #pragma unroll 1
           for (int i = 0; i < 16; ++i) {
             const float ri = fabsf(Dv[i]) - cthr;
@@ -274,12 +327,13 @@ __global__ __launch_bounds__(kPrBS) void k_score_pruned(
         c += __shfl_xor(c, 32);
         if (hh == 0 && col && c) atomicAdd(&s_cnt[j], (int32_t)c);
       };
+      int jn = lane < nlp ? (int)lps[lane] : 0;  // the list is read one chunk ahead
       for (int c0 = 0; c0 < nlp; c0 += kWave) {
         const int k = c0 + lane;
+        const int j = jn;
+        jn = k + kWave < nlp ? (int)lps[k + kWave] : 0;
         bool near = false;
-        int j = 0;
         if (k < nlp) {
-          j = s_lp[k];
           const float4 cf = s_cf[j];
           const float h = __builtin_fmaf(cf.x, tb.x, __builtin_fmaf(cf.y, tb.y, __builtin_fmaf(cf.z, tb.z, cf.w)));
           near = fabsf(h) <= tlim;
@@ -289,19 +343,24 @@ __global__ __launch_bounds__(kPrBS) void k_score_pruned(
         nq += (int)__popcll(m);
         __builtin_amdgcn_wave_barrier();
         while (nq - head >= 32) {
-          group(32);
+          if (pend) compute();
+          issue(32);
           head += 32;
         }
       }
-      if (nq > head) group(nq - head);
+      if (pend) compute();
+      if (nq > head) {
+        issue(nq - head);
+        compute();
+      }
     }
-    __syncthreads();  // the queue / lists of this super-tile are reset at the top
   }
   __syncthreads();
   for (int j = threadIdx.x; j < D; j += kPrBS) {
     const int c = s_cnt[j];
     if (c) atomicAdd(&counts[j], c);
   }
+  if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
 }
 
 }  // namespace
@@ -353,12 +412,16 @@ float prune_margin(float cthr, const float amax[3]) {
 
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
                          const float* band, int D, float cthr, float margin, int32_t* counts,
-                         uint32_t* work, int num_cus, hipStream_t s) {
+                         uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
+                         unsigned long long* stats) {
   if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) return;
   const int64_t ns = sp_supers(v.n);
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(num_cus, ns));
-  hipLaunchKernelGGL(k_score_pruned, dim3(grid), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
-                     v.tiles, v.supers, hyps, bcol, band, D, cthr, margin, counts, work);
+  const unsigned ga = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2 * num_cus, ns));
+  hipLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, v.supers, (int)ns, hyps, D,
+                     margin, lp, lp_n);
+  const int64_t items = (sp_tiles(v.n) + kPrChunk - 1) / kPrChunk;
+  const unsigned gb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(num_cus, (items + kPrWaves - 1) / kPrWaves));
+  hipLaunchKernelGGL(k_score_tiles, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
+                     v.tiles, lp, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
 }
-
 }  // namespace dlg

@@ -57,10 +57,11 @@ void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_
 // margin = smallest float >= (cthr + 2 e_max)(1 + 2^-19), e_max = 64 u 2.0001 (ax + ay + az)
 float prune_margin(float cthr, const float amax[3]);
 // pruned countWithinDistance of D plane hypotheses over the spatial points.  hyps / bcol / band
-// as prepared for k_score_bf16 (launch_prep_bf16); counts[D] zeroed by the caller; work = one
-// uint32 zeroed by the caller (super-tile queue).
+// as prepared for k_score_bf16 (launch_prep_bf16); counts[D] zeroed by the caller; lp / lp_n:
+// scratch of sp_supers(n) * D uint16 and sp_supers(n) int32 (per super-tile plane lists).
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
                          const float* band, int D, float cthr, float margin, int32_t* counts,
-                         uint32_t* work, int num_cus, hipStream_t s);
+                         uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
+                         unsigned long long* stats = nullptr);  // [6] counters (A/B tool)
 
 }  // namespace dlg

@@ -16,7 +16,7 @@ from dialog_amd.synth import SEED_BASE, plane_cloud  # noqa: E402
 NAMES = {0: "exact_p8", 1: "band_p8", 2: "min3_p8", 3: "exact_p16", 4: "min3_p16", 5: "exact_p4",
          6: "min3_p4", 7: "exactS_p8g8", 8: "min3S_p8g8", 9: "exactS_p4g8", 10: "exactS_p8g4",
          11: "mfma_pa32", 12: "mfma_pa16", 13: "mfma_pa8", 14: "lanes_exact", 15: "lanes_min3",
-         16: "lds_exact", 17: "lds_min3", 18: "bf16_t4", 19: "bf16_t8"}
+         16: "lds_exact", 17: "lds_min3", 18: "bf16_t4", 19: "bf16_t8", 20: "pruned"}
 
 
 def main():
