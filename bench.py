@@ -154,10 +154,13 @@ def main():
                         refit_mode=D.DLG_REFIT_FAST if a.refit == "fast" else D.DLG_REFIT_PCL,
                         hypotheses_per_launch=a.hyps, gather_inliers=False)
 
+    # the caller's inlier-id buffer, kept across steps (a C++ caller's std::vector)
+    inl_buf = np.empty(a.points * world if prm.gather_inliers else a.points, np.int32)
+
     def step():
         cloud.reset()
         return D.extract_planes(cloud, prm, max_planes=a.planes, min_inliers=a.min_inliers,
-                                capacity=a.points)
+                                out=inl_buf)
 
     for _ in range(a.warmup):
         step()

@@ -44,16 +44,45 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", *CXXFLAGS, "-shared",
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp", "-ldl", "-lpthread"]
+def _compile(src: str, obj: str, verbose: bool) -> None:
+    cmd = [hipcc(), f"--offload-arch={ARCH}", *CXXFLAGS, "-c", src, "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+        raise RuntimeError(f"hipcc failed on {os.path.basename(src)} ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(obj + ".tmp", obj)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile each translation unit in parallel (objects under dialog_amd/build/), then link."""
+    if not force and not _stale():
+        return LIB
+    from concurrent.futures import ThreadPoolExecutor
+    odir = os.path.join(HERE, "build")
+    os.makedirs(odir, exist_ok=True)
+    hdr_t = max(os.path.getmtime(d) for d in
+                [os.path.join(CSRC, h) for h in HEADERS] +
+                [os.path.join(HERE, "..", "include", "dialog_ransac.h"), os.path.abspath(__file__)]
+                if os.path.exists(d))
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        obj = os.path.join(odir, src + ".o")
+        objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(hdr_t, os.path.getmtime(sp)):
+            jobs.append((sp, obj))
+    workers = max(1, min(len(jobs), os.cpu_count() or 1, 16))
+    with ThreadPoolExecutor(workers) as ex:
+        for f in [ex.submit(_compile, sp, obj, verbose) for sp, obj in jobs]:
+            f.result()
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", LIB + ".tmp", "-ldl", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed ({r.returncode}):\n{r.stderr[-4000:]}")
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

@@ -174,7 +174,7 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
     launch_gather_order(cl->pristine.view(n), i1.p, m, cl->sp_pristine.out(), c->stream);
     cl->sp_tiles_pr.ensure((size_t)std::max<int64_t>(sp_tiles(m), 1));
     cl->sp_supers_pr.ensure((size_t)std::max<int64_t>(sp_supers(m), 1));
-    launch_sphere_bounds(cl->sp_pristine.x.p, cl->sp_pristine.y.p, cl->sp_pristine.z.p, m,
+    launch_sphere_bounds(cl->sp_pristine.x.p, cl->sp_pristine.y.p, cl->sp_pristine.z.p, m, nullptr,
                          cl->sp_tiles_pr.p, cl->sp_supers_pr.p, c->stream);
     HIPCHK(hipGetLastError());
     sync(c);
@@ -192,8 +192,21 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
 SpatialView spatial_view(const dlg_cloud* cl) {
   const SoA& s = cl->sp_soa();
   const bool pr = cl->sp_cur < 0;
-  return SpatialView{s.x.p, s.y.p, s.z.p, cl->sp_n, pr ? cl->sp_tiles_pr.p : cl->sp_tiles.p,
-                     pr ? cl->sp_supers_pr.p : cl->sp_supers.p};
+  return SpatialView{s.x.p, s.y.p, s.z.p, cl->sp_n, pr ? cl->sp_tiles_pr.p : cl->sp_tb[cl->sp_cur].p,
+                     pr ? cl->sp_supers_pr.p : cl->sp_sb[cl->sp_cur].p};
+}
+
+// (re)compute the sphere bounds of the working spatial copy when they are stale
+void ensure_sphere_bounds(dlg_ctx* c, dlg_cloud* cl) {
+  if (cl->sp_dirty && cl->sp_cur >= 0 && cl->sp_n > 0) {
+    const int b = cl->sp_cur;
+    cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+    cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+    const SoA& s = cl->sp_soa();
+    launch_sphere_bounds(s.x.p, s.y.p, s.z.p, cl->sp_n, nullptr, cl->sp_tb[b].p, cl->sp_sb[b].p,
+                         c->stream);
+  }
+  cl->sp_dirty = false;
 }
 
 // one SACSegmentation::segment() over the cloud's active list (all ranks)
@@ -230,16 +243,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // pruned scoring over the spatial copy (plane model, default kernel, spatial copy in step)
   const bool pruned = !np && cl->sp_valid && score_variant() == kScoreDefault && prune_mode() != 0;
   const float pmargin = pruned ? prune_margin(cthr, cl->amax) : 0.0f;
-  if (pruned) {
-    if (cl->sp_dirty && cl->sp_n > 0) {
-      cl->sp_tiles.ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
-      cl->sp_supers.ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
-      const SoA& s = cl->sp_soa();
-      launch_sphere_bounds(s.x.p, s.y.p, s.z.p, cl->sp_n, cl->sp_tiles.p, cl->sp_supers.p,
-                           c->stream);
-    }
-    cl->sp_dirty = false;
-  }
+  if (pruned) ensure_sphere_bounds(c, cl);
   // device slots: winning HypRec (its first float4 is the plane), its 3 samples, refined plane
   c->small.ensure(8);
   HypRec* best_dev = reinterpret_cast<HypRec*>(c->small.p);
@@ -276,10 +280,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       const uint4* bcol = nullptr;
       const float* band = nullptr;
       launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
-      c->lp.ensure((size_t)sp_supers(cl->sp_n) * D + 1);
+      c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
-      launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr, pmargin, c->res.p,
-                          c->lp.p, c->lp_n.p, c->num_cus, c->stream);
+      launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr, pmargin, cl->amax,
+                          c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream);
     } else
       launch_score(src, c->hyps.p, D, cthr, c->res.p, score_variant(), c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
@@ -395,7 +399,22 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                         c->stream));
   HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 6 * sizeof(float4), hipMemcpyDeviceToHost,
                         c->stream));
-  sync(c);
+  if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(c->ev_tot, c->stream));
+  if (sp_compact) {
+    // sphere bounds of the survivors, queued behind the totals copy: they run while the host
+    // reads the totals and draws the next round.  Into the spare buffer's own bound arrays
+    // (sized for the current count, an upper bound; the kernel reads the survivor count from
+    // totals[3]), so a round whose plane is rejected leaves the current bounds intact.
+    const int b = cl->sp_spare();
+    cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+    cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+    const SoA& sd = cl->sp_buf[b];
+    launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 3, cl->sp_tb[b].p,
+                         cl->sp_sb[b].p, c->stream);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventSynchronize(c->ev_tot));
   if (c->profiling && xs) xs->select_ms += event_ms(c, 2, 3);
   const HypRec* bh = reinterpret_cast<const HypRec*>(c->h_small.p);
   const SampleRec* bs = reinterpret_cast<const SampleRec*>(c->h_small.p + 2);
@@ -595,6 +614,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->nw.release();
   c->pw.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
+  if (c->ev_tot) (void)hipEventDestroy(c->ev_tot);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -697,8 +717,10 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
   cl->sp_buf[1].release();
   cl->sp_tiles_pr.release();
   cl->sp_supers_pr.release();
-  cl->sp_tiles.release();
-  cl->sp_supers.release();
+  for (int b = 0; b < 2; ++b) {
+    cl->sp_tb[b].release();
+    cl->sp_sb[b].release();
+  }
   delete cl;
   return DLG_OK;
 }
@@ -824,7 +846,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       if (so.sp_compacted) {
         cl->sp_cur = cl->sp_spare();
         cl->sp_n = so.sp_n_out;
-        cl->sp_dirty = true;
+        cl->sp_dirty = false;  // bounds queued by segment_impl behind the compaction
       } else {
         cl->sp_valid = false;  // (SACMODEL_NORMAL_PLANE rounds do not carry the spatial copy)
       }
@@ -851,14 +873,7 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
     c->hyps.ensure(kHypScratchBytes / sizeof(HypRec) + 1);
     c->res.ensure(2 * (size_t)kMaxHypPerLaunch + 64);
     const float cthr = thr_ceil(threshold);
-    if (variant == kScorePruned && cl->sp_valid && cl->sp_dirty && cl->sp_n > 0) {
-      cl->sp_tiles.ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
-      cl->sp_supers.ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
-      const SoA& s = cl->sp_soa();
-      launch_sphere_bounds(s.x.p, s.y.p, s.z.p, cl->sp_n, cl->sp_tiles.p, cl->sp_supers.p,
-                           c->stream);
-      cl->sp_dirty = false;
-    }
+    if (variant == kScorePruned && cl->sp_valid) ensure_sphere_bounds(c, cl);
     HIPCHK(hipMemcpyAsync(c->pos.p, c->h_pos.p, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
     launch_gather_samples(c->pos.p, 3 * D, 0, src, c->samples.p, c->stream);
     const int Dp = (D + 63) / 64 * 64;
@@ -873,7 +888,7 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
         const uint4* bcol = nullptr;
         const float* band = nullptr;
         launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
-        c->lp.ensure((size_t)sp_supers(cl->sp_n) * D + 1);
+        c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
         c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
         static const bool want_stats = std::getenv("DLG_PRUNE_STATS") != nullptr;
         unsigned long long* stp = nullptr;
@@ -883,7 +898,7 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
           HIPCHK(hipMemsetAsync(stp, 0, 48, c->stream));
         }
         launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr,
-                            prune_margin(cthr, cl->amax), c->res.p, c->lp.p, c->lp_n.p,
+                            prune_margin(cthr, cl->amax), cl->amax, c->res.p, c->lp.p, c->lp_n.p,
                             c->num_cus, c->stream, stp);
         if (want_stats) {
           unsigned long long h[6];

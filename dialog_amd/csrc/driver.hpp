@@ -179,6 +179,7 @@ struct dlg_ctx {
   // kernel executes (the host would otherwise only wait for it)
   PinBuf<int32_t> h_stage;
   hipEvent_t ev_stage = nullptr;
+  hipEvent_t ev_tot = nullptr;  // end of a round's totals D2H (work queued after it may still run)
   int32_t* pending_dst = nullptr;
   int64_t pending_n = 0;
   NormalsWork nw;
@@ -203,7 +204,8 @@ struct dlg_cloud {
   int sp_cur = -1;         // -1 pristine, 0 / 1 ping-pong
   int64_t sp_n_pristine = 0, sp_n = 0;
   SoA sp_pristine, sp_buf[2];
-  DevBuf<float4> sp_tiles_pr, sp_supers_pr, sp_tiles, sp_supers;
+  // sphere bounds of the pristine copy and of each ping-pong buffer sp_buf[i]
+  DevBuf<float4> sp_tiles_pr, sp_supers_pr, sp_tb[2], sp_sb[2];
   const SoA& sp_soa() const { return sp_cur < 0 ? sp_pristine : sp_buf[sp_cur]; }
   int sp_spare() const { return sp_cur == 0 ? 1 : 0; }
   PointsView view() const {

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "dev_common.hpp"
 
@@ -65,10 +66,12 @@ __global__ void k_gather_order(PointsView src, const int32_t* __restrict__ order
 constexpr int kSbBS = 256;
 __global__ __launch_bounds__(kSbBS) void k_sphere_bounds(const float* __restrict__ X,
                                                          const float* __restrict__ Y,
-                                                         const float* __restrict__ Z, int64_t n,
+                                                         const float* __restrict__ Z, int64_t n_arg,
+                                                         const int32_t* __restrict__ n_dev,
                                                          float4* __restrict__ tiles,
                                                          float4* __restrict__ supers) {
   __shared__ float4 s_t[kSbBS / kWave][kSuperTiles];
+  const int64_t n = n_dev ? (int64_t)*n_dev : n_arg;
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int r32 = lane & 31, hh = lane >> 5;
   const int64_t s = (int64_t)blockIdx.x * (kSbBS / kWave) + wv;
@@ -155,7 +158,7 @@ __device__ __forceinline__ float prune_lim(float margin, float r) {
 
 __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict__ supers,
                                                         int nsup, const HypRec* __restrict__ hyps,
-                                                        int D, float margin,
+                                                        int D, int ls, float margin,
                                                         uint16_t* __restrict__ lp,
                                                         int32_t* __restrict__ lp_n) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
     __syncthreads();
     const float4 sp = supers[sidx];
     const float slim = prune_lim(margin, sp.w);
-    uint16_t* out = lp + (int64_t)sidx * D;
+    uint16_t* out = lp + (int64_t)sidx * ls;
     for (int b = 0; b < D; b += kPrBS) {  // block-uniform trip count
       const int j = b + threadIdx.x;
       bool near = false;
@@ -192,14 +195,16 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
   }
 }
 
-__global__ __launch_bounds__(kPrBS) void k_score_tiles(
+__device__ __forceinline__ void score_tiles_body(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp,
+    int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
     const int32_t* __restrict__ lp_n, const HypRec* __restrict__ hyps,
     const uint4* __restrict__ bcol, const float* __restrict__ band, int D, float cthr,
     float margin, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
-  __shared__ int32_t s_cnt[kMaxHypPerLaunch];
+  // per-plane counts, two 16-bit halves per word (the grid is sized so that no workgroup sees
+  // more than 65535 points, launch_score_pruned): 76 KB of LDS in all -> two workgroups per CU
+  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];
   __shared__ uint16_t s_ring[kPrWaves][kPrRing];
   __shared__ unsigned long long s_st[6];
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -207,8 +212,8 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles(
   for (int j = threadIdx.x; j < D; j += kPrBS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
-    s_cnt[j] = 0;
   }
+  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += kPrBS) s_cnt[j] = 0u;
   if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
   __syncthreads();
   const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -220,7 +225,7 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles(
     for (int t = it * kPrChunk; t < t_end; ++t) {
       const int sidx = t / kSuperTiles;
       const int nlp = lp_n[sidx];
-      const uint16_t* lps = lp + (int64_t)sidx * D;
+      const uint16_t* lps = lp + (int64_t)sidx * ls;
       const float4 tb = tiles[t];
       const float tlim = prune_lim(margin, tb.w);
       const int64_t p0 = (int64_t)t * kTileP;
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles(
         }
         uint32_t c = acc / 255u;
         c += __shfl_xor(c, 32);
-        if (hh == 0 && col && c) atomicAdd(&s_cnt[j], (int32_t)c);
+        if (hh == 0 && col && c) atomicAdd(&s_cnt[j >> 1], c << (16 * (j & 1)));
       };
       int jn = lane < nlp ? (int)lps[lane] : 0;  // the list is read one chunk ahead
       for (int c0 = 0; c0 < nlp; c0 += kWave) {
@@ -357,12 +362,230 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles(
   }
   __syncthreads();
   for (int j = threadIdx.x; j < D; j += kPrBS) {
-    const int c = s_cnt[j];
+    const int c = (int)((s_cnt[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
     if (c) atomicAdd(&counts[j], c);
   }
   if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
 }
 
+// two occupancy points of the same body: 4 waves/SIMD (one workgroup per CU, no spills) and
+// 8 waves/SIMD (two workgroups per CU, VGPRs capped at 64)
+#define DLG_SCORE_TILES_ARGS                                                                    \
+  const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n, \
+      const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,                \
+      const int32_t* __restrict__ lp_n, const HypRec* __restrict__ hyps,                        \
+      const uint4* __restrict__ bcol, const float* __restrict__ band, int D, float cthr,        \
+      float margin, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats
+__global__ __launch_bounds__(kPrBS) void k_score_tiles(DLG_SCORE_TILES_ARGS) {
+  score_tiles_body(X, Y, Z, n, tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
+}
+__global__ __launch_bounds__(kPrBS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_score_tiles_o8(
+    DLG_SCORE_TILES_ARGS) {
+  score_tiles_body(X, Y, Z, n, tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
+}
+#undef DLG_SCORE_TILES_ARGS
+
+
+// ---------------------------------------------------------------------------------------------
+// k_score_tiles_rl: the same (tile, plane) decisions as k_score_tiles with no global load on the
+// group path.  A work item (4 consecutive tiles of one super-tile) loads its super-tile's plane
+// list once into registers (up to kListCap entries, two uint16 per dword, 8 dwords per lane);
+// per tile the list is tested against the tile sphere from registers + LDS, near planes go to
+// the wave's LDS ring, and every 32 queued planes are scored with B columns built from the
+// LDS coefficients (exact bf16 split of a, b, c and of the double-evaluated h = n.c + d) and a
+// rounding band computed from S = |a| ax + |b| ay + |c| az + |d| (4.25 u S >= the 4.21 u S of
+// k_prep_bf16's band x 0.065).  The next tile's header and points are loaded while the current
+// tile is processed.
+constexpr int kListRegs = 8;
+constexpr int kListCap = kListRegs * 2 * kWave;  // 1024 entries
+constexpr int kRing2 = 256;                       // >= 31 queued + 128 appended per list step
+
+__global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
+    const int32_t* __restrict__ lp_n, const HypRec* __restrict__ hyps, int D, float cthr,
+    float margin, float ax, float ay, float az, int32_t* __restrict__ counts,
+    unsigned long long* __restrict__ stats) {
+  __shared__ float4 s_cf[kMaxHypPerLaunch];
+  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves (see k_score_tiles)
+  __shared__ uint16_t s_ring[kPrWaves][kRing2];
+  __shared__ unsigned long long s_st[6];
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int r32 = lane & 31, hh = lane >> 5;
+  for (int j = threadIdx.x; j < D; j += kPrBS) {
+    const HypRec h = hyps[j];
+    s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
+  }
+  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += kPrBS) s_cnt[j] = 0u;
+  if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
+  __syncthreads();
+  const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int ntiles = (n + kTileP - 1) / kTileP;
+  const int nitems = (ntiles + kPrChunk - 1) / kPrChunk;
+  const int gw = blockIdx.x * kPrWaves + wv, nw = gridDim.x * kPrWaves;
+  uint16_t* ring = s_ring[wv];
+  for (int it = gw; it < nitems; it += nw) {
+    const int t0 = it * kPrChunk, t_end = min(ntiles, t0 + kPrChunk);
+    const int sidx = t0 / kSuperTiles;  // kSuperTiles % kPrChunk == 0: one super-tile per item
+    const int nlp = lp_n[sidx];
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
+    uint32_t L[kListRegs];
+#pragma unroll
+    for (int k = 0; k < kListRegs; ++k) L[k] = 0u;
+    const bool inreg = nlp <= kListCap;
+    if (inreg) {
+#pragma unroll
+      for (int k = 0; k < kListRegs; ++k)
+        if (2 * (lane + k * kWave) < nlp) L[k] = lw[lane + k * kWave];
+    }
+    // first tile of the item
+    float4 tb = tiles[t0];
+    float x = 0.f, y = 0.f, z = 0.f;
+    {
+      const int64_t p = (int64_t)t0 * kTileP + r32;
+      if (p < n) { x = X[p]; y = Y[p]; z = Z[p]; }
+    }
+    for (int t = t0; t < t_end; ++t) {
+      // prefetch the next tile of the item
+      float4 tb_n = make_float4(0.f, 0.f, 0.f, 0.f);
+      float xn = 0.f, yn = 0.f, zn = 0.f;
+      if (t + 1 < t_end) {
+        tb_n = tiles[t + 1];
+        const int64_t p = (int64_t)(t + 1) * kTileP + r32;
+        if (p < n) { xn = X[p]; yn = Y[p]; zn = Z[p]; }
+      }
+      const int64_t p0 = (int64_t)t * kTileP;
+      const bool valid = p0 + r32 < n;
+      const float tlim = prune_lim(margin, tb.w);
+      if (stats && lane == 0) { atomicAdd(&s_st[2], 1ull); atomicAdd(&s_st[1], (unsigned long long)nlp); }
+      bool a_ready = false, bad = false;
+      u32x4 a1 = {0u, 0u, 0u, 0u}, a2 = {0u, 0u, 0u, 0u};
+      int nq = 0, head = 0;
+      auto score = [&](int m) {
+        if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
+        const bool col = r32 < m;
+        const int j = col ? (int)ring[(head + r32) & (kRing2 - 1)] : 0;
+        const float4 cf = s_cf[j];
+        if (!a_ready) {
+          a_ready = true;
+          bad = ballot(!valid || !(isfinite(x) && isfinite(y) && isfinite(z))) != 0;
+          const float dx = valid ? x - tb.x : 0.f, dy = valid ? y - tb.y : 0.f;
+          const float dz = valid ? z - tb.z : 0.f;
+          const Split3 sx = split3(dx), sy = split3(dy), sz = split3(dz);
+          if (hh == 0) {
+            a1 = u32x4{pk(sx.p1, sx.p1), pk(sx.p2, sx.p1), pk(sx.p3, sx.p2), pk(sy.p1, sy.p1)};
+            a2 = u32x4{pk(sz.p3, sz.p2), pk(kBf16One, kBf16One), pk(kBf16One, 0u), 0u};
+          } else {
+            a1 = u32x4{pk(sy.p2, sy.p1), pk(sy.p3, sy.p2), pk(sz.p1, sz.p1), pk(sz.p2, sz.p1)};
+            a2 = u32x4{0u, 0u, 0u, 0u};
+          }
+        }
+        // B column of plane j (k_prep_bf16's layout, d slots = split of h = n.c + d)
+        u32x4 b1 = {0u, 0u, 0u, 0u}, b2 = {0u, 0u, 0u, 0u};
+        float w = 0.0f;
+        if (col) {
+          const Split3 sa = split3(cf.x), sb = split3(cf.y), sc = split3(cf.z);
+          const double hd = __builtin_fma((double)cf.x, (double)tb.x,
+                                          __builtin_fma((double)cf.y, (double)tb.y,
+                                                        __builtin_fma((double)cf.z, (double)tb.z, (double)cf.w)));
+          const float hf = (float)hd;
+          if (hh == 0) {
+            const Split3 sh = split3(hf);
+            b1 = u32x4{pk(sa.p1, sa.p2), pk(sa.p1, sa.p3), pk(sa.p1, sa.p2), pk(sb.p1, sb.p2)};
+            b2 = u32x4{pk(sc.p1, sc.p2), pk(sh.p1, sh.p2), pk(sh.p3, 0u), 0u};
+          } else {
+            b1 = u32x4{pk(sb.p1, sb.p3), pk(sb.p1, sb.p2), pk(sc.p1, sc.p2), pk(sc.p1, sc.p3)};
+          }
+          // |D - pcl_dot| <= 4.1 u S + 44 u (|n|_1 r + |h|) (see k_score_tiles); S in float
+          // (<= 4 roundings) times 4.25 u covers the 4.21 u S there
+          const float S = __builtin_fmaf(fabsf(cf.x), ax, __builtin_fmaf(fabsf(cf.y), ay,
+                                         __builtin_fmaf(fabsf(cf.z), az, fabsf(cf.w))));
+          w = __builtin_fmaf(0x1.1p-22f, S, 3.0e-6f * __builtin_fmaf(1.8f, tb.w, fabsf(hf))) + 1e-8f;
+          if (!(w <= INFINITY)) w = INFINITY;  // NaN (0 x inf): re-decide everything
+        } else if (hh == 0) {
+          b2 = u32x4{0u, pk(0x4000u, 0u), 0u, 0u};  // not a plane: D = 2, never counted
+        }
+        f32x16 Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a1), as_bf16x8(b1), zero, 0, 0, 0);
+        Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a2), as_bf16x8(b2), Dv, 0, 0, 0);
+        uint32_t acc = 0;
+        float mn = INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+          const float r0 = fabsf(Dv[i]) - cthr, r1 = fabsf(Dv[i + 1]) - cthr;
+          const float r2 = fabsf(Dv[i + 2]) - cthr, r3 = fabsf(Dv[i + 3]) - cthr;
+          acc = count4(r0, r1, r2, r3, acc);
+          mn = min3_abs(mn, r0, r1);
+          mn = min3_abs(mn, r2, r3);
+        }
+        const bool need = bad || mn <= w;
+        if (ballot(need)) {  // rare: re-decide the band elements in PCL op order
+          if (stats && lane == 0) atomicAdd(&s_st[5], 1ull);
+#pragma unroll 1
+          for (int i = 0; i < 16; ++i) {
+            const float ri = fabsf(Dv[i]) - cthr;
+            const bool inb = need && (bad || fabsf(ri) <= w);
+            if (ballot(inb)) {
+              const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+              const float px = __shfl(x, row), py = __shfl(y, row), pz = __shfl(z, row);
+              const bool ex = p0 + row < n && fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, px, py, pz)) < cthr;
+              const uint32_t approx = __float_as_uint(ri) >> 31;
+              if (inb) acc = acc + (ex ? 255u : 0u) - 255u * approx;
+            }
+          }
+        }
+        uint32_t c = acc / 255u;
+        c += __shfl_xor(c, 32);
+        if (hh == 0 && col && c) atomicAdd(&s_cnt[j >> 1], c << (16 * (j & 1)));
+        head += m;
+      };
+      // tile-sphere test of two list entries per lane (entries e0 = 2 (lane + 64 k), e0 + 1)
+      auto test2 = [&](uint32_t wd, int e0) {
+        const int j0 = (int)(wd & 0xFFFFu), j1 = (int)(wd >> 16);
+        const float4 c0 = s_cf[j0], c1 = s_cf[j1];
+        const float h0 = __builtin_fmaf(c0.x, tb.x, __builtin_fmaf(c0.y, tb.y, __builtin_fmaf(c0.z, tb.z, c0.w)));
+        const float h1 = __builtin_fmaf(c1.x, tb.x, __builtin_fmaf(c1.y, tb.y, __builtin_fmaf(c1.z, tb.z, c1.w)));
+        const bool n0 = e0 < nlp && fabsf(h0) <= tlim;
+        const bool n1 = e0 + 1 < nlp && fabsf(h1) <= tlim;
+        const uint64_t m0 = ballot(n0), m1 = ballot(n1);
+        if (n0) ring[(nq + lanes_below(m0)) & (kRing2 - 1)] = (uint16_t)j0;
+        nq += (int)__popcll(m0);
+        if (n1) ring[(nq + lanes_below(m1)) & (kRing2 - 1)] = (uint16_t)j1;
+        nq += (int)__popcll(m1);
+        __builtin_amdgcn_wave_barrier();
+        while (nq - head >= 32) score(32);
+      };
+      if (inreg) {
+#pragma unroll
+        for (int k = 0; k < kListRegs; ++k) {
+          if (k * 2 * kWave >= nlp) break;
+          test2(L[k], 2 * (lane + k * kWave));
+        }
+      } else {
+        for (int b = 0; b < nlp; b += kListCap) {  // long lists: batches of kListCap entries
+          uint32_t Lb[kListRegs];
+#pragma unroll
+          for (int k = 0; k < kListRegs; ++k) {
+            const int e = b + 2 * (lane + k * kWave);
+            Lb[k] = e < nlp ? lw[(b >> 1) + lane + k * kWave] : 0u;
+          }
+#pragma unroll
+          for (int k = 0; k < kListRegs; ++k) {
+            if (b + k * 2 * kWave >= nlp) break;
+            test2(Lb[k], b + 2 * (lane + k * kWave));
+          }
+        }
+      }
+      if (nq > head) score(nq - head);
+      tb = tb_n; x = xn; y = yn; z = zn;
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < D; j += kPrBS) {
+    const int c = (int)((s_cnt[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+    if (c) atomicAdd(&counts[j], c);
+  }
+  if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
+}
 }  // namespace
 
 void launch_morton_keys(PointsView src, float ax, float ay, float az, uint32_t* keys,
@@ -393,12 +616,12 @@ void launch_gather_order(PointsView src, const int32_t* order, int64_t n, Points
 }
 
 void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_t n,
-                          float4* tiles, float4* supers, hipStream_t s) {
+                          const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s) {
   if (n <= 0) return;
   const int64_t ns = sp_supers(n);
   const int wpb = kSbBS / kWave;
   hipLaunchKernelGGL(k_sphere_bounds, dim3((unsigned)((ns + wpb - 1) / wpb)), dim3(kSbBS), 0, s,
-                     x, y, z, n, tiles, supers);
+                     x, y, z, n, n_dev, tiles, supers);
 }
 
 float prune_margin(float cthr, const float amax[3]) {
@@ -411,17 +634,43 @@ float prune_margin(float cthr, const float amax[3]) {
 }
 
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
-                         const float* band, int D, float cthr, float margin, int32_t* counts,
-                         uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
+                         const float* band, int D, float cthr, float margin, const float amax[3],
+                         int32_t* counts, uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
                          unsigned long long* stats) {
   if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) return;
   const int64_t ns = sp_supers(v.n);
+  const int ls = prune_list_stride(D);
   const unsigned ga = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2 * num_cus, ns));
-  hipLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, v.supers, (int)ns, hyps, D,
+  hipLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, v.supers, (int)ns, hyps, D, ls,
                      margin, lp, lp_n);
+  // one workgroup per CU (LDS + VGPRs), and enough of them that no workgroup takes more than 31
+  // items per wave (31 x 16 waves x 4 tiles x 32 points = 63488 <= 65535: 16-bit LDS counters)
   const int64_t items = (sp_tiles(v.n) + kPrChunk - 1) / kPrChunk;
-  const unsigned gb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(num_cus, (items + kPrWaves - 1) / kPrWaves));
-  hipLaunchKernelGGL(k_score_tiles, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
-                     v.tiles, lp, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
+  constexpr int64_t kMaxItemsPerWave = 65535 / (kPrWaves * kPrChunk * kTileP);
+  static_assert(kMaxItemsPerWave >= 1, "16-bit counters");
+  static const int kern = [] {
+    const char* e = std::getenv("DLG_PRUNE_KERNEL");
+    return e ? std::atoi(e) : 2;
+  }();
+  static const int occ = [] {
+    const char* e = std::getenv("DLG_PRUNE_OCC");
+    return e ? std::atoi(e) : 4;
+  }();
+  const int per_cu = (kern == 1 && occ == 8) ? 2 : 1;
+  const int64_t g_fill = std::min<int64_t>((int64_t)per_cu * num_cus, (items + kPrWaves - 1) / kPrWaves);
+  const int64_t g_cnt = (items + kPrWaves * kMaxItemsPerWave - 1) / (kPrWaves * kMaxItemsPerWave);
+  const unsigned gb = (unsigned)std::max<int64_t>(1, std::max(g_fill, g_cnt));
+  if (kern == 2) {
+    if (!band) {}  // (the register-list kernel derives its band from the coefficients)
+    hipLaunchKernelGGL(k_score_tiles_rl, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
+                       v.tiles, lp, ls, lp_n, hyps, D, cthr, margin, amax[0], amax[1], amax[2],
+                       counts, stats);
+  } else if (occ == 8) {
+    hipLaunchKernelGGL(k_score_tiles_o8, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
+                       v.tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
+  } else {
+    hipLaunchKernelGGL(k_score_tiles, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
+                       v.tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
+  }
 }
 }  // namespace dlg

@@ -51,17 +51,22 @@ hipError_t morton_sort(void* tmp, size_t tmp_bytes, uint32_t* keys_in, uint32_t*
 // dst[i] = src[order[i]], i < n
 void launch_gather_order(PointsView src, const int32_t* order, int64_t n, PointsOut dst,
                          hipStream_t s);
-// tile and super-tile bounding spheres of n points
+// tile and super-tile bounding spheres of n points; with n_dev the count is read on the device
+// (*n_dev <= n, the grid is sized for n)
 void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_t n,
-                          float4* tiles, float4* supers, hipStream_t s);
+                          const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s);
 // margin = smallest float >= (cthr + 2 e_max)(1 + 2^-19), e_max = 64 u 2.0001 (ax + ay + az)
 float prune_margin(float cthr, const float amax[3]);
 // pruned countWithinDistance of D plane hypotheses over the spatial points.  hyps / bcol / band
 // as prepared for k_score_bf16 (launch_prep_bf16); counts[D] zeroed by the caller; lp / lp_n:
-// scratch of sp_supers(n) * D uint16 and sp_supers(n) int32 (per super-tile plane lists).
+// scratch of sp_supers(n) * prune_list_stride(D) uint16 and sp_supers(n) int32 (per super-tile plane lists).
+// list stride per super-tile (D rounded up to 64 entries: dword-aligned entry pairs)
+inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
+// amax: the cloud's per-axis max |coordinate| (the scoring band's S bound).  DLG_PRUNE_KERNEL=1
+// selects the first version (k_score_tiles: global B columns, list read per tile), default 2.
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
-                         const float* band, int D, float cthr, float margin, int32_t* counts,
-                         uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
+                         const float* band, int D, float cthr, float margin, const float amax[3],
+                         int32_t* counts, uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
                          unsigned long long* stats = nullptr);  // [6] counters (A/B tool)
 
 }  // namespace dlg

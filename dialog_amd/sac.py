@@ -220,16 +220,24 @@ def segment_cloud(cloud: Cloud, params, capacity=None):
     st = _lib.SacStats()
     ctx.check(ctx._L.dlg_sac_segment(ctx.h, cloud.h, C.byref(params), _f32p(coeff), _i32p(inl),
                                      cap, C.byref(n), C.byref(st)))
-    return inl[:n.value].copy(), coeff, _stats_dict(st)
+    return inl[:n.value], coeff, _stats_dict(st)  # a view: the buffer is this call's own
 
 
-def extract_planes(cloud: Cloud, params, max_planes=20, min_inliers=0, capacity=None):
-    """Sequential extract-and-remove -> dict(coeffs [P,4], offsets [P+1], inliers, stats)."""
+def extract_planes(cloud: Cloud, params, max_planes=20, min_inliers=0, capacity=None, out=None):
+    """Sequential extract-and-remove -> dict(coeffs [P,4], offsets [P+1], inliers, stats).
+
+    `out`: optional caller-owned int32 buffer for the inlier ids (reused across calls, like a
+    std::vector the caller keeps); `inliers` is then a view of it."""
     ctx = cloud.ctx
-    cap = int(capacity if capacity is not None else max(cloud.n_active * max(ctx.world, 1), 1))
+    if out is not None:
+        if out.dtype != np.int32 or not out.flags.c_contiguous or out.ndim != 1:
+            raise ValueError("out must be a contiguous 1-D int32 array")
+        inl, cap = out, int(out.size)
+    else:
+        cap = int(capacity if capacity is not None else max(cloud.n_active * max(ctx.world, 1), 1))
+        inl = np.empty(max(cap, 1), np.int32)
     coeffs = np.zeros((max(max_planes, 1), 4), np.float32)
     offs = np.zeros(max_planes + 1, np.int64)
-    inl = np.empty(max(cap, 1), np.int32)
     npl = C.c_int()
     xs = _lib.ExtractStats()
     ctx.check(ctx._L.dlg_extract_planes(ctx.h, cloud.h, C.byref(params), int(max_planes),
@@ -241,7 +249,7 @@ def extract_planes(cloud: Cloud, params, max_planes=20, min_inliers=0, capacity=
                  score_launches=xs.score_launches, score_ms=xs.score_ms, select_ms=xs.select_ms,
                  wall_ms=xs.wall_ms)
     return dict(coeffs=coeffs[:k].copy(), offsets=offs[:k + 1].copy(),
-                inliers=inl[:offs[k]].copy(), n_planes=k, stats=stats)
+                inliers=inl[:offs[k]], n_planes=k, stats=stats)
 
 
 class RansacControl:

@@ -35,6 +35,12 @@ for s in $STEPS; do
     benchtorch) run bench_torch 600 python3 bench.py --torch-dist --no-cpu-baseline --steps 2 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 ;;
     pmc)    run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 1 --warmup 0 ;;
+    pstats) DLG_PRUNE_STATS=1 VARIANTS="${VARIANTS:-20,19}" run pstats 300 python3 tools/score_ab.py 10000000 4096 2 ;;
+    abocc)  DLG_PRUNE_OCC=4 VARIANTS=20 run abocc4 300 python3 tools/score_ab.py 10000000 4096 5 && \
+            DLG_PRUNE_OCC=8 VARIANTS=20 run abocc8 300 python3 tools/score_ab.py 10000000 4096 5 ;;
+    ptest)  run ptest 600 python3 -u -m pytest tests/test_pruned.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    abk)    DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=1 VARIANTS=20,19 run abk1 300 python3 tools/score_ab.py 10000000 4096 5 && \
+            DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=2 VARIANTS=20,19 run abk2 300 python3 tools/score_ab.py 10000000 4096 5 ;;
     ab)     run score_ab 600 python3 tools/score_ab.py ;;
     list)   run counters 120 rocprofv3 -L ;;
     sqpmc)  VARIANTS="${VARIANTS:-0,2}" run sqpmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \

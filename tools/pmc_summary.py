@@ -10,9 +10,10 @@ for f in sys.argv[1:]:
     disp = collections.defaultdict(set)
     for r in rows:
         k = r["Kernel_Name"]
-        if "k_score" not in k:
+        m = re.search(r"(k_score\w*<[^>]*>|k_\w+)", k)
+        if not m or not any(t in k for t in ("k_score", "k_prune")):
             continue
-        name = re.search(r"k_score\w*<[^>]*>", k).group(0)
+        name = m.group(0)
         disp[name].add(r["Dispatch_Id"])
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
     for name, d in agg.items():

@@ -52,10 +52,13 @@ def main():
             cal = (12.0 * n) / (1024 * sc[0][1])
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, bench.py --steps 1 --warmup 0",
            "kernels": res, "read_calibration_dword_loads": cal}
-    key = "k_score_bf16" if "k_score_bf16" in res else "k_score"
-    if key in res and cal:
-        out["kernel"] = key
-        out["hbm_bytes_per_launch"] = res[key]["fetch_bytes_mean"] * cal + res[key].get("write_bytes_mean", 0.0)
+    # one scoring launch = k_prune_supers + k_score_tiles (pruned, default), else the exhaustive kernel
+    keys = [k for k in ("k_prune_supers", "k_score_tiles") if k in res] or \
+           (["k_score_bf16"] if "k_score_bf16" in res else ["k_score"])
+    if all(k in res for k in keys) and cal:
+        out["kernel"] = " + ".join(keys)
+        out["hbm_bytes_per_launch"] = sum(res[k]["fetch_bytes_mean"] * cal + res[k].get("write_bytes_mean", 0.0)
+                                          for k in keys)
     json.dump(out, open(os.path.join(ROOT, "profiles", "score_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
