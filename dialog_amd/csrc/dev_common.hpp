@@ -35,6 +35,7 @@ __device__ __forceinline__ float pcl_dot(float a, float b, float c, float d, flo
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t kBf16One = 0x3F80u;
 

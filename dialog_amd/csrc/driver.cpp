@@ -279,7 +279,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     else if (pruned) {
       const uint4* bcol = nullptr;
       const float* band = nullptr;
-      launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
+      if (prune_kernel() == 1) launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
       launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr, pmargin, cl->amax,

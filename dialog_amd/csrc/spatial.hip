@@ -390,16 +390,22 @@ __global__ __launch_bounds__(kPrBS) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 // k_score_tiles_rl: the same (tile, plane) decisions as k_score_tiles with no global load on the
 // group path.  A work item (4 consecutive tiles of one super-tile) loads its super-tile's plane
 // list once into registers (up to kListCap entries, two uint16 per dword, 8 dwords per lane);
-// per tile the list is tested against the tile sphere from registers + LDS, near planes go to
-// the wave's LDS ring, and every 32 queued planes are scored with B columns built from the
-// LDS coefficients (exact bf16 split of a, b, c and of the double-evaluated h = n.c + d) and a
-// rounding band computed from S = |a| ax + |b| ay + |c| az + |d| (4.25 u S >= the 4.21 u S of
-// k_prep_bf16's band x 0.065).  The next tile's header and points are loaded while the current
-// tile is processed.
+// per tile the list is tested against the tile sphere from registers + LDS (packed FMAs, two
+// entries per lane), near planes go to the wave's LDS ring, and every 32 queued planes are
+// scored with B columns split from the LDS coefficients (exact bf16 split of a, b, c and of the
+// double-evaluated h = n.c + d) and a rounding band computed from S = |a| ax + |b| ay + |c| az +
+// |d| (4.25 u S >= the 4.21 u S of k_prep_bf16's band x 0.065).  The next tile's header and
+// points are loaded after the current tile's A operand is built (vmcnt is in order: the wait
+// for this tile's data never waits for the prefetch).  LDS: coefficients 64 KB + counts 8 KB +
+// rings 8 KB.  (An 80 KB per-plane LDS record of the B splits, assembled with byte permutes,
+// measured no faster.)
 constexpr int kListRegs = 8;
 constexpr int kListCap = kListRegs * 2 * kWave;  // 1024 entries
 constexpr int kRing2 = 256;                       // >= 31 queued + 128 appended per list step
 
+// EXP: timing experiments only (1: groups not scored, 2: no band re-decision) -- counts are
+// then wrong
+template <int EXP>
 __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
@@ -429,14 +435,16 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
     const int sidx = t0 / kSuperTiles;  // kSuperTiles % kPrChunk == 0: one super-tile per item
     const int nlp = lp_n[sidx];
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
+    // the item's tiles take the list kListCap entries at a time (one pass unless it is long)
+#pragma unroll 1
+    for (int lb = 0; lb < nlp; lb += kListCap) {
+    const int le = min(nlp, lb + kListCap);
     uint32_t L[kListRegs];
 #pragma unroll
-    for (int k = 0; k < kListRegs; ++k) L[k] = 0u;
-    const bool inreg = nlp <= kListCap;
-    if (inreg) {
-#pragma unroll
-      for (int k = 0; k < kListRegs; ++k)
-        if (2 * (lane + k * kWave) < nlp) L[k] = lw[lane + k * kWave];
+    for (int k = 0; k < kListRegs; ++k) {
+      const int e = lb + 2 * (lane + k * kWave);
+      L[k] = e < le ? lw[(lb >> 1) + lane + k * kWave] : 0u;
+      if (e + 1 >= le) L[k] &= 0xFFFFu;  // (past the end: plane 0, never counted)
     }
     // first tile of the item
     float4 tb = tiles[t0];
@@ -446,6 +454,26 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
       if (p < n) { x = X[p]; y = Y[p]; z = Z[p]; }
     }
     for (int t = t0; t < t_end; ++t) {
+      const int64_t p0 = (int64_t)t * kTileP;
+      const bool valid = p0 + r32 < n;
+      const float tlim = prune_lim(margin, tb.w);
+      if (stats && lane == 0) { atomicAdd(&s_st[2], 1ull); atomicAdd(&s_st[1], (unsigned long long)nlp); }
+      // A operand (the tile's points relative to its centre) before the next tile's loads are
+      // issued: waiting for this tile's data then never waits for the prefetch (vmcnt is in order)
+      const bool bad = ballot(!valid || !(isfinite(x) && isfinite(y) && isfinite(z))) != 0;
+      u32x4 a1, a2;
+      {
+        const float dx = valid ? x - tb.x : 0.f, dy = valid ? y - tb.y : 0.f;
+        const float dz = valid ? z - tb.z : 0.f;
+        const Split3 sx = split3(dx), sy = split3(dy), sz = split3(dz);
+        if (hh == 0) {
+          a1 = u32x4{pk(sx.p1, sx.p1), pk(sx.p2, sx.p1), pk(sx.p3, sx.p2), pk(sy.p1, sy.p1)};
+          a2 = u32x4{pk(sz.p3, sz.p2), pk(kBf16One, kBf16One), pk(kBf16One, 0u), 0u};
+        } else {
+          a1 = u32x4{pk(sy.p2, sy.p1), pk(sy.p3, sy.p2), pk(sz.p1, sz.p1), pk(sz.p2, sz.p1)};
+          a2 = u32x4{0u, 0u, 0u, 0u};
+        }
+      }
       // prefetch the next tile of the item
       float4 tb_n = make_float4(0.f, 0.f, 0.f, 0.f);
       float xn = 0.f, yn = 0.f, zn = 0.f;
@@ -454,52 +482,41 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
         const int64_t p = (int64_t)(t + 1) * kTileP + r32;
         if (p < n) { xn = X[p]; yn = Y[p]; zn = Z[p]; }
       }
-      const int64_t p0 = (int64_t)t * kTileP;
-      const bool valid = p0 + r32 < n;
-      const float tlim = prune_lim(margin, tb.w);
-      if (stats && lane == 0) { atomicAdd(&s_st[2], 1ull); atomicAdd(&s_st[1], (unsigned long long)nlp); }
-      bool a_ready = false, bad = false;
-      u32x4 a1 = {0u, 0u, 0u, 0u}, a2 = {0u, 0u, 0u, 0u};
       int nq = 0, head = 0;
       auto score = [&](int m) {
         if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
         const bool col = r32 < m;
         const int j = col ? (int)ring[(head + r32) & (kRing2 - 1)] : 0;
-        const float4 cf = s_cf[j];
-        if (!a_ready) {
-          a_ready = true;
-          bad = ballot(!valid || !(isfinite(x) && isfinite(y) && isfinite(z))) != 0;
-          const float dx = valid ? x - tb.x : 0.f, dy = valid ? y - tb.y : 0.f;
-          const float dz = valid ? z - tb.z : 0.f;
-          const Split3 sx = split3(dx), sy = split3(dy), sz = split3(dz);
-          if (hh == 0) {
-            a1 = u32x4{pk(sx.p1, sx.p1), pk(sx.p2, sx.p1), pk(sx.p3, sx.p2), pk(sy.p1, sy.p1)};
-            a2 = u32x4{pk(sz.p3, sz.p2), pk(kBf16One, kBf16One), pk(kBf16One, 0u), 0u};
-          } else {
-            a1 = u32x4{pk(sy.p2, sy.p1), pk(sy.p3, sy.p2), pk(sz.p1, sz.p1), pk(sz.p2, sz.p1)};
-            a2 = u32x4{0u, 0u, 0u, 0u};
-          }
+        if constexpr (EXP == 1) {
+          if (hh == 0 && col) atomicAdd(&s_cnt[j >> 1], 1u << (16 * (j & 1)));
+          head += m;
+          return;
         }
-        // B column of plane j (k_prep_bf16's layout, d slots = split of h = n.c + d)
+        const float4 cf = s_cf[j];
+        // B column of plane j (k_prep_bf16's layout, d slots = split of h = n.c + d), assembled
+        // from the LDS record with byte permutes
         u32x4 b1 = {0u, 0u, 0u, 0u}, b2 = {0u, 0u, 0u, 0u};
         float w = 0.0f;
         if (col) {
-          const Split3 sa = split3(cf.x), sb = split3(cf.y), sc = split3(cf.z);
           const double hd = __builtin_fma((double)cf.x, (double)tb.x,
                                           __builtin_fma((double)cf.y, (double)tb.y,
                                                         __builtin_fma((double)cf.z, (double)tb.z, (double)cf.w)));
           const float hf = (float)hd;
-          if (hh == 0) {
-            const Split3 sh = split3(hf);
-            b1 = u32x4{pk(sa.p1, sa.p2), pk(sa.p1, sa.p3), pk(sa.p1, sa.p2), pk(sb.p1, sb.p2)};
-            b2 = u32x4{pk(sc.p1, sc.p2), pk(sh.p1, sh.p2), pk(sh.p3, 0u), 0u};
-          } else {
-            b1 = u32x4{pk(sb.p1, sb.p3), pk(sb.p1, sb.p2), pk(sc.p1, sc.p2), pk(sc.p1, sc.p3)};
+          float S;
+          {
+            const Split3 sa = split3(cf.x), sb = split3(cf.y), sc = split3(cf.z);
+            if (hh == 0) {
+              const Split3 sh = split3(hf);
+              b1 = u32x4{pk(sa.p1, sa.p2), pk(sa.p1, sa.p3), pk(sa.p1, sa.p2), pk(sb.p1, sb.p2)};
+              b2 = u32x4{pk(sc.p1, sc.p2), pk(sh.p1, sh.p2), pk(sh.p3, 0u), 0u};
+            } else {
+              b1 = u32x4{pk(sb.p1, sb.p3), pk(sb.p1, sb.p2), pk(sc.p1, sc.p2), pk(sc.p1, sc.p3)};
+            }
+            S = __builtin_fmaf(fabsf(cf.x), ax, __builtin_fmaf(fabsf(cf.y), ay,
+                               __builtin_fmaf(fabsf(cf.z), az, fabsf(cf.w))));
           }
           // |D - pcl_dot| <= 4.1 u S + 44 u (|n|_1 r + |h|) (see k_score_tiles); S in float
-          // (<= 4 roundings) times 4.25 u covers the 4.21 u S there
-          const float S = __builtin_fmaf(fabsf(cf.x), ax, __builtin_fmaf(fabsf(cf.y), ay,
-                                         __builtin_fmaf(fabsf(cf.z), az, fabsf(cf.w))));
+          // (<= 4 roundings, possibly rounded up to bf16) times 4.25 u covers the 4.21 u S there
           w = __builtin_fmaf(0x1.1p-22f, S, 3.0e-6f * __builtin_fmaf(1.8f, tb.w, fabsf(hf))) + 1e-8f;
           if (!(w <= INFINITY)) w = INFINITY;  // NaN (0 x inf): re-decide everything
         } else if (hh == 0) {
@@ -517,20 +534,26 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
           mn = min3_abs(mn, r0, r1);
           mn = min3_abs(mn, r2, r3);
         }
-        const bool need = bad || mn <= w;
+        const bool need = EXP != 2 && (bad || mn <= w);
         if (ballot(need)) {  // rare: re-decide the band elements in PCL op order
           if (stats && lane == 0) atomicAdd(&s_st[5], 1ull);
-#pragma unroll 1
-          for (int i = 0; i < 16; ++i) {
-            const float ri = fabsf(Dv[i]) - cthr;
-            const bool inb = need && (bad || fabsf(ri) <= w);
-            if (ballot(inb)) {
-              const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-              const float px = __shfl(x, row), py = __shfl(y, row), pz = __shfl(z, row);
-              const bool ex = p0 + row < n && fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, px, py, pz)) < cthr;
-              const uint32_t approx = __float_as_uint(ri) >> 31;
-              if (inb) acc = acc + (ex ? 255u : 0u) - 255u * approx;
+          uint32_t bm = 0u, am = 0u;  // per lane: band elements, and their approximate verdicts
+          if (need) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const float ri = fabsf(Dv[i]) - cthr;
+              bm |= (uint32_t)(bad || fabsf(ri) <= w) << i;
+              am |= (__float_as_uint(ri) >> 31) << i;
             }
+          }
+          while (ballot(bm != 0u)) {  // one band element per lane per pass
+            const int i = bm ? __builtin_ctz(bm) : 0;
+            const bool inb = bm != 0u;
+            bm &= bm - 1u;
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const float px = __shfl(x, row), py = __shfl(y, row), pz = __shfl(z, row);
+            const bool ex = p0 + row < n && fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, px, py, pz)) < cthr;
+            if (inb) acc = acc + (ex ? 255u : 0u) - 255u * ((am >> i) & 1u);
           }
         }
         uint32_t c = acc / 255u;
@@ -539,45 +562,40 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
         head += m;
       };
       // tile-sphere test of two list entries per lane (entries e0 = 2 (lane + 64 k), e0 + 1)
+      // tile-sphere test of two list entries per lane (entries e0 = 2 (lane + 64 k), e0 + 1;
+      // entries past the list end were zeroed at load: plane 0, masked here), packed FMAs
+      const f32x2 tbx = {tb.x, tb.x}, tby = {tb.y, tb.y}, tbz = {tb.z, tb.z};
       auto test2 = [&](uint32_t wd, int e0) {
         const int j0 = (int)(wd & 0xFFFFu), j1 = (int)(wd >> 16);
         const float4 c0 = s_cf[j0], c1 = s_cf[j1];
-        const float h0 = __builtin_fmaf(c0.x, tb.x, __builtin_fmaf(c0.y, tb.y, __builtin_fmaf(c0.z, tb.z, c0.w)));
-        const float h1 = __builtin_fmaf(c1.x, tb.x, __builtin_fmaf(c1.y, tb.y, __builtin_fmaf(c1.z, tb.z, c1.w)));
-        const bool n0 = e0 < nlp && fabsf(h0) <= tlim;
-        const bool n1 = e0 + 1 < nlp && fabsf(h1) <= tlim;
+        const f32x2 cx = {c0.x, c1.x}, cy = {c0.y, c1.y}, cz = {c0.z, c1.z}, cw = {c0.w, c1.w};
+        const f32x2 h = __builtin_elementwise_fma(cx, tbx, __builtin_elementwise_fma(cy, tby,
+                                                  __builtin_elementwise_fma(cz, tbz, cw)));
+        const bool n0 = e0 < le && fabsf(h.x) <= tlim;
+        const bool n1 = e0 + 1 < le && fabsf(h.y) <= tlim;
         const uint64_t m0 = ballot(n0), m1 = ballot(n1);
+        const int k0 = (int)__popcll(m0);
         if (n0) ring[(nq + lanes_below(m0)) & (kRing2 - 1)] = (uint16_t)j0;
-        nq += (int)__popcll(m0);
-        if (n1) ring[(nq + lanes_below(m1)) & (kRing2 - 1)] = (uint16_t)j1;
-        nq += (int)__popcll(m1);
+        if (n1) ring[(nq + k0 + lanes_below(m1)) & (kRing2 - 1)] = (uint16_t)j1;
+        nq += k0 + (int)__popcll(m1);
         __builtin_amdgcn_wave_barrier();
         while (nq - head >= 32) score(32);
       };
-      if (inreg) {
+      {  // one copy of the test/score code: the list registers rotate through R[0]
+        uint32_t R[kListRegs];
 #pragma unroll
-        for (int k = 0; k < kListRegs; ++k) {
-          if (k * 2 * kWave >= nlp) break;
-          test2(L[k], 2 * (lane + k * kWave));
-        }
-      } else {
-        for (int b = 0; b < nlp; b += kListCap) {  // long lists: batches of kListCap entries
-          uint32_t Lb[kListRegs];
+        for (int k = 0; k < kListRegs; ++k) R[k] = L[k];
+#pragma unroll 1
+        for (int k = 0; lb + k * 2 * kWave < le; ++k) {
+          test2(R[0], lb + 2 * (lane + k * kWave));
 #pragma unroll
-          for (int k = 0; k < kListRegs; ++k) {
-            const int e = b + 2 * (lane + k * kWave);
-            Lb[k] = e < nlp ? lw[(b >> 1) + lane + k * kWave] : 0u;
-          }
-#pragma unroll
-          for (int k = 0; k < kListRegs; ++k) {
-            if (b + k * 2 * kWave >= nlp) break;
-            test2(Lb[k], b + 2 * (lane + k * kWave));
-          }
+          for (int q = 0; q + 1 < kListRegs; ++q) R[q] = R[q + 1];
         }
       }
       if (nq > head) score(nq - head);
       tb = tb_n; x = xn; y = yn; z = zn;
     }
+    }  // list passes
   }
   __syncthreads();
   for (int j = threadIdx.x; j < D; j += kPrBS) {
@@ -633,6 +651,14 @@ float prune_margin(float cthr, const float amax[3]) {
   return f;
 }
 
+int prune_kernel() {
+  static const int k = [] {
+    const char* e = std::getenv("DLG_PRUNE_KERNEL");
+    return e ? std::atoi(e) : 2;
+  }();
+  return k;
+}
+
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
                          const float* band, int D, float cthr, float margin, const float amax[3],
                          int32_t* counts, uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
@@ -648,10 +674,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
   const int64_t items = (sp_tiles(v.n) + kPrChunk - 1) / kPrChunk;
   constexpr int64_t kMaxItemsPerWave = 65535 / (kPrWaves * kPrChunk * kTileP);
   static_assert(kMaxItemsPerWave >= 1, "16-bit counters");
-  static const int kern = [] {
-    const char* e = std::getenv("DLG_PRUNE_KERNEL");
-    return e ? std::atoi(e) : 2;
-  }();
+  const int kern = prune_kernel();
   static const int occ = [] {
     const char* e = std::getenv("DLG_PRUNE_OCC");
     return e ? std::atoi(e) : 4;
@@ -661,10 +684,13 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
   const int64_t g_cnt = (items + kPrWaves * kMaxItemsPerWave - 1) / (kPrWaves * kMaxItemsPerWave);
   const unsigned gb = (unsigned)std::max<int64_t>(1, std::max(g_fill, g_cnt));
   if (kern == 2) {
-    if (!band) {}  // (the register-list kernel derives its band from the coefficients)
-    hipLaunchKernelGGL(k_score_tiles_rl, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
-                       v.tiles, lp, ls, lp_n, hyps, D, cthr, margin, amax[0], amax[1], amax[2],
-                       counts, stats);
+    static const int exp = [] {
+      const char* e = std::getenv("DLG_PRUNE_EXP");  // timing experiments only (wrong counts)
+      return e ? std::atoi(e) : 0;
+    }();
+    auto* kfn = exp == 1 ? k_score_tiles_rl<1> : exp == 2 ? k_score_tiles_rl<2> : k_score_tiles_rl<0>;
+    hipLaunchKernelGGL(kfn, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls,
+                       lp_n, hyps, D, cthr, margin, amax[0], amax[1], amax[2], counts, stats);
   } else if (occ == 8) {
     hipLaunchKernelGGL(k_score_tiles_o8, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
                        v.tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);

@@ -62,6 +62,8 @@ float prune_margin(float cthr, const float amax[3]);
 // scratch of sp_supers(n) * prune_list_stride(D) uint16 and sp_supers(n) int32 (per super-tile plane lists).
 // list stride per super-tile (D rounded up to 64 entries: dword-aligned entry pairs)
 inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
+// which pruned scoring kernel runs (DLG_PRUNE_KERNEL); only kernel 1 reads bcol / band
+int prune_kernel();
 // amax: the cloud's per-axis max |coordinate| (the scoring band's S bound).  DLG_PRUNE_KERNEL=1
 // selects the first version (k_score_tiles: global B columns, list read per tile), default 2.
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,

@@ -41,6 +41,10 @@ for s in $STEPS; do
     ptest)  run ptest 600 python3 -u -m pytest tests/test_pruned.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     abk)    DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=1 VARIANTS=20,19 run abk1 300 python3 tools/score_ab.py 10000000 4096 5 && \
             DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=2 VARIANTS=20,19 run abk2 300 python3 tools/score_ab.py 10000000 4096 5 ;;
+    ldspmc) VARIANTS=20 run ldspmc 300 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/ldspmc -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
+    expm)   for kk in 2; do for ee in 0 1 2; do
+              DLG_PRUNE_KERNEL=$kk DLG_PRUNE_EXP=$ee SCORE_AB_NOCHECK=1 VARIANTS=20 run expm_k${kk}_e${ee} 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3
+            done; done ;;
     ab)     run score_ab 600 python3 tools/score_ab.py ;;
     list)   run counters 120 rocprofv3 -L ;;
     sqpmc)  VARIANTS="${VARIANTS:-0,2}" run sqpmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \
