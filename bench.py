@@ -169,9 +169,13 @@ def main():
     tests = scored = launches = 0
     score_ms = select_ms = 0.0
     planes = []
+    inliers_local = 0  # this rank's inliers over the timed steps
     t0 = time.perf_counter()
+    step_ms = []
     for _ in range(a.steps):
+        ts = time.perf_counter()
         e = step()
+        step_ms.append((time.perf_counter() - ts) * 1e3)
         s = e["stats"]
         tests += s["tests"]
         scored += s["tests_scored"]
@@ -179,6 +183,7 @@ def main():
         score_ms += s["score_ms"]
         select_ms += s["select_ms"]
         planes.append(e["n_planes"])
+        inliers_local += int(e["offsets"][-1])
     ctx.synchronize()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
@@ -225,11 +230,29 @@ def main():
         "note": "north-star definition: tests/s against the HBM roofline of streaming each "
                 "active point (12 B) once per 4096-hypothesis launch, i.e. achieved = algorithmic "
                 "bytes (12 B x active points + 36 B x hypotheses per launch) / kernel time vs "
-                "8 TB/s; frac = tests/s / hbm_roofline_tests_per_s.  Kernel time from HIP events "
-                "on the library's stream.  valu_view restates the same tests as PCL's 7 f32 ops "
-                "each (the pruned kernel evaluates only the (tile, plane) pairs its bounding "
-                "spheres cannot rule out, so this exceeds the VALU peak)",
+                "8 TB/s; frac = tests/s / hbm_roofline_tests_per_s.  At 4096 hypotheses per "
+                "pass the launch is not memory-bound (2.7e15 tests/s HBM roof); it is issue/"
+                "latency-bound on the (tile, plane) pairs the bounding spheres cannot rule out "
+                "(DESIGN.md sec. 5).  Kernel time from HIP events on the library's stream.  "
+                "valu_view restates the same tests as PCL's 7 f32 ops each (exceeds the VALU "
+                "peak because the pruned kernel skips the pairs it rules out).  "
+                "memory_bound_passes: the H_pass = 1 passes of each round against HBM",
     }
+    # the memory-bound passes of a round (H_pass = 1): fast refit moments (12 B/pt), then
+    # selectWithinDistance + compaction of the list-ordered SoA and of the Morton copy (each: a
+    # 12 B/pt count pass, a 16 B/pt read + 16 B/survivor write scatter; 4 B per inlier id);
+    # timed with HIP events around the phase (incl. the small reduce/refit kernels between)
+    sum_active = per_rank_tests / max(a.hyps, 1)  # sum over rounds of this rank's active points
+    n_copies = 2 if pruned else 1
+    sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))
+                 + 4.0 * inliers_local)
+    sel_gbs = sel_bytes / (select_ms / 1e3) / 1e9 if select_ms > 0 else 0.0
+    roofline["memory_bound_passes"] = {
+        "phase": "refit moments + selectWithinDistance + compaction (%s)"
+                 % ("list-ordered SoA and Morton copy" if pruned else "list-ordered SoA"),
+        "bound": "hbm", "achieved": round(sel_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(sel_gbs / HBM_PEAK_GBS, 4), "bytes_per_step": round(sel_bytes / a.steps),
+        "ms_per_step": round(select_ms / a.steps, 3)}
     traffic_file = os.path.join(ROOT, "profiles", "score_traffic.json")
     if os.path.exists(traffic_file):
         try:
@@ -274,6 +297,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "secondary": secondary,
+            "step_ms": [round(x, 2) for x in step_ms],  # this rank's host time per step
             "tests_per_step": tests // max(a.steps, 1),
             "tests_scored_per_step": scored // max(a.steps, 1),
             "score_ms_per_step_max_rank": round(score_ms_max / a.steps, 3),

@@ -152,6 +152,15 @@ int prune_mode() {
 }
 
 // Morton-ordered copy of the pristine cloud's finite points + its bounding spheres
+// speculative device pick for probability-1 rounds (segment_impl); DLG_SPEC_PICK=0 disables
+bool spec_pick_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLG_SPEC_PICK");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
   const int64_t n = cl->n_total;
   DevBuf<uint32_t> k0, k1;
@@ -239,7 +248,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   mt.normal_plane = np ? 1 : 0;
   mt.thr = prm.threshold;
   mt.lambda = prm.normal_distance_weight;
-  RansacControl ctl(prm, N, cap_h);
+  const double t_ctl0 = trace_on() ? now_ms() : 0.0;
+  RansacControl ctl(prm, N, cap_h, &c->replay);
+  if (trace_on()) std::fprintf(stderr, "[dlg] segment start %.3fms ctl %.3fms\n", t_ctl0 - c->t_tot, now_ms() - t_ctl0);
   // pruned scoring over the spatial copy (plane model, default kernel, spatial copy in step)
   const bool pruned = !np && cl->sp_valid && score_variant() == kScoreDefault && prune_mode() != 0;
   const float pmargin = pruned ? prune_margin(cthr, cl->amax) : 0.0f;
@@ -251,8 +262,22 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   float4* rc_dev = c->small.p + 5;
   const float4* bc_dev = c->small.p;
   int launches = 0;
+  // Speculative pick (probability 1, fast refit): the first batch holds all max_iterations + 1
+  // draws, so k_pick_p1 can take computeModel's decision on the device and the refit + select
+  // follow without a host round trip (one sync per round).  The counts still come back with
+  // that sync and the host replays them (RansacControl::consume); on any disagreement, or when
+  // the loop needs more draws (bad samples), the round continues on the exact host path.
+  const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
+  const bool spec = spec_pick_enabled() && !pcl_refit && prm.probability == 1.0 &&
+                    prm.max_iterations >= 0 && (int64_t)prm.max_iterations + 1 <= cap_h;
+  c->pick.ensure(4);
+  c->h_pick.ensure(4);
+  int spec_D = 0, spec_Dp = 0;
+  bool spec_pending = false;
 
-  while (!ctl.done()) {
+  // one batch of draws: replay, gather, build, score; then either the host replay (sync) or,
+  // for the first batch of a speculative round, the device pick
+  auto one_batch = [&](bool speculate) {
     const int D = ctl.next_size();
     // ---- host: drawIndexSample over positions
     const double t_draw0 = trace_on() ? now_ms() : 0.0;
@@ -290,16 +315,32 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
     c->h_res.ensure((size_t)Dp + D);
+    ++launches;
+    st->tests_scored += (int64_t)D * N;
+    if (speculate) {
+      // (the counts and the pick come back with the round's totals: a copy here would sit
+      // between the scoring and the pick on the stream)
+      launch_pick_p1(c->res.p, Dp, D, prm.max_iterations + 1, c->hyps.p, c->samples.p, best_dev,
+                     best_smp_dev, c->pick.p, c->stream);
+      HIPCHK(hipGetLastError());
+      spec_pending = true;
+      spec_D = D;
+      spec_Dp = Dp;
+      drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
+      if (trace_on())
+        std::fprintf(stderr, "[dlg] N=%lld D=%d totals->draw=%.3fms draw=%.3fms (speculative pick)\n",
+                     (long long)N, D, c->t_tot > 0 ? t_draw0 - c->t_tot : 0.0, t_draw1 - t_draw0);
+      return;
+    }
     HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 4 * ((size_t)Dp + D), hipMemcpyDeviceToHost, c->stream));
+    const double t_launch = trace_on() ? now_ms() : 0.0;
     drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
     sync(c);
     if (trace_on())
-      std::fprintf(stderr, "[dlg] N=%lld D=%d draw=%.3fms score+wait=%.3fms\n", (long long)N, D,
-                   t_draw1 - t_draw0, now_ms() - t_draw1);
-    ++launches;
-    st->tests_scored += (int64_t)D * N;
+      std::fprintf(stderr, "[dlg] N=%lld D=%d totals->draw=%.3fms draw=%.3fms launch=%.3fms score+wait=%.3fms\n",
+                   (long long)N, D, c->t_tot > 0 ? t_draw0 - c->t_tot : 0.0, t_draw1 - t_draw0,
+                   t_launch - t_draw1, now_ms() - t_launch);
     if (c->profiling) st->score_ms += event_ms(c, 0, 1);
-
     // ---- host: computeModel replay over the batch
     const int best_d = ctl.consume(c->h_res.p, c->h_res.p + Dp, D);
     if (best_d >= 0) {  // keep the winner on the device (the next batch overwrites hyps)
@@ -308,29 +349,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       HIPCHK(hipMemcpyAsync(best_smp_dev, c->samples.p + 3 * best_d, 3 * sizeof(SampleRec),
                             hipMemcpyDeviceToDevice, c->stream));
     }
-  }
-  const int iterations = ctl.iterations();
-  const bool have = ctl.have_model();
-  const int best = ctl.best_count();
-  st->draws = ctl.draws();
-  st->tests = ctl.tests();
-  st->iterations = iterations;
-  st->launches = launches;
-  if (xs) {
-    xs->tests += st->tests;
-    xs->tests_scored += st->tests_scored;
-    xs->score_launches += launches;
-    xs->score_ms += st->score_ms;
-  }
-  if (!have) return out;
+  };
 
-  st->has_model = 1;
-  st->n_unrefined = best;
-
-  // Refit + final select.  Fast mode (and no optimisation) never leave the device: moments of
-  // the unrefined plane's inliers (k_moments, centred on the winning sample), the double eigen33
-  // refit in a one-thread kernel, then the select with the refined plane read from device memory;
-  // one D2H + sync at the end.  PCL mode needs the host's sequential float sums in between.
+  // refit + final select (+ compaction of both copies, sphere bounds of the survivors); ends
+  // with the round's sync
   const double t_ref0 = trace_on() ? now_ms() : 0.0;
   const int nt = select_tiles(src.n);
   c->tile_in.ensure(nt + 1);
@@ -348,74 +370,128 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (src.nrm) sp.ensure_nrm((size_t)std::max<int64_t>(src.n, 1));
     dst = sp.out();
   }
-  if (c->profiling) HIPCHK(hipEventRecord(c->ev[2], c->stream));
-  const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
-  if (!pcl_refit) {
-    if (prm.optimize) {
-      const int nb = moments_blocks(src.n);
-      c->partials.ensure((size_t)nb * kMomentK);
-      launch_moments(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p, c->stream);
-      if (c->comm->world() > 1)
-        c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
-    }
-    launch_refit_moments(c->moments.p, best_smp_dev, bc_dev, prm.optimize, rc_dev, c->stream);
-  } else {
-    // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
-    c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
-    launch_select(src, bc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
-                  c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
-    HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 5 * sizeof(float4), hipMemcpyDeviceToHost,
-                          c->stream));
-    sync(c);
-    const HypRec* bh = reinterpret_cast<const HypRec*>(c->h_small.p);
-    const float bc[4] = {bh->a, bh->b, bh->c, bh->d};
-    std::vector<int32_t> xyz_bits;
-    gather_lists(c, reinterpret_cast<const int32_t*>(c->inl_xyz.p), c->h_tot.p[0], 3, &xyz_bits);
-    float rc[4];
-    refit_pcl_float(reinterpret_cast<const float*>(xyz_bits.data()), (int64_t)xyz_bits.size() / 3,
-                    bc, rc);
-    c->h_small.p[5] = make_float4(rc[0], rc[1], rc[2], rc[3]);
-    HIPCHK(hipMemcpyAsync(rc_dev, c->h_small.p + 5, sizeof(float4), hipMemcpyHostToDevice,
-                          c->stream));
-  }
-  // final selectWithinDistance with the refined model (+ compaction of the survivors)
-  launch_select(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
-                c->inl_gid.p, nullptr, compact ? &dst : nullptr, c->stream);
-  // the spatial copy loses the same points (same predicate, same float inputs)
   const bool sp_compact = compact && !np && cl->sp_valid;
-  if (sp_compact) {
-    SoA& sd = cl->sp_buf[cl->sp_spare()];
-    sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
-    const PointsOut spo = sd.out();
-    const SoA& ss = cl->sp_soa();
-    const PointsView spv{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n, nullptr};
-    launch_select(spv, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
-                  c->totals.p + 2, nullptr, nullptr, &spo, c->stream);
-  }
-  HIPCHK(hipGetLastError());
-  if (c->profiling) HIPCHK(hipEventRecord(c->ev[3], c->stream));
-  HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, sp_compact ? 16 : 8, hipMemcpyDeviceToHost,
-                        c->stream));
-  HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 6 * sizeof(float4), hipMemcpyDeviceToHost,
-                        c->stream));
-  if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(c->ev_tot, c->stream));
-  if (sp_compact) {
-    // sphere bounds of the survivors, queued behind the totals copy: they run while the host
-    // reads the totals and draws the next round.  Into the spare buffer's own bound arrays
-    // (sized for the current count, an upper bound; the kernel reads the survivor count from
-    // totals[3]), so a round whose plane is rejected leaves the current bounds intact.
-    const int b = cl->sp_spare();
-    cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
-    cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
-    const SoA& sd = cl->sp_buf[b];
-    launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 3, cl->sp_tb[b].p,
-                         cl->sp_sb[b].p, c->stream);
+  auto refit_select = [&]() {
+    // Fast mode (and no optimisation) never leave the device: moments of the unrefined plane's
+    // inliers (k_moments, centred on the winning sample), the double eigen33 refit in a
+    // one-thread kernel, then the select with the refined plane read from device memory.  PCL
+    // mode needs the host's sequential float sums in between.
+    if (c->profiling) HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    if (!pcl_refit) {
+      if (prm.optimize) {
+        const int nb = moments_blocks(src.n);
+        c->partials.ensure((size_t)nb * kMomentK);
+        launch_moments(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p, c->stream);
+        if (c->comm->world() > 1)
+          c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
+      }
+      launch_refit_moments(c->moments.p, best_smp_dev, bc_dev, prm.optimize, rc_dev, c->stream);
+    } else {
+      // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
+      c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
+      launch_select(src, bc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
+                    c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
+      HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 5 * sizeof(float4), hipMemcpyDeviceToHost,
+                            c->stream));
+      sync(c);
+      const HypRec* bh = reinterpret_cast<const HypRec*>(c->h_small.p);
+      const float bc[4] = {bh->a, bh->b, bh->c, bh->d};
+      std::vector<int32_t> xyz_bits;
+      gather_lists(c, reinterpret_cast<const int32_t*>(c->inl_xyz.p), c->h_tot.p[0], 3, &xyz_bits);
+      float rc[4];
+      refit_pcl_float(reinterpret_cast<const float*>(xyz_bits.data()), (int64_t)xyz_bits.size() / 3,
+                      bc, rc);
+      c->h_small.p[5] = make_float4(rc[0], rc[1], rc[2], rc[3]);
+      HIPCHK(hipMemcpyAsync(rc_dev, c->h_small.p + 5, sizeof(float4), hipMemcpyHostToDevice,
+                            c->stream));
+    }
+    // final selectWithinDistance with the refined model (+ compaction of the survivors)
+    launch_select(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
+                  c->inl_gid.p, nullptr, compact ? &dst : nullptr, c->stream);
+    // the spatial copy loses the same points (same predicate, same float inputs)
+    if (sp_compact) {
+      SoA& sd = cl->sp_buf[cl->sp_spare()];
+      sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
+      const PointsOut spo = sd.out();
+      const SoA& ss = cl->sp_soa();
+      const PointsView spv{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n, nullptr};
+      launch_select(spv, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
+                    c->totals.p + 2, nullptr, nullptr, &spo, c->stream);
+    }
     HIPCHK(hipGetLastError());
+    if (c->profiling) HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, sp_compact ? 16 : 8, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 6 * sizeof(float4), hipMemcpyDeviceToHost,
+                          c->stream));
+    if (spec_pending) {  // the speculative round's counts and pick, for the host replay
+      spec_pending = false;
+      HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 4 * ((size_t)spec_Dp + spec_D),
+                            hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipMemcpyAsync(c->h_pick.p, c->pick.p, 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ev_tot, c->stream));
+    if (sp_compact) {
+      // sphere bounds of the survivors, queued behind the totals copy: they run while the host
+      // reads the totals and draws the next round.  Into the spare buffer's own bound arrays
+      // (sized for the current count, an upper bound; the kernel reads the survivor count from
+      // totals[3]), so a round whose plane is rejected leaves the current bounds intact.
+      const int b = cl->sp_spare();
+      cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+      cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+      const SoA& sd = cl->sp_buf[b];
+      launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 3, cl->sp_tb[b].p,
+                           cl->sp_sb[b].p, c->stream);
+      HIPCHK(hipGetLastError());
+    }
+    wait_event(c->ev_tot);
+    if (trace_on()) c->t_tot = now_ms();
+    if (c->profiling && xs) xs->select_ms += event_ms(c, 2, 3);
+  };
+
+  bool selected = false;
+  if (spec && !ctl.done()) {
+    one_batch(true);
+    refit_select();  // on the device's pick
+    selected = true;
+    // the exact host replay of the same counts
+    if (c->profiling) st->score_ms += event_ms(c, 0, 1);
+    const int best_d = ctl.consume(c->h_res.p, c->h_res.p + spec_Dp, spec_D);
+    if (!(ctl.done() && best_d == c->h_pick.p[0] && c->h_pick.p[1] == 1)) {
+      ++c->spec_misses;
+      if (trace_on())
+        std::fprintf(stderr, "[dlg] speculative pick overturned: host %d done %d, device %d complete %d\n",
+                     best_d, ctl.done() ? 1 : 0, c->h_pick.p[0], c->h_pick.p[1]);
+      selected = false;
+      if (best_d >= 0) {
+        HIPCHK(hipMemcpyAsync(best_dev, c->hyps.p + best_d, sizeof(HypRec), hipMemcpyDeviceToDevice,
+                              c->stream));
+        HIPCHK(hipMemcpyAsync(best_smp_dev, c->samples.p + 3 * best_d, 3 * sizeof(SampleRec),
+                              hipMemcpyDeviceToDevice, c->stream));
+      }
+    }
   }
-  HIPCHK(hipEventSynchronize(c->ev_tot));
-  if (c->profiling && xs) xs->select_ms += event_ms(c, 2, 3);
+  while (!ctl.done()) one_batch(false);
+  const int iterations = ctl.iterations();
+  const bool have = ctl.have_model();
+  const int best = ctl.best_count();
+  st->draws = ctl.draws();
+  st->tests = ctl.tests();
+  st->iterations = iterations;
+  st->launches = launches;
+  if (xs) {
+    xs->tests += st->tests;
+    xs->tests_scored += st->tests_scored;
+    xs->score_launches += launches;
+    xs->score_ms += st->score_ms;
+  }
+  if (!have) return out;
+
+  st->has_model = 1;
+  st->n_unrefined = best;
+  if (!selected) refit_select();
   const HypRec* bh = reinterpret_cast<const HypRec*>(c->h_small.p);
   const SampleRec* bs = reinterpret_cast<const SampleRec*>(c->h_small.p + 2);
   const float4 rc = c->h_small.p[5];
@@ -456,12 +532,19 @@ int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, in
     throw DlgError(DLG_ERR_CAPACITY, "inlier buffer too small: need " + std::to_string(so.n_in_local));
   if (so.n_in_local) {
     if (deferred) {
+      const double t0 = trace_on() ? now_ms() : 0.0;
       drain_pending(c);
+      const double t1 = trace_on() ? now_ms() : 0.0;
       c->h_stage.ensure((size_t)so.n_in_local);
       if (!c->ev_stage) HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+      const double t2 = trace_on() ? now_ms() : 0.0;
       HIPCHK(hipMemcpyAsync(c->h_stage.p, c->inl_gid.p, (size_t)so.n_in_local * 4,
                             hipMemcpyDeviceToHost, c->stream));
+      const double t3 = trace_on() ? now_ms() : 0.0;
       HIPCHK(hipEventRecord(c->ev_stage, c->stream));
+      if (trace_on())
+        std::fprintf(stderr, "[dlg] emit n=%lld cap=%zu drain %.3f ensure %.3f copy %.3f record %.3f ms\n",
+                     (long long)so.n_in_local, c->h_stage.cap, t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
       c->pending_dst = dst;
       c->pending_n = so.n_in_local;
     } else {
@@ -835,8 +918,12 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       const int64_t n_in = allgather_i64(c, so.n_in_local, &tot);
       if (n_in == 0 || n_in < min_inliers) break;  // plane rejected: active list unchanged
       int64_t g = 0;
+      const double t_e0 = trace_on() ? now_ms() : 0.0;
       int64_t n = emit_inliers(c, so, prm->gather_inliers != 0, inliers_out + written,
                                cap - written, &g, /*deferred=*/true);
+      if (trace_on())
+        std::fprintf(stderr, "[dlg] after-round: segment-return %.3fms emit %.3fms\n",
+                     t_e0 - c->t_tot, now_ms() - t_e0);
       std::memcpy(coeffs_out + 4 * p, so.coeff, sizeof(so.coeff));
       written += n;
       offsets_out[p + 1] = written;
@@ -852,6 +939,10 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       }
     }
     drain_pending(c);
+    // A stream synchronisation lets the HIP runtime reclaim the per-command resources of the
+    // rounds: with event waits alone they pile up until a D2H copy blocks the host for ~10 ms
+    // (measured: every ~55 rounds).  The stream only holds the last sphere bounds here.
+    sync(c);
   });
   c->pending_dst = nullptr;  // (error path: never write into the caller's buffer later)
   c->pending_n = 0;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -14,6 +15,7 @@
 #include "../../include/dialog_ransac.h"
 #include "comm.hpp"
 #include "kernels.hpp"
+#include "sac_control.hpp"
 #include "postprocess.hpp"
 
 namespace dlg {
@@ -179,7 +181,12 @@ struct dlg_ctx {
   // kernel executes (the host would otherwise only wait for it)
   PinBuf<int32_t> h_stage;
   hipEvent_t ev_stage = nullptr;
-  hipEvent_t ev_tot = nullptr;  // end of a round's totals D2H (work queued after it may still run)
+  hipEvent_t ev_tot = nullptr;
+  DevBuf<int32_t> pick;   // k_pick_p1 result
+  PinBuf<int32_t> h_pick;
+  int64_t spec_misses = 0;  // speculative picks the host replay overturned
+  double t_tot = 0.0;    // (DLG_TRACE) host time the last round's totals arrived
+  ShuffleReplay replay;  // drawIndexSample replay table, reused by every segment on this context  // end of a round's totals D2H (work queued after it may still run)
   int32_t* pending_dst = nullptr;
   int64_t pending_n = 0;
   NormalsWork nw;
@@ -219,6 +226,29 @@ namespace dlg {
 
 inline void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
 inline void sync(dlg_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); }
+
+// wait for an event of the per-round loop.  DLG_WAIT_MODE: 0 hipEventSynchronize, 1 poll with
+// a pause back-off (no sleep: a blocking wait that outlasts the runtime's spin phase sleeps and
+// the wake-up adds tens of microseconds to a round)
+inline int wait_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("DLG_WAIT_MODE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return m;
+}
+inline void wait_event(hipEvent_t ev) {
+  if (wait_mode() != 1) {
+    HIPCHK(hipEventSynchronize(ev));
+    return;
+  }
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIPCHK(e);
+    for (int i = 0; i < 256; ++i) __builtin_ia32_pause();
+  }
+}
 
 inline dlg_status fail(dlg_ctx* c, dlg_status code, const std::string& msg) {
   if (c) c->err = msg;

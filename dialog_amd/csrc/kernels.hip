@@ -943,6 +943,93 @@ __global__ void k_refit_moments(const double* __restrict__ mom, const SampleRec*
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_pick_p1: RandomSampleConsensus::computeModel's decision over one batch of draws when the
+// probability is 1 (log(1 - p) = -inf, so k = +inf and only the iteration cap ends the loop):
+// the loop ends at the need_good-th good draw (need_good = max_iterations + 1) and keeps the
+// first good draw with the largest count (strict '>').  A bad draw only consumes a getSamples
+// try; with fewer than 1000 bad draws in the batch no run of 1000 can end the loop early.
+// out[0] = batch index of the best draw (-1: none), out[1] = 1 if the loop ended inside the
+// batch.  The winner's HypRec and samples are copied to best / best_smp.  Speculative: the host
+// replays the same counts (RansacControl::consume) after the round's sync and redoes the round
+// on any disagreement.  One workgroup.
+constexpr int kPickBS = 1024;
+__global__ __launch_bounds__(kPickBS) void k_pick_p1(const int32_t* __restrict__ res, int Dp, int D,
+                                                     int need_good, const HypRec* __restrict__ hyps,
+                                                     const SampleRec* __restrict__ samples,
+                                                     HypRec* __restrict__ best,
+                                                     SampleRec* __restrict__ best_smp,
+                                                     int32_t* __restrict__ out) {
+  __shared__ int s_good[kPickBS / kWave], s_bad[kPickBS / kWave];
+  __shared__ unsigned long long s_key[kPickBS / kWave];
+  __shared__ int s_end;
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const int per = (D + kPickBS - 1) / kPickBS;
+  const int d0 = min(D, t * per), d1 = min(D, d0 + per);
+  int g = 0, b = 0;
+  for (int d = d0; d < d1; ++d) {
+    if (res[Dp + d]) ++g; else ++b;
+  }
+  // block exclusive scan of the good counts (wave scans + wave totals)
+  int incl = g;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  int bt = b;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) bt += __shfl_xor(bt, o);
+  if (lane == kWave - 1) s_good[w] = incl;
+  if (lane == 0) s_bad[w] = bt;
+  if (t == 0) s_end = -1;
+  __syncthreads();
+  int base = 0, total_good = 0, total_bad = 0;
+  for (int q = 0; q < kPickBS / kWave; ++q) {
+    base += q < w ? s_good[q] : 0;
+    total_good += s_good[q];
+    total_bad += s_bad[q];
+  }
+  base += incl - g;
+  // the draw at which the need_good-th good draw happens
+  if (base < need_good && base + g >= need_good) {
+    int c = base;
+    for (int d = d0; d < d1; ++d)
+      if (res[Dp + d] && ++c == need_good) { s_end = d; break; }
+  }
+  __syncthreads();
+  const int end = s_end;  // -1: the loop goes on past this batch
+  // first maximum over the good draws up to the end: key = (count, ~index)
+  unsigned long long key = 0ull;
+  for (int d = d0; d < d1; ++d) {
+    if (end >= 0 && d > end) break;
+    if (!res[Dp + d]) continue;
+    const unsigned long long k = ((unsigned long long)(uint32_t)res[d] << 32) |
+                                 (unsigned long long)(0xFFFFFFFFu - (uint32_t)d);
+    key = k > key ? k : key;
+  }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const unsigned long long v = __shfl_xor(key, o);
+    key = v > key ? v : key;
+  }
+  if (lane == 0) s_key[w] = key;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long k = 0ull;
+    for (int q = 0; q < kPickBS / kWave; ++q) k = s_key[q] > k ? s_key[q] : k;
+    const int bd = k ? (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : -1;
+    out[0] = bd;
+    out[1] = (end >= 0 && total_bad < 1000 && total_good >= need_good) ? 1 : 0;
+    if (bd >= 0) {
+      *best = hyps[bd];
+      best_smp[0] = samples[3 * bd];
+      best_smp[1] = samples[3 * bd + 1];
+      best_smp[2] = samples[3 * bd + 2];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // select / compact (selectWithinDistance + removal of the inliers from the active list)
 constexpr int kSelBS = 256;
 constexpr int kSelIt = kSelTile / kSelBS;
@@ -1441,6 +1528,13 @@ void launch_moments(PointsView src, const float4* coef, const ModelTest& mt,
     hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
                        partials);
   hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kMomentK * kWave), 0, s, partials, nblocks, out);
+}
+
+void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
+                    const SampleRec* samples, HypRec* best, SampleRec* best_smp, int32_t* out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_pick_p1, dim3(1), dim3(kPickBS), 0, s, res, Dp, D, need_good, hyps, samples,
+                     best, best_smp, out);
 }
 
 int select_tiles(int64_t n) { return (int)((n + kSelTile - 1) / kSelTile); }

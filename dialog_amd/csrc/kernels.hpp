@@ -100,6 +100,11 @@ int score_variant();
 void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
                            hipStream_t s);
 // writes hyps[D] and good[D] (int32 flags next to the counts for one D2H copy)
+// speculative computeModel decision for probability 1 over one batch (k_pick_p1): out[0] best
+// batch index (-1 none), out[1] loop ended inside the batch; winner copied to best / best_smp
+void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
+                    const SampleRec* samples, HypRec* best, SampleRec* best_smp, int32_t* out,
+                    hipStream_t s);
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,
                        HypRec* hyps, int32_t* good, hipStream_t s);
 // counts[D] = #{i < n : |plane_h . (x_i, y_i, z_i, 1)| < cthr}, PCL (Eigen SSE) op order.

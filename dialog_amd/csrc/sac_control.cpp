@@ -14,30 +14,62 @@ namespace dlg {
 
 void Overlay::reset(size_t expect) {
   size_t cap = 64;
-  while (cap < expect * 2) cap <<= 1;
-  keys_.assign(cap, -1);
-  vals_.assign(cap, 0);
-  mask_ = cap - 1;
+  while (cap < expect * 4) cap <<= 1;
+  if (slots_.size() < cap || ++gen_ == 0) {  // (a wrapped generation counter clears the table)
+    slots_.assign(std::max(cap, slots_.size()), Slot{0, 0, 0});
+    gen_ = 1;
+  }
+  mask_ = slots_.size() - 1;
   size_ = 0;
 }
 
 void Overlay::grow() {
-  std::vector<int32_t> ok = std::move(keys_), ov = std::move(vals_);
-  keys_.assign(ok.size() * 2, -1);
-  vals_.assign(ok.size() * 2, 0);
-  mask_ = keys_.size() - 1;
+  std::vector<Slot> old;
+  old.swap(slots_);
+  const uint32_t g = gen_;
+  slots_.assign(old.size() * 2, Slot{0, 0, 0});
+  gen_ = 1;
+  mask_ = slots_.size() - 1;
   size_ = 0;
-  for (size_t t = 0; t < ok.size(); ++t)
-    if (ok[t] != -1) set(ok[t], ov[t]);
+  for (const Slot& s : old)
+    if (s.gen == g) (void)exchange(s.key, s.val);
 }
 
-RansacControl::RansacControl(const dlg_sac_params& prm, int64_t N, int cap_h)
-    : prm_(prm), N_(N), cap_h_(std::max(cap_h, 1)), rng_(prm.seed) {
+namespace {
+// the rnd() stream of one seed, generated once per thread and extended on demand: every
+// segment() restarts PCL's generator at the same seed, so successive extraction rounds replay
+// the same prefix
+struct RndCache {
+  uint32_t seed = 0;
+  bool valid = false;
+  Mt19937 gen;
+  std::vector<uint32_t> v;
+  const uint32_t* get(uint32_t s, int64_t upto) {
+    if (!valid || s != seed) {
+      seed = s;
+      valid = true;
+      gen = Mt19937(s);
+      v.clear();
+    }
+    if ((int64_t)v.size() < upto) {
+      v.reserve((size_t)upto);
+      while ((int64_t)v.size() < upto) v.push_back((uint32_t)gen.rnd());
+    }
+    return v.data();
+  }
+};
+thread_local RndCache t_rnd;
+}  // namespace
+
+RansacControl::RansacControl(const dlg_sac_params& prm, int64_t N, int cap_h,
+                             ShuffleReplay* replay)
+    : prm_(prm), N_(N), cap_h_(std::max(cap_h, 1)), seed_(prm.seed),
+      own_(replay ? nullptr : new ShuffleReplay()), ov_(replay ? replay : own_.get()) {
   log_probability_ = std::log(1.0 - prm.probability);
   one_over_indices_ = 1.0 / (double)N;
   // getSamples cannot select 3 unique points -> computeModel fails without an iteration
   if (N < 3) done_ = true;
-  ov_.reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h_) + 16);
+  ov_->reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h_) + 16);
 }
 
 int RansacControl::next_size() const {
@@ -53,14 +85,19 @@ int RansacControl::next_size() const {
 
 int RansacControl::next_batch(int32_t* pos) {
   const int D = next_size();
-  for (int d = 0; d < D; ++d) {
-    for (int i = 0; i < 3; ++i) {
-      const int64_t j = i + (int64_t)((uint64_t)(uint32_t)rng_.rnd() % (uint64_t)(N_ - i));
-      ov_.swap(i, j);
-    }
-    pos[3 * d] = ov_.at(0);
-    pos[3 * d + 1] = ov_.at(1);
-    pos[3 * d + 2] = ov_.at(2);
+  if (D <= 0) return 0;
+  const uint32_t* r = t_rnd.get(seed_, rnd_pos_ + 3 * (int64_t)D) + rnd_pos_;
+  rnd_pos_ += 3 * (int64_t)D;
+  // rnd() % (N - i): rnd() < 2^31 and N <= INT32_MAX, so 32-bit remainders are exact
+  const FastMod32 m0((uint32_t)N_), m1((uint32_t)(N_ - 1)), m2((uint32_t)(N_ - 2));
+  ShuffleReplay& ov = *ov_;
+  for (int d = 0; d < D; ++d, r += 3) {
+    ov.swap(0, (int64_t)m0.mod(r[0]));
+    ov.swap(1, 1 + (int64_t)m1.mod(r[1]));
+    ov.swap(2, 2 + (int64_t)m2.mod(r[2]));
+    pos[3 * d] = ov.at(0);
+    pos[3 * d + 1] = ov.at(1);
+    pos[3 * d + 2] = ov.at(2);
   }
   batch_base_ = drawn_;
   drawn_ += D;

@@ -20,6 +20,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "../../include/dialog_ransac.h"
@@ -27,38 +28,47 @@
 
 namespace dlg {
 
-// sparse overlay of SampleConsensusModel::shuffled_indices_ over list positions: pos -> pos'
+// sparse overlay of SampleConsensusModel::shuffled_indices_ over list positions: pos -> pos'.
+// Open addressing with interleaved (key, value, generation) slots; reset() bumps the
+// generation instead of clearing, so a table reused across segments costs nothing to reset.
 class Overlay {
  public:
   void reset(size_t expect);
-  int32_t get(int32_t k) const {
+  // returns the value at k (k itself when absent) and stores v there: one probe sequence
+  int32_t exchange(int32_t k, int32_t v) {
     size_t h = hash(k) & mask_;
-    while (keys_[h] != -1) {
-      if (keys_[h] == k) return vals_[h];
+    for (;;) {
+      Slot& s = slots_[h];
+      if (s.gen != gen_) {  // empty in this generation: insert
+        s.gen = gen_;
+        s.key = k;
+        s.val = v;
+        if (++size_ * 4 > slots_.size()) grow();
+        return k;
+      }
+      if (s.key == k) {
+        const int32_t old = s.val;
+        s.val = v;
+        return old;
+      }
       h = (h + 1) & mask_;
     }
-    return k;
-  }
-  void set(int32_t k, int32_t v) {
-    if ((size_ + 1) * 2 > keys_.size()) grow();
-    size_t h = hash(k) & mask_;
-    while (keys_[h] != -1 && keys_[h] != k) h = (h + 1) & mask_;
-    if (keys_[h] == -1) {
-      keys_[h] = k;
-      ++size_;
-    }
-    vals_[h] = v;
   }
 
  private:
+  struct Slot {
+    int32_t key, val;
+    uint32_t gen;
+  };
   static size_t hash(int32_t k) { return (size_t)((uint32_t)k * 2654435761u); }
   void grow();
-  std::vector<int32_t> keys_, vals_;
+  std::vector<Slot> slots_;
   size_t mask_ = 0, size_ = 0;
+  uint32_t gen_ = 0;
 };
 
 // drawIndexSample's swaps over list positions: positions 0..2 (touched by every draw) live in
-// registers, the random partners >= 3 in the overlay -- one hash lookup and one insert per swap
+// registers, the random partners >= 3 in the overlay -- one probe sequence per swap
 class ShuffleReplay {
  public:
   void reset(size_t expect) {
@@ -72,9 +82,7 @@ class ShuffleReplay {
       head_[j] = t;
       return;
     }
-    const int32_t vj = tail_.get((int32_t)j);
-    tail_.set((int32_t)j, head_[i]);
-    head_[i] = vj;
+    head_[i] = tail_.exchange((int32_t)j, head_[i]);
   }
   int32_t at(int i) const { return head_[i]; }
 
@@ -83,10 +91,26 @@ class ShuffleReplay {
   Overlay tail_;
 };
 
+// x mod d for 32-bit x and a fixed 32-bit d >= 1 without a division (Lemire, Kaser & Kurz,
+// "Faster remainder by direct computation", 2019): exact for every 32-bit x
+class FastMod32 {
+ public:
+  explicit FastMod32(uint32_t d = 1) : d_(d), m_(UINT64_C(0xFFFFFFFFFFFFFFFF) / d + 1) {}
+  uint32_t mod(uint32_t x) const {
+    const uint64_t low = m_ * x;
+    return (uint32_t)(((__uint128_t)low * d_) >> 64);
+  }
+
+ private:
+  uint32_t d_;
+  uint64_t m_;
+};
+
 class RansacControl {
  public:
-  // N = active points over all ranks; cap_h = largest batch the caller can score at once
-  RansacControl(const dlg_sac_params& prm, int64_t N, int cap_h);
+  // N = active points over all ranks; cap_h = largest batch the caller can score at once;
+  // replay: a table to reuse across segments (the context's; nullptr: the controller owns one)
+  RansacControl(const dlg_sac_params& prm, int64_t N, int cap_h, ShuffleReplay* replay = nullptr);
 
   bool done() const { return done_; }
   // batch size PCL can still use (0 once the loop has ended)
@@ -110,8 +134,10 @@ class RansacControl {
   dlg_sac_params prm_;
   int64_t N_;
   int cap_h_;
-  Mt19937 rng_;
-  ShuffleReplay ov_;
+  uint32_t seed_;
+  int64_t rnd_pos_ = 0;  // rnd() values consumed (the stream restarts at the seed every segment)
+  std::unique_ptr<ShuffleReplay> own_;
+  ShuffleReplay* ov_;
   int iterations_ = 0;
   int best_ = -2147483647;
   double k_ = 1.0;
