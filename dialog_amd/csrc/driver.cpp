@@ -262,14 +262,15 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   float4* rc_dev = c->small.p + 5;
   const float4* bc_dev = c->small.p;
   int launches = 0;
-  // Speculative pick (probability 1, fast refit): the first batch holds all max_iterations + 1
-  // draws, so k_pick_p1 can take computeModel's decision on the device and the refit + select
-  // follow without a host round trip (one sync per round).  The counts still come back with
-  // that sync and the host replays them (RansacControl::consume); on any disagreement, or when
-  // the loop needs more draws (bad samples), the round continues on the exact host path.
+  // Speculative pick (probability 1): the first batch holds all max_iterations + 1 draws, so
+  // k_pick_p1 can take computeModel's decision on the device and the refit + select follow
+  // without a host round trip (one sync per round in fast-refit mode, one less in PCL mode).
+  // The counts still come back with the round's sync and the host replays them
+  // (RansacControl::consume); on any disagreement, or when the loop needs more draws (bad
+  // samples), the round continues on the exact host path and the refit + select are redone.
   const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
-  const bool spec = spec_pick_enabled() && !pcl_refit && prm.probability == 1.0 &&
-                    prm.max_iterations >= 0 && (int64_t)prm.max_iterations + 1 <= cap_h;
+  const bool spec = spec_pick_enabled() && prm.probability == 1.0 && prm.max_iterations >= 0 &&
+                    (int64_t)prm.max_iterations + 1 <= cap_h;
   c->pick.ensure(4);
   c->h_pick.ensure(4);
   int spec_D = 0, spec_Dp = 0;

@@ -69,6 +69,10 @@ RansacControl::RansacControl(const dlg_sac_params& prm, int64_t N, int cap_h,
   one_over_indices_ = 1.0 / (double)N;
   // getSamples cannot select 3 unique points -> computeModel fails without an iteration
   if (N < 3) done_ = true;
+  // while (iterations_ < k && skipped_count < max_skip), max_skip = (unsigned)(max_iterations * 10):
+  // with max_iterations = 0 the loop never runs (no draw, no model).  skipped_count itself stays
+  // 0: computeModelCoefficients repeats isSampleGood's test, which getSamples already passed.
+  if ((uint32_t)((int64_t)prm.max_iterations * 10) == 0u) done_ = true;
   ov_->reset(3 * (size_t)std::min<int64_t>((int64_t)prm.max_iterations + 1, cap_h_) + 16);
 }
 

@@ -90,3 +90,9 @@ def test_control_matches_oracle_single_rank():
         assert list(best) == list(ref["best_sample"])
     ctl = D.RansacControl(D.make_params(0.02), 2)   # < 3 points: no draw, no model
     assert ctl.next().shape[0] == 0 and not ctl.result()["has_model"]
+    # max_iterations = 0: PCL's max_skip = 10 * max_iterations = 0, the loop never runs
+    ctl = D.RansacControl(D.make_params(0.02, max_iterations=0, probability=1.0), 100)
+    ref = O.sac_segment(np.random.default_rng(1).random((100, 3)).astype(np.float32), 0.02,
+                        max_iterations=0, probability=1.0)
+    assert ctl.next().shape[0] == 0 and not ctl.result()["has_model"] and not ref["ok"]
+    assert ref["draws"] == 0

@@ -265,3 +265,36 @@ def test_rccl_one_rank_path(monkeypatch, gpu_ctx):
     ctx.barrier()
     c1.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("mi", [0, 5, 50, 400])
+def test_probability_one_bad_draws(gpu_ctx, mi):
+    """probability = 1 rounds take the speculative device pick (k_pick_p1); with many bad
+    (collinear) draws the batch of max_iterations + 1 draws cannot finish PCL's loop, so the
+    host replay overturns the pick and the round continues on the exact path.  Both must equal
+    the PCL restatement (iterations, draws, best sample, coefficients, inliers)."""
+    rng = np.random.default_rng(77 + mi)
+    t = rng.random(60).astype(np.float32)
+    line = np.stack([t, 2 * t, 4 * t], 1)  # collinear triples: isSampleGood false
+    off = rng.random((12, 3)).astype(np.float32)  # a few points off the line
+    p = np.concatenate([line, off]).astype(np.float32)
+    r = O.sac_segment(p, 0.05, max_iterations=mi, probability=1.0)
+    inl, coeff, st = gpu_segment(gpu_ctx, p, 0.05, max_iterations=mi, probability=1.0)
+    assert_same_as_oracle(inl, coeff, st, r)
+    assert st["draws"] > mi + 1 or not r["ok"]  # bad draws were consumed beyond one batch
+
+
+def test_probability_one_extract_rounds(gpu_ctx):
+    """extract-and-remove with probability 1 (every round speculative) equals the oracle's
+    sequential extraction, with the refined planes and inliers bit-identical."""
+    p, _, _ = plane_cloud(6000, 4, seed=99, outlier_frac=0.2)
+    prm = D.make_params(0.02, max_iterations=255, probability=1.0)
+    cloud = D.Cloud(gpu_ctx, p)
+    try:
+        e = D.extract_planes(cloud, prm, max_planes=5, min_inliers=50)
+    finally:
+        cloud.close()
+    r = O.extract_planes(p, 0.02, max_planes=5, min_inliers=50, max_iterations=255, probability=1.0)
+    assert e["n_planes"] == r["n_planes"]
+    assert np.array_equal(e["coeffs"].view(np.uint32), r["coeffs"].view(np.uint32))
+    assert np.array_equal(e["offsets"], r["offsets"]) and np.array_equal(e["inliers"], r["inliers"])
