@@ -138,6 +138,8 @@ struct SegOut {
   int64_t n_in_global = 0;
   bool sp_compacted = false;  // the spatial copy's survivors are in its spare buffer
   int64_t sp_n_out = 0;
+  // every rank's refined inliers / survivors (device allgather folded into the round's sync)
+  std::vector<int64_t> in_ranks, out_ranks;
 };
 
 // pruned scoring (spatial.hpp): DLG_PRUNE=0 disables it, DLG_PRUNE=1 also builds the spatial
@@ -219,8 +221,11 @@ void ensure_sphere_bounds(dlg_ctx* c, dlg_cloud* cl) {
 }
 
 // one SACSegmentation::segment() over the cloud's active list (all ranks)
+// active_ranks: every rank's active count when the caller already knows it (the extract loop
+// carries it from the previous round's survivors), else allgathered here
 SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool compact,
-                    dlg_sac_stats* st, dlg_extract_stats* xs) {
+                    dlg_sac_stats* st, dlg_extract_stats* xs,
+                    const std::vector<int64_t>* active_ranks = nullptr) {
   SegOut out;
   std::memset(st, 0, sizeof(*st));
   const bool np = prm.model == DLG_SACMODEL_NORMAL_PLANE;
@@ -233,7 +238,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                         ? std::min(prm.hypotheses_per_launch, kMaxHypPerLaunch)
                         : kMaxHypPerLaunch;
   std::vector<int64_t> per_rank;
-  const int64_t N = allgather_i64(c, cl->n_active, &per_rank);
+  int64_t N = 0;
+  if (active_ranks && (int)active_ranks->size() == c->comm->world() &&
+      (*active_ranks)[c->comm->rank()] == cl->n_active) {
+    per_rank = *active_ranks;
+    for (int64_t v : per_rank) N += v;
+  } else {
+    N = allgather_i64(c, cl->n_active, &per_rank);
+  }
   int64_t offset = 0;
   for (int r = 0; r < c->comm->rank(); ++r) offset += per_rank[r];
   st->n_active = N;
@@ -424,6 +436,13 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[3], c->stream));
     HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, sp_compact ? 16 : 8, hipMemcpyDeviceToHost,
                           c->stream));
+    const int W = c->comm->world();
+    if (W > 1) {  // every rank's (in, out): the extract loop needs no host-synced allgather
+      c->rk.ensure(2 * (size_t)W + 2);
+      c->h_rk.ensure(2 * (size_t)W + 2);
+      c->comm->allgather(c->totals.p, c->rk.p, 2, DType::I32, c->stream);
+      HIPCHK(hipMemcpyAsync(c->h_rk.p, c->rk.p, 8 * (size_t)W, hipMemcpyDeviceToHost, c->stream));
+    }
     HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 6 * sizeof(float4), hipMemcpyDeviceToHost,
                           c->stream));
     if (spec_pending) {  // the speculative round's counts and pick, for the host replay
@@ -503,6 +522,19 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   out.has_model = true;
   out.n_in_local = c->h_tot.p[0];
   out.n_out_local = src.n == 0 ? 0 : c->h_tot.p[1];
+  {
+    const int W = c->comm->world();
+    out.in_ranks.assign(W, 0);
+    out.out_ranks.assign(W, 0);
+    for (int r = 0; r < W; ++r) {
+      // (a rank with no active points skips its select kernels: its totals are zero)
+      const bool empty = per_rank[r] == 0;
+      out.in_ranks[r] = W == 1 ? out.n_in_local : (empty ? 0 : c->h_rk.p[2 * r]);
+      out.out_ranks[r] = W == 1 ? out.n_out_local : (empty ? 0 : c->h_rk.p[2 * r + 1]);
+    }
+    out.n_in_global = 0;
+    for (int64_t v : out.in_ranks) out.n_in_global += v;
+  }
   if (sp_compact) {
     out.sp_compacted = true;
     out.sp_n_out = cl->sp_n == 0 ? 0 : c->h_tot.p[3];
@@ -518,7 +550,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
 
 // copy this rank's (or every rank's) refined inliers to the caller buffer
 int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, int64_t cap,
-                     int64_t* global_count, bool deferred = false) {
+                     int64_t* global_count, bool deferred = false, bool counts_known = false) {
   if (gather && c->comm->world() > 1) {
     gather_lists(c, c->inl_gid.p, so.n_in_local, 1, &c->h_inl);
     int64_t n = (int64_t)c->h_inl.size();
@@ -527,8 +559,12 @@ int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, in
     if (n) std::memcpy(dst, c->h_inl.data(), (size_t)n * 4);
     return n;
   }
-  std::vector<int64_t> all;
-  *global_count = allgather_i64(c, so.n_in_local, &all);
+  if (counts_known) {
+    *global_count = so.n_in_global;
+  } else {
+    std::vector<int64_t> all;
+    *global_count = allgather_i64(c, so.n_in_local, &all);
+  }
   if (so.n_in_local > cap)
     throw DlgError(DLG_ERR_CAPACITY, "inlier buffer too small: need " + std::to_string(so.n_in_local));
   if (so.n_in_local) {
@@ -695,6 +731,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->gath64.release(); c->gath32.release();
   c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
   c->h_stage.release();
+  c->pick.release(); c->h_pick.release(); c->rk.release(); c->h_rk.release();
   c->nw.release();
   c->pw.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
@@ -907,21 +944,21 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
     if (max_planes > 0) offsets_out[0] = 0;
     int64_t written = 0;
     const int64_t floor_n = std::max<int64_t>(3, min_inliers);
+    // every rank's active count: gathered once, then carried from each round's survivors
+    std::vector<int64_t> active;
+    int64_t N = allgather_i64(c, cl->n_active, &active);
     for (int p = 0; p < max_planes; ++p) {
-      std::vector<int64_t> all;
-      const int64_t N = allgather_i64(c, cl->n_active, &all);
       if (N < floor_n) break;
       dlg_sac_stats st;
-      SegOut so = segment_impl(c, cl, *prm, true, &st, xs);
+      SegOut so = segment_impl(c, cl, *prm, true, &st, xs, &active);
       xs->rounds++;
       if (!so.has_model) break;
-      std::vector<int64_t> tot;
-      const int64_t n_in = allgather_i64(c, so.n_in_local, &tot);
+      const int64_t n_in = so.n_in_global;
       if (n_in == 0 || n_in < min_inliers) break;  // plane rejected: active list unchanged
       int64_t g = 0;
       const double t_e0 = trace_on() ? now_ms() : 0.0;
       int64_t n = emit_inliers(c, so, prm->gather_inliers != 0, inliers_out + written,
-                               cap - written, &g, /*deferred=*/true);
+                               cap - written, &g, /*deferred=*/true, /*counts_known=*/true);
       if (trace_on())
         std::fprintf(stderr, "[dlg] after-round: segment-return %.3fms emit %.3fms\n",
                      t_e0 - c->t_tot, now_ms() - t_e0);
@@ -931,6 +968,9 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       *n_planes = p + 1;
       cl->cur = cl->spare();  // commit the removal
       cl->n_active = so.n_out_local;
+      active = so.out_ranks;
+      N = 0;
+      for (int64_t v : active) N += v;
       if (so.sp_compacted) {
         cl->sp_cur = cl->sp_spare();
         cl->sp_n = so.sp_n_out;

@@ -183,6 +183,8 @@ struct dlg_ctx {
   hipEvent_t ev_stage = nullptr;
   hipEvent_t ev_tot = nullptr;
   DevBuf<int32_t> pick;   // k_pick_p1 result
+  DevBuf<int32_t> rk;     // every rank's (inliers, survivors) of a round
+  PinBuf<int32_t> h_rk;
   PinBuf<int32_t> h_pick;
   int64_t spec_misses = 0;  // speculative picks the host replay overturned
   double t_tot = 0.0;    // (DLG_TRACE) host time the last round's totals arrived
