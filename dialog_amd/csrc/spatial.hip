@@ -160,10 +160,12 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
                                                         int nsup, const HypRec* __restrict__ hyps,
                                                         int D, int ls, float margin,
                                                         uint16_t* __restrict__ lp,
-                                                        int32_t* __restrict__ lp_n) {
+                                                        int32_t* __restrict__ lp_n,
+                                                        int32_t* __restrict__ work) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ int s_nlp;
   const int lane = threadIdx.x & (kWave - 1);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *work = 0;  // k_score_tiles_rl's item counter
   for (int j = threadIdx.x; j < D; j += kPrBS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
@@ -409,30 +411,48 @@ template <int EXP>
 __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
-    const int32_t* __restrict__ lp_n, const HypRec* __restrict__ hyps, int D, float cthr,
-    float margin, float ax, float ay, float az, int32_t* __restrict__ counts,
-    unsigned long long* __restrict__ stats) {
+    const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int chunk,
+    const HypRec* __restrict__ hyps, int D, float cthr, float margin, float ax, float ay,
+    float az, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves (see k_score_tiles)
   __shared__ uint16_t s_ring[kPrWaves][kRing2];
   __shared__ unsigned long long s_st[6];
+  __shared__ int s_taken;  // items this workgroup has claimed (<= blk_cap: 16-bit counters)
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int r32 = lane & 31, hh = lane >> 5;
   for (int j = threadIdx.x; j < D; j += kPrBS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
   }
+  if (threadIdx.x == 0) s_taken = 0;
   for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += kPrBS) s_cnt[j] = 0u;
   if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
   __syncthreads();
   const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int ntiles = (n + kTileP - 1) / kTileP;
-  const int nitems = (ntiles + kPrChunk - 1) / kPrChunk;
-  const int gw = blockIdx.x * kPrWaves + wv, nw = gridDim.x * kPrWaves;
+  const int nitems = (ntiles + chunk - 1) / chunk;
   uint16_t* ring = s_ring[wv];
-  for (int it = gw; it < nitems; it += nw) {
-    const int t0 = it * kPrChunk, t_end = min(ntiles, t0 + kPrChunk);
-    const int sidx = t0 / kSuperTiles;  // kSuperTiles % kPrChunk == 0: one super-tile per item
+  // a workgroup owns items blockIdx.x + k * gridDim.x (interleaved over the cloud); its waves
+  // claim them dynamically through an LDS counter (balances the waves of a CU; a global
+  // counter measured 3x slower: one contended L2 atomic per item), one claim ahead.  The grid
+  // keeps each workgroup <= blk_cap items (16-bit LDS counters).
+  auto claim = [&]() -> int {
+    int v = nitems;
+    if (lane == 0) {
+      const int k = atomicAdd(&s_taken, 1);
+      if (k < blk_cap) v = (int)min((int64_t)nitems, (int64_t)blockIdx.x + (int64_t)k * gridDim.x);
+    }
+    return __shfl(v, 0);
+  };
+  (void)work;
+  int it_next = claim();
+  for (;;) {
+    const int it = it_next;
+    if (it >= nitems) break;
+    it_next = claim();
+    const int t0 = it * chunk, t_end = min(ntiles, t0 + chunk);
+    const int sidx = t0 / kSuperTiles;  // kSuperTiles % chunk == 0: one super-tile per item
     const int nlp = lp_n[sidx];
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
     // the item's tiles take the list kListCap entries at a time (one pass unless it is long)
@@ -667,8 +687,9 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
   const int64_t ns = sp_supers(v.n);
   const int ls = prune_list_stride(D);
   const unsigned ga = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2 * num_cus, ns));
+  int32_t* work = lp_n + ns;  // (lp_n holds sp_supers(n) + 1 entries)
   hipLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, v.supers, (int)ns, hyps, D, ls,
-                     margin, lp, lp_n);
+                     margin, lp, lp_n, work);
   // one workgroup per CU (LDS + VGPRs), and enough of them that no workgroup takes more than 31
   // items per wave (31 x 16 waves x 4 tiles x 32 points = 63488 <= 65535: 16-bit LDS counters)
   const int64_t items = (sp_tiles(v.n) + kPrChunk - 1) / kPrChunk;
@@ -689,8 +710,21 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
       return e ? std::atoi(e) : 0;
     }();
     auto* kfn = exp == 1 ? k_score_tiles_rl<1> : exp == 2 ? k_score_tiles_rl<2> : k_score_tiles_rl<0>;
-    hipLaunchKernelGGL(kfn, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls,
-                       lp_n, hyps, D, cthr, margin, amax[0], amax[1], amax[2], counts, stats);
+    // dynamic item claims: one workgroup per CU, each capped at blk_cap items (16-bit counters),
+    // and enough workgroups that the caps cover every item
+    static const int chunk = [] {  // tiles per work item (1, 2, 4, 8, 16 or 32)
+      const char* e = std::getenv("DLG_PRUNE_CHUNK");
+      const int c = e ? std::atoi(e) : 2;
+      return (c >= 1 && c <= kSuperTiles && kSuperTiles % c == 0) ? c : 2;
+    }();
+    const int64_t items_rl = (sp_tiles(v.n) + chunk - 1) / chunk;
+    const int blk_cap = 65535 / (chunk * kTileP);
+    const int64_t g_rl = std::max<int64_t>(
+        1, std::max<int64_t>(std::min<int64_t>(num_cus, (items_rl + kPrWaves - 1) / kPrWaves),
+                             (items_rl + blk_cap - 1) / blk_cap));
+    hipLaunchKernelGGL(kfn, dim3((unsigned)g_rl), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
+                       v.tiles, lp, ls, lp_n, work, blk_cap, chunk, hyps, D, cthr, margin, amax[0],
+                       amax[1], amax[2], counts, stats);
   } else if (occ == 8) {
     hipLaunchKernelGGL(k_score_tiles_o8, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
                        v.tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
