@@ -407,8 +407,8 @@ constexpr int kRing2 = 256;                       // >= 31 queued + 128 appended
 
 // EXP: timing experiments only (1: groups not scored, 2: no band re-decision) -- counts are
 // then wrong
-template <int EXP>
-__global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
+template <int EXP, int BS>
+__global__ __launch_bounds__(BS) void k_score_tiles_rl(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
     const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int chunk,
@@ -416,17 +416,17 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
     float az, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves (see k_score_tiles)
-  __shared__ uint16_t s_ring[kPrWaves][kRing2];
+  __shared__ uint16_t s_ring[(BS / kWave)][kRing2];
   __shared__ unsigned long long s_st[6];
   __shared__ int s_taken;  // items this workgroup has claimed (<= blk_cap: 16-bit counters)
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int r32 = lane & 31, hh = lane >> 5;
-  for (int j = threadIdx.x; j < D; j += kPrBS) {
+  for (int j = threadIdx.x; j < D; j += BS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
   }
   if (threadIdx.x == 0) s_taken = 0;
-  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += kPrBS) s_cnt[j] = 0u;
+  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += BS) s_cnt[j] = 0u;
   if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
   __syncthreads();
   const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -435,8 +435,9 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
   uint16_t* ring = s_ring[wv];
   // a workgroup owns items blockIdx.x + k * gridDim.x (interleaved over the cloud); its waves
   // claim them dynamically through an LDS counter (balances the waves of a CU; a global
-  // counter measured 3x slower: one contended L2 atomic per item), one claim ahead.  The grid
-  // keeps each workgroup <= blk_cap items (16-bit LDS counters).
+  // counter measured 3x slower: one contended L2 atomic per item; dealing super-tiles to the
+  // workgroups of one XCD so that a plane list is fetched into one L2 only: no faster), one
+  // claim ahead.  The grid keeps each workgroup <= blk_cap items (16-bit LDS counters).
   auto claim = [&]() -> int {
     int v = nitems;
     if (lane == 0) {
@@ -618,7 +619,7 @@ __global__ __launch_bounds__(kPrBS) void k_score_tiles_rl(
     }  // list passes
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < D; j += kPrBS) {
+  for (int j = threadIdx.x; j < D; j += BS) {
     const int c = (int)((s_cnt[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
     if (c) atomicAdd(&counts[j], c);
   }
@@ -709,9 +710,17 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
       const char* e = std::getenv("DLG_PRUNE_EXP");  // timing experiments only (wrong counts)
       return e ? std::atoi(e) : 0;
     }();
-    auto* kfn = exp == 1 ? k_score_tiles_rl<1> : exp == 2 ? k_score_tiles_rl<2> : k_score_tiles_rl<0>;
-    // dynamic item claims: one workgroup per CU, each capped at blk_cap items (16-bit counters),
-    // and enough workgroups that the caps cover every item
+    static const int bpc = [] {  // workgroups per CU: 1 (1024 threads) or 2/4 (512 threads)
+      const char* e = std::getenv("DLG_PRUNE_BPC");
+      const int b = e ? std::atoi(e) : 1;
+      return (b == 2 || b == 4) ? b : 1;
+    }();
+    const bool small = bpc > 1;
+    auto* kfn = small ? (exp == 1 ? k_score_tiles_rl<1, 512> : exp == 2 ? k_score_tiles_rl<2, 512> : k_score_tiles_rl<0, 512>)
+                      : (exp == 1 ? k_score_tiles_rl<1, 1024> : exp == 2 ? k_score_tiles_rl<2, 1024> : k_score_tiles_rl<0, 1024>);
+    const int bs = small ? 512 : 1024;
+    // dynamic item claims within a workgroup; workgroups capped at blk_cap items (16-bit
+    // counters), and enough of them that the caps cover every item
     static const int chunk = [] {  // tiles per work item (1, 2, 4, 8, 16 or 32)
       const char* e = std::getenv("DLG_PRUNE_CHUNK");
       const int c = e ? std::atoi(e) : 2;
@@ -720,9 +729,9 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
     const int64_t items_rl = (sp_tiles(v.n) + chunk - 1) / chunk;
     const int blk_cap = 65535 / (chunk * kTileP);
     const int64_t g_rl = std::max<int64_t>(
-        1, std::max<int64_t>(std::min<int64_t>(num_cus, (items_rl + kPrWaves - 1) / kPrWaves),
+        1, std::max<int64_t>(std::min<int64_t>((int64_t)bpc * num_cus, (items_rl + bs / kWave - 1) / (bs / kWave)),
                              (items_rl + blk_cap - 1) / blk_cap));
-    hipLaunchKernelGGL(kfn, dim3((unsigned)g_rl), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
+    hipLaunchKernelGGL(kfn, dim3((unsigned)g_rl), dim3(bs), 0, s, v.x, v.y, v.z, (int)v.n,
                        v.tiles, lp, ls, lp_n, work, blk_cap, chunk, hyps, D, cthr, margin, amax[0],
                        amax[1], amax[2], counts, stats);
   } else if (occ == 8) {

@@ -46,6 +46,7 @@ for s in $STEPS; do
               DLG_PRUNE_KERNEL=$kk DLG_PRUNE_EXP=$ee SCORE_AB_NOCHECK=1 VARIANTS=20 run expm_k${kk}_e${ee} 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3
             done; done ;;
     chunk)  for cc in 1 2 4; do DLG_PRUNE_CHUNK=$cc VARIANTS=20,19 run chunk_$cc 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
+    bpc)    for bb in 1 2 4; do DLG_PRUNE_BPC=$bb VARIANTS=20,19 run bpc_$bb 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
     ab)     run score_ab 600 python3 tools/score_ab.py ;;
     list)   run counters 120 rocprofv3 -L ;;
     sqpmc)  VARIANTS="${VARIANTS:-0,2}" run sqpmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \

@@ -53,7 +53,7 @@ def main():
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, bench.py --steps 1 --warmup 0",
            "kernels": res, "read_calibration_dword_loads": cal}
     # one scoring launch = k_prune_supers + k_score_tiles (pruned, default), else the exhaustive kernel
-    keys = [k for k in ("k_prune_supers", "k_score_tiles") if k in res] or \
+    keys = [k for k in ("k_prune_supers", "k_score_tiles_rl", "k_score_tiles") if k in res][:2] or \
            (["k_score_bf16"] if "k_score_bf16" in res else ["k_score"])
     if all(k in res for k in keys) and cal:
         out["kernel"] = " + ".join(keys)
