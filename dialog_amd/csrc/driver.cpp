@@ -61,6 +61,52 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// spin until k_publish has released `seq` into c->pub[0] (the round's results are then in
+// c->pub).  ev_tot (recorded right after the publish) backs it up: once the event has
+// completed the word must be visible; an error of the stream surfaces through the event query.
+void wait_published(dlg_ctx* c, int32_t seq) {
+  for (uint32_t k = 1;; ++k) {
+    if (__atomic_load_n(c->pub, __ATOMIC_ACQUIRE) == seq) return;
+    if ((k & 1023u) == 0) {
+      const hipError_t e = hipEventQuery(c->ev_tot);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(c->pub, __ATOMIC_ACQUIRE) == seq) return;
+        throw DlgError(DLG_ERR_INTERNAL, "round results not visible after the round completed");
+      }
+      if (e != hipErrorNotReady) HIPCHK(e);
+    }
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+}
+
+// the previous compaction's Morton-copy totals (in, out) against what the list copy predicted
+void check_sp_totals(dlg_ctx* c, const int32_t* sp_tot) {
+  if (!c->sp_check) return;
+  c->sp_check = false;
+  if (c->sp_expect_in != 0 || c->sp_expect_out != 0) {
+    if (sp_tot[0] != c->sp_expect_in || sp_tot[1] != c->sp_expect_out)
+      throw DlgError(DLG_ERR_INTERNAL, "spatial copy out of step with the active list");
+  }
+}
+
+// after a stream synchronisation: the last compaction's Morton-copy totals and select timing
+void settle_round(dlg_ctx* c) {
+  if (c->sp_check) {
+    int32_t t[2] = {0, 0};
+    HIPCHK(hipMemcpy(t, c->totals.p + 2, 8, hipMemcpyDeviceToHost));
+    check_sp_totals(c, t);
+  }
+  if (c->sel_pending) {
+    const int k = c->sel_k ^ 1;  // the last round's pair
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_sel[k][0], c->ev_sel[k][1]));
+    c->sel_pending->select_ms += ms;
+    c->sel_pending = nullptr;
+  }
+}
+
 int64_t allgather_i64(dlg_ctx* c, int64_t v, std::vector<int64_t>* all) {
   const int W = c->comm->world();
   all->assign(W, 0);
@@ -341,8 +387,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       spec_Dp = Dp;
       drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
       if (trace_on())
-        std::fprintf(stderr, "[dlg] N=%lld D=%d totals->draw=%.3fms draw=%.3fms (speculative pick)\n",
-                     (long long)N, D, c->t_tot > 0 ? t_draw0 - c->t_tot : 0.0, t_draw1 - t_draw0);
+        std::fprintf(stderr, "[dlg] N=%lld D=%d totals->draw=%.3fms draw=%.3fms enqueue=%.3fms (speculative pick)\n",
+                     (long long)N, D, c->t_tot > 0 ? t_draw0 - c->t_tot : 0.0, t_draw1 - t_draw0,
+                     now_ms() - t_draw1);
       return;
     }
     HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 4 * ((size_t)Dp + D), hipMemcpyDeviceToHost, c->stream));
@@ -389,7 +436,12 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // inliers (k_moments, centred on the winning sample), the double eigen33 refit in a
     // one-thread kernel, then the select with the refined plane read from device memory.  PCL
     // mode needs the host's sequential float sums in between.
-    if (c->profiling) HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    const int sk = c->sel_k;  // this round's pair of select timing events
+    if (c->profiling) {
+      for (auto& ev : c->ev_sel[sk])
+        if (!ev) HIPCHK(hipEventCreate(&ev));
+      HIPCHK(hipEventRecord(c->ev_sel[sk][0], c->stream));
+    }
     if (!pcl_refit) {
       if (prm.optimize) {
         const int nb = moments_blocks(src.n);
@@ -419,10 +471,45 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       HIPCHK(hipMemcpyAsync(rc_dev, c->h_small.p + 5, sizeof(float4), hipMemcpyHostToDevice,
                             c->stream));
     }
-    // final selectWithinDistance with the refined model (+ compaction of the survivors)
-    launch_select(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
-                  c->inl_gid.p, nullptr, compact ? &dst : nullptr, c->stream);
-    // the spatial copy loses the same points (same predicate, same float inputs)
+    // final selectWithinDistance with the refined model: the head (counts + scan) makes the
+    // round's totals final, they are published right away, and the scatters (inlier ids,
+    // survivors of both copies) and the sphere bounds run while the host reads them and draws
+    // the next round
+    launch_select_head(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
+                       c->totals.p, c->stream);
+    HIPCHK(hipGetLastError());
+    const int W = c->comm->world();
+    if (W > 1) {  // every rank's (in, out): the extract loop needs no host-synced allgather
+      c->rk.ensure(2 * (size_t)W + 2);
+      c->h_rk.ensure(2 * (size_t)W + 2);
+      c->comm->allgather(c->totals.p, c->rk.p, 2, DType::I32, c->stream);
+    }
+    // the round's results into the coherent pinned buffer + a sequence number the host spins on
+    // (totals[2..3] still hold the previous compaction's Morton-copy totals: checked below)
+    const bool with_counts = spec_pending;
+    const int nres = with_counts ? spec_Dp + spec_D : 0;
+    const size_t need = (size_t)kPubRk + (W > 1 ? 2 * (size_t)W : 0) + (size_t)nres;
+    if (need > c->pub_cap) {
+      if (c->pub) HIPCHK(hipHostFree(c->pub));
+      c->pub = nullptr;
+      c->pub_cap = 0;
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pub), std::max<size_t>(need, 16384) * 4,
+                           hipHostMallocCoherent));
+      c->pub_cap = std::max<size_t>(need, 16384);
+      c->pub[0] = 0;
+    }
+    const int32_t seq = ++c->pub_seq == 0 ? ++c->pub_seq : c->pub_seq;
+    launch_publish(c->totals.p, 4, c->small.p, 6, W > 1 ? c->rk.p : nullptr, W > 1 ? 2 * W : 0,
+                   with_counts ? c->pick.p : nullptr, with_counts ? 2 : 0,
+                   with_counts ? c->res.p : nullptr, nres, c->pub, seq, c->stream);
+    HIPCHK(hipGetLastError());
+    spec_pending = false;
+    if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ev_tot, c->stream));
+    launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p, nullptr,
+                       compact ? &dst : nullptr, c->stream);
+    // the Morton copy loses the same points (same predicate, same float inputs): its totals
+    // land in totals[2..3], checked at the next publish / the end of the extraction
     if (sp_compact) {
       SoA& sd = cl->sp_buf[cl->sp_spare()];
       sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
@@ -431,44 +518,40 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       const PointsView spv{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n, nullptr};
       launch_select(spv, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
                     c->totals.p + 2, nullptr, nullptr, &spo, c->stream);
-    }
-    HIPCHK(hipGetLastError());
-    if (c->profiling) HIPCHK(hipEventRecord(c->ev[3], c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, sp_compact ? 16 : 8, hipMemcpyDeviceToHost,
-                          c->stream));
-    const int W = c->comm->world();
-    if (W > 1) {  // every rank's (in, out): the extract loop needs no host-synced allgather
-      c->rk.ensure(2 * (size_t)W + 2);
-      c->h_rk.ensure(2 * (size_t)W + 2);
-      c->comm->allgather(c->totals.p, c->rk.p, 2, DType::I32, c->stream);
-      HIPCHK(hipMemcpyAsync(c->h_rk.p, c->rk.p, 8 * (size_t)W, hipMemcpyDeviceToHost, c->stream));
-    }
-    HIPCHK(hipMemcpyAsync(c->h_small.p, c->small.p, 6 * sizeof(float4), hipMemcpyDeviceToHost,
-                          c->stream));
-    if (spec_pending) {  // the speculative round's counts and pick, for the host replay
-      spec_pending = false;
-      HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 4 * ((size_t)spec_Dp + spec_D),
-                            hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipMemcpyAsync(c->h_pick.p, c->pick.p, 8, hipMemcpyDeviceToHost, c->stream));
-    }
-    if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(c->ev_tot, c->stream));
-    if (sp_compact) {
-      // sphere bounds of the survivors, queued behind the totals copy: they run while the host
-      // reads the totals and draws the next round.  Into the spare buffer's own bound arrays
-      // (sized for the current count, an upper bound; the kernel reads the survivor count from
-      // totals[3]), so a round whose plane is rejected leaves the current bounds intact.
+      if (c->profiling) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
+      // sphere bounds of the survivors, into the spare buffer's own bound arrays (sized for
+      // the current count, an upper bound; the kernel reads the survivor count from
+      // totals[3]), so a round whose plane is rejected leaves the current bounds intact
       const int b = cl->sp_spare();
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
       cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
-      const SoA& sd = cl->sp_buf[b];
       launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 3, cl->sp_tb[b].p,
                            cl->sp_sb[b].p, c->stream);
-      HIPCHK(hipGetLastError());
     }
-    wait_event(c->ev_tot);
+    HIPCHK(hipGetLastError());
+    if (c->profiling && !sp_compact) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
+    const double t_wait0 = trace_on() ? now_ms() : 0.0;
+    wait_published(c, seq);
+    if (trace_on())
+      std::fprintf(stderr, "[dlg] select enqueue=%.3fms wait=%.3fms\n", t_wait0 - t_ref0, now_ms() - t_wait0);
     if (trace_on()) c->t_tot = now_ms();
-    if (c->profiling && xs) xs->select_ms += event_ms(c, 2, 3);
+    std::memcpy(c->h_tot.p, c->pub + kPubTot, 16);
+    std::memcpy(c->h_small.p, c->pub + kPubSmall, 6 * sizeof(float4));
+    if (W > 1) std::memcpy(c->h_rk.p, c->pub + kPubRk, 8 * (size_t)W);
+    check_sp_totals(c, c->h_tot.p + 2);
+    if (with_counts) {
+      std::memcpy(c->h_pick.p, c->pub + kPubPick, 8);
+      std::memcpy(c->h_res.p, c->pub + kPubRk + (W > 1 ? 2 * W : 0), 4 * (size_t)nres);
+    }
+    // the previous round's select events precede this publish on the stream: complete now
+    if (c->sel_pending) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, c->ev_sel[sk ^ 1][0], c->ev_sel[sk ^ 1][1]));
+      c->sel_pending->select_ms += ms;
+      c->sel_pending = nullptr;
+    }
+    if (c->profiling && xs) c->sel_pending = xs;  // this round's: read at the next publish / end
+    c->sel_k = sk ^ 1;
   };
 
   bool selected = false;
@@ -536,11 +619,13 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     for (int64_t v : out.in_ranks) out.n_in_global += v;
   }
   if (sp_compact) {
+    // non-finite points are never inliers: the Morton copy loses exactly the list's inliers
+    // (its own totals are checked at the next publish, check_sp_totals)
     out.sp_compacted = true;
-    out.sp_n_out = cl->sp_n == 0 ? 0 : c->h_tot.p[3];
-    // non-finite points are never inliers: both copies must lose exactly the same points
-    if ((cl->sp_n == 0 ? 0 : c->h_tot.p[2]) != out.n_in_local)
-      throw DlgError(DLG_ERR_INTERNAL, "spatial copy out of step with the active list");
+    out.sp_n_out = cl->sp_n - out.n_in_local;
+    c->sp_expect_in = cl->sp_n == 0 ? 0 : out.n_in_local;
+    c->sp_expect_out = out.sp_n_out;
+    c->sp_check = true;
   }
   if (trace_on())
     std::fprintf(stderr, "[dlg] refit+select=%.3fms n_in=%lld\n", now_ms() - t_ref0,
@@ -732,10 +817,16 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
   c->h_stage.release();
   c->pick.release(); c->h_pick.release(); c->rk.release(); c->h_rk.release();
+  if (c->pub) (void)hipHostFree(c->pub);
+  c->pub = nullptr;
+  c->pub_cap = 0;
   c->nw.release();
   c->pw.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
   if (c->ev_tot) (void)hipEventDestroy(c->ev_tot);
+  for (auto& pr : c->ev_sel)
+    for (auto& ev : pr)
+      if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -982,11 +1073,14 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
     drain_pending(c);
     // A stream synchronisation lets the HIP runtime reclaim the per-command resources of the
     // rounds: with event waits alone they pile up until a D2H copy blocks the host for ~10 ms
-    // (measured: every ~55 rounds).  The stream only holds the last sphere bounds here.
+    // (measured: every ~55 rounds).  The stream only holds the last round's tails here.
     sync(c);
+    settle_round(c);
   });
   c->pending_dst = nullptr;  // (error path: never write into the caller's buffer later)
   c->pending_n = 0;
+  c->sel_pending = nullptr;  // (never read into the caller's stats after the call)
+  c->sp_check = false;
   xs->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return s;
 }

@@ -183,6 +183,15 @@ struct dlg_ctx {
   hipEvent_t ev_stage = nullptr;
   hipEvent_t ev_tot = nullptr;
   DevBuf<int32_t> pick;   // k_pick_p1 result
+  int32_t* pub = nullptr;  // coherent pinned: k_publish's round results (pub[0] = sequence)
+  size_t pub_cap = 0;
+  int32_t pub_seq = 0;
+  // the last compaction's predicted Morton-copy totals, checked at the next publish
+  bool sp_check = false;
+  int64_t sp_expect_in = 0, sp_expect_out = 0;
+  dlg_extract_stats* sel_pending = nullptr;  // select_ms of the last round, not yet read
+  hipEvent_t ev_sel[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // per-round pairs
+  int sel_k = 0;
   DevBuf<int32_t> rk;     // every rank's (inliers, survivors) of a round
   PinBuf<int32_t> h_rk;
   PinBuf<int32_t> h_pick;

@@ -1030,6 +1030,29 @@ __global__ __launch_bounds__(kPickBS) void k_pick_p1(const int32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_publish: the round's small results (select totals, winner + refined plane, every rank's
+// totals, the speculative pick and counts) written straight into a coherent pinned host buffer,
+// then a system-scope release of the sequence number in pub[0]: the host spins on that word
+// instead of waiting on a HIP event (whose wake-up costs ~50 us per round).  One workgroup.
+__global__ __launch_bounds__(256) void k_publish(const int32_t* __restrict__ totals, int ntot,
+                                                 const float4* __restrict__ small, int nsmall,
+                                                 const int32_t* __restrict__ rk, int nrk,
+                                                 const int32_t* __restrict__ pick, int npick,
+                                                 const int32_t* __restrict__ res, int nres,
+                                                 int32_t* pub, int32_t seq) {
+  const int t = threadIdx.x;
+  for (int i = t; i < ntot; i += 256) pub[kPubTot + i] = totals[i];
+  for (int i = t; i < 4 * nsmall; i += 256)
+    pub[kPubSmall + i] = __float_as_int(reinterpret_cast<const float*>(small)[i]);
+  for (int i = t; i < npick; i += 256) pub[kPubPick + i] = pick[i];
+  for (int i = t; i < nrk; i += 256) pub[kPubRk + i] = rk[i];
+  for (int i = t; i < nres; i += 256) pub[kPubRk + nrk + i] = res[i];
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(pub, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ---------------------------------------------------------------------------------------------
 // select / compact (selectWithinDistance + removal of the inliers from the active list)
 constexpr int kSelBS = 256;
 constexpr int kSelIt = kSelTile / kSelBS;
@@ -1537,11 +1560,20 @@ void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypR
                      best, best_smp, out);
 }
 
+void launch_publish(const int32_t* totals, int ntot, const float4* small, int nsmall,
+                    const int32_t* rk, int nrk, const int32_t* pick, int npick,
+                    const int32_t* res, int nres, int32_t* pub, int32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, totals, ntot, small, nsmall, rk, nrk,
+                     pick, npick, res, nres, pub, seq);
+}
+
 int select_tiles(int64_t n) { return (int)((n + kSelTile - 1) / kSelTile); }
 
-void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int32_t* tile_in,
-                   int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid,
-                   float* inl_xyz, const PointsOut* dst, hipStream_t s) {
+// selectWithinDistance in two halves: head = per-tile counts + scan (totals[0..1] final),
+// tail = ordered scatter of the inlier ids / survivors
+void launch_select_head(PointsView src, const float4* coef, const ModelTest& mt, int32_t* tile_in,
+                        int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals,
+                        hipStream_t s) {
   const int nt = select_tiles(src.n);
   if (nt == 0) {
     (void)hipMemsetAsync(totals, 0, 2 * sizeof(int32_t), s);
@@ -1553,6 +1585,13 @@ void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int3
     hipLaunchKernelGGL(k_select_count<false>, dim3(nt), dim3(kSelBS), 0, s, src, coef, mt, tile_in);
   hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanBS), 0, s, tile_in, nt, src.n, tile_off_in,
                      tile_off_out, totals);
+}
+
+void launch_select_tail(PointsView src, const float4* coef, const ModelTest& mt,
+                        const int32_t* tile_off_in, const int32_t* tile_off_out, int32_t* inl_gid,
+                        float* inl_xyz, const PointsOut* dst, hipStream_t s) {
+  const int nt = select_tiles(src.n);
+  if (nt == 0) return;
   PointsOut d = dst ? *dst : PointsOut{nullptr, nullptr, nullptr, nullptr, nullptr};
   if (mt.normal_plane)
     hipLaunchKernelGGL(k_select_scatter<true>, dim3(nt), dim3(kSelBS), 0, s, src, coef, mt,
@@ -1560,6 +1599,13 @@ void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int3
   else
     hipLaunchKernelGGL(k_select_scatter<false>, dim3(nt), dim3(kSelBS), 0, s, src, coef, mt,
                        tile_off_in, tile_off_out, inl_gid, inl_xyz, d, dst ? 1 : 0);
+}
+
+void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int32_t* tile_in,
+                   int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid,
+                   float* inl_xyz, const PointsOut* dst, hipStream_t s) {
+  launch_select_head(src, coef, mt, tile_in, tile_off_in, tile_off_out, totals, s);
+  launch_select_tail(src, coef, mt, tile_off_in, tile_off_out, inl_gid, inl_xyz, dst, s);
 }
 
 void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest& mt,

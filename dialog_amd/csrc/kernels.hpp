@@ -100,6 +100,12 @@ int score_variant();
 void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
                            hipStream_t s);
 // writes hyps[D] and good[D] (int32 flags next to the counts for one D2H copy)
+// round results into the coherent pinned buffer pub (layout below), then pub[0] = seq (release,
+// system scope)
+constexpr int kPubTot = 1, kPubPick = 5, kPubSmall = 8, kPubRk = 32;  // + nrk: counts
+void launch_publish(const int32_t* totals, int ntot, const float4* small, int nsmall,
+                    const int32_t* rk, int nrk, const int32_t* pick, int npick,
+                    const int32_t* res, int nres, int32_t* pub, int32_t seq, hipStream_t s);
 // speculative computeModel decision for probability 1 over one batch (k_pick_p1): out[0] best
 // batch index (-1 none), out[1] loop ended inside the batch; winner copied to best / best_smp
 void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
@@ -137,6 +143,13 @@ int select_tiles(int64_t n);
 void launch_select(PointsView src, const float4* coef, const ModelTest& mt, int32_t* tile_in,
                    int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals, int32_t* inl_gid,
                    float* inl_xyz, const PointsOut* dst, hipStream_t s);
+// the two halves of launch_select: counts + scan (totals final), then the ordered scatter
+void launch_select_head(PointsView src, const float4* coef, const ModelTest& mt, int32_t* tile_in,
+                        int32_t* tile_off_in, int32_t* tile_off_out, int32_t* totals,
+                        hipStream_t s);
+void launch_select_tail(PointsView src, const float4* coef, const ModelTest& mt,
+                        const int32_t* tile_off_in, const int32_t* tile_off_out, int32_t* inl_gid,
+                        float* inl_xyz, const PointsOut* dst, hipStream_t s);
 // raw caller normals (n records of stride_f floats, curvature at curv_off) gathered by the
 // cloud's local point index (gid - id_base) -> (normalized normal, curvature)
 void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,
