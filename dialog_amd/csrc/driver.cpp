@@ -200,6 +200,15 @@ int prune_mode() {
 }
 
 // Morton-ordered copy of the pristine cloud's finite points + its bounding spheres
+// pruned NORMAL_PLANE scoring (DLG_PRUNE_NP=0: the exhaustive k_score_np)
+bool np_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLG_PRUNE_NP");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 // speculative device pick for probability-1 rounds (segment_impl); DLG_SPEC_PICK=0 disables
 bool spec_pick_enabled() {
   static const bool on = [] {
@@ -229,6 +238,13 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
     const int64_t m = n - nonfinite;
     cl->sp_pristine.ensure((size_t)std::max<int64_t>(m, 1));
     launch_gather_order(cl->pristine.view(n), i1.p, m, cl->sp_pristine.out(), c->stream);
+    cl->sp_order.ensure((size_t)std::max<int64_t>(m, 1));
+    if (m > 0)
+      HIPCHK(hipMemcpyAsync(cl->sp_order.p, i1.p, (size_t)m * 4, hipMemcpyDeviceToDevice, c->stream));
+    if (cl->has_normals) {
+      cl->sp_pristine.ensure_nrm((size_t)std::max<int64_t>(m, 1));
+      launch_gather_nrm(cl->pristine.nrm.p, cl->sp_order.p, m, cl->sp_pristine.nrm.p, c->stream);
+    }
     cl->sp_tiles_pr.ensure((size_t)std::max<int64_t>(sp_tiles(m), 1));
     cl->sp_supers_pr.ensure((size_t)std::max<int64_t>(sp_supers(m), 1));
     launch_sphere_bounds(cl->sp_pristine.x.p, cl->sp_pristine.y.p, cl->sp_pristine.z.p, m, nullptr,
@@ -311,8 +327,20 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   if (trace_on()) std::fprintf(stderr, "[dlg] segment start %.3fms ctl %.3fms\n", t_ctl0 - c->t_tot, now_ms() - t_ctl0);
   // pruned scoring over the spatial copy (plane model, default kernel, spatial copy in step)
   const bool pruned = !np && cl->sp_valid && score_variant() == kScoreDefault && prune_mode() != 0;
-  const float pmargin = pruned ? prune_margin(cthr, cl->amax) : 0.0f;
-  if (pruned) ensure_sphere_bounds(c, cl);
+  // NORMAL_PLANE over the Morton copy: the prefilter d_euclid < lim(w) holds for the cloud's
+  // largest w = lambda (1 - min curvature) when every w lies in [0, 1) (then lim is finite and
+  // monotone in w); NaN curvatures never pass PCL's test.  Otherwise the exhaustive kernel.
+  float np_lim = INFINITY;
+  if (np && cl->curv_known) {
+    const double w_max = prm.normal_distance_weight * (1.0 - (double)cl->curv_min);
+    const double w_min = prm.normal_distance_weight * (1.0 - (double)cl->curv_max);
+    if (w_min >= 0.0 && w_max < 1.0) np_lim = np_lim_max(w_max, prm.threshold);
+  }
+  const bool pruned_np = np && cl->sp_valid && cl->sp_soa().with_nrm && prune_mode() != 0 &&
+                         np_enabled() && np_lim < INFINITY;
+  const float pmargin = pruned ? prune_margin(cthr, cl->amax)
+                               : pruned_np ? prune_margin(np_lim, cl->amax) : 0.0f;
+  if (pruned || pruned_np) ensure_sphere_bounds(c, cl);
   // device slots: winning HypRec (its first float4 is the plane), its 3 samples, refined plane
   c->small.ensure(8);
   HypRec* best_dev = reinterpret_cast<HypRec*>(c->small.p);
@@ -358,7 +386,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                       c->res.p + Dp, c->stream);
     HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    if (np)
+    if (pruned_np) {
+      c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
+      c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
+      const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold};
+      launch_score_pruned(spatial_view(cl), c->hyps.p, nullptr, nullptr, D, cthr, pmargin,
+                          cl->amax, c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream, nullptr,
+                          &npp);
+    } else if (np)
       launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
     else if (pruned) {
       const uint4* bcol = nullptr;
@@ -430,7 +465,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (src.nrm) sp.ensure_nrm((size_t)std::max<int64_t>(src.n, 1));
     dst = sp.out();
   }
-  const bool sp_compact = compact && !np && cl->sp_valid;
+  const bool sp_compact = compact && cl->sp_valid && (!np || cl->sp_soa().with_nrm);
   auto refit_select = [&]() {
     // Fast mode (and no optimisation) never leave the device: moments of the unrefined plane's
     // inliers (k_moments, centred on the winning sample), the double eigen33 refit in a
@@ -513,9 +548,12 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (sp_compact) {
       SoA& sd = cl->sp_buf[cl->sp_spare()];
       sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
-      const PointsOut spo = sd.out();
       const SoA& ss = cl->sp_soa();
-      const PointsView spv{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n, nullptr};
+      if (ss.with_nrm) sd.ensure_nrm((size_t)std::max<int64_t>(cl->sp_n, 1));
+      PointsOut spo = sd.out();
+      if (!ss.with_nrm) spo.nrm = nullptr;  // (normals travel only when the source has them)
+      const PointsView spv{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n,
+                           ss.with_nrm ? ss.nrm.p : nullptr};
       launch_select(spv, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
                     c->totals.p + 2, nullptr, nullptr, &spo, c->stream);
       if (c->profiling) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
@@ -929,6 +967,7 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
   cl->sp_buf[1].release();
   cl->sp_tiles_pr.release();
   cl->sp_supers_pr.release();
+  cl->sp_order.release();
   for (int b = 0; b < 2; ++b) {
     cl->sp_tb[b].release();
     cl->sp_sb[b].release();
@@ -983,9 +1022,37 @@ dlg_status dlg_cloud_set_normals(dlg_ctx* c, dlg_cloud* cl, const float* normals
                                 stride_bytes == 16 ? 3 : 4, cl->pristine.view(cl->n_total),
                                 cl->id_base, cl->pristine.nrm.p, c->stream);
       HIPCHK(hipGetLastError());
+      // the Morton copy carries the normals too (pruned NORMAL_PLANE scoring)
+      if (cl->sp_built) {
+        cl->sp_pristine.ensure_nrm((size_t)std::max<int64_t>(cl->sp_n_pristine, 1));
+        launch_gather_nrm(cl->pristine.nrm.p, cl->sp_order.p, cl->sp_n_pristine,
+                          cl->sp_pristine.nrm.p, c->stream);
+      }
+      // curvature range -> the largest w = lambda (1 - curvature) of the cloud
+      c->small.ensure(8);
+      uint32_t* cr = reinterpret_cast<uint32_t*>(c->small.p + 7);
+      launch_curv_range(cl->pristine.nrm.p, cl->n_total, cr, c->stream);
+      uint32_t h[2] = {0u, 0u};
+      HIPCHK(hipMemcpyAsync(h, cr, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipGetLastError());
       sync(c);
+      auto ord2f = [](uint32_t o) {
+        const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f;
+      };
+      cl->curv_known = h[0] <= h[1];  // (all NaN: no finite curvature)
+      if (cl->curv_known) {
+        cl->curv_min = ord2f(h[0]);
+        cl->curv_max = ord2f(h[1]);
+      }
     }
     cl->has_normals = true;
+    cl->sp_cur = -1;  // (the reset above also resets the Morton copy)
+    cl->sp_n = cl->sp_n_pristine;
+    cl->sp_valid = cl->sp_built;
+    cl->sp_dirty = false;
   });
 }
 

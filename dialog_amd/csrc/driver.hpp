@@ -221,6 +221,10 @@ struct dlg_cloud {
   bool sp_dirty = false;   // sphere bounds of the working copy need recomputing
   int sp_cur = -1;         // -1 pristine, 0 / 1 ping-pong
   int64_t sp_n_pristine = 0, sp_n = 0;
+  DevBuf<int32_t> sp_order;  // pristine index of each Morton-copy point (normals gathered by it)
+  // curvature range of the uploaded normals (NaN ignored): bounds w = lambda (1 - curvature)
+  bool curv_known = false;
+  float curv_min = 0.0f, curv_max = 0.0f;
   SoA sp_pristine, sp_buf[2];
   // sphere bounds of the pristine copy and of each ping-pong buffer sp_buf[i]
   DevBuf<float4> sp_tiles_pr, sp_supers_pr, sp_tb[2], sp_sb[2];

@@ -14,6 +14,7 @@
 //   computeMeanAndCovarianceMatrix (fast mode, double)  -> k_moments
 #include "kernels.hpp"
 #include "dev_common.hpp"
+#include "np_dev.hpp"
 #include "host_math.hpp"
 
 #include <algorithm>
@@ -24,43 +25,6 @@
 namespace dlg {
 
 namespace {
-
-// Eigen Vector4f(v0, v1, v2, 0).normalized(): z = (v0^2 + v2^2) + (v1^2 + 0); z > 0 ? v / sqrt(z)
-__device__ __forceinline__ float4 eigen_normalized3(float v0, float v1, float v2, float w) {
-  const float z = (v0 * v0 + v2 * v2) + (v1 * v1 + 0.0f * 0.0f);
-  if (z > 0.0f) {
-    const float s = sqrtf(z);
-    return make_float4(v0 / s, v1 / s, v2 / s, w);
-  }
-  return make_float4(v0, v1, v2, w);
-}
-
-// SampleConsensusModelNormalPlane (PCL 1.8 sac_model_normal_plane.hpp), one point:
-//   d_euclid = fabs(coeff.dot(p) + c3), coeff = (c0, c1, c2, 0), p = (x, y, z, 0)  [float]
-//   d_normal = min(a, pi - a), a = acos(clamp(n.normalized() . coeff.normalized()))   [double]
-//   fabs(w d_normal + (1 - w) d_euclid) < thr,  w = lambda (1 - curvature)          [double]
-// cn = coeff.normalized(); nn = (n.normalized(), curvature); omw = 1 - w.  Prefilter: w >= 0 and
-// d_normal >= 0 give fl(w d_normal + b) >= b = (1 - w) d_euclid, so b >= thr rejects exactly and
-// the acos is only evaluated near the plane.
-__device__ __forceinline__ float np_deuclid(float4 c, float x, float y, float z) {
-  return fabsf(((c.x * x + c.z * z) + (c.y * y + 0.0f * 0.0f)) + c.w);
-}
-__device__ __forceinline__ bool np_full(float4 cn, float4 nn, double w, double b, double thr) {
-  double rad = (double)((nn.x * cn.x + nn.z * cn.z) + (nn.y * cn.y + 0.0f * 0.0f));
-  if (rad < -1.0) rad = -1.0;
-  else if (rad > 1.0) rad = 1.0;
-  double dn = fabs(acos(rad));
-  const double alt = 3.14159265358979323846 - dn;  // M_PI
-  if (alt < dn) dn = alt;                          // std::min(dn, M_PI - dn)
-  return fabs(w * dn + b) < thr;
-}
-__device__ __forceinline__ bool np_test(float4 c, float4 cn, float x, float y, float z, float4 nn,
-                                        double lambda, double thr) {
-  const double w = lambda * (1.0 - (double)nn.w);
-  const double b = (1.0 - w) * (double)np_deuclid(c, x, y, z);
-  if (w >= 0.0 && !(b < thr)) return false;
-  return np_full(cn, nn, w, b, thr);
-}
 
 template <bool NP>
 __device__ __forceinline__ bool model_in(const PointsView& src, int64_t e, float4 cf, float4 cn,
@@ -1194,22 +1158,6 @@ __global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src,
 constexpr int kNpBS = 256;
 constexpr int kNpWaves = kNpBS / kWave;
 constexpr int kNpQ = 128;
-
-__device__ float np_de_limit(double w, double thr) {
-  if (!(w >= 0.0)) return INFINITY;
-  const double omw = 1.0 - w;
-  if (!(omw > 0.0)) return INFINITY;
-  if (!(thr > 0.0)) return thr == thr ? 0.0f : __builtin_nanf("");
-  float x = (float)(thr / omw);
-  if (!(x == x)) return INFINITY;
-  while (!(omw * (double)x >= thr) && x < INFINITY) x = nextafterf(x, INFINITY);
-  while (x > 0.0f) {
-    const float y = nextafterf(x, -INFINITY);
-    if (omw * (double)y >= thr) x = y;
-    else break;
-  }
-  return x;
-}
 
 template <int kNpP, int kNpHT>
 __global__ __launch_bounds__(kNpBS) void k_score_np(PointsView src, const HypRec* __restrict__ hyps,

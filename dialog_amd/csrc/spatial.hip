@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include "dev_common.hpp"
+#include "np_dev.hpp"
 
 namespace dlg {
 
@@ -407,18 +408,29 @@ constexpr int kRing2 = 256;                       // >= 31 queued + 128 appended
 
 // EXP: timing experiments only (1: groups not scored, 2: no band re-decision) -- counts are
 // then wrong
-template <int EXP, int BS>
+// NPM: SACMODEL_NORMAL_PLANE (PCL's exact prefilter b = (1 - w) d_euclid < thr as the per-point
+// float compare d_euclid < lim, k_score_np; passing pairs queued per wave and decided with full
+// lanes in double as in k_score_np), the spheres ruled out with the margin of the cloud's
+// largest lim; plane model otherwise.
+template <int EXP, int BS, bool NPM>
 __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
     const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int chunk,
     const HypRec* __restrict__ hyps, int D, float cthr, float margin, float ax, float ay,
-    float az, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats) {
+    float az, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats,
+    const float4* __restrict__ NRM, double lambda, double thr) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves (see k_score_tiles)
   __shared__ uint16_t s_ring[(BS / kWave)][kRing2];
   __shared__ unsigned long long s_st[6];
   __shared__ int s_taken;  // items this workgroup has claimed (<= blk_cap: 16-bit counters)
+  // NPM: the tile's (normalised normal, curvature) per point, and the per-wave queue of
+  // prefilter-passing (point slot | plane << 5, b = (1 - w) d_euclid) pairs
+  constexpr int kQ = NPM ? 128 : 1;
+  __shared__ float4 s_pn[NPM ? BS / kWave : 1][NPM ? kTileP : 1];
+  __shared__ uint32_t s_qk[NPM ? BS / kWave : 1][kQ];
+  __shared__ double s_qb[NPM ? BS / kWave : 1][kQ];
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int r32 = lane & 31, hh = lane >> 5;
   for (int j = threadIdx.x; j < D; j += BS) {
@@ -470,9 +482,13 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     // first tile of the item
     float4 tb = tiles[t0];
     float x = 0.f, y = 0.f, z = 0.f;
+    float4 nn = make_float4(0.f, 0.f, 0.f, 0.f);
     {
       const int64_t p = (int64_t)t0 * kTileP + r32;
-      if (p < n) { x = X[p]; y = Y[p]; z = Z[p]; }
+      if (p < n) {
+        x = X[p]; y = Y[p]; z = Z[p];
+        if constexpr (NPM) nn = NRM[p];
+      }
     }
     for (int t = t0; t < t_end; ++t) {
       const int64_t p0 = (int64_t)t * kTileP;
@@ -482,8 +498,16 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
       // A operand (the tile's points relative to its centre) before the next tile's loads are
       // issued: waiting for this tile's data then never waits for the prefetch (vmcnt is in order)
       const bool bad = ballot(!valid || !(isfinite(x) && isfinite(y) && isfinite(z))) != 0;
-      u32x4 a1, a2;
-      {
+      u32x4 a1 = {0u, 0u, 0u, 0u}, a2 = {0u, 0u, 0u, 0u};
+      float plim = -INFINITY;  // NPM: d_euclid < plim passes PCL's prefilter
+      double pomw = 0.0;
+      if constexpr (NPM) {
+        const double w = lambda * (1.0 - (double)nn.w);
+        pomw = 1.0 - w;
+        // (NaN w: the exact test is NaN < thr, never an inlier)
+        plim = valid && w == w ? np_de_limit(w, thr) : -INFINITY;
+        if (hh == 0) s_pn[wv][r32] = nn;
+      } else {
         const float dx = valid ? x - tb.x : 0.f, dy = valid ? y - tb.y : 0.f;
         const float dz = valid ? z - tb.z : 0.f;
         const Split3 sx = split3(dx), sy = split3(dy), sz = split3(dz);
@@ -498,18 +522,73 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
       // prefetch the next tile of the item
       float4 tb_n = make_float4(0.f, 0.f, 0.f, 0.f);
       float xn = 0.f, yn = 0.f, zn = 0.f;
+      float4 nn_n = make_float4(0.f, 0.f, 0.f, 0.f);
       if (t + 1 < t_end) {
         tb_n = tiles[t + 1];
         const int64_t p = (int64_t)(t + 1) * kTileP + r32;
-        if (p < n) { xn = X[p]; yn = Y[p]; zn = Z[p]; }
+        if (p < n) {
+          xn = X[p]; yn = Y[p]; zn = Z[p];
+          if constexpr (NPM) nn_n = NRM[p];
+        }
       }
       int nq = 0, head = 0;
+      int qn = 0;  // NPM queue length (wave-uniform)
+      // NPM: decide the first m queued pairs with full lanes (k_score_np's np_full), keep the rest
+      auto drain = [&](int m) {
+        __builtin_amdgcn_wave_barrier();
+        if (lane < m) {
+          const uint32_t e = s_qk[wv][lane];
+          const float4 pn = s_pn[wv][e & 31u];
+          const int jj = (int)(e >> 5);
+          const float4 cf = s_cf[jj];
+          const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
+          const double w = lambda * (1.0 - (double)pn.w);
+          if (np_full(cn, pn, w, s_qb[wv][lane], thr))
+            atomicAdd(&s_cnt[jj >> 1], 1u << (16 * (jj & 1)));
+        }
+        const int rest = qn - m;
+        uint32_t mk = 0;
+        double mb = 0.0;
+        if (lane < rest) {
+          mk = s_qk[wv][m + lane];
+          mb = s_qb[wv][m + lane];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < rest) {
+          s_qk[wv][lane] = mk;
+          s_qb[wv][lane] = mb;
+        }
+        qn = rest;
+      };
       auto score = [&](int m) {
         if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
         const bool col = r32 < m;
         const int j = col ? (int)ring[(head + r32) & (kRing2 - 1)] : 0;
         if constexpr (EXP == 1) {
           if (hh == 0 && col) atomicAdd(&s_cnt[j >> 1], 1u << (16 * (j & 1)));
+          head += m;
+          return;
+        }
+        if constexpr (NPM) {
+          // lane: point r32 of the tile, planes hh * 16 .. hh * 16 + 15 of the group
+          (void)j;
+#pragma unroll 1
+          for (int q = 0; q < 16; ++q) {
+            const int kq = hh * 16 + q;
+            const bool cq = kq < m;
+            const int jq = cq ? (int)ring[(head + kq) & (kRing2 - 1)] : 0;
+            const float4 cq4 = s_cf[jq];
+            const float de = np_deuclid(cq4, x, y, z);
+            const bool near = cq && de < plim;
+            const uint64_t mm = ballot(near);
+            if (near) {
+              const int pos = qn + lanes_below(mm);
+              s_qk[wv][pos] = (uint32_t)r32 | ((uint32_t)jq << 5);
+              s_qb[wv][pos] = pomw * (double)de;
+            }
+            qn += (int)__popcll(mm);
+            if (qn >= kWave) drain(kWave);
+          }
           head += m;
           return;
         }
@@ -614,6 +693,10 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
         }
       }
       if (nq > head) score(nq - head);
+      if constexpr (NPM) {
+        if (qn > 0) drain(qn);  // the queue refers to this tile's points
+        nn = nn_n;
+      }
       tb = tb_n; x = xn; y = yn; z = zn;
     }
     }  // list passes
@@ -624,6 +707,39 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     if (c) atomicAdd(&counts[j], c);
   }
   if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
+}
+
+__global__ void k_gather_nrm(const float4* __restrict__ src, const int32_t* __restrict__ order,
+                             int64_t n, float4* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[order[i]];
+}
+
+__device__ __forceinline__ uint32_t f2ord(float f) {  // float -> order-preserving uint
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ void k_curv_range(const float4* __restrict__ nrm, int64_t n, uint32_t* __restrict__ out2) {
+  uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float c = nrm[i].w;
+    if (c == c) {
+      const uint32_t o = f2ord(c);
+      lo = min(lo, o);
+      hi = max(hi, o);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+    hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    atomicMin(&out2[0], lo);
+    atomicMax(&out2[1], hi);
+  }
 }
 }  // namespace
 
@@ -672,6 +788,37 @@ float prune_margin(float cthr, const float amax[3]) {
   return f;
 }
 
+void launch_gather_nrm(const float4* src, const int32_t* order, int64_t n, float4* dst,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_nrm, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, order,
+                     n, dst);
+}
+
+void launch_curv_range(const float4* nrm, int64_t n, uint32_t* out2, hipStream_t s) {
+  const uint32_t init[2] = {0xFFFFFFFFu, 0u};
+  (void)hipMemcpyAsync(out2, init, 8, hipMemcpyHostToDevice, s);
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(k_curv_range, dim3((unsigned)blocks), dim3(256), 0, s, nrm, n, out2);
+}
+
+float np_lim_max(double w, double thr) {  // np_de_limit (np_dev.hpp) on the host
+  if (!(w >= 0.0)) return INFINITY;
+  const double omw = 1.0 - w;
+  if (!(omw > 0.0)) return INFINITY;
+  if (!(thr > 0.0)) return thr == thr ? 0.0f : NAN;
+  float x = (float)(thr / omw);
+  if (!(x == x)) return INFINITY;
+  while (!(omw * (double)x >= thr) && x < INFINITY) x = std::nextafter(x, INFINITY);
+  while (x > 0.0f) {
+    const float y = std::nextafter(x, -INFINITY);
+    if (omw * (double)y >= thr) x = y;
+    else break;
+  }
+  return x;
+}
+
 int prune_kernel() {
   static const int k = [] {
     const char* e = std::getenv("DLG_PRUNE_KERNEL");
@@ -683,7 +830,7 @@ int prune_kernel() {
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
                          const float* band, int D, float cthr, float margin, const float amax[3],
                          int32_t* counts, uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
-                         unsigned long long* stats) {
+                         unsigned long long* stats, const PrunedNp* np) {
   if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) return;
   const int64_t ns = sp_supers(v.n);
   const int ls = prune_list_stride(D);
@@ -696,7 +843,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
   const int64_t items = (sp_tiles(v.n) + kPrChunk - 1) / kPrChunk;
   constexpr int64_t kMaxItemsPerWave = 65535 / (kPrWaves * kPrChunk * kTileP);
   static_assert(kMaxItemsPerWave >= 1, "16-bit counters");
-  const int kern = prune_kernel();
+  const int kern = np ? 2 : prune_kernel();
   static const int occ = [] {
     const char* e = std::getenv("DLG_PRUNE_OCC");
     return e ? std::atoi(e) : 4;
@@ -715,9 +862,10 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
       const int b = e ? std::atoi(e) : 1;
       return (b == 2 || b == 4) ? b : 1;
     }();
-    const bool small = bpc > 1;
-    auto* kfn = small ? (exp == 1 ? k_score_tiles_rl<1, 512> : exp == 2 ? k_score_tiles_rl<2, 512> : k_score_tiles_rl<0, 512>)
-                      : (exp == 1 ? k_score_tiles_rl<1, 1024> : exp == 2 ? k_score_tiles_rl<2, 1024> : k_score_tiles_rl<0, 1024>);
+    const bool small = bpc > 1 && !np;
+    auto* kfn = np ? k_score_tiles_rl<0, 1024, true>
+              : small ? (exp == 1 ? k_score_tiles_rl<1, 512, false> : exp == 2 ? k_score_tiles_rl<2, 512, false> : k_score_tiles_rl<0, 512, false>)
+                      : (exp == 1 ? k_score_tiles_rl<1, 1024, false> : exp == 2 ? k_score_tiles_rl<2, 1024, false> : k_score_tiles_rl<0, 1024, false>);
     const int bs = small ? 512 : 1024;
     // dynamic item claims within a workgroup; workgroups capped at blk_cap items (16-bit
     // counters), and enough of them that the caps cover every item
@@ -733,7 +881,8 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
                              (items_rl + blk_cap - 1) / blk_cap));
     hipLaunchKernelGGL(kfn, dim3((unsigned)g_rl), dim3(bs), 0, s, v.x, v.y, v.z, (int)v.n,
                        v.tiles, lp, ls, lp_n, work, blk_cap, chunk, hyps, D, cthr, margin, amax[0],
-                       amax[1], amax[2], counts, stats);
+                       amax[1], amax[2], counts, stats, np ? np->nrm : nullptr,
+                       np ? np->lambda : 0.0, np ? np->thr : 0.0);
   } else if (occ == 8) {
     hipLaunchKernelGGL(k_score_tiles_o8, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
                        v.tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);

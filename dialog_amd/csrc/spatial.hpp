@@ -66,9 +66,24 @@ inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
 int prune_kernel();
 // amax: the cloud's per-axis max |coordinate| (the scoring band's S bound).  DLG_PRUNE_KERNEL=1
 // selects the first version (k_score_tiles: global B columns, list read per tile), default 2.
+// SACMODEL_NORMAL_PLANE scoring over the spatial copy: its (normalised normal, curvature) per
+// point, and the model's lambda / threshold; margin then comes from prune_margin(lim_max, amax)
+struct PrunedNp {
+  const float4* nrm;
+  double lambda, thr;
+};
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
                          const float* band, int D, float cthr, float margin, const float amax[3],
                          int32_t* counts, uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
-                         unsigned long long* stats = nullptr);  // [6] counters (A/B tool)
+                         unsigned long long* stats = nullptr,  // [6] counters (A/B tool)
+                         const PrunedNp* np = nullptr);
+// the NORMAL_PLANE prefilter limit of the largest w (host restatement of np_de_limit): every
+// point's d_euclid limit is <= this when 0 <= w < 1 for all points; +inf otherwise
+float np_lim_max(double w_max, double thr);
+// gather the pristine normals into the Morton-ordered copy: dst[i] = src[order[i]]
+void launch_gather_nrm(const float4* src, const int32_t* order, int64_t n, float4* dst,
+                       hipStream_t s);
+// min / max of the curvature (.w) of n normals (NaN ignored) -> out2 (as ordered uint bits)
+void launch_curv_range(const float4* nrm, int64_t n, uint32_t* out2, hipStream_t s);
 
 }  // namespace dlg

@@ -101,11 +101,18 @@ def test_oracle_np_fixture():
 
 # ------------------------------------------------------------------------------------- GPU tests
 @pytest.mark.gpu
-def test_gpu_np_segment_golden(gpu_ctx):
+@pytest.mark.parametrize("pruned", ["none", "before", "after"])
+def test_gpu_np_segment_golden(gpu_ctx, pruned):
+    """pruned: the Morton-ordered copy (pruned NORMAL_PLANE scoring, spatial.hip) built before
+    or after the normals are attached (normals gathered into it either way)."""
     import dialog_amd as D
     z = np.load(os.path.join(GOLDEN, "normal_plane_small.npz"))
     cloud = D.Cloud(gpu_ctx, z["points"])
+    if pruned == "before":
+        cloud.build_spatial()
     cloud.set_normals(z["normals"])
+    if pruned == "after":
+        cloud.build_spatial()
     prm = D.make_params(float(z["seg_threshold"]), max_iterations=int(z["seg_max_iterations"]),
                         probability=float(z["seg_probability"]), model=D.SACMODEL_NORMAL_PLANE,
                         normal_distance_weight=float(z["seg_lambda"]))
@@ -118,10 +125,13 @@ def test_gpu_np_segment_golden(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_gpu_np_extract_golden(gpu_ctx):
+@pytest.mark.parametrize("pruned", [False, True])
+def test_gpu_np_extract_golden(gpu_ctx, pruned):
     import dialog_amd as D
     z = np.load(os.path.join(GOLDEN, "normal_plane_small.npz"))
     cloud = D.Cloud(gpu_ctx, z["points"])
+    if pruned:  # the Morton copy is compacted with the list (normals included) every round
+        cloud.build_spatial()
     # pcl::Normal records (stride 32) must give the same result as (n, curvature) float4
     rec = np.zeros((z["normals"].shape[0], 8), np.float32)
     rec[:, :3] = z["normals"][:, :3]
@@ -139,9 +149,10 @@ def test_gpu_np_extract_golden(gpu_ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pruned", [False, True])
 @pytest.mark.parametrize("seed,lam,thr", [(1, 0.1, 0.05), (2, 0.5, 0.1), (3, 0.0, 0.02),
                                           (4, 1.0, 0.3), (5, 0.2, 0.05)])
-def test_gpu_np_random_vs_oracle(gpu_ctx, seed, lam, thr):
+def test_gpu_np_random_vs_oracle(gpu_ctx, seed, lam, thr, pruned):
     import dialog_amd as D
     p, nrm, _, _ = cloud_with_normals(int(2000 + 3000 * seed), seed=seed, outliers=0.2)
     if seed == 5:  # NaN normals (isolated points) and a zero normal
@@ -153,6 +164,8 @@ def test_gpu_np_random_vs_oracle(gpu_ctx, seed, lam, thr):
     r = O.sac_segment(p, thr, indices=idx, max_iterations=300, normals=nrm,
                       normal_distance_weight=lam)
     cloud = D.Cloud(gpu_ctx, p, indices=idx)
+    if pruned:  # (lam = 1 with zero curvatures: w reaches 1, the exhaustive kernel runs)
+        cloud.build_spatial()
     cloud.set_normals(nrm)
     prm = D.make_params(thr, max_iterations=300, model=D.SACMODEL_NORMAL_PLANE,
                         normal_distance_weight=lam)
