@@ -404,7 +404,7 @@ __global__ __launch_bounds__(kPrBS) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 // measured no faster.)
 constexpr int kListRegs = 8;
 constexpr int kListCap = kListRegs * 2 * kWave;  // 1024 entries
-constexpr int kRing2 = 256;                       // >= 31 queued + 128 appended per list step
+constexpr int kRing2 = 512;                       // >= 31 queued + 256 appended per list step
 
 // EXP: timing experiments only (1: groups not scored, 2: no band re-decision) -- counts are
 // then wrong
@@ -665,31 +665,42 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
       // tile-sphere test of two list entries per lane (entries e0 = 2 (lane + 64 k), e0 + 1;
       // entries past the list end were zeroed at load: plane 0, masked here), packed FMAs
       const f32x2 tbx = {tb.x, tb.x}, tby = {tb.y, tb.y}, tbz = {tb.z, tb.z};
-      auto test2 = [&](uint32_t wd, int e0) {
-        const int j0 = (int)(wd & 0xFFFFu), j1 = (int)(wd >> 16);
-        const float4 c0 = s_cf[j0], c1 = s_cf[j1];
-        const f32x2 cx = {c0.x, c1.x}, cy = {c0.y, c1.y}, cz = {c0.z, c1.z}, cw = {c0.w, c1.w};
-        const f32x2 h = __builtin_elementwise_fma(cx, tbx, __builtin_elementwise_fma(cy, tby,
-                                                  __builtin_elementwise_fma(cz, tbz, cw)));
-        const bool n0 = e0 < le && fabsf(h.x) <= tlim;
-        const bool n1 = e0 + 1 < le && fabsf(h.y) <= tlim;
-        const uint64_t m0 = ballot(n0), m1 = ballot(n1);
-        const int k0 = (int)__popcll(m0);
+      // four list entries per lane per step (two list registers): four LDS reads in flight, two
+      // packed FMA chains; the ring takes <= 31 queued + 256 appended
+      auto test4 = [&](uint32_t wa, uint32_t wb, int ea) {
+        const int j0 = (int)(wa & 0xFFFFu), j1 = (int)(wa >> 16);
+        const int j2 = (int)(wb & 0xFFFFu), j3 = (int)(wb >> 16);
+        const float4 c0 = s_cf[j0], c1 = s_cf[j1], c2 = s_cf[j2], c3 = s_cf[j3];
+        const f32x2 ax2 = {c0.x, c1.x}, ay2 = {c0.y, c1.y}, az2 = {c0.z, c1.z}, aw2 = {c0.w, c1.w};
+        const f32x2 bx2 = {c2.x, c3.x}, by2 = {c2.y, c3.y}, bz2 = {c2.z, c3.z}, bw2 = {c2.w, c3.w};
+        const f32x2 ha = __builtin_elementwise_fma(ax2, tbx, __builtin_elementwise_fma(ay2, tby,
+                                                   __builtin_elementwise_fma(az2, tbz, aw2)));
+        const f32x2 hb = __builtin_elementwise_fma(bx2, tbx, __builtin_elementwise_fma(by2, tby,
+                                                   __builtin_elementwise_fma(bz2, tbz, bw2)));
+        const int eb = ea + 2 * kWave;
+        const bool n0 = ea < le && fabsf(ha.x) <= tlim;
+        const bool n1 = ea + 1 < le && fabsf(ha.y) <= tlim;
+        const bool n2 = eb < le && fabsf(hb.x) <= tlim;
+        const bool n3 = eb + 1 < le && fabsf(hb.y) <= tlim;
+        const uint64_t m0 = ballot(n0), m1 = ballot(n1), m2 = ballot(n2), m3 = ballot(n3);
+        const int k0 = (int)__popcll(m0), k1 = k0 + (int)__popcll(m1), k2 = k1 + (int)__popcll(m2);
         if (n0) ring[(nq + lanes_below(m0)) & (kRing2 - 1)] = (uint16_t)j0;
         if (n1) ring[(nq + k0 + lanes_below(m1)) & (kRing2 - 1)] = (uint16_t)j1;
-        nq += k0 + (int)__popcll(m1);
+        if (n2) ring[(nq + k1 + lanes_below(m2)) & (kRing2 - 1)] = (uint16_t)j2;
+        if (n3) ring[(nq + k2 + lanes_below(m3)) & (kRing2 - 1)] = (uint16_t)j3;
+        nq += k2 + (int)__popcll(m3);
         __builtin_amdgcn_wave_barrier();
         while (nq - head >= 32) score(32);
       };
-      {  // one copy of the test/score code: the list registers rotate through R[0]
+      {  // one copy of the test/score code: the list registers rotate through R[0], R[1]
         uint32_t R[kListRegs];
 #pragma unroll
         for (int k = 0; k < kListRegs; ++k) R[k] = L[k];
 #pragma unroll 1
-        for (int k = 0; lb + k * 2 * kWave < le; ++k) {
-          test2(R[0], lb + 2 * (lane + k * kWave));
+        for (int k = 0; lb + k * 2 * kWave < le; k += 2) {
+          test4(R[0], R[1], lb + 2 * (lane + k * kWave));
 #pragma unroll
-          for (int q = 0; q + 1 < kListRegs; ++q) R[q] = R[q + 1];
+          for (int q = 0; q + 2 < kListRegs; ++q) R[q] = R[q + 2];
         }
       }
       if (nq > head) score(nq - head);

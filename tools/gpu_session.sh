@@ -45,7 +45,7 @@ for s in $STEPS; do
     expm)   for kk in 2; do for ee in 0 1 2; do
               DLG_PRUNE_KERNEL=$kk DLG_PRUNE_EXP=$ee SCORE_AB_NOCHECK=1 VARIANTS=20 run expm_k${kk}_e${ee} 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3
             done; done ;;
-    chunk)  for cc in 1 2 4; do DLG_PRUNE_CHUNK=$cc VARIANTS=20,19 run chunk_$cc 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
+    chunk)  for cc in 2 4 8; do DLG_PRUNE_CHUNK=$cc VARIANTS=20,19 run chunk_$cc 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
     bpc)    for bb in 1 2 4; do DLG_PRUNE_BPC=$bb VARIANTS=20,19 run bpc_$bb 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
     ab)     run score_ab 600 python3 tools/score_ab.py ;;
     list)   run counters 120 rocprofv3 -L ;;
