@@ -406,8 +406,8 @@ constexpr int kListRegs = 8;
 constexpr int kListCap = kListRegs * 2 * kWave;  // 1024 entries
 constexpr int kRing2 = 512;                       // >= 31 queued + 256 appended per list step
 
-// EXP: timing experiments only (1: groups not scored, 2: no band re-decision) -- counts are
-// then wrong
+// EXP: timing experiments only (1: groups not scored, 2: no band re-decision, 3: no list
+// tests: the item/tile skeleton) -- counts are then wrong
 // NPM: SACMODEL_NORMAL_PLANE (PCL's exact prefilter b = (1 - w) d_euclid < thr as the per-point
 // float compare d_euclid < lim, k_score_np; passing pairs queued per wave and decided with full
 // lanes in double as in k_score_np), the spheres ruled out with the margin of the cloud's
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
 #pragma unroll
         for (int k = 0; k < kListRegs; ++k) R[k] = L[k];
 #pragma unroll 1
-        for (int k = 0; lb + k * 2 * kWave < le; k += 2) {
+        for (int k = 0; EXP != 3 && lb + k * 2 * kWave < le; k += 2) {
           test4(R[0], R[1], lb + 2 * (lane + k * kWave));
 #pragma unroll
           for (int q = 0; q + 2 < kListRegs; ++q) R[q] = R[q + 2];
@@ -876,7 +876,8 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
     const bool small = bpc > 1 && !np;
     auto* kfn = np ? k_score_tiles_rl<0, 1024, true>
               : small ? (exp == 1 ? k_score_tiles_rl<1, 512, false> : exp == 2 ? k_score_tiles_rl<2, 512, false> : k_score_tiles_rl<0, 512, false>)
-                      : (exp == 1 ? k_score_tiles_rl<1, 1024, false> : exp == 2 ? k_score_tiles_rl<2, 1024, false> : k_score_tiles_rl<0, 1024, false>);
+                      : (exp == 1 ? k_score_tiles_rl<1, 1024, false> : exp == 2 ? k_score_tiles_rl<2, 1024, false>
+                         : exp == 3 ? k_score_tiles_rl<3, 1024, false> : k_score_tiles_rl<0, 1024, false>);
     const int bs = small ? 512 : 1024;
     // dynamic item claims within a workgroup; workgroups capped at blk_cap items (16-bit
     // counters), and enough of them that the caps cover every item

@@ -42,7 +42,7 @@ for s in $STEPS; do
     abk)    DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=1 VARIANTS=20,19 run abk1 300 python3 tools/score_ab.py 10000000 4096 5 && \
             DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=2 VARIANTS=20,19 run abk2 300 python3 tools/score_ab.py 10000000 4096 5 ;;
     ldspmc) VARIANTS=20 run ldspmc 300 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/ldspmc -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
-    expm)   for kk in 2; do for ee in 0 1 2; do
+    expm)   for kk in 2; do for ee in 0 1 2 3; do
               DLG_PRUNE_KERNEL=$kk DLG_PRUNE_EXP=$ee SCORE_AB_NOCHECK=1 VARIANTS=20 run expm_k${kk}_e${ee} 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3
             done; done ;;
     chunk)  for cc in 2 4 8; do DLG_PRUNE_CHUNK=$cc VARIANTS=20,19 run chunk_$cc 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
