@@ -128,6 +128,74 @@ __global__ __launch_bounds__(kSbBS) void k_sphere_bounds(const float* __restrict
   if (lane == 0) supers[s] = make_float4(Cx, Cy, Cz, R * (1.0f + 0x1p-18f) + 1e-30f);
 }
 
+// k_sphere_bounds2: the same spheres with one lane per tile.  A wave stages 64 tiles (2048
+// points, two super-tiles) in LDS with coalesced loads (padded rows: lane l reads row l without
+// bank conflicts), each lane reduces its tile's box and radius, then the 32 lanes of a super-tile
+// combine their spheres.  ~4x less VALU work than a half-wave per tile.
+constexpr int kSb2Pts = 2 * kSuperP;  // points per wave (64 tiles)
+__global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__ X,
+                                                       const float* __restrict__ Y,
+                                                       const float* __restrict__ Z, int64_t n_arg,
+                                                       const int32_t* __restrict__ n_dev,
+                                                       float4* __restrict__ tiles,
+                                                       float4* __restrict__ supers) {
+  __shared__ float s_p[3][kSb2Pts + kSb2Pts / kTileP];  // row t: 33 floats
+  const int64_t n = n_dev ? (int64_t)*n_dev : n_arg;
+  const int lane = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kSb2Pts;
+  if (base >= n) return;
+  const int cnt = (int)min<int64_t>(kSb2Pts, n - base);
+#pragma unroll 4
+  for (int i = lane; i < kSb2Pts; i += kWave) {
+    const int r = i + i / kTileP;
+    if (i < cnt) {
+      s_p[0][r] = X[base + i];
+      s_p[1][r] = Y[base + i];
+      s_p[2][r] = Z[base + i];
+    }
+  }
+  __syncthreads();
+  const int np = min(kTileP, cnt - lane * kTileP);  // this lane's tile size (<= 0: none)
+  const float* px = &s_p[0][lane * (kTileP + 1)];
+  const float* py = &s_p[1][lane * (kTileP + 1)];
+  const float* pz = &s_p[2][lane * (kTileP + 1)];
+  float x0 = INFINITY, y0 = INFINITY, z0 = INFINITY, x1 = -INFINITY, y1 = -INFINITY, z1 = -INFINITY;
+  for (int i = 0; i < np; ++i) {
+    const float x = px[i], y = py[i], z = pz[i];
+    x0 = fminf(x0, x); y0 = fminf(y0, y); z0 = fminf(z0, z);
+    x1 = fmaxf(x1, x); y1 = fmaxf(y1, y); z1 = fmaxf(z1, z);
+  }
+  const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), cz = 0.5f * (z0 + z1);
+  float d = 0.0f;
+  for (int i = 0; i < np; ++i) {
+    const float dx = px[i] - cx, dy = py[i] - cy, dz = pz[i] - cz;
+    d = fmaxf(d, sqrtf(dx * dx + dy * dy + dz * dz));
+  }
+  const float rt = d * (1.0f + 0x1p-18f) + 1e-30f;
+  const int64_t t = (int64_t)blockIdx.x * (kSb2Pts / kTileP) + lane;
+  if (np > 0) tiles[t] = make_float4(cx, cy, cz, rt);
+  // super-tile of lanes 0..31 / 32..63: box over its tiles, then max |c_t - C| + r_t
+  float bx0 = x0, by0 = y0, bz0 = z0, bx1 = x1, by1 = y1, bz1 = z1;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    bx0 = fminf(bx0, __shfl_xor(bx0, o)); by0 = fminf(by0, __shfl_xor(by0, o));
+    bz0 = fminf(bz0, __shfl_xor(bz0, o));
+    bx1 = fmaxf(bx1, __shfl_xor(bx1, o)); by1 = fmaxf(by1, __shfl_xor(by1, o));
+    bz1 = fmaxf(bz1, __shfl_xor(bz1, o));
+  }
+  const float Cx = 0.5f * (bx0 + bx1), Cy = 0.5f * (by0 + by1), Cz = 0.5f * (bz0 + bz1);
+  float R = 0.0f;
+  if (np > 0) {
+    const float dx = cx - Cx, dy = cy - Cy, dz = cz - Cz;
+    R = sqrtf(dx * dx + dy * dy + dz * dz) + rt;
+  }
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) R = fmaxf(R, __shfl_xor(R, o));
+  const int half = lane >> 5;
+  if ((lane & 31) == 0 && half * kSuperP < cnt)
+    supers[(int64_t)blockIdx.x * 2 + half] = make_float4(Cx, Cy, Cz, R * (1.0f + 0x1p-18f) + 1e-30f);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Pruned countWithinDistance in two launches:
 //   k_prune_supers : every plane against every super-tile sphere (planes in LDS, 1024 threads =
@@ -784,6 +852,15 @@ void launch_gather_order(PointsView src, const int32_t* order, int64_t n, Points
 void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_t n,
                           const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s) {
   if (n <= 0) return;
+  static const int v = [] {
+    const char* e = std::getenv("DLG_SPHERE_KERNEL");
+    return e ? std::atoi(e) : 2;
+  }();
+  if (v == 2) {
+    hipLaunchKernelGGL(k_sphere_bounds2, dim3((unsigned)((n + kSb2Pts - 1) / kSb2Pts)), dim3(64), 0,
+                       s, x, y, z, n, n_dev, tiles, supers);
+    return;
+  }
   const int64_t ns = sp_supers(n);
   const int wpb = kSbBS / kWave;
   hipLaunchKernelGGL(k_sphere_bounds, dim3((unsigned)((ns + wpb - 1) / wpb)), dim3(kSbBS), 0, s,
