@@ -377,14 +377,21 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     c->samples.ensure(3 * (size_t)D);
     c->hyps.ensure(kHypScratchBytes / sizeof(HypRec) + 1);
     c->res.ensure(2 * (size_t)kMaxHypPerLaunch + 64);
-    HIPCHK(hipMemcpyAsync(c->pos.p, hp, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
-    launch_gather_samples(c->pos.p, 3 * D, offset, src, c->samples.p, c->stream);
-    if (c->comm->world() > 1) c->comm->allreduce_sum(c->samples.p, 12 * (size_t)D, DType::I32, c->stream);
     // res = counts[Dp] | good[D]  (Dp = D rounded up to the 64-hypothesis groups of k_score)
     const int Dp = (D + 63) / 64 * 64;
-    launch_build_hyps(c->samples.p, D, cthr, cl->amax[0], cl->amax[1], cl->amax[2], c->hyps.p,
-                      c->res.p + Dp, c->stream);
-    HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
+    if (c->comm->world() == 1) {
+      // one launch: positions read from the pinned host buffer (the next round's draw rewrites
+      // it only after this round's results were published, i.e. after this kernel ran)
+      launch_gather_build(hp, D, src, c->samples.p, cthr, cl->amax[0], cl->amax[1], cl->amax[2],
+                          c->hyps.p, c->res.p, c->stream);
+    } else {
+      HIPCHK(hipMemcpyAsync(c->pos.p, hp, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
+      launch_gather_samples(c->pos.p, 3 * D, offset, src, c->samples.p, c->stream);
+      c->comm->allreduce_sum(c->samples.p, 12 * (size_t)D, DType::I32, c->stream);
+      launch_build_hyps(c->samples.p, D, cthr, cl->amax[0], cl->amax[1], cl->amax[2], c->hyps.p,
+                        c->res.p + Dp, c->stream);
+      HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
+    }
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     if (pruned_np) {
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);

@@ -48,20 +48,10 @@ __global__ void k_gather_samples(const int32_t* __restrict__ pos, int m, int64_t
 }
 
 // isSampleGood + computeModelCoefficients (sac_model_plane.hpp), one thread per draw.
-__global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, int Dp, float cthr, float ax,
-                             float ay, float az, HypRec* __restrict__ hyps,
-                             int32_t* __restrict__ good_out) {
-  int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= Dp) return;
-  if (d >= D) {  // padding up to the 64-plane groups of k_score: NaN planes count nothing
-    HypRec h;
-    h.a = h.b = h.c = h.d = __builtin_nanf("");
-    h.tlo = h.thi = h.w = 0.0f;
-    h.good = 0;
-    hyps[d] = h;
-    return;
-  }
-  const SampleRec s0 = s[3 * d], s1 = s[3 * d + 1], s2 = s[3 * d + 2];
+// isSampleGood + computeModelCoefficients of one draw, in PCL's op order
+__device__ __forceinline__ HypRec build_hyp(const SampleRec s0, const SampleRec s1,
+                                            const SampleRec s2, float cthr, float ax, float ay,
+                                            float az) {
   float a0 = s1.x - s0.x, a1 = s1.y - s0.y, a2 = s1.z - s0.z;
   float b0 = s2.x - s0.x, b1 = s2.y - s0.y, b2 = s2.z - s0.z;
   float r0 = a0 / b0, r1 = a1 / b1, r2 = a2 / b2;
@@ -94,8 +84,56 @@ __global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, int Dp, flo
     h.a = h.b = h.c = h.d = __builtin_nanf("");
     h.tlo = h.thi = h.w = 0.0f;
   }
+  return h;
+}
+
+__device__ __forceinline__ HypRec nan_hyp() {  // padding / not a plane: counts nothing
+  HypRec h;
+  h.a = h.b = h.c = h.d = __builtin_nanf("");
+  h.tlo = h.thi = h.w = 0.0f;
+  h.good = 0;
+  return h;
+}
+
+__global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, int Dp, float cthr, float ax,
+                             float ay, float az, HypRec* __restrict__ hyps,
+                             int32_t* __restrict__ good_out) {
+  int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= Dp) return;
+  if (d >= D) {  // padding up to the 64-plane groups of k_score: NaN planes count nothing
+    hyps[d] = nan_hyp();
+    return;
+  }
+  const HypRec h = build_hyp(s[3 * d], s[3 * d + 1], s[3 * d + 2], cthr, ax, ay, az);
   hyps[d] = h;
   good_out[d] = h.good;
+}
+
+// one rank: gather the three samples of each draw (positions read from the pinned host buffer),
+// build the hypothesis, zero its count -- one launch instead of copy + gather + build + memset
+__global__ void k_gather_build(const int32_t* pos, int D, int Dp, PointsView src,
+                               SampleRec* __restrict__ samples, float cthr, float ax, float ay,
+                               float az, HypRec* __restrict__ hyps, int32_t* __restrict__ res) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= Dp) return;
+  res[d] = 0;  // counts[Dp]
+  if (d >= D) {
+    hyps[d] = nan_hyp();
+    return;
+  }
+  SampleRec r[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int64_t p = pos[3 * d + i];
+    r[i].gid = 0; r[i].x = 0.0f; r[i].y = 0.0f; r[i].z = 0.0f;
+    if (p >= 0 && p < src.n) {
+      r[i].gid = src.gid[p]; r[i].x = src.x[p]; r[i].y = src.y[p]; r[i].z = src.z[p];
+    }
+    samples[3 * d + i] = r[i];
+  }
+  const HypRec h = build_hyp(r[0], r[1], r[2], cthr, ax, ay, az);
+  hyps[d] = h;
+  res[Dp + d] = h.good;  // good[D]
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1301,6 +1339,15 @@ void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src
                            hipStream_t s) {
   if (m <= 0) return;
   hipLaunchKernelGGL(k_gather_samples, dim3(cdiv(m, 256)), dim3(256), 0, s, pos, m, lo, src, out);
+}
+
+void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleRec* samples,
+                         float cthr, float ax, float ay, float az, HypRec* hyps, int32_t* res,
+                         hipStream_t s) {
+  if (D <= 0) return;
+  const int Dp = (D + 63) / 64 * 64;
+  hipLaunchKernelGGL(k_gather_build, dim3(cdiv(Dp, 256)), dim3(256), 0, s, pos_host, D, Dp, src,
+                     samples, cthr, ax, ay, az, hyps, res);
 }
 
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,

@@ -111,6 +111,11 @@ void launch_publish(const int32_t* totals, int ntot, const float4* small, int ns
 void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
                     const SampleRec* samples, HypRec* best, SampleRec* best_smp, int32_t* out,
                     hipStream_t s);
+// one rank: positions (pinned host buffer, 3 per draw) -> samples, hypotheses, good flags in
+// res[Dp + d] and zeroed counts res[0, Dp)  (gather + build + memset in one launch)
+void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleRec* samples,
+                         float cthr, float ax, float ay, float az, HypRec* hyps, int32_t* res,
+                         hipStream_t s);
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,
                        HypRec* hyps, int32_t* good, hipStream_t s);
 // counts[D] = #{i < n : |plane_h . (x_i, y_i, z_i, 1)| < cthr}, PCL (Eigen SSE) op order.
