@@ -485,14 +485,20 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       HIPCHK(hipEventRecord(c->ev_sel[sk][0], c->stream));
     }
     if (!pcl_refit) {
-      if (prm.optimize) {
+      if (prm.optimize && c->comm->world() == 1) {
         const int nb = moments_blocks(src.n);
         c->partials.ensure((size_t)nb * kMomentK);
-        launch_moments(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p, c->stream);
-        if (c->comm->world() > 1)
+        launch_moments_refit(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p,
+                             rc_dev, c->stream);
+      } else {
+        if (prm.optimize) {
+          const int nb = moments_blocks(src.n);
+          c->partials.ensure((size_t)nb * kMomentK);
+          launch_moments(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p, c->stream);
           c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
+        }
+        launch_refit_moments(c->moments.p, best_smp_dev, bc_dev, prm.optimize, rc_dev, c->stream);
       }
-      launch_refit_moments(c->moments.p, best_smp_dev, bc_dev, prm.optimize, rc_dev, c->stream);
     } else {
       // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
       c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));

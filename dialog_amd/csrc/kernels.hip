@@ -944,6 +944,32 @@ __global__ void k_refit_moments(const double* __restrict__ mom, const SampleRec*
   *cout = make_float4(co[0], co[1], co[2], co[3]);
 }
 
+// one rank: k_reduce_partials + k_refit_moments in one launch (the allreduce of the moments that
+// separates them with several ranks is the identity)
+__global__ void k_reduce_refit(const double* __restrict__ partials, int nb, double* __restrict__ out,
+                               const SampleRec* __restrict__ shp, const float4* __restrict__ cin,
+                               float4* __restrict__ cout) {
+  __shared__ double s_m[kMomentK];
+  const int k = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  if (k < kMomentK) {
+    double v = 0.0;
+    for (int b = lane; b < nb; b += kWave) v += partials[(int64_t)b * kMomentK + k];
+    v = wave_sum_d(v);
+    if (lane == 0) {
+      s_m[k] = v;
+      out[k] = v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const float4 c = *cin;
+  const float ci[4] = {c.x, c.y, c.z, c.w};
+  float co[4] = {c.x, c.y, c.z, c.w};
+  const double sh[3] = {(double)shp->x, (double)shp->y, (double)shp->z};
+  refit_from_moments(s_m, sh, ci, co);
+  *cout = make_float4(co[0], co[1], co[2], co[3]);
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_pick_p1: RandomSampleConsensus::computeModel's decision over one batch of draws when the
 // probability is 1 (log(1 - p) = -inf, so k = +inf and only the iteration cap ends the loop):
@@ -1534,6 +1560,19 @@ int moments_blocks(int64_t n) {
 void launch_refit_moments(const double* moments, const SampleRec* shift, const float4* cin,
                           int optimize, float4* cout, hipStream_t s) {
   hipLaunchKernelGGL(k_refit_moments, dim3(1), dim3(64), 0, s, moments, shift, cin, optimize, cout);
+}
+
+void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt,
+                          const SampleRec* shift, double* partials, int nblocks, double* out,
+                          float4* cout, hipStream_t s) {
+  if (mt.normal_plane)
+    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
+                       partials);
+  else
+    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
+                       partials);
+  hipLaunchKernelGGL(k_reduce_refit, dim3(1), dim3(kMomentK * kWave), 0, s, partials, nblocks, out,
+                     shift, coef, cout);
 }
 
 void launch_moments(PointsView src, const float4* coef, const ModelTest& mt,

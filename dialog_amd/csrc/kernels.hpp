@@ -134,6 +134,10 @@ void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest&
 // partials [nblocks][10] -> out[10] (fixed-order reduction: deterministic)
 int moments_blocks(int64_t n);
 // coef: device float4 (a, b, c, d); shift: the device sample point the moments are centred on
+// one rank: moments of the unrefined plane's inliers + reduction + refit in two launches
+void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt,
+                          const SampleRec* shift, double* partials, int nblocks, double* out,
+                          float4* cout, hipStream_t s);
 void launch_moments(PointsView src, const float4* coef, const ModelTest& mt,
                     const SampleRec* shift, double* partials, int nblocks, double* out,
                     hipStream_t s);
