@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--torch-dist", action="store_true",
                     help="rendezvous through torch.distributed even at N=1 (runtime check)")
+    ap.add_argument("--no-events", action="store_true",
+                    help="no HIP timing events in the timed steps (A/B of their host cost)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the C5 (normals + NORMAL_PLANE + post-process) secondary measurement")
     return ap.parse_args()
@@ -140,7 +142,7 @@ def main():
         ctx = D.Context.distributed(local, rank, world, box[0])
     else:
         ctx = D.Context(local)
-    ctx.set_profiling(True)
+    ctx.set_profiling(not a.no_events)
 
     seed = SEED_BASE + 3
     t0 = time.time()

@@ -184,6 +184,7 @@ struct SegOut {
   int64_t n_in_global = 0;
   bool sp_compacted = false;  // the spatial copy's survivors are in its spare buffer
   int64_t sp_n_out = 0;
+  bool lean = false;  // lean-list round: the spare list buffer holds pristine indices only
   // every rank's refined inliers / survivors (device allgather folded into the round's sync)
   std::vector<int64_t> in_ranks, out_ranks;
 };
@@ -227,7 +228,7 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
     k0.ensure(n); k1.ensure(n); i0.ensure(n); i1.ensure(n);
     const size_t tb = morton_sort_temp_bytes(n);
     tmp.ensure(std::max<size_t>(tb, 16));
-    c->totals.ensure(4);
+    c->totals.ensure(8);
     HIPCHK(hipMemsetAsync(c->totals.p, 0, 4, c->stream));
     launch_morton_keys(cl->pristine.view(n), cl->amax[0], cl->amax[1], cl->amax[2], k0.p, i0.p,
                        c->totals.p, c->stream);
@@ -282,6 +283,37 @@ void ensure_sphere_bounds(dlg_ctx* c, dlg_cloud* cl) {
   cl->sp_dirty = false;
 }
 
+// lean-list rounds (single-pass selects driven by the Morton copy): DLG_LEAN=0 disables them
+bool lean_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLG_LEAN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// a lean list's coordinates (and ids, normals) from the pristine copy, before any path that
+// reads them
+void ensure_list_xyz(dlg_ctx* c, dlg_cloud* cl) {
+  if (!cl->list_lean()) return;
+  SoA& b = cl->buf[cl->cur];
+  if (cl->pristine.with_nrm) b.ensure_nrm((size_t)std::max<int64_t>(cl->n_active, 1));
+  PointsOut io = b.out();
+  if (!cl->pristine.with_nrm) io.nrm = nullptr;
+  launch_list_materialize(cl->pristine.view(cl->n_total), cl->n_active, io, c->stream);
+  HIPCHK(hipGetLastError());
+  cl->buf_lean[cl->cur] = false;
+}
+
+void ensure_sel1(dlg_ctx* c, int64_t n) {
+  const size_t nt = (size_t)select_tiles(n) + 1;
+  if (nt > c->sel1_status.cap) {
+    c->sel1_status.ensure(nt);
+    HIPCHK(hipMemsetAsync(c->sel1_status.p, 0, sizeof(uint64_t) * c->sel1_status.cap, c->stream));
+  }
+  c->sel1.status = c->sel1_status.p;
+}
+
 // one SACSegmentation::segment() over the cloud's active list (all ranks)
 // active_ranks: every rank's active count when the caller already knows it (the extract loop
 // carries it from the previous round's survivors), else allgathered here
@@ -315,7 +347,17 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   if (prm.threshold == DBL_MAX) return out;  // PCL: "No threshold set!" -> computeModel false
   if (N < 3) return out;                      // getSamples: cannot select 3 unique points
 
+  // lean-list round: plane model over the Morton copy, single rank, device refit, a list that
+  // is pristine or already lean (a list compacted with coordinates stays on the full path)
+  const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
+  const bool lean = compact && !np && !pcl_refit && lean_enabled() && c->comm->world() == 1 &&
+                    cl->sp_valid && cl->sp_n > 0 && cl->n_total < (int64_t(1) << 30) &&
+                    score_variant() == kScoreDefault && prune_mode() != 0 &&
+                    (cl->cur < 0 || cl->buf_lean[cl->cur]);
+  if (!lean) ensure_list_xyz(c, cl);
   const PointsView src = cl->view();
+  // the lean list's pristine indices (null while the list is the pristine one)
+  const int32_t* lidx = lean && cl->cur >= 0 ? cl->buf[cl->cur].gid.p : nullptr;
   const float cthr = thr_ceil(prm.threshold);
   ModelTest mt;
   mt.cthr = cthr;
@@ -354,7 +396,6 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // The counts still come back with the round's sync and the host replays them
   // (RansacControl::consume); on any disagreement, or when the loop needs more draws (bad
   // samples), the round continues on the exact host path and the refit + select are redone.
-  const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
   const bool spec = spec_pick_enabled() && prm.probability == 1.0 && prm.max_iterations >= 0 &&
                     (int64_t)prm.max_iterations + 1 <= cap_h;
   c->pick.ensure(4);
@@ -382,8 +423,13 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (c->comm->world() == 1) {
       // one launch: positions read from the pinned host buffer (the next round's draw rewrites
       // it only after this round's results were published, i.e. after this kernel ran)
-      launch_gather_build(hp, D, src, c->samples.p, cthr, cl->amax[0], cl->amax[1], cl->amax[2],
-                          c->hyps.p, c->res.p, c->stream);
+      if (lean)
+        launch_gather_build(hp, D, cl->pristine.view(cl->n_total), c->samples.p, cthr,
+                            cl->amax[0], cl->amax[1], cl->amax[2], c->hyps.p, c->res.p, c->stream,
+                            lidx, src.n);
+      else
+        launch_gather_build(hp, D, src, c->samples.p, cthr, cl->amax[0], cl->amax[1],
+                            cl->amax[2], c->hyps.p, c->res.p, c->stream);
     } else {
       HIPCHK(hipMemcpyAsync(c->pos.p, hp, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
       launch_gather_samples(c->pos.p, 3 * D, offset, src, c->samples.p, c->stream);
@@ -460,7 +506,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   c->tile_in.ensure(nt + 1);
   c->tile_off_in.ensure(nt + 1);
   c->tile_off_out.ensure(nt + 1);
-  c->totals.ensure(4);
+  c->totals.ensure(8);
   c->h_tot.ensure(4);
   c->h_small.ensure(8);
   c->inl_gid.ensure((size_t)std::max<int64_t>(src.n, 1));
@@ -473,11 +519,24 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     dst = sp.out();
   }
   const bool sp_compact = compact && cl->sp_valid && (!np || cl->sp_soa().with_nrm);
+  auto sp_cur_view = [&]() {
+    const SoA& ss = cl->sp_soa();
+    return PointsView{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n, nullptr};
+  };
+  if (lean && cl->tag.cap < (size_t)cl->n_total) {
+    cl->tag.ensure((size_t)std::max<int64_t>(cl->n_total, 1));
+    HIPCHK(hipMemsetAsync(cl->tag.p, 0, cl->tag.cap, c->stream));
+    cl->tagv = 0;
+  }
   auto refit_select = [&]() {
     // Fast mode (and no optimisation) never leave the device: moments of the unrefined plane's
     // inliers (k_moments, centred on the winning sample), the double eigen33 refit in a
     // one-thread kernel, then the select with the refined plane read from device memory.  PCL
     // mode needs the host's sequential float sums in between.
+    if (c->stage_inflight) {  // the previous round's inlier copy still reads inl_gid
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_stage, 0));
+      c->stage_inflight = false;
+    }
     const int sk = c->sel_k;  // this round's pair of select timing events
     if (c->profiling) {
       for (auto& ev : c->ev_sel[sk])
@@ -486,9 +545,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     }
     if (!pcl_refit) {
       if (prm.optimize && c->comm->world() == 1) {
-        const int nb = moments_blocks(src.n);
+        // (lean: the moments of the Morton copy -- the same finite inliers)
+        const PointsView mv = lean ? sp_cur_view() : src;
+        const int nb = moments_blocks(mv.n);
         c->partials.ensure((size_t)nb * kMomentK);
-        launch_moments_refit(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p,
+        launch_moments_refit(mv, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p,
                              rc_dev, c->stream);
       } else {
         if (prm.optimize) {
@@ -523,8 +584,23 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // round's totals final, they are published right away, and the scatters (inlier ids,
     // survivors of both copies) and the sphere bounds run while the host reads them and draws
     // the next round
-    launch_select_head(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
-                       c->totals.p, c->stream);
+    // (lean: the Morton copy's single-pass select makes the totals final and stamps the inliers)
+    if (lean) {
+      if (++cl->tagv > 255) {
+        HIPCHK(hipMemsetAsync(cl->tag.p, 0, (size_t)cl->n_total, c->stream));
+        cl->tagv = 1;
+      }
+      ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n));
+      SoA& sd = cl->sp_buf[cl->sp_spare()];
+      sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
+      PointsOut spo = sd.out();
+      spo.nrm = nullptr;
+      launch_sel1_morton(sp_cur_view(), rc_dev, mt, c->sel1, cl->tag.p, (uint8_t)cl->tagv, spo,
+                         src.n, c->totals.p, c->stream);
+    } else {
+      launch_select_head(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
+                         c->totals.p, c->stream);
+    }
     HIPCHK(hipGetLastError());
     const int W = c->comm->world();
     if (W > 1) {  // every rank's (in, out): the extract loop needs no host-synced allgather
@@ -554,11 +630,25 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     spec_pending = false;
     if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_tot, c->stream));
-    launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p, nullptr,
-                       compact ? &dst : nullptr, c->stream);
+    if (lean) {
+      // the list from the stamps (ids in list order; survivors' pristine indices), then the
+      // sphere bounds of the Morton survivors (count in totals[4])
+      launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv, cl->pristine.gid.p, c->sel1,
+                       c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream);
+      if (c->profiling) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
+      const int b = cl->sp_spare();
+      SoA& sd = cl->sp_buf[b];
+      cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+      cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+      launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
+                           cl->sp_sb[b].p, c->stream);
+    } else {
+      launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
+                         nullptr, compact ? &dst : nullptr, c->stream);
+    }
     // the Morton copy loses the same points (same predicate, same float inputs): its totals
     // land in totals[2..3], checked at the next publish / the end of the extraction
-    if (sp_compact) {
+    if (sp_compact && !lean) {
       SoA& sd = cl->sp_buf[cl->sp_spare()];
       sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
       const SoA& ss = cl->sp_soa();
@@ -580,13 +670,15 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                            cl->sp_sb[b].p, c->stream);
     }
     HIPCHK(hipGetLastError());
-    if (c->profiling && !sp_compact) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
+    if (c->profiling && !sp_compact && !lean) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
     const double t_wait0 = trace_on() ? now_ms() : 0.0;
     wait_published(c, seq);
     if (trace_on())
       std::fprintf(stderr, "[dlg] select enqueue=%.3fms wait=%.3fms\n", t_wait0 - t_ref0, now_ms() - t_wait0);
     if (trace_on()) c->t_tot = now_ms();
     std::memcpy(c->h_tot.p, c->pub + kPubTot, 16);
+    if (c->h_tot.p[0] < 0)  // (k_sel1_morton's look-back gave up: nothing was scattered)
+      throw DlgError(DLG_ERR_INTERNAL, "single-pass select did not complete");
     std::memcpy(c->h_small.p, c->pub + kPubSmall, 6 * sizeof(float4));
     if (W > 1) std::memcpy(c->h_rk.p, c->pub + kPubRk, 8 * (size_t)W);
     check_sp_totals(c, c->h_tot.p + 2);
@@ -669,7 +761,16 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     out.n_in_global = 0;
     for (int64_t v : out.in_ranks) out.n_in_global += v;
   }
-  if (sp_compact) {
+  if (lean) {
+    // the Morton copy decided the inliers; the list pass's own totals (totals[2..3]) must agree
+    // with them (checked at the next publish, check_sp_totals)
+    out.lean = true;
+    out.sp_compacted = true;
+    out.sp_n_out = cl->sp_n - out.n_in_local;
+    c->sp_expect_in = out.n_in_local;
+    c->sp_expect_out = out.n_out_local;
+    c->sp_check = out.n_in_local != 0 || out.n_out_local != 0;
+  } else if (sp_compact) {
     // non-finite points are never inliers: the Morton copy loses exactly the list's inliers
     // (its own totals are checked at the next publish, check_sp_totals)
     out.sp_compacted = true;
@@ -711,10 +812,14 @@ int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, in
       c->h_stage.ensure((size_t)so.n_in_local);
       if (!c->ev_stage) HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
       const double t2 = trace_on() ? now_ms() : 0.0;
+      if (!c->ev_inl) HIPCHK(hipEventCreateWithFlags(&c->ev_inl, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(c->ev_inl, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_inl, 0));
       HIPCHK(hipMemcpyAsync(c->h_stage.p, c->inl_gid.p, (size_t)so.n_in_local * 4,
-                            hipMemcpyDeviceToHost, c->stream));
+                            hipMemcpyDeviceToHost, c->cstream));
       const double t3 = trace_on() ? now_ms() : 0.0;
-      HIPCHK(hipEventRecord(c->ev_stage, c->stream));
+      HIPCHK(hipEventRecord(c->ev_stage, c->cstream));
+      c->stage_inflight = true;  // inl_gid is read until ev_stage
       if (trace_on())
         std::fprintf(stderr, "[dlg] emit n=%lld cap=%zu drain %.3f ensure %.3f copy %.3f record %.3f ms\n",
                      (long long)so.n_in_local, c->h_stage.cap, t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
@@ -746,6 +851,7 @@ dlg_status init_ctx(dlg_ctx* c, int device) {
   c->num_cus = p.multiProcessorCount;
   return guarded(c, [&] {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
   });
 }
@@ -874,6 +980,11 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->nw.release();
   c->pw.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
+  if (c->ev_inl) (void)hipEventDestroy(c->ev_inl);
+  if (c->cstream) {
+    (void)hipStreamSynchronize(c->cstream);
+    (void)hipStreamDestroy(c->cstream);
+  }
   if (c->ev_tot) (void)hipEventDestroy(c->ev_tot);
   for (auto& pr : c->ev_sel)
     for (auto& ev : pr)
@@ -948,7 +1059,7 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
       HIPCHK(hipMemcpyAsync(cl->pristine.gid.p, g.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
       sync(c);  // the host vectors go out of scope
     }
-    c->totals.ensure(4);
+    c->totals.ensure(8);
     launch_absmax(cl->pristine.view(n), reinterpret_cast<uint32_t*>(c->totals.p), c->stream);
     uint32_t bits[3];
     HIPCHK(hipMemcpyAsync(bits, c->totals.p, 12, hipMemcpyDeviceToHost, c->stream));
@@ -1137,6 +1248,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       written += n;
       offsets_out[p + 1] = written;
       *n_planes = p + 1;
+      cl->buf_lean[cl->spare()] = so.lean;
       cl->cur = cl->spare();  // commit the removal
       cl->n_active = so.n_out_local;
       active = so.out_ranks;
@@ -1169,6 +1281,7 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
                                double threshold, double* ms_per_launch, int32_t* counts_out) {
   if (!c || !cl || D < 1 || D > kMaxHypPerLaunch || reps < 1 || !ms_per_launch) return DLG_ERR_INVALID;
   return guarded(c, [&] {
+    ensure_list_xyz(c, cl);
     const PointsView src = cl->view();
     if (src.n < 3) throw DlgError(DLG_ERR_INVALID, "need >= 3 active points");
     Mt19937 rng(777u);

@@ -161,6 +161,8 @@ struct dlg_ctx {
   DevBuf<HypRec> hyps;
   DevBuf<int32_t> res;  // counts[D] | good[D]
   DevBuf<int32_t> tile_in, tile_off_in, tile_off_out, totals;
+  dlg::Sel1State sel1;  // single-pass selects: tile status words + launch epoch
+  DevBuf<uint64_t> sel1_status;
   DevBuf<double> partials, moments;
   DevBuf<int32_t> inl_gid;
   DevBuf<float> inl_xyz;
@@ -181,6 +183,11 @@ struct dlg_ctx {
   // kernel executes (the host would otherwise only wait for it)
   PinBuf<int32_t> h_stage;
   hipEvent_t ev_stage = nullptr;
+  // the deferred inlier copy runs on its own stream, off the rounds' critical path: it waits for
+  // ev_inl (the round's select on the main stream); the next select waits for ev_stage
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_inl = nullptr;
+  bool stage_inflight = false;
   hipEvent_t ev_tot = nullptr;
   DevBuf<int32_t> pick;   // k_pick_p1 result
   int32_t* pub = nullptr;  // coherent pinned: k_publish's round results (pub[0] = sequence)
@@ -235,6 +242,12 @@ struct dlg_cloud {
     return s.view(n_active);
   }
   int spare() const { return cur == 0 ? 1 : 0; }
+  // lean-list rounds (driver.cpp): the list buffer holds only pristine indices (in its gid
+  // field; x, y, z, normals stale) until a path that reads coordinates materialises it
+  bool buf_lean[2] = {false, false};
+  bool list_lean() const { return cur >= 0 && buf_lean[cur]; }
+  DevBuf<uint8_t> tag;  // per pristine point: the stamp of the select that took it
+  int tagv = 0;         // last stamp used (tag[] is zeroed when the byte wraps)
 };
 
 namespace dlg {

@@ -112,6 +112,7 @@ __global__ void k_build_hyps(const SampleRec* __restrict__ s, int D, int Dp, flo
 // one rank: gather the three samples of each draw (positions read from the pinned host buffer),
 // build the hypothesis, zero its count -- one launch instead of copy + gather + build + memset
 __global__ void k_gather_build(const int32_t* pos, int D, int Dp, PointsView src,
+                               const int32_t* __restrict__ lidx, int64_t n_list,
                                SampleRec* __restrict__ samples, float cthr, float ax, float ay,
                                float az, HypRec* __restrict__ hyps, int32_t* __restrict__ res) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -126,8 +127,9 @@ __global__ void k_gather_build(const int32_t* pos, int D, int Dp, PointsView src
   for (int i = 0; i < 3; ++i) {
     const int64_t p = pos[3 * d + i];
     r[i].gid = 0; r[i].x = 0.0f; r[i].y = 0.0f; r[i].z = 0.0f;
-    if (p >= 0 && p < src.n) {
-      r[i].gid = src.gid[p]; r[i].x = src.x[p]; r[i].y = src.y[p]; r[i].z = src.z[p];
+    if (p >= 0 && p < n_list) {
+      const int64_t q = lidx ? lidx[p] : p;  // lean list: pristine index -> pristine copy
+      r[i].gid = src.gid[q]; r[i].x = src.x[q]; r[i].y = src.y[q]; r[i].z = src.z[q];
     }
     samples[3 * d + i] = r[i];
   }
@@ -1209,6 +1211,266 @@ __global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Single-pass select / compaction (the "lean list" rounds).  The plane's inliers are decided
+// once, on the Morton copy: k_sel1_morton compacts the survivors of the Morton copy and stamps
+// each inlier's pristine index in a byte array with the select's tag; the active list, which
+// then only holds pristine indices (ascending: list order is pristine order minus the removed
+// points), is compacted by k_sel1_list from the stamps alone, emitting the inlier ids in list
+// order (PCL's order) -- 9 B per list point instead of the 44 B of count + scatter over the
+// list-ordered xyz.
+//
+// Both are one pass: a workgroup claims the next 4096-point tile from a monotone counter, counts
+// its inliers, and takes its exclusive prefix by decoupled look-back over the tile status words
+// (epoch << 32 | flag << 30 | value; flag 1 = tile aggregate, 2 = inclusive prefix).  Tiles are
+// claimed in order, so every tile a workgroup waits on is already running: the look-back always
+// completes.  Survivor positions need no second scan: every tile but the last is full, so the
+// survivors before element e of tile t are t * 4096 + local(e) - (inliers before e).
+// (large tiles keep the look-back short: a round's few hundred tiles are all resident at once,
+// and each look-back window of 64 tiles costs one uncached round trip)
+constexpr int kS1BS = 1024;
+constexpr int kS1It = 16;                          // points per lane, lane-strided
+constexpr int kS1Tile = kS1BS * kS1It;             // 16384 points per tile
+constexpr int kS1Slots = kS1It * (kS1BS / kWave);  // (j, wave) counts of a tile: 256
+static_assert(kS1Slots % kWave == 0 && kS1Slots <= kS1BS, "slot scan layout");
+int sel1_tiles(int64_t n) { return (int)((n + kS1Tile - 1) / kS1Tile); }
+
+// tile = workgroup index: workgroups are dispatched in index order on each XCD, so the lowest
+// unfinished tile has every predecessor done and always completes (a claim counter would be
+// one same-address device atomic per tile, measured slower).  The look-back still carries an
+// exit: after kS1Spin empty polls the tile gives up, scatters nothing and reports -1 in its
+// totals, which the host turns into an error.
+constexpr int kS1Spin = 1 << 20;
+
+// in-tile exclusive ranks from the (j, wave) counts in s_cnt, the tile's exclusive prefix by
+// look-back; returns the prefix (workgroup-uniform), s_pre[] = in-tile exclusive offsets
+__device__ __forceinline__ int sel1_scan(const Sel1State& L, int tile, int* s_cnt, int* s_pre,
+                                         int* s_base) {
+  __shared__ int s_wt[kS1Slots / kWave];
+  __syncthreads();
+  const int t = threadIdx.x, lane = t & (kWave - 1);
+  int v = 0, inc = 0;
+  if (t < kS1Slots) {
+    v = s_cnt[t];
+    inc = v;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int u = __shfl_up(inc, off, kWave);
+      if (lane >= off) inc += u;
+    }
+    if (lane == kWave - 1) s_wt[t / kWave] = inc;
+  }
+  __syncthreads();
+  int agg = 0;
+#pragma unroll
+  for (int q = 0; q < kS1Slots / kWave; ++q) {
+    if (t < kS1Slots && q < t / kWave) inc += s_wt[q];
+    agg += s_wt[q];
+  }
+  if (t < kS1Slots) s_pre[t] = inc - v;
+  if (t < kWave) {
+    const uint64_t ep = (uint64_t)L.epoch << 32;
+    int excl = 0;
+    if (tile == 0) {
+      if (lane == 0)
+        __hip_atomic_store(L.status, ep | (2ull << 30) | (uint32_t)agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(L.status + tile, ep | (1ull << 30) | (uint32_t)agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      // K windows of 64 tiles per round trip: with every tile of a round resident at once,
+      // a tile's nearest published prefix can be hundreds of tiles back
+      constexpr int K = 1;
+      int look = tile - 1, spins = 0;
+      for (;;) {
+        uint32_t f[K], val[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int idx = look - lane - k * kWave;
+          f[k] = 2u;
+          val[k] = 0u;
+          if (idx >= 0) {
+            const uint64_t w = __hip_atomic_load(L.status + idx, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            f[k] = (uint32_t)(w >> 32) == L.epoch ? (uint32_t)(w >> 30) & 3u : 0u;
+            val[k] = (uint32_t)w & 0x3FFFFFFFu;
+          }
+        }
+        // the nearest window holding a prefix, and the lanes of it that are needed
+        int kp = K, fp = kWave;
+        bool missing = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (kp == K && !missing) {
+            const uint64_t pm = ballot(f[k] == 2u), zm = ballot(f[k] == 0u);
+            const int q = pm ? __builtin_ctzll(pm) : kWave;
+            const uint64_t need = q >= kWave - 1 ? ~0ull : ((2ull << q) - 1ull);
+            if (zm & need) missing = true;
+            else if (q < kWave) { kp = k; fp = q; }
+          }
+        }
+        if (missing) {
+          if (++spins > kS1Spin) {
+            excl = -1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;  // a tile in range has not published yet
+        }
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          c += (k < kp || (k == kp && lane <= fp)) ? (int)val[k] : 0;
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, kWave);
+        excl += c;
+        if (kp < K) break;
+        look -= K * kWave;
+      }
+      if (lane == 0 && excl >= 0)
+        __hip_atomic_store(L.status + tile, ep | (2ull << 30) | (uint32_t)(excl + agg),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_base[0] = excl;
+      s_base[1] = agg;
+    }
+  }
+  __syncthreads();
+  return s_base[0];
+}
+
+// the Morton copy's select: survivors compacted into dst (Morton order kept), inliers stamped
+// in tag[] by pristine index (the Morton copy's gid field holds it); the last tile writes
+// totals[0] = inliers, totals[1] = list survivors (n_list - inliers), totals[4] = Morton survivors
+template <bool NP>
+__global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const float4* __restrict__ cfp,
+                                                       ModelTest mt, Sel1State L,
+                                                       uint8_t* __restrict__ tag, uint8_t tagv,
+                                                       PointsOut dst, int64_t n_list, int ntiles,
+                                                       int32_t* __restrict__ totals) {
+  __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
+  const int tile = blockIdx.x;
+  const float4 cf = *cfp;
+  const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
+  const int w = threadIdx.x / kWave;
+  const int64_t base = (int64_t)tile * kS1Tile;
+  float x[kS1It], y[kS1It], z[kS1It];
+  int32_t g[kS1It];
+  uint64_t m[kS1It];
+  // (clamped, unconditional loads: all 64 in flight at once; a guarded load per element would
+  // be a branch, and the compiler waits for each before the next)
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = min<int64_t>(base + j * kS1BS + threadIdx.x, src.n - 1);
+    x[j] = src.x[e]; y[j] = src.y[e]; z[j] = src.z[e]; g[j] = src.gid[e];
+  }
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = base + j * kS1BS + threadIdx.x;
+    const bool in = e < src.n && model_in<NP>(src, e, cf, cn, mt, x[j], y[j], z[j]);
+    m[j] = ballot(in);
+    if ((threadIdx.x & (kWave - 1)) == 0) s_cnt[j * (kS1BS / kWave) + w] = __popcll(m[j]);
+  }
+  const int excl = sel1_scan(L, tile, s_cnt, s_pre, s_base);
+  if (excl < 0) {
+    if (threadIdx.x == 0) totals[0] = -1;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = base + j * kS1BS + threadIdx.x;
+    if (e >= src.n) break;
+    const int r = s_pre[j * (kS1BS / kWave) + w] + lanes_below(m[j]);  // inliers before e in tile
+    if ((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull) {
+      tag[g[j]] = tagv;
+    } else {
+      const int64_t q = base + j * kS1BS + threadIdx.x - (excl + r);
+      dst.x[q] = x[j]; dst.y[q] = y[j]; dst.z[q] = z[j]; dst.gid[q] = g[j];
+      if (NP && dst.nrm) dst.nrm[q] = src.nrm[e];
+    }
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) {
+    const int in = excl + s_base[1];
+    totals[0] = in;
+    totals[1] = (int32_t)(n_list - in);
+    totals[4] = (int32_t)(src.n - in);
+  }
+}
+
+// the active list's compaction from the stamps: lidx = pristine index per list point (null: the
+// pristine list, lidx[e] = e); inliers -> inl_gid (their ids, list order), survivors' pristine
+// indices -> out_lidx; the last tile writes totals[0..1] = (inliers, survivors)
+template <bool IDENT>
+__global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__ lidx, int64_t n,
+                                                     const uint8_t* __restrict__ tag, uint8_t tagv,
+                                                     const int32_t* __restrict__ pgid, Sel1State L,
+                                                     int32_t* __restrict__ inl_gid,
+                                                     int32_t* __restrict__ out_lidx, int ntiles,
+                                                     int32_t* __restrict__ totals) {
+  __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
+  const int tile = blockIdx.x;
+  const int w = threadIdx.x / kWave;
+  const int64_t base = (int64_t)tile * kS1Tile;
+  int32_t p[kS1It];
+  uint8_t tv[kS1It];
+  uint64_t m[kS1It];
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = min<int64_t>(base + j * kS1BS + threadIdx.x, n - 1);
+    p[j] = IDENT ? (int32_t)e : lidx[e];
+  }
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) tv[j] = tag[p[j]];
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = base + j * kS1BS + threadIdx.x;
+    const bool in = e < n && tv[j] == tagv;
+    m[j] = ballot(in);
+    if ((threadIdx.x & (kWave - 1)) == 0) s_cnt[j * (kS1BS / kWave) + w] = __popcll(m[j]);
+  }
+  const int excl = sel1_scan(L, tile, s_cnt, s_pre, s_base);
+  if (excl < 0) {
+    if (threadIdx.x == 0) totals[0] = -1;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = base + j * kS1BS + threadIdx.x;
+    if (e >= n) break;
+    const int r = s_pre[j * (kS1BS / kWave) + w] + lanes_below(m[j]);
+    if ((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull)
+      inl_gid[excl + r] = pgid[p[j]];
+    else
+      out_lidx[base + j * kS1BS + threadIdx.x - (excl + r)] = p[j];
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) {
+    const int in = excl + s_base[1];
+    totals[0] = in;
+    totals[1] = (int32_t)(n - in);
+  }
+}
+
+__global__ void k_sel1_empty(int64_t n_list, int32_t* totals) {
+  totals[0] = 0;
+  totals[1] = (int32_t)n_list;
+  totals[4] = 0;
+}
+
+// the list's x, y, z, gid (+ normals) from the pristine copy by pristine index, in place (a
+// lean list is materialised before any path that reads its coordinates)
+__global__ void k_list_materialize(PointsView pristine, int64_t n, PointsOut io) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int32_t p = io.gid[e];
+  io.x[e] = pristine.x[p];
+  io.y[e] = pristine.y[p];
+  io.z[e] = pristine.z[p];
+  io.gid[e] = pristine.gid[p];
+  if (io.nrm) io.nrm[e] = pristine.nrm[p];
+}
+
 // k_score_np: counts[h] for SACMODEL_NORMAL_PLANE.
 //
 // Per point the exact prefilter b = (1 - w) d_euclid < thr becomes one float compare: b is
@@ -1369,11 +1631,53 @@ void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src
 
 void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleRec* samples,
                          float cthr, float ax, float ay, float az, HypRec* hyps, int32_t* res,
-                         hipStream_t s) {
+                         hipStream_t s, const int32_t* lidx, int64_t n_list) {
   if (D <= 0) return;
   const int Dp = (D + 63) / 64 * 64;
   hipLaunchKernelGGL(k_gather_build, dim3(cdiv(Dp, 256)), dim3(256), 0, s, pos_host, D, Dp, src,
-                     samples, cthr, ax, ay, az, hyps, res);
+                     lidx, lidx ? n_list : src.n, samples, cthr, ax, ay, az, hyps, res);
+}
+
+// single-pass selects (lean-list rounds): every launch stamps its status words with a fresh epoch
+static void sel1_next(Sel1State& L, int) { ++L.epoch; }
+
+void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
+                        uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
+                        int32_t* totals, hipStream_t s) {
+  const int nt = sel1_tiles(sp.n);
+  if (nt == 0) {
+    hipLaunchKernelGGL(k_sel1_empty, dim3(1), dim3(1), 0, s, n_list, totals);
+    return;
+  }
+  sel1_next(L, nt);
+  if (mt.normal_plane)
+    hipLaunchKernelGGL(k_sel1_morton<true>, dim3(nt), dim3(kS1BS), 0, s, sp, coef, mt, L, tag,
+                       tagv, dst, n_list, nt, totals);
+  else
+    hipLaunchKernelGGL(k_sel1_morton<false>, dim3(nt), dim3(kS1BS), 0, s, sp, coef, mt, L, tag,
+                       tagv, dst, n_list, nt, totals);
+}
+
+void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_t tagv,
+                      const int32_t* pgid, Sel1State& L, int32_t* inl_gid, int32_t* out_lidx,
+                      int32_t* totals, hipStream_t s) {
+  const int nt = sel1_tiles(n);
+  if (nt == 0) {
+    (void)hipMemsetAsync(totals, 0, 2 * sizeof(int32_t), s);
+    return;
+  }
+  sel1_next(L, nt);
+  if (lidx)
+    hipLaunchKernelGGL(k_sel1_list<false>, dim3(nt), dim3(kS1BS), 0, s, lidx, n, tag, tagv, pgid,
+                       L, inl_gid, out_lidx, nt, totals);
+  else
+    hipLaunchKernelGGL(k_sel1_list<true>, dim3(nt), dim3(kS1BS), 0, s, lidx, n, tag, tagv, pgid,
+                       L, inl_gid, out_lidx, nt, totals);
+}
+
+void launch_list_materialize(PointsView pristine, int64_t n, const PointsOut& io, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_list_materialize, dim3(cdiv(n, 256)), dim3(256), 0, s, pristine, n, io);
 }
 
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,

@@ -113,9 +113,30 @@ void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypR
                     hipStream_t s);
 // one rank: positions (pinned host buffer, 3 per draw) -> samples, hypotheses, good flags in
 // res[Dp + d] and zeroed counts res[0, Dp)  (gather + build + memset in one launch)
+// lidx: the lean list's pristine indices (src = the pristine copy, n_list = list length)
 void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleRec* samples,
                          float cthr, float ax, float ay, float az, HypRec* hyps, int32_t* res,
-                         hipStream_t s);
+                         hipStream_t s, const int32_t* lidx = nullptr, int64_t n_list = 0);
+
+// single-pass select (decoupled look-back) of the lean-list rounds: status words per tile, an
+// epoch per launch (so the words never need clearing)
+struct Sel1State {
+  uint64_t* status = nullptr;
+  uint32_t epoch = 0;
+};
+// the Morton copy's select: survivors -> dst, inliers stamped tag[pristine index] = tagv;
+// totals[0] = inliers, totals[1] = n_list - inliers, totals[4] = Morton survivors
+void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
+                        uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
+                        int32_t* totals, hipStream_t s);
+// the lean list's compaction from the stamps (lidx null: the pristine list): inlier ids in list
+// order -> inl_gid, survivors' pristine indices -> out_lidx; totals[0..1] = (in, out)
+void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_t tagv,
+                      const int32_t* pgid, Sel1State& L, int32_t* inl_gid, int32_t* out_lidx,
+                      int32_t* totals, hipStream_t s);
+// a lean list's x, y, z, gid (+ normals) from the pristine copy, in place (io.gid holds the
+// pristine indices on entry)
+void launch_list_materialize(PointsView pristine, int64_t n, const PointsOut& io, hipStream_t s);
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,
                        HypRec* hyps, int32_t* good, hipStream_t s);
 // counts[D] = #{i < n : |plane_h . (x_i, y_i, z_i, 1)| < cthr}, PCL (Eigen SSE) op order.

@@ -57,7 +57,7 @@ __global__ void k_gather_order(PointsView src, const int32_t* __restrict__ order
   dst.x[i] = src.x[k];
   dst.y[i] = src.y[k];
   dst.z[i] = src.z[k];
-  dst.gid[i] = src.gid[k];
+  dst.gid[i] = k;  // the Morton copy's "gid" is the pristine index (lean-list rounds stamp it)
 }
 
 // one wave per super-tile: the two half-waves take one tile each per step.  Tile sphere: centre
