@@ -593,10 +593,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n));
       SoA& sd = cl->sp_buf[cl->sp_spare()];
       sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
+      const SoA& ss = cl->sp_soa();
+      if (ss.with_nrm) sd.ensure_nrm((size_t)std::max<int64_t>(cl->sp_n, 1));
       PointsOut spo = sd.out();
-      spo.nrm = nullptr;
-      launch_sel1_morton(sp_cur_view(), rc_dev, mt, c->sel1, cl->tag.p, (uint8_t)cl->tagv, spo,
-                         src.n, c->totals.p, c->stream);
+      PointsView spv = sp_cur_view();
+      if (ss.with_nrm) spv.nrm = ss.nrm.p;  // (a later NORMAL_PLANE round reads them)
+      else spo.nrm = nullptr;
+      launch_sel1_morton(spv, rc_dev, mt, c->sel1, cl->tag.p, (uint8_t)cl->tagv, spo, src.n,
+                         c->totals.p, c->stream);
     } else {
       launch_select_head(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
                          c->totals.p, c->stream);

@@ -1388,7 +1388,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const flo
     } else {
       const int64_t q = base + j * kS1BS + threadIdx.x - (excl + r);
       dst.x[q] = x[j]; dst.y[q] = y[j]; dst.z[q] = z[j]; dst.gid[q] = g[j];
-      if (NP && dst.nrm) dst.nrm[q] = src.nrm[e];
+      if (dst.nrm) dst.nrm[q] = src.nrm[e];  // (normals travel when the copy has them)
     }
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) {

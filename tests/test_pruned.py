@@ -172,3 +172,58 @@ def test_pruned_counts_c3_full_size(gpu_ctx):
             assert ref.sum() > 0 and np.array_equal(got, ref), int((got != ref).sum())
     finally:
         cloud.close()
+
+
+def test_lean_list_continue_segment_and_normal_plane(gpu_ctx):
+    """Lean-list rounds (the Morton copy decides the inliers, the list keeps pristine indices):
+    extraction continued over several calls equals one call; a plain segment and a
+    SACMODEL_NORMAL_PLANE round afterwards read the materialised list; all against the oracle."""
+    p, _, _ = plane_cloud(40000, 6, seed=41)
+    p[::17, 2] = np.nan
+    kw = dict(max_iterations=255, probability=1.0)
+    prm = D.make_params(0.02, **kw)
+    ref = O.extract_planes(p, 0.02, max_planes=5, min_inliers=50, **kw)
+    cloud = D.Cloud(gpu_ctx, p)
+    cloud.build_spatial()
+    got = []
+    for k in (2, 2, 1):  # 5 planes over three calls
+        e = D.extract_planes(cloud, prm, max_planes=k, min_inliers=50)
+        got.append(e["inliers"].copy())
+    assert np.array_equal(np.concatenate(got), ref["inliers"])
+    taken = np.concatenate(got)
+    rem = np.setdiff1d(np.arange(p.shape[0]), taken).astype(np.int32)
+    # plain segment over the remaining (lean) list: materialised from the pristine copy
+    inl, coeff, st = D.segment_cloud(cloud, prm)
+    r = O.sac_segment(p, 0.02, indices=rem, **kw)
+    same(inl, coeff, st, r)
+    # a NORMAL_PLANE round on the same list
+    nrm = np.zeros((p.shape[0], 4), np.float32)
+    nrm[:, 2] = 1.0
+    cloud.set_normals(nrm)  # (resets the cloud)
+    e = D.extract_planes(cloud, prm, max_planes=2, min_inliers=50)
+    assert np.array_equal(e["inliers"], ref["inliers"][:ref["offsets"][2]])
+    npp = D.make_params(0.05, max_iterations=100, model=D.SACMODEL_NORMAL_PLANE,
+                        normal_distance_weight=0.1)
+    e2 = D.extract_planes(cloud, npp, max_planes=1, min_inliers=10)
+    rem2 = np.setdiff1d(np.arange(p.shape[0]), e["inliers"]).astype(np.int32)
+    r2 = O.sac_segment(p, 0.05, indices=rem2, max_iterations=100, normals=nrm,
+                       normal_distance_weight=0.1)
+    assert np.array_equal(e2["inliers"][:e2["offsets"][1]], r2["inliers"])
+    cloud.close()
+
+
+def test_lean_list_indexed_cloud(gpu_ctx):
+    """setIndices clouds: the list's pristine indices differ from the point ids (and from list
+    order of the ids when the indices are unsorted)."""
+    p, _, _ = plane_cloud(50000, 5, seed=43)
+    rng = np.random.default_rng(9)
+    idx = rng.choice(p.shape[0], 30000, replace=False).astype(np.int32)  # unsorted
+    kw = dict(max_iterations=200, probability=1.0)
+    cloud = D.Cloud(gpu_ctx, p, indices=idx)
+    cloud.build_spatial()
+    e = D.extract_planes(cloud, D.make_params(0.02, **kw), max_planes=4, min_inliers=50)
+    ref = O.extract_planes(p[idx], 0.02, max_planes=4, min_inliers=50, **kw)
+    assert e["n_planes"] == ref["n_planes"] >= 3
+    assert np.array_equal(e["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
+    assert np.array_equal(e["inliers"], idx[ref["inliers"]])
+    cloud.close()
