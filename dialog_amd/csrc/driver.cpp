@@ -64,9 +64,12 @@ double now_ms() {
 // spin until k_publish has released `seq` into c->pub[0] (the round's results are then in
 // c->pub).  ev_tot (recorded right after the publish) backs it up: once the event has
 // completed the word must be visible; an error of the stream surfaces through the event query.
+void pump_pending(dlg_ctx* c, int64_t ids);
+
 void wait_published(dlg_ctx* c, int32_t seq) {
   for (uint32_t k = 1;; ++k) {
     if (__atomic_load_n(c->pub, __ATOMIC_ACQUIRE) == seq) return;
+    pump_pending(c, 16384);
     if ((k & 1023u) == 0) {
       const hipError_t e = hipEventQuery(c->ev_tot);
       if (e == hipSuccess) {
@@ -170,10 +173,50 @@ float event_ms(dlg_ctx* c, int a, int b) {
 
 void drain_pending(dlg_ctx* c) {
   if (!c->pending_dst) return;
-  HIPCHK(hipEventSynchronize(c->ev_stage));
-  std::memcpy(c->pending_dst, c->h_stage.p, (size_t)c->pending_n * 4);
+  if (!c->stage_ready) HIPCHK(hipEventSynchronize(c->ev_stage));
+  std::memcpy(c->pending_dst + c->pending_off, c->h_stage.p + c->pending_off,
+              (size_t)(c->pending_n - c->pending_off) * 4);
   c->pending_dst = nullptr;
-  c->pending_n = 0;
+  c->pending_n = c->pending_off = 0;
+}
+
+// part of the staged ids to the caller, once the copy has landed (called while the host spins
+// on a round's results, so the copy costs the rounds nothing)
+void pump_pending(dlg_ctx* c, int64_t ids) {
+  if (!c->pending_dst) return;
+  if (!c->stage_ready) {
+    const hipError_t e = hipEventQuery(c->ev_stage);
+    if (e == hipErrorNotReady) return;
+    HIPCHK(e);
+    c->stage_ready = true;
+  }
+  const int64_t n = std::min<int64_t>(ids, c->pending_n - c->pending_off);
+  std::memcpy(c->pending_dst + c->pending_off, c->h_stage.p + c->pending_off, (size_t)n * 4);
+  c->pending_off += n;
+  if (c->pending_off == c->pending_n) {
+    c->pending_dst = nullptr;
+    c->pending_n = c->pending_off = 0;
+  }
+}
+
+// the requested inlier copy: device -> pinned stage on the copy stream, behind the select that
+// wrote inl_gid (ev_inl); enqueued after the next round's launches, off the host's critical path
+void flush_emit(dlg_ctx* c) {
+  if (!c->emit_dst) return;
+  drain_pending(c);  // (the stage is reused)
+  c->h_stage.ensure((size_t)c->emit_n);
+  if (!c->ev_stage) HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+  HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_inl, 0));
+  HIPCHK(hipMemcpyAsync(c->h_stage.p, c->inl_gid.p, (size_t)c->emit_n * 4, hipMemcpyDeviceToHost,
+                        c->cstream));
+  HIPCHK(hipEventRecord(c->ev_stage, c->cstream));
+  c->stage_inflight = true;  // inl_gid is read until ev_stage
+  c->pending_dst = c->emit_dst;
+  c->pending_n = c->emit_n;
+  c->pending_off = 0;
+  c->stage_ready = false;
+  c->emit_dst = nullptr;
+  c->emit_n = 0;
 }
 
 struct SegOut {
@@ -473,7 +516,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       spec_pending = true;
       spec_D = D;
       spec_Dp = Dp;
-      drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
+      flush_emit(c);  // the previous round's inlier copy, behind this round's launches
       if (trace_on())
         std::fprintf(stderr, "[dlg] N=%lld D=%d totals->draw=%.3fms draw=%.3fms enqueue=%.3fms (speculative pick)\n",
                      (long long)N, D, c->t_tot > 0 ? t_draw0 - c->t_tot : 0.0, t_draw1 - t_draw0,
@@ -482,7 +525,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     }
     HIPCHK(hipMemcpyAsync(c->h_res.p, c->res.p, 4 * ((size_t)Dp + D), hipMemcpyDeviceToHost, c->stream));
     const double t_launch = trace_on() ? now_ms() : 0.0;
-    drain_pending(c);  // host copy of the previous round's inliers overlaps the scoring kernel
+    flush_emit(c);  // the previous round's inlier copy, behind this round's launches
     sync(c);
     if (trace_on())
       std::fprintf(stderr, "[dlg] N=%lld D=%d totals->draw=%.3fms draw=%.3fms launch=%.3fms score+wait=%.3fms\n",
@@ -639,6 +682,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       // sphere bounds of the Morton survivors (count in totals[4])
       launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv, cl->pristine.gid.p, c->sel1,
                        c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream);
+      HIPCHK(hipEventRecord(c->ev_inl, c->stream));  // inl_gid final (flush_emit)
       if (c->profiling) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
       const int b = cl->sp_spare();
       SoA& sd = cl->sp_buf[b];
@@ -649,6 +693,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     } else {
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
                          nullptr, compact ? &dst : nullptr, c->stream);
+      HIPCHK(hipEventRecord(c->ev_inl, c->stream));  // inl_gid final (flush_emit)
     }
     // the Morton copy loses the same points (same predicate, same float inputs): its totals
     // land in totals[2..3], checked at the next publish / the end of the extraction
@@ -810,25 +855,10 @@ int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, in
     throw DlgError(DLG_ERR_CAPACITY, "inlier buffer too small: need " + std::to_string(so.n_in_local));
   if (so.n_in_local) {
     if (deferred) {
-      const double t0 = trace_on() ? now_ms() : 0.0;
-      drain_pending(c);
-      const double t1 = trace_on() ? now_ms() : 0.0;
-      c->h_stage.ensure((size_t)so.n_in_local);
-      if (!c->ev_stage) HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
-      const double t2 = trace_on() ? now_ms() : 0.0;
-      if (!c->ev_inl) HIPCHK(hipEventCreateWithFlags(&c->ev_inl, hipEventDisableTiming));
-      HIPCHK(hipEventRecord(c->ev_inl, c->stream));
-      HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_inl, 0));
-      HIPCHK(hipMemcpyAsync(c->h_stage.p, c->inl_gid.p, (size_t)so.n_in_local * 4,
-                            hipMemcpyDeviceToHost, c->cstream));
-      const double t3 = trace_on() ? now_ms() : 0.0;
-      HIPCHK(hipEventRecord(c->ev_stage, c->cstream));
-      c->stage_inflight = true;  // inl_gid is read until ev_stage
-      if (trace_on())
-        std::fprintf(stderr, "[dlg] emit n=%lld cap=%zu drain %.3f ensure %.3f copy %.3f record %.3f ms\n",
-                     (long long)so.n_in_local, c->h_stage.cap, t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
-      c->pending_dst = dst;
-      c->pending_n = so.n_in_local;
+      // (copied by flush_emit after the next round's launches, or at the end of the loop)
+      flush_emit(c);
+      c->emit_dst = dst;
+      c->emit_n = so.n_in_local;
     } else {
       HIPCHK(hipMemcpyAsync(dst, c->inl_gid.p, (size_t)so.n_in_local * 4, hipMemcpyDeviceToHost,
                             c->stream));
@@ -856,6 +886,7 @@ dlg_status init_ctx(dlg_ctx* c, int device) {
   return guarded(c, [&] {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_inl, hipEventDisableTiming));
     for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
   });
 }
@@ -1266,6 +1297,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
         cl->sp_valid = false;  // (SACMODEL_NORMAL_PLANE rounds do not carry the spatial copy)
       }
     }
+    flush_emit(c);
     drain_pending(c);
     // A stream synchronisation lets the HIP runtime reclaim the per-command resources of the
     // rounds: with event waits alone they pile up until a D2H copy blocks the host for ~10 ms
@@ -1274,7 +1306,9 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
     settle_round(c);
   });
   c->pending_dst = nullptr;  // (error path: never write into the caller's buffer later)
-  c->pending_n = 0;
+  c->pending_n = c->pending_off = 0;
+  c->emit_dst = nullptr;
+  c->emit_n = 0;
   c->sel_pending = nullptr;  // (never read into the caller's stats after the call)
   c->sp_check = false;
   xs->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -207,6 +207,10 @@ struct dlg_ctx {
   ShuffleReplay replay;  // drawIndexSample replay table, reused by every segment on this context  // end of a round's totals D2H (work queued after it may still run)
   int32_t* pending_dst = nullptr;
   int64_t pending_n = 0;
+  int64_t pending_off = 0;   // ids already copied to the caller (pumped while waiting)
+  bool stage_ready = false;  // ev_stage has completed
+  int32_t* emit_dst = nullptr;  // a round's inliers to copy (enqueued after the next launches)
+  int64_t emit_n = 0;
   NormalsWork nw;
   PostWork pw;
 };

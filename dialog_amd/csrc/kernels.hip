@@ -891,15 +891,27 @@ __global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, const float4*
   double acc[kMomentK];
 #pragma unroll
   for (int k = 0; k < kMomentK; ++k) acc[k] = 0.0;
-  const int64_t stride = (int64_t)gridDim.x * kMoBS;
-  for (int64_t e = (int64_t)blockIdx.x * kMoBS + threadIdx.x; e < src.n; e += stride) {
-    float x = src.x[e], y = src.y[e], z = src.z[e];
-    if (model_in<NP>(src, e, cf, cn, mt, x, y, z)) {
-      double dx = (double)x - sh.x, dy = (double)y - sh.y, dz = (double)z - sh.z;
-      acc[0] += 1.0;
-      acc[1] += dx; acc[2] += dy; acc[3] += dz;
-      acc[4] += dx * dx; acc[5] += dx * dy; acc[6] += dx * dz;
-      acc[7] += dy * dy; acc[8] += dy * dz; acc[9] += dz * dz;
+  // kMoIt points per lane per pass, their loads all in flight before the tests (clamped,
+  // unconditional: one guarded load per iteration would wait out each load in turn)
+  constexpr int kMoIt = 8;
+  const int64_t stride = (int64_t)gridDim.x * kMoBS * kMoIt;
+  for (int64_t b0 = (int64_t)blockIdx.x * kMoBS * kMoIt; b0 < src.n; b0 += stride) {
+    float x[kMoIt], y[kMoIt], z[kMoIt];
+#pragma unroll
+    for (int j = 0; j < kMoIt; ++j) {
+      const int64_t e = min<int64_t>(b0 + j * kMoBS + threadIdx.x, src.n - 1);
+      x[j] = src.x[e]; y[j] = src.y[e]; z[j] = src.z[e];
+    }
+#pragma unroll
+    for (int j = 0; j < kMoIt; ++j) {
+      const int64_t e = b0 + j * kMoBS + threadIdx.x;
+      if (e < src.n && model_in<NP>(src, e, cf, cn, mt, x[j], y[j], z[j])) {
+        double dx = (double)x[j] - sh.x, dy = (double)y[j] - sh.y, dz = (double)z[j] - sh.z;
+        acc[0] += 1.0;
+        acc[1] += dx; acc[2] += dy; acc[3] += dz;
+        acc[4] += dx * dx; acc[5] += dx * dy; acc[6] += dx * dz;
+        acc[7] += dy * dy; acc[8] += dy * dz; acc[9] += dz * dz;
+      }
     }
   }
   __shared__ double s_red[kMoBS / kWave][kMomentK];

@@ -145,14 +145,19 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
   const int64_t base = (int64_t)blockIdx.x * kSb2Pts;
   if (base >= n) return;
   const int cnt = (int)min<int64_t>(kSb2Pts, n - base);
-#pragma unroll 4
-  for (int i = lane; i < kSb2Pts; i += kWave) {
-    const int r = i + i / kTileP;
-    if (i < cnt) {
-      s_p[0][r] = X[base + i];
-      s_p[1][r] = Y[base + i];
-      s_p[2][r] = Z[base + i];
-    }
+  // all 96 loads in flight before the first LDS store (clamped, unconditional: a guarded load
+  // per point is a branch, and the compiler waits for each before the next)
+  constexpr int kPer = kSb2Pts / kWave;
+  float vx[kPer], vy[kPer], vz[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t e = base + min(k * kWave + lane, cnt - 1);
+    vx[k] = X[e]; vy[k] = Y[e]; vz[k] = Z[e];
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = k * kWave + lane, r = i + i / kTileP;
+    s_p[0][r] = vx[k]; s_p[1][r] = vy[k]; s_p[2][r] = vz[k];
   }
   __syncthreads();
   const int np = min(kTileP, cnt - lane * kTileP);  // this lane's tile size (<= 0: none)
