@@ -1442,6 +1442,12 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__
     m[j] = ballot(in);
     if ((threadIdx.x & (kWave - 1)) == 0) s_cnt[j * (kS1BS / kWave) + w] = __popcll(m[j]);
   }
+  // the inliers' ids, loaded before the scan so the loads overlap it (every lane loads: the
+  // others re-read their first point's id, so no lane waits on a branch)
+  int32_t gi[kS1It];
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j)
+    gi[j] = pgid[((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull) ? p[j] : p[0]];
   const int excl = sel1_scan(L, tile, s_cnt, s_pre, s_base);
   if (excl < 0) {
     if (threadIdx.x == 0) totals[0] = -1;
@@ -1453,7 +1459,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__
     if (e >= n) break;
     const int r = s_pre[j * (kS1BS / kWave) + w] + lanes_below(m[j]);
     if ((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull)
-      inl_gid[excl + r] = pgid[p[j]];
+      inl_gid[excl + r] = gi[j];
     else
       out_lidx[base + j * kS1BS + threadIdx.x - (excl + r)] = p[j];
   }
