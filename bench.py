@@ -246,12 +246,23 @@ def main():
     # timed with HIP events around the phase (incl. the small reduce/refit kernels between)
     sum_active = per_rank_tests / max(a.hyps, 1)  # sum over rounds of this rank's active points
     n_copies = 2 if pruned else 1
-    sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))
-                 + 4.0 * inliers_local)
+    lean = pruned and world == 1 and os.environ.get("DLG_LEAN", "") != "0" and a.refit == "fast"
+    if lean:
+        # lean-list rounds: moments (12 B/pt) and the single-pass select of the Morton copy (16 B
+        # read, 16 B per survivor, a 1 B stamp per inlier), then the list from the stamps (4 B
+        # index + 1 B stamp read, 4 B per survivor index, 4 + 4 B per inlier id)
+        sel_bytes = (12.0 * sum_active + 16.0 * sum_active + 16.0 * (sum_active - inliers_local)
+                     + 1.0 * inliers_local + 5.0 * sum_active
+                     + 4.0 * (sum_active - inliers_local) + 8.0 * inliers_local)
+    else:
+        sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))
+                     + 4.0 * inliers_local)
     sel_gbs = sel_bytes / (select_ms / 1e3) / 1e9 if select_ms > 0 else 0.0
     roofline["memory_bound_passes"] = {
         "phase": "refit moments + selectWithinDistance + compaction (%s)"
-                 % ("list-ordered SoA and Morton copy" if pruned else "list-ordered SoA"),
+                 % ("lean rounds: single-pass select of the Morton copy + the index list from "
+                    "the inlier stamps" if lean else
+                    "list-ordered SoA and Morton copy" if pruned else "list-ordered SoA"),
         "bound": "hbm", "achieved": round(sel_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(sel_gbs / HBM_PEAK_GBS, 4), "bytes_per_step": round(sel_bytes / a.steps),
         "ms_per_step": round(select_ms / a.steps, 3)}
