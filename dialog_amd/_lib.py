@@ -27,8 +27,20 @@ SYMBOLS = [
     "dlg_cloud_set_normals", "dlg_orient_normals_nn", "dlg_preprocess", "dlg_refit_planes",
     "dlg_post_process_planes", "dlg_cluster_filter", "dlg_sac_control_create",
     "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
-    "dlg_sac_control_result", "dlg_cloud_build_spatial",
+    "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
+    "dlg_ctx_get_option", "dlg_prune_stats",
 ]
+
+# context options (include/dialog_ransac.h): equivalent execution paths, identical results
+DLG_OPT_PRUNE = 1
+DLG_OPT_LEAN_ROUNDS = 2
+DLG_OPT_SPEC_PICK = 3
+DLG_OPT_PRUNE_NP = 4
+DLG_OPT_SCORE_KERNEL = 5
+DLG_OPT_PRUNE_STATS = 6
+DLG_SCORE_EXACT = 0
+DLG_SCORE_BF16 = 1
+DLG_SCORE_PRUNED = 2
 
 
 class Points(C.Structure):
@@ -66,7 +78,7 @@ class SacStats(C.Structure):
 class ExtractStats(C.Structure):
     _fields_ = [("rounds", C.c_int), ("tests", C.c_int64), ("tests_scored", C.c_int64),
                 ("score_launches", C.c_int), ("score_ms", C.c_double), ("select_ms", C.c_double),
-                ("wall_ms", C.c_double)]
+                ("wall_ms", C.c_double), ("lean_rounds", C.c_int), ("spec_misses", C.c_int)]
 
 
 _lib = None
@@ -117,6 +129,9 @@ def load():
     L.dlg_barrier.argtypes = [vp]
     L.dlg_score_benchmark.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                       C.POINTER(C.c_double), i32p]
+    L.dlg_ctx_set_option.argtypes = [vp, C.c_int, C.c_int64]
+    L.dlg_ctx_get_option.argtypes = [vp, C.c_int, i64p]
+    L.dlg_prune_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int]
     L.dlg_preprocess.argtypes = [vp, C.POINTER(Points), C.c_int, C.c_float, fp, C.c_int64, i32p,
                                  C.c_int64, i64p, fp]
     L.dlg_orient_normals_nn.argtypes = [vp, C.POINTER(Points), fp, C.c_int64, C.POINTER(Points),

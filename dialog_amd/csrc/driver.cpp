@@ -69,7 +69,9 @@ void pump_pending(dlg_ctx* c, int64_t ids);
 void wait_published(dlg_ctx* c, int32_t seq) {
   for (uint32_t k = 1;; ++k) {
     if (__atomic_load_n(c->pub, __ATOMIC_ACQUIRE) == seq) return;
-    pump_pending(c, 16384);
+    // the staged ids go to the caller while we wait; until their copy has landed, its event is
+    // queried only every 16th spin (a HIP API call takes the runtime lock)
+    if (c->stage_ready || (k & 15u) == 0) pump_pending(c, 16384);
     if ((k & 1023u) == 0) {
       const hipError_t e = hipEventQuery(c->ev_tot);
       if (e == hipSuccess) {
@@ -84,6 +86,13 @@ void wait_published(dlg_ctx* c, int32_t seq) {
   }
 }
 
+// a single-pass select's look-back failed (sticky word set): clear it and fail the call
+[[noreturn]] void sel1_failed(dlg_ctx* c) {
+  (void)hipMemsetAsync(c->sel1_err.p, 0, sizeof(int32_t), c->stream);
+  (void)hipStreamSynchronize(c->stream);
+  throw DlgError(DLG_ERR_INTERNAL, "single-pass select did not complete (look-back gave up)");
+}
+
 // the previous compaction's Morton-copy totals (in, out) against what the list copy predicted
 void check_sp_totals(dlg_ctx* c, const int32_t* sp_tot) {
   if (!c->sp_check) return;
@@ -96,6 +105,11 @@ void check_sp_totals(dlg_ctx* c, const int32_t* sp_tot) {
 
 // after a stream synchronisation: the last compaction's Morton-copy totals and select timing
 void settle_round(dlg_ctx* c) {
+  if (c->sel1_err.p) {
+    int32_t e = 0;
+    HIPCHK(hipMemcpy(&e, c->sel1_err.p, 4, hipMemcpyDeviceToHost));
+    if (e) sel1_failed(c);
+  }
   if (c->sp_check) {
     int32_t t[2] = {0, 0};
     HIPCHK(hipMemcpy(t, c->totals.p + 2, 8, hipMemcpyDeviceToHost));
@@ -232,34 +246,12 @@ struct SegOut {
   std::vector<int64_t> in_ranks, out_ranks;
 };
 
-// pruned scoring (spatial.hpp): DLG_PRUNE=0 disables it, DLG_PRUNE=1 also builds the spatial
-// copy for small clouds (tests); by default clouds of >= kPruneMinPoints points get one
+// pruned scoring (spatial.hpp): by default clouds of >= kPruneMinPoints points get a Morton copy
 constexpr int64_t kPruneMinPoints = 131072;
-int prune_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("DLG_PRUNE");
-    return e ? std::atoi(e) : -1;
-  }();
-  return m;
-}
 
-// Morton-ordered copy of the pristine cloud's finite points + its bounding spheres
-// pruned NORMAL_PLANE scoring (DLG_PRUNE_NP=0: the exhaustive k_score_np)
-bool np_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DLG_PRUNE_NP");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
-
-// speculative device pick for probability-1 rounds (segment_impl); DLG_SPEC_PICK=0 disables
-bool spec_pick_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DLG_SPEC_PICK");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
+// the pruned kernel's work counters (DLG_OPT_PRUNE_STATS), accumulated over its launches
+unsigned long long* prune_stats_ptr(dlg_ctx* c) {
+  return c->opt.prune_stats ? c->pstats.p : nullptr;
 }
 
 void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
@@ -326,15 +318,6 @@ void ensure_sphere_bounds(dlg_ctx* c, dlg_cloud* cl) {
   cl->sp_dirty = false;
 }
 
-// lean-list rounds (single-pass selects driven by the Morton copy): DLG_LEAN=0 disables them
-bool lean_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DLG_LEAN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // a lean list's coordinates (and ids, normals) from the pristine copy, before any path that
 // reads them
 void ensure_list_xyz(dlg_ctx* c, dlg_cloud* cl) {
@@ -349,12 +332,17 @@ void ensure_list_xyz(dlg_ctx* c, dlg_cloud* cl) {
 }
 
 void ensure_sel1(dlg_ctx* c, int64_t n) {
-  const size_t nt = (size_t)select_tiles(n) + 1;
+  const size_t nt = (size_t)sel1_tiles(n) + 1;
   if (nt > c->sel1_status.cap) {
     c->sel1_status.ensure(nt);
     HIPCHK(hipMemsetAsync(c->sel1_status.p, 0, sizeof(uint64_t) * c->sel1_status.cap, c->stream));
   }
+  if (!c->sel1_err.p) {
+    c->sel1_err.ensure(1);
+    HIPCHK(hipMemsetAsync(c->sel1_err.p, 0, sizeof(int32_t), c->stream));
+  }
   c->sel1.status = c->sel1_status.p;
+  c->sel1.err = c->sel1_err.p;
 }
 
 // one SACSegmentation::segment() over the cloud's active list (all ranks)
@@ -393,10 +381,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // lean-list round: plane model over the Morton copy, single rank, device refit, a list that
   // is pristine or already lean (a list compacted with coordinates stays on the full path)
   const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
-  const bool lean = compact && !np && !pcl_refit && lean_enabled() && c->comm->world() == 1 &&
+  const bool lean = compact && !np && !pcl_refit && c->opt.lean && c->comm->world() == 1 &&
                     cl->sp_valid && cl->sp_n > 0 && cl->n_total < (int64_t(1) << 30) &&
-                    score_variant() == kScoreDefault && prune_mode() != 0 &&
-                    (cl->cur < 0 || cl->buf_lean[cl->cur]);
+                    c->opt.prune != 0 && (cl->cur < 0 || cl->buf_lean[cl->cur]);
   if (!lean) ensure_list_xyz(c, cl);
   const PointsView src = cl->view();
   // the lean list's pristine indices (null while the list is the pristine one)
@@ -411,7 +398,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   RansacControl ctl(prm, N, cap_h, &c->replay);
   if (trace_on()) std::fprintf(stderr, "[dlg] segment start %.3fms ctl %.3fms\n", t_ctl0 - c->t_tot, now_ms() - t_ctl0);
   // pruned scoring over the spatial copy (plane model, default kernel, spatial copy in step)
-  const bool pruned = !np && cl->sp_valid && score_variant() == kScoreDefault && prune_mode() != 0;
+  const bool pruned = !np && cl->sp_valid && c->opt.prune != 0;
   // NORMAL_PLANE over the Morton copy: the prefilter d_euclid < lim(w) holds for the cloud's
   // largest w = lambda (1 - min curvature) when every w lies in [0, 1) (then lim is finite and
   // monotone in w); NaN curvatures never pass PCL's test.  Otherwise the exhaustive kernel.
@@ -421,8 +408,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     const double w_min = prm.normal_distance_weight * (1.0 - (double)cl->curv_max);
     if (w_min >= 0.0 && w_max < 1.0) np_lim = np_lim_max(w_max, prm.threshold);
   }
-  const bool pruned_np = np && cl->sp_valid && cl->sp_soa().with_nrm && prune_mode() != 0 &&
-                         np_enabled() && np_lim < INFINITY;
+  const bool pruned_np = np && cl->sp_valid && cl->sp_soa().with_nrm && c->opt.prune != 0 &&
+                         c->opt.prune_np && np_lim < INFINITY;
   const float pmargin = pruned ? prune_margin(cthr, cl->amax)
                                : pruned_np ? prune_margin(np_lim, cl->amax) : 0.0f;
   if (pruned || pruned_np) ensure_sphere_bounds(c, cl);
@@ -439,7 +426,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // The counts still come back with the round's sync and the host replays them
   // (RansacControl::consume); on any disagreement, or when the loop needs more draws (bad
   // samples), the round continues on the exact host path and the refit + select are redone.
-  const bool spec = spec_pick_enabled() && prm.probability == 1.0 && prm.max_iterations >= 0 &&
+  const bool spec = c->opt.spec_pick && prm.probability == 1.0 && prm.max_iterations >= 0 &&
                     (int64_t)prm.max_iterations + 1 <= cap_h;
   c->pick.ensure(4);
   c->h_pick.ensure(4);
@@ -486,21 +473,17 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
       const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold};
-      launch_score_pruned(spatial_view(cl), c->hyps.p, nullptr, nullptr, D, cthr, pmargin,
-                          cl->amax, c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream, nullptr,
-                          &npp);
+      launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
+                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), &npp);
     } else if (np)
       launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
     else if (pruned) {
-      const uint4* bcol = nullptr;
-      const float* band = nullptr;
-      if (prune_kernel() == 1) launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
-      launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr, pmargin, cl->amax,
-                          c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream);
+      launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
+                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c));
     } else
-      launch_score(src, c->hyps.p, D, cthr, c->res.p, score_variant(), c->num_cus, c->stream);
+      launch_score(src, c->hyps.p, D, cthr, c->res.p, c->opt.score_kernel, c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
@@ -672,7 +655,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     const int32_t seq = ++c->pub_seq == 0 ? ++c->pub_seq : c->pub_seq;
     launch_publish(c->totals.p, 4, c->small.p, 6, W > 1 ? c->rk.p : nullptr, W > 1 ? 2 * W : 0,
                    with_counts ? c->pick.p : nullptr, with_counts ? 2 : 0,
-                   with_counts ? c->res.p : nullptr, nres, c->pub, seq, c->stream);
+                   with_counts ? c->res.p : nullptr, nres, c->sel1_err.p, c->pub, seq, c->stream);
     HIPCHK(hipGetLastError());
     spec_pending = false;
     if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
@@ -726,8 +709,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       std::fprintf(stderr, "[dlg] select enqueue=%.3fms wait=%.3fms\n", t_wait0 - t_ref0, now_ms() - t_wait0);
     if (trace_on()) c->t_tot = now_ms();
     std::memcpy(c->h_tot.p, c->pub + kPubTot, 16);
-    if (c->h_tot.p[0] < 0)  // (k_sel1_morton's look-back gave up: nothing was scattered)
-      throw DlgError(DLG_ERR_INTERNAL, "single-pass select did not complete");
+    if (c->pub[kPubErr] != 0) sel1_failed(c);  // (this round's or the last list pass's look-back)
     std::memcpy(c->h_small.p, c->pub + kPubSmall, 6 * sizeof(float4));
     if (W > 1) std::memcpy(c->h_rk.p, c->pub + kPubRk, 8 * (size_t)W);
     check_sp_totals(c, c->h_tot.p + 2);
@@ -756,6 +738,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     const int best_d = ctl.consume(c->h_res.p, c->h_res.p + spec_Dp, spec_D);
     if (!(ctl.done() && best_d == c->h_pick.p[0] && c->h_pick.p[1] == 1)) {
       ++c->spec_misses;
+      if (xs) xs->spec_misses++;
       if (trace_on())
         std::fprintf(stderr, "[dlg] speculative pick overturned: host %d done %d, device %d complete %d\n",
                      best_d, ctl.done() ? 1 : 0, c->h_pick.p[0], c->h_pick.p[1]);
@@ -961,8 +944,7 @@ dlg_status dlg_ctx_create_dist(dlg_ctx** out, int device, int rank, int world, c
     g_last_create_error = c->err;
     return s;
   }
-  const char* force = std::getenv("DLG_FORCE_RCCL");  // 1-rank RCCL communicator (path test)
-  if (world == 1 && !(force && force[0] == '1' && uid)) {
+  if (world == 1 && !uid) {  // (world 1 with an id: a 1-rank RCCL communicator)
     c->comm = make_single_comm();
   } else {
     std::string err;
@@ -1014,6 +996,11 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->pub_cap = 0;
   c->nw.release();
   c->pw.release();
+  c->pstats.release();
+  c->sel1_status.release();
+  c->sel1_err.release();
+  c->lp.release();
+  c->lp_n.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
   if (c->ev_inl) (void)hipEventDestroy(c->ev_inl);
   if (c->cstream) {
@@ -1100,7 +1087,7 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     HIPCHK(hipMemcpyAsync(bits, c->totals.p, 12, hipMemcpyDeviceToHost, c->stream));
     sync(c);
     for (int k = 0; k < 3; ++k) std::memcpy(&cl->amax[k], &bits[k], 4);
-    if (prune_mode() != 0 && n >= 3 && (n >= kPruneMinPoints || prune_mode() == 1))
+    if (c->opt.prune != 0 && n >= 3 && (n >= kPruneMinPoints || c->opt.prune == 1))
       build_spatial(c, cl.get());
   });
   if (s != DLG_OK) {
@@ -1270,6 +1257,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       SegOut so = segment_impl(c, cl, *prm, true, &st, xs, &active);
       xs->rounds++;
       if (!so.has_model) break;
+      if (so.lean) xs->lean_rounds++;
       const int64_t n_in = so.n_in_global;
       if (n_in == 0 || n_in < min_inliers) break;  // plane rejected: active list unchanged
       int64_t g = 0;
@@ -1315,9 +1303,11 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
   return s;
 }
 
-dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, int reps,
+dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int kernel, int reps,
                                double threshold, double* ms_per_launch, int32_t* counts_out) {
   if (!c || !cl || D < 1 || D > kMaxHypPerLaunch || reps < 1 || !ms_per_launch) return DLG_ERR_INVALID;
+  if (kernel != kScoreExact && kernel != kScoreBf16 && kernel != kScorePruned) return DLG_ERR_INVALID;
+  const int variant = kernel;
   return guarded(c, [&] {
     ensure_list_xyz(c, cl);
     const PointsView src = cl->view();
@@ -1342,31 +1332,11 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
       if (variant == kScorePruned) {
         if (!cl->sp_valid) throw DlgError(DLG_ERR_INVALID, "cloud has no spatial copy");
-        const uint4* bcol = nullptr;
-        const float* band = nullptr;
-        launch_prep_bf16(c->hyps.p, D, &bcol, &band, c->stream);
         c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
         c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
-        static const bool want_stats = std::getenv("DLG_PRUNE_STATS") != nullptr;
-        unsigned long long* stp = nullptr;
-        if (want_stats) {
-          c->gath64.ensure(8);
-          stp = reinterpret_cast<unsigned long long*>(c->gath64.p);
-          HIPCHK(hipMemsetAsync(stp, 0, 48, c->stream));
-        }
-        launch_score_pruned(spatial_view(cl), c->hyps.p, bcol, band, D, cthr,
-                            prune_margin(cthr, cl->amax), cl->amax, c->res.p, c->lp.p, c->lp_n.p,
-                            c->num_cus, c->stream, stp);
-        if (want_stats) {
-          unsigned long long h[6];
-          HIPCHK(hipMemcpyAsync(h, stp, 48, hipMemcpyDeviceToHost, c->stream));
-          sync(c);
-          std::fprintf(stderr, "[prune] n=%lld D=%d mean_nlp=%.1f tiles=%llu "
-                       "groups=%llu pairs=%llu (%.4f of tile x plane) fill=%.3f recheck=%.4f\n",
-                       (long long)cl->sp_n, D, h[2] ? (double)h[1] / h[2] : 0.0, h[2], h[3],
-                       h[4], h[2] ? (double)h[4] / ((double)h[2] * D) : 0.0,
-                       h[3] ? (double)h[4] / (32.0 * h[3]) : 0.0, h[3] ? (double)h[5] / h[3] : 0.0);
-        }
+        unsigned long long* stp = prune_stats_ptr(c);
+        launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, prune_margin(cthr, cl->amax),
+                            cl->amax, c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream, stp);
       } else {
         launch_score(src, c->hyps.p, D, cthr, c->res.p, variant, c->num_cus, c->stream);
       }
@@ -1380,6 +1350,61 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int variant, in
       HIPCHK(hipMemcpyAsync(counts_out, c->res.p, 4 * (size_t)D, hipMemcpyDeviceToHost, c->stream));
       sync(c);
     }
+  });
+}
+
+dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
+  if (!c) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    PathOptions& o = c->opt;
+    switch (option) {
+      case DLG_OPT_PRUNE:
+        if (value < -1 || value > 1) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE: -1, 0 or 1");
+        o.prune = (int)value;
+        break;
+      case DLG_OPT_LEAN_ROUNDS: o.lean = value != 0; break;
+      case DLG_OPT_SPEC_PICK: o.spec_pick = value != 0; break;
+      case DLG_OPT_PRUNE_NP: o.prune_np = value != 0; break;
+      case DLG_OPT_SCORE_KERNEL:
+        if (value != DLG_SCORE_BF16 && value != DLG_SCORE_EXACT)
+          throw DlgError(DLG_ERR_INVALID, "DLG_OPT_SCORE_KERNEL: DLG_SCORE_BF16 or DLG_SCORE_EXACT");
+        o.score_kernel = value == DLG_SCORE_EXACT ? kScoreExact : kScoreBf16;
+        break;
+      case DLG_OPT_PRUNE_STATS:
+        o.prune_stats = value != 0;
+        if (o.prune_stats) {
+          c->pstats.ensure(8);
+          HIPCHK(hipMemsetAsync(c->pstats.p, 0, 8 * sizeof(unsigned long long), c->stream));
+        }
+        break;
+      default: throw DlgError(DLG_ERR_INVALID, "unknown option");
+    }
+  });
+}
+
+dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
+  if (!c || !value) return DLG_ERR_INVALID;
+  const PathOptions& o = c->opt;
+  switch (option) {
+    case DLG_OPT_PRUNE: *value = o.prune; break;
+    case DLG_OPT_LEAN_ROUNDS: *value = o.lean; break;
+    case DLG_OPT_SPEC_PICK: *value = o.spec_pick; break;
+    case DLG_OPT_PRUNE_NP: *value = o.prune_np; break;
+    case DLG_OPT_SCORE_KERNEL: *value = o.score_kernel == kScoreExact ? DLG_SCORE_EXACT : DLG_SCORE_BF16; break;
+    case DLG_OPT_PRUNE_STATS: *value = o.prune_stats; break;
+    default: return DLG_ERR_INVALID;
+  }
+  return DLG_OK;
+}
+
+dlg_status dlg_prune_stats(dlg_ctx* c, uint64_t out[6], int reset) {
+  if (!c || !out) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    std::memset(out, 0, 6 * sizeof(uint64_t));
+    if (!c->opt.prune_stats) return;
+    HIPCHK(hipMemcpyAsync(out, c->pstats.p, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    if (reset) HIPCHK(hipMemsetAsync(c->pstats.p, 0, 8 * sizeof(unsigned long long), c->stream));
+    sync(c);
   });
 }
 

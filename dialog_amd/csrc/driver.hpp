@@ -148,8 +148,20 @@ struct PostWork {
 
 using namespace dlg;
 
+// execution-path options of a context (dlg_ctx_set_option).  Every combination gives the same
+// results: they only select among equivalent paths (tests run each against the oracle).
+struct PathOptions {
+  int prune = -1;       // Morton copy + pruned scoring: -1 clouds >= 131072 points, 0 never, 1 always
+  bool lean = true;     // lean-list rounds (single-pass selects driven by the Morton copy)
+  bool spec_pick = true;  // device pick for probability-1 rounds
+  bool prune_np = true;   // pruned NORMAL_PLANE scoring
+  int score_kernel = kScoreBf16;  // exhaustive scorer: kScoreBf16 or kScoreExact
+  bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
+};
+
 struct dlg_ctx {
   int device = 0;
+  PathOptions opt;
   int num_cus = 256;
   hipStream_t stream = nullptr;
   std::unique_ptr<Comm> comm;
@@ -163,6 +175,7 @@ struct dlg_ctx {
   DevBuf<int32_t> tile_in, tile_off_in, tile_off_out, totals;
   dlg::Sel1State sel1;  // single-pass selects: tile status words + launch epoch
   DevBuf<uint64_t> sel1_status;
+  DevBuf<int32_t> sel1_err;  // sticky look-back failure word of the single-pass selects
   DevBuf<double> partials, moments;
   DevBuf<int32_t> inl_gid;
   DevBuf<float> inl_xyz;
@@ -174,6 +187,7 @@ struct dlg_ctx {
   DevBuf<float4> small;    // winning plane + samples + refined plane (segment_impl)
   DevBuf<uint16_t> lp;     // pruned scoring: per super-tile lists of near planes
   DevBuf<int32_t> lp_n;
+  DevBuf<unsigned long long> pstats;  // pruned-kernel work counters (DLG_OPT_PRUNE_STATS)
   PinBuf<float4> h_small;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<int32_t> h_inl;
@@ -258,29 +272,6 @@ namespace dlg {
 
 inline void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
 inline void sync(dlg_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); }
-
-// wait for an event of the per-round loop.  DLG_WAIT_MODE: 0 hipEventSynchronize, 1 poll with
-// a pause back-off (no sleep: a blocking wait that outlasts the runtime's spin phase sleeps and
-// the wake-up adds tens of microseconds to a round)
-inline int wait_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("DLG_WAIT_MODE");
-    return e ? std::atoi(e) : 0;
-  }();
-  return m;
-}
-inline void wait_event(hipEvent_t ev) {
-  if (wait_mode() != 1) {
-    HIPCHK(hipEventSynchronize(ev));
-    return;
-  }
-  for (;;) {
-    const hipError_t e = hipEventQuery(ev);
-    if (e == hipSuccess) return;
-    if (e != hipErrorNotReady) HIPCHK(e);
-    for (int i = 0; i < 256; ++i) __builtin_ia32_pause();
-  }
-}
 
 inline dlg_status fail(dlg_ctx* c, dlg_status code, const std::string& msg) {
   if (c) c->err = msg;

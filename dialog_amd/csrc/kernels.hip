@@ -148,16 +148,13 @@ __global__ void k_gather_build(const int32_t* pos, int D, int Dp, PointsView src
 // global counts once (one atomic per hypothesis per workgroup).  Grid-stride over chunks of
 // 256 * P points with the grid sized to the resident capacity.
 //
-// Prefilter variants (band, min3) evaluate f = fma(a, x, fma(b, y, fma(c, z, d))) and decide
-// only outside the band |f| in [cthr - E, cthr + E), E = 7 u S >= |f - pcl_dot| (k_build_hyps);
-// any wave with a point inside the band recomputes those points in PCL op order, so the counts
-// stay bit-identical to the exact variant.
 constexpr int kScBS = 512;  // 8 waves share one LDS copy of the hypotheses
 constexpr int kHT = 1024;
 
-enum Kind { kExact = 0, kBand = 1, kMin3 = 2 };
-
-template <int KIND, int P>
+// the exact VALU kernel (PCL op order for every test): the reference the matrix-core and pruned
+// kernels are checked against (tests/test_score_variants.py), and the scorer of contexts with
+// DLG_OPT_SCORE_KERNEL = DLG_SCORE_EXACT
+template <int P>
 __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
                                                  const float* __restrict__ Y,
                                                  const float* __restrict__ Z, int n,
@@ -166,7 +163,6 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
                                                  int32_t* __restrict__ counts) {
   constexpr int kChunk = kScBS * P;
   __shared__ float4 s_coef[kHT + 1];  // +1: the prefetch of the group's last plane reads past
-  __shared__ float2 s_band[KIND == kExact ? 1 : kHT + 1];
   __shared__ int s_cnt[kHT];
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
@@ -177,8 +173,6 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
     s_cnt[i] = 0;
     const HypRec hr = hyps[h0 + i];
     s_coef[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
-    if (KIND == kBand) s_band[i] = make_float2(hr.tlo, hr.thi);
-    if (KIND == kMin3) s_band[i] = make_float2(hr.w, 0.0f);
   }
   __syncthreads();
   const int nchunks = (n + kChunk - 1) / kChunk;
@@ -193,254 +187,30 @@ __global__ __launch_bounds__(kScBS) void k_score(const float* __restrict__ X,
       py[j] = ok ? Y[e] : qnan;
       pz[j] = ok ? Z[e] : qnan;
     }
-    {
-      constexpr int t0 = 0;
-      for (int g0 = 0; g0 < nt; g0 += kWave) {  // nt is a multiple of 64 (D padded with NaN planes)
-        int my = 0;
-        // software pipeline: the next hypothesis' LDS broadcast read is in flight while the
-        // current one is evaluated (the wait lands at the loop back-edge, not at first use)
-        float4 cnext = s_coef[g0];
-        float2 bnext = KIND == kExact ? make_float2(0.f, 0.f) : s_band[g0];
+    for (int g0 = 0; g0 < nt; g0 += kWave) {  // nt is a multiple of 64 (D padded with NaN planes)
+      int my = 0;
+      // software pipeline: the next hypothesis' LDS broadcast read is in flight while the
+      // current one is evaluated (the wait lands at the loop back-edge, not at first use)
+      float4 cnext = s_coef[g0];
 #pragma unroll 8
-        for (int k = 0; k < kWave; ++k) {
-          const float4 c = cnext;
-          const float2 bcur = bnext;
-          cnext = s_coef[g0 + k + 1];
-          if (KIND != kExact) bnext = s_band[g0 + k + 1];
-          int cnt = 0;
-          if (KIND == kExact) {
+      for (int k = 0; k < kWave; ++k) {
+        const float4 c = cnext;
+        cnext = s_coef[g0 + k + 1];
+        int cnt = 0;
 #pragma unroll
-            for (int j = 0; j < P; ++j) {
-              float dd = pcl_dot(c.x, c.y, c.z, c.w, px[j], py[j], pz[j]);
-              cnt += __popcll(ballot(fabsf(dd) < cthr));
-            }
-          } else if (KIND == kBand) {
-            const float2 band = bcur;
-            uint64_t border = 0;
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-              float f = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
-              uint64_t lo = ballot(fabsf(f) < band.x);
-              uint64_t hi = ballot(fabsf(f) < band.y);
-              cnt += __popcll(lo);
-              border |= lo ^ hi;
-            }
-            if (border) {  // rare: some lane is inside the rounding band -> exact PCL test there
-#pragma unroll
-              for (int j = 0; j < P; ++j) {
-                float f = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
-                bool inb = (fabsf(f) >= band.x) && (fabsf(f) < band.y);
-                float dd = pcl_dot(c.x, c.y, c.z, c.w, px[j], py[j], pz[j]);
-                cnt += __popcll(ballot(inb && (fabsf(dd) < cthr)));
-              }
-            }
-          } else {  // kMin3
-            const float w = bcur.x;
-            float m = INFINITY;
-#pragma unroll
-            for (int j = 0; j < P; j += 2) {
-              float f0 = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
-              float f1 = __builtin_fmaf(c.x, px[j + 1], __builtin_fmaf(c.y, py[j + 1], __builtin_fmaf(c.z, pz[j + 1], c.w)));
-              float r0 = fabsf(f0) - cthr, r1 = fabsf(f1) - cthr;
-              cnt += __popcll(ballot(r0 < -w));
-              cnt += __popcll(ballot(r1 < -w));
-              m = fminf(fminf(m, fabsf(r0)), fabsf(r1));  // v_min3_f32 m, |r0|, |r1|
-            }
-            if (ballot(m < w)) {  // rare: a point of this wave is within the band -> exact there
-#pragma unroll
-              for (int j = 0; j < P; ++j) {
-                float f = __builtin_fmaf(c.x, px[j], __builtin_fmaf(c.y, py[j], __builtin_fmaf(c.z, pz[j], c.w)));
-                bool inb = fabsf(fabsf(f) - cthr) < w;
-                float dd = pcl_dot(c.x, c.y, c.z, c.w, px[j], py[j], pz[j]);
-                cnt += __popcll(ballot(inb && (fabsf(dd) < cthr)));
-              }
-            }
-          }
-          my = writelane(my, cnt, k);
+        for (int j = 0; j < P; ++j) {
+          float dd = pcl_dot(c.x, c.y, c.z, c.w, px[j], py[j], pz[j]);
+          cnt += __popcll(ballot(fabsf(dd) < cthr));
         }
-        atomicAdd(&s_cnt[t0 + g0 + lane], my);
+        my = writelane(my, cnt, k);
       }
+      atomicAdd(&s_cnt[g0 + lane], my);
     }
   }
   __syncthreads();
   for (int i = tid; i < nt; i += kScBS) {
     int v = s_cnt[i];
     if (v) atomicAdd(&counts[h0 + i], v);
-  }
-}
-
-// k_score_s: the same counts, hypothesis coefficients in SGPRs.  A wave walks the hypotheses in
-// groups of GH (fully unrolled): the group's GH plane vectors come in by scalar loads (s_load,
-// scalar cache; wave-uniform), every VALU op takes its coefficient as the SGPR operand, so the
-// loop holds no LDS reads and no VGPRs for coefficients.  coef4 is padded with NaN planes to a
-// multiple of 64 (Dp); counts must have room for Dp entries.
-template <int KIND, int P, int GH>
-__global__ __launch_bounds__(kScBS) void k_score_s(const float* __restrict__ X,
-                                                   const float* __restrict__ Y,
-                                                   const float* __restrict__ Z, int n,
-                                                   const float4* __restrict__ coef4,
-                                                   const float* __restrict__ wband, int Dp,
-                                                   float cthr, int32_t* __restrict__ counts) {
-  constexpr int kChunk = kScBS * P;
-  __shared__ int s_cnt[kMaxHypPerLaunch];
-  const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1);
-  for (int i = tid; i < Dp; i += kScBS) s_cnt[i] = 0;
-  __syncthreads();
-  const int nchunks = (n + kChunk - 1) / kChunk;
-  const float qnan = __builtin_nanf("");
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    float px[P], py[P], pz[P];
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-      int e = ch * kChunk + j * kScBS + tid;
-      bool ok = e < n;
-      px[j] = ok ? X[e] : qnan;
-      py[j] = ok ? Y[e] : qnan;
-      pz[j] = ok ? Z[e] : qnan;
-    }
-    for (int g0 = 0; g0 < Dp; g0 += kWave) {
-      int my = 0;
-      for (int h0 = g0; h0 < g0 + kWave; h0 += GH) {
-        float4 c[GH];
-        float w[GH];
-#pragma unroll
-        for (int k = 0; k < GH; ++k) {
-          c[k] = coef4[h0 + k];
-          if (KIND == kMin3) w[k] = wband[h0 + k];
-        }
-#pragma unroll
-        for (int k = 0; k < GH; ++k) {
-          int cnt = 0;
-          if (KIND == kExact) {
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-              float dd = pcl_dot(c[k].x, c[k].y, c[k].z, c[k].w, px[j], py[j], pz[j]);
-              cnt += __popcll(ballot(fabsf(dd) < cthr));
-            }
-          } else {
-            float m = INFINITY;
-#pragma unroll
-            for (int j = 0; j < P; j += 2) {
-              float f0 = __builtin_fmaf(c[k].x, px[j], __builtin_fmaf(c[k].y, py[j], __builtin_fmaf(c[k].z, pz[j], c[k].w)));
-              float f1 = __builtin_fmaf(c[k].x, px[j + 1], __builtin_fmaf(c[k].y, py[j + 1], __builtin_fmaf(c[k].z, pz[j + 1], c[k].w)));
-              float r0 = fabsf(f0) - cthr, r1 = fabsf(f1) - cthr;
-              cnt += __popcll(ballot(r0 < -w[k]));
-              cnt += __popcll(ballot(r1 < -w[k]));
-              m = fminf(fminf(m, fabsf(r0)), fabsf(r1));
-            }
-            if (ballot(m < w[k])) {
-#pragma unroll
-              for (int j = 0; j < P; ++j) {
-                float f = __builtin_fmaf(c[k].x, px[j], __builtin_fmaf(c[k].y, py[j], __builtin_fmaf(c[k].z, pz[j], c[k].w)));
-                bool inb = fabsf(fabsf(f) - cthr) < w[k];
-                float dd = pcl_dot(c[k].x, c[k].y, c[k].z, c[k].w, px[j], py[j], pz[j]);
-                cnt += __popcll(ballot(inb && (fabsf(dd) < cthr)));
-              }
-            }
-          }
-          my = writelane(my, cnt, (h0 - g0) + k);
-        }
-      }
-      atomicAdd(&s_cnt[g0 + lane], my);
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < Dp; i += kScBS) {
-    int v = s_cnt[i];
-    if (v) atomicAdd(&counts[i], v);
-  }
-}
-
-// k_score_mfma: the same counts with the FMA chains on the matrix pipe.
-// v_mfma_f32_16x16x4f32 computes D[i][j] = fma(1, d_j, fma(z_i, c_j, fma(y_i, b_j, fma(x_i, a_j, 0))))
-// for 16 points i x 16 planes j (bit-for-bit a k-ordered f32 fmaf chain; |D - pcl_dot| <= 7 u S
-// as for the VALU prefilter).  A operand = 16 points (lane l: coordinate l>>4 of point l&15,
-// lanes 48..63 hold the homogeneous 1), B operand = 16 planes (lane l: coefficient l>>4 of plane
-// l&15), D in 4 VGPRs (lane l: rows 4(l>>4)+r of column l&15).  The VALU then only does
-// r = |D| - cthr, in iff r < -w (per-lane counter via the carry), and tracks min |r| per MFMA;
-// an MFMA tile with a value inside the band |r| < w is re-evaluated in PCL op order for exactly
-// those elements (points and planes fetched by cross-lane reads), so counts stay bit-identical.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <int PA>
-__global__ __launch_bounds__(kScBS) void k_score_mfma(const float* __restrict__ X,
-                                                      const float* __restrict__ Y,
-                                                      const float* __restrict__ Z, int n,
-                                                      const HypRec* __restrict__ hyps, int Dp,
-                                                      float cthr, int32_t* __restrict__ counts) {
-  constexpr int kWavePts = 16 * PA;                  // points held by one wave
-  constexpr int kChunk = (kScBS / kWave) * kWavePts;  // points per workgroup pass
-  __shared__ float s_b[kHT * 4];
-  __shared__ float s_w[kHT];
-  __shared__ int s_cnt[kMaxHypPerLaunch];
-  const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1);
-  const int wv = tid / kWave;
-  const int q = lane >> 4, r16 = lane & 15;
-  for (int i = tid; i < Dp; i += kScBS) s_cnt[i] = 0;
-  const int nchunks = (n + kChunk - 1) / kChunk;
-  const float qnan = __builtin_nanf("");
-  const float* base = q == 0 ? X : (q == 1 ? Y : Z);
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    float A[PA];
-    const int p0 = ch * kChunk + wv * kWavePts;
-#pragma unroll
-    for (int p = 0; p < PA; ++p) {
-      const int e = p0 + p * 16 + r16;
-      A[p] = q == 3 ? 1.0f : (e < n ? base[e] : qnan);
-    }
-    for (int t0 = 0; t0 < Dp; t0 += kHT) {
-      const int nt = min(kHT, Dp - t0);
-      __syncthreads();
-      for (int i = tid; i < nt; i += kScBS) {
-        const HypRec hr = hyps[t0 + i];
-        reinterpret_cast<float4*>(s_b)[i] = make_float4(hr.a, hr.b, hr.c, hr.d);
-        s_w[i] = hr.w;
-      }
-      __syncthreads();
-      for (int h0 = 0; h0 < nt; h0 += 16) {
-        const float bop = s_b[(h0 + r16) * 4 + q];  // conflict-free: 64 consecutive floats
-        const float w = s_w[h0 + r16];
-        int cnt = 0;
-        float m = INFINITY;
-        // branch-free main pass: MFMA p+1 overlaps the VALU work on the result of MFMA p
-#pragma unroll
-        for (int p = 0; p < PA; ++p) {
-          const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(A[p], bop, zero, 0, 0, 0);
-          const float r0 = fabsf(d[0]) - cthr, r1 = fabsf(d[1]) - cthr;
-          const float r2 = fabsf(d[2]) - cthr, r3 = fabsf(d[3]) - cthr;
-          cnt += (r0 < -w) + (r1 < -w) + (r2 < -w) + (r3 < -w);
-          m = fminf(fminf(m, fabsf(r0)), fabsf(r1));
-          m = fminf(fminf(m, fabsf(r2)), fabsf(r3));
-        }
-        if (ballot(m < w)) {  // rare: an element of this tile lies in the band -> PCL order there
-          const float ca = __shfl(bop, r16), cb = __shfl(bop, 16 + r16);
-          const float cc = __shfl(bop, 32 + r16), cd = __shfl(bop, 48 + r16);
-          for (int p = 0; p < PA; ++p) {
-            const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(A[p], bop, zero, 0, 0, 0);
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              const int i = 4 * q + rr;
-              const float px = __shfl(A[p], i), py = __shfl(A[p], 16 + i), pz = __shfl(A[p], 32 + i);
-              const bool band = fabsf(fabsf(d[rr]) - cthr) < w;
-              const float ex = pcl_dot(ca, cb, cc, cd, px, py, pz);
-              cnt += (band && fabsf(ex) < cthr) ? 1 : 0;
-            }
-          }
-        }
-        // lanes r16, r16 + 16, r16 + 32, r16 + 48 hold partial counts of plane h0 + r16
-        cnt += __shfl_xor(cnt, 16);
-        cnt += __shfl_xor(cnt, 32);
-        if (q == 0) atomicAdd(&s_cnt[t0 + h0 + r16], cnt);
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < Dp; i += kScBS) {
-    int v = s_cnt[i];
-    if (v) atomicAdd(&counts[i], v);
   }
 }
 
@@ -622,251 +392,6 @@ __global__ __launch_bounds__(kBfBS) void k_score_bf16(const float* __restrict__ 
     c += __shfl_xor(c, 32);  // lanes l and l + 32 hold the two row halves of column l & 31
     const int h = (g * TH + t) * 32 + r32;
     if (hh == 0 && c && h < D) atomicAdd(&counts[h], (int32_t)c);
-  }
-}
-
-// v_min_f32 m, m, |r| without the canonicalising v_max that fminf() brings along
-__device__ __forceinline__ float min_abs(float m, float r) {
-  float o;
-  asm("v_min_f32_e64 %0, %1, |%2|" : "=v"(o) : "v"(m), "v"(r));
-  return o;
-}
-
-// one block of points (wave-uniform) against this lane's hypothesis; NB = 16 -> full block,
-// NB = 0 -> tail of nb < 16 points (guarded).  Returns the lane's inlier count for the block.
-template <int KIND, int NB>
-__device__ __forceinline__ int score_block(const float* __restrict__ X, const float* __restrict__ Y,
-                                           const float* __restrict__ Z, int jb, int nb, float a,
-                                           float b, float c, float d, float tlo, float W2,
-                                           float cthr) {
-  float px[16], py[16], pz[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const bool ok = NB == 16 || k < nb;
-    px[k] = ok ? X[jb + k] : 0.f;
-    py[k] = ok ? Y[jb + k] : 0.f;
-    pz[k] = ok ? Z[jb + k] : 0.f;
-  }
-  int cnt = 0;
-  if (KIND == kExact) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      if (NB == 16 || k < nb) {
-        float dd = pcl_dot(a, b, c, d, px[k], py[k], pz[k]);
-        cnt += fabsf(dd) < cthr ? 1 : 0;
-      }
-    }
-    return cnt;
-  }
-  float m = INFINITY;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    if (NB == 16 || k < nb) {
-      float f = __builtin_fmaf(a, px[k], __builtin_fmaf(b, py[k], __builtin_fmaf(c, pz[k], d)));
-      float r = fabsf(f) - tlo;
-      cnt += r < 0.0f ? 1 : 0;
-      m = min_abs(m, r);
-    }
-  }
-  if (__builtin_amdgcn_ballot_w64(m <= W2)) {  // rare: a point in some lane's band -> PCL order
-    int ex = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      if (NB == 16 || k < nb) {
-        float dd = pcl_dot(a, b, c, d, px[k], py[k], pz[k]);
-        ex += fabsf(dd) < cthr ? 1 : 0;
-      }
-    }
-    cnt = ex;
-  }
-  return cnt;
-}
-
-// k_score_h: lanes = hypotheses, points = wave-uniform scalars.
-// A wave owns 64 hypotheses (one per lane: a, b, c, d and its band in VGPRs) and streams one
-// partition of the points through the scalar cache (s_load_dwordx16 of X, Y, Z: 16 points per
-// block, the same addresses for every wave of the workgroup).  Each lane counts its own
-// hypothesis with v_cmp + v_addc -- no ballot/popcount on the scalar unit and no cross-lane
-// reduction; at the end one atomic per lane.  Every VALU op takes the point coordinate as its
-// one SGPR operand.
-//   kExact : PCL op order, 3 v_mul + 3 v_add + v_cmp + v_addc             8 VALU / test
-//   kMin3  : f = fma chain; r = |f| - tlo; in iff r < 0 (exact since |f| < tlo guarantees
-//            |pcl| < cthr); band iff |r| <= W2 = thi - tlo tracked by v_min3, re-evaluated in
-//            PCL order for the 16-point block                             6.5 VALU / test
-// X/Y/Z must be readable up to n rounded up to 16 (allocation slack); the tail block is
-// handled by a wave-uniform bound.
-template <int KIND>
-__global__ __launch_bounds__(kScBS) void k_score_h(const float* __restrict__ X,
-                                                   const float* __restrict__ Y,
-                                                   const float* __restrict__ Z, int n,
-                                                   const HypRec* __restrict__ hyps, int Dp,
-                                                   int part, float cthr,
-                                                   int32_t* __restrict__ counts) {
-  constexpr int kWpg = kScBS / kWave;                  // waves (hypothesis groups) per workgroup
-  const int ngroups = Dp / kWave;
-  const int gblocks = (ngroups + kWpg - 1) / kWpg;      // workgroups per point partition
-  const int wv = threadIdx.x / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int hg = (blockIdx.x % gblocks) * kWpg + wv;    // this wave's hypothesis group
-  const int pp = blockIdx.x / gblocks;                  // point partition
-  if (hg >= ngroups) return;
-  const int h = hg * kWave + lane;
-  const HypRec hr = hyps[h];
-  const float a = hr.a, b = hr.b, c = hr.c, d = hr.d;
-  const float tlo = hr.tlo;
-  const float W2 = (hr.thi - hr.tlo) * (1.0f + 1.0f / 4194304.0f);  // >= fl(thi - tlo)
-  const int j0 = pp * part;
-  const int j1 = min(n, j0 + part);
-  int cnt = 0;
-  // full 16-point blocks (no per-point guards: the loop body is straight-line VALU)
-  int jb = j0;
-  for (; jb + 16 <= j1; jb += 16) cnt += score_block<KIND, 16>(X, Y, Z, jb, 16, a, b, c, d, tlo, W2, cthr);
-  if (jb < j1) cnt += score_block<KIND, 0>(X, Y, Z, jb, j1 - jb, a, b, c, d, tlo, W2, cthr);
-  atomicAdd(&counts[h], cnt);
-}
-
-// k_score_hl: lanes = hypotheses (as k_score_h), points staged per workgroup in LDS.
-// The workgroup (8 waves = 8 groups of 64 hypotheses) walks its point partition in chunks of
-// kHlChunk points: coalesced float4 global loads of the next chunk are issued before the current
-// chunk is evaluated and written to the other LDS buffer afterwards (one barrier per chunk).
-// A wave reads 4 points at a time with wave-uniform ds_read_b128 (broadcast) and moves them to
-// SGPRs with v_readfirstlane, so each FMA / mul has one SGPR operand.
-constexpr int kHlChunk = 1024;
-
-__device__ __forceinline__ float sgpr(float v) {
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-
-template <int KIND>
-__device__ __forceinline__ int hl_quad(const float4& xs, const float4& ys, const float4& zs, float a,
-                                       float b, float c, float d, float tlo, float cthr, float& m) {
-  const float px[4] = {sgpr(xs.x), sgpr(xs.y), sgpr(xs.z), sgpr(xs.w)};
-  const float py[4] = {sgpr(ys.x), sgpr(ys.y), sgpr(ys.z), sgpr(ys.w)};
-  const float pz[4] = {sgpr(zs.x), sgpr(zs.y), sgpr(zs.z), sgpr(zs.w)};
-  int cnt = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (KIND == kExact) {
-      float dd = pcl_dot(a, b, c, d, px[k], py[k], pz[k]);
-      cnt += fabsf(dd) < cthr ? 1 : 0;
-    } else {
-      float f = __builtin_fmaf(a, px[k], __builtin_fmaf(b, py[k], __builtin_fmaf(c, pz[k], d)));
-      float r = fabsf(f) - tlo;
-      cnt += r < 0.0f ? 1 : 0;
-      m = min_abs(m, r);
-    }
-  }
-  return cnt;
-}
-
-template <int KIND>
-__global__ __launch_bounds__(kScBS) void k_score_hl(const float* __restrict__ X,
-                                                    const float* __restrict__ Y,
-                                                    const float* __restrict__ Z, int n,
-                                                    const HypRec* __restrict__ hyps, int Dp,
-                                                    int part, float cthr,
-                                                    int32_t* __restrict__ counts) {
-  constexpr int kWpg = kScBS / kWave;
-  __shared__ float4 s_pts[2][3][kHlChunk / 4];  // [buffer][x|y|z][chunk/4]: 24 KB
-  const int ngroups = Dp / kWave;
-  const int gblocks = (ngroups + kWpg - 1) / kWpg;
-  const int wv = threadIdx.x / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int hg = (blockIdx.x % gblocks) * kWpg + wv;
-  const int pp = blockIdx.x / gblocks;
-  const bool active = hg < ngroups;           // wave-uniform; idle waves still help stage
-  const int h = min(hg, ngroups - 1) * kWave + lane;
-  const HypRec hr = hyps[h];
-  const float a = hr.a, b = hr.b, c = hr.c, d = hr.d;
-  const float tlo = hr.tlo;
-  const float W2 = (hr.thi - hr.tlo) * (1.0f + 1.0f / 4194304.0f);
-  const int j0 = pp * part;
-  const int j1 = min(n, j0 + part);
-  const int nch = (j1 - j0 + kHlChunk - 1) / kHlChunk;
-  const float qnan = __builtin_nanf("");
-  // staging: thread t loads float4 #(t % 256) of array (t / 256) (two rounds cover x, y, z)
-  auto load_chunk = [&](int cj, float4 (&v)[2]) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int idx = threadIdx.x + r * kScBS;  // 0 .. 1023 (768 used)
-      const int arr = idx / (kHlChunk / 4), q4 = idx % (kHlChunk / 4);
-      float4 t = make_float4(qnan, qnan, qnan, qnan);
-      if (arr < 3) {
-        const float* P = arr == 0 ? X : (arr == 1 ? Y : Z);
-        const int e = cj + 4 * q4;
-        if (e + 3 < j1) {
-          t = *reinterpret_cast<const float4*>(P + e);  // partitions/chunks are 4-aligned
-        } else {
-          if (e < j1) t.x = P[e];
-          if (e + 1 < j1) t.y = P[e + 1];
-          if (e + 2 < j1) t.z = P[e + 2];
-        }
-      }
-      v[r] = t;
-    }
-  };
-  auto store_chunk = [&](int buf, const float4 (&v)[2]) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int idx = threadIdx.x + r * kScBS;
-      const int arr = idx / (kHlChunk / 4), q4 = idx % (kHlChunk / 4);
-      if (arr < 3) s_pts[buf][arr][q4] = v[r];
-    }
-  };
-  int cnt = 0;
-  float4 stage[2];
-  if (nch > 0) {
-    load_chunk(j0, stage);
-    store_chunk(0, stage);
-  }
-  __syncthreads();
-  for (int ci = 0; ci < nch; ++ci) {
-    const int buf = ci & 1;
-    const int cj = j0 + ci * kHlChunk;
-    if (ci + 1 < nch) load_chunk(cj + kHlChunk, stage);  // in flight during the compute below
-    if (active) {
-      const int npts = min(kHlChunk, j1 - cj);
-      for (int q = 0; q < npts; q += 16) {  // 16-point blocks: 4 quads, one band check
-        float m = INFINITY;
-        int blk = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int qi = (q >> 2) + t;
-          blk += hl_quad<KIND>(s_pts[buf][0][qi], s_pts[buf][1][qi], s_pts[buf][2][qi], a, b, c,
-                               d, tlo, cthr, m);
-        }
-        if (KIND != kExact && __builtin_amdgcn_ballot_w64(m <= W2)) {
-          float mm = INFINITY;
-          int ex = 0;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int qi = (q >> 2) + t;
-            ex += hl_quad<kExact>(s_pts[buf][0][qi], s_pts[buf][1][qi], s_pts[buf][2][qi], a, b,
-                                  c, d, tlo, cthr, mm);
-          }
-          blk = ex;
-        }
-        cnt += blk;
-      }
-    }
-    if (ci + 1 < nch) store_chunk(buf ^ 1, stage);
-    __syncthreads();
-  }
-  if (active) atomicAdd(&counts[h], cnt);
-}
-
-__global__ void k_pack_coef(const HypRec* __restrict__ hyps, int D, int Dp, float4* __restrict__ coef4,
-                            float* __restrict__ wband) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= Dp) return;
-  const float qnan = __builtin_nanf("");
-  if (i < D) {
-    const HypRec h = hyps[i];
-    coef4[i] = make_float4(h.a, h.b, h.c, h.d);
-    wband[i] = h.w;
-  } else {
-    coef4[i] = make_float4(qnan, qnan, qnan, qnan);
-    wband[i] = 0.0f;
   }
 }
 
@@ -1081,8 +606,10 @@ __global__ __launch_bounds__(256) void k_publish(const int32_t* __restrict__ tot
                                                  const int32_t* __restrict__ rk, int nrk,
                                                  const int32_t* __restrict__ pick, int npick,
                                                  const int32_t* __restrict__ res, int nres,
-                                                 int32_t* pub, int32_t seq) {
+                                                 const int32_t* __restrict__ err, int32_t* pub,
+                                                 int32_t seq) {
   const int t = threadIdx.x;
+  if (t == 0) pub[kPubErr] = err ? *err : 0;
   for (int i = t; i < ntot; i += 256) pub[kPubTot + i] = totals[i];
   for (int i = t; i < 4 * nsmall; i += 256)
     pub[kPubSmall + i] = __float_as_int(reinterpret_cast<const float*>(small)[i]);
@@ -1245,13 +772,16 @@ constexpr int kS1It = 16;                          // points per lane, lane-stri
 constexpr int kS1Tile = kS1BS * kS1It;             // 16384 points per tile
 constexpr int kS1Slots = kS1It * (kS1BS / kWave);  // (j, wave) counts of a tile: 256
 static_assert(kS1Slots % kWave == 0 && kS1Slots <= kS1BS, "slot scan layout");
-int sel1_tiles(int64_t n) { return (int)((n + kS1Tile - 1) / kS1Tile); }
 
 // tile = workgroup index: workgroups are dispatched in index order on each XCD, so the lowest
 // unfinished tile has every predecessor done and always completes (a claim counter would be
 // one same-address device atomic per tile, measured slower).  The look-back still carries an
-// exit: after kS1Spin empty polls the tile gives up, scatters nothing and reports -1 in its
-// totals, which the host turns into an error.
+// exit: after kS1Spin empty polls the tile gives up, scatters nothing, publishes flag 3 (failed)
+// and sets the sticky error word *L.err, which the last tile never writes; a tile whose
+// look-back meets a failed tile fails the same way.  (A successor may already have summed a
+// failed tile's aggregate and completed: only the sticky word is reliable, so the host checks
+// it -- in the round's publish for k_sel1_morton, at the next publish / the end of the
+// extraction for k_sel1_list.)
 constexpr int kS1Spin = 1 << 20;
 
 // in-tile exclusive ranks from the (j, wave) counts in s_cnt, the tile's exclusive prefix by
@@ -1311,16 +841,22 @@ __device__ __forceinline__ int sel1_scan(const Sel1State& L, int tile, int* s_cn
         }
         // the nearest window holding a prefix, and the lanes of it that are needed
         int kp = K, fp = kWave;
-        bool missing = false;
+        bool missing = false, failed = false;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          if (kp == K && !missing) {
+          if (kp == K && !missing && !failed) {
             const uint64_t pm = ballot(f[k] == 2u), zm = ballot(f[k] == 0u);
+            const uint64_t fm = ballot(f[k] == 3u);
             const int q = pm ? __builtin_ctzll(pm) : kWave;
             const uint64_t need = q >= kWave - 1 ? ~0ull : ((2ull << q) - 1ull);
-            if (zm & need) missing = true;
+            if (fm & need) failed = true;
+            else if (zm & need) missing = true;
             else if (q < kWave) { kp = k; fp = q; }
           }
+        }
+        if (failed) {
+          excl = -1;
+          break;
         }
         if (missing) {
           if (++spins > kS1Spin) {
@@ -1340,9 +876,16 @@ __device__ __forceinline__ int sel1_scan(const Sel1State& L, int tile, int* s_cn
         if (kp < K) break;
         look -= K * kWave;
       }
-      if (lane == 0 && excl >= 0)
-        __hip_atomic_store(L.status + tile, ep | (2ull << 30) | (uint32_t)(excl + agg),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {
+        if (excl >= 0) {
+          __hip_atomic_store(L.status + tile, ep | (2ull << 30) | (uint32_t)(excl + agg),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {  // failed: successors fail too; the sticky word tells the host
+          __hip_atomic_store(L.status + tile, ep | (3ull << 30), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          atomicOr(L.err, 1);
+        }
+      }
     }
     if (lane == 0) {
       s_base[0] = excl;
@@ -1386,10 +929,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const flo
     if ((threadIdx.x & (kWave - 1)) == 0) s_cnt[j * (kS1BS / kWave) + w] = __popcll(m[j]);
   }
   const int excl = sel1_scan(L, tile, s_cnt, s_pre, s_base);
-  if (excl < 0) {
-    if (threadIdx.x == 0) totals[0] = -1;
-    return;
-  }
+  if (excl < 0) return;  // (look-back failed: *L.err is set)
 #pragma unroll
   for (int j = 0; j < kS1It; ++j) {
     const int64_t e = base + j * kS1BS + threadIdx.x;
@@ -1449,10 +989,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__
   for (int j = 0; j < kS1It; ++j)
     gi[j] = pgid[((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull) ? p[j] : p[0]];
   const int excl = sel1_scan(L, tile, s_cnt, s_pre, s_base);
-  if (excl < 0) {
-    if (threadIdx.x == 0) totals[0] = -1;
-    return;
-  }
+  if (excl < 0) return;  // (look-back failed: *L.err is set)
 #pragma unroll
   for (int j = 0; j < kS1It; ++j) {
     const int64_t e = base + j * kS1BS + threadIdx.x;
@@ -1656,6 +1193,8 @@ void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleR
                      lidx, lidx ? n_list : src.n, samples, cthr, ax, ay, az, hyps, res);
 }
 
+int sel1_tiles(int64_t n) { return (int)((n + kS1Tile - 1) / kS1Tile); }
+
 // single-pass selects (lean-list rounds): every launch stamps its status words with a fresh epoch
 static void sel1_next(Sel1State& L, int) { ++L.epoch; }
 
@@ -1706,20 +1245,7 @@ void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, fl
                      ay, az, hyps, good);
 }
 
-// fastest measured with bit-identical counts (tools/score_ab.py, tests/test_score_variants.py):
-// bf16 matrix-core distances + VALU band check 10.8 T tests/s vs 7.6 T for the exact VALU kernel
-int kScoreDefault = kScoreBf16T8;
-
-int score_variant() {
-  static const int v = [] {
-    const char* e = std::getenv("DLG_SCORE_VARIANT");
-    const int x = e ? std::atoi(e) : -1;
-    return x >= 0 && x < kScorePruned ? x : kScoreDefault;
-  }();
-  return v;
-}
-
-template <int KIND, int P>
+template <int P>
 static void launch_score_t(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
                            int num_cus, hipStream_t s) {
   constexpr int kChunk = kScBS * P;
@@ -1742,38 +1268,8 @@ static void launch_score_t(PointsView src, const HypRec* hyps, int D, float cthr
   // so with gridDim.x a multiple of 8 the slices of one chunk run on the same XCD at the same
   // time and share its L2 (the chunk is fetched from HBM once, not once per slice)
   if (slices > 1 && bx >= 8) bx = std::min<int64_t>((bx + 7) / 8 * 8, std::max<int64_t>(8, cap / slices / 8 * 8));
-  hipLaunchKernelGGL((k_score<KIND, P>), dim3((unsigned)bx, (unsigned)slices), dim3(kScBS), 0, s,
+  hipLaunchKernelGGL((k_score<P>), dim3((unsigned)bx, (unsigned)slices), dim3(kScBS), 0, s,
                      src.x, src.y, src.z, (int)src.n, hyps, D, w, cthr, counts);
-}
-
-template <int KIND, int P, int GH>
-static void launch_score_s(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
-                           int num_cus, hipStream_t s) {
-  constexpr int kChunk = kScBS * P;
-  const int Dp = (D + kWave - 1) / kWave * kWave;
-  // packed plane vectors live behind the hypothesis records' scratch tail (see score_scratch)
-  float4* coef4 = reinterpret_cast<float4*>(const_cast<HypRec*>(hyps) + kMaxHypPerLaunch);
-  float* wband = reinterpret_cast<float*>(coef4 + kMaxHypPerLaunch);
-  hipLaunchKernelGGL(k_pack_coef, dim3((Dp + 255) / 256), dim3(256), 0, s, hyps, D, Dp, coef4, wband);
-  const int64_t nchunks = (src.n + kChunk - 1) / kChunk;
-  const int64_t cap = (int64_t)num_cus * 4;
-  const int64_t per = (nchunks + cap - 1) / cap;
-  const unsigned grid = (unsigned)((nchunks + per - 1) / per);
-  hipLaunchKernelGGL((k_score_s<KIND, P, GH>), dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
-                     (int)src.n, coef4, wband, Dp, cthr, counts);
-}
-
-template <int PA>
-static void launch_score_mfma(PointsView src, const HypRec* hyps, int D, float cthr,
-                              int32_t* counts, int num_cus, hipStream_t s) {
-  constexpr int kChunk = (kScBS / kWave) * 16 * PA;
-  const int Dp = (D + kWave - 1) / kWave * kWave;  // hyps[D..Dp) must be NaN planes (padded)
-  const int64_t nchunks = (src.n + kChunk - 1) / kChunk;
-  const int64_t cap = (int64_t)num_cus * 4;
-  const int64_t per = (nchunks + cap - 1) / cap;
-  const unsigned grid = (unsigned)((nchunks + per - 1) / per);
-  hipLaunchKernelGGL((k_score_mfma<PA>), dim3(grid), dim3(kScBS), 0, s, src.x, src.y, src.z,
-                     (int)src.n, hyps, Dp, cthr, counts);
 }
 
 template <int TH>
@@ -1812,63 +1308,13 @@ void launch_prep_bf16(const HypRec* hyps, int D, const uint4** bcol_out, const f
   *band_out = band;
 }
 
-template <int KIND>
-static void launch_score_h(PointsView src, const HypRec* hyps, int D, float cthr,
-                           int32_t* counts, int num_cus, hipStream_t s) {
-  constexpr int kWpg = kScBS / kWave;
-  const int Dp = (D + kWave - 1) / kWave * kWave;  // hyps[D..Dp) are NaN planes
-  const int ngroups = Dp / kWave;
-  const int gblocks = (ngroups + kWpg - 1) / kWpg;
-  // enough partitions for ~8 resident waves per SIMD, partitions a multiple of 16 points
-  const int64_t want_waves = (int64_t)num_cus * 4 * 8;
-  int64_t nparts = (want_waves + ngroups - 1) / ngroups;
-  int64_t part = (src.n + nparts - 1) / nparts;
-  part = std::max<int64_t>(256, (part + 15) / 16 * 16);
-  nparts = (src.n + part - 1) / part;
-  hipLaunchKernelGGL((k_score_h<KIND>), dim3((unsigned)(nparts * gblocks)), dim3(kScBS), 0, s,
-                     src.x, src.y, src.z, (int)src.n, hyps, Dp, (int)part, cthr, counts);
-}
-
-template <int KIND>
-static void launch_score_hl(PointsView src, const HypRec* hyps, int D, float cthr,
-                            int32_t* counts, int num_cus, hipStream_t s) {
-  constexpr int kWpg = kScBS / kWave;
-  const int Dp = (D + kWave - 1) / kWave * kWave;
-  const int ngroups = Dp / kWave;
-  const int gblocks = (ngroups + kWpg - 1) / kWpg;
-  const int64_t want_blocks = (int64_t)num_cus * 4 * 2;  // 2 x (4 resident 8-wave blocks / CU)
-  int64_t nparts = std::max<int64_t>(1, (want_blocks + gblocks - 1) / gblocks);
-  int64_t part = (src.n + nparts - 1) / nparts;
-  part = std::max<int64_t>(kHlChunk, (part + kHlChunk - 1) / kHlChunk * kHlChunk);
-  nparts = (src.n + part - 1) / part;
-  hipLaunchKernelGGL((k_score_hl<KIND>), dim3((unsigned)(nparts * gblocks)), dim3(kScBS), 0, s,
-                     src.x, src.y, src.z, (int)src.n, hyps, Dp, (int)part, cthr, counts);
-}
-
 void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
-                  int variant, int num_cus, hipStream_t s) {
+                  int kernel, int num_cus, hipStream_t s) {
   if (D <= 0 || src.n <= 0) return;
-  switch (variant) {
-    case kScoreBf16T4: launch_score_bf16<4>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreBf16T8: launch_score_bf16<8>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreLdsExact: launch_score_hl<kExact>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreLdsMin3: launch_score_hl<kMin3>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreLanesExact: launch_score_h<kExact>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreLanesMin3: launch_score_h<kMin3>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreMfma32: launch_score_mfma<32>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreMfma16: launch_score_mfma<16>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreMfma8: launch_score_mfma<8>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreExactS8: launch_score_s<kExact, 8, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreMin3S8: launch_score_s<kMin3, 8, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreExactS4: launch_score_s<kExact, 4, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreExactS8G4: launch_score_s<kExact, 8, 4>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreBandP8: launch_score_t<kBand, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreMin3P8: launch_score_t<kMin3, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreExactP16: launch_score_t<kExact, 16>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreMin3P16: launch_score_t<kMin3, 16>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreExactP4: launch_score_t<kExact, 4>(src, hyps, D, cthr, counts, num_cus, s); break;
-    case kScoreMin3P4: launch_score_t<kMin3, 4>(src, hyps, D, cthr, counts, num_cus, s); break;
-    default: launch_score_t<kExact, 8>(src, hyps, D, cthr, counts, num_cus, s); break;
+  switch (kernel) {
+    case kScoreExact: launch_score_t<4>(src, hyps, D, cthr, counts, num_cus, s); break;
+    case kScoreBf16: launch_score_bf16<8>(src, hyps, D, cthr, counts, num_cus, s); break;
+    default: break;
   }
 }
 
@@ -1918,9 +1364,10 @@ void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypR
 
 void launch_publish(const int32_t* totals, int ntot, const float4* small, int nsmall,
                     const int32_t* rk, int nrk, const int32_t* pick, int npick,
-                    const int32_t* res, int nres, int32_t* pub, int32_t seq, hipStream_t s) {
+                    const int32_t* res, int nres, const int32_t* err, int32_t* pub, int32_t seq,
+                    hipStream_t s) {
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, totals, ntot, small, nsmall, rk, nrk,
-                     pick, npick, res, nres, pub, seq);
+                     pick, npick, res, nres, err, pub, seq);
 }
 
 int select_tiles(int64_t n) { return (int)((n + kSelTile - 1) / kSelTile); }
@@ -1968,10 +1415,6 @@ void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest&
                      int32_t* counts, int num_cus, hipStream_t s) {
   if (D <= 0 || src.n <= 0) return;
   const int Dp = (D + kWave - 1) / kWave * kWave;
-  static const int variant = [] {
-    const char* e = std::getenv("DLG_NP_VARIANT");
-    return e ? std::atoi(e) : 0;
-  }();
   auto go = [&](auto kern, int P, int per_cu) {
     const int64_t chunks = (src.n + (int64_t)kNpBS * P - 1) / ((int64_t)kNpBS * P);
     const int64_t cap = (int64_t)num_cus * per_cu;
@@ -1980,19 +1423,10 @@ void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest&
                        counts);
   };
   // LDS per block: 16 KB counts + 32 B x HT planes + 4 KB x P point normals + 6 KB queue.
-  // Measured on C5 (10M points, 4096 planes/launch; tools/bench_c5.py, DLG_NP_VARIANT):
-  // <2,256> x4/CU 2.55 T tests/s > <2,128> 2.50 > <2,64> 2.43 > <4,256> x3 2.40 > <1,256> 2.21 >
-  // <4,512>, <8,256>, <4,1024> x2 1.69-1.73 (occupancy-bound: 2 waves/SIMD)
-  switch (variant) {
-    case 1: go(k_score_np<4, 1024>, 4, 2); break;
-    case 2: go(k_score_np<8, 256>, 8, 2); break;
-    case 3: go(k_score_np<4, 512>, 4, 2); break;
-    case 4: go(k_score_np<4, 256>, 4, 3); break;
-    case 5: go(k_score_np<2, 128>, 2, 4); break;
-    case 6: go(k_score_np<1, 256>, 1, 4); break;
-    case 7: go(k_score_np<2, 64>, 2, 4); break;
-    default: go(k_score_np<2, 256>, 2, 4); break;
-  }
+  // Measured on C5 (10M points, 4096 planes/launch; round 1, tools/bench_c5.py):
+  // <P=2, HT=256> x4/CU 2.55 T tests/s > <2,128> 2.50 > <2,64> 2.43 > <4,256> x3 2.40 >
+  // <1,256> 2.21 > <4,512>, <8,256>, <4,1024> x2 1.69-1.73 (occupancy-bound: 2 waves/SIMD)
+  go(k_score_np<2, 256>, 2, 4);
 }
 
 void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,

@@ -18,12 +18,12 @@ struct alignas(16) SampleRec {
   float x, y, z;
 };
 
-// plane hypothesis: PCL coefficients + the prefilter band [tlo, thi) around the exact threshold
+// plane hypothesis: PCL coefficients + the rounding band of an FMA evaluation around cthr
 struct alignas(16) HypRec {
   float a, b, c, d;
-  float tlo, thi;
-  int32_t good;  // SampleConsensusModelPlane::isSampleGood
-  float w;       // band half-width around cthr for the |fma(...)| - cthr test (variant 2)
+  float tlo, thi;  // [cthr - 7 u S, cthr + 7 u S) rounded outwards
+  int32_t good;    // SampleConsensusModelPlane::isSampleGood
+  float w;         // >= 7 u S (k_prep_bf16 derives the matrix-core band from it)
 };
 
 // nrm (optional, SACMODEL_NORMAL_PLANE): per point (n.normalized() as Eigen computes it for
@@ -59,32 +59,15 @@ constexpr int kMaxHypPerLaunch = 4096;  // LDS count array of the scoring kernel
 constexpr int kSelTile = 4096;          // points per select/compact workgroup
 constexpr int kMomentK = 10;            // n, sx, sy, sz, sxx, sxy, sxz, syy, syz, szz
 
-// Scoring kernel variants (A/B via dlg_score_benchmark; the product uses kScoreDefault).
-//   exact : PCL op order (3 mul + 3 add) + compare                          7 VALU + 2 SALU / slot
-//   band  : FMA chain, two compares against [tlo, thi), exact recheck in band  5 VALU + 4 SALU
-//   min3  : FMA chain, r = |f| - cthr, in iff r < -w, band tracked by v_min3   5.5 VALU + 2 SALU
-// P = points per lane.
-enum ScoreVariant {
-  kScoreExactP8 = 0, kScoreBandP8 = 1, kScoreMin3P8 = 2, kScoreExactP16 = 3, kScoreMin3P16 = 4,
-  kScoreExactP4 = 5, kScoreMin3P4 = 6,
-  // coefficients in SGPRs (scalar loads), G hypotheses unrolled per group
-  kScoreExactS8 = 7, kScoreMin3S8 = 8, kScoreExactS4 = 9, kScoreExactS8G4 = 10,
-  // FMA chains on v_mfma_f32_16x16x4f32, band compare + counting on the VALU (PA x 16 points/wave)
-  kScoreMfma32 = 11, kScoreMfma16 = 12, kScoreMfma8 = 13,
-  // lanes = hypotheses, points as wave-uniform scalars (s_load), per-lane v_addc counting
-  kScoreLanesExact = 14, kScoreLanesMin3 = 15,
-  // lanes = hypotheses, points staged in LDS, broadcast-read and moved to SGPRs
-  kScoreLdsExact = 16, kScoreLdsMin3 = 17,
-  // plane distances on the bf16 matrix cores (3-way split operands, products exact), counting +
-  // band tracking on the VALU (~2.25 ops / test), exact PCL recheck inside the rounding band;
-  // T = 32-plane tiles held per wave
-  kScoreBf16T4 = 18, kScoreBf16T8 = 19,
-  // k_score_bf16's 32 x 32 blocks only for (tile, plane) pairs the bounding spheres cannot rule
-  // out, over the cloud's Morton-ordered copy (spatial.hpp; dlg_score_benchmark only -- the
-  // product takes it whenever the cloud has a spatial copy)
-  kScorePruned = 20,
-  kScoreNumVariants = 21
-};
+// Exhaustive scoring kernels (every active point against every hypothesis; the pruned kernel
+// of spatial.hpp is the default whenever the cloud has a Morton copy).  All give bit-identical
+// counts (tests/test_score_variants.py); dlg_score_benchmark takes these values.
+//   exact  : PCL op order (3 mul + 3 add) + compare on the VALU, 4 points per lane
+//   bf16   : plane distances on the bf16 matrix cores (3-way split operands, products exact),
+//            counting + band tracking on the VALU, exact PCL re-decision inside the rounding band
+//   pruned : k_score_bf16's 32 x 32 blocks only for (tile, plane) pairs the bounding spheres
+//            cannot rule out (dlg_score_benchmark only: the driver takes it whenever it can)
+enum ScoreKernel { kScoreExact = 0, kScoreBf16 = 1, kScorePruned = 2 };
 // hyps buffer layout for launch_score: HypRec[kMaxHypPerLaunch] followed by the packed float4
 // plane vectors and float band widths (score_scratch_bytes); counts need room for D rounded up
 // to a multiple of 64.
@@ -93,19 +76,17 @@ enum ScoreVariant {
 constexpr size_t kHypScratchBytes =
     kMaxHypPerLaunch * (sizeof(HypRec) + sizeof(float4) + sizeof(float) + 4 * sizeof(uint4) +
                         sizeof(float2));
-extern int kScoreDefault;
-// kScoreDefault unless DLG_SCORE_VARIANT names another variant (A/B of the full pipeline)
-int score_variant();
-
 void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
                            hipStream_t s);
 // writes hyps[D] and good[D] (int32 flags next to the counts for one D2H copy)
 // round results into the coherent pinned buffer pub (layout below), then pub[0] = seq (release,
 // system scope)
-constexpr int kPubTot = 1, kPubPick = 5, kPubSmall = 8, kPubRk = 32;  // + nrk: counts
+// (err: the single-pass selects' sticky look-back error word, or null)
+constexpr int kPubTot = 1, kPubPick = 5, kPubErr = 7, kPubSmall = 8, kPubRk = 32;  // + nrk: counts
 void launch_publish(const int32_t* totals, int ntot, const float4* small, int nsmall,
                     const int32_t* rk, int nrk, const int32_t* pick, int npick,
-                    const int32_t* res, int nres, int32_t* pub, int32_t seq, hipStream_t s);
+                    const int32_t* res, int nres, const int32_t* err, int32_t* pub, int32_t seq,
+                    hipStream_t s);
 // speculative computeModel decision for probability 1 over one batch (k_pick_p1): out[0] best
 // batch index (-1 none), out[1] loop ended inside the batch; winner copied to best / best_smp
 void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
@@ -123,7 +104,10 @@ void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleR
 struct Sel1State {
   uint64_t* status = nullptr;
   uint32_t epoch = 0;
+  int32_t* err = nullptr;  // sticky: != 0 once a tile's look-back failed (host checks and clears)
 };
+// tiles (status words) of a single-pass select over n points
+int sel1_tiles(int64_t n);
 // the Morton copy's select: survivors -> dst, inliers stamped tag[pristine index] = tagv;
 // totals[0] = inliers, totals[1] = n_list - inliers, totals[4] = Morton survivors
 void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
@@ -139,10 +123,10 @@ void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_
 void launch_list_materialize(PointsView pristine, int64_t n, const PointsOut& io, hipStream_t s);
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,
                        HypRec* hyps, int32_t* good, hipStream_t s);
-// counts[D] = #{i < n : |plane_h . (x_i, y_i, z_i, 1)| < cthr}, PCL (Eigen SSE) op order.
-// counts must be zeroed by the caller (memset on the same stream).
+// counts[D] = #{i < n : |plane_h . (x_i, y_i, z_i, 1)| < cthr}, PCL (Eigen SSE) op order, with
+// kernel kScoreExact or kScoreBf16.  counts must be zeroed by the caller (same stream).
 void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t* counts,
-                  int variant, int num_cus, hipStream_t s);
+                  int kernel, int num_cus, hipStream_t s);
 // B columns (bf16 split plane coefficients) and band widths of D plane hypotheses for the bf16
 // matrix-core scoring kernels, written into the hyps scratch tail; returns pointers to them
 void launch_prep_bf16(const HypRec* hyps, int D, const uint4** bcol, const float** band,

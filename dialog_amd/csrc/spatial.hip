@@ -60,75 +60,11 @@ __global__ void k_gather_order(PointsView src, const int32_t* __restrict__ order
   dst.gid[i] = k;  // the Morton copy's "gid" is the pristine index (lean-list rounds stamp it)
 }
 
-// one wave per super-tile: the two half-waves take one tile each per step.  Tile sphere: centre
-// = midpoint of the tile's bounding box, radius = max |p - c| (float) inflated by 2^-18 (covers
-// the few roundings of the distance evaluation).  Super sphere: centre = midpoint of the super
-// box, radius = max over its tiles of |c_t - C| + r_t, inflated the same way.
-constexpr int kSbBS = 256;
-__global__ __launch_bounds__(kSbBS) void k_sphere_bounds(const float* __restrict__ X,
-                                                         const float* __restrict__ Y,
-                                                         const float* __restrict__ Z, int64_t n_arg,
-                                                         const int32_t* __restrict__ n_dev,
-                                                         float4* __restrict__ tiles,
-                                                         float4* __restrict__ supers) {
-  __shared__ float4 s_t[kSbBS / kWave][kSuperTiles];
-  const int64_t n = n_dev ? (int64_t)*n_dev : n_arg;
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  const int r32 = lane & 31, hh = lane >> 5;
-  const int64_t s = (int64_t)blockIdx.x * (kSbBS / kWave) + wv;
-  if (s * kSuperP >= n) return;
-  const int ntile = (int)std::min<int64_t>(kSuperTiles, (n - s * kSuperP + kTileP - 1) / kTileP);
-  float bx0 = INFINITY, by0 = INFINITY, bz0 = INFINITY;
-  float bx1 = -INFINITY, by1 = -INFINITY, bz1 = -INFINITY;
-  for (int tt = 0; tt < kSuperTiles; tt += 2) {
-    const int tl = tt + hh;
-    const int64_t t = s * kSuperTiles + tl;
-    const int64_t p = t * kTileP + r32;
-    const bool ok = tl < ntile && p < n;
-    float x = 0.f, y = 0.f, z = 0.f;
-    if (ok) { x = X[p]; y = Y[p]; z = Z[p]; }
-    float x0 = ok ? x : INFINITY, y0 = ok ? y : INFINITY, z0 = ok ? z : INFINITY;
-    float x1 = ok ? x : -INFINITY, y1 = ok ? y : -INFINITY, z1 = ok ? z : -INFINITY;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      x0 = fminf(x0, __shfl_xor(x0, o)); y0 = fminf(y0, __shfl_xor(y0, o)); z0 = fminf(z0, __shfl_xor(z0, o));
-      x1 = fmaxf(x1, __shfl_xor(x1, o)); y1 = fmaxf(y1, __shfl_xor(y1, o)); z1 = fmaxf(z1, __shfl_xor(z1, o));
-    }
-    const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), cz = 0.5f * (z0 + z1);
-    float d = 0.0f;
-    if (ok) {
-      const float dx = x - cx, dy = y - cy, dz = z - cz;
-      d = sqrtf(dx * dx + dy * dy + dz * dz);
-    }
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) d = fmaxf(d, __shfl_xor(d, o));
-    const float r = d * (1.0f + 0x1p-18f) + 1e-30f;
-    if (r32 == 0 && tl < ntile) {
-      const float4 ts = make_float4(cx, cy, cz, r);
-      tiles[t] = ts;
-      s_t[wv][tl] = ts;
-    }
-    // super box over both halves
-    bx0 = fminf(bx0, fminf(x0, __shfl_xor(x0, 32))); by0 = fminf(by0, fminf(y0, __shfl_xor(y0, 32)));
-    bz0 = fminf(bz0, fminf(z0, __shfl_xor(z0, 32)));
-    bx1 = fmaxf(bx1, fmaxf(x1, __shfl_xor(x1, 32))); by1 = fmaxf(by1, fmaxf(y1, __shfl_xor(y1, 32)));
-    bz1 = fmaxf(bz1, fmaxf(z1, __shfl_xor(z1, 32)));
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const float Cx = 0.5f * (bx0 + bx1), Cy = 0.5f * (by0 + by1), Cz = 0.5f * (bz0 + bz1);
-  float R = 0.0f;
-  if (lane < ntile) {
-    const float4 ts = s_t[wv][lane];
-    const float dx = ts.x - Cx, dy = ts.y - Cy, dz = ts.z - Cz;
-    R = sqrtf(dx * dx + dy * dy + dz * dz) + ts.w;
-  }
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) R = fmaxf(R, __shfl_xor(R, o));
-  if (lane == 0) supers[s] = make_float4(Cx, Cy, Cz, R * (1.0f + 0x1p-18f) + 1e-30f);
-}
-
-// k_sphere_bounds2: the same spheres with one lane per tile.  A wave stages 64 tiles (2048
+// Tile sphere: centre = midpoint of the tile's bounding box, radius = max |p - c| (float)
+// inflated by 2^-18 (covers the few roundings of the distance evaluation).  Super sphere: centre
+// = midpoint of the super box, radius = max over its tiles of |c_t - C| + r_t, inflated the same
+// way.
+// k_sphere_bounds2: one lane per tile.  A wave stages 64 tiles (2048
 // points, two super-tiles) in LDS with coalesced loads (padded rows: lane l reads row l without
 // bank conflicts), each lane reduces its tile's box and radius, then the 32 lanes of a super-tile
 // combine their spheres.  ~4x less VALU work than a half-wave per tile.
@@ -206,13 +142,11 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
 //   k_prune_supers : every plane against every super-tile sphere (planes in LDS, 1024 threads =
 //                    4 planes per thread per super-tile); the planes that may hold an inlier go
 //                    to the super-tile's list lp[s * D ...], their number to lp_n[s];
-//   k_score_tiles  : waves walk the tiles independently (blocks of 4 consecutive tiles dealt
-//                    round-robin over all waves: no workgroup barrier inside the loop); per tile
-//                    the planes of its super-tile's list are tested against the tile sphere (64
-//                    per step, lanes = planes), the near ones appended to the wave's ring, and
-//                    every 32 queued planes (and the remainder) scored against the tile's 32
-//                    points as one 32 x 32 bf16 matrix-core block with exact band re-decision;
-//                    per-plane counts in LDS, flushed once per workgroup.
+//   k_score_tiles_rl : per tile, the planes of its super-tile's list are tested against the tile
+//                    sphere, the near ones appended to the wave's ring, and every 32 queued
+//                    planes (and the remainder) scored against the tile's 32 points as one
+//                    32 x 32 bf16 matrix-core block with exact band re-decision; per-plane
+//                    counts in LDS, flushed once per workgroup.
 // A (sphere, plane) pair is ruled out only when fl(|h|) > (margin + r)(1 + 2^-20), i.e. the
 // exact distance of the plane to the sphere centre exceeds cthr + r + 2 e_max: no point of the
 // sphere can then pass PCL's test (spatial.hpp).
@@ -223,8 +157,6 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
 // and the re-decision band is ~15x narrower than k_score_bf16's 64 u S.
 constexpr int kPrBS = 1024;
 constexpr int kPrWaves = kPrBS / kWave;
-constexpr int kPrRing = 128;
-constexpr int kPrChunk = 4;  // consecutive tiles per work item of k_score_tiles
 
 __device__ __forceinline__ float prune_lim(float margin, float r) {
   return (margin + r) * (1.0f + 0x1p-20f);
@@ -271,200 +203,9 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
   }
 }
 
-__device__ __forceinline__ void score_tiles_body(
-    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
-    const int32_t* __restrict__ lp_n, const HypRec* __restrict__ hyps,
-    const uint4* __restrict__ bcol, const float* __restrict__ band, int D, float cthr,
-    float margin, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats) {
-  __shared__ float4 s_cf[kMaxHypPerLaunch];
-  // per-plane counts, two 16-bit halves per word (the grid is sized so that no workgroup sees
-  // more than 65535 points, launch_score_pruned): 76 KB of LDS in all -> two workgroups per CU
-  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];
-  __shared__ uint16_t s_ring[kPrWaves][kPrRing];
-  __shared__ unsigned long long s_st[6];
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  const int r32 = lane & 31, hh = lane >> 5;
-  for (int j = threadIdx.x; j < D; j += kPrBS) {
-    const HypRec h = hyps[j];
-    s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
-  }
-  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += kPrBS) s_cnt[j] = 0u;
-  if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
-  __syncthreads();
-  const f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int ntiles = (n + kTileP - 1) / kTileP;
-  const int nitems = (ntiles + kPrChunk - 1) / kPrChunk;
-  const int gw = blockIdx.x * kPrWaves + wv, nw = gridDim.x * kPrWaves;
-  for (int it = gw; it < nitems; it += nw) {
-    const int t_end = min(ntiles, (it + 1) * kPrChunk);
-    for (int t = it * kPrChunk; t < t_end; ++t) {
-      const int sidx = t / kSuperTiles;
-      const int nlp = lp_n[sidx];
-      const uint16_t* lps = lp + (int64_t)sidx * ls;
-      const float4 tb = tiles[t];
-      const float tlim = prune_lim(margin, tb.w);
-      const int64_t p0 = (int64_t)t * kTileP;
-      if (stats && lane == 0) { atomicAdd(&s_st[2], 1ull); atomicAdd(&s_st[1], (unsigned long long)nlp); }
-      // the tile's points (A operand, relative to the tile centre) -- loaded up front
-      const bool valid = p0 + r32 < n;
-      float x = 0.f, y = 0.f, z = 0.f;
-      if (valid) { x = X[p0 + r32]; y = Y[p0 + r32]; z = Z[p0 + r32]; }
-      bool a_ready = false, bad = false;
-      u32x4 a1 = {0u, 0u, 0u, 0u}, a2 = {0u, 0u, 0u, 0u};
-      int nq = 0, head = 0;
-      // pending group: its loads are issued when it fills and it is scored at the next event,
-      // so the B-column / LDS latency overlaps the tile tests in between
-      bool pend = false;
-      int pj = 0;
-      bool pcol = false;
-      uint4 pq = make_uint4(0u, 0u, 0u, 0u), pq2 = pq;
-      float pband = 0.0f;
-      float4 pcf = make_float4(0.f, 0.f, 0.f, 0.f);
-      auto issue = [&](int m) {
-        pcol = r32 < m;
-        pj = pcol ? (int)s_ring[wv][(head + r32) & (kPrRing - 1)] : 0;
-        pcf = s_cf[pj];
-        if (pcol) {
-          pq = bcol[4 * pj + hh];
-          pq2 = bcol[4 * pj + 2 + hh];
-          pband = band[pj];
-        }
-        pend = true;
-        if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
-      };
-      auto compute = [&]() {
-        pend = false;
-        if (!a_ready) {
-          a_ready = true;
-          bad = ballot(!valid || !(isfinite(x) && isfinite(y) && isfinite(z))) != 0;
-          // coordinates relative to the tile centre (|p - c| <= r)
-          const float dx = valid ? x - tb.x : 0.f, dy = valid ? y - tb.y : 0.f;
-          const float dz = valid ? z - tb.z : 0.f;
-          const Split3 sx = split3(dx), sy = split3(dy), sz = split3(dz);
-          if (hh == 0) {
-            a1 = u32x4{pk(sx.p1, sx.p1), pk(sx.p2, sx.p1), pk(sx.p3, sx.p2), pk(sy.p1, sy.p1)};
-            a2 = u32x4{pk(sz.p3, sz.p2), pk(kBf16One, kBf16One), pk(kBf16One, 0u), 0u};
-          } else {
-            a1 = u32x4{pk(sy.p2, sy.p1), pk(sy.p3, sy.p2), pk(sz.p1, sz.p1), pk(sz.p2, sz.p1)};
-            a2 = u32x4{0u, 0u, 0u, 0u};
-          }
-        }
-        const int j = pj;
-        const bool col = pcol;
-        const float4 cf = pcf;
-        u32x4 b1 = {0u, 0u, 0u, 0u}, b2 = {0u, 0u, 0u, 0u};
-        float w = 0.0f;
-        if (col) {
-          b1 = u32x4{pq.x, pq.y, pq.z, pq.w};
-          b2 = u32x4{pq2.x, pq2.y, pq2.z, pq2.w};
-          // the plane's offset from the tile centre h = n.c + d: double (products exact), rounded
-          // once to float and split exactly into the d slots of the B column (k 18..20)
-          const double hd = __builtin_fma((double)cf.x, (double)tb.x,
-                                          __builtin_fma((double)cf.y, (double)tb.y,
-                                                        __builtin_fma((double)cf.z, (double)tb.z, (double)cf.w)));
-          const float hf = (float)hd;
-          if (hh == 0) {
-            const Split3 sh = split3(hf);
-            b2.y = pk(sh.p1, sh.p2);
-            b2.z = pk(sh.p3, 0u);
-          }
-          // |D - pcl_dot| <= 4.1 u S (PCL's rounding; band[j] >= 15.8 x that, k_prep_bf16)
-          //                + 44 u (|n|_1 r + |h|) (centring, dropped products, <= 20 roundings
-          //                  even if truncated) -- the constants carry >= 2 % slack
-          w = __builtin_fmaf(0.065f, pband, 3.0e-6f * __builtin_fmaf(1.8f, tb.w, fabsf(hf))) + 1e-9f;
-        } else if (hh == 0) {
-          b2 = u32x4{0u, pk(0x4000u, 0u), 0u, 0u};  // not a plane: D = 2, never counted
-        }
-        f32x16 Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a1), as_bf16x8(b1), zero, 0, 0, 0);
-        Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a2), as_bf16x8(b2), Dv, 0, 0, 0);
-        uint32_t acc = 0;
-        float mn = INFINITY;
-#pragma unroll
-        for (int i = 0; i < 16; i += 4) {
-          const float r0 = fabsf(Dv[i]) - cthr, r1 = fabsf(Dv[i + 1]) - cthr;
-          const float r2 = fabsf(Dv[i + 2]) - cthr, r3 = fabsf(Dv[i + 3]) - cthr;
-          acc = count4(r0, r1, r2, r3, acc);
-          mn = min3_abs(mn, r0, r1);
-          mn = min3_abs(mn, r2, r3);
-        }
-        const bool need = bad || mn <= w;
-        if (ballot(need)) {  // rare: re-decide the band elements in PCL op order
-          if (stats && lane == 0) atomicAdd(&s_st[5], 1ull);
-#pragma unroll 1
-          for (int i = 0; i < 16; ++i) {
-            const float ri = fabsf(Dv[i]) - cthr;
-            const bool inb = need && (bad || fabsf(ri) <= w);
-            if (ballot(inb)) {
-              const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-              const float px = __shfl(x, row), py = __shfl(y, row), pz = __shfl(z, row);
-              const bool ex = p0 + row < n && fabsf(pcl_dot(cf.x, cf.y, cf.z, cf.w, px, py, pz)) < cthr;
-              const uint32_t approx = __float_as_uint(ri) >> 31;
-              if (inb) acc = acc + (ex ? 255u : 0u) - 255u * approx;
-            }
-          }
-        }
-        uint32_t c = acc / 255u;
-        c += __shfl_xor(c, 32);
-        if (hh == 0 && col && c) atomicAdd(&s_cnt[j >> 1], c << (16 * (j & 1)));
-      };
-      int jn = lane < nlp ? (int)lps[lane] : 0;  // the list is read one chunk ahead
-      for (int c0 = 0; c0 < nlp; c0 += kWave) {
-        const int k = c0 + lane;
-        const int j = jn;
-        jn = k + kWave < nlp ? (int)lps[k + kWave] : 0;
-        bool near = false;
-        if (k < nlp) {
-          const float4 cf = s_cf[j];
-          const float h = __builtin_fmaf(cf.x, tb.x, __builtin_fmaf(cf.y, tb.y, __builtin_fmaf(cf.z, tb.z, cf.w)));
-          near = fabsf(h) <= tlim;
-        }
-        const uint64_t m = ballot(near);
-        if (near) s_ring[wv][(nq + lanes_below(m)) & (kPrRing - 1)] = (uint16_t)j;
-        nq += (int)__popcll(m);
-        __builtin_amdgcn_wave_barrier();
-        while (nq - head >= 32) {
-          if (pend) compute();
-          issue(32);
-          head += 32;
-        }
-      }
-      if (pend) compute();
-      if (nq > head) {
-        issue(nq - head);
-        compute();
-      }
-    }
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < D; j += kPrBS) {
-    const int c = (int)((s_cnt[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
-    if (c) atomicAdd(&counts[j], c);
-  }
-  if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
-}
-
-// two occupancy points of the same body: 4 waves/SIMD (one workgroup per CU, no spills) and
-// 8 waves/SIMD (two workgroups per CU, VGPRs capped at 64)
-#define DLG_SCORE_TILES_ARGS                                                                    \
-  const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n, \
-      const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,                \
-      const int32_t* __restrict__ lp_n, const HypRec* __restrict__ hyps,                        \
-      const uint4* __restrict__ bcol, const float* __restrict__ band, int D, float cthr,        \
-      float margin, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats
-__global__ __launch_bounds__(kPrBS) void k_score_tiles(DLG_SCORE_TILES_ARGS) {
-  score_tiles_body(X, Y, Z, n, tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
-}
-__global__ __launch_bounds__(kPrBS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_score_tiles_o8(
-    DLG_SCORE_TILES_ARGS) {
-  score_tiles_body(X, Y, Z, n, tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
-}
-#undef DLG_SCORE_TILES_ARGS
-
-
 // ---------------------------------------------------------------------------------------------
-// k_score_tiles_rl: the same (tile, plane) decisions as k_score_tiles with no global load on the
-// group path.  A work item (4 consecutive tiles of one super-tile) loads its super-tile's plane
+// k_score_tiles_rl: no global load on the group path.  A work item (2 consecutive tiles of one
+// super-tile) loads its super-tile's plane
 // list once into registers (up to kListCap entries, two uint16 per dword, 8 dwords per lane);
 // per tile the list is tested against the tile sphere from registers + LDS (packed FMAs, two
 // entries per lane), near planes go to the wave's LDS ring, and every 32 queued planes are
@@ -479,13 +220,11 @@ constexpr int kListRegs = 8;
 constexpr int kListCap = kListRegs * 2 * kWave;  // 1024 entries
 constexpr int kRing2 = 512;                       // >= 31 queued + 256 appended per list step
 
-// EXP: timing experiments only (1: groups not scored, 2: no band re-decision, 3: no list
-// tests: the item/tile skeleton) -- counts are then wrong
 // NPM: SACMODEL_NORMAL_PLANE (PCL's exact prefilter b = (1 - w) d_euclid < thr as the per-point
 // float compare d_euclid < lim, k_score_np; passing pairs queued per wave and decided with full
 // lanes in double as in k_score_np), the spheres ruled out with the margin of the cloud's
 // largest lim; plane model otherwise.
-template <int EXP, int BS, bool NPM>
+template <int BS, bool NPM>
 __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
@@ -494,7 +233,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     float az, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats,
     const float4* __restrict__ NRM, double lambda, double thr) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
-  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves (see k_score_tiles)
+  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves: <= 65535 points per workgroup
   __shared__ uint16_t s_ring[(BS / kWave)][kRing2];
   __shared__ unsigned long long s_st[6];
   __shared__ int s_taken;  // items this workgroup has claimed (<= blk_cap: 16-bit counters)
@@ -637,11 +376,6 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
         if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
         const bool col = r32 < m;
         const int j = col ? (int)ring[(head + r32) & (kRing2 - 1)] : 0;
-        if constexpr (EXP == 1) {
-          if (hh == 0 && col) atomicAdd(&s_cnt[j >> 1], 1u << (16 * (j & 1)));
-          head += m;
-          return;
-        }
         if constexpr (NPM) {
           // lane: point r32 of the tile, planes hh * 16 .. hh * 16 + 15 of the group
           (void)j;
@@ -688,7 +422,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
             S = __builtin_fmaf(fabsf(cf.x), ax, __builtin_fmaf(fabsf(cf.y), ay,
                                __builtin_fmaf(fabsf(cf.z), az, fabsf(cf.w))));
           }
-          // |D - pcl_dot| <= 4.1 u S + 44 u (|n|_1 r + |h|) (see k_score_tiles); S in float
+          // |D - pcl_dot| <= 4.1 u S + 44 u (|n|_1 r + |h|) (PCL rounding + centring); S in float
           // (<= 4 roundings, possibly rounded up to bf16) times 4.25 u covers the 4.21 u S there
           w = __builtin_fmaf(0x1.1p-22f, S, 3.0e-6f * __builtin_fmaf(1.8f, tb.w, fabsf(hf))) + 1e-8f;
           if (!(w <= INFINITY)) w = INFINITY;  // NaN (0 x inf): re-decide everything
@@ -707,7 +441,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
           mn = min3_abs(mn, r0, r1);
           mn = min3_abs(mn, r2, r3);
         }
-        const bool need = EXP != 2 && (bad || mn <= w);
+        const bool need = bad || mn <= w;
         if (ballot(need)) {  // rare: re-decide the band elements in PCL op order
           if (stats && lane == 0) atomicAdd(&s_st[5], 1ull);
           uint32_t bm = 0u, am = 0u;  // per lane: band elements, and their approximate verdicts
@@ -734,7 +468,6 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
         if (hh == 0 && col && c) atomicAdd(&s_cnt[j >> 1], c << (16 * (j & 1)));
         head += m;
       };
-      // tile-sphere test of two list entries per lane (entries e0 = 2 (lane + 64 k), e0 + 1)
       // tile-sphere test of two list entries per lane (entries e0 = 2 (lane + 64 k), e0 + 1;
       // entries past the list end were zeroed at load: plane 0, masked here), packed FMAs
       const f32x2 tbx = {tb.x, tb.x}, tby = {tb.y, tb.y}, tbz = {tb.z, tb.z};
@@ -770,7 +503,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
 #pragma unroll
         for (int k = 0; k < kListRegs; ++k) R[k] = L[k];
 #pragma unroll 1
-        for (int k = 0; EXP != 3 && lb + k * 2 * kWave < le; k += 2) {
+        for (int k = 0; lb + k * 2 * kWave < le; k += 2) {
           test4(R[0], R[1], lb + 2 * (lane + k * kWave));
 #pragma unroll
           for (int q = 0; q + 2 < kListRegs; ++q) R[q] = R[q + 2];
@@ -857,18 +590,7 @@ void launch_gather_order(PointsView src, const int32_t* order, int64_t n, Points
 void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_t n,
                           const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s) {
   if (n <= 0) return;
-  static const int v = [] {
-    const char* e = std::getenv("DLG_SPHERE_KERNEL");
-    return e ? std::atoi(e) : 2;
-  }();
-  if (v == 2) {
-    hipLaunchKernelGGL(k_sphere_bounds2, dim3((unsigned)((n + kSb2Pts - 1) / kSb2Pts)), dim3(64), 0,
-                       s, x, y, z, n, n_dev, tiles, supers);
-    return;
-  }
-  const int64_t ns = sp_supers(n);
-  const int wpb = kSbBS / kWave;
-  hipLaunchKernelGGL(k_sphere_bounds, dim3((unsigned)((ns + wpb - 1) / wpb)), dim3(kSbBS), 0, s,
+  hipLaunchKernelGGL(k_sphere_bounds2, dim3((unsigned)((n + kSb2Pts - 1) / kSb2Pts)), dim3(64), 0, s,
                      x, y, z, n, n_dev, tiles, supers);
 }
 
@@ -912,18 +634,9 @@ float np_lim_max(double w, double thr) {  // np_de_limit (np_dev.hpp) on the hos
   return x;
 }
 
-int prune_kernel() {
-  static const int k = [] {
-    const char* e = std::getenv("DLG_PRUNE_KERNEL");
-    return e ? std::atoi(e) : 2;
-  }();
-  return k;
-}
-
-void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
-                         const float* band, int D, float cthr, float margin, const float amax[3],
-                         int32_t* counts, uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
-                         unsigned long long* stats, const PrunedNp* np) {
+void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float cthr, float margin,
+                         const float amax[3], int32_t* counts, uint16_t* lp, int32_t* lp_n,
+                         int num_cus, hipStream_t s, unsigned long long* stats, const PrunedNp* np) {
   if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) return;
   const int64_t ns = sp_supers(v.n);
   const int ls = prune_list_stride(D);
@@ -931,58 +644,20 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* 
   int32_t* work = lp_n + ns;  // (lp_n holds sp_supers(n) + 1 entries)
   hipLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, v.supers, (int)ns, hyps, D, ls,
                      margin, lp, lp_n, work);
-  // one workgroup per CU (LDS + VGPRs), and enough of them that no workgroup takes more than 31
-  // items per wave (31 x 16 waves x 4 tiles x 32 points = 63488 <= 65535: 16-bit LDS counters)
-  const int64_t items = (sp_tiles(v.n) + kPrChunk - 1) / kPrChunk;
-  constexpr int64_t kMaxItemsPerWave = 65535 / (kPrWaves * kPrChunk * kTileP);
-  static_assert(kMaxItemsPerWave >= 1, "16-bit counters");
-  const int kern = np ? 2 : prune_kernel();
-  static const int occ = [] {
-    const char* e = std::getenv("DLG_PRUNE_OCC");
-    return e ? std::atoi(e) : 4;
-  }();
-  const int per_cu = (kern == 1 && occ == 8) ? 2 : 1;
-  const int64_t g_fill = std::min<int64_t>((int64_t)per_cu * num_cus, (items + kPrWaves - 1) / kPrWaves);
-  const int64_t g_cnt = (items + kPrWaves * kMaxItemsPerWave - 1) / (kPrWaves * kMaxItemsPerWave);
-  const unsigned gb = (unsigned)std::max<int64_t>(1, std::max(g_fill, g_cnt));
-  if (kern == 2) {
-    static const int exp = [] {
-      const char* e = std::getenv("DLG_PRUNE_EXP");  // timing experiments only (wrong counts)
-      return e ? std::atoi(e) : 0;
-    }();
-    static const int bpc = [] {  // workgroups per CU: 1 (1024 threads) or 2/4 (512 threads)
-      const char* e = std::getenv("DLG_PRUNE_BPC");
-      const int b = e ? std::atoi(e) : 1;
-      return (b == 2 || b == 4) ? b : 1;
-    }();
-    const bool small = bpc > 1 && !np;
-    auto* kfn = np ? k_score_tiles_rl<0, 1024, true>
-              : small ? (exp == 1 ? k_score_tiles_rl<1, 512, false> : exp == 2 ? k_score_tiles_rl<2, 512, false> : k_score_tiles_rl<0, 512, false>)
-                      : (exp == 1 ? k_score_tiles_rl<1, 1024, false> : exp == 2 ? k_score_tiles_rl<2, 1024, false>
-                         : exp == 3 ? k_score_tiles_rl<3, 1024, false> : k_score_tiles_rl<0, 1024, false>);
-    const int bs = small ? 512 : 1024;
-    // dynamic item claims within a workgroup; workgroups capped at blk_cap items (16-bit
-    // counters), and enough of them that the caps cover every item
-    static const int chunk = [] {  // tiles per work item (1, 2, 4, 8, 16 or 32)
-      const char* e = std::getenv("DLG_PRUNE_CHUNK");
-      const int c = e ? std::atoi(e) : 2;
-      return (c >= 1 && c <= kSuperTiles && kSuperTiles % c == 0) ? c : 2;
-    }();
-    const int64_t items_rl = (sp_tiles(v.n) + chunk - 1) / chunk;
-    const int blk_cap = 65535 / (chunk * kTileP);
-    const int64_t g_rl = std::max<int64_t>(
-        1, std::max<int64_t>(std::min<int64_t>((int64_t)bpc * num_cus, (items_rl + bs / kWave - 1) / (bs / kWave)),
-                             (items_rl + blk_cap - 1) / blk_cap));
-    hipLaunchKernelGGL(kfn, dim3((unsigned)g_rl), dim3(bs), 0, s, v.x, v.y, v.z, (int)v.n,
-                       v.tiles, lp, ls, lp_n, work, blk_cap, chunk, hyps, D, cthr, margin, amax[0],
-                       amax[1], amax[2], counts, stats, np ? np->nrm : nullptr,
-                       np ? np->lambda : 0.0, np ? np->thr : 0.0);
-  } else if (occ == 8) {
-    hipLaunchKernelGGL(k_score_tiles_o8, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
-                       v.tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
-  } else {
-    hipLaunchKernelGGL(k_score_tiles, dim3(gb), dim3(kPrBS), 0, s, v.x, v.y, v.z, (int)v.n,
-                       v.tiles, lp, ls, lp_n, hyps, bcol, band, D, cthr, margin, counts, stats);
-  }
+  // one 1024-thread workgroup per CU (LDS + VGPRs); its waves claim 2-tile items dynamically,
+  // each workgroup capped at blk_cap items (16-bit LDS counters: <= 65535 points per
+  // workgroup), and enough workgroups that the caps cover every item
+  constexpr int kBS = 1024, kChunkTiles = 2;
+  static_assert(kSuperTiles % kChunkTiles == 0, "an item stays inside one super-tile");
+  const int64_t items = (sp_tiles(v.n) + kChunkTiles - 1) / kChunkTiles;
+  const int blk_cap = 65535 / (kChunkTiles * kTileP);
+  const int64_t g = std::max<int64_t>(
+      1, std::max<int64_t>(std::min<int64_t>(num_cus, (items + kBS / kWave - 1) / (kBS / kWave)),
+                           (items + blk_cap - 1) / blk_cap));
+  auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(kBS), 0, s, v.x, v.y, v.z, (int)v.n, v.tiles, lp,
+                     ls, lp_n, work, blk_cap, kChunkTiles, hyps, D, cthr, margin, amax[0], amax[1],
+                     amax[2], counts, stats, np ? np->nrm : nullptr, np ? np->lambda : 0.0,
+                     np ? np->thr : 0.0);
 }
 }  // namespace dlg

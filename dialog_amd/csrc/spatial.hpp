@@ -57,24 +57,21 @@ void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_
                           const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s);
 // margin = smallest float >= (cthr + 2 e_max)(1 + 2^-19), e_max = 64 u 2.0001 (ax + ay + az)
 float prune_margin(float cthr, const float amax[3]);
-// pruned countWithinDistance of D plane hypotheses over the spatial points.  hyps / bcol / band
-// as prepared for k_score_bf16 (launch_prep_bf16); counts[D] zeroed by the caller; lp / lp_n:
-// scratch of sp_supers(n) * prune_list_stride(D) uint16 and sp_supers(n) int32 (per super-tile plane lists).
+// pruned countWithinDistance of D plane hypotheses over the spatial points (k_prune_supers +
+// k_score_tiles_rl); counts[D] zeroed by the caller; lp / lp_n: scratch of sp_supers(n) *
+// prune_list_stride(D) uint16 and sp_supers(n) + 1 int32 (per super-tile plane lists).
+// amax: the cloud's per-axis max |coordinate| (the scoring band's S bound).
 // list stride per super-tile (D rounded up to 64 entries: dword-aligned entry pairs)
 inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
-// which pruned scoring kernel runs (DLG_PRUNE_KERNEL); only kernel 1 reads bcol / band
-int prune_kernel();
-// amax: the cloud's per-axis max |coordinate| (the scoring band's S bound).  DLG_PRUNE_KERNEL=1
-// selects the first version (k_score_tiles: global B columns, list read per tile), default 2.
 // SACMODEL_NORMAL_PLANE scoring over the spatial copy: its (normalised normal, curvature) per
 // point, and the model's lambda / threshold; margin then comes from prune_margin(lim_max, amax)
 struct PrunedNp {
   const float4* nrm;
   double lambda, thr;
 };
-void launch_score_pruned(const SpatialView& v, const HypRec* hyps, const uint4* bcol,
-                         const float* band, int D, float cthr, float margin, const float amax[3],
-                         int32_t* counts, uint16_t* lp, int32_t* lp_n, int num_cus, hipStream_t s,
+void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float cthr, float margin,
+                         const float amax[3], int32_t* counts, uint16_t* lp, int32_t* lp_n,
+                         int num_cus, hipStream_t s,
                          unsigned long long* stats = nullptr,  // [6] counters (A/B tool)
                          const PrunedNp* np = nullptr);
 // the NORMAL_PLANE prefilter limit of the largest w (host restatement of np_de_limit): every

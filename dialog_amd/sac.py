@@ -113,6 +113,22 @@ class Context:
     def check(self, status):
         _lib.check(status, self.h)
 
+    def set_option(self, option: int, value: int):
+        """dlg_ctx_set_option: choose among equivalent device paths (identical results)."""
+        self.check(self._L.dlg_ctx_set_option(self.h, int(option), int(value)))
+
+    def get_option(self, option: int) -> int:
+        v = C.c_int64()
+        self.check(self._L.dlg_ctx_get_option(self.h, int(option), C.byref(v)))
+        return v.value
+
+    def prune_stats(self, reset: bool = False) -> dict:
+        """The pruned scoring kernel's work counters (needs DLG_OPT_PRUNE_STATS = 1)."""
+        a = (C.c_uint64 * 6)()
+        self.check(self._L.dlg_prune_stats(self.h, a, int(bool(reset))))
+        return {"list_entries": a[1], "tiles": a[2], "blocks": a[3], "pairs": a[4],
+                "redecided_blocks": a[5]}
+
     def set_profiling(self, on=True):
         self.check(self._L.dlg_set_profiling(self.h, int(bool(on))))
 
@@ -247,7 +263,7 @@ def extract_planes(cloud: Cloud, params, max_planes=20, min_inliers=0, capacity=
     k = npl.value
     stats = dict(rounds=xs.rounds, tests=xs.tests, tests_scored=xs.tests_scored,
                  score_launches=xs.score_launches, score_ms=xs.score_ms, select_ms=xs.select_ms,
-                 wall_ms=xs.wall_ms)
+                 wall_ms=xs.wall_ms, lean_rounds=xs.lean_rounds, spec_misses=xs.spec_misses)
     return dict(coeffs=coeffs[:k].copy(), offsets=offs[:k + 1].copy(),
                 inliers=inl[:offs[k]], n_planes=k, stats=stats)
 

@@ -99,6 +99,8 @@ typedef struct {
   double score_ms;             /* sum of scoring-kernel device time */
   double select_ms;            /* sum of select/compact/moments device time */
   double wall_ms;              /* host wall time of the call */
+  int lean_rounds;             /* rounds that took the single-pass (lean-list) select */
+  int spec_misses;             /* speculative device picks the host replay overturned */
 } dlg_extract_stats;
 
 void dlg_sac_params_default(dlg_sac_params* p);   /* PCL SACSegmentation defaults */
@@ -108,7 +110,8 @@ int dlg_abi_version(void);
 /* ---- contexts ------------------------------------------------------------------------------ */
 dlg_status dlg_ctx_create(dlg_ctx** out, int device);
 /* one process per GPU: rank/world over RCCL (xGMI).  unique_id: 128 bytes from dlg_get_unique_id
- * on rank 0, distributed out of band (e.g. torch.distributed gloo). */
+ * on rank 0, distributed out of band (e.g. torch.distributed gloo).  world 1 with a NULL id is a
+ * plain context; world 1 with an id runs a 1-rank RCCL communicator. */
 dlg_status dlg_get_unique_id(void* unique_id_128);
 dlg_status dlg_ctx_create_dist(dlg_ctx** out, int device, int rank, int world,
                                const void* unique_id_128);
@@ -132,7 +135,7 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cloud);
 dlg_status dlg_cloud_reset(dlg_cloud* cloud);
 /* Morton-ordered copy of the cloud's finite points + tile bounding spheres for the pruned
  * scoring kernel (same counts, fewer evaluated tests).  Built by dlg_cloud_upload for clouds of
- * >= 131072 points (environment DLG_PRUNE=0: never, =1: always); this forces it for any cloud
+ * >= 131072 points (context option DLG_OPT_PRUNE: 0 never, 1 always); this forces it for any cloud
  * (call right after upload or dlg_cloud_reset).  Kept in step by SACMODEL_PLANE extraction. */
 dlg_status dlg_cloud_build_spatial(dlg_ctx* ctx, dlg_cloud* cloud);
 dlg_status dlg_cloud_active(const dlg_cloud* cloud, int64_t* n_active_local);
@@ -302,11 +305,34 @@ dlg_status dlg_sac_control_result(const dlg_sac_control* ctl, dlg_sac_stats* st,
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);
 dlg_status dlg_synchronize(dlg_ctx* ctx);
 /* Scoring-kernel micro-benchmark (kernel A/B on the device): D random plane hypotheses through
- * the same gather/build path, `variant` (0 = exact PCL op order, 1 = FMA prefilter + exact band
- * recheck, ...) launched `reps` times on the cloud's active points; returns the mean device
- * time per launch and (optional) the counts of the last launch. */
-dlg_status dlg_score_benchmark(dlg_ctx* ctx, dlg_cloud* cloud, int D, int variant, int reps,
+ * the same gather/build path, `kernel` (DLG_SCORE_EXACT, DLG_SCORE_BF16 or DLG_SCORE_PRUNED, the
+ * last needing the cloud's Morton copy) launched `reps` times on the cloud's active points;
+ * returns the mean device time per launch and (optional) the counts of the last launch. */
+dlg_status dlg_score_benchmark(dlg_ctx* ctx, dlg_cloud* cloud, int D, int kernel, int reps,
                                double threshold, double* ms_per_launch, int32_t* counts_out);
+/* Execution-path options of a context.  Every setting gives identical results (planes, inliers,
+ * counts): they only choose among equivalent device paths, for tests and measurement.  There are
+ * no environment switches in the library. */
+enum {
+  DLG_OPT_PRUNE = 1,        /* Morton copy + pruned countWithinDistance: -1 (default) clouds of
+                               >= 131072 points, 0 never, 1 every cloud (applies at upload) */
+  DLG_OPT_LEAN_ROUNDS = 2,  /* 1 (default): single-pass selects driven by the Morton copy in
+                               fast-refit / no-optimise SACMODEL_PLANE extraction; 0: two-pass */
+  DLG_OPT_SPEC_PICK = 3,    /* 1 (default): device-side computeModel decision for probability-1
+                               rounds (host replay confirms it); 0: host decision only */
+  DLG_OPT_PRUNE_NP = 4,     /* 1 (default): pruned SACMODEL_NORMAL_PLANE scoring; 0: exhaustive */
+  DLG_OPT_SCORE_KERNEL = 5, /* exhaustive scorer (no Morton copy): DLG_SCORE_BF16 (default) or
+                               DLG_SCORE_EXACT */
+  DLG_OPT_PRUNE_STATS = 6   /* 1: count the pruned kernel's work (dlg_prune_stats); 0 (default) */
+};
+enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
+dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);
+dlg_status dlg_ctx_get_option(const dlg_ctx* ctx, int option, int64_t* value);
+/* the pruned scoring kernel's counters since DLG_OPT_PRUNE_STATS was set (or the last reset):
+ * [0] unused, [1] super-tile list entries tested against tile spheres, [2] tiles visited,
+ * [3] 32x32 blocks scored, [4] (tile, plane) pairs scored, [5] blocks with a band re-decision */
+dlg_status dlg_prune_stats(dlg_ctx* ctx, uint64_t out[6], int reset);
+
 /* max over ranks of a host double (bench timing) and a barrier; no-ops for world == 1 */
 dlg_status dlg_allreduce_max_f64(dlg_ctx* ctx, double* value);
 dlg_status dlg_barrier(dlg_ctx* ctx);

@@ -245,10 +245,10 @@ def test_cpp_shim_runs_on_gpu(tmp_path):
     assert post[0] + post[1] <= 64 * 64 + 500
 
 
-def test_rccl_one_rank_path(monkeypatch, gpu_ctx):
+def test_rccl_one_rank_path(gpu_ctx):
     """The RCCL communicator code (dlopen, ncclCommInitRank, in-place allreduce, allgather,
-    allreduce-max) on a real device with one rank: same planes as the plain context."""
-    monkeypatch.setenv("DLG_FORCE_RCCL", "1")
+    allreduce-max) on a real device with one rank (world 1 + a unique id): same planes as the
+    plain context."""
     p, _, _ = plane_cloud(30000, 4, seed=5)
     prm = D.make_params(0.02, max_iterations=255, probability=1.0)
     c0 = D.Cloud(gpu_ctx, p)

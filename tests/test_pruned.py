@@ -167,28 +167,35 @@ def test_pruned_counts_c3_full_size(gpu_ctx):
     cloud = D.Cloud(gpu_ctx, p)
     try:
         for thr in (0.02, 0.2):
-            ref = counts(gpu_ctx, cloud, 4096, 19, thr)
-            got = counts(gpu_ctx, cloud, 4096, 20, thr)
+            ref = counts(gpu_ctx, cloud, 4096, 1, thr)
+            got = counts(gpu_ctx, cloud, 4096, 2, thr)
             assert ref.sum() > 0 and np.array_equal(got, ref), int((got != ref).sum())
     finally:
         cloud.close()
 
 
-def test_lean_list_continue_segment_and_normal_plane(gpu_ctx):
-    """Lean-list rounds (the Morton copy decides the inliers, the list keeps pristine indices):
-    extraction continued over several calls equals one call; a plain segment and a
-    SACMODEL_NORMAL_PLANE round afterwards read the materialised list; all against the oracle."""
+@pytest.mark.parametrize("optimize", [False, True])
+def test_lean_list_continue_segment_and_normal_plane(gpu_ctx, optimize):
+    """Lean-list rounds (the Morton copy decides the inliers, the list keeps pristine indices)
+    run whenever the refit stays on the device: optimize=False here (bit-exact against the
+    oracle's optimize-off extraction) -- optimize=True takes PCL's host refit and the two-pass
+    path, the control.  Extraction continued over several calls equals one call; a plain
+    segment and a SACMODEL_NORMAL_PLANE round afterwards read the materialised list; all
+    against the oracle."""
     p, _, _ = plane_cloud(40000, 6, seed=41)
     p[::17, 2] = np.nan
-    kw = dict(max_iterations=255, probability=1.0)
+    kw = dict(max_iterations=255, probability=1.0, optimize=optimize)
     prm = D.make_params(0.02, **kw)
     ref = O.extract_planes(p, 0.02, max_planes=5, min_inliers=50, **kw)
     cloud = D.Cloud(gpu_ctx, p)
     cloud.build_spatial()
     got = []
+    lean = 0
     for k in (2, 2, 1):  # 5 planes over three calls
         e = D.extract_planes(cloud, prm, max_planes=k, min_inliers=50)
         got.append(e["inliers"].copy())
+        lean += e["stats"]["lean_rounds"]
+    assert lean == (0 if optimize else 5)
     assert np.array_equal(np.concatenate(got), ref["inliers"])
     taken = np.concatenate(got)
     rem = np.setdiff1d(np.arange(p.shape[0]), taken).astype(np.int32)
@@ -203,27 +210,63 @@ def test_lean_list_continue_segment_and_normal_plane(gpu_ctx):
     e = D.extract_planes(cloud, prm, max_planes=2, min_inliers=50)
     assert np.array_equal(e["inliers"], ref["inliers"][:ref["offsets"][2]])
     npp = D.make_params(0.05, max_iterations=100, model=D.SACMODEL_NORMAL_PLANE,
-                        normal_distance_weight=0.1)
+                        normal_distance_weight=0.1, optimize=optimize)
     e2 = D.extract_planes(cloud, npp, max_planes=1, min_inliers=10)
+    assert e2["stats"]["lean_rounds"] == 0  # (NORMAL_PLANE rounds read the list's coordinates)
     rem2 = np.setdiff1d(np.arange(p.shape[0]), e["inliers"]).astype(np.int32)
     r2 = O.sac_segment(p, 0.05, indices=rem2, max_iterations=100, normals=nrm,
-                       normal_distance_weight=0.1)
+                       normal_distance_weight=0.1, optimize=optimize)
     assert np.array_equal(e2["inliers"][:e2["offsets"][1]], r2["inliers"])
     cloud.close()
 
 
-def test_lean_list_indexed_cloud(gpu_ctx):
+@pytest.mark.parametrize("optimize", [False, True])
+def test_lean_list_indexed_cloud(gpu_ctx, optimize):
     """setIndices clouds: the list's pristine indices differ from the point ids (and from list
-    order of the ids when the indices are unsorted)."""
+    order of the ids when the indices are unsorted); lean rounds with optimize=False."""
     p, _, _ = plane_cloud(50000, 5, seed=43)
     rng = np.random.default_rng(9)
     idx = rng.choice(p.shape[0], 30000, replace=False).astype(np.int32)  # unsorted
-    kw = dict(max_iterations=200, probability=1.0)
+    kw = dict(max_iterations=200, probability=1.0, optimize=optimize)
     cloud = D.Cloud(gpu_ctx, p, indices=idx)
     cloud.build_spatial()
     e = D.extract_planes(cloud, D.make_params(0.02, **kw), max_planes=4, min_inliers=50)
     ref = O.extract_planes(p[idx], 0.02, max_planes=4, min_inliers=50, **kw)
+    assert e["stats"]["lean_rounds"] == (0 if optimize else e["stats"]["rounds"])
     assert e["n_planes"] == ref["n_planes"] >= 3
     assert np.array_equal(e["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
     assert np.array_equal(e["inliers"], idx[ref["inliers"]])
     cloud.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_path_options_identical(gpu_ctx, seed):
+    """Every execution-path option (dlg_ctx_set_option) gives the same planes and inliers: lean
+    vs two-pass selects, speculative vs host pick, pruned vs exhaustive bf16 vs exact VALU
+    scoring -- each against the oracle's optimize-off extraction (the paths lean rounds take)."""
+    rng = np.random.default_rng(900 + seed)
+    p, _, _ = plane_cloud(int(rng.integers(20000, 80000)), int(rng.integers(2, 7)),
+                          seed=seed + 300, outlier_frac=float(rng.uniform(0.05, 0.4)))
+    if seed % 2:
+        p[::29, 1] = np.nan
+    kw = dict(max_iterations=int(rng.choice([63, 255, 1023])), probability=1.0, optimize=False)
+    ref = O.extract_planes(p, 0.02, max_planes=6, min_inliers=50, **kw)
+    prm = D.make_params(0.02, **kw)
+    combos = [dict(), {D.DLG_OPT_LEAN_ROUNDS: 0}, {D.DLG_OPT_SPEC_PICK: 0},
+              {D.DLG_OPT_PRUNE: 0}, {D.DLG_OPT_PRUNE: 0, D.DLG_OPT_SCORE_KERNEL: D.DLG_SCORE_EXACT}]
+    for opts in combos:
+        ctx = D.Context(0)
+        try:
+            ctx.set_option(D.DLG_OPT_PRUNE, 1)
+            for k, v in opts.items():
+                ctx.set_option(k, v)
+            cloud = D.Cloud(ctx, p)
+            e = D.extract_planes(cloud, prm, max_planes=6, min_inliers=50)
+            cloud.close()
+        finally:
+            ctx.close()
+        assert e["n_planes"] == ref["n_planes"], opts
+        assert np.array_equal(e["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32)), opts
+        assert np.array_equal(e["offsets"], ref["offsets"]) and np.array_equal(e["inliers"], ref["inliers"]), opts
+        lean_expected = opts.get(D.DLG_OPT_LEAN_ROUNDS, 1) and opts.get(D.DLG_OPT_PRUNE, 1)
+        assert (e["stats"]["lean_rounds"] > 0) == bool(lean_expected), (opts, e["stats"])

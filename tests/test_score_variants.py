@@ -12,7 +12,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-VARIANTS = (5, 18, 19, 20)  # exact (PCL op order), bf16 x 4 / x 8 tiles, pruned (spatial copy)
+VARIANTS = (0, 1, 2)  # DLG_SCORE_EXACT (PCL op order), DLG_SCORE_BF16 (matrix cores), DLG_SCORE_PRUNED
 
 
 def counts(ctx, cloud, D, v, thr):

@@ -35,24 +35,13 @@ for s in $STEPS; do
     benchtorch) run bench_torch 600 python3 bench.py --torch-dist --no-cpu-baseline --steps 2 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 3 ;;
     pmc)    run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 1 --warmup 0 ;;
-    pstats) DLG_PRUNE_STATS=1 VARIANTS="${VARIANTS:-20,19}" run pstats 300 python3 tools/score_ab.py 10000000 4096 2 ;;
-    abocc)  DLG_PRUNE_OCC=4 VARIANTS=20 run abocc4 300 python3 tools/score_ab.py 10000000 4096 5 && \
-            DLG_PRUNE_OCC=8 VARIANTS=20 run abocc8 300 python3 tools/score_ab.py 10000000 4096 5 ;;
+    pstats) PRUNE_STATS=1 KERNELS="${KERNELS:-2,1}" run pstats 300 python3 tools/score_ab.py 10000000 4096 2 ;;
     ptest)  run ptest 600 python3 -u -m pytest tests/test_pruned.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
-    abk)    DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=1 VARIANTS=20,19 run abk1 300 python3 tools/score_ab.py 10000000 4096 5 && \
-            DLG_PRUNE_STATS=1 DLG_PRUNE_KERNEL=2 VARIANTS=20,19 run abk2 300 python3 tools/score_ab.py 10000000 4096 5 ;;
-    ldspmc) VARIANTS=20 run ldspmc 300 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/ldspmc -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
-    expm)   for kk in 2; do for ee in 0 1 2 3; do
-              DLG_PRUNE_KERNEL=$kk DLG_PRUNE_EXP=$ee SCORE_AB_NOCHECK=1 VARIANTS=20 run expm_k${kk}_e${ee} 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3
-            done; done ;;
-    chunk)  for cc in 2 4 8; do DLG_PRUNE_CHUNK=$cc VARIANTS=20,19 run chunk_$cc 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
-    bpc)    for bb in 1 2 4; do DLG_PRUNE_BPC=$bb VARIANTS=20,19 run bpc_$bb 120 python3 tools/score_ab.py 10000000 4096 5 || exit 3; done ;;
+    ldspmc) KERNELS=2 run ldspmc 300 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/ldspmc -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
     ab)     run score_ab 600 python3 tools/score_ab.py ;;
     list)   run counters 120 rocprofv3 -L ;;
-    sqpmc)  VARIANTS="${VARIANTS:-0,2}" run sqpmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \
-            VARIANTS="${VARIANTS:-0,2}" run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM GRBM_COUNT --output-format csv -d gpurun_out/sqpmc2 -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
-    mpmc)   VARIANTS="${VARIANTS:-5,12}" run mpmc1 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_SALU SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/mpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \
-            VARIANTS="${VARIANTS:-5,12}" run mpmc2 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVES --output-format csv -d gpurun_out/mpmc2 -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
+    sqpmc)  KERNELS="${KERNELS:-0,2}" run sqpmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc1 -o run -- python3 tools/score_ab.py 10000000 4096 1 && \
+            KERNELS="${KERNELS:-0,2}" run sqpmc2 600 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM GRBM_COUNT --output-format csv -d gpurun_out/sqpmc2 -o run -- python3 tools/score_ab.py 10000000 4096 1 ;;
     pmcw)   run pmcw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 1 --warmup 0 ;;
     *) echo "unknown step $s" ;;
   esac

@@ -1,5 +1,9 @@
-"""A/B of the scoring-kernel variants on the GPU (one process, interleaved rounds, counts checked
-equal across variants).  Usage: python tools/score_ab.py [n_points] [D] [rounds]"""
+"""A/B of the scoring kernels on the GPU (one process, interleaved rounds, counts checked equal
+across kernels).  Usage: python tools/score_ab.py [n_points] [D] [rounds]
+KERNELS=0,1,2 (DLG_SCORE_EXACT, DLG_SCORE_BF16, DLG_SCORE_PRUNED); PRUNE_STATS=1 also prints the
+pruned kernel's work counters per launch (dlg_prune_stats).  The round-1 A/B of the retired
+variants (FMA prefilters, scalar coefficients, f32 MFMA, lanes-as-planes) is recorded in
+profiles/r01_score_variants_ab.json and DESIGN.md."""
 import json
 import os
 import sys
@@ -13,19 +17,19 @@ import dialog_amd as D  # noqa: E402
 from dialog_amd import _lib  # noqa: E402
 from dialog_amd.synth import SEED_BASE, plane_cloud  # noqa: E402
 
-NAMES = {0: "exact_p8", 1: "band_p8", 2: "min3_p8", 3: "exact_p16", 4: "min3_p16", 5: "exact_p4",
-         6: "min3_p4", 7: "exactS_p8g8", 8: "min3S_p8g8", 9: "exactS_p4g8", 10: "exactS_p8g4",
-         11: "mfma_pa32", 12: "mfma_pa16", 13: "mfma_pa8", 14: "lanes_exact", 15: "lanes_min3",
-         16: "lds_exact", 17: "lds_min3", 18: "bf16_t4", 19: "bf16_t8", 20: "pruned"}
+NAMES = {0: "exact_p4", 1: "bf16_t8", 2: "pruned"}
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
     nh = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    variants = [int(v) for v in os.environ.get("VARIANTS", "0,5,12,16,17").split(",")]
+    variants = [int(v) for v in os.environ.get("KERNELS", "2,1").split(",")]
+    want_stats = os.environ.get("PRUNE_STATS") == "1"
     pts, _, _ = plane_cloud(n, 20, seed=SEED_BASE + 3, shard=0)
     ctx = D.Context(0)
+    if want_stats:
+        ctx.set_option(D.DLG_OPT_PRUNE_STATS, 1)
     cloud = D.Cloud(ctx, pts)
     L = _lib.load()
     res = {v: [] for v in variants}
@@ -39,18 +43,22 @@ def main():
             res[v].append(ms.value)
             if ref is None:
                 ref = cnt.copy()
-            if not os.environ.get("SCORE_AB_NOCHECK"):
-                assert np.array_equal(cnt, ref), f"variant {v} counts differ"
-            elif not np.array_equal(cnt, ref):
-                print(f"variant {v}: {int((cnt != ref).sum())} counts differ", file=sys.stderr)
+            assert np.array_equal(cnt, ref), f"kernel {v} counts differ"
     out = {}
     for v in variants:
         med = float(np.median(res[v]))
         tps = n * nh / (med / 1e3)
         out[NAMES[v]] = dict(ms_median=round(med, 4), ms_min=round(min(res[v]), 4),
                              T_tests_per_s=round(tps / 1e12, 3))
+    extra = {}
+    if want_stats:
+        st = ctx.prune_stats(reset=True)
+        launches = rounds * 3 if 2 in variants else 0
+        if launches:
+            extra["pruned_per_launch"] = {k: v / launches for k, v in st.items()}
+            extra["pruned_per_launch"]["pair_fraction"] = st["pairs"] / launches / (n * nh / 32)
     print(json.dumps(dict(n=n, D=nh, rounds=rounds, counts_equal=True, total_inliers=int(ref.sum()),
-                          variants=out), indent=1))
+                          kernels=out, **extra), indent=1))
 
 
 if __name__ == "__main__":
