@@ -536,7 +536,21 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   c->h_tot.ensure(4);
   c->h_small.ensure(8);
   c->inl_gid.ensure((size_t)std::max<int64_t>(src.n, 1));
-  c->moments.ensure(kMomentK);
+  c->moments.ensure(kMomDigits);
+  if (!cl->qexp_known && prm.optimize && !pcl_refit) {
+    // the fast refit's quantum comes from the largest finite |coordinate| of the whole cloud
+    // (all ranks: one max-allreduce per cloud)
+    double f = (double)cl->fmax;
+    if (c->comm->world() > 1) {
+      c->scratch_f64.ensure(1);
+      HIPCHK(hipMemcpyAsync(c->scratch_f64.p, &f, 8, hipMemcpyHostToDevice, c->stream));
+      c->comm->allreduce_max_f64(c->scratch_f64.p, 1, c->stream);
+      HIPCHK(hipMemcpyAsync(&f, c->scratch_f64.p, 8, hipMemcpyDeviceToHost, c->stream));
+      sync(c);
+    }
+    cl->qexp = fast_qexp((float)f);
+    cl->qexp_known = true;
+  }
   PointsOut dst{};
   if (compact) {
     SoA& sp = cl->buf[cl->spare()];
@@ -574,17 +588,18 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         // (lean: the moments of the Morton copy -- the same finite inliers)
         const PointsView mv = lean ? sp_cur_view() : src;
         const int nb = moments_blocks(mv.n);
-        c->partials.ensure((size_t)nb * kMomentK);
-        launch_moments_refit(mv, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p,
-                             rc_dev, c->stream);
+        c->partials.ensure((size_t)nb * kMomDigits);
+        launch_moments_refit(mv, bc_dev, mt, cl->qexp, c->partials.p, nb, c->moments.p, rc_dev,
+                             c->stream);
       } else {
         if (prm.optimize) {
           const int nb = moments_blocks(src.n);
-          c->partials.ensure((size_t)nb * kMomentK);
-          launch_moments(src, bc_dev, mt, best_smp_dev, c->partials.p, nb, c->moments.p, c->stream);
-          c->comm->allreduce_sum(c->moments.p, kMomentK, DType::F64, c->stream);
+          c->partials.ensure((size_t)nb * kMomDigits);
+          launch_moments(src, bc_dev, mt, cl->qexp, c->partials.p, nb, c->moments.p, c->stream);
+          // exact integers: the rank sum is the one-rank result, whatever the sharding
+          c->comm->allreduce_sum(c->moments.p, kMomDigits, DType::I64, c->stream);
         }
-        launch_refit_moments(c->moments.p, best_smp_dev, bc_dev, prm.optimize, rc_dev, c->stream);
+        launch_refit_moments(c->moments.p, cl->qexp, bc_dev, prm.optimize, rc_dev, c->stream);
       }
     } else {
       // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
@@ -985,7 +1000,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->comm.reset();
   c->pos.release(); c->samples.release(); c->hyps.release(); c->res.release();
   c->tile_in.release(); c->tile_off_in.release(); c->tile_off_out.release(); c->totals.release();
-  c->partials.release(); c->moments.release(); c->inl_gid.release(); c->inl_xyz.release();
+  c->partials.release(); c->moments.release(); c->scratch_f64.release(); c->inl_gid.release(); c->inl_xyz.release();
   c->small.release(); c->h_small.release();
   c->gath64.release(); c->gath32.release();
   c->h_pos.release(); c->h_res.release(); c->h_tot.release(); c->h_mom.release(); c->h_g64.release();
@@ -1083,10 +1098,11 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     }
     c->totals.ensure(8);
     launch_absmax(cl->pristine.view(n), reinterpret_cast<uint32_t*>(c->totals.p), c->stream);
-    uint32_t bits[3];
-    HIPCHK(hipMemcpyAsync(bits, c->totals.p, 12, hipMemcpyDeviceToHost, c->stream));
+    uint32_t bits[4];
+    HIPCHK(hipMemcpyAsync(bits, c->totals.p, 16, hipMemcpyDeviceToHost, c->stream));
     sync(c);
     for (int k = 0; k < 3; ++k) std::memcpy(&cl->amax[k], &bits[k], 4);
+    std::memcpy(&cl->fmax, &bits[3], 4);
     if (c->opt.prune != 0 && n >= 3 && (n >= kPruneMinPoints || c->opt.prune == 1))
       build_spatial(c, cl.get());
   });
@@ -1423,10 +1439,10 @@ dlg_status dlg_allreduce_max_f64(dlg_ctx* c, double* v) {
   if (!c || !v) return DLG_ERR_INVALID;
   if (c->comm->world() == 1) return DLG_OK;
   return guarded(c, [&] {
-    c->moments.ensure(kMomentK);
-    HIPCHK(hipMemcpyAsync(c->moments.p, v, 8, hipMemcpyHostToDevice, c->stream));
-    c->comm->allreduce_max_f64(c->moments.p, 1, c->stream);
-    HIPCHK(hipMemcpyAsync(v, c->moments.p, 8, hipMemcpyDeviceToHost, c->stream));
+    c->scratch_f64.ensure(1);
+    HIPCHK(hipMemcpyAsync(c->scratch_f64.p, v, 8, hipMemcpyHostToDevice, c->stream));
+    c->comm->allreduce_max_f64(c->scratch_f64.p, 1, c->stream);
+    HIPCHK(hipMemcpyAsync(v, c->scratch_f64.p, 8, hipMemcpyDeviceToHost, c->stream));
     sync(c);
   });
 }

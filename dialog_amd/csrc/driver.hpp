@@ -176,7 +176,8 @@ struct dlg_ctx {
   dlg::Sel1State sel1;  // single-pass selects: tile status words + launch epoch
   DevBuf<uint64_t> sel1_status;
   DevBuf<int32_t> sel1_err;  // sticky look-back failure word of the single-pass selects
-  DevBuf<double> partials, moments;
+  DevBuf<int64_t> partials, moments;  // fast refit: exact moment digits (exact_refit.hpp)
+  DevBuf<double> scratch_f64;          // max-allreduce of host doubles
   DevBuf<int32_t> inl_gid;
   DevBuf<float> inl_xyz;
   DevBuf<int64_t> gath64;
@@ -239,6 +240,9 @@ struct dlg_cloud {
   int cur = -1;  // -1 pristine, 0 = A, 1 = B
   SoA pristine, buf[2];
   float amax[3] = {0, 0, 0};
+  float fmax = 0.0f;         // largest |coordinate| of the finite points (this rank's)
+  bool qexp_known = false;   // fast refit quantum exponent (global over ranks), set lazily
+  int qexp = 0;
   // Morton-ordered copy of the finite active points for the pruned scoring kernel (spatial.hpp):
   // built at upload (large clouds), compacted with the list in every SACMODEL_PLANE extract round
   bool sp_built = false;   // the pristine spatial copy exists

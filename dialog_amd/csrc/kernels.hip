@@ -16,6 +16,7 @@
 #include "dev_common.hpp"
 #include "np_dev.hpp"
 #include "host_math.hpp"
+#include "exact_refit.hpp"
 
 #include <algorithm>
 #include <cfloat>
@@ -396,11 +397,12 @@ __global__ __launch_bounds__(kBfBS) void k_score_bf16(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_moments (fast refit): count + first/second moments of the inliers of coef, in double, on
-// coordinates shifted by a point of the plane (limits cancellation in cov = E[pp^T] - E[p]E[p]^T).
+// k_moments (fast refit): the exact integer moments of the inliers of coef (exact_refit.hpp):
+// per lane kMomDigits int64 digit sums, then wave / workgroup / grid sums of the digits -- integer
+// adds, so the result is independent of the visiting order, the grid and the rank count.
 constexpr int kMoBS = 256;
 
-__device__ __forceinline__ double wave_sum_d(double v) {
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   return v;
@@ -408,14 +410,13 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 template <bool NP>
 __global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, const float4* __restrict__ cfp,
-                                                   ModelTest mt, const SampleRec* __restrict__ shp,
-                                                   double* __restrict__ partials) {
+                                                   ModelTest mt, double qscale,
+                                                   int64_t* __restrict__ partials) {
   const float4 cf = *cfp;
-  const double3 sh = make_double3((double)shp->x, (double)shp->y, (double)shp->z);
   const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
-  double acc[kMomentK];
+  int64_t acc[kMomDigits];
 #pragma unroll
-  for (int k = 0; k < kMomentK; ++k) acc[k] = 0.0;
+  for (int k = 0; k < kMomDigits; ++k) acc[k] = 0;
   // kMoIt points per lane per pass, their loads all in flight before the tests (clamped,
   // unconditional: one guarded load per iteration would wait out each load in turn)
   constexpr int kMoIt = 8;
@@ -430,82 +431,76 @@ __global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, const float4*
 #pragma unroll
     for (int j = 0; j < kMoIt; ++j) {
       const int64_t e = b0 + j * kMoBS + threadIdx.x;
-      if (e < src.n && model_in<NP>(src, e, cf, cn, mt, x[j], y[j], z[j])) {
-        double dx = (double)x[j] - sh.x, dy = (double)y[j] - sh.y, dz = (double)z[j] - sh.z;
-        acc[0] += 1.0;
-        acc[1] += dx; acc[2] += dy; acc[3] += dz;
-        acc[4] += dx * dx; acc[5] += dx * dy; acc[6] += dx * dz;
-        acc[7] += dy * dy; acc[8] += dy * dz; acc[9] += dz * dz;
-      }
+      if (e < src.n && model_in<NP>(src, e, cf, cn, mt, x[j], y[j], z[j]))
+        mom_add(acc, fast_q(x[j], qscale), fast_q(y[j], qscale), fast_q(z[j], qscale));
     }
   }
-  __shared__ double s_red[kMoBS / kWave][kMomentK];
+  __shared__ int64_t s_red[kMoBS / kWave][kMomDigits];
   const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
 #pragma unroll
-  for (int k = 0; k < kMomentK; ++k) {
-    double v = wave_sum_d(acc[k]);
+  for (int k = 0; k < kMomDigits; ++k) {
+    const int64_t v = wave_sum_i64(acc[k]);
     if (lane == 0) s_red[w][k] = v;
   }
   __syncthreads();
-  if (threadIdx.x < kMomentK) {
-    double v = 0.0;
+  if (threadIdx.x < kMomDigits) {
+    int64_t v = 0;
     for (int q = 0; q < kMoBS / kWave; ++q) v += s_red[q][threadIdx.x];
-    partials[(int64_t)blockIdx.x * kMomentK + threadIdx.x] = v;
+    partials[(int64_t)blockIdx.x * kMomDigits + threadIdx.x] = v;
   }
 }
 
-__global__ void k_reduce_partials(const double* __restrict__ partials, int nb,
-                                  double* __restrict__ out) {
-  // fixed order (deterministic): wave k sums column k, lane l takes blocks l, l+64, ...; then a
-  // fixed xor-butterfly across the wave
-  const int k = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  if (k >= kMomentK) return;
-  double v = 0.0;
-  for (int b = lane; b < nb; b += kWave) v += partials[(int64_t)b * kMomentK + k];
-  v = wave_sum_d(v);
-  if (lane == 0) out[k] = v;
+constexpr int kRedBS = 256;
+
+// digit sums over the nb workgroup partials (wave w takes digits w, w + 4, ...) -> s_m
+__device__ __forceinline__ void reduce_digits(const int64_t* __restrict__ partials, int nb,
+                                              int64_t* s_m) {
+  const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  for (int k = w; k < kMomDigits; k += kRedBS / kWave) {
+    int64_t v = 0;
+    for (int b = lane; b < nb; b += kWave) v += partials[(int64_t)b * kMomDigits + k];
+    v = wave_sum_i64(v);
+    if (lane == 0) s_m[k] = v;
+  }
 }
 
-// fast refit on the device (one thread): moments -> double covariance -> pcl::eigen33 -> plane
-// through the centroid; < 4 inliers (or optimize off) keep the unrefined plane.  Keeps the
-// refined plane on the device for the final select (no host round trip between them).
-__global__ void k_refit_moments(const double* __restrict__ mom, const SampleRec* __restrict__ shp,
+__global__ __launch_bounds__(kRedBS) void k_reduce_partials(const int64_t* __restrict__ partials,
+                                                            int nb, int64_t* __restrict__ out) {
+  __shared__ int64_t s_m[kMomDigits];
+  reduce_digits(partials, nb, s_m);
+  __syncthreads();
+  if (threadIdx.x < kMomDigits) out[threadIdx.x] = s_m[threadIdx.x];
+}
+
+// fast refit on the device (one thread): exact moments -> plane (exact_refit.hpp); < 4 inliers
+// (or optimize off) keep the unrefined plane.  Keeps the refined plane on the device for the
+// final select (no host round trip between them).
+__global__ void k_refit_moments(const int64_t* __restrict__ mom, int qexp,
                                 const float4* __restrict__ cin, int optimize,
                                 float4* __restrict__ cout) {
   if (threadIdx.x != 0) return;
   const float4 c = *cin;
   const float ci[4] = {c.x, c.y, c.z, c.w};
   float co[4] = {c.x, c.y, c.z, c.w};
-  if (optimize) {
-    const double sh[3] = {(double)shp->x, (double)shp->y, (double)shp->z};
-    refit_from_moments(mom, sh, ci, co);
-  }
+  if (optimize) refit_exact(mom, qexp, ci, co);
   *cout = make_float4(co[0], co[1], co[2], co[3]);
 }
 
 // one rank: k_reduce_partials + k_refit_moments in one launch (the allreduce of the moments that
 // separates them with several ranks is the identity)
-__global__ void k_reduce_refit(const double* __restrict__ partials, int nb, double* __restrict__ out,
-                               const SampleRec* __restrict__ shp, const float4* __restrict__ cin,
-                               float4* __restrict__ cout) {
-  __shared__ double s_m[kMomentK];
-  const int k = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  if (k < kMomentK) {
-    double v = 0.0;
-    for (int b = lane; b < nb; b += kWave) v += partials[(int64_t)b * kMomentK + k];
-    v = wave_sum_d(v);
-    if (lane == 0) {
-      s_m[k] = v;
-      out[k] = v;
-    }
-  }
+__global__ __launch_bounds__(kRedBS) void k_reduce_refit(const int64_t* __restrict__ partials,
+                                                         int nb, int64_t* __restrict__ out,
+                                                         int qexp, const float4* __restrict__ cin,
+                                                         float4* __restrict__ cout) {
+  __shared__ int64_t s_m[kMomDigits];
+  reduce_digits(partials, nb, s_m);
   __syncthreads();
+  if (threadIdx.x < kMomDigits) out[threadIdx.x] = s_m[threadIdx.x];
   if (threadIdx.x != 0) return;
   const float4 c = *cin;
   const float ci[4] = {c.x, c.y, c.z, c.w};
   float co[4] = {c.x, c.y, c.z, c.w};
-  const double sh[3] = {(double)shp->x, (double)shp->y, (double)shp->z};
-  refit_from_moments(s_m, sh, ci, co);
+  refit_exact(s_m, qexp, ci, co);
   *cout = make_float4(co[0], co[1], co[2], co[3]);
 }
 
@@ -1156,20 +1151,23 @@ __global__ void k_upload_gather(const float* __restrict__ raw, int64_t stride_f,
   out.gid[i] = (int32_t)(id_base + k);
 }
 
-__global__ void k_absmax(PointsView src, uint32_t* __restrict__ out3) {
-  float m[3] = {0.f, 0.f, 0.f};
+__global__ void k_absmax(PointsView src, uint32_t* __restrict__ out4) {
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < src.n; e += stride) {
-    m[0] = fmaxf(m[0], fabsf(src.x[e]));
-    m[1] = fmaxf(m[1], fabsf(src.y[e]));
-    m[2] = fmaxf(m[2], fabsf(src.z[e]));
+    const float ax = fabsf(src.x[e]), ay = fabsf(src.y[e]), az = fabsf(src.z[e]);
+    m[0] = fmaxf(m[0], ax);
+    m[1] = fmaxf(m[1], ay);
+    m[2] = fmaxf(m[2], az);
+    // the largest finite |coordinate| of the finite points (fast refit quantum)
+    if (ax < INFINITY && ay < INFINITY && az < INFINITY) m[3] = fmaxf(m[3], fmaxf(ax, fmaxf(ay, az)));
   }
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < 4; ++k) {
     float v = m[k];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
     // non-negative floats order like their bit patterns; NaN/inf -> +inf bits dominate
-    if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(&out3[k], __float_as_uint(v));
+    if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(&out4[k], __float_as_uint(v));
   }
 }
 
@@ -1325,34 +1323,31 @@ int moments_blocks(int64_t n) {
   return (int)b;
 }
 
-void launch_refit_moments(const double* moments, const SampleRec* shift, const float4* cin,
-                          int optimize, float4* cout, hipStream_t s) {
-  hipLaunchKernelGGL(k_refit_moments, dim3(1), dim3(64), 0, s, moments, shift, cin, optimize, cout);
-}
-
-void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt,
-                          const SampleRec* shift, double* partials, int nblocks, double* out,
+void launch_refit_moments(const int64_t* moments, int qexp, const float4* cin, int optimize,
                           float4* cout, hipStream_t s) {
-  if (mt.normal_plane)
-    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
-                       partials);
-  else
-    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
-                       partials);
-  hipLaunchKernelGGL(k_reduce_refit, dim3(1), dim3(kMomentK * kWave), 0, s, partials, nblocks, out,
-                     shift, coef, cout);
+  hipLaunchKernelGGL(k_refit_moments, dim3(1), dim3(64), 0, s, moments, qexp, cin, optimize, cout);
 }
 
-void launch_moments(PointsView src, const float4* coef, const ModelTest& mt,
-                    const SampleRec* shift, double* partials, int nblocks, double* out,
-                    hipStream_t s) {
+void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
+                          int64_t* partials, int nblocks, int64_t* out, float4* cout,
+                          hipStream_t s) {
+  const double qs = pow2d(kFastBits - qexp);
   if (mt.normal_plane)
-    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
-                       partials);
+    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
   else
-    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, shift,
-                       partials);
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kMomentK * kWave), 0, s, partials, nblocks, out);
+    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
+  hipLaunchKernelGGL(k_reduce_refit, dim3(1), dim3(kRedBS), 0, s, partials, nblocks, out, qexp,
+                     coef, cout);
+}
+
+void launch_moments(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
+                    int64_t* partials, int nblocks, int64_t* out, hipStream_t s) {
+  const double qs = pow2d(kFastBits - qexp);
+  if (mt.normal_plane)
+    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
+  else
+    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kRedBS), 0, s, partials, nblocks, out);
 }
 
 void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
@@ -1443,12 +1438,12 @@ void launch_upload_gather(const float* raw, int64_t stride_f, const int32_t* idx
                      id_base, out);
 }
 
-void launch_absmax(PointsView src, uint32_t* out3, hipStream_t s) {
-  (void)hipMemsetAsync(out3, 0, 3 * sizeof(uint32_t), s);
+void launch_absmax(PointsView src, uint32_t* out4, hipStream_t s) {
+  (void)hipMemsetAsync(out4, 0, 4 * sizeof(uint32_t), s);
   if (src.n <= 0) return;
   unsigned g = cdiv(src.n, 256);
   if (g > 1024) g = 1024;
-  hipLaunchKernelGGL(k_absmax, dim3(g), dim3(256), 0, s, src, out3);
+  hipLaunchKernelGGL(k_absmax, dim3(g), dim3(256), 0, s, src, out4);
 }
 
 }  // namespace dlg

@@ -10,6 +10,8 @@
 
 #include <cstdint>
 
+#include "exact_refit.hpp"
+
 namespace dlg {
 
 // one sampled point of a hypothesis (gathered by list position; zero on ranks not holding it)
@@ -57,7 +59,6 @@ struct ModelTest {
 
 constexpr int kMaxHypPerLaunch = 4096;  // LDS count array of the scoring kernel
 constexpr int kSelTile = 4096;          // points per select/compact workgroup
-constexpr int kMomentK = 10;            // n, sx, sy, sz, sxx, sxy, sxz, syy, syz, szz
 
 // Exhaustive scoring kernels (every active point against every hypothesis; the pruned kernel
 // of spatial.hpp is the default whenever the cloud has a Morton copy).  All give bit-identical
@@ -135,21 +136,20 @@ void launch_prep_bf16(const HypRec* hyps, int D, const uint4** bcol, const float
 // counts need room for D rounded up to 64 and must be zeroed by the caller
 void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest& mt,
                      int32_t* counts, int num_cus, hipStream_t s);
-// moments (count + 9 sums, double, coordinates shifted by `shift`) of the inliers of coef;
-// partials [nblocks][10] -> out[10] (fixed-order reduction: deterministic)
+// fast refit (exact_refit.hpp): the exact integer moments (kMomDigits int64 digit sums) of the
+// inliers of coef, quantised with exponent qexp; partials [nblocks][kMomDigits] -> out
 int moments_blocks(int64_t n);
-// coef: device float4 (a, b, c, d); shift: the device sample point the moments are centred on
+// coef: device float4 (a, b, c, d)
 // one rank: moments of the unrefined plane's inliers + reduction + refit in two launches
-void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt,
-                          const SampleRec* shift, double* partials, int nblocks, double* out,
+void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
+                          int64_t* partials, int nblocks, int64_t* out, float4* cout,
+                          hipStream_t s);
+void launch_moments(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
+                    int64_t* partials, int nblocks, int64_t* out, hipStream_t s);
+// device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
+// than 4 inliers
+void launch_refit_moments(const int64_t* moments, int qexp, const float4* cin, int optimize,
                           float4* cout, hipStream_t s);
-void launch_moments(PointsView src, const float4* coef, const ModelTest& mt,
-                    const SampleRec* shift, double* partials, int nblocks, double* out,
-                    hipStream_t s);
-// device fast refit: cout = plane of moments[10] (centred on shift), or cin when optimize == 0
-// or fewer than 4 inliers
-void launch_refit_moments(const double* moments, const SampleRec* shift, const float4* cin,
-                          int optimize, float4* cout, hipStream_t s);
 // select: inliers of coef in list order; optional inlier xyz (AoS, 3 floats); optional
 // compaction of the outliers (and their normals) into dst.  tile_in/out: [ntiles] scratch;
 // totals[2] = {in, out}.
@@ -171,7 +171,8 @@ void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off,
 // cloud upload: records of stride_f floats (xyz first), optional index list -> SoA + ids
 void launch_upload_gather(const float* raw, int64_t stride_f, const int32_t* idx, int64_t n,
                           int32_t id_base, PointsOut out, hipStream_t s);
-// max |x|, |y|, |z| over the cloud (prefilter error bound); out: 3 floats (as uint bits)
-void launch_absmax(PointsView src, uint32_t* out3, hipStream_t s);
+// max |x|, |y|, |z| over the cloud (prefilter error bound; NaN ignored, inf kept) and the
+// largest |coordinate| of its finite points (fast refit quantum); out: 4 floats (as uint bits)
+void launch_absmax(PointsView src, uint32_t* out4, hipStream_t s);
 
 }  // namespace dlg

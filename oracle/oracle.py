@@ -32,7 +32,10 @@ class SacParams(C.Structure):
     _fields_ = [("threshold", C.c_double), ("max_iterations", C.c_int),
                 ("probability", C.c_double), ("optimize", C.c_int),
                 ("seed", C.c_uint32), ("refit_double", C.c_int), ("model", C.c_int),
-                ("normal_distance_weight", C.c_double), ("normals", C.POINTER(C.c_float))]
+                ("normal_distance_weight", C.c_double), ("normals", C.POINTER(C.c_float)),
+                ("fast_qexp", C.c_int)]
+
+QEXP_AUTO = -100000
 
 
 class SacStats(C.Structure):
@@ -58,6 +61,12 @@ def lib():
         L.orc_rnd.argtypes = [C.POINTER(MT)]
         L.orc_rnd.restype = C.c_int
         L.orc_plane_coefficients.argtypes = [fp, fp, fp, fp]
+        L.orc_set_threads.argtypes = [C.c_int]
+        L.orc_set_threads.restype = None
+        L.orc_fast_qexp.argtypes = [fp, C.c_int64, i32p, C.c_int64]
+        L.orc_fast_qexp.restype = C.c_int
+        L.orc_refit_exact.argtypes = [fp, C.c_int64, i32p, C.c_int64, C.c_int, fp, fp]
+        L.orc_refit_exact.restype = C.c_int
         L.orc_plane_sample_good.argtypes = [fp, fp, fp]
         L.orc_thr_ceil.argtypes = [C.c_double]
         L.orc_thr_ceil.restype = C.c_float
@@ -113,6 +122,28 @@ def _xyz(points):
     return p, p.shape[1]
 
 
+def set_threads(n: int) -> None:
+    """OpenMP threads of the oracle's countWithinDistance (1 = PCL's serial loop)."""
+    lib().orc_set_threads(int(n))
+
+
+def fast_qexp(points, indices=None) -> int:
+    p, stride = _xyz(points)
+    if indices is not None:
+        idx = np.ascontiguousarray(indices, np.int32)
+        return int(lib().orc_fast_qexp(_f(p), stride, _i32(idx), idx.shape[0]))
+    return int(lib().orc_fast_qexp(_f(p), stride, None, p.shape[0]))
+
+
+def refit_exact(points, indices, coeff_in, qexp):
+    p, stride = _xyz(points)
+    idx = np.ascontiguousarray(indices, np.int32)
+    ci = np.ascontiguousarray(coeff_in, np.float32)
+    co = np.zeros(4, np.float32)
+    lib().orc_refit_exact(_f(p), stride, _i32(idx), idx.shape[0], int(qexp), _f(ci), _f(co))
+    return co
+
+
 def rnd_stream(n, seed=12345):
     g = MT()
     lib().orc_mt_seed(C.byref(g), seed)
@@ -126,11 +157,18 @@ def mt_stream(n, seed=12345):
 
 
 def params(threshold, max_iterations=50, probability=0.99, optimize=True, seed=12345,
-           refit_double=False, normals=None, normal_distance_weight=0.1):
+           refit_double=False, normals=None, normal_distance_weight=0.1, refit="pcl",
+           fast_qexp=None):
     """normals (float32 [N,4]: nx, ny, nz, curvature) selects SACMODEL_NORMAL_PLANE; the caller
-    keeps the array alive for the call (params_keep)."""
+    keeps the array alive for the call (params_keep).  refit: "pcl" (PCL float), "double" (the
+    two-pass double LS reference; also refit_double=True) or "fast" (the product's
+    DLG_REFIT_FAST, orc_refit_exact); fast_qexp overrides its quantum exponent."""
+    mode = {"pcl": 0, "double": 1, "fast": 2}[refit]
+    if refit_double:
+        mode = 1
     prm = SacParams(float(threshold), int(max_iterations), float(probability),
-                    int(bool(optimize)), int(seed), int(bool(refit_double)))
+                    int(bool(optimize)), int(seed), mode)
+    prm.fast_qexp = QEXP_AUTO if fast_qexp is None else int(fast_qexp)
     if normals is not None:
         assert normals.dtype == np.float32 and normals.flags.c_contiguous and normals.shape[1] == 4
         prm.model = SACMODEL_NORMAL_PLANE

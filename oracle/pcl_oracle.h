@@ -51,6 +51,13 @@ void orc_eigen33(const float m[9], float* eval, float evec[3]);
 void orc_eigen33_d(const double m[9], double* eval, double evec[3]);
 int  orc_refit_double(const float* xyz, int64_t stride, const int32_t* idx, int64_t n,
                       const float coeff_in[4], float coeff_out[4]);
+/* the product's DLG_REFIT_FAST restated (dialog_amd/csrc/exact_refit.hpp definition) */
+int  orc_fast_qexp(const float* xyz, int64_t stride, const int32_t* idx, int64_t n);
+int  orc_refit_exact(const float* xyz, int64_t stride, const int32_t* idx, int64_t n, int qexp,
+                     const float coeff_in[4], float coeff_out[4]);
+/* threads of countWithinDistance (OpenMP; default 1 = PCL's serial loop) */
+void orc_set_threads(int n);
+int  orc_get_threads(void);
 
 /* ---- SACSegmentation<PointXYZ>::segment with SACMODEL_PLANE / SAC_RANSAC, and
  *      SACSegmentationFromNormals with SACMODEL_NORMAL_PLANE ---- */
@@ -62,11 +69,15 @@ typedef struct {
   double   probability;      /* setProbability (default 0.99) */
   int      optimize;         /* setOptimizeCoefficients (default true) */
   uint32_t seed;             /* 12345u unless random_ */
-  int      refit_double;     /* 0: PCL float refit; 1: double-exact refit (fast-mode twin) */
+  int      refit_double;     /* 0: PCL float refit; 1: two-pass double refit (LS reference);
+                                2: the product's fast refit (exact moments, orc_refit_exact) */
   int      model;            /* ORC_SACMODEL_PLANE | ORC_SACMODEL_NORMAL_PLANE */
   double   normal_distance_weight;  /* setNormalDistanceWeight (PCL default 0.1) */
   const float* normals;      /* NORMAL_PLANE: 4 floats per point (nx, ny, nz, curvature) */
+  int      fast_qexp;        /* refit_double 2: quantum exponent, ORC_QEXP_AUTO = from the
+                                segmented points (extract: from the whole cloud) */
 } orc_sac_params;
+#define ORC_QEXP_AUTO (-100000)
 
 typedef struct {
   int     iterations;        /* RandomSampleConsensus::iterations_ at exit */
