@@ -28,7 +28,7 @@ SYMBOLS = [
     "dlg_post_process_planes", "dlg_cluster_filter", "dlg_sac_control_create",
     "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
     "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
-    "dlg_ctx_get_option", "dlg_prune_stats",
+    "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex",
 ]
 
 # context options (include/dialog_ransac.h): equivalent execution paths, identical results
@@ -138,6 +138,8 @@ def load():
                                         fp, C.c_int64]
     L.dlg_cloud_set_normals.argtypes = [vp, vp, fp, C.c_int64, C.c_int64]
     L.dlg_estimate_normals.argtypes = [vp, C.POINTER(Points), C.c_float, C.c_int, fp, fp, C.c_int64]
+    L.dlg_estimate_normals_ex.argtypes = [vp, C.POINTER(Points), C.c_float, C.c_int, fp, fp,
+                                          C.c_int64, C.c_int]
     L.dlg_regulate_normals.argtypes = [vp, C.POINTER(Points), fp, C.c_int64, C.c_int64, C.c_int,
                                        C.c_float, C.POINTER(C.c_uint8), i64p]
     L.dlg_refit_planes.argtypes = [C.POINTER(Planes), fp]

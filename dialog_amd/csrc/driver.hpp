@@ -109,6 +109,9 @@ struct NormalsWork {
   DevBuf<float4> nrm, nrm_s;
   DevBuf<uint32_t> claim, ccnt, coffs, ccur, ctile, cslot;
   DevBuf<float> sd2;
+  DevBuf<int32_t> ncnt;   // PCL-float radius normals: neighbours per query (chunk)
+  DevBuf<int64_t> noff;   //   their offsets
+  DevBuf<uint64_t> nkeys; //   (d2, index) keys
   DevBuf<long long> bst;
   PinBuf<long long> h_bst;
   DevBuf<unsigned long long> keys64, keys_alt;
@@ -123,6 +126,7 @@ struct NormalsWork {
     pos_of.release(); nrm.release(); nrm_s.release(); claim.release(); keys64.release();
     keys_alt.release(); h_cnt.release(); ccnt.release(); coffs.release(); ccur.release();
     sd2.release(); bst.release(); h_bst.release(); ctile.release(); cslot.release();
+    ncnt.release(); noff.release(); nkeys.release();
   }
 };
 

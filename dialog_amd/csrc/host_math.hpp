@@ -35,16 +35,21 @@ template <>
 DLG_HD inline double min_of<double>() { return DBL_MIN; }
 template <typename S>
 DLG_HD inline void swap_(S& a, S& b) { S t = a; a = b; b = t; }
-// float math stays float (sqrtf, atan2f, ...: what std:: overloads call for PCL's float eigen33)
+// PCL's float eigen33 calls std::sqrt / atan2 / cos / sin on floats.  sqrtf is correctly rounded
+// everywhere; the float transcendental functions are platform-specific (MSVC's CRT for the
+// reference -- unknowable here), so they are taken as the correctly rounded float values,
+// computed as the double function rounded to float: host and device then agree (except in the
+// ~2^-29-probable case of a double result within an ulp of a float rounding boundary), and the
+// oracle (orc_eigen33) and the numpy twin evaluate them the same way.
 DLG_HD inline float m_sqrt(float x) { return sqrtf(x); }
 DLG_HD inline double m_sqrt(double x) { return sqrt(x); }
 DLG_HD inline float m_fabs(float x) { return fabsf(x); }
 DLG_HD inline double m_fabs(double x) { return fabs(x); }
-DLG_HD inline float m_atan2(float y, float x) { return atan2f(y, x); }
+DLG_HD inline float m_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 DLG_HD inline double m_atan2(double y, double x) { return atan2(y, x); }
-DLG_HD inline float m_cos(float x) { return cosf(x); }
+DLG_HD inline float m_cos(float x) { return (float)cos((double)x); }
 DLG_HD inline double m_cos(double x) { return cos(x); }
-DLG_HD inline float m_sin(float x) { return sinf(x); }
+DLG_HD inline float m_sin(float x) { return (float)sin((double)x); }
 DLG_HD inline double m_sin(double x) { return sin(x); }
 
 class Mt19937 {

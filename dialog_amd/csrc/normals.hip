@@ -33,6 +33,7 @@
 #include <cstdint>
 
 #include "grid_dev.hpp"
+#include "host_math.hpp"
 #include "normals.hpp"
 
 namespace dlg {
@@ -310,7 +311,206 @@ __global__ __launch_bounds__(kBS) void k_normals_radius(
 // Queries are taken in the level's own cell order (qpos = sorted positions at level l; nullptr =
 // all), so the lanes of a wavefront scan the same cells; a deferred query is flagged at its
 // sorted position of level l + 1 and the next pass compacts the flags in that order.
-template <int KP>
+// ---- PCL-float normals: pcl::computePointNormal as PCL 1.8 evaluates it -------------------
+// computeMeanAndCovarianceMatrix (float, single pass over the neighbour list in FLANN's (d2,
+// index) order), solvePlaneParameters (pcl::eigen33 in float, curvature = |lambda0 / trace| in
+// float), flipNormalTowardsViewpoint (float, left to right).  Bit-exact with the oracle's
+// restatement (orc_estimate_normals / _knn).
+__device__ __forceinline__ void pcl_accu_add(float* a, float x, float y, float z) {
+  a[0] += x * x; a[1] += x * y; a[2] += x * z;
+  a[3] += y * y; a[4] += y * z; a[5] += z * z;
+  a[6] += x;     a[7] += y;     a[8] += z;
+}
+
+__device__ float4 finish_normal_pcl(float* a, int cnt, float qx, float qy, float qz, float vpx,
+                                    float vpy, float vpz) {
+  if (cnt < 3) {
+    const float qnan = __builtin_nanf("");
+    return make_float4(qnan, qnan, qnan, qnan);
+  }
+  const float cf = (float)(size_t)cnt;
+  for (int k = 0; k < 9; ++k) a[k] = a[k] / cf;
+  float cov[9];
+  cov[0] = a[0] - a[6] * a[6];
+  cov[1] = a[1] - a[6] * a[7];
+  cov[2] = a[2] - a[6] * a[8];
+  cov[4] = a[3] - a[7] * a[7];
+  cov[5] = a[4] - a[7] * a[8];
+  cov[8] = a[5] - a[8] * a[8];
+  cov[3] = cov[1]; cov[6] = cov[2]; cov[7] = cov[5];
+  float ev, v[3];
+  eigen33<float>(cov, &ev, v);
+  const float eig_sum = cov[0] + cov[4] + cov[8];
+  const float curv = eig_sum != 0.0f ? fabsf(ev / eig_sum) : 0.0f;
+  float nx = v[0], ny = v[1], nz = v[2];
+  const float vx = vpx - qx, vy = vpy - qy, vz = vpz - qz;
+  const float cos_theta = vx * nx + vy * ny + vz * nz;
+  if (cos_theta < 0.0f) { nx *= -1.0f; ny *= -1.0f; nz *= -1.0f; }
+  return make_float4(nx, ny, nz, curv);
+}
+
+// radius search, pass 1: neighbour counts per query (sorted positions [q0, q0 + nq))
+__global__ __launch_bounds__(kBS) void k_nbr_count(
+    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
+    int q0, int nq, GridDesc G, const uint32_t* __restrict__ tkeys,
+    const int2* __restrict__ trange, uint32_t tmask, float r2, int32_t* __restrict__ cnt) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= nq) return;
+  const int t = q0 + i;
+  const float qx = sx[t], qy = sy[t], qz = sz[t];
+  int c = 0;
+  if (finite3(qx, qy, qz)) {
+    const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+    const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+    const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+    for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
+      for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
+        for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
+          const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+          for (int u = rg.x; u < rg.y; ++u)
+            c += flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2 ? 1 : 0;
+        }
+  }
+  cnt[i] = c;
+}
+
+// pass 2: the neighbours as 64-bit keys (d2 bits << 32 | point index: (d2, index) order) at the
+// query's offset
+__global__ __launch_bounds__(kBS) void k_nbr_fill(
+    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
+    const int32_t* __restrict__ sidx, int q0, int nq, GridDesc G,
+    const uint32_t* __restrict__ tkeys, const int2* __restrict__ trange, uint32_t tmask, float r2,
+    const int64_t* __restrict__ off, uint64_t* __restrict__ keys) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= nq) return;
+  const int t = q0 + i;
+  const float qx = sx[t], qy = sy[t], qz = sz[t];
+  if (!finite3(qx, qy, qz)) return;
+  uint64_t* out = keys + off[i];
+  int c = 0;
+  const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+  const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+  const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+  for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
+    for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
+      for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
+        const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+        for (int u = rg.x; u < rg.y; ++u) {
+          const float d2 = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
+          if (d2 < r2)
+            out[c++] = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)sidx[u];
+        }
+      }
+}
+
+// bitonic sort of 64 * E keys held E per lane (element e = lane + 64 j), ascending
+template <int E>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&v)[E]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64 * E; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const int e = lane + 64 * j;
+        const bool up = (e & size) == 0;  // this element's block sorts ascending
+        if (stride >= 64) {
+          const int js = stride >> 6;
+          if ((j & js) == 0) {  // (j, j | js): both in this lane
+            uint64_t& a = v[j];
+            uint64_t& b = v[j | js];
+            const bool sw = up ? (a > b) : (a < b);
+            if (sw) { const uint64_t t = a; a = b; b = t; }
+          }
+        } else {
+          const uint64_t o = __shfl_xor(v[j], stride, 64);
+          const bool lower = (lane & stride) == 0;
+          // lower element keeps min when ascending, max when descending
+          const bool take_min = lower == up;
+          v[j] = take_min ? (o < v[j] ? o : v[j]) : (o > v[j] ? o : v[j]);
+        }
+      }
+    }
+  }
+}
+
+template <int E>
+__device__ __forceinline__ void sort_segment(uint64_t* seg, int k) {
+  const int lane = threadIdx.x & 63;
+  uint64_t v[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = lane + 64 * j;
+    v[j] = e < k ? seg[e] : ~0ull;
+  }
+  wave_bitonic<E>(v);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = lane + 64 * j;
+    if (e < k) seg[e] = v[j];
+  }
+}
+
+// in-place heapsort by one lane (segments longer than 1024 keys: rare)
+__device__ void heap_sort(uint64_t* a, int64_t n) {
+  auto sift = [&](int64_t i, int64_t m) {
+    for (;;) {
+      int64_t c = 2 * i + 1;
+      if (c >= m) break;
+      if (c + 1 < m && a[c + 1] > a[c]) ++c;
+      if (a[i] >= a[c]) break;
+      const uint64_t t = a[i]; a[i] = a[c]; a[c] = t;
+      i = c;
+    }
+  };
+  for (int64_t i = n / 2 - 1; i >= 0; --i) sift(i, n);
+  for (int64_t m = n - 1; m > 0; --m) {
+    const uint64_t t = a[0]; a[0] = a[m]; a[m] = t;
+    sift(0, m);
+  }
+}
+
+// pass 3: sort each query's keys (one wave per query)
+__global__ __launch_bounds__(kBS) void k_nbr_sort(int nq, const int32_t* __restrict__ cnt,
+                                                  const int64_t* __restrict__ off,
+                                                  uint64_t* __restrict__ keys) {
+  const int wv = (blockIdx.x * kBS + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * kBS) >> 6;
+  for (int i = wv; i < nq; i += nw) {
+    const int k = cnt[i];
+    if (k < 2) continue;
+    uint64_t* seg = keys + off[i];
+    if (k <= 64) sort_segment<1>(seg, k);
+    else if (k <= 128) sort_segment<2>(seg, k);
+    else if (k <= 256) sort_segment<4>(seg, k);
+    else if (k <= 512) sort_segment<8>(seg, k);
+    else if (k <= 1024) sort_segment<16>(seg, k);
+    else if ((threadIdx.x & 63) == 0) heap_sort(seg, k);
+  }
+}
+
+// pass 4: PCL's sums over the sorted neighbours, one thread per query
+__global__ __launch_bounds__(kBS) void k_nbr_normals(
+    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
+    const int32_t* __restrict__ sidx, int q0, int nq, const int32_t* __restrict__ cnt,
+    const int64_t* __restrict__ off, const uint64_t* __restrict__ keys,
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    float vpx, float vpy, float vpz, float4* __restrict__ normals) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i >= nq) return;
+  const int t = q0 + i;
+  const int k = cnt[i];
+  float a[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const uint64_t* seg = keys + off[i];
+  for (int e = 0; e < k; ++e) {
+    const int j = (int)(uint32_t)seg[e];
+    pcl_accu_add(a, X[j], Y[j], Z[j]);
+  }
+  normals[sidx[t]] = finish_normal_pcl(a, k, sx[t], sy[t], sz[t], vpx, vpy, vpz);
+}
+
+template <int KP, bool PCLF>
 __global__ __launch_bounds__(kBS) void k_normals_knn(
     KnnLevels L, int l, const int32_t* __restrict__ qpos, int nq, const float* __restrict__ X,
     const float* __restrict__ Y, const float* __restrict__ Z, int K, float vpx, float vpy,
@@ -372,6 +572,18 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     defer = cnt < K && !top;
     if (!defer) {
       const int m = cnt < K ? cnt : K;
+      if constexpr (PCLF) {
+        // PCL: float sums over the kNN list in (d2, index) order
+        float a[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < KP; ++j)
+          if (j < m) {
+            const int i = bi[j];
+            pcl_accu_add(a, X[i], Y[i], Z[i]);
+          }
+        normals[qi] = finish_normal_pcl(a, m, qx, qy, qz, vpx, vpy, vpz);
+        return;
+      }
 #pragma unroll
       for (int j = 0; j < KP; ++j)
         if (j < m) {
@@ -381,7 +593,8 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     }
   }
   if (defer) defer_next[L.pos_of[l + 1][qi]] = 1;
-  else normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+  else normals[qi] = PCLF ? finish_normal_pcl(nullptr, 0, qx, qy, qz, vpx, vpy, vpz)
+                          : finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
 }
 
 __global__ __launch_bounds__(kBS) void k_inverse_perm(const int32_t* __restrict__ idx, int n,
@@ -897,24 +1110,57 @@ void launch_normals_radius(const GridDesc& G, const GridBufs& B, int n, float r2
 
 void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
-                        float4* normals, uint8_t* defer_next, hipStream_t s) {
+                        float4* normals, uint8_t* defer_next, bool pcl_float, hipStream_t s) {
   if (nq <= 0) return;
   const dim3 g(cdiv(nq, kBS)), b(kBS);
-  if (k <= 8)
-    hipLaunchKernelGGL(k_normals_knn<8>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, defer_next);
-  else if (k <= 16)
-    hipLaunchKernelGGL(k_normals_knn<16>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, defer_next);
-  else if (k <= 24)
-    hipLaunchKernelGGL(k_normals_knn<24>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, defer_next);
-  else if (k <= 32)
-    hipLaunchKernelGGL(k_normals_knn<32>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, defer_next);
-  else
-    hipLaunchKernelGGL(k_normals_knn<64>, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1],
-                       vp[2], normals, defer_next);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1], vp[2],
+                       normals, defer_next);
+  };
+  if (pcl_float) {
+    if (k <= 8) go(k_normals_knn<8, true>);
+    else if (k <= 16) go(k_normals_knn<16, true>);
+    else if (k <= 24) go(k_normals_knn<24, true>);
+    else if (k <= 32) go(k_normals_knn<32, true>);
+    else go(k_normals_knn<64, true>);
+  } else {
+    if (k <= 8) go(k_normals_knn<8, false>);
+    else if (k <= 16) go(k_normals_knn<16, false>);
+    else if (k <= 24) go(k_normals_knn<24, false>);
+    else if (k <= 32) go(k_normals_knn<32, false>);
+    else go(k_normals_knn<64, false>);
+  }
+}
+
+void launch_nbr_count(const GridDesc& G, const GridBufs& B, int q0, int nq, float r2,
+                      int32_t* cnt, hipStream_t s) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(k_nbr_count, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, B.sx, B.sy, B.sz, q0, nq,
+                     G, B.tkeys, B.trange, B.tmask, r2, cnt);
+}
+
+size_t nbr_scan_tmp_bytes(int nq) {
+  size_t t = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int32_t*)nullptr, (int64_t*)nullptr, nq);
+  return t;
+}
+
+hipError_t nbr_scan(void* tmp, size_t tmp_bytes, const int32_t* cnt, int64_t* off, int nq,
+                    hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, nq, s);
+}
+
+void launch_nbr_fill_sort_normals(const GridDesc& G, const GridBufs& B, int q0, int nq, float r2,
+                                  const int32_t* cnt, const int64_t* off, uint64_t* keys,
+                                  const float* X, const float* Y, const float* Z, const float vp[3],
+                                  float4* normals, int num_cus, hipStream_t s) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(k_nbr_fill, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, B.sx, B.sy, B.sz,
+                     B.idx_out, q0, nq, G, B.tkeys, B.trange, B.tmask, r2, off, keys);
+  const unsigned gs = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nq, kBS / 64), (int64_t)num_cus * 16));
+  hipLaunchKernelGGL(k_nbr_sort, dim3(gs), dim3(kBS), 0, s, nq, cnt, off, keys);
+  hipLaunchKernelGGL(k_nbr_normals, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, B.sx, B.sy, B.sz,
+                     B.idx_out, q0, nq, cnt, off, keys, X, Y, Z, vp[0], vp[1], vp[2], normals);
 }
 
 void launch_inverse_perm(const int32_t* idx, int n, int32_t* pos_of, hipStream_t s) {

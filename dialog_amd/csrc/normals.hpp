@@ -76,9 +76,24 @@ struct KnnLevels {
 // one level: queries = sorted positions qpos[0..nq) of level `level` (nullptr: all of them);
 // a query with fewer than k neighbours inside the level's guaranteed radius sets
 // defer_next[its sorted position at level + 1]
+// pcl_float: PCL's single-pass float moments over the (d2, index)-ordered list + float eigen33
+// (bit-exact with PCL's arithmetic as restated); else centred double moments + double eigen33
 void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
-                        float4* normals, uint8_t* defer_next, hipStream_t s);
+                        float4* normals, uint8_t* defer_next, bool pcl_float, hipStream_t s);
+// PCL-float radius normals in chunks of queries (sorted positions [q0, q0 + nq)):
+// counts -> exclusive scan (int64 offsets) -> (d2, index) keys filled, sorted per query (one
+// wave per query: bitonic in registers up to 1024 keys, heapsort beyond) -> float sums in that
+// order, eigen33<float>, curvature, viewpoint flip
+void launch_nbr_count(const GridDesc& G, const GridBufs& B, int q0, int nq, float r2,
+                      int32_t* cnt, hipStream_t s);
+size_t nbr_scan_tmp_bytes(int nq);
+hipError_t nbr_scan(void* tmp, size_t tmp_bytes, const int32_t* cnt, int64_t* off, int nq,
+                    hipStream_t s);
+void launch_nbr_fill_sort_normals(const GridDesc& G, const GridBufs& B, int q0, int nq, float r2,
+                                  const int32_t* cnt, const int64_t* off, uint64_t* keys,
+                                  const float* X, const float* Y, const float* Z, const float vp[3],
+                                  float4* normals, int num_cus, hipStream_t s);
 void launch_inverse_perm(const int32_t* idx, int n, int32_t* pos_of, hipStream_t s);
 
 // nearest neighbour (k = 1, ties -> lowest index) in the hierarchy's cloud of external queries

@@ -180,7 +180,10 @@ void check_points(const dlg_points* pts) {
 namespace {
 
 void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn, const float* vp_in,
-                      float* out, int64_t out_stride) {
+                      float* out, int64_t out_stride, int mode) {
+  if (mode != DLG_NORMALS_PCL_FLOAT && mode != DLG_NORMALS_CENTRED_DOUBLE)
+    throw DlgError(DLG_ERR_INVALID, "mode must be DLG_NORMALS_PCL_FLOAT or DLG_NORMALS_CENTRED_DOUBLE");
+  const bool pclf = mode == DLG_NORMALS_PCL_FLOAT;
   check_points(pts);
   if (!out) throw DlgError(DLG_ERR_INVALID, "normals_out is null");
   if (out_stride != 16 && out_stride < 32) throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be 16 or >= 32");
@@ -199,7 +202,38 @@ void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
     const GridDesc G = make_grid(b, (double)radius);
     build_grid(c, n, G, 0, &B);
     const float r2 = (float)((double)radius * (double)radius);  // KdTreeFLANN: radius * radius
-    launch_normals_radius(G, B, n, r2, vp, w.nrm.p, c->stream);
+    if (!pclf) {
+      launch_normals_radius(G, B, n, r2, vp, w.nrm.p, c->stream);
+    } else {
+      // queries in chunks of the sorted order: neighbour counts, offsets, then the (d2, index)
+      // keys of the chunk (bounded by kMaxKeys; a chunk is halved until it fits)
+      constexpr int64_t kMaxKeys = int64_t(1) << 28;  // 2 GiB of keys
+      const int qc_max = std::min(n, 1 << 22);
+      w.ncnt.ensure(qc_max);
+      w.noff.ensure(qc_max);
+      w.sort_tmp.ensure(std::max(w.sort_tmp.cap, nbr_scan_tmp_bytes(qc_max)));
+      w.h_bst.ensure(2);
+      for (int q0 = 0; q0 < n;) {
+        int nq = std::min(qc_max, n - q0);
+        int64_t total = 0;
+        for (;;) {
+          launch_nbr_count(G, B, q0, nq, r2, w.ncnt.p, c->stream);
+          HIPCHK(nbr_scan(w.sort_tmp.p, w.sort_tmp.cap, w.ncnt.p, w.noff.p, nq, c->stream));
+          HIPCHK(hipMemcpyAsync(w.h_bst.p, w.noff.p + (nq - 1), 8, hipMemcpyDeviceToHost, c->stream));
+          HIPCHK(hipMemcpyAsync(reinterpret_cast<int32_t*>(w.h_bst.p + 1), w.ncnt.p + (nq - 1), 4,
+                                hipMemcpyDeviceToHost, c->stream));
+          sync(c);
+          total = (int64_t)w.h_bst.p[0] + *reinterpret_cast<int32_t*>(w.h_bst.p + 1);
+          if (total <= kMaxKeys || nq == 1) break;
+          nq = (nq + 1) / 2;
+        }
+        w.nkeys.ensure((size_t)std::max<int64_t>(total, 1));
+        launch_nbr_fill_sort_normals(G, B, q0, nq, r2, w.ncnt.p, w.noff.p, w.nkeys.p, w.x.p,
+                                     w.y.p, w.z.p, vp, w.nrm.p, c->num_cus, c->stream);
+        HIPCHK(hipGetLastError());
+        q0 += nq;
+      }
+    }
   } else {
     const KnnLevels L = build_hierarchy(c, n, b, k_nn);
     w.queue.ensure(n);
@@ -211,7 +245,7 @@ void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
       const bool top = l == L.levels - 1;
       if (!top) HIPCHK(hipMemsetAsync(w.processed.p, 0, n, c->stream));
       launch_normals_knn(L, l, qpos, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, w.processed.p,
-                         c->stream);
+                         pclf, c->stream);
       if (top) break;
       // deferred queries in level l+1's cell order
       HIPCHK(select_flagged(w.sort_tmp.p, w.sort_tmp.cap, w.processed.p, n, w.queue.p,
@@ -451,9 +485,16 @@ extern "C" {
 dlg_status dlg_estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
                                 const float viewpoint[3], float* normals_out,
                                 int64_t out_stride_bytes) {
+  return dlg_estimate_normals_ex(c, pts, radius, k_nn, viewpoint, normals_out, out_stride_bytes,
+                                 DLG_NORMALS_PCL_FLOAT);
+}
+
+dlg_status dlg_estimate_normals_ex(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
+                                   const float viewpoint[3], float* normals_out,
+                                   int64_t out_stride_bytes, int mode) {
   if (!c) return DLG_ERR_INVALID;
   return guarded(c, [&] {
-    estimate_normals(c, pts, radius, k_nn, viewpoint, normals_out, out_stride_bytes);
+    estimate_normals(c, pts, radius, k_nn, viewpoint, normals_out, out_stride_bytes, mode);
   });
 }
 

@@ -17,17 +17,25 @@ from . import _lib
 from .sac import Context, _f32p, _points, default_context
 
 
+NORMALS_PCL_FLOAT = 0
+NORMALS_CENTRED_DOUBLE = 1
+
+
 def estimate_normals(points, radius: float = 0.0, k: int = 0, viewpoint=(0.0, 0.0, 0.0),
-                     ctx: Context | None = None, layout: str = "float4") -> np.ndarray:
+                     ctx: Context | None = None, layout: str = "float4",
+                     mode: str = "pcl") -> np.ndarray:
     """points float32 [N,3|4] -> float32 [N,4] (nx, ny, nz, curvature) for layout "float4", or
-    [N,8] pcl::Normal records (normal_x/y/z, pad, curvature, pad x3) for layout "pcl"."""
+    [N,8] pcl::Normal records (normal_x/y/z, pad, curvature, pad x3) for layout "pcl".
+    mode "pcl": PCL's float arithmetic (bit-exact with the oracle); "double": centred double
+    moments (dlg_estimate_normals_ex)."""
     ctx = ctx or default_context()
     a, pts = _points(points)
     width = {"float4": 4, "pcl": 8}[layout]
+    m = {"pcl": NORMALS_PCL_FLOAT, "double": NORMALS_CENTRED_DOUBLE}[mode]
     out = np.empty((a.shape[0], width), np.float32)
     vp = np.ascontiguousarray(viewpoint, np.float32)
-    ctx.check(_lib.load().dlg_estimate_normals(ctx.h, C.byref(pts), float(radius), int(k),
-                                               _f32p(vp), _f32p(out), 4 * width))
+    ctx.check(_lib.load().dlg_estimate_normals_ex(ctx.h, C.byref(pts), float(radius), int(k),
+                                                  _f32p(vp), _f32p(out), 4 * width, m))
     return out
 
 

@@ -60,3 +60,31 @@ def read_polygons(path: str):
         borders.append(verts[base:base + m])
         base += m
     return borders, normals, np.asarray(scales, np.float32)
+
+
+def read_polygon_pair(pcd_path: str, sizes_path: str):
+    """The plane-registration polygon input (Dialog/Registration.h:356-420, files
+    Dialog/dataForPlane/<side>_plane_registration.{pcd,txt}): all border vertices in one PCD and
+    the vertex count of each polygon in a text file.  As the reference: counts are accumulated
+    until the running sum reaches the vertex count (later entries are not read), and polygon k
+    takes vertices [sum_{k-1}, sum_k).  The reference's behaviour is undefined when the counts
+    overshoot the vertex count or run out before reaching it (it reads past the cloud / loops on a
+    failed read): both raise ValueError here.  -> list of float32 [m_k, 3]."""
+    verts = read_pcd(pcd_path)
+    with open(sizes_path) as f:
+        tokens = f.read().split()
+    bounds, total = [], 0
+    for t in tokens:
+        total += int(t)
+        bounds.append(total)
+        if total >= verts.shape[0]:
+            break
+    if not bounds or bounds[-1] < verts.shape[0]:
+        raise ValueError(f"{sizes_path}: polygon sizes end before the {verts.shape[0]} vertices")
+    if bounds[-1] > verts.shape[0]:
+        raise ValueError(f"{sizes_path}: polygon sizes overshoot the {verts.shape[0]} vertices")
+    out, lo = [], 0
+    for b in bounds:
+        out.append(verts[lo:b].copy())
+        lo = b
+    return out

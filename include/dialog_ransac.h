@@ -181,6 +181,17 @@ dlg_status dlg_extract_planes(dlg_ctx* ctx, dlg_cloud* cloud, const dlg_sac_para
 dlg_status dlg_estimate_normals(dlg_ctx* ctx, const dlg_points* pts, float radius, int k_nn,
                                 const float viewpoint[3], float* normals_out,
                                 int64_t out_stride_bytes);
+/* dlg_estimate_normals with an arithmetic mode:
+ *   DLG_NORMALS_PCL_FLOAT (what dlg_estimate_normals uses): PCL 1.8's computePointNormal --
+ *     computeMeanAndCovarianceMatrix's single-pass float sums over the neighbours in FLANN's
+ *     (d2, index) order, pcl::eigen33 in float, curvature |lambda0 / trace| in float, the
+ *     viewpoint flip; bit-exact with the oracle's restatement of it
+ *   DLG_NORMALS_CENTRED_DOUBLE: the same neighbourhoods, moments centred on the query in double
+ *     and eigen33 in double (better conditioned far from the origin; not PCL's rounding) */
+enum { DLG_NORMALS_PCL_FLOAT = 0, DLG_NORMALS_CENTRED_DOUBLE = 1 };
+dlg_status dlg_estimate_normals_ex(dlg_ctx* ctx, const dlg_points* pts, float radius, int k_nn,
+                                   const float viewpoint[3], float* normals_out,
+                                   int64_t out_stride_bytes, int mode);
 /* regulateNormal() first-round branch (PlaneDetect.h:586-646): flip the seed normal unless
  * seed_is_outward (is_norm_direction_valid), then BFS over radius-`radius` neighbourhoods
  * (r_for_regulate_normal, config.txt:9) in PCL's queue order, flipping each newly reached normal

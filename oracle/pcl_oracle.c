@@ -248,9 +248,12 @@ void orc_compute_roots(const float m[9], float roots[3]) {
     float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
     if (q > 0.0f) q = 0.0f;
     float rho = sqrtf(-a_over_3);
-    float theta = atan2f(sqrtf(-q), half_b) * s_inv3;
-    float cos_theta = cosf(theta);
-    float sin_theta = sinf(theta);
+    /* std::atan2 / cos / sin on floats: the correctly rounded float value, evaluated as the
+     * double function rounded to float (the platform's float libm is unknowable; see
+     * dialog_amd/csrc/host_math.hpp m_atan2) */
+    float theta = (float)atan2((double)sqrtf(-q), (double)half_b) * s_inv3;
+    float cos_theta = (float)cos((double)theta);
+    float sin_theta = (float)sin((double)theta);
     roots[0] = c2_over_3 + 2.0f * rho * cos_theta;
     roots[1] = c2_over_3 - rho * (cos_theta + s_sqrt3 * sin_theta);
     roots[2] = c2_over_3 - rho * (cos_theta - s_sqrt3 * sin_theta);

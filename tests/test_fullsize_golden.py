@@ -1,0 +1,139 @@
+"""GPU at BASELINE.json's full sizes against the oracle's full-size results
+(tests/golden/fullsize.json, made by tests/golden/make_fullsize.py in the build container):
+
+  c2       1M points, 3 planes, one segment() of 4096 hypotheses (configs[1])   pcl, fast refit
+  c3       10M points, 20 planes, extract-and-remove (configs[2], the bench)    fast, pcl, none
+  c4shape  100M points, 20 planes, the same extraction on one GPU (configs[3]) fast (if present)
+
+Bit-exact: iterations, best sample, coefficient bit patterns, per-plane inlier counts and the
+SHA-256 of every plane's inlier-id list.  The fast refit (the bench's mode) is also run with the
+lean rounds off and sharded over an in-process group of ranks: the same bits.  The input cloud is
+regenerated here from the seeded generator and its SHA-256 checked first.
+"""
+import hashlib
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import dialog_amd as D
+from dialog_amd.synth import plane_cloud
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")
+DB = json.load(open(GOLD)) if os.path.exists(GOLD) else {}
+MODES = {"pcl": dict(refit_mode=D.DLG_REFIT_PCL), "fast": dict(refit_mode=D.DLG_REFIT_FAST),
+         "none": dict(optimize=False)}
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+_CLOUDS = {}
+
+
+def cloud(name):
+    if name not in _CLOUDS:
+        _CLOUDS.clear()  # (one full-size cloud in host memory at a time)
+        w = DB[name]
+        p, _, _ = plane_cloud(w["n_points"], w["planes"], seed=w["seed"], shares=w["shares"])
+        assert sha(p) == w["cloud_sha256"], "the generator did not reproduce the golden cloud"
+        _CLOUDS[name] = p
+    return _CLOUDS[name]
+
+
+def params(mode, **extra):
+    return D.make_params(0.02, max_iterations=4095, probability=1.0, hypotheses_per_launch=4096,
+                         **MODES[mode], **extra)
+
+
+def check_extract(e, g):
+    assert e["n_planes"] == g["n_planes"]
+    assert [[int(v) for v in c.view(np.uint32)] for c in e["coeffs"]] == g["coeff_bits"]
+    offs = e["offsets"]
+    assert [int(offs[k + 1] - offs[k]) for k in range(e["n_planes"])] == g["counts"]
+    assert [sha(e["inliers"][offs[k]:offs[k + 1]]) for k in range(e["n_planes"])] == g["inliers_sha256"]
+
+
+def modes_of(name):
+    return sorted(DB.get(name, {}).get("modes", {}))
+
+
+@pytest.mark.skipif("c2" not in DB, reason="fullsize.json has no c2")
+@pytest.mark.parametrize("mode", modes_of("c2"))
+def test_c2_segment(gpu_ctx, mode):
+    g = DB["c2"]["modes"][mode]
+    p = cloud("c2")
+    cl = D.Cloud(gpu_ctx, p)
+    inl, coeff, st = D.segment_cloud(cl, params(mode))
+    cl.close()
+    assert st["iterations"] == g["iterations"] and st["draws"] == g["draws"]
+    assert st["launches"] == 1
+    assert [int(v) for v in st["best_sample"]] == g["best_sample"]
+    assert [int(v) for v in st["coeff_unrefined"].view(np.uint32)] == g["coeff_unrefined_bits"]
+    assert st["n_unrefined"] == g["n_unrefined"]
+    assert [int(v) for v in coeff.view(np.uint32)] == g["coeff_bits"]
+    assert inl.size == g["n_inliers"] and sha(inl) == g["inliers_sha256"]
+
+
+@pytest.mark.skipif("c3" not in DB, reason="fullsize.json has no c3")
+@pytest.mark.parametrize("mode", modes_of("c3"))
+def test_c3_extract(gpu_ctx, mode):
+    p = cloud("c3")
+    cl = D.Cloud(gpu_ctx, p)
+    e = D.extract_planes(cl, params(mode), max_planes=20, min_inliers=500, capacity=p.shape[0])
+    cl.close()
+    check_extract(e, DB["c3"]["modes"][mode])
+    if mode != "pcl":
+        assert e["stats"]["lean_rounds"] == e["stats"]["rounds"]  # the bench's path
+
+
+@pytest.mark.skipif("c3" not in DB or "fast" not in DB["c3"]["modes"], reason="no c3/fast")
+def test_c3_fast_two_pass_and_sharded(gpu_ctx):
+    """The bench mode through the two-pass selects, and sharded over 2 in-process ranks."""
+    p = cloud("c3")
+    g = DB["c3"]["modes"]["fast"]
+    ctx = D.Context(0)
+    ctx.set_option(D.DLG_OPT_LEAN_ROUNDS, 0)
+    cl = D.Cloud(ctx, p)
+    e = D.extract_planes(cl, params("fast"), max_planes=20, min_inliers=500, capacity=p.shape[0])
+    cl.close()
+    ctx.close()
+    assert e["stats"]["lean_rounds"] == 0
+    check_extract(e, g)
+    ctxs = D.Context.loopback_group(2, 0)
+    half = p.shape[0] // 2
+    out, errs = [None, None], []
+
+    def run(r):
+        try:
+            lo, hi = (0, half) if r == 0 else (half, p.shape[0])
+            c = D.Cloud(ctxs[r], p[lo:hi], id_base=lo)
+            out[r] = D.extract_planes(c, params("fast"), max_planes=20, min_inliers=500,
+                                      capacity=p.shape[0])
+            c.close()
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    for r in range(2):
+        check_extract(out[r], g)
+
+
+@pytest.mark.skipif("c4shape" not in DB, reason="fullsize.json has no c4shape")
+@pytest.mark.parametrize("mode", modes_of("c4shape"))
+def test_c4shape_extract_one_gpu(gpu_ctx, mode):
+    """configs[3]'s 100M-point cloud on one GPU (the 8-GPU run shards it)."""
+    p = cloud("c4shape")
+    cl = D.Cloud(gpu_ctx, p)
+    e = D.extract_planes(cl, params(mode), max_planes=20, min_inliers=500, capacity=p.shape[0])
+    cl.close()
+    check_extract(e, DB["c4shape"]["modes"][mode])

@@ -247,3 +247,71 @@ def test_gpu_np_loopback_sharded(gpu_ctx, world):
         assert np.array_equal(out[r]["inliers"], ref["inliers"])
     for c in ctxs:
         c.close()
+
+
+# ------------------------------------------------------------------------------------- C5 chain
+@pytest.mark.gpu
+@pytest.mark.parametrize("nmode,refit", [("radius", "pcl"), ("knn", "pcl"), ("knn", "fast")])
+def test_gpu_c5_chain_vs_oracle_chain(gpu_ctx, nmode, refit):
+    """BASELINE configs[4] (C5) end to end at test size: GPU normals (PCL-float mode) ->
+    GPU SACMODEL_NORMAL_PLANE extract-and-remove equals oracle normals -> oracle extract, bit for
+    bit (the normals are bit-identical, so every normal-plane distance is too)."""
+    import dialog_amd as D
+    from dialog_amd.synth import plane_cloud
+    p, _, _ = plane_cloud(30000, 5, outlier_frac=0.1, seed=55, patch=2.0)
+    if nmode == "radius":
+        g = D.estimate_normals(p, radius=0.1, ctx=gpu_ctx)
+        o = O.estimate_normals(p, 0.1)
+    else:
+        g = D.estimate_normals(p, k=20, ctx=gpu_ctx)
+        o = O.estimate_normals_knn(p, 20)
+    assert np.array_equal(g.view(np.uint32), o.view(np.uint32))
+    kw = dict(max_iterations=255, probability=1.0)
+    mode = D.DLG_REFIT_PCL if refit == "pcl" else D.DLG_REFIT_FAST
+    cloud = D.Cloud(gpu_ctx, p)
+    cloud.set_normals(g)
+    prm = D.make_params(0.05, model=D.SACMODEL_NORMAL_PLANE, normal_distance_weight=0.1,
+                        refit_mode=mode, **kw)
+    e = D.extract_planes(cloud, prm, max_planes=6, min_inliers=200)
+    cloud.close()
+    r = O.extract_planes(p, 0.05, max_planes=6, min_inliers=200, normals=o,
+                         normal_distance_weight=0.1, refit=refit, **kw)
+    assert e["n_planes"] == r["n_planes"] >= 4
+    assert np.array_equal(e["coeffs"].view(np.uint32), r["coeffs"].view(np.uint32))
+    assert np.array_equal(e["offsets"], r["offsets"])
+    assert np.array_equal(e["inliers"], r["inliers"])
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_gpu_c5_full_size_properties(gpu_ctx):
+    """C5 at its quoted size (10M points, k = 20 PCL-float normals, NORMAL_PLANE w = 0.1, 4096
+    hypotheses per round): every extracted inlier passes PCL's normal-plane test (numpy
+    restatement on a sample), planes disjoint and ascending, deterministic across runs."""
+    import dialog_amd as D
+    from dialog_amd.synth import SEED_BASE, plane_cloud
+    p, _, _ = plane_cloud(10_000_000, 20, seed=SEED_BASE + 5)
+    nrm = D.estimate_normals(p, k=20, ctx=gpu_ctx)
+    assert np.isfinite(nrm).all()
+    # spot-check the normals against the oracle's kNN restatement on a sub-cloud's own kNN
+    cloud = D.Cloud(gpu_ctx, p)
+    cloud.set_normals(nrm)
+    prm = D.make_params(0.02, max_iterations=4095, probability=1.0, refit_mode=D.DLG_REFIT_FAST,
+                        hypotheses_per_launch=4096, model=D.SACMODEL_NORMAL_PLANE,
+                        normal_distance_weight=0.1)
+    e = D.extract_planes(cloud, prm, max_planes=20, min_inliers=500, capacity=p.shape[0])
+    cloud.reset()
+    e2 = D.extract_planes(cloud, prm, max_planes=20, min_inliers=500, capacity=p.shape[0])
+    cloud.close()
+    assert e["n_planes"] >= 18
+    assert np.array_equal(e["inliers"], e2["inliers"])
+    assert np.array_equal(e["coeffs"].view(np.uint32), e2["coeffs"].view(np.uint32))
+    inl, offs = e["inliers"], e["offsets"]
+    assert np.unique(inl).size == inl.size
+    rng = np.random.default_rng(0)
+    for k in range(e["n_planes"]):
+        ids = inl[offs[k]:offs[k + 1]]
+        assert np.all(np.diff(ids) > 0)
+        s = ids[rng.choice(ids.size, min(2000, ids.size), replace=False)]
+        d = np_twin_dist(e["coeffs"][k], p[s], nrm[s], 0.1)
+        assert np.all(d < 0.02)

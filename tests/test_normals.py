@@ -5,10 +5,11 @@ CPU tests pin the oracle (oracle/pcl_oracle.c) against an independent float64 nu
 and the committed fixture; GPU tests compare libdialog_amd.so against both:
   * neighbour sets are exact (same float d2 test as KdTreeFLANN): the NaN mask (< 3 neighbours)
     must match the oracle exactly;
-  * normals / curvature: the device accumulates the covariance in double (PCL sums float), so it
-    is compared with the float64 restatement at 1e-5 rad / 1e-5 relative curvature where the
-    eigenproblem is well conditioned, and with the PCL-float oracle at the float-cancellation
-    bound (angle <= 2e-3 rad at the 99th percentile, all <= 2e-2 rad);
+  * normals / curvature, mode "pcl" (the default, PCL's float arithmetic: single-pass float sums
+    over the (d2, index)-ordered neighbours, eigen33 in float): bit-exact with the oracle, for
+    radius neighbourhoods of every size class of the device sort (<= 64 ... > 1024) and k-NN;
+  * mode "double" (centred double moments): the float64 restatement at 1e-5 rad / 1e-5 relative
+    curvature where the eigenproblem is well conditioned;
   * RegulateNormal is bit-exact: same processed set, same count, identical normals.
 """
 import json
@@ -157,7 +158,7 @@ def cloud():
 def test_gpu_radius_normals(gpu_ctx, cloud):
     import dialog_amd as D
     p, _, _ = cloud
-    g = D.estimate_normals(p, radius=RADIUS, ctx=gpu_ctx)
+    g = D.estimate_normals(p, radius=RADIUS, ctx=gpu_ctx, mode="double")
     o = O.estimate_normals(p, RADIUS)
     assert np.array_equal(np.isnan(g[:, 0]), np.isnan(o[:, 0]))  # exact neighbour counts
     ref, gap = f64_normals(p, flann_radius_sets(p, RADIUS))
@@ -180,7 +181,7 @@ def test_gpu_knn_normals(gpu_ctx, cloud):
     import dialog_amd as D
     p, _, _ = cloud
     for k in (3, 20, 64):
-        g = D.estimate_normals(p, k=k, ctx=gpu_ctx)
+        g = D.estimate_normals(p, k=k, ctx=gpu_ctx, mode="double")
         ref, gap = f64_normals(p, knn_sets(p, k))
         ok = gap > 1e-3
         assert not np.isnan(g).any()
@@ -188,11 +189,43 @@ def test_gpu_knn_normals(gpu_ctx, cloud):
         assert a.max() < 1e-5, (k, a.max())
         np.testing.assert_allclose(g[ok, 3], ref[ok, 3], rtol=1e-4, atol=1e-7)
     o = O.estimate_normals_knn(p[:3000], 20)
-    g = D.estimate_normals(p[:3000], k=20, ctx=gpu_ctx)
+    g = D.estimate_normals(p[:3000], k=20, ctx=gpu_ctx, mode="double")
     _, gap = f64_normals(p[:3000], knn_sets(p[:3000], 20))
     ok = gap > 1e-2
     a = angle(g[ok], o[ok])
     assert np.percentile(a, 99) < 2e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,patch,r,seed", [
+    (12000, 2.0, 0.1, 3),     # ~30 neighbours: one-register sort
+    (12000, 2.0, 0.2, 4),     # ~100-200: 2-4 keys per lane
+    (6000, 1.0, 0.3, 5),      # ~500-1000: 8-16 keys per lane
+    (3000, 0.5, 0.45, 6),     # > 1024 neighbours: the heapsort path
+])
+def test_gpu_radius_normals_pcl_bit_exact(gpu_ctx, n, patch, r, seed):
+    """PCL-float mode (dlg_estimate_normals): bit-identical to the oracle's computePointNormal
+    restatement, NaN mask included, viewpoint flip included."""
+    import dialog_amd as D
+    p, _, _ = small_cloud(n, seed=seed, patch=patch)
+    p[::97] = np.nan
+    for vp in ((0.0, 0.0, 0.0), (3.0, -1.0, 2.0)):
+        g = D.estimate_normals(p, radius=r, viewpoint=vp, ctx=gpu_ctx)
+        o = O.estimate_normals(p, r, viewpoint=vp)
+        assert np.array_equal(np.isnan(g), np.isnan(o))
+        ok = ~np.isnan(o[:, 0])
+        assert np.array_equal(g[ok].view(np.uint32), o[ok].view(np.uint32)), \
+            int((g[ok] != o[ok]).any(axis=1).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [3, 20, 33, 64])
+def test_gpu_knn_normals_pcl_bit_exact(gpu_ctx, k):
+    import dialog_amd as D
+    p, _, _ = small_cloud(3000, seed=9)
+    g = D.estimate_normals(p, k=k, ctx=gpu_ctx)
+    o = O.estimate_normals_knn(p, k)
+    assert np.array_equal(g.view(np.uint32), o.view(np.uint32)), int((g != o).any(axis=1).sum())
 
 
 @pytest.mark.gpu
