@@ -192,8 +192,11 @@ def test_gpu_np_requires_normals_and_fast_refit(gpu_ctx):
     prm_f = D.make_params(0.05, max_iterations=100, model=D.SACMODEL_NORMAL_PLANE,
                           refit_mode=D.DLG_REFIT_FAST)
     inl, coeff, st = D.segment_cloud(cloud, prm_f)
-    r = O.sac_segment(p, 0.05, max_iterations=100, normals=nrm, refit_double=True)
-    assert np.abs(coeff - r["coeff"]).max() < 1e-5
+    r = O.sac_segment(p, 0.05, max_iterations=100, normals=nrm, refit="fast")
+    assert np.array_equal(coeff.view(np.uint32), r["coeff"].view(np.uint32))
+    rd = O.sac_segment(p, 0.05, max_iterations=100, normals=nrm, refit="double")
+    sg = 1.0 if coeff[:3] @ rd["coeff"][:3] > 0 else -1.0  # (the double twin is not oriented)
+    assert np.abs(coeff - sg * rd["coeff"]).max() < 1e-5
     d = np_twin_dist(coeff, p, nrm, 0.1)
     assert np.array_equal(inl, np.flatnonzero(d < 0.05).astype(np.int32))
     # the PCL mirror
