@@ -9,15 +9,24 @@
 // -ffp-contract=off.  [PCL-1.8 ext] = third-party source, not vendored in the reference.
 #pragma once
 
-#include <hip/hip_runtime.h>
-
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <limits>
 #include <utility>
 
+// (host-only builds -- the sanitizer harness tests/cpp/sac_control_san.cpp -- compile without
+// HIP: g++ -fsanitize=address,undefined)
+#if defined(__HIP__) || defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#ifndef DLG_HD
 #define DLG_HD __host__ __device__
+#endif
+#else
+#ifndef DLG_HD
+#define DLG_HD
+#endif
+#endif
 
 namespace dlg {
 
