@@ -74,10 +74,13 @@ def test_no_device_fails_loudly(monkeypatch):
         seg.segment()
 
 
-def test_cpp_shim_compiles_and_links(tmp_path):
-    """The PCL-compatible C++ host shim compiles with g++ against the header and links the .so."""
-    src = os.path.join(ROOT, "tests", "cpp", "shim_smoke.cpp")
-    exe = tmp_path / "shim_smoke"
+@pytest.mark.parametrize("prog", ["shim_smoke", "plane_clouds_glue"])
+def test_cpp_shim_compiles_and_links(tmp_path, prog):
+    """The PCL-compatible C++ host shim compiles with g++ against the header and links the .so
+    (shim_smoke: every shim entry; plane_clouds_glue: INTEGRATION.md §3's PlaneDetect.h adapter
+    with the reference's struct Plane)."""
+    src = os.path.join(ROOT, "tests", "cpp", prog + ".cpp")
+    exe = tmp_path / prog
     cmd = ["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"), src, "-o", str(exe),
            "-L", os.path.dirname(_lib.LIB_PATH), "-ldialog_amd",
            f"-Wl,-rpath,{os.path.dirname(_lib.LIB_PATH)}"]

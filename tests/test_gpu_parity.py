@@ -242,6 +242,20 @@ def test_cpp_shim_runs_on_gpu(tmp_path):
     assert post[0] + post[1] <= 64 * 64 + 500
 
 
+def test_cpp_plane_clouds_glue_runs_on_gpu(tmp_path):
+    """INTEGRATION.md §3's segmentPlanesRansac() compiled against the shim with the reference's
+    struct Plane (HeaderFile.h:81-88): six box faces -> six planes whose coeff.values are the
+    3-component outward normals and whose border is left for polyPlanes (PlaneDetect.h:1364)."""
+    exe = tmp_path / "plane_clouds_glue"
+    lib = os.path.dirname(D.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "plane_clouds_glue.cpp"), "-o", str(exe),
+                    "-L", lib, "-ldialog_amd", f"-Wl,-rpath,{lib}"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, (out.stdout, out.stderr)
+    assert out.stdout.strip() == "planes 6 bad 0"
+
+
 def test_rccl_one_rank_path(gpu_ctx):
     """The RCCL communicator code (dlopen, ncclCommInitRank, in-place allreduce, allgather,
     allreduce-max) on a real device with one rank (world 1 + a unique id): same planes as the
