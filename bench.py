@@ -3,18 +3,23 @@
 Workload (BASELINE.json configs[2], the 10M-point cloud the metric is quoted on): per GPU a 10M-
 point synthetic cloud with 20 planes (+10 % outliers, BASELINE.md §3 generator), sequential
 extract-and-remove RANSAC: each round scores 4096 hypotheses (max_iterations 4095, probability 1.0
--> k = inf, exactly 4096 PCL iterations) over the remaining points, refits (fast double mode),
-selects and compacts the inliers; stop after 20 planes or when a plane has < 500 inliers.
-One step = one full extraction from the pristine cloud (inputs resident in HBM).
+-> k = inf, exactly 4096 PCL iterations) over the remaining points, refits (DLG_REFIT_FAST: the
+exact-moment LS refit, bit-exact with the oracle's restatement), selects and compacts the
+inliers; stop after 20 planes or when a plane has < 500 inliers.  One step = one full
+extraction from the pristine cloud (inputs resident in HBM).
 
-Multi-GPU (weak scaling, torchrun one process per GPU): rank r holds its own 10M-point shard of
-one global cloud (same 20 planes); every round all ranks score the same hypotheses on their
-shards with one RCCL allreduce of the int32[4096] counts.
+Multi-GPU (torchrun, one process per GPU): weak scaling by default -- rank r holds its own 10M-
+point shard of one global cloud (same 20 planes); --global-points 100000000 runs configs[3] (C4)
+strong-sharded.  Every round all ranks score the same hypotheses on their shards with one RCCL
+allreduce of the int32[4096] counts, and sum the exact refit moments.
 
 value = useful point-plane tests (PCL iterations x global active points, summed over rounds) / s,
-whole job.  Roofline: the scoring kernel (k_score_bf16 by default), against the f32 VALU peak with
-SURVEY 8(d)'s algorithmic 7 ops per test, timed with HIP events on the library's stream.  cpu_baseline: the PCL-1.8 restatement (oracle, 1 thread) on
-a bounded sample of the same workload, rank 0 at N = 1 only.
+whole job.  Roofline: the pruned scoring launch against HBM with SURVEY 8(d)'s algorithmic bytes,
+with its PMC traffic, issue view and the work the pruning leaves (pruned_work).  Extra lines in
+the same JSON object: refit_pcl (the PCL-float-refit mode, bit-exact with PCL's arithmetic as
+restated), incl_index_build (the Morton copy + spheres rebuilt every step), secondary (C5).
+cpu_baseline: the PCL-1.8 restatement (oracle) on the box's host cores (16 OpenMP threads for
+countWithinDistance, plus a single-thread sample), rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -40,13 +45,23 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--points", type=int, default=10_000_000, help="points per GPU")
+    ap.add_argument("--points", type=int, default=10_000_000, help="points per GPU (weak scaling)")
+    ap.add_argument("--global-points", type=int, default=0,
+                    help="strong scaling: this many points in all, sharded over the GPUs "
+                         "(BASELINE configs[3], C4: 100M)")
     ap.add_argument("--planes", type=int, default=20)
     ap.add_argument("--hyps", type=int, default=4096)
     ap.add_argument("--threshold", type=float, default=0.02)
     ap.add_argument("--min-inliers", type=int, default=500)
     ap.add_argument("--refit", choices=["fast", "pcl"], default="fast")
-    ap.add_argument("--cpu-hyps", type=int, default=1024, help="hypotheses in the CPU-baseline sample")
+    ap.add_argument("--cpu-hyps", type=int, default=1024,
+                    help="hypotheses in the single-thread CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the all-core CPU leg (the GPU box's CPU share: 16)")
+    ap.add_argument("--pcl-steps", type=int, default=3,
+                    help="steps of the bit-exact PCL-refit line (0: skip)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the PCL-refit, index-build and pruning-work measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--torch-dist", action="store_true",
                     help="rendezvous through torch.distributed even at N=1 (runtime check)")
@@ -144,12 +159,19 @@ def main():
         ctx = D.Context(local)
     ctx.set_profiling(not a.no_events)
 
-    seed = SEED_BASE + 3
+    strong = a.global_points > 0
+    if strong:  # C4: one global cloud sharded over the ranks (last rank takes the remainder)
+        per = a.global_points // world
+        a.points = per + (a.global_points - per * world if rank == world - 1 else 0)
+        id_base = rank * per
+    else:
+        id_base = rank * a.points
+    seed = SEED_BASE + (4 if strong else 3)
     t0 = time.time()
     pts, _, _ = plane_cloud(a.points, a.planes, seed=seed, shard=rank)
     gen_s = time.time() - t0
     t0 = time.perf_counter()
-    cloud = D.Cloud(ctx, pts, id_base=rank * a.points)
+    cloud = D.Cloud(ctx, pts, id_base=id_base)
     ctx.synchronize()
     upload_s = time.perf_counter() - t0
     prm = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
@@ -158,6 +180,7 @@ def main():
 
     # the caller's inlier-id buffer, kept across steps (a C++ caller's std::vector)
     inl_buf = np.empty(a.points * world if prm.gather_inliers else a.points, np.int32)
+    global_points = a.global_points if strong else a.points * world
 
     def step():
         cloud.reset()
@@ -193,24 +216,86 @@ def main():
     score_ms_max = ctx.allreduce_max(score_ms)
 
     value = tests / elapsed / 1e9  # G tests/s, whole job (tests counted over the global cloud)
+    lean_rounds = int(e["stats"]["lean_rounds"])
+    rounds_per_step = int(e["stats"]["rounds"])
+
+    extras = {}
+    if not a.no_extras:
+        def timed_steps(fn, k):
+            ctx.barrier()
+            ctx.synchronize()
+            t = time.perf_counter()
+            out = [fn() for _ in range(k)]
+            ctx.synchronize()
+            ctx.barrier()
+            return out, ctx.allreduce_max(time.perf_counter() - t) / k
+
+        # (1) the bit-exact mode: PCL's float refit (host-sequential sums, two-pass selects)
+        if a.pcl_steps > 0:
+            prm_pcl = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
+                                    refit_mode=D.DLG_REFIT_PCL, hypotheses_per_launch=a.hyps,
+                                    gather_inliers=False)
+
+            def step_pcl():
+                cloud.reset()
+                return D.extract_planes(cloud, prm_pcl, max_planes=a.planes,
+                                        min_inliers=a.min_inliers, out=inl_buf)
+            step_pcl()
+            outs, sec = timed_steps(step_pcl, a.pcl_steps)
+            t_pcl = sum(o["stats"]["tests"] for o in outs) / len(outs)
+            extras["refit_pcl"] = {
+                "mode": "DLG_REFIT_PCL (PCL's float refit, bit-exact with the oracle; "
+                        "two-pass selects, host-sequential sums between them)",
+                "value": round(t_pcl / sec / 1e9, 3), "unit": "G point-plane tests/s",
+                "ms_per_step": round(sec * 1e3, 3), "steps": a.pcl_steps,
+                "planes_extracted": int(outs[-1]["n_planes"])}
+
+        # (2) device-side, including the spatial index (Morton sort + sphere bounds) per step
+        def step_index():
+            cloud.drop_spatial()
+            cloud.build_spatial()
+            return step()
+        step_index()
+        outs, sec = timed_steps(step_index, max(2, min(a.steps, 5)))
+        extras["incl_index_build"] = {
+            "value": round(sum(o["stats"]["tests"] for o in outs) / len(outs) / sec / 1e9, 3),
+            "unit": "G point-plane tests/s", "ms_per_step": round(sec * 1e3, 3),
+            "note": "each step rebuilds the Morton-ordered copy and its bounding spheres from "
+                    "the device-resident cloud (dlg_cloud_drop_spatial + dlg_cloud_build_spatial), "
+                    "then extracts; inputs resident in HBM"}
+
+        # (3) the pruned kernel's actual work (one untimed extraction with its counters on)
+        ctx.set_option(D.DLG_OPT_PRUNE_STATS, 1)
+        ctx.set_profiling(False)
+        ep = step()
+        st = ctx.prune_stats(reset=True)
+        ctx.set_option(D.DLG_OPT_PRUNE_STATS, 0)
+        ctx.set_profiling(not a.no_events)
+        nl = max(int(ep["stats"]["score_launches"]), 1)
+        full_pairs = ep["stats"]["tests_scored"] / world / 32.0  # (tile, plane) pairs if unpruned
+        extras["pruned_work"] = {
+            "pairs_evaluated_per_launch": round(st["pairs"] / nl),
+            "pair_fraction": round(st["pairs"] / max(full_pairs, 1.0), 5),
+            "blocks_per_launch": round(st["blocks"] / nl),
+            "block_fill": round(st["pairs"] / max(32.0 * st["blocks"], 1.0), 4),
+            "redecided_block_fraction": round(st["redecided_blocks"] / max(st["blocks"], 1), 4),
+            "tile_list_entries_per_launch": round(st["list_entries"] / nl),
+            "evaluated_tests_per_step": int(32 * st["pairs"] * world),
+            "note": "(tile, plane) pairs the bounding spheres could not rule out, each scored as "
+                    "32 point tests in a 32x32 bf16 matrix-core block; `value` counts PCL's "
+                    "tests (iterations x active points), the kernel evaluates pair_fraction of them"}
     ms_per_step = elapsed / a.steps * 1e3
-    # dominant kernel: k_score (this rank's launches; tests per rank = scored / world)
+    # dominant kernel: the scoring launch (this rank's launches; tests per rank = scored / world)
     per_rank_tests = scored / world
     avg_launch_ms = score_ms / max(launches, 1)
     ktests_per_s = per_rank_tests / (score_ms / 1e3) if score_ms > 0 else 0.0
-    variant = int(os.environ.get("DLG_SCORE_VARIANT", "19"))
-    pruned = variant == 19 and os.environ.get("DLG_PRUNE", "") != "0" and a.points >= 131072
-    if pruned:
-        kname = ("k_score_pruned (countWithinDistance over the Morton-ordered copy: super-tile and "
-                 "tile bounding spheres rule out (tile, plane) pairs with no possible PCL inlier; "
-                 "the rest as k_score_bf16's 32x32 bf16 matrix-core blocks + exact band "
-                 "re-decision; 4096 hypotheses/launch)")
-    else:
-        kname = {19: "k_score_bf16<8> (countWithinDistance: plane distances on the bf16 matrix "
-                     "cores, exact 3-way split operands; VALU sign count + rounding-band "
-                     "re-decision in PCL op order; 4096 hypotheses/launch)",
-                 5: "k_score<exact,4> (countWithinDistance in PCL op order on the VALU, 4096 "
-                    "hypotheses/launch)"}.get(variant, f"score variant {variant}")
+    pruned = a.points >= 131072  # (the library builds the Morton copy for such clouds)
+    kname = ("k_prune_supers + k_score_tiles_rl (countWithinDistance over the Morton-ordered copy: "
+             "super-tile and tile bounding spheres rule out (tile, plane) pairs with no possible "
+             "PCL inlier; the rest as 32x32 bf16 matrix-core blocks + exact band re-decision; "
+             f"{a.hyps} hypotheses/launch)" if pruned else
+             "k_score_bf16<8> (countWithinDistance on the bf16 matrix cores + exact band "
+             f"re-decision; {a.hyps} hypotheses/launch)")
     # SURVEY 8(d) algorithmic bytes of a scoring launch: the active points once (12 B each) +
     # the hypotheses (32 B plane record + 4 B count); sum over launches / kernel time
     alg_bytes = 12.0 * per_rank_tests / max(a.hyps, 1) + 36.0 * a.hyps * launches
@@ -223,6 +308,7 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": None,
+        "algorithmic_bytes_per_launch": round(alg_bytes / max(launches, 1)),
         "avg_launch_ms": round(avg_launch_ms, 4),
         "launches": launches,
         "tests_per_s_in_kernel": ktests_per_s,
@@ -232,29 +318,28 @@ def main():
         "note": "north-star definition: tests/s against the HBM roofline of streaming each "
                 "active point (12 B) once per 4096-hypothesis launch, i.e. achieved = algorithmic "
                 "bytes (12 B x active points + 36 B x hypotheses per launch) / kernel time vs "
-                "8 TB/s; frac = tests/s / hbm_roofline_tests_per_s.  At 4096 hypotheses per "
-                "pass the launch is not memory-bound (2.7e15 tests/s HBM roof); it is issue/"
-                "latency-bound on the (tile, plane) pairs the bounding spheres cannot rule out "
-                "(DESIGN.md sec. 5).  Kernel time from HIP events on the library's stream.  "
-                "valu_view restates the same tests as PCL's 7 f32 ops each (exceeds the VALU "
-                "peak because the pruned kernel skips the pairs it rules out).  "
-                "memory_bound_passes: the H_pass = 1 passes of each round against HBM",
+                "8 TB/s.  At 4096 hypotheses per pass the launch is not memory-bound (2.7e15 "
+                "tests/s HBM roof): it is issue/latency-bound on the (tile, plane) pairs the "
+                "bounding spheres cannot rule out -- see issue_view (PMC) and pruned_work.  "
+                "Kernel time from HIP events on the library's stream.  traffic: PMC FETCH_SIZE "
+                "(calibrated) + WRITE_SIZE per launch.  memory_bound_passes: the H_pass = 1 "
+                "passes of each round against HBM",
     }
-    # the memory-bound passes of a round (H_pass = 1): fast refit moments (12 B/pt), then
-    # selectWithinDistance + compaction of the list-ordered SoA and of the Morton copy (each: a
-    # 12 B/pt count pass, a 16 B/pt read + 16 B/survivor write scatter; 4 B per inlier id);
-    # timed with HIP events around the phase (incl. the small reduce/refit kernels between)
+    if "pruned_work" in extras:
+        roofline["pruned_work"] = extras.pop("pruned_work")
+    # the memory-bound passes of a round (H_pass = 1), timed with HIP events around the phase
+    # (incl. the small reduce/refit kernels between)
     sum_active = per_rank_tests / max(a.hyps, 1)  # sum over rounds of this rank's active points
-    n_copies = 2 if pruned else 1
-    lean = pruned and world == 1 and os.environ.get("DLG_LEAN", "") != "0" and a.refit == "fast"
+    lean = pruned and lean_rounds == rounds_per_step and a.refit == "fast"
     if lean:
-        # lean-list rounds: moments (12 B/pt) and the single-pass select of the Morton copy (16 B
-        # read, 16 B per survivor, a 1 B stamp per inlier), then the list from the stamps (4 B
-        # index + 1 B stamp read, 4 B per survivor index, 4 + 4 B per inlier id)
+        # lean-list rounds: moments over the Morton copy (12 B/pt), the single-pass select of the
+        # Morton copy (16 B read, 16 B per survivor, a 1 B stamp per inlier), then the list from
+        # the stamps (4 B index + 1 B stamp read, 4 B per survivor index, 4 + 4 B per inlier id)
         sel_bytes = (12.0 * sum_active + 16.0 * sum_active + 16.0 * (sum_active - inliers_local)
                      + 1.0 * inliers_local + 5.0 * sum_active
                      + 4.0 * (sum_active - inliers_local) + 8.0 * inliers_local)
     else:
+        n_copies = 2 if pruned else 1
         sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))
                      + 4.0 * inliers_local)
     sel_gbs = sel_bytes / (select_ms / 1e3) / 1e9 if select_ms > 0 else 0.0
@@ -266,14 +351,28 @@ def main():
         "bound": "hbm", "achieved": round(sel_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(sel_gbs / HBM_PEAK_GBS, 4), "bytes_per_step": round(sel_bytes / a.steps),
         "ms_per_step": round(select_ms / a.steps, 3)}
-    traffic_file = os.path.join(ROOT, "profiles", "score_traffic.json")
-    if os.path.exists(traffic_file):
-        try:
-            tj = json.load(open(traffic_file))
-            roofline["traffic"] = tj.get("hbm_bytes_per_launch")
-            roofline["traffic_source"] = tj.get("source")
-        except Exception:
-            pass
+    # PMC-derived numbers of the same binary and workload (tools/traffic.py, tools/pmc_issue.py
+    # over separate rocprofv3 --pmc passes of `bench.py --steps 1`), when present
+    for fname, key in (("score_traffic.json", "traffic"), ("score_issue.json", "issue_view")):
+        f = os.path.join(ROOT, "profiles", fname)
+        if os.path.exists(f) and a.points == 10_000_000 and not strong:
+            try:
+                tj = json.load(open(f))
+                if key == "traffic":
+                    roofline["traffic"] = tj.get("hbm_bytes_per_launch")
+                    roofline["traffic_source"] = tj.get("source")
+                    if roofline["traffic"]:
+                        roofline["traffic_over_algorithmic"] = round(
+                            roofline["traffic"] / roofline["algorithmic_bytes_per_launch"], 3)
+                else:
+                    roofline["issue_view"] = tj
+                    pw = roofline.get("pruned_work")
+                    vi = tj.get("per_launch", {}).get("SQ_INSTS_VALU")
+                    if pw and vi and pw["blocks_per_launch"]:
+                        # (wave instructions; blocks from the stats run of the same workload)
+                        tj["valu_insts_per_block"] = round(vi / pw["blocks_per_launch"], 1)
+            except Exception:
+                pass
 
     secondary = None
     if world == 1 and not a.no_secondary:
@@ -282,33 +381,60 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O
+        model = platform.processor() or platform.machine()
+        try:
+            for ln in open("/proc/cpuinfo"):
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+        # the all-core leg: the oracle's countWithinDistance over cpu_threads OpenMP threads
+        # (integer sums: the same counts), one full first round of 4096 hypotheses
+        thr = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+        O.set_threads(thr)
         t0 = time.perf_counter()
-        r = O.sac_segment(pts, a.threshold, max_iterations=a.cpu_hyps - 1, probability=1.0)
+        r = O.sac_segment(pts, a.threshold, max_iterations=a.hyps - 1, probability=1.0)
         cdt = time.perf_counter() - t0
+        O.set_threads(1)
+        t1 = time.perf_counter()
+        r1 = O.sac_segment(pts, a.threshold, max_iterations=a.cpu_hyps - 1, probability=1.0)
+        cdt1 = time.perf_counter() - t1
         cpu = {"value": round(r["iterations"] * pts.shape[0] / cdt / 1e9, 4),
-               "unit": "G point-plane tests/s", "cores": 1, "kind": "port",
-               "sample": f"one PCL SACSegmentation::segment (first extraction round) on the same "
-                         f"{pts.shape[0]}-pt cloud with {a.cpu_hyps} hypotheses + refit + select, "
-                         f"oracle/pcl_oracle.c single thread, {cdt:.1f} s",
-               "host_cpu": platform.processor() or platform.machine(),
-               "host_nproc": os.cpu_count()}
+               "unit": "G point-plane tests/s", "cores": thr, "kind": "port",
+               "sample": f"one PCL SACSegmentation::segment (the first extraction round) on the "
+                         f"same {pts.shape[0]}-pt cloud with {a.hyps} hypotheses + refit + select, "
+                         f"oracle/pcl_oracle.c with countWithinDistance over {thr} OpenMP threads, "
+                         f"{cdt:.1f} s",
+               "single_thread": {
+                   "value": round(r1["iterations"] * pts.shape[0] / cdt1 / 1e9, 4), "cores": 1,
+                   "sample": f"the same segment() with {a.cpu_hyps} hypotheses, one thread (PCL "
+                             f"1.8's RANSAC is serial), {cdt1:.1f} s"},
+               "host_cpu": model, "host_nproc": os.cpu_count()}
 
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "G point-plane tests/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "C3: sequential extract-and-remove RANSAC, 10M-pt 20-plane "
-                                   "synthetic cloud per GPU (BASELINE.json configs[2]; C4 shape "
-                                   "when N>1: shards of one cloud, RCCL allreduce of counts)",
-                       "points_per_gpu": a.points, "global_points": a.points * world,
+            "config": {"workload": (
+                           "C4: 100M-pt 20-plane synthetic cloud sharded over the GPUs "
+                           "(BASELINE.json configs[3]), sequential extract-and-remove RANSAC, "
+                           "RCCL allreduce of counts and exact refit moments" if strong else
+                           "C3: sequential extract-and-remove RANSAC, 10M-pt 20-plane synthetic "
+                           "cloud per GPU (BASELINE.json configs[2]; N>1: shards of one cloud, "
+                           "RCCL allreduce of counts and exact refit moments)"),
+                       "points_per_gpu": a.points, "global_points": global_points,
                        "planes": a.planes, "hypotheses_per_round": a.hyps,
                        "threshold": a.threshold, "min_inliers": a.min_inliers,
                        "refit": a.refit, "planes_extracted": planes[-1] if planes else 0,
+                       "lean_rounds": lean_rounds, "rounds": rounds_per_step,
                        "parallelism": f"point-sharded x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            **extras,
             "secondary": secondary,
             "step_ms": [round(x, 2) for x in step_ms],  # this rank's host time per step
             "tests_per_step": tests // max(a.steps, 1),

@@ -28,7 +28,7 @@ SYMBOLS = [
     "dlg_post_process_planes", "dlg_cluster_filter", "dlg_sac_control_create",
     "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
     "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
-    "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex",
+    "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex", "dlg_cloud_drop_spatial",
 ]
 
 # context options (include/dialog_ransac.h): equivalent execution paths, identical results
@@ -115,6 +115,7 @@ def load():
     L.dlg_cloud_destroy.argtypes = [vp]
     L.dlg_cloud_reset.argtypes = [vp]
     L.dlg_cloud_build_spatial.argtypes = [vp, vp]
+    L.dlg_cloud_drop_spatial.argtypes = [vp]
     L.dlg_cloud_active.argtypes = [vp, i64p]
     L.dlg_sac_segment.argtypes = [vp, vp, C.POINTER(SacParams), fp, i32p, C.c_int64, i64p,
                                   C.POINTER(SacStats)]

@@ -381,9 +381,12 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // lean-list round: plane model over the Morton copy, single rank, device refit, a list that
   // is pristine or already lean (a list compacted with coordinates stays on the full path)
   const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
-  const bool lean = compact && !np && !pcl_refit && c->opt.lean && c->comm->world() == 1 &&
-                    cl->sp_valid && cl->sp_n > 0 && cl->n_total < (int64_t(1) << 30) &&
-                    c->opt.prune != 0 && (cl->cur < 0 || cl->buf_lean[cl->cur]);
+  // (any rank count: the fast refit's moments are exact integers, so summing them over the
+  // Morton copies of the shards gives the list's bits; every rank decides alike, as the inputs
+  // of the decision -- spatial copy present, list lean -- evolve identically on every rank)
+  const bool lean = compact && !np && !pcl_refit && c->opt.lean && cl->sp_valid &&
+                    cl->n_total < (int64_t(1) << 30) && c->opt.prune != 0 &&
+                    (cl->cur < 0 || cl->buf_lean[cl->cur]);
   if (!lean) ensure_list_xyz(c, cl);
   const PointsView src = cl->view();
   // the lean list's pristine indices (null while the list is the pristine one)
@@ -462,7 +465,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                             cl->amax[2], c->hyps.p, c->res.p, c->stream);
     } else {
       HIPCHK(hipMemcpyAsync(c->pos.p, hp, 12 * (size_t)D, hipMemcpyHostToDevice, c->stream));
-      launch_gather_samples(c->pos.p, 3 * D, offset, src, c->samples.p, c->stream);
+      if (lean)
+        launch_gather_samples(c->pos.p, 3 * D, offset, cl->pristine.view(cl->n_total),
+                              c->samples.p, c->stream, lidx, src.n);
+      else
+        launch_gather_samples(c->pos.p, 3 * D, offset, src, c->samples.p, c->stream);
       c->comm->allreduce_sum(c->samples.p, 12 * (size_t)D, DType::I32, c->stream);
       launch_build_hyps(c->samples.p, D, cthr, cl->amax[0], cl->amax[1], cl->amax[2], c->hyps.p,
                         c->res.p + Dp, c->stream);
@@ -593,9 +600,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                              c->stream);
       } else {
         if (prm.optimize) {
-          const int nb = moments_blocks(src.n);
+          const PointsView mv = lean ? sp_cur_view() : src;
+          const int nb = moments_blocks(mv.n);
           c->partials.ensure((size_t)nb * kMomDigits);
-          launch_moments(src, bc_dev, mt, cl->qexp, c->partials.p, nb, c->moments.p, c->stream);
+          launch_moments(mv, bc_dev, mt, cl->qexp, c->partials.p, nb, c->moments.p, c->stream);
           // exact integers: the rank sum is the one-rank result, whatever the sharding
           c->comm->allreduce_sum(c->moments.p, kMomDigits, DType::I64, c->stream);
         }
@@ -1145,6 +1153,31 @@ dlg_status dlg_cloud_build_spatial(dlg_ctx* c, dlg_cloud* cl) {
     if (cl->cur >= 0) throw DlgError(DLG_ERR_INVALID, "build the spatial copy before extracting (or after dlg_cloud_reset)");
     build_spatial(c, cl);
   });
+}
+
+dlg_status dlg_cloud_drop_spatial(dlg_cloud* cl) {
+  if (!cl) return DLG_ERR_INVALID;
+  if (cl->ctx) {
+    (void)hipSetDevice(cl->ctx->device);
+    (void)hipStreamSynchronize(cl->ctx->stream);
+  }
+  cl->sp_pristine.release();
+  cl->sp_buf[0].release();
+  cl->sp_buf[1].release();
+  cl->sp_tiles_pr.release();
+  cl->sp_supers_pr.release();
+  cl->sp_order.release();
+  for (int b = 0; b < 2; ++b) {
+    cl->sp_tb[b].release();
+    cl->sp_sb[b].release();
+  }
+  cl->sp_built = cl->sp_valid = false;
+  cl->sp_n = cl->sp_n_pristine = 0;
+  cl->cur = -1;  // (a lean list needs the Morton copy: back to the pristine list)
+  cl->n_active = cl->n_total;
+  cl->sp_cur = -1;
+  cl->sp_dirty = false;
+  return DLG_OK;
 }
 
 dlg_status dlg_cloud_reset(dlg_cloud* cl) {

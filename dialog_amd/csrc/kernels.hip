@@ -35,15 +35,19 @@ __device__ __forceinline__ bool model_in(const PointsView& src, int64_t e, float
 }
 
 // ---------------------------------------------------------------------------------------------
+// lidx (lean lists): the list holds pristine indices only; src = the pristine copy, n_list the
+// list length
 __global__ void k_gather_samples(const int32_t* __restrict__ pos, int m, int64_t lo,
-                                 PointsView src, SampleRec* __restrict__ out) {
+                                 PointsView src, const int32_t* __restrict__ lidx, int64_t n_list,
+                                 SampleRec* __restrict__ out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   int64_t p = (int64_t)pos[i] - lo;
   SampleRec r;
   r.gid = 0; r.x = 0.0f; r.y = 0.0f; r.z = 0.0f;
-  if (p >= 0 && p < src.n) {
-    r.gid = src.gid[p]; r.x = src.x[p]; r.y = src.y[p]; r.z = src.z[p];
+  if (p >= 0 && p < n_list) {
+    const int64_t q = lidx ? lidx[p] : p;
+    r.gid = src.gid[q]; r.x = src.x[q]; r.y = src.y[q]; r.z = src.z[q];
   }
   out[i] = r;
 }
@@ -1177,9 +1181,10 @@ __global__ void k_absmax(PointsView src, uint32_t* __restrict__ out4) {
 static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
 void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
-                           hipStream_t s) {
+                           hipStream_t s, const int32_t* lidx, int64_t n_list) {
   if (m <= 0) return;
-  hipLaunchKernelGGL(k_gather_samples, dim3(cdiv(m, 256)), dim3(256), 0, s, pos, m, lo, src, out);
+  hipLaunchKernelGGL(k_gather_samples, dim3(cdiv(m, 256)), dim3(256), 0, s, pos, m, lo, src, lidx,
+                     lidx || n_list ? n_list : src.n, out);
 }
 
 void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleRec* samples,

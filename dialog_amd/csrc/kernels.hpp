@@ -77,8 +77,11 @@ enum ScoreKernel { kScoreExact = 0, kScoreBf16 = 1, kScorePruned = 2 };
 constexpr size_t kHypScratchBytes =
     kMaxHypPerLaunch * (sizeof(HypRec) + sizeof(float4) + sizeof(float) + 4 * sizeof(uint4) +
                         sizeof(float2));
+// positions pos[m] (global list positions; this rank's list starts at lo) -> SampleRecs (zero
+// when another rank owns the position).  Lean lists: lidx = the list's pristine indices (null
+// while the list is the pristine one), src = the pristine copy, n_list = the list length.
 void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src, SampleRec* out,
-                           hipStream_t s);
+                           hipStream_t s, const int32_t* lidx = nullptr, int64_t n_list = 0);
 // writes hyps[D] and good[D] (int32 flags next to the counts for one D2H copy)
 // round results into the coherent pinned buffer pub (layout below), then pub[0] = seq (release,
 // system scope)

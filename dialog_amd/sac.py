@@ -167,6 +167,10 @@ class Cloud:
         """Morton-ordered copy for the pruned scoring kernel (automatic for >= 131072 points)."""
         self.ctx.check(self.ctx._L.dlg_cloud_build_spatial(self.ctx.h, self.h))
 
+    def drop_spatial(self):
+        """release the Morton copy (resets the cloud); build_spatial() builds it again."""
+        self.ctx.check(self.ctx._L.dlg_cloud_drop_spatial(self.h))
+
     def reset(self):
         self.ctx.check(self.ctx._L.dlg_cloud_reset(self.h))
 

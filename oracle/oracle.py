@@ -67,6 +67,10 @@ def lib():
         L.orc_fast_qexp.restype = C.c_int
         L.orc_refit_exact.argtypes = [fp, C.c_int64, i32p, C.c_int64, C.c_int, fp, fp]
         L.orc_refit_exact.restype = C.c_int
+        L.orc_mom_digits.argtypes = [fp, C.c_int64, i32p, C.c_int64, C.c_int, i64p]
+        L.orc_mom_digits.restype = None
+        L.orc_refit_digits.argtypes = [i64p, C.c_int, fp, fp]
+        L.orc_refit_digits.restype = C.c_int
         L.orc_plane_sample_good.argtypes = [fp, fp, fp]
         L.orc_thr_ceil.argtypes = [C.c_double]
         L.orc_thr_ceil.restype = C.c_float
@@ -141,6 +145,24 @@ def refit_exact(points, indices, coeff_in, qexp):
     ci = np.ascontiguousarray(coeff_in, np.float32)
     co = np.zeros(4, np.float32)
     lib().orc_refit_exact(_f(p), stride, _i32(idx), idx.shape[0], int(qexp), _f(ci), _f(co))
+    return co
+
+
+def mom_digits(points, indices, qexp):
+    """the fast refit's 25 int64 moment digits of points[indices] (sums over disjoint sets add)"""
+    p, stride = _xyz(points)
+    idx = np.ascontiguousarray(indices, np.int32)
+    d = np.zeros(25, np.int64)
+    lib().orc_mom_digits(_f(p), stride, _i32(idx), idx.shape[0], int(qexp),
+                         d.ctypes.data_as(C.POINTER(C.c_int64)))
+    return d
+
+
+def refit_digits(digits, coeff_in, qexp):
+    d = np.ascontiguousarray(digits, np.int64)
+    ci = np.ascontiguousarray(coeff_in, np.float32)
+    co = np.zeros(4, np.float32)
+    lib().orc_refit_digits(d.ctypes.data_as(C.POINTER(C.c_int64)), int(qexp), _f(ci), _f(co))
     return co
 
 

@@ -516,19 +516,41 @@ int orc_fast_qexp(const float* xyz, int64_t stride, const int32_t* idx, int64_t 
   return e;
 }
 
-int orc_refit_exact(const float* xyz, int64_t stride, const int32_t* idx, int64_t n, int qexp,
-                    const float cin[4], float cout[4]) {
-  if (n < 4) { memcpy(cout, cin, 4 * sizeof(float)); return 0; }
+/* the product's moment digits (exact_refit.hpp layout) of the points idx[0..n) */
+void orc_mom_digits(const float* xyz, int64_t stride, const int32_t* idx, int64_t n, int qexp,
+                    int64_t d[25]) {
   const double scale = ldexp(1.0, 48 - qexp);
-  __int128 L[3] = {0, 0, 0}, P[6] = {0, 0, 0, 0, 0, 0};
+  memset(d, 0, 25 * sizeof(int64_t));
+  static const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
   for (int64_t i = 0; i < n; ++i) {
     const float* p = xyz + (int64_t)idx[i] * stride;
     int64_t q[3];
     for (int a = 0; a < 3; ++a) q[a] = (int64_t)((double)p[a] * scale);
-    for (int a = 0; a < 3; ++a) L[a] += q[a];
-    P[0] += (__int128)q[0] * q[0]; P[1] += (__int128)q[0] * q[1]; P[2] += (__int128)q[0] * q[2];
-    P[3] += (__int128)q[1] * q[1]; P[4] += (__int128)q[1] * q[2]; P[5] += (__int128)q[2] * q[2];
+    d[0] += 1;
+    for (int a = 0; a < 3; ++a) {
+      d[1 + 2 * a] += q[a] & 0xFFFFFFFFll;
+      d[2 + 2 * a] += q[a] >> 32;   /* arithmetic shift (gcc) */
+    }
+    for (int k = 0; k < 6; ++k) {
+      __int128 pr = (__int128)q[ia[k]] * q[ib[k]];
+      unsigned __int128 u = (unsigned __int128)pr;
+      d[7 + 3 * k] += (int64_t)(uint64_t)(u & 0xFFFFFFFFull);
+      d[8 + 3 * k] += (int64_t)(uint64_t)((u >> 32) & 0xFFFFFFFFull);
+      d[9 + 3 * k] += (int64_t)(pr >> 64);
+    }
   }
+}
+
+/* the refit from summed digits (any split of the points over ranks gives the same sums) */
+int orc_refit_digits(const int64_t d[25], int qexp, const float cin[4], float cout[4]) {
+  const int64_t n = d[0];
+  if (n < 4) { memcpy(cout, cin, 4 * sizeof(float)); return 0; }
+  __int128 L[3], P[6];
+  const __int128 two32 = (__int128)1 << 32, two64 = (__int128)1 << 64;  /* (no shifts of
+                                                                          negatives: UB in C) */
+  for (int a = 0; a < 3; ++a) L[a] = (__int128)d[2 + 2 * a] * two32 + d[1 + 2 * a];
+  for (int k = 0; k < 6; ++k)
+    P[k] = (__int128)d[9 + 3 * k] * two64 + (__int128)d[8 + 3 * k] * two32 + d[7 + 3 * k];
   static const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
   double m6[6];
   for (int k = 0; k < 6; ++k) {
@@ -548,9 +570,16 @@ int orc_refit_exact(const float* xyz, int64_t stride, const int32_t* idx, int64_
   double c0 = orc_i256_to_double(orc_i256_from_i128(L[0])) / nd * back;
   double c1 = orc_i256_to_double(orc_i256_from_i128(L[1])) / nd * back;
   double c2 = orc_i256_to_double(orc_i256_from_i128(L[2])) / nd * back;
-  double d = -((v0 * c0 + v1 * c1) + v2 * c2);
-  cout[0] = (float)v0; cout[1] = (float)v1; cout[2] = (float)v2; cout[3] = (float)d;
+  double dd = -((v0 * c0 + v1 * c1) + v2 * c2);
+  cout[0] = (float)v0; cout[1] = (float)v1; cout[2] = (float)v2; cout[3] = (float)dd;
   return 1;
+}
+
+int orc_refit_exact(const float* xyz, int64_t stride, const int32_t* idx, int64_t n, int qexp,
+                    const float cin[4], float cout[4]) {
+  int64_t d[25];
+  orc_mom_digits(xyz, stride, idx, n, qexp, d);
+  return orc_refit_digits(d, qexp, cin, cout);
 }
 
 /* optimizeModelCoefficients (sac_model_plane.hpp): < 4 inliers keep the coefficients; else

@@ -55,6 +55,11 @@ int  orc_refit_double(const float* xyz, int64_t stride, const int32_t* idx, int6
 int  orc_fast_qexp(const float* xyz, int64_t stride, const int32_t* idx, int64_t n);
 int  orc_refit_exact(const float* xyz, int64_t stride, const int32_t* idx, int64_t n, int qexp,
                      const float coeff_in[4], float coeff_out[4]);
+/* its two halves: the 25 int64 moment digits of a point set (exact_refit.hpp layout; digit sums
+ * of disjoint sets add), and the refit from summed digits (the multi-rank protocol) */
+void orc_mom_digits(const float* xyz, int64_t stride, const int32_t* idx, int64_t n, int qexp,
+                    int64_t digits[25]);
+int  orc_refit_digits(const int64_t digits[25], int qexp, const float coeff_in[4], float coeff_out[4]);
 /* threads of countWithinDistance (OpenMP; default 1 = PCL's serial loop) */
 void orc_set_threads(int n);
 int  orc_get_threads(void);

@@ -2,19 +2,30 @@
 SURVEY.md §8(e) run by world_size CPU processes over torch.distributed `gloo`.
 
 Every rank drives the product's host controller (dialog_amd.RansacControl = dlg_sac_control_*,
-the same replay dlg_sac_segment runs between its kernels) on the global active count, and does
-per rank what the library does per GPU, with the oracle standing in for the device kernels
-(test infrastructure):
+the replay dlg_extract_planes runs between its kernels) on the global active count, and issues
+exactly the collectives the library issues per GPU (driver.cpp), in the same order
+and with the same types and sizes, with the oracle standing in for the device kernels (test
+infrastructure):
 
-  * rank r holds a contiguous block of the global list (ascending global ids);
-  * draws: the controller's global list positions -> the owning rank contributes the point, the
-    others zeros, summed as int32 bit patterns (allreduce; exact, keeps -0.0) -- k_gather_samples;
-  * isSampleGood + coefficients (oracle; k_build_hyps), inlier counts on the local shard
-    (oracle; k_score) -> allreduce(sum) of int32[D] -> RansacControl.consume;
-  * PCL refit: the unrefined inliers' xyz gathered in rank order (= PCL's list order) and summed
-    sequentially in float; final select on each shard, gathered in rank order; compaction local.
+  once per extraction:
+    allgather int64[1]            every rank's active count (allgather_i64)
+    allreduce-max f64[1]          fast refit: the cloud's largest finite |coordinate| (its quantum;
+                                  once per cloud)
+  per round, per batch of D draws:
+    allreduce-sum int32[12 D]     the draws' SampleRecs {gid, x, y, z} as int32 bit patterns: the
+                                  owning rank contributes, the others zeros (k_gather_samples)
+    allreduce-sum int32[D]        inlier counts of the rank's shard (k_score)
+  per round, refit:
+    pcl : allgather int64[1] + padded allgather int32[3 m]   the unrefined inliers' xyz in rank
+          order (= PCL's list order), summed sequentially in float on every rank
+    fast: allreduce-sum int64[25] the exact moment digits (exact_refit.hpp)
+  per round, select:
+    allgather int32[2]            every rank's (inliers, survivors): the next round's counts
+  per accepted plane (gather_inliers):
+    allgather int64[1] + padded allgather int32[m]           the inlier ids in rank order
 
-The result must equal the single-process PCL restatement (oracle.extract_planes) bit for bit.
+Each rank logs (op, dtype, count) of every collective; the test checks the logs are identical
+across ranks and that the result equals the single-process restatement bit for bit.
 """
 from __future__ import annotations
 
@@ -27,19 +38,41 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
-def _allgather_var(dist, torch, arr, dtype):
-    """rank-ordered concatenation of variable-length 1-D arrays (padded all_gather)."""
-    n = torch.tensor([arr.shape[0]], dtype=torch.int64)
-    world = dist.get_world_size()
-    ns = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(ns, n)
-    ns = [int(v.item()) for v in ns]
-    m = max(max(ns), 1)
-    buf = torch.zeros(m, dtype=dtype)
-    buf[:arr.shape[0]] = torch.from_numpy(arr)
-    outs = [torch.zeros(m, dtype=dtype) for _ in range(world)]
-    dist.all_gather(outs, buf)
-    return np.concatenate([o[:k].numpy() for o, k in zip(outs, ns)]), ns
+class Coll:
+    """the collectives of comm.cpp over gloo, logged"""
+
+    def __init__(self, dist, torch):
+        self.dist, self.torch, self.log = dist, torch, []
+
+    def allreduce_sum(self, arr):
+        self.log.append(("allreduce_sum", str(arr.dtype), int(arr.size)))
+        t = self.torch.from_numpy(np.ascontiguousarray(arr).copy())
+        self.dist.all_reduce(t)
+        return t.numpy()
+
+    def allreduce_max_f64(self, v):
+        self.log.append(("allreduce_max", "float64", 1))
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allgather(self, arr):
+        self.log.append(("allgather", str(arr.dtype), int(arr.size)))
+        t = self.torch.from_numpy(np.ascontiguousarray(arr).copy())
+        outs = [self.torch.zeros_like(t) for _ in range(self.dist.get_world_size())]
+        self.dist.all_gather(outs, t)
+        return np.stack([o.numpy() for o in outs])
+
+    def gather_lists(self, arr, width):
+        """driver.cpp gather_lists: counts by allgather_i64, then one padded allgather"""
+        cnt = self.allgather(np.array([arr.size // width], np.int64))[:, 0]
+        m = int(cnt.max())
+        if m == 0:
+            return arr[:0]
+        buf = np.zeros(m * width, arr.dtype)
+        buf[:arr.size] = arr
+        g = self.allgather(buf)
+        return np.concatenate([g[r, :cnt[r] * width] for r in range(len(cnt))])
 
 
 def _pcl_refit(O, xyz, coeff):
@@ -54,7 +87,7 @@ def _pcl_refit(O, xyz, coeff):
 
 
 def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, min_inliers,
-        max_iterations, probability, batch, sizes):
+        max_iterations, probability, batch, sizes, refit="pcl", gather=True):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -67,48 +100,56 @@ def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, m
     from oracle import numpy_twin as T
     from oracle import oracle as O
 
+    cc = Coll(dist, torch)
     pts, _, _ = plane_cloud(n_points, n_planes, seed=913)   # the global cloud (host copy)
     bounds = np.concatenate([[0], np.cumsum(sizes)])
-    local = np.arange(bounds[rank], bounds[rank + 1], dtype=np.int32)  # active global ids
+    mine_ids = np.arange(bounds[rank], bounds[rank + 1], dtype=np.int32)
+    local = mine_ids.copy()                                  # active global ids, list order
     prm = D.make_params(threshold, max_iterations=max_iterations, probability=probability,
-                        hypotheses_per_launch=batch)
+                        hypotheses_per_launch=batch,
+                        refit_mode=D.DLG_REFIT_FAST if refit == "fast" else D.DLG_REFIT_PCL)
     coeffs, inliers, offsets, decisions = [], [], [0], []
     floor_n = max(3, min_inliers)
+    active = cc.allgather(np.array([local.shape[0]], np.int64))[:, 0]
+    qexp = None
     while len(coeffs) < max_planes:
-        # allgather of n_active -> global N and this rank's offset in the global list
-        na, ns = _allgather_var(dist, torch, np.array([local.shape[0]], np.int64), torch.int64)
-        N = int(na.sum())
-        offset = int(na[:rank].sum())
+        N = int(active.sum())
+        offset = int(active[:rank].sum())
         if N < floor_n:
             break
+        if refit == "fast" and qexp is None and world > 1:
+            # the cloud's global quantum, before the first round's draws (driver.cpp segment_impl)
+            fin_pts = pts[mine_ids][np.isfinite(pts[mine_ids]).all(axis=1)]
+            f = float(np.abs(fin_pts).max()) if fin_pts.size else 0.0
+            qexp = int(np.frexp(cc.allreduce_max_f64(f))[1])
         ctl = D.RansacControl(prm, N, batch)
         best_coeff = None
+        shard = np.ascontiguousarray(pts[local])
         while True:
             pos = ctl.next()
             if pos.shape[0] == 0:
                 break
             Dn = pos.shape[0]
-            # k_gather_samples: owner contributes, int32 bit-pattern sum across ranks
-            smp = np.zeros((Dn, 3, 3), np.float32)
+            # k_gather_samples: SampleRec {gid, x, y, z}, owner contributes, int32 bit patterns
+            rec = np.zeros((Dn, 3, 4), np.int32)
             mine = (pos >= offset) & (pos < offset + local.shape[0])
-            smp[mine] = pts[local[pos[mine] - offset]]
-            t = torch.from_numpy(smp.view(np.int32).copy())
-            dist.all_reduce(t)
-            smp = t.numpy().view(np.float32)
+            g = local[pos[mine] - offset]
+            rec[mine, 0] = g
+            rec[mine, 1:] = pts[g].view(np.int32)
+            rec = cc.allreduce_sum(rec.reshape(-1)).reshape(Dn, 3, 4)
+            smp = np.ascontiguousarray(rec[:, :, 1:]).view(np.float32)
             # k_build_hyps + k_score on the local shard, allreduce of the counts
             good = np.zeros(Dn, np.int32)
             cnt = np.zeros(Dn, np.int32)
             hyp = np.zeros((Dn, 4), np.float32)
-            shard = np.ascontiguousarray(pts[local])
             for d in range(Dn):
                 ok, c = O.plane_coefficients(smp[d, 0], smp[d, 1], smp[d, 2])
                 good[d] = int(ok)
                 hyp[d] = c
                 if ok:
                     cnt[d] = O.count_within(shard, c, threshold) if shard.shape[0] else 0
-            t = torch.from_numpy(cnt.copy())
-            dist.all_reduce(t)
-            b, fin = ctl.consume(t.numpy(), good)
+            cnt = cc.allreduce_sum(cnt)
+            b, fin = ctl.consume(cnt, good)
             if b >= 0:
                 best_coeff = hyp[b].copy()
             if fin:
@@ -118,21 +159,29 @@ def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, m
         if best_coeff is None:
             break
         decisions.append((res["iterations"], res["draws"], res["n_unrefined"], res["best_draw"]))
-        shard = np.ascontiguousarray(pts[local])
         sel = T.within(best_coeff, shard, threshold) if shard.shape[0] else np.zeros(0, bool)
-        xyz, _ = _allgather_var(dist, torch, shard[sel].reshape(-1).copy(), torch.float32)
-        refined = _pcl_refit(O, xyz.reshape(-1, 3), best_coeff)
+        if refit == "pcl":
+            xyz = cc.gather_lists(shard[sel].reshape(-1).view(np.int32).copy(), 3)
+            refined = _pcl_refit(O, xyz.view(np.float32).reshape(-1, 3), best_coeff)
+        else:
+            dig = O.mom_digits(pts, local[sel], qexp) if sel.any() else np.zeros(25, np.int64)
+            dig = cc.allreduce_sum(dig)
+            refined = O.refit_digits(dig, best_coeff, qexp)
         sel = T.within(refined, shard, threshold) if shard.shape[0] else np.zeros(0, bool)
-        ids, _ = _allgather_var(dist, torch, local[sel].copy(), torch.int32)
-        if ids.shape[0] == 0 or ids.shape[0] < min_inliers:
+        rk = cc.allgather(np.array([int(sel.sum()), int((~sel).sum())], np.int32))
+        n_in = int(rk[:, 0].sum())
+        if n_in == 0 or n_in < min_inliers:
             break
+        ids = cc.gather_lists(local[sel].copy(), 1) if gather else local[sel].copy()
         coeffs.append(refined)
         inliers.append(ids)
-        offsets.append(offsets[-1] + ids.shape[0])
+        offsets.append(offsets[-1] + n_in)
         local = local[~sel]                     # local compaction, order kept
+        active = rk[:, 1].astype(np.int64)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"),
              coeffs=np.array(coeffs, np.float32).reshape(-1, 4),
              inliers=np.concatenate(inliers).astype(np.int32) if inliers else np.zeros(0, np.int32),
-             offsets=np.array(offsets, np.int64), decisions=np.array(decisions, np.int64))
+             offsets=np.array(offsets, np.int64), decisions=np.array(decisions, np.int64),
+             log=np.array([f"{o}:{t}:{n}" for o, t, n in cc.log]))
     dist.barrier()
     dist.destroy_process_group()

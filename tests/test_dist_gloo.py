@@ -33,25 +33,54 @@ def _entry(rank, world, port, out_dir, kw):
     dist_protocol.run(rank, world, port, out_dir, **kw)
 
 
-@pytest.mark.parametrize("world,sizes", [(2, None), (3, [1500, 4000, 500])],
-                         ids=["ws2-even", "ws3-ragged"])
-def test_sharded_extract_gloo(tmp_path, world, sizes):
+@pytest.mark.parametrize("world,sizes,refit", [(2, None, "pcl"), (3, [1500, 4000, 500], "pcl"),
+                                               (2, None, "fast"), (4, [0, 2500, 2000, 1500], "fast")],
+                         ids=["ws2-even-pcl", "ws3-ragged-pcl", "ws2-even-fast", "ws4-empty-rank-fast"])
+def test_sharded_extract_gloo(tmp_path, world, sizes, refit):
     n = 6000
     if sizes is None:
         sizes = [n // world] * world
         sizes[-1] += n - sum(sizes)
     kw = dict(n_points=n, n_planes=3, threshold=0.02, max_planes=4, min_inliers=50,
-              max_iterations=120, probability=0.99, batch=64, sizes=sizes)
+              max_iterations=120, probability=0.99, batch=64, sizes=sizes, refit=refit)
     mp.start_processes(_entry, args=(world, _port(), str(tmp_path), kw), nprocs=world,
                        join=True, start_method="spawn")
     outs = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
-    for o in outs[1:]:   # identical decisions and results on every rank
-        for k in ("coeffs", "inliers", "offsets", "decisions"):
+    for o in outs[1:]:   # identical decisions, results and collective sequence on every rank
+        for k in ("coeffs", "inliers", "offsets", "decisions", "log"):
             assert np.array_equal(o[k], outs[0][k]), k
+    # the driver's sequence: one active-count allgather, [the quantum], then per
+    # round samples + counts per batch, the refit exchange, the (in, out) allgather, the ids
+    log = [tuple(e.split(":")) for e in outs[0]["log"]]
+    assert log[0] == ("allgather", "int64", "1")
+    i = 1
+    if refit == "fast":
+        assert log[1] == ("allreduce_max", "float64", "1")
+        i = 2
+    rounds = 0
+    while i < len(log):
+        assert log[i][0] == "allreduce_sum" and log[i][1] == "int32"
+        d = int(log[i][2]) // 12
+        while log[i][:2] == ("allreduce_sum", "int32") and int(log[i][2]) % 12 == 0 and \
+                log[i + 1] == ("allreduce_sum", "int32", str(int(log[i][2]) // 12)):
+            i += 2  # one batch: samples (12 D int32), counts (D int32)
+        assert d > 0
+        if refit == "fast":
+            assert log[i] == ("allreduce_sum", "int64", "25")
+            i += 1
+        else:
+            assert log[i] == ("allgather", "int64", "1") and log[i + 1][:2] == ("allgather", "int32")
+            i += 2
+        assert log[i] == ("allgather", "int32", "2")
+        i += 1
+        if i < len(log) and log[i] == ("allgather", "int64", "1"):  # accepted plane: its ids
+            i += 2 if i + 1 < len(log) and log[i + 1][:2] == ("allgather", "int32") else 1
+        rounds += 1
+    assert rounds >= 3
     from dialog_amd.synth import plane_cloud
     pts, _, _ = plane_cloud(n, 3, seed=913)
     ref = O.extract_planes(pts, 0.02, max_planes=4, min_inliers=50, max_iterations=120,
-                           probability=0.99)
+                           probability=0.99, refit=refit)
     got = outs[0]
     assert ref["n_planes"] >= 3 and got["coeffs"].shape[0] == ref["n_planes"]
     assert np.array_equal(got["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))

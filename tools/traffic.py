@@ -2,9 +2,11 @@
 runs of `bench.py --steps 1 --warmup 0` (separate passes, as MI355X_MICROARCH.md prescribes).
 
 FETCH_SIZE/WRITE_SIZE are in KB (1024 B).  gfx950 counts exactly half of the bytes of a wide
-(16 B/lane) coalesced read; other widths are uncalibrated, so the factor for our 4-B/lane SoA
-reads is measured here on k_select_count, whose algorithmic read is known exactly
-(12 B per active point, read once).  Writes -> profiles/score_traffic.json.
+(16 B/lane) coalesced read; other widths are uncalibrated (MI355X_MICROARCH.md: calibrate on a
+known byte count in your own access pattern), so the factor for our 4-B/lane SoA reads is
+measured here on k_absmax, which reads x, y, z of every uploaded point exactly once (12 B per
+point, the same 4-B/lane pattern as the scoring kernel's point loads).  Writes ->
+profiles/score_traffic.json.
 """
 import collections
 import csv
@@ -42,15 +44,13 @@ def main():
         if k in write:
             w = [v for _, v, _ in write[k]]
             res[k]["write_bytes_mean"] = 1024 * sum(w) / len(w)
-    # calibration on k_select_count: grid = tiles * 256 threads, 4096 points per tile
-    sc = sorted(fetch.get("k_select_count", []))
+    # calibration on k_absmax (upload: 12 B per point, read once, 4-B lane loads)
+    ab = sorted(fetch.get("k_absmax", []))
     cal = None
-    if sc:
-        # first launch of a step runs on the full cloud: 12 B per point
-        n = bench["config"]["points_per_gpu"] if bench else None
-        if n:
-            cal = (12.0 * n) / (1024 * sc[0][1])
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, bench.py --steps 1 --warmup 0",
+    if ab and bench:
+        cal = (12.0 * bench["config"]["points_per_gpu"]) / (1024 * ab[0][1])
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py --steps 1 "
+                     "--warmup 0; reads x calibration (k_absmax: 12 B/point)",
            "kernels": res, "read_calibration_dword_loads": cal}
     # one scoring launch = k_prune_supers + k_score_tiles (pruned, default), else the exhaustive kernel
     keys = [k for k in ("k_prune_supers", "k_score_tiles_rl", "k_score_tiles") if k in res][:2] or \
