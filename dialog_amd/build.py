@@ -17,8 +17,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdialog_amd.so")
 SOURCES = ["kernels.hip", "spatial.hip", "normals.hip", "postprocess.hip", "comm.cpp", "driver.cpp", "sac_control.cpp",
            "normals_host.cpp", "postprocess_host.cpp"]
-HEADERS = ["kernels.hpp", "spatial.hpp", "dev_common.hpp", "sac_control.hpp", "normals.hpp", "comm.hpp", "driver.hpp", "host_math.hpp", "grid_host.hpp",
-           "pp_math.hpp", "postprocess.hpp", "grid_dev.hpp", "np_dev.hpp"]
+# every header under csrc/ (a header change rebuilds every object: no per-file dependency scan)
+HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp") or f.endswith(".h"))
 ARCH = os.environ.get("DLG_OFFLOAD_ARCH", "gfx950")
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",

@@ -345,6 +345,12 @@ void ensure_sel1(dlg_ctx* c, int64_t n) {
   c->sel1.err = c->sel1_err.p;
 }
 
+void ensure_mom_done(dlg_ctx* c) {
+  if (c->mom_done.p) return;
+  c->mom_done.ensure(1);
+  HIPCHK(hipMemsetAsync(c->mom_done.p, 0, sizeof(unsigned), c->stream));
+}
+
 // one SACSegmentation::segment() over the cloud's active list (all ranks)
 // active_ranks: every rank's active count when the caller already knows it (the extract loop
 // carries it from the previous round's survivors), else allgathered here
@@ -591,22 +597,29 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       HIPCHK(hipEventRecord(c->ev_sel[sk][0], c->stream));
     }
     if (!pcl_refit) {
-      if (prm.optimize && c->comm->world() == 1) {
-        // (lean: the moments of the Morton copy -- the same finite inliers)
+      const bool one = c->comm->world() == 1;
+      if (prm.optimize) {
+        // (lean: the moments of the Morton copy -- the same finite inliers -- over the tiles
+        // whose sphere may hold one; one rank: the refit in the same launch)
         const PointsView mv = lean ? sp_cur_view() : src;
-        const int nb = moments_blocks(mv.n);
+        const int nb = lean ? moments_sp_blocks(mv.n) : moments_blocks(mv.n);
         c->partials.ensure((size_t)nb * kMomDigits);
-        launch_moments_refit(mv, bc_dev, mt, cl->qexp, c->partials.p, nb, c->moments.p, rc_dev,
-                             c->stream);
-      } else {
-        if (prm.optimize) {
-          const PointsView mv = lean ? sp_cur_view() : src;
-          const int nb = moments_blocks(mv.n);
-          c->partials.ensure((size_t)nb * kMomDigits);
-          launch_moments(mv, bc_dev, mt, cl->qexp, c->partials.p, nb, c->moments.p, c->stream);
-          // exact integers: the rank sum is the one-rank result, whatever the sharding
-          c->comm->allreduce_sum(c->moments.p, kMomDigits, DType::I64, c->stream);
+        ensure_mom_done(c);
+        if (lean) {
+          const SpatialView sv = spatial_view(cl);
+          launch_moments_sp(mv, sv.tiles, sv.supers, pmargin, bc_dev, mt, cl->qexp, c->partials.p,
+                            c->mom_done.p, nb, c->moments.p, one ? rc_dev : nullptr, c->stream);
+        } else if (one) {
+          launch_moments_refit(mv, bc_dev, mt, cl->qexp, c->partials.p, c->mom_done.p, nb,
+                               c->moments.p, rc_dev, c->stream);
+        } else {
+          launch_moments(mv, bc_dev, mt, cl->qexp, c->partials.p, c->mom_done.p, nb,
+                         c->moments.p, c->stream);
         }
+      }
+      if (!(prm.optimize && one)) {
+        // exact integers: the rank sum is the one-rank result, whatever the sharding
+        if (prm.optimize) c->comm->allreduce_sum(c->moments.p, kMomDigits, DType::I64, c->stream);
         launch_refit_moments(c->moments.p, cl->qexp, bc_dev, prm.optimize, rc_dev, c->stream);
       }
     } else {

@@ -181,6 +181,7 @@ struct dlg_ctx {
   DevBuf<uint64_t> sel1_status;
   DevBuf<int32_t> sel1_err;  // sticky look-back failure word of the single-pass selects
   DevBuf<int64_t> partials, moments;  // fast refit: exact moment digits (exact_refit.hpp)
+  DevBuf<unsigned> mom_done;           // k_moments' last-workgroup counter (zero between launches)
   DevBuf<double> scratch_f64;          // max-allreduce of host doubles
   DevBuf<int32_t> inl_gid;
   DevBuf<float> inl_xyz;

@@ -13,6 +13,7 @@
 //   SampleConsensusModelPlane::isSampleGood + computeModelCoefficients -> k_build_hyps
 //   computeMeanAndCovarianceMatrix (fast mode, double)  -> k_moments
 #include "kernels.hpp"
+#include "spatial.hpp"
 #include "dev_common.hpp"
 #include "np_dev.hpp"
 #include "host_math.hpp"
@@ -412,18 +413,126 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
   return v;
 }
 
-template <bool NP>
+// the fast refit from summed digits s_m (LDS) by the first wave: lanes 0..8 evaluate the nine
+// correctly rounded entries (refit_entry) in parallel, lane 0 finishes (Jacobi, orientation,
+// centre); bit-identical to refit_exact.  < 4 inliers or optimize off keep the unrefined plane.
+__device__ __forceinline__ void refit_wave0(const int64_t* s_m, int qexp,
+                                            const float4* __restrict__ cin, int optimize,
+                                            float4* __restrict__ cout) {
+  __shared__ double s_e[9];
+  const int t = threadIdx.x;
+  const bool go = optimize && s_m[0] >= 4;
+  if (go && t < 9) s_e[t] = refit_entry(s_m, t);
+  __syncthreads();
+  if (t != 0) return;
+  const float4 c = *cin;
+  const float ci[4] = {c.x, c.y, c.z, c.w};
+  float co[4] = {c.x, c.y, c.z, c.w};
+  if (go) {
+    double e[9];
+    for (int k = 0; k < 9; ++k) e[k] = s_e[k];
+    refit_finish(e, s_m[0], qexp, ci, co);
+  }
+  *cout = make_float4(co[0], co[1], co[2], co[3]);
+}
+
+// the grid's digit sums: partials [kMomDigits][nb] (digit-major) -> s_m.  Thread t < 31 * 8
+// sums every eighth block sum of digit t / 8 (independent loads, all in flight), then LDS.
+constexpr int kMoParts = 8;  // (kMomDigits x kMoParts <= 256 threads)
+__device__ __forceinline__ void reduce_digits(const int64_t* __restrict__ partials, int nb,
+                                              int64_t* s_m) {
+  __shared__ int64_t s_p[kMomDigits * kMoParts];
+  const int t = threadIdx.x;
+  if (t < kMomDigits * kMoParts) {
+    const int k = t / kMoParts, part = t % kMoParts;
+    const int64_t* p = partials + (int64_t)k * nb;
+    int64_t v = 0;
+    int b = part;
+    for (; b + 15 * kMoParts < nb; b += 16 * kMoParts) {  // (nb <= 512: at most 4 batches)
+      int64_t u[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        u[j] = __hip_atomic_load(p + b + j * kMoParts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v += u[j];
+    }
+    for (; b < nb; b += kMoParts)
+      v += __hip_atomic_load(p + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_p[t] = v;
+  }
+  __syncthreads();
+  if (t < kMomDigits) {
+    int64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < kMoParts; ++q) v += s_p[t * kMoParts + q];
+    s_m[t] = v;
+  }
+  __syncthreads();
+}
+
+// the block's digit sums -> partials [kMomDigits][nb]; the last workgroup to finish (device-scope
+// counter, reset by it for the next launch) reduces them -> out (MODE 1: and refits -> cout)
+template <int MODE>
+__device__ __forceinline__ void moments_tail(const int64_t* acc, int64_t* __restrict__ partials,
+                                             unsigned* __restrict__ done,
+                                             int64_t* __restrict__ out, int qexp,
+                                             const float4* __restrict__ cfp,
+                                             float4* __restrict__ cout) {
+  // (most waves of a filtered pass saw no inlier -- each inlier counts into acc[0] -- and skip
+  // the reduction; the others add their wave sums into LDS)
+  __shared__ unsigned long long s_sum[kMomDigits];
+  const int lane = threadIdx.x & (kWave - 1);
+  if (threadIdx.x < kMomDigits) s_sum[threadIdx.x] = 0ull;
+  __syncthreads();
+  if (ballot(acc[0] != 0)) {
+#pragma unroll
+    for (int k = 0; k < kMomDigits; ++k) {
+      const int64_t v = wave_sum_i64(acc[k]);
+      if (lane == 0 && v != 0) atomicAdd(&s_sum[k], (unsigned long long)v);
+    }
+  }
+  __syncthreads();
+  const int nb = (int)gridDim.x;
+  // last workgroup: the partials go out as device-coherent (agent-scope atomic) stores, complete
+  // (vmcnt) before this block takes its ticket; the last one reads them with coherent loads.  (An
+  // agent-scope release / acquire fence instead writes back / invalidates the whole L2 of the XCD
+  // in every workgroup: ~30 us per launch.)
+  if (threadIdx.x < kMomDigits)
+    __hip_atomic_store(partials + (int64_t)threadIdx.x * nb + blockIdx.x, (int64_t)s_sum[threadIdx.x],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_s_waitcnt(0);  // (the stores are acknowledged before the barrier)
+  __shared__ unsigned s_ticket;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_ticket = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ticket != (unsigned)nb - 1) return;
+  __shared__ int64_t s_m[kMomDigits];
+  reduce_digits(partials, nb, s_m);
+  if (threadIdx.x == 0) *done = 0u;  // (the next launch on this stream starts from zero)
+  if (threadIdx.x < kMomDigits) out[threadIdx.x] = s_m[threadIdx.x];
+  if (MODE == 1) refit_wave0(s_m, qexp, cfp, 1, cout);
+}
+
+// MODE 0: the grid's digit sums -> out; MODE 1: also the refit -> cout (one rank)
+template <bool NP, int MODE>
 __global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, const float4* __restrict__ cfp,
                                                    ModelTest mt, double qscale,
-                                                   int64_t* __restrict__ partials) {
+                                                   int64_t* __restrict__ partials,
+                                                   unsigned* __restrict__ done,
+                                                   int64_t* __restrict__ out, int qexp,
+                                                   float4* __restrict__ cout) {
   const float4 cf = *cfp;
   const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   int64_t acc[kMomDigits];
 #pragma unroll
   for (int k = 0; k < kMomDigits; ++k) acc[k] = 0;
+  MomAcc m;
+  mom_zero(m);
   // kMoIt points per lane per pass, their loads all in flight before the tests (clamped,
   // unconditional: one guarded load per iteration would wait out each load in turn)
   constexpr int kMoIt = 8;
+  static_assert(kMoIt <= kMomFlush, "one flush per pass");
   const int64_t stride = (int64_t)gridDim.x * kMoBS * kMoIt;
   for (int64_t b0 = (int64_t)blockIdx.x * kMoBS * kMoIt; b0 < src.n; b0 += stride) {
     float x[kMoIt], y[kMoIt], z[kMoIt];
@@ -436,76 +545,83 @@ __global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, const float4*
     for (int j = 0; j < kMoIt; ++j) {
       const int64_t e = b0 + j * kMoBS + threadIdx.x;
       if (e < src.n && model_in<NP>(src, e, cf, cn, mt, x[j], y[j], z[j]))
-        mom_add(acc, fast_q(x[j], qscale), fast_q(y[j], qscale), fast_q(z[j], qscale));
+        mom_point(m, fast_q(x[j], qscale), fast_q(y[j], qscale), fast_q(z[j], qscale));
+    }
+    if (m.n != 0.0) mom_flush(acc, m);  // (kMoIt <= kMomFlush points since the last flush)
+  }
+  moments_tail<MODE>(acc, partials, done, out, qexp, cfp, cout);
+}
+
+// lean rounds (plane model over the Morton copy): only the tiles whose bounding sphere may hold an
+// inlier of cf are read -- k_prune_supers' test (a ruled-out sphere holds no point that passes
+// PCL's test), first per super-tile, then per tile.  The same digits as k_moments (integer sums).
+template <int MODE>
+__global__ __launch_bounds__(kMoBS) void k_moments_sp(PointsView src,
+                                                      const float4* __restrict__ tiles,
+                                                      const float4* __restrict__ supers,
+                                                      float margin, const float4* __restrict__ cfp,
+                                                      ModelTest mt, double qscale,
+                                                      int64_t* __restrict__ partials,
+                                                      unsigned* __restrict__ done,
+                                                      int64_t* __restrict__ out, int qexp,
+                                                      float4* __restrict__ cout) {
+  const float4 cf = *cfp;
+  const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
+  int64_t acc[kMomDigits];
+#pragma unroll
+  for (int k = 0; k < kMomDigits; ++k) acc[k] = 0;
+  MomAcc m;
+  mom_zero(m);
+  // every wave tests 64 super-tiles at a time (lane l: super s0 + l W, W = waves in the grid, so
+  // a run of near super-tiles spreads over consecutive waves), then walks its near ones: the 32
+  // tile spheres in lanes 0..31, then the points of the near tiles, 16 per lane, all in flight
+  const int64_t nsup = (src.n + kSuperP - 1) / kSuperP, ntile = (src.n + kTileP - 1) / kTileP;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t W = (int64_t)gridDim.x * (kMoBS / kWave);
+  const int64_t wid = (int64_t)blockIdx.x * (kMoBS / kWave) + threadIdx.x / kWave;
+  constexpr int kIt = kSuperP / kWave;
+  static_assert(kIt <= kMomFlush, "one flush per super-tile");
+  for (int64_t s0 = wid; s0 < nsup; s0 += kWave * W) {
+    const int64_t sl = s0 + lane * W;
+    uint64_t near = ballot(sl < nsup && sphere_near(cf, supers[sl], margin));
+    while (near) {
+      const int64_t s = s0 + (int64_t)(__ffsll((unsigned long long)near) - 1) * W;
+      near &= near - 1;
+      const int64_t tl = s * kSuperTiles + (lane & (kSuperTiles - 1));
+      const uint32_t tm = (uint32_t)ballot(lane < kSuperTiles && tl < ntile &&
+                                           sphere_near(cf, tiles[tl], margin));
+      const int64_t base = s * kSuperP;
+      float x[kIt], y[kIt], z[kIt];
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) {
+        const int64_t e = base + j * kWave + lane;
+        if (((tm >> (2 * j + (lane >> 5))) & 1u) && e < src.n) {
+          x[j] = src.x[e]; y[j] = src.y[e]; z[j] = src.z[e];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) {
+        const int64_t e = base + j * kWave + lane;
+        if (((tm >> (2 * j + (lane >> 5))) & 1u) && e < src.n &&
+            model_in<false>(src, e, cf, cn, mt, x[j], y[j], z[j]))
+          mom_point(m, fast_q(x[j], qscale), fast_q(y[j], qscale), fast_q(z[j], qscale));
+      }
+      if (m.n != 0.0) mom_flush(acc, m);  // (kIt = kMomFlush points per lane per super-tile)
     }
   }
-  __shared__ int64_t s_red[kMoBS / kWave][kMomDigits];
-  const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-#pragma unroll
-  for (int k = 0; k < kMomDigits; ++k) {
-    const int64_t v = wave_sum_i64(acc[k]);
-    if (lane == 0) s_red[w][k] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < kMomDigits) {
-    int64_t v = 0;
-    for (int q = 0; q < kMoBS / kWave; ++q) v += s_red[q][threadIdx.x];
-    partials[(int64_t)blockIdx.x * kMomDigits + threadIdx.x] = v;
-  }
+  moments_tail<MODE>(acc, partials, done, out, qexp, cfp, cout);
 }
 
-constexpr int kRedBS = 256;
-
-// digit sums over the nb workgroup partials (wave w takes digits w, w + 4, ...) -> s_m
-__device__ __forceinline__ void reduce_digits(const int64_t* __restrict__ partials, int nb,
-                                              int64_t* s_m) {
-  const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  for (int k = w; k < kMomDigits; k += kRedBS / kWave) {
-    int64_t v = 0;
-    for (int b = lane; b < nb; b += kWave) v += partials[(int64_t)b * kMomDigits + k];
-    v = wave_sum_i64(v);
-    if (lane == 0) s_m[k] = v;
-  }
-}
-
-__global__ __launch_bounds__(kRedBS) void k_reduce_partials(const int64_t* __restrict__ partials,
-                                                            int nb, int64_t* __restrict__ out) {
+// fast refit on the device from the (rank-summed) digits: < 4 inliers or optimize off keep the
+// unrefined plane.  Keeps the refined plane on the device for the final select (no host round
+// trip between them).
+__global__ __launch_bounds__(kWave) void k_refit_moments(const int64_t* __restrict__ mom, int qexp,
+                                                         const float4* __restrict__ cin,
+                                                         int optimize, float4* __restrict__ cout) {
   __shared__ int64_t s_m[kMomDigits];
-  reduce_digits(partials, nb, s_m);
+  if (threadIdx.x < kMomDigits) s_m[threadIdx.x] = optimize ? mom[threadIdx.x] : 0;
   __syncthreads();
-  if (threadIdx.x < kMomDigits) out[threadIdx.x] = s_m[threadIdx.x];
-}
-
-// fast refit on the device (one thread): exact moments -> plane (exact_refit.hpp); < 4 inliers
-// (or optimize off) keep the unrefined plane.  Keeps the refined plane on the device for the
-// final select (no host round trip between them).
-__global__ void k_refit_moments(const int64_t* __restrict__ mom, int qexp,
-                                const float4* __restrict__ cin, int optimize,
-                                float4* __restrict__ cout) {
-  if (threadIdx.x != 0) return;
-  const float4 c = *cin;
-  const float ci[4] = {c.x, c.y, c.z, c.w};
-  float co[4] = {c.x, c.y, c.z, c.w};
-  if (optimize) refit_exact(mom, qexp, ci, co);
-  *cout = make_float4(co[0], co[1], co[2], co[3]);
-}
-
-// one rank: k_reduce_partials + k_refit_moments in one launch (the allreduce of the moments that
-// separates them with several ranks is the identity)
-__global__ __launch_bounds__(kRedBS) void k_reduce_refit(const int64_t* __restrict__ partials,
-                                                         int nb, int64_t* __restrict__ out,
-                                                         int qexp, const float4* __restrict__ cin,
-                                                         float4* __restrict__ cout) {
-  __shared__ int64_t s_m[kMomDigits];
-  reduce_digits(partials, nb, s_m);
-  __syncthreads();
-  if (threadIdx.x < kMomDigits) out[threadIdx.x] = s_m[threadIdx.x];
-  if (threadIdx.x != 0) return;
-  const float4 c = *cin;
-  const float ci[4] = {c.x, c.y, c.z, c.w};
-  float co[4] = {c.x, c.y, c.z, c.w};
-  refit_exact(s_m, qexp, ci, co);
-  *cout = make_float4(co[0], co[1], co[2], co[3]);
+  refit_wave0(s_m, qexp, cin, optimize, cout);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1322,37 +1438,56 @@ void launch_score(PointsView src, const HypRec* hyps, int D, float cthr, int32_t
 }
 
 int moments_blocks(int64_t n) {
+  // (<= 512: the last workgroup reduces 25 x nb block sums)
   int64_t b = (n + kMoBS * 8 - 1) / (kMoBS * 8);
   if (b < 1) b = 1;
-  if (b > 2048) b = 2048;
+  if (b > 512) b = 512;
   return (int)b;
 }
 
 void launch_refit_moments(const int64_t* moments, int qexp, const float4* cin, int optimize,
                           float4* cout, hipStream_t s) {
-  hipLaunchKernelGGL(k_refit_moments, dim3(1), dim3(64), 0, s, moments, qexp, cin, optimize, cout);
+  hipLaunchKernelGGL(k_refit_moments, dim3(1), dim3(kWave), 0, s, moments, qexp, cin, optimize, cout);
 }
 
+// done: a device counter that is zero between launches (the last workgroup resets it)
 void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
-                          int64_t* partials, int nblocks, int64_t* out, float4* cout,
-                          hipStream_t s) {
+                          int64_t* partials, unsigned* done, int nblocks, int64_t* out,
+                          float4* cout, hipStream_t s) {
   const double qs = pow2d(kFastBits - qexp);
   if (mt.normal_plane)
-    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
+    hipLaunchKernelGGL((k_moments<true, 1>), dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs,
+                       partials, done, out, qexp, cout);
   else
-    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
-  hipLaunchKernelGGL(k_reduce_refit, dim3(1), dim3(kRedBS), 0, s, partials, nblocks, out, qexp,
-                     coef, cout);
+    hipLaunchKernelGGL((k_moments<false, 1>), dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs,
+                       partials, done, out, qexp, cout);
+}
+
+int moments_sp_blocks(int64_t n) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(256, sp_supers(n)));
+}
+
+void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers, float margin,
+                       const float4* coef, const ModelTest& mt, int qexp, int64_t* partials,
+                       unsigned* done, int nblocks, int64_t* out, float4* cout, hipStream_t s) {
+  const double qs = pow2d(kFastBits - qexp);
+  if (cout)
+    hipLaunchKernelGGL(k_moments_sp<1>, dim3(nblocks), dim3(kMoBS), 0, s, src, tiles, supers,
+                       margin, coef, mt, qs, partials, done, out, qexp, cout);
+  else
+    hipLaunchKernelGGL(k_moments_sp<0>, dim3(nblocks), dim3(kMoBS), 0, s, src, tiles, supers,
+                       margin, coef, mt, qs, partials, done, out, qexp, nullptr);
 }
 
 void launch_moments(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
-                    int64_t* partials, int nblocks, int64_t* out, hipStream_t s) {
+                    int64_t* partials, unsigned* done, int nblocks, int64_t* out, hipStream_t s) {
   const double qs = pow2d(kFastBits - qexp);
   if (mt.normal_plane)
-    hipLaunchKernelGGL(k_moments<true>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
+    hipLaunchKernelGGL((k_moments<true, 0>), dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs,
+                       partials, done, out, qexp, nullptr);
   else
-    hipLaunchKernelGGL(k_moments<false>, dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs, partials);
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kRedBS), 0, s, partials, nblocks, out);
+    hipLaunchKernelGGL((k_moments<false, 0>), dim3(nblocks), dim3(kMoBS), 0, s, src, coef, mt, qs,
+                       partials, done, out, qexp, nullptr);
 }
 
 void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,

@@ -140,15 +140,24 @@ void launch_prep_bf16(const HypRec* hyps, int D, const uint4** bcol, const float
 void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest& mt,
                      int32_t* counts, int num_cus, hipStream_t s);
 // fast refit (exact_refit.hpp): the exact integer moments (kMomDigits int64 digit sums) of the
-// inliers of coef, quantised with exponent qexp; partials [nblocks][kMomDigits] -> out
+// inliers of coef, quantised with exponent qexp; partials [kMomDigits][nblocks] scratch, reduced
+// by the launch's last workgroup -> out.  done: a device counter, zero before the first launch
+// (each launch leaves it zero)
 int moments_blocks(int64_t n);
 // coef: device float4 (a, b, c, d)
-// one rank: moments of the unrefined plane's inliers + reduction + refit in two launches
+// one rank: moments of the unrefined plane's inliers + reduction + refit in one launch
 void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
-                          int64_t* partials, int nblocks, int64_t* out, float4* cout,
-                          hipStream_t s);
+                          int64_t* partials, unsigned* done, int nblocks, int64_t* out,
+                          float4* cout, hipStream_t s);
 void launch_moments(PointsView src, const float4* coef, const ModelTest& mt, int qexp,
-                    int64_t* partials, int nblocks, int64_t* out, hipStream_t s);
+                    int64_t* partials, unsigned* done, int nblocks, int64_t* out, hipStream_t s);
+// lean rounds (plane model): the same moments over the Morton copy reading only the tiles whose
+// sphere may hold an inlier (tiles / supers: the copy's spheres, margin: the scoring's
+// prune_margin); cout non-null: one rank, refit too (as launch_moments_refit)
+int moments_sp_blocks(int64_t n);
+void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers, float margin,
+                       const float4* coef, const ModelTest& mt, int qexp, int64_t* partials,
+                       unsigned* done, int nblocks, int64_t* out, float4* cout, hipStream_t s);
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers
 void launch_refit_moments(const int64_t* moments, int qexp, const float4* cin, int optimize,

@@ -158,10 +158,6 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
 constexpr int kPrBS = 1024;
 constexpr int kPrWaves = kPrBS / kWave;
 
-__device__ __forceinline__ float prune_lim(float margin, float r) {
-  return (margin + r) * (1.0f + 0x1p-20f);
-}
-
 __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict__ supers,
                                                         int nsup, const HypRec* __restrict__ hyps,
                                                         int D, int ls, float margin,
@@ -180,15 +176,12 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
     if (threadIdx.x == 0) s_nlp = 0;
     __syncthreads();
     const float4 sp = supers[sidx];
-    const float slim = prune_lim(margin, sp.w);
     uint16_t* out = lp + (int64_t)sidx * ls;
     for (int b = 0; b < D; b += kPrBS) {  // block-uniform trip count
       const int j = b + threadIdx.x;
       bool near = false;
       if (j < D) {
-        const float4 cf = s_cf[j];
-        const float h = __builtin_fmaf(cf.x, sp.x, __builtin_fmaf(cf.y, sp.y, __builtin_fmaf(cf.z, sp.z, cf.w)));
-        near = fabsf(h) <= slim;  // NaN planes: never near (PCL counts nothing for them)
+        near = sphere_near(s_cf[j], sp, margin);  // NaN planes: never near
       }
       const uint64_t m = ballot(near);
       if (m) {

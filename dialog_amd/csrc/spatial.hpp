@@ -41,6 +41,16 @@ struct SpatialView {
   const float4* supers;  // [sp_supers(n)]
 };
 
+// the pruning test: may the sphere sp = (c, r) hold a point that passes PCL's test for the plane
+// cf?  No when fl(|n.c + d|) > (margin + r)(1 + 2^-20) (module comment).  NaN planes: never near.
+__device__ __forceinline__ float prune_lim(float margin, float r) {
+  return (margin + r) * (1.0f + 0x1p-20f);
+}
+__device__ __forceinline__ bool sphere_near(float4 cf, float4 sp, float margin) {
+  const float h = __builtin_fmaf(cf.x, sp.x, __builtin_fmaf(cf.y, sp.y, __builtin_fmaf(cf.z, sp.z, cf.w)));
+  return fabsf(h) <= prune_lim(margin, sp.w);
+}
+
 // Morton keys over [-amax, amax] per axis; non-finite points get key 0xFFFFFFFF (sorted last)
 // and are counted into *n_nonfinite (never inliers of any plane: PCL's distance is NaN or inf)
 void launch_morton_keys(PointsView src, float ax, float ay, float az, uint32_t* keys,

@@ -105,3 +105,31 @@ def test_oracle_fast_segment_close_to_double(tmp_path):
     sg = 1.0 if a["coeff"][:3] @ b["coeff"][:3] > 0 else -1.0  # (the double twin has no orientation)
     assert np.abs(a["coeff"] - sg * b["coeff"]).max() < 1e-6
     assert a["coeff"][:3] @ a["coeff_unrefined"][:3] > 0  # fast refit keeps the unrefined side
+
+
+def test_big_to_double_correctly_rounded(harness):
+    """big_to_double (192-bit two's complement -> double) against Python's correctly rounded
+    int -> float: random magnitudes of every bit length, exact ties, ties +- 1, all-ones runs."""
+    rng = np.random.default_rng(7)
+    vals = [0, 1, -1, 2**53, 2**53 + 1, 2**54 + 2, 2**54 + 6, -(2**190), 2**190 - 1]
+    for L in range(1, 191):
+        for _ in range(6):
+            vals.append(int(rng.integers(0, 2**62)) << max(0, L - 62) | int(rng.integers(0, 2**62)))
+            vals[-1] &= (1 << L) - 1
+            vals[-1] |= 1 << (L - 1)
+        if L > 54:
+            m = (int(rng.integers(0, 2**52)) | 2**52) << (L - 53)
+            half = 1 << (L - 54)
+            vals += [m + half, m + half - 1, m + half + 1, m + 3 * half, (1 << L) - 1]
+    vals += [-v for v in list(vals)]
+    vals = [v for v in vals if -(2**191) <= v < 2**191]
+    lines = []
+    for v in vals:
+        u = v & ((1 << 192) - 1)
+        lines.append(" ".join(f"{(u >> (32 * k)) & 0xFFFFFFFF:x}" for k in range(6)))
+    out = subprocess.run([harness, "B"], input="\n".join(lines) + "\n", capture_output=True,
+                         text=True, check=True).stdout.split()
+    got = np.array([int(w, 16) for w in out], np.uint64).view(np.float64)
+    want = np.array([float(v) for v in vals], np.float64)
+    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
+    assert bad.size == 0, [(vals[i], got[i], want[i]) for i in bad[:5]]
