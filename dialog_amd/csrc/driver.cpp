@@ -62,8 +62,9 @@ double now_ms() {
 }
 
 // spin until k_publish has released `seq` into c->pub[0] (the round's results are then in
-// c->pub).  ev_tot (recorded right after the publish) backs it up: once the event has
-// completed the word must be visible; an error of the stream surfaces through the event query.
+// c->pub).  A stream query backs it up (no event marker on the stream: each one costs the GPU
+// a few microseconds between kernels): once the stream has drained the word must be visible; an
+// error of the stream surfaces through the query.
 void pump_pending(dlg_ctx* c, int64_t ids);
 
 void wait_published(dlg_ctx* c, int32_t seq) {
@@ -73,7 +74,7 @@ void wait_published(dlg_ctx* c, int32_t seq) {
     // queried only every 16th spin (a HIP API call takes the runtime lock)
     if (c->stage_ready || (k & 15u) == 0) pump_pending(c, 16384);
     if ((k & 1023u) == 0) {
-      const hipError_t e = hipEventQuery(c->ev_tot);
+      const hipError_t e = hipStreamQuery(c->stream);
       if (e == hipSuccess) {
         if (__atomic_load_n(c->pub, __ATOMIC_ACQUIRE) == seq) return;
         throw DlgError(DLG_ERR_INTERNAL, "round results not visible after the round completed");
@@ -220,7 +221,7 @@ void flush_emit(dlg_ctx* c) {
   drain_pending(c);  // (the stage is reused)
   c->h_stage.ensure((size_t)c->emit_n);
   if (!c->ev_stage) HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
-  HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_inl, 0));
+  HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_inl_cur, 0));
   HIPCHK(hipMemcpyAsync(c->h_stage.p, c->inl_gid.p, (size_t)c->emit_n * 4, hipMemcpyDeviceToHost,
                         c->cstream));
   HIPCHK(hipEventRecord(c->ev_stage, c->cstream));
@@ -587,14 +588,23 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // one-thread kernel, then the select with the refined plane read from device memory.  PCL
     // mode needs the host's sequential float sums in between.
     if (c->stage_inflight) {  // the previous round's inlier copy still reads inl_gid
-      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_stage, 0));
+      // (a stream wait only when the copy is still running: it has almost always landed)
+      const hipError_t q = hipEventQuery(c->ev_stage);
+      if (q == hipErrorNotReady) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_stage, 0));
+      else HIPCHK(q);
       c->stage_inflight = false;
     }
     const int sk = c->sel_k;  // this round's pair of select timing events
     if (c->profiling) {
       for (auto& ev : c->ev_sel[sk])
         if (!ev) HIPCHK(hipEventCreate(&ev));
-      HIPCHK(hipEventRecord(c->ev_sel[sk][0], c->stream));
+      if (spec_pending) {
+        // the scoring's end event (just recorded) opens the select phase: no second marker
+        std::swap(c->ev[1], c->ev_sel[sk][0]);
+        c->ev_score_end = c->ev_sel[sk][0];
+      } else {
+        HIPCHK(hipEventRecord(c->ev_sel[sk][0], c->stream));
+      }
     }
     if (!pcl_refit) {
       const bool one = c->comm->world() == 1;
@@ -694,15 +704,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                    with_counts ? c->res.p : nullptr, nres, c->sel1_err.p, c->pub, seq, c->stream);
     HIPCHK(hipGetLastError());
     spec_pending = false;
-    if (!c->ev_tot) HIPCHK(hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(c->ev_tot, c->stream));
     if (lean) {
       // the list from the stamps (ids in list order; survivors' pristine indices), then the
       // sphere bounds of the Morton survivors (count in totals[4])
       launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv, cl->pristine.gid.p, c->sel1,
                        c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream);
-      HIPCHK(hipEventRecord(c->ev_inl, c->stream));  // inl_gid final (flush_emit)
-      if (c->profiling) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
       const int b = cl->sp_spare();
       SoA& sd = cl->sp_buf[b];
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
@@ -712,7 +718,6 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     } else {
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
                          nullptr, compact ? &dst : nullptr, c->stream);
-      HIPCHK(hipEventRecord(c->ev_inl, c->stream));  // inl_gid final (flush_emit)
     }
     // the Morton copy loses the same points (same predicate, same float inputs): its totals
     // land in totals[2..3], checked at the next publish / the end of the extraction
@@ -727,7 +732,6 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                            ss.with_nrm ? ss.nrm.p : nullptr};
       launch_select(spv, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
                     c->totals.p + 2, nullptr, nullptr, &spo, c->stream);
-      if (c->profiling) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
       // sphere bounds of the survivors, into the spare buffer's own bound arrays (sized for
       // the current count, an upper bound; the kernel reads the survivor count from
       // totals[3]), so a round whose plane is rejected leaves the current bounds intact
@@ -738,7 +742,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                            cl->sp_sb[b].p, c->stream);
     }
     HIPCHK(hipGetLastError());
-    if (c->profiling && !sp_compact && !lean) HIPCHK(hipEventRecord(c->ev_sel[sk][1], c->stream));
+    // one marker at the end of the round's work: inl_gid is final there (flush_emit's copy waits
+    // for it) and, when profiling, it closes the select phase.  (The GPU then waits for the
+    // host's next draw anyway.)
+    c->ev_inl_cur = c->profiling ? c->ev_sel[sk][1] : c->ev_inl;
+    HIPCHK(hipEventRecord(c->ev_inl_cur, c->stream));
     const double t_wait0 = trace_on() ? now_ms() : 0.0;
     wait_published(c, seq);
     if (trace_on())
@@ -770,7 +778,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     refit_select();  // on the device's pick
     selected = true;
     // the exact host replay of the same counts
-    if (c->profiling) st->score_ms += event_ms(c, 0, 1);
+    if (c->profiling) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev_score_end));
+      st->score_ms += ms;
+    }
     const int best_d = ctl.consume(c->h_res.p, c->h_res.p + spec_Dp, spec_D);
     if (!(ctl.done() && best_d == c->h_pick.p[0] && c->h_pick.p[1] == 1)) {
       ++c->spec_misses;
@@ -1043,7 +1055,6 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
     (void)hipStreamSynchronize(c->cstream);
     (void)hipStreamDestroy(c->cstream);
   }
-  if (c->ev_tot) (void)hipEventDestroy(c->ev_tot);
   for (auto& pr : c->ev_sel)
     for (auto& ev : pr)
       if (ev) (void)hipEventDestroy(ev);

@@ -207,8 +207,10 @@ struct dlg_ctx {
   // ev_inl (the round's select on the main stream); the next select waits for ev_stage
   hipStream_t cstream = nullptr;
   hipEvent_t ev_inl = nullptr;
+  hipEvent_t ev_inl_cur = nullptr;    // the marker the copy waits for (ev_inl, or the round's
+                                      // end-of-select timing event when profiling)
+  hipEvent_t ev_score_end = nullptr;  // (profiling) the last speculative round's scoring end
   bool stage_inflight = false;
-  hipEvent_t ev_tot = nullptr;
   DevBuf<int32_t> pick;   // k_pick_p1 result
   int32_t* pub = nullptr;  // coherent pinned: k_publish's round results (pub[0] = sequence)
   size_t pub_cap = 0;
