@@ -332,12 +332,17 @@ def main():
     sum_active = per_rank_tests / max(a.hyps, 1)  # sum over rounds of this rank's active points
     lean = pruned and lean_rounds == rounds_per_step and a.refit == "fast"
     if lean:
-        # lean-list rounds: moments over the Morton copy (12 B/pt), the single-pass select of the
-        # Morton copy (16 B read, 16 B per survivor, a 1 B stamp per inlier), then the list from
-        # the stamps (4 B index + 1 B stamp read, 4 B per survivor index, 4 + 4 B per inlier id)
-        sel_bytes = (12.0 * sum_active + 16.0 * sum_active + 16.0 * (sum_active - inliers_local)
-                     + 1.0 * inliers_local + 5.0 * sum_active
-                     + 4.0 * (sum_active - inliers_local) + 8.0 * inliers_local)
+        # lean-list rounds, the phase from the scoring's end to the round's end: the speculative
+        # pick, the moments over the Morton copy's near tiles (counted as 12 B per inlier: the
+        # tiles whose sphere can hold one), the single-pass select of the Morton copy (16 B read,
+        # 16 B per survivor, a 1 B stamp per inlier), the list from the stamps (4 B index + 1 B
+        # stamp read, 4 B per survivor index, 4 + 4 B per inlier id) and the survivors' tile
+        # bounding spheres (12 B per survivor read, 16 B per 32-point tile written)
+        surv = sum_active - inliers_local
+        sel_bytes = (12.0 * inliers_local
+                     + 16.0 * sum_active + 16.0 * surv + 1.0 * inliers_local
+                     + 5.0 * sum_active + 4.0 * surv + 8.0 * inliers_local
+                     + 12.0 * surv + 0.5 * surv)
     else:
         n_copies = 2 if pruned else 1
         sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))

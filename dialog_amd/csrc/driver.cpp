@@ -656,34 +656,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // round's totals final, they are published right away, and the scatters (inlier ids,
     // survivors of both copies) and the sphere bounds run while the host reads them and draws
     // the next round
-    // (lean: the Morton copy's single-pass select makes the totals final and stamps the inliers)
-    if (lean) {
-      if (++cl->tagv > 255) {
-        HIPCHK(hipMemsetAsync(cl->tag.p, 0, (size_t)cl->n_total, c->stream));
-        cl->tagv = 1;
-      }
-      ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n));
-      SoA& sd = cl->sp_buf[cl->sp_spare()];
-      sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
-      const SoA& ss = cl->sp_soa();
-      if (ss.with_nrm) sd.ensure_nrm((size_t)std::max<int64_t>(cl->sp_n, 1));
-      PointsOut spo = sd.out();
-      PointsView spv = sp_cur_view();
-      if (ss.with_nrm) spv.nrm = ss.nrm.p;  // (a later NORMAL_PLANE round reads them)
-      else spo.nrm = nullptr;
-      launch_sel1_morton(spv, rc_dev, mt, c->sel1, cl->tag.p, (uint8_t)cl->tagv, spo, src.n,
-                         c->totals.p, c->stream);
-    } else {
-      launch_select_head(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
-                         c->totals.p, c->stream);
-    }
-    HIPCHK(hipGetLastError());
+    // (lean: the Morton copy's single-pass select makes the totals final and stamps the inliers;
+    // on one rank its last tile publishes the round too)
     const int W = c->comm->world();
-    if (W > 1) {  // every rank's (in, out): the extract loop needs no host-synced allgather
-      c->rk.ensure(2 * (size_t)W + 2);
-      c->h_rk.ensure(2 * (size_t)W + 2);
-      c->comm->allgather(c->totals.p, c->rk.p, 2, DType::I32, c->stream);
-    }
     // the round's results into the coherent pinned buffer + a sequence number the host spins on
     // (totals[2..3] still hold the previous compaction's Morton-copy totals: checked below)
     const bool with_counts = spec_pending;
@@ -698,10 +673,51 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       c->pub_cap = std::max<size_t>(need, 16384);
       c->pub[0] = 0;
     }
+    if (W > 1) {
+      c->rk.ensure(2 * (size_t)W + 2);
+      c->h_rk.ensure(2 * (size_t)W + 2);
+    }
     const int32_t seq = ++c->pub_seq == 0 ? ++c->pub_seq : c->pub_seq;
-    launch_publish(c->totals.p, 4, c->small.p, 6, W > 1 ? c->rk.p : nullptr, W > 1 ? 2 * W : 0,
-                   with_counts ? c->pick.p : nullptr, with_counts ? 2 : 0,
-                   with_counts ? c->res.p : nullptr, nres, c->sel1_err.p, c->pub, seq, c->stream);
+    PubArgs pa;
+    pa.totals = c->totals.p;
+    pa.ntot = 4;
+    pa.small = c->small.p;
+    pa.nsmall = 6;
+    pa.rk = W > 1 ? c->rk.p : nullptr;
+    pa.nrk = W > 1 ? 2 * W : 0;
+    pa.pick = with_counts ? c->pick.p : nullptr;
+    pa.npick = with_counts ? 2 : 0;
+    pa.res = with_counts ? c->res.p : nullptr;
+    pa.nres = nres;
+    pa.err = c->sel1_err.p;
+    pa.pub = c->pub;
+    pa.seq = seq;
+    const bool fused_pub = lean && W == 1;
+    if (lean) {
+      if (++cl->tagv > 255) {
+        HIPCHK(hipMemsetAsync(cl->tag.p, 0, (size_t)cl->n_total, c->stream));
+        cl->tagv = 1;
+      }
+      ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n));
+      pa.err = c->sel1_err.p;
+      SoA& sd = cl->sp_buf[cl->sp_spare()];
+      sd.ensure((size_t)std::max<int64_t>(cl->sp_n, 1));
+      const SoA& ss = cl->sp_soa();
+      if (ss.with_nrm) sd.ensure_nrm((size_t)std::max<int64_t>(cl->sp_n, 1));
+      PointsOut spo = sd.out();
+      PointsView spv = sp_cur_view();
+      if (ss.with_nrm) spv.nrm = ss.nrm.p;  // (a later NORMAL_PLANE round reads them)
+      else spo.nrm = nullptr;
+      launch_sel1_morton(spv, rc_dev, mt, c->sel1, cl->tag.p, (uint8_t)cl->tagv, spo, src.n,
+                         c->totals.p, c->stream, fused_pub ? &pa : nullptr);
+    } else {
+      launch_select_head(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
+                         c->totals.p, c->stream);
+    }
+    HIPCHK(hipGetLastError());
+    if (W > 1)  // every rank's (in, out): the extract loop needs no host-synced allgather
+      c->comm->allgather(c->totals.p, c->rk.p, 2, DType::I32, c->stream);
+    if (!fused_pub) launch_publish(pa, c->stream);
     HIPCHK(hipGetLastError());
     spec_pending = false;
     if (lean) {

@@ -716,24 +716,25 @@ __global__ __launch_bounds__(kPickBS) void k_pick_p1(const int32_t* __restrict__
 // totals, the speculative pick and counts) written straight into a coherent pinned host buffer,
 // then a system-scope release of the sequence number in pub[0]: the host spins on that word
 // instead of waiting on a HIP event (whose wake-up costs ~50 us per round).  One workgroup.
-__global__ __launch_bounds__(256) void k_publish(const int32_t* __restrict__ totals, int ntot,
-                                                 const float4* __restrict__ small, int nsmall,
-                                                 const int32_t* __restrict__ rk, int nrk,
-                                                 const int32_t* __restrict__ pick, int npick,
-                                                 const int32_t* __restrict__ res, int nres,
-                                                 const int32_t* __restrict__ err, int32_t* pub,
-                                                 int32_t seq) {
-  const int t = threadIdx.x;
-  if (t == 0) pub[kPubErr] = err ? *err : 0;
-  for (int i = t; i < ntot; i += 256) pub[kPubTot + i] = totals[i];
-  for (int i = t; i < 4 * nsmall; i += 256)
-    pub[kPubSmall + i] = __float_as_int(reinterpret_cast<const float*>(small)[i]);
-  for (int i = t; i < npick; i += 256) pub[kPubPick + i] = pick[i];
-  for (int i = t; i < nrk; i += 256) pub[kPubRk + i] = rk[i];
-  for (int i = t; i < nres; i += 256) pub[kPubRk + nrk + i] = res[i];
+// the publish by the nthr threads of one workgroup (k_publish, or the last tile of a fused
+// select); tot01: the select's own totals[0..1] when the caller has just computed them (the
+// global words may not be visible yet), else null
+__device__ __forceinline__ void publish_body(const PubArgs& a, const int32_t* tot01, int t, int nthr) {
+  if (t == 0) a.pub[kPubErr] = a.err ? *a.err : 0;
+  for (int i = t; i < a.ntot; i += nthr)
+    a.pub[kPubTot + i] = tot01 && i < 2 ? tot01[i] : a.totals[i];
+  for (int i = t; i < 4 * a.nsmall; i += nthr)
+    a.pub[kPubSmall + i] = __float_as_int(reinterpret_cast<const float*>(a.small)[i]);
+  for (int i = t; i < a.npick; i += nthr) a.pub[kPubPick + i] = a.pick[i];
+  for (int i = t; i < a.nrk; i += nthr) a.pub[kPubRk + i] = a.rk[i];
+  for (int i = t; i < a.nres; i += nthr) a.pub[kPubRk + a.nrk + i] = a.res[i];
   __threadfence_system();
   __syncthreads();
-  if (t == 0) __hip_atomic_store(pub, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) __hip_atomic_store(a.pub, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void k_publish(PubArgs a) {
+  publish_body(a, nullptr, threadIdx.x, 256);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1014,12 +1015,14 @@ __device__ __forceinline__ int sel1_scan(const Sel1State& L, int tile, int* s_cn
 // the Morton copy's select: survivors compacted into dst (Morton order kept), inliers stamped
 // in tag[] by pristine index (the Morton copy's gid field holds it); the last tile writes
 // totals[0] = inliers, totals[1] = list survivors (n_list - inliers), totals[4] = Morton survivors
+// pa.pub non-null: the last tile also publishes the round (publish_body) once its totals are
+// final, without waiting for the other tiles' scatters (nothing published depends on them)
 template <bool NP>
 __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const float4* __restrict__ cfp,
                                                        ModelTest mt, Sel1State L,
                                                        uint8_t* __restrict__ tag, uint8_t tagv,
                                                        PointsOut dst, int64_t n_list, int ntiles,
-                                                       int32_t* __restrict__ totals) {
+                                                       int32_t* __restrict__ totals, PubArgs pa) {
   __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
   const int tile = blockIdx.x;
   const float4 cf = *cfp;
@@ -1058,11 +1061,17 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const flo
       if (dst.nrm) dst.nrm[q] = src.nrm[e];  // (normals travel when the copy has them)
     }
   }
-  if (tile == ntiles - 1 && threadIdx.x == 0) {
+  if (tile == ntiles - 1) {
     const int in = excl + s_base[1];
-    totals[0] = in;
-    totals[1] = (int32_t)(n_list - in);
-    totals[4] = (int32_t)(src.n - in);
+    if (threadIdx.x == 0) {
+      totals[0] = in;
+      totals[1] = (int32_t)(n_list - in);
+      totals[4] = (int32_t)(src.n - in);
+    }
+    if (pa.pub) {
+      const int32_t t01[2] = {in, (int32_t)(n_list - in)};
+      publish_body(pa, t01, threadIdx.x, kS1BS);
+    }
   }
 }
 
@@ -1319,19 +1328,22 @@ static void sel1_next(Sel1State& L, int) { ++L.epoch; }
 
 void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
                         uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
-                        int32_t* totals, hipStream_t s) {
+                        int32_t* totals, hipStream_t s, const PubArgs* pub) {
   const int nt = sel1_tiles(sp.n);
   if (nt == 0) {
     hipLaunchKernelGGL(k_sel1_empty, dim3(1), dim3(1), 0, s, n_list, totals);
+    if (pub) hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, *pub);
     return;
   }
   sel1_next(L, nt);
+  PubArgs pa{};
+  if (pub) pa = *pub;
   if (mt.normal_plane)
     hipLaunchKernelGGL(k_sel1_morton<true>, dim3(nt), dim3(kS1BS), 0, s, sp, coef, mt, L, tag,
-                       tagv, dst, n_list, nt, totals);
+                       tagv, dst, n_list, nt, totals, pa);
   else
     hipLaunchKernelGGL(k_sel1_morton<false>, dim3(nt), dim3(kS1BS), 0, s, sp, coef, mt, L, tag,
-                       tagv, dst, n_list, nt, totals);
+                       tagv, dst, n_list, nt, totals, pa);
 }
 
 void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_t tagv,
@@ -1497,12 +1509,8 @@ void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypR
                      best, best_smp, out);
 }
 
-void launch_publish(const int32_t* totals, int ntot, const float4* small, int nsmall,
-                    const int32_t* rk, int nrk, const int32_t* pick, int npick,
-                    const int32_t* res, int nres, const int32_t* err, int32_t* pub, int32_t seq,
-                    hipStream_t s) {
-  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, totals, ntot, small, nsmall, rk, nrk,
-                     pick, npick, res, nres, err, pub, seq);
+void launch_publish(const PubArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, a);
 }
 
 int select_tiles(int64_t n) { return (int)((n + kSelTile - 1) / kSelTile); }

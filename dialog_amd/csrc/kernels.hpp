@@ -87,10 +87,22 @@ void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src
 // system scope)
 // (err: the single-pass selects' sticky look-back error word, or null)
 constexpr int kPubTot = 1, kPubPick = 5, kPubErr = 7, kPubSmall = 8, kPubRk = 32;  // + nrk: counts
-void launch_publish(const int32_t* totals, int ntot, const float4* small, int nsmall,
-                    const int32_t* rk, int nrk, const int32_t* pick, int npick,
-                    const int32_t* res, int nres, const int32_t* err, int32_t* pub, int32_t seq,
-                    hipStream_t s);
+struct PubArgs {
+  const int32_t* totals = nullptr;
+  int ntot = 0;
+  const float4* small = nullptr;
+  int nsmall = 0;
+  const int32_t* rk = nullptr;
+  int nrk = 0;
+  const int32_t* pick = nullptr;
+  int npick = 0;
+  const int32_t* res = nullptr;
+  int nres = 0;
+  const int32_t* err = nullptr;
+  int32_t* pub = nullptr;
+  int32_t seq = 0;
+};
+void launch_publish(const PubArgs& a, hipStream_t s);
 // speculative computeModel decision for probability 1 over one batch (k_pick_p1): out[0] best
 // batch index (-1 none), out[1] loop ended inside the batch; winner copied to best / best_smp
 void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
@@ -114,9 +126,11 @@ struct Sel1State {
 int sel1_tiles(int64_t n);
 // the Morton copy's select: survivors -> dst, inliers stamped tag[pristine index] = tagv;
 // totals[0] = inliers, totals[1] = n_list - inliers, totals[4] = Morton survivors
+// pub non-null: the last tile also publishes the round (as launch_publish) once the totals are
+// final
 void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
                         uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
-                        int32_t* totals, hipStream_t s);
+                        int32_t* totals, hipStream_t s, const PubArgs* pub = nullptr);
 // the lean list's compaction from the stamps (lidx null: the pristine list): inlier ids in list
 // order -> inl_gid, survivors' pristine indices -> out_lidx; totals[0..1] = (in, out)
 void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_t tagv,
