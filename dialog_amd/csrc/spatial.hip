@@ -158,41 +158,100 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
 constexpr int kPrBS = 1024;
 constexpr int kPrWaves = kPrBS / kWave;
 
+// One workgroup per "hyper" of H consecutive super-tiles (a compact region in Morton order): the
+// bounding sphere of their spheres first takes the D planes down to the few near it (LDS list),
+// then each super-tile tests only those.  A plane ruled out by the hyper sphere has no PCL
+// inlier anywhere in it (the same test on a sphere that bounds every super-tile sphere), so the
+// super-tile lists keep every plane that can score.
 __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict__ supers,
                                                         int nsup, const HypRec* __restrict__ hyps,
-                                                        int D, int ls, float margin,
+                                                        int D, int ls, float margin, int H,
                                                         uint16_t* __restrict__ lp,
                                                         int32_t* __restrict__ lp_n,
                                                         int32_t* __restrict__ work) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
-  __shared__ int s_nlp;
-  const int lane = threadIdx.x & (kWave - 1);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *work = 0;  // k_score_tiles_rl's item counter
-  for (int j = threadIdx.x; j < D; j += kPrBS) {
+  __shared__ uint16_t s_hl[kMaxHypPerLaunch];  // the planes near this hyper's sphere
+  __shared__ float4 s_sp[kWave];
+  __shared__ float4 s_hyp;
+  __shared__ int s_nh, s_nl[kPrWaves];
+  const int t = threadIdx.x, lane = t & (kWave - 1);
+  if (blockIdx.x == 0 && t == 0) *work = 0;  // k_score_tiles_rl's item counter
+  for (int j = t; j < D; j += kPrBS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
   }
-  for (int sidx = blockIdx.x; sidx < nsup; sidx += gridDim.x) {
-    if (threadIdx.x == 0) s_nlp = 0;
-    __syncthreads();
-    const float4 sp = supers[sidx];
-    uint16_t* out = lp + (int64_t)sidx * ls;
-    for (int b = 0; b < D; b += kPrBS) {  // block-uniform trip count
-      const int j = b + threadIdx.x;
-      bool near = false;
-      if (j < D) {
-        near = sphere_near(s_cf[j], sp, margin);  // NaN planes: never near
+  for (int64_t h0 = (int64_t)blockIdx.x * H; h0 < nsup; h0 += (int64_t)gridDim.x * H) {
+    const int ns = (int)min<int64_t>(H, nsup - h0);
+    __syncthreads();  // (the previous hyper's s_sp / s_hl are no longer read)
+    if (t < kWave) {  // wave 0: the hyper sphere (box midpoint, max |c_s - C| + r_s, inflated)
+      const bool v = lane < ns;
+      const float4 sp = v ? supers[h0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (v) s_sp[lane] = sp;
+      float x0 = v ? sp.x - sp.w : INFINITY, y0 = v ? sp.y - sp.w : INFINITY;
+      float z0 = v ? sp.z - sp.w : INFINITY, x1 = v ? sp.x + sp.w : -INFINITY;
+      float y1 = v ? sp.y + sp.w : -INFINITY, z1 = v ? sp.z + sp.w : -INFINITY;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        x0 = fminf(x0, __shfl_xor(x0, o)); y0 = fminf(y0, __shfl_xor(y0, o));
+        z0 = fminf(z0, __shfl_xor(z0, o)); x1 = fmaxf(x1, __shfl_xor(x1, o));
+        y1 = fmaxf(y1, __shfl_xor(y1, o)); z1 = fmaxf(z1, __shfl_xor(z1, o));
       }
-      const uint64_t m = ballot(near);
-      if (m) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&s_nlp, (int)__popcll(m));
-        base = __shfl(base, 0);
-        if (near) out[base + lanes_below(m)] = (uint16_t)j;
+      const float Cx = 0.5f * (x0 + x1), Cy = 0.5f * (y0 + y1), Cz = 0.5f * (z0 + z1);
+      float R = 0.0f;
+      if (v) {
+        const float dx = sp.x - Cx, dy = sp.y - Cy, dz = sp.z - Cz;
+        R = sqrtf(dx * dx + dy * dy + dz * dz) + sp.w;
+      }
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) R = fmaxf(R, __shfl_xor(R, o));
+      if (lane == 0) {
+        s_hyp = make_float4(Cx, Cy, Cz, R * (1.0f + 0x1p-18f) + 1e-30f);
+        s_nh = 0;
       }
     }
     __syncthreads();
-    if (threadIdx.x == 0) lp_n[sidx] = s_nlp;
+    const float4 hs = s_hyp;
+    for (int b = 0; b < D; b += kPrBS) {  // block-uniform trip count
+      const int j = b + t;
+      const bool near = j < D && sphere_near(s_cf[j], hs, margin);  // NaN planes: never near
+      const uint64_t m = ballot(near);
+      if (m) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_nh, (int)__popcll(m));
+        base = __shfl(base, 0);
+        if (near) s_hl[base + lanes_below(m)] = (uint16_t)j;
+      }
+    }
+    __syncthreads();
+    // the near planes against the super-tiles, P super-tiles at a time (a slice of SL = kPrBS / P
+    // threads each, a multiple of the wave: a wave's lanes serve one super-tile)
+    const int nh = s_nh;
+    int P = 1;
+    while (P < ns && P < kPrWaves && (kPrBS / (2 * P)) >= nh) P *= 2;
+    const int SL = kPrBS / P, ks = t / SL, it = t % SL;
+    for (int k0 = 0; k0 < ns; k0 += P) {
+      const int k = k0 + ks;
+      if (t < P) s_nl[t] = 0;
+      __syncthreads();
+      if (k < ns) {
+        const float4 sp = s_sp[k];
+        uint16_t* out = lp + (h0 + k) * ls;
+        for (int b = 0; b < nh; b += SL) {  // uniform per wave
+          const int i = b + it;
+          const int j = i < nh ? (int)s_hl[i] : 0;
+          const bool near = i < nh && sphere_near(s_cf[j], sp, margin);
+          const uint64_t m = ballot(near);
+          if (m) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&s_nl[ks], (int)__popcll(m));
+            base = __shfl(base, 0);
+            if (near) out[base + lanes_below(m)] = (uint16_t)j;
+          }
+        }
+      }
+      __syncthreads();
+      if (t < P && k0 + t < ns) lp_n[h0 + k0 + t] = s_nl[t];
+    }
   }
 }
 
@@ -633,10 +692,13 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) return;
   const int64_t ns = sp_supers(v.n);
   const int ls = prune_list_stride(D);
-  const unsigned ga = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2 * num_cus, ns));
+  // hypers of H super-tiles (H <= 32, a power of two), as large as keeps >= 2 workgroups per CU
+  int H = 1;
+  while (H < 32 && ns / (2 * H) >= 2 * (int64_t)num_cus) H *= 2;
+  const unsigned ga = (unsigned)std::max<int64_t>(1, (ns + H - 1) / H);
   int32_t* work = lp_n + ns;  // (lp_n holds sp_supers(n) + 1 entries)
   hipLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, v.supers, (int)ns, hyps, D, ls,
-                     margin, lp, lp_n, work);
+                     margin, H, lp, lp_n, work);
   // one 1024-thread workgroup per CU (LDS + VGPRs); its waves claim 2-tile items dynamically,
   // each workgroup capped at blk_cap items (16-bit LDS counters: <= 65535 points per
   // workgroup), and enough workgroups that the caps cover every item
