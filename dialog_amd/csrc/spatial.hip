@@ -68,7 +68,8 @@ __global__ void k_gather_order(PointsView src, const int32_t* __restrict__ order
 // points, two super-tiles) in LDS with coalesced loads (padded rows: lane l reads row l without
 // bank conflicts), each lane reduces its tile's box and radius, then the 32 lanes of a super-tile
 // combine their spheres.  ~4x less VALU work than a half-wave per tile.
-constexpr int kSb2Pts = 2 * kSuperP;  // points per wave (64 tiles)
+constexpr int kSb2Pts = kWave * kTileP;  // points per wave (64 tiles)
+constexpr int kSb2Sup = kWave / kSuperTiles;  // super-tiles per wave
 __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__ X,
                                                        const float* __restrict__ Y,
                                                        const float* __restrict__ Z, int64_t n_arg,
@@ -115,10 +116,10 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
   const float rt = d * (1.0f + 0x1p-18f) + 1e-30f;
   const int64_t t = (int64_t)blockIdx.x * (kSb2Pts / kTileP) + lane;
   if (np > 0) tiles[t] = make_float4(cx, cy, cz, rt);
-  // super-tile of lanes 0..31 / 32..63: box over its tiles, then max |c_t - C| + r_t
+  // super-tile of each kSuperTiles lanes: box over its tiles, then max |c_t - C| + r_t
   float bx0 = x0, by0 = y0, bz0 = z0, bx1 = x1, by1 = y1, bz1 = z1;
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
+  for (int o = 1; o < kSuperTiles; o <<= 1) {
     bx0 = fminf(bx0, __shfl_xor(bx0, o)); by0 = fminf(by0, __shfl_xor(by0, o));
     bz0 = fminf(bz0, __shfl_xor(bz0, o));
     bx1 = fmaxf(bx1, __shfl_xor(bx1, o)); by1 = fmaxf(by1, __shfl_xor(by1, o));
@@ -131,10 +132,10 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
     R = sqrtf(dx * dx + dy * dy + dz * dz) + rt;
   }
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) R = fmaxf(R, __shfl_xor(R, o));
-  const int half = lane >> 5;
-  if ((lane & 31) == 0 && half * kSuperP < cnt)
-    supers[(int64_t)blockIdx.x * 2 + half] = make_float4(Cx, Cy, Cz, R * (1.0f + 0x1p-18f) + 1e-30f);
+  for (int o = 1; o < kSuperTiles; o <<= 1) R = fmaxf(R, __shfl_xor(R, o));
+  const int sub = lane / kSuperTiles;
+  if ((lane % kSuperTiles) == 0 && sub * kSuperP < cnt)
+    supers[(int64_t)blockIdx.x * kSb2Sup + sub] = make_float4(Cx, Cy, Cz, R * (1.0f + 0x1p-18f) + 1e-30f);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
   __shared__ uint16_t s_hl[kMaxHypPerLaunch];  // the planes near this hyper's sphere
   __shared__ float4 s_sp[kWave];
   __shared__ float4 s_hyp;
-  __shared__ int s_nh, s_nl[kPrWaves];
+  __shared__ int s_nh;
   const int t = threadIdx.x, lane = t & (kWave - 1);
   if (blockIdx.x == 0 && t == 0) *work = 0;  // k_score_tiles_rl's item counter
   for (int j = t; j < D; j += kPrBS) {
@@ -223,34 +224,22 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
       }
     }
     __syncthreads();
-    // the near planes against the super-tiles, P super-tiles at a time (a slice of SL = kPrBS / P
-    // threads each, a multiple of the wave: a wave's lanes serve one super-tile)
-    const int nh = s_nh;
-    int P = 1;
-    while (P < ns && P < kPrWaves && (kPrBS / (2 * P)) >= nh) P *= 2;
-    const int SL = kPrBS / P, ks = t / SL, it = t % SL;
-    for (int k0 = 0; k0 < ns; k0 += P) {
-      const int k = k0 + ks;
-      if (t < P) s_nl[t] = 0;
-      __syncthreads();
-      if (k < ns) {
-        const float4 sp = s_sp[k];
-        uint16_t* out = lp + (h0 + k) * ls;
-        for (int b = 0; b < nh; b += SL) {  // uniform per wave
-          const int i = b + it;
-          const int j = i < nh ? (int)s_hl[i] : 0;
-          const bool near = i < nh && sphere_near(s_cf[j], sp, margin);
-          const uint64_t m = ballot(near);
-          if (m) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&s_nl[ks], (int)__popcll(m));
-            base = __shfl(base, 0);
-            if (near) out[base + lanes_below(m)] = (uint16_t)j;
-          }
-        }
+    // the near planes against the super-tiles: one wave per super-tile (no workgroup barrier),
+    // list positions from the wave's own running count
+    const int nh = s_nh, w = t / kWave;
+    for (int k = w; k < ns; k += kPrWaves) {
+      const float4 sp = s_sp[k];
+      uint16_t* out = lp + (h0 + k) * ls;
+      int cnt = 0;
+      for (int b = 0; b < nh; b += kWave) {
+        const int i = b + lane;
+        const int j = i < nh ? (int)s_hl[i] : 0;
+        const bool near = i < nh && sphere_near(s_cf[j], sp, margin);
+        const uint64_t m = ballot(near);
+        if (near) out[cnt + lanes_below(m)] = (uint16_t)j;
+        cnt += (int)__popcll(m);
       }
-      __syncthreads();
-      if (t < P && k0 + t < ns) lp_n[h0 + k0 + t] = s_nl[t];
+      if (lane == 0) lp_n[h0 + k] = cnt;
     }
   }
 }

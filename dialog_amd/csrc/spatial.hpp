@@ -26,7 +26,7 @@
 namespace dlg {
 
 constexpr int kTileP = 32;       // points per tile (the 32 rows of one MFMA block)
-constexpr int kSuperTiles = 32;  // tiles per super-tile
+constexpr int kSuperTiles = 16;  // tiles per super-tile (a power of two <= 32)
 constexpr int kSuperP = kTileP * kSuperTiles;
 
 inline int64_t sp_tiles(int64_t n) { return (n + kTileP - 1) / kTileP; }
