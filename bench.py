@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--torch-dist", action="store_true",
                     help="rendezvous through torch.distributed even at N=1 (runtime check)")
+    ap.add_argument("--select-tile", type=int, default=0,
+                    help="points per single-pass select tile (DLG_OPT_SELECT_TILE; 0: library default)")
     ap.add_argument("--no-events", action="store_true",
                     help="no HIP timing events in the timed steps (A/B of their host cost)")
     ap.add_argument("--no-secondary", action="store_true",
@@ -158,6 +160,8 @@ def main():
     else:
         ctx = D.Context(local)
     ctx.set_profiling(not a.no_events)
+    if a.select_tile:
+        ctx.set_option(D.DLG_OPT_SELECT_TILE, a.select_tile)
 
     strong = a.global_points > 0
     if strong:  # C4: one global cloud sharded over the ranks (last rank takes the remainder)

@@ -38,6 +38,7 @@ DLG_OPT_SPEC_PICK = 3
 DLG_OPT_PRUNE_NP = 4
 DLG_OPT_SCORE_KERNEL = 5
 DLG_OPT_PRUNE_STATS = 6
+DLG_OPT_SELECT_TILE = 7
 DLG_SCORE_EXACT = 0
 DLG_SCORE_BF16 = 1
 DLG_SCORE_PRUNED = 2

@@ -483,19 +483,43 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
     }
     if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    // the speculative pick: fused into the pruned scoring's last workgroup on one rank (at N > 1
+    // it needs the allreduced counts: its own launch after the collective)
+    PickArgs pk;
+    if (speculate) {
+      pk.res = c->res.p;
+      pk.Dp = Dp;
+      pk.D = D;
+      pk.need_good = prm.max_iterations + 1;
+      pk.hyps = c->hyps.p;
+      pk.samples = c->samples.p;
+      pk.best = best_dev;
+      pk.best_smp = best_smp_dev;
+      pk.out = c->pick.p;
+    }
+    const bool fuse_pick = speculate && (pruned_np || (!np && pruned)) && c->comm->world() == 1;
+    if (fuse_pick) {
+      if (!c->pick_done.p) {
+        c->pick_done.ensure(1);
+        HIPCHK(hipMemsetAsync(c->pick_done.p, 0, sizeof(unsigned), c->stream));
+      }
+      pk.done = c->pick_done.p;
+    }
     if (pruned_np) {
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
       const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold};
       launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
-                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), &npp);
+                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), &npp,
+                          fuse_pick ? &pk : nullptr);
     } else if (np)
       launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
     else if (pruned) {
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
       launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
-                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c));
+                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), nullptr,
+                          fuse_pick ? &pk : nullptr);
     } else
       launch_score(src, c->hyps.p, D, cthr, c->res.p, c->opt.score_kernel, c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
@@ -507,8 +531,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (speculate) {
       // (the counts and the pick come back with the round's totals: a copy here would sit
       // between the scoring and the pick on the stream)
-      launch_pick_p1(c->res.p, Dp, D, prm.max_iterations + 1, c->hyps.p, c->samples.p, best_dev,
-                     best_smp_dev, c->pick.p, c->stream);
+      if (!fuse_pick) launch_pick_p1(pk, c->stream);
       HIPCHK(hipGetLastError());
       spec_pending = true;
       spec_D = D;
@@ -709,7 +732,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       if (ss.with_nrm) spv.nrm = ss.nrm.p;  // (a later NORMAL_PLANE round reads them)
       else spo.nrm = nullptr;
       launch_sel1_morton(spv, rc_dev, mt, c->sel1, cl->tag.p, (uint8_t)cl->tagv, spo, src.n,
-                         c->totals.p, c->stream, fused_pub ? &pa : nullptr);
+                         c->totals.p, c->stream, fused_pub ? &pa : nullptr, c->opt.sel1_tile);
     } else {
       launch_select_head(src, rc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
                          c->totals.p, c->stream);
@@ -723,8 +746,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (lean) {
       // the list from the stamps (ids in list order; survivors' pristine indices), then the
       // sphere bounds of the Morton survivors (count in totals[4])
-      launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv, cl->pristine.gid.p, c->sel1,
-                       c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream);
+      launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv,
+                       cl->gid_ident ? nullptr : cl->pristine.gid.p, cl->id_base, c->sel1,
+                       c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream, c->opt.sel1_tile);
       const int b = cl->sp_spare();
       SoA& sd = cl->sp_buf[b];
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
@@ -1108,6 +1132,7 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     cl->n_total = n;
     cl->n_points = pts->n;
     cl->id_base = id_base;
+    cl->gid_ident = indices == nullptr;
     cl->n_active = n;
     cl->pristine.ensure((size_t)std::max<int64_t>(n, 1));
     if (indices)
@@ -1466,6 +1491,11 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
           HIPCHK(hipMemsetAsync(c->pstats.p, 0, 8 * sizeof(unsigned long long), c->stream));
         }
         break;
+      case DLG_OPT_SELECT_TILE:
+        if (value != kSel1Points[0] && value != kSel1Points[1] && value != kSel1Points[2])
+          throw DlgError(DLG_ERR_INVALID, "DLG_OPT_SELECT_TILE: 4096, 8192 or 16384");
+        o.sel1_tile = (int)value;
+        break;
       default: throw DlgError(DLG_ERR_INVALID, "unknown option");
     }
   });
@@ -1481,6 +1511,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_PRUNE_NP: *value = o.prune_np; break;
     case DLG_OPT_SCORE_KERNEL: *value = o.score_kernel == kScoreExact ? DLG_SCORE_EXACT : DLG_SCORE_BF16; break;
     case DLG_OPT_PRUNE_STATS: *value = o.prune_stats; break;
+    case DLG_OPT_SELECT_TILE: *value = o.sel1_tile; break;
     default: return DLG_ERR_INVALID;
   }
   return DLG_OK;

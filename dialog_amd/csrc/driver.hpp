@@ -161,6 +161,7 @@ struct PathOptions {
   bool prune_np = true;   // pruned NORMAL_PLANE scoring
   int score_kernel = kScoreBf16;  // exhaustive scorer: kScoreBf16 or kScoreExact
   bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
+  int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
 };
 
 struct dlg_ctx {
@@ -181,6 +182,7 @@ struct dlg_ctx {
   DevBuf<uint64_t> sel1_status;
   DevBuf<int32_t> sel1_err;  // sticky look-back failure word of the single-pass selects
   DevBuf<int64_t> partials, moments;  // fast refit: exact moment digits (exact_refit.hpp)
+  DevBuf<unsigned> pick_done;          // the fused pick's workgroup ticket (zero between launches)
   DevBuf<unsigned> mom_done;           // k_moments' last-workgroup counter (zero between launches)
   DevBuf<double> scratch_f64;          // max-allreduce of host doubles
   DevBuf<int32_t> inl_gid;
@@ -241,6 +243,7 @@ struct dlg_cloud {
   dlg_ctx* ctx = nullptr;
   int64_t n_points = 0;  // records of the uploaded dlg_points (normals must match)
   int32_t id_base = 0;
+  bool gid_ident = false;  // pristine gid[i] == id_base + i (uploaded without setIndices)
   bool has_normals = false;
   int64_t n_total = 0;
   int64_t n_active = 0;

@@ -16,6 +16,7 @@
 #include "spatial.hpp"
 #include "dev_common.hpp"
 #include "np_dev.hpp"
+#include "pick_dev.hpp"
 #include "host_math.hpp"
 #include "exact_refit.hpp"
 
@@ -128,17 +129,32 @@ __global__ void k_gather_build(const int32_t* pos, int D, int Dp, PointsView src
     hyps[d] = nan_hyp();
     return;
   }
+  // three dependent hops (positions over PCIe, list index, point): each hop's three loads are
+  // issued together, and no store sits between the hops
+  int64_t q[3];
+  bool ok[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) q[i] = pos[3 * d + i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    ok[i] = q[i] >= 0 && q[i] < n_list;
+    q[i] = ok[i] ? q[i] : 0;
+  }
+  if (lidx) {  // lean list: pristine index -> pristine copy
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (ok[i]) q[i] = lidx[q[i]];
+  }
   SampleRec r[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const int64_t p = pos[3 * d + i];
     r[i].gid = 0; r[i].x = 0.0f; r[i].y = 0.0f; r[i].z = 0.0f;
-    if (p >= 0 && p < n_list) {
-      const int64_t q = lidx ? lidx[p] : p;  // lean list: pristine index -> pristine copy
-      r[i].gid = src.gid[q]; r[i].x = src.x[q]; r[i].y = src.y[q]; r[i].z = src.z[q];
+    if (ok[i]) {
+      r[i].gid = src.gid[q[i]]; r[i].x = src.x[q[i]]; r[i].y = src.y[q[i]]; r[i].z = src.z[q[i]];
     }
-    samples[3 * d + i] = r[i];
   }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) samples[3 * d + i] = r[i];
   const HypRec h = build_hyp(r[0], r[1], r[2], cthr, ax, ay, az);
   hyps[d] = h;
   res[Dp + d] = h.good;  // good[D]
@@ -635,81 +651,7 @@ __global__ __launch_bounds__(kWave) void k_refit_moments(const int64_t* __restri
 // replays the same counts (RansacControl::consume) after the round's sync and redoes the round
 // on any disagreement.  One workgroup.
 constexpr int kPickBS = 1024;
-__global__ __launch_bounds__(kPickBS) void k_pick_p1(const int32_t* __restrict__ res, int Dp, int D,
-                                                     int need_good, const HypRec* __restrict__ hyps,
-                                                     const SampleRec* __restrict__ samples,
-                                                     HypRec* __restrict__ best,
-                                                     SampleRec* __restrict__ best_smp,
-                                                     int32_t* __restrict__ out) {
-  __shared__ int s_good[kPickBS / kWave], s_bad[kPickBS / kWave];
-  __shared__ unsigned long long s_key[kPickBS / kWave];
-  __shared__ int s_end;
-  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
-  const int per = (D + kPickBS - 1) / kPickBS;
-  const int d0 = min(D, t * per), d1 = min(D, d0 + per);
-  int g = 0, b = 0;
-  for (int d = d0; d < d1; ++d) {
-    if (res[Dp + d]) ++g; else ++b;
-  }
-  // block exclusive scan of the good counts (wave scans + wave totals)
-  int incl = g;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  int bt = b;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) bt += __shfl_xor(bt, o);
-  if (lane == kWave - 1) s_good[w] = incl;
-  if (lane == 0) s_bad[w] = bt;
-  if (t == 0) s_end = -1;
-  __syncthreads();
-  int base = 0, total_good = 0, total_bad = 0;
-  for (int q = 0; q < kPickBS / kWave; ++q) {
-    base += q < w ? s_good[q] : 0;
-    total_good += s_good[q];
-    total_bad += s_bad[q];
-  }
-  base += incl - g;
-  // the draw at which the need_good-th good draw happens
-  if (base < need_good && base + g >= need_good) {
-    int c = base;
-    for (int d = d0; d < d1; ++d)
-      if (res[Dp + d] && ++c == need_good) { s_end = d; break; }
-  }
-  __syncthreads();
-  const int end = s_end;  // -1: the loop goes on past this batch
-  // first maximum over the good draws up to the end: key = (count, ~index)
-  unsigned long long key = 0ull;
-  for (int d = d0; d < d1; ++d) {
-    if (end >= 0 && d > end) break;
-    if (!res[Dp + d]) continue;
-    const unsigned long long k = ((unsigned long long)(uint32_t)res[d] << 32) |
-                                 (unsigned long long)(0xFFFFFFFFu - (uint32_t)d);
-    key = k > key ? k : key;
-  }
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const unsigned long long v = __shfl_xor(key, o);
-    key = v > key ? v : key;
-  }
-  if (lane == 0) s_key[w] = key;
-  __syncthreads();
-  if (t == 0) {
-    unsigned long long k = 0ull;
-    for (int q = 0; q < kPickBS / kWave; ++q) k = s_key[q] > k ? s_key[q] : k;
-    const int bd = k ? (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : -1;
-    out[0] = bd;
-    out[1] = (end >= 0 && total_bad < 1000 && total_good >= need_good) ? 1 : 0;
-    if (bd >= 0) {
-      *best = hyps[bd];
-      best_smp[0] = samples[3 * bd];
-      best_smp[1] = samples[3 * bd + 1];
-      best_smp[2] = samples[3 * bd + 2];
-    }
-  }
-}
+__global__ __launch_bounds__(kPickBS) void k_pick_p1(PickArgs a) { pick_body<kPickBS, false>(a); }
 
 // ---------------------------------------------------------------------------------------------
 // k_publish: the round's small results (select totals, winner + refined plane, every rank's
@@ -875,19 +817,21 @@ __global__ __launch_bounds__(kSelBS) void k_select_scatter(PointsView src,
 // order (PCL's order) -- 9 B per list point instead of the 44 B of count + scatter over the
 // list-ordered xyz.
 //
-// Both are one pass: a workgroup claims the next 4096-point tile from a monotone counter, counts
-// its inliers, and takes its exclusive prefix by decoupled look-back over the tile status words
-// (epoch << 32 | flag << 30 | value; flag 1 = tile aggregate, 2 = inclusive prefix).  Tiles are
-// claimed in order, so every tile a workgroup waits on is already running: the look-back always
-// completes.  Survivor positions need no second scan: every tile but the last is full, so the
-// survivors before element e of tile t are t * 4096 + local(e) - (inliers before e).
-// (large tiles keep the look-back short: a round's few hundred tiles are all resident at once,
-// and each look-back window of 64 tiles costs one uncached round trip)
-constexpr int kS1BS = 1024;
-constexpr int kS1It = 16;                          // points per lane, lane-strided
-constexpr int kS1Tile = kS1BS * kS1It;             // 16384 points per tile
-constexpr int kS1Slots = kS1It * (kS1BS / kWave);  // (j, wave) counts of a tile: 256
-static_assert(kS1Slots % kWave == 0 && kS1Slots <= kS1BS, "slot scan layout");
+// Both are one pass: workgroup t takes tile t (BS threads x 16 points, BS = 256 / 512 / 1024:
+// 4096 / 8192 / 16384-point tiles, kSel1Points), counts its inliers, and takes its exclusive
+// prefix by decoupled look-back over the tile status words (epoch << 32 | flag << 30 | value;
+// flag 1 = tile aggregate, 2 = inclusive prefix).  Survivor positions need no second scan: every
+// tile but the last is full, so the survivors before element e of tile t are t * tile + local(e)
+// - (inliers before e).  Large tiles keep the look-back short (each window of 64 tiles costs one
+// uncached round trip); small ones let several workgroups share a CU, so one tile's loads
+// overlap another's scan and scatter (one 1024-thread workgroup of 128 VGPRs fills a CU alone).
+constexpr int kS1It = 16;  // points per lane, lane-strided
+template <int BS>
+struct S1 {
+  static constexpr int kTile = BS * kS1It;
+  static constexpr int kSlots = kS1It * (BS / kWave);  // (j, wave) counts of a tile
+  static_assert(kSlots % kWave == 0 && kSlots <= BS, "slot scan layout");
+};
 
 // tile = workgroup index: workgroups are dispatched in index order on each XCD, so the lowest
 // unfinished tile has every predecessor done and always completes (a claim counter would be
@@ -902,8 +846,10 @@ constexpr int kS1Spin = 1 << 20;
 
 // in-tile exclusive ranks from the (j, wave) counts in s_cnt, the tile's exclusive prefix by
 // look-back; returns the prefix (workgroup-uniform), s_pre[] = in-tile exclusive offsets
+template <int BS>
 __device__ __forceinline__ int sel1_scan(const Sel1State& L, int tile, int* s_cnt, int* s_pre,
                                          int* s_base) {
+  constexpr int kS1Slots = S1<BS>::kSlots;
   __shared__ int s_wt[kS1Slots / kWave];
   __syncthreads();
   const int t = threadIdx.x, lane = t & (kWave - 1);
@@ -1017,12 +963,13 @@ __device__ __forceinline__ int sel1_scan(const Sel1State& L, int tile, int* s_cn
 // totals[0] = inliers, totals[1] = list survivors (n_list - inliers), totals[4] = Morton survivors
 // pa.pub non-null: the last tile also publishes the round (publish_body) once its totals are
 // final, without waiting for the other tiles' scatters (nothing published depends on them)
-template <bool NP>
+template <bool NP, int kS1BS>
 __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const float4* __restrict__ cfp,
                                                        ModelTest mt, Sel1State L,
                                                        uint8_t* __restrict__ tag, uint8_t tagv,
                                                        PointsOut dst, int64_t n_list, int ntiles,
                                                        int32_t* __restrict__ totals, PubArgs pa) {
+  constexpr int kS1Slots = S1<kS1BS>::kSlots, kS1Tile = S1<kS1BS>::kTile;
   __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
   const int tile = blockIdx.x;
   const float4 cf = *cfp;
@@ -1046,7 +993,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const flo
     m[j] = ballot(in);
     if ((threadIdx.x & (kWave - 1)) == 0) s_cnt[j * (kS1BS / kWave) + w] = __popcll(m[j]);
   }
-  const int excl = sel1_scan(L, tile, s_cnt, s_pre, s_base);
+  const int excl = sel1_scan<kS1BS>(L, tile, s_cnt, s_pre, s_base);
   if (excl < 0) return;  // (look-back failed: *L.err is set)
 #pragma unroll
   for (int j = 0; j < kS1It; ++j) {
@@ -1078,13 +1025,15 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const flo
 // the active list's compaction from the stamps: lidx = pristine index per list point (null: the
 // pristine list, lidx[e] = e); inliers -> inl_gid (their ids, list order), survivors' pristine
 // indices -> out_lidx; the last tile writes totals[0..1] = (inliers, survivors)
-template <bool IDENT>
+template <bool IDENT, bool GID_IDENT, int kS1BS>
 __global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__ lidx, int64_t n,
                                                      const uint8_t* __restrict__ tag, uint8_t tagv,
-                                                     const int32_t* __restrict__ pgid, Sel1State L,
+                                                     const int32_t* __restrict__ pgid, int32_t gid_base,
+                                                     Sel1State L,
                                                      int32_t* __restrict__ inl_gid,
                                                      int32_t* __restrict__ out_lidx, int ntiles,
                                                      int32_t* __restrict__ totals) {
+  constexpr int kS1Slots = S1<kS1BS>::kSlots, kS1Tile = S1<kS1BS>::kTile;
   __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
   const int tile = blockIdx.x;
   const int w = threadIdx.x / kWave;
@@ -1111,8 +1060,8 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__
   int32_t gi[kS1It];
 #pragma unroll
   for (int j = 0; j < kS1It; ++j)
-    gi[j] = pgid[((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull) ? p[j] : p[0]];
-  const int excl = sel1_scan(L, tile, s_cnt, s_pre, s_base);
+    gi[j] = GID_IDENT ? gid_base + p[j] : pgid[((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull) ? p[j] : p[0]];
+  const int excl = sel1_scan<kS1BS>(L, tile, s_cnt, s_pre, s_base);
   if (excl < 0) return;  // (look-back failed: *L.err is set)
 #pragma unroll
   for (int j = 0; j < kS1It; ++j) {
@@ -1321,15 +1270,37 @@ void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleR
                      lidx, lidx ? n_list : src.n, samples, cthr, ax, ay, az, hyps, res);
 }
 
-int sel1_tiles(int64_t n) { return (int)((n + kS1Tile - 1) / kS1Tile); }
+int sel1_tiles(int64_t n) { return (int)((n + kSel1Points[0] - 1) / kSel1Points[0]); }
 
 // single-pass selects (lean-list rounds): every launch stamps its status words with a fresh epoch
 static void sel1_next(Sel1State& L, int) { ++L.epoch; }
 
+template <bool NP, int BS>
+static void sel1_morton_bs(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
+                           uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
+                           int nt, int32_t* totals, hipStream_t s, const PubArgs& pa) {
+  hipLaunchKernelGGL((k_sel1_morton<NP, BS>), dim3(nt), dim3(BS), 0, s, sp, coef, mt, L, tag, tagv,
+                     dst, n_list, nt, totals, pa);
+}
+
+template <bool NP>
+static void sel1_morton_np(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
+                           uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
+                           int nt, int32_t* totals, hipStream_t s, const PubArgs& pa, int bs) {
+  if (bs == 256) sel1_morton_bs<NP, 256>(sp, coef, mt, L, tag, tagv, dst, n_list, nt, totals, s, pa);
+  else if (bs == 512) sel1_morton_bs<NP, 512>(sp, coef, mt, L, tag, tagv, dst, n_list, nt, totals, s, pa);
+  else sel1_morton_bs<NP, 1024>(sp, coef, mt, L, tag, tagv, dst, n_list, nt, totals, s, pa);
+}
+
+static int sel1_bs(int tile_pts) {
+  return tile_pts == kSel1Points[0] ? 256 : tile_pts == kSel1Points[1] ? 512 : 1024;
+}
+
 void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
                         uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
-                        int32_t* totals, hipStream_t s, const PubArgs* pub) {
-  const int nt = sel1_tiles(sp.n);
+                        int32_t* totals, hipStream_t s, const PubArgs* pub, int tile_pts) {
+  const int bs = sel1_bs(tile_pts);
+  const int nt = (int)((sp.n + bs * kS1It - 1) / (bs * kS1It));
   if (nt == 0) {
     hipLaunchKernelGGL(k_sel1_empty, dim3(1), dim3(1), 0, s, n_list, totals);
     if (pub) hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, *pub);
@@ -1339,28 +1310,47 @@ void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, 
   PubArgs pa{};
   if (pub) pa = *pub;
   if (mt.normal_plane)
-    hipLaunchKernelGGL(k_sel1_morton<true>, dim3(nt), dim3(kS1BS), 0, s, sp, coef, mt, L, tag,
-                       tagv, dst, n_list, nt, totals, pa);
+    sel1_morton_np<true>(sp, coef, mt, L, tag, tagv, dst, n_list, nt, totals, s, pa, bs);
   else
-    hipLaunchKernelGGL(k_sel1_morton<false>, dim3(nt), dim3(kS1BS), 0, s, sp, coef, mt, L, tag,
-                       tagv, dst, n_list, nt, totals, pa);
+    sel1_morton_np<false>(sp, coef, mt, L, tag, tagv, dst, n_list, nt, totals, s, pa, bs);
+}
+
+template <bool IDENT, bool GID_IDENT>
+static void sel1_list_k(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_t tagv,
+                        const int32_t* pgid, int32_t gid_base, Sel1State& L, int32_t* inl_gid,
+                        int32_t* out_lidx, int nt, int32_t* totals, hipStream_t s, int bs) {
+  if (bs == 256)
+    hipLaunchKernelGGL((k_sel1_list<IDENT, GID_IDENT, 256>), dim3(nt), dim3(256), 0, s, lidx, n, tag,
+                       tagv, pgid, gid_base, L, inl_gid, out_lidx, nt, totals);
+  else if (bs == 512)
+    hipLaunchKernelGGL((k_sel1_list<IDENT, GID_IDENT, 512>), dim3(nt), dim3(512), 0, s, lidx, n, tag,
+                       tagv, pgid, gid_base, L, inl_gid, out_lidx, nt, totals);
+  else
+    hipLaunchKernelGGL((k_sel1_list<IDENT, GID_IDENT, 1024>), dim3(nt), dim3(1024), 0, s, lidx, n,
+                       tag, tagv, pgid, gid_base, L, inl_gid, out_lidx, nt, totals);
 }
 
 void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_t tagv,
-                      const int32_t* pgid, Sel1State& L, int32_t* inl_gid, int32_t* out_lidx,
-                      int32_t* totals, hipStream_t s) {
-  const int nt = sel1_tiles(n);
+                      const int32_t* pgid, int32_t gid_base, Sel1State& L, int32_t* inl_gid,
+                      int32_t* out_lidx, int32_t* totals, hipStream_t s, int tile_pts) {
+  const int bs = sel1_bs(tile_pts);
+  const int nt = (int)((n + bs * kS1It - 1) / (bs * kS1It));
   if (nt == 0) {
     (void)hipMemsetAsync(totals, 0, 2 * sizeof(int32_t), s);
     return;
   }
   sel1_next(L, nt);
-  if (lidx)
-    hipLaunchKernelGGL(k_sel1_list<false>, dim3(nt), dim3(kS1BS), 0, s, lidx, n, tag, tagv, pgid,
-                       L, inl_gid, out_lidx, nt, totals);
-  else
-    hipLaunchKernelGGL(k_sel1_list<true>, dim3(nt), dim3(kS1BS), 0, s, lidx, n, tag, tagv, pgid,
-                       L, inl_gid, out_lidx, nt, totals);
+  if (lidx) {
+    if (pgid)
+      sel1_list_k<false, false>(lidx, n, tag, tagv, pgid, gid_base, L, inl_gid, out_lidx, nt, totals, s, bs);
+    else
+      sel1_list_k<false, true>(lidx, n, tag, tagv, pgid, gid_base, L, inl_gid, out_lidx, nt, totals, s, bs);
+  } else {
+    if (pgid)
+      sel1_list_k<true, false>(lidx, n, tag, tagv, pgid, gid_base, L, inl_gid, out_lidx, nt, totals, s, bs);
+    else
+      sel1_list_k<true, true>(lidx, n, tag, tagv, pgid, gid_base, L, inl_gid, out_lidx, nt, totals, s, bs);
+  }
 }
 
 void launch_list_materialize(PointsView pristine, int64_t n, const PointsOut& io, hipStream_t s) {
@@ -1502,11 +1492,8 @@ void launch_moments(PointsView src, const float4* coef, const ModelTest& mt, int
                        partials, done, out, qexp, nullptr);
 }
 
-void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
-                    const SampleRec* samples, HypRec* best, SampleRec* best_smp, int32_t* out,
-                    hipStream_t s) {
-  hipLaunchKernelGGL(k_pick_p1, dim3(1), dim3(kPickBS), 0, s, res, Dp, D, need_good, hyps, samples,
-                     best, best_smp, out);
+void launch_pick_p1(const PickArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_pick_p1, dim3(1), dim3(kPickBS), 0, s, a);
 }
 
 void launch_publish(const PubArgs& a, hipStream_t s) {

@@ -105,9 +105,18 @@ struct PubArgs {
 void launch_publish(const PubArgs& a, hipStream_t s);
 // speculative computeModel decision for probability 1 over one batch (k_pick_p1): out[0] best
 // batch index (-1 none), out[1] loop ended inside the batch; winner copied to best / best_smp
-void launch_pick_p1(const int32_t* res, int Dp, int D, int need_good, const HypRec* hyps,
-                    const SampleRec* samples, HypRec* best, SampleRec* best_smp, int32_t* out,
-                    hipStream_t s);
+struct PickArgs {
+  const int32_t* res = nullptr;  // counts[Dp] | good[D]
+  int Dp = 0, D = 0, need_good = 0;
+  const HypRec* hyps = nullptr;
+  const SampleRec* samples = nullptr;
+  HypRec* best = nullptr;
+  SampleRec* best_smp = nullptr;
+  int32_t* out = nullptr;
+  unsigned* done = nullptr;  // fused into the pruned scoring: its workgroup ticket (zero between
+                             // launches; the last workgroup resets it)
+};
+void launch_pick_p1(const PickArgs& a, hipStream_t s);
 // one rank: positions (pinned host buffer, 3 per draw) -> samples, hypotheses, good flags in
 // res[Dp + d] and zeroed counts res[0, Dp)  (gather + build + memset in one launch)
 // lidx: the lean list's pristine indices (src = the pristine copy, n_list = list length)
@@ -122,20 +131,24 @@ struct Sel1State {
   uint32_t epoch = 0;
   int32_t* err = nullptr;  // sticky: != 0 once a tile's look-back failed (host checks and clears)
 };
-// tiles (status words) of a single-pass select over n points
+// tiles (status words) a single-pass select over n points may use (the smallest tile size: an
+// upper bound for every kSel1Points choice)
 int sel1_tiles(int64_t n);
+// points per single-pass select tile (workgroups of tile / 16 threads, 16 points per lane)
+constexpr int kSel1Points[3] = {4096, 8192, 16384};
 // the Morton copy's select: survivors -> dst, inliers stamped tag[pristine index] = tagv;
 // totals[0] = inliers, totals[1] = n_list - inliers, totals[4] = Morton survivors
 // pub non-null: the last tile also publishes the round (as launch_publish) once the totals are
-// final
+// final.  tile_pts: one of kSel1Points
 void launch_sel1_morton(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,
                         uint8_t* tag, uint8_t tagv, const PointsOut& dst, int64_t n_list,
-                        int32_t* totals, hipStream_t s, const PubArgs* pub = nullptr);
+                        int32_t* totals, hipStream_t s, const PubArgs* pub, int tile_pts);
 // the lean list's compaction from the stamps (lidx null: the pristine list): inlier ids in list
-// order -> inl_gid, survivors' pristine indices -> out_lidx; totals[0..1] = (in, out)
+// order -> inl_gid, survivors' pristine indices -> out_lidx; totals[0..1] = (in, out).
+// pgid null: the pristine ids are gid_base + pristine index (an upload without setIndices)
 void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_t tagv,
-                      const int32_t* pgid, Sel1State& L, int32_t* inl_gid, int32_t* out_lidx,
-                      int32_t* totals, hipStream_t s);
+                      const int32_t* pgid, int32_t gid_base, Sel1State& L, int32_t* inl_gid,
+                      int32_t* out_lidx, int32_t* totals, hipStream_t s, int tile_pts);
 // a lean list's x, y, z, gid (+ normals) from the pristine copy, in place (io.gid holds the
 // pristine indices on entry)
 void launch_list_materialize(PointsView pristine, int64_t n, const PointsOut& io, hipStream_t s);

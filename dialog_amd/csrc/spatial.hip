@@ -10,6 +10,7 @@
 
 #include "dev_common.hpp"
 #include "np_dev.hpp"
+#include "pick_dev.hpp"
 
 namespace dlg {
 
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int chunk,
     const HypRec* __restrict__ hyps, int D, float cthr, float margin, float ax, float ay,
     float az, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats,
-    const float4* __restrict__ NRM, double lambda, double thr) {
+    const float4* __restrict__ NRM, double lambda, double thr, PickArgs pick_args) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves: <= 65535 points per workgroup
   __shared__ uint16_t s_ring[(BS / kWave)][kRing2];
@@ -565,6 +566,21 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     if (c) atomicAdd(&counts[j], c);
   }
   if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
+  if (pick_args.done) {
+    // the speculative pick in the launch's last workgroup (no k_pick_p1 launch and no gap on the
+    // round's critical path): this workgroup's count atomics are acknowledged (vmcnt) before it
+    // takes its ticket, and the last one reads the sums with device-coherent loads
+    __builtin_amdgcn_s_waitcnt(0);
+    __shared__ unsigned s_ticket;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_ticket = __hip_atomic_fetch_add(pick_args.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_ticket != gridDim.x - 1) return;
+    if (threadIdx.x == 0)  // (the next launch on this stream starts from zero)
+      __hip_atomic_store(pick_args.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pick_body<BS, true>(pick_args);
+  }
 }
 
 __global__ void k_gather_nrm(const float4* __restrict__ src, const int32_t* __restrict__ order,
@@ -677,8 +693,12 @@ float np_lim_max(double w, double thr) {  // np_de_limit (np_dev.hpp) on the hos
 
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float cthr, float margin,
                          const float amax[3], int32_t* counts, uint16_t* lp, int32_t* lp_n,
-                         int num_cus, hipStream_t s, unsigned long long* stats, const PrunedNp* np) {
-  if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) return;
+                         int num_cus, hipStream_t s, unsigned long long* stats, const PrunedNp* np,
+                         const PickArgs* pick) {
+  if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) {
+    if (pick) launch_pick_p1(*pick, s);  // (nothing to score: the pick still runs)
+    return;
+  }
   const int64_t ns = sp_supers(v.n);
   const int ls = prune_list_stride(D);
   // hypers of H super-tiles (H <= 32, a power of two), as large as keeps >= 2 workgroups per CU
@@ -702,6 +722,6 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(kBS), 0, s, v.x, v.y, v.z, (int)v.n, v.tiles, lp,
                      ls, lp_n, work, blk_cap, kChunkTiles, hyps, D, cthr, margin, amax[0], amax[1],
                      amax[2], counts, stats, np ? np->nrm : nullptr, np ? np->lambda : 0.0,
-                     np ? np->thr : 0.0);
+                     np ? np->thr : 0.0, pick ? *pick : PickArgs{});
 }
 }  // namespace dlg

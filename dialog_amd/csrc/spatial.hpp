@@ -83,7 +83,8 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
                          const float amax[3], int32_t* counts, uint16_t* lp, int32_t* lp_n,
                          int num_cus, hipStream_t s,
                          unsigned long long* stats = nullptr,  // [6] counters (A/B tool)
-                         const PrunedNp* np = nullptr);
+                         const PrunedNp* np = nullptr,
+                         const PickArgs* pick = nullptr);  // fused speculative pick (one rank)
 // the NORMAL_PLANE prefilter limit of the largest w (host restatement of np_de_limit): every
 // point's d_euclid limit is <= this when 0 <= w < 1 for all points; +inf otherwise
 float np_lim_max(double w_max, double thr);

@@ -338,7 +338,9 @@ enum {
   DLG_OPT_PRUNE_NP = 4,     /* 1 (default): pruned SACMODEL_NORMAL_PLANE scoring; 0: exhaustive */
   DLG_OPT_SCORE_KERNEL = 5, /* exhaustive scorer (no Morton copy): DLG_SCORE_BF16 (default) or
                                DLG_SCORE_EXACT */
-  DLG_OPT_PRUNE_STATS = 6   /* 1: count the pruned kernel's work (dlg_prune_stats); 0 (default) */
+  DLG_OPT_PRUNE_STATS = 6,  /* 1: count the pruned kernel's work (dlg_prune_stats); 0 (default) */
+  DLG_OPT_SELECT_TILE = 7   /* points per tile of the lean rounds' single-pass selects: 4096,
+                               8192 or 16384 (default) */
 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
 dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);

@@ -253,7 +253,9 @@ def test_path_options_identical(gpu_ctx, seed):
     ref = O.extract_planes(p, 0.02, max_planes=6, min_inliers=50, **kw)
     prm = D.make_params(0.02, **kw)
     combos = [dict(), {D.DLG_OPT_LEAN_ROUNDS: 0}, {D.DLG_OPT_SPEC_PICK: 0},
-              {D.DLG_OPT_PRUNE: 0}, {D.DLG_OPT_PRUNE: 0, D.DLG_OPT_SCORE_KERNEL: D.DLG_SCORE_EXACT}]
+              {D.DLG_OPT_PRUNE: 0}, {D.DLG_OPT_PRUNE: 0, D.DLG_OPT_SCORE_KERNEL: D.DLG_SCORE_EXACT},
+              {D.DLG_OPT_SELECT_TILE: 4096}, {D.DLG_OPT_SELECT_TILE: 8192},
+              {D.DLG_OPT_SELECT_TILE: 16384}]
     for opts in combos:
         ctx = D.Context(0)
         try:
