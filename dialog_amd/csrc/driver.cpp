@@ -605,18 +605,22 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     HIPCHK(hipMemsetAsync(cl->tag.p, 0, cl->tag.cap, c->stream));
     cl->tagv = 0;
   }
+  // before the first launch of a round that writes inl_gid: the previous round's inlier copy
+  // (copy stream) may still read it.  A stream wait only when the copy is still running (it
+  // has almost always landed by then); placed at the writer, not at the round's start, so a
+  // wait never sits between the scoring and the refit on the critical path.
+  auto stage_wait = [&]() {
+    if (!c->stage_inflight) return;
+    const hipError_t q = hipEventQuery(c->ev_stage);
+    if (q == hipErrorNotReady) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_stage, 0));
+    else HIPCHK(q);
+    c->stage_inflight = false;
+  };
   auto refit_select = [&]() {
     // Fast mode (and no optimisation) never leave the device: moments of the unrefined plane's
     // inliers (k_moments, centred on the winning sample), the double eigen33 refit in a
     // one-thread kernel, then the select with the refined plane read from device memory.  PCL
     // mode needs the host's sequential float sums in between.
-    if (c->stage_inflight) {  // the previous round's inlier copy still reads inl_gid
-      // (a stream wait only when the copy is still running: it has almost always landed)
-      const hipError_t q = hipEventQuery(c->ev_stage);
-      if (q == hipErrorNotReady) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_stage, 0));
-      else HIPCHK(q);
-      c->stage_inflight = false;
-    }
     const int sk = c->sel_k;  // this round's pair of select timing events
     if (c->profiling) {
       for (auto& ev : c->ev_sel[sk])
@@ -658,6 +662,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     } else {
       // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
       c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
+      stage_wait();
       launch_select(src, bc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p, c->totals.p,
                     c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
       HIPCHK(hipMemcpyAsync(c->h_tot.p, c->totals.p, 8, hipMemcpyDeviceToHost, c->stream));
@@ -746,6 +751,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (lean) {
       // the list from the stamps (ids in list order; survivors' pristine indices), then the
       // sphere bounds of the Morton survivors (count in totals[4])
+      stage_wait();
       launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv,
                        cl->gid_ident ? nullptr : cl->pristine.gid.p, cl->id_base, c->sel1,
                        c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream, c->opt.sel1_tile);
@@ -756,6 +762,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
                            cl->sp_sb[b].p, c->stream);
     } else {
+      stage_wait();
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
                          nullptr, compact ? &dst : nullptr, c->stream);
     }

@@ -1466,7 +1466,9 @@ void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& m
 }
 
 int moments_sp_blocks(int64_t n) {
-  return (int)std::max<int64_t>(1, std::min<int64_t>(256, sp_supers(n)));
+  // (2 waves/SIMD at 228 VGPRs: 512 four-wave workgroups are all resident at once, so each wave
+  // walks half as many near super-tiles as with 256; the last workgroup reduces <= 512 partials)
+  return (int)std::max<int64_t>(1, std::min<int64_t>(512, sp_supers(n)));
 }
 
 void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers, float margin,

@@ -37,11 +37,22 @@ __device__ __forceinline__ void pick_body(const PickArgs& a) {
   const int32_t* __restrict__ res = a.res;
   const int Dp = a.Dp, D = a.D, need_good = a.need_good;
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  // (D <= kMaxHypPerLaunch: at most kPer draws per thread, their flags and counts loaded
+  // together up front -- the fused pick's coherent loads would otherwise wait out one by one)
+  constexpr int kPer = (kMaxHypPerLaunch + NT - 1) / NT;
   const int per = (D + NT - 1) / NT;
   const int d0 = min(D, t * per), d1 = min(D, d0 + per);
+  int gf[kPer], cnt[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) gf[i] = d0 + i < d1 ? res[Dp + d0 + i] : 0;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) cnt[i] = d0 + i < d1 ? pick_count<COH>(res + d0 + i) : 0;
   int g = 0, b = 0;
-  for (int d = d0; d < d1; ++d) {
-    if (res[Dp + d]) ++g; else ++b;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    if (d0 + i < d1) {
+      if (gf[i]) ++g; else ++b;
+    }
   }
   // block exclusive scan of the good counts (wave scans + wave totals)
   int incl = g;
@@ -66,18 +77,21 @@ __device__ __forceinline__ void pick_body(const PickArgs& a) {
   base += incl - g;
   // the draw at which the need_good-th good draw happens
   if (base < need_good && base + g >= need_good) {
-    int c = base;
-    for (int d = d0; d < d1; ++d)
-      if (res[Dp + d] && ++c == need_good) { s_end = d; break; }
+    int c = base, e = -1;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+      if (e < 0 && d0 + i < d1 && gf[i] && ++c == need_good) e = d0 + i;
+    s_end = e;
   }
   __syncthreads();
   const int end = s_end;  // -1: the loop goes on past this batch
   // first maximum over the good draws up to the end: key = (count, ~index)
   unsigned long long key = 0ull;
-  for (int d = d0; d < d1; ++d) {
-    if (end >= 0 && d > end) break;
-    if (!res[Dp + d]) continue;
-    const unsigned long long k = ((unsigned long long)(uint32_t)pick_count<COH>(res + d) << 32) |
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int d = d0 + i;
+    if (d >= d1 || (end >= 0 && d > end) || !gf[i]) continue;
+    const unsigned long long k = ((unsigned long long)(uint32_t)cnt[i] << 32) |
                                  (unsigned long long)(0xFFFFFFFFu - (uint32_t)d);
     key = k > key ? k : key;
   }
