@@ -482,7 +482,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                         c->res.p + Dp, c->stream);
       HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
     }
-    if (c->profiling) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    // the pruned scorer records its timing events on its own dispatches (no marker packets)
+    const bool ext_ev = c->profiling && (pruned_np || (!np && pruned));
+    if (c->profiling && !ext_ev) HIPCHK(hipEventRecord(c->ev[0], c->stream));
     // the speculative pick: fused into the pruned scoring's last workgroup on one rank (at N > 1
     // it needs the allreduced counts: its own launch after the collective)
     PickArgs pk;
@@ -511,7 +513,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold};
       launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
                           c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), &npp,
-                          fuse_pick ? &pk : nullptr);
+                          fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
+                          ext_ev ? c->ev[1] : nullptr);
     } else if (np)
       launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
     else if (pruned) {
@@ -519,11 +522,12 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
       launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
                           c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), nullptr,
-                          fuse_pick ? &pk : nullptr);
+                          fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
+                          ext_ev ? c->ev[1] : nullptr);
     } else
       launch_score(src, c->hyps.p, D, cthr, c->res.p, c->opt.score_kernel, c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
-    if (c->profiling) HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    if (c->profiling && !ext_ev) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
     c->h_res.ensure((size_t)Dp + D);
     ++launches;

@@ -84,7 +84,9 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
                          int num_cus, hipStream_t s,
                          unsigned long long* stats = nullptr,  // [6] counters (A/B tool)
                          const PrunedNp* np = nullptr,
-                         const PickArgs* pick = nullptr);  // fused speculative pick (one rank)
+                         const PickArgs* pick = nullptr,  // fused speculative pick (one rank)
+                         hipEvent_t ev_start = nullptr,   // timing events of the launch pair
+                         hipEvent_t ev_stop = nullptr);
 // the NORMAL_PLANE prefilter limit of the largest w (host restatement of np_de_limit): every
 // point's d_euclid limit is <= this when 0 <= w < 1 for all points; +inf otherwise
 float np_lim_max(double w_max, double thr);
