@@ -432,9 +432,13 @@ def main():
                            "C4: 100M-pt 20-plane synthetic cloud sharded over the GPUs "
                            "(BASELINE.json configs[3]), sequential extract-and-remove RANSAC, "
                            "RCCL allreduce of counts and exact refit moments" if strong else
-                           "C3: sequential extract-and-remove RANSAC, 10M-pt 20-plane synthetic "
-                           "cloud per GPU (BASELINE.json configs[2]; N>1: shards of one cloud, "
-                           "RCCL allreduce of counts and exact refit moments)"),
+                           ("C3: sequential extract-and-remove RANSAC, 10M-pt 20-plane synthetic "
+                            "cloud per GPU (BASELINE.json configs[2]; N>1: shards of one cloud, "
+                            "RCCL allreduce of counts and exact refit moments)"
+                            if a.points == 10_000_000 and a.planes == 20 else
+                            f"sequential extract-and-remove RANSAC, {a.points / 1e6:g}M-pt "
+                            f"{a.planes}-plane synthetic cloud per GPU (not the C3 size: "
+                            f"{'C4 shape on one GPU' if a.points == 100_000_000 else 'custom'})")),
                        "points_per_gpu": a.points, "global_points": global_points,
                        "planes": a.planes, "hypotheses_per_round": a.hyps,
                        "threshold": a.threshold, "min_inliers": a.min_inliers,
@@ -447,7 +451,9 @@ def main():
             "secondary": secondary,
             "step_ms": [round(x, 2) for x in step_ms],  # this rank's host time per step
             "tests_per_step": tests // max(a.steps, 1),
-            "tests_scored_per_step": scored // max(a.steps, 1),
+            # hypotheses launched x active points (= tests_per_step for p = 1 workloads); the
+            # tests the pruned kernel actually evaluates: roofline.pruned_work
+            "tests_launched_per_step": scored // max(a.steps, 1),
             "score_ms_per_step_max_rank": round(score_ms_max / a.steps, 3),
             "select_ms_per_step": round(select_ms / a.steps, 3),
             "gen_s": round(gen_s, 2),
