@@ -271,7 +271,7 @@ template <int BS, bool NPM>
 __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     int n, const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
-    const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int chunk,
+    const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int chunk, int xcd,
     const HypRec* __restrict__ hyps, int D, float cthr, float margin, float ax, float ay,
     float az, int32_t* __restrict__ counts, unsigned long long* __restrict__ stats,
     const float4* __restrict__ NRM, double lambda, double thr, PickArgs pick_args) {
@@ -305,11 +305,25 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
   // counter measured 3x slower: one contended L2 atomic per item; dealing super-tiles to the
   // workgroups of one XCD so that a plane list is fetched into one L2 only: no faster), one
   // claim ahead.  The grid keeps each workgroup <= blk_cap items (16-bit LDS counters).
+  // xcd (gridDim.x a multiple of 8): the items of a super-tile go to workgroups of one XCD
+  // (workgroups are dealt round-robin over the 8 XCDs), so its plane list is fetched into one L2
+  // instead of eight: XCD x takes super-tiles x, x + 8, ...; their items are dealt round-robin
+  // to its gridDim.x / 8 workgroups.  Either mapping visits every item once, in increasing order
+  // per workgroup (the first index past nitems ends the workgroup's loop).
+  const int ips = kSuperTiles / chunk;  // items per super-tile
   auto claim = [&]() -> int {
     int v = nitems;
     if (lane == 0) {
       const int k = atomicAdd(&s_taken, 1);
-      if (k < blk_cap) v = (int)min((int64_t)nitems, (int64_t)blockIdx.x + (int64_t)k * gridDim.x);
+      if (k < blk_cap) {
+        if (xcd) {
+          const int64_t l = (int64_t)k * (gridDim.x >> 3) + (blockIdx.x >> 3);
+          const int64_t s = (int64_t)(blockIdx.x & 7) + 8 * (l / ips);
+          v = (int)min((int64_t)nitems, s * ips + l % ips);
+        } else {
+          v = (int)min((int64_t)nitems, (int64_t)blockIdx.x + (int64_t)k * gridDim.x);
+        }
+      }
     }
     return __shfl(v, 0);
   };
@@ -720,12 +734,23 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   static_assert(kSuperTiles % kChunkTiles == 0, "an item stays inside one super-tile");
   const int64_t items = (sp_tiles(v.n) + kChunkTiles - 1) / kChunkTiles;
   const int blk_cap = 65535 / (kChunkTiles * kTileP);
-  const int64_t g = std::max<int64_t>(
+  int64_t g = std::max<int64_t>(
       1, std::max<int64_t>(std::min<int64_t>(num_cus, (items + kBS / kWave - 1) / (kBS / kWave)),
                            (items + blk_cap - 1) / blk_cap));
+  // the XCD-aware item mapping needs a multiple of 8 workgroups, each within blk_cap items: at
+  // most ceil(ceil(ns / 8) * ips / (g / 8)) per workgroup
+  const int ips = kSuperTiles / kChunkTiles;
+  int xcd = 0;
+  if (g >= 8) {
+    int64_t gx = (g + 7) / 8 * 8;
+    const int64_t per_xcd = (ns + 7) / 8 * ips;
+    while ((per_xcd + gx / 8 - 1) / (gx / 8) > blk_cap) gx += 8;
+    g = gx;
+    xcd = 1;
+  }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;
   hipExtLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop, 0u, v.x, v.y,
-                        v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, kChunkTiles, hyps, D,
+                        v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, kChunkTiles, xcd, hyps, D,
                         cthr, margin, amax[0], amax[1], amax[2], counts, stats,
                         np ? np->nrm : nullptr, np ? np->lambda : 0.0, np ? np->thr : 0.0,
                         pick ? *pick : PickArgs{});
