@@ -464,13 +464,13 @@ __device__ __forceinline__ void reduce_digits(const int64_t* __restrict__ partia
     const int64_t* p = partials + (int64_t)k * nb;
     int64_t v = 0;
     int b = part;
-    for (; b + 15 * kMoParts < nb; b += 16 * kMoParts) {  // (nb <= 512: at most 4 batches)
-      int64_t u[16];
+    for (; b + 31 * kMoParts < nb; b += 32 * kMoParts) {  // (nb <= 512: at most 2 batches)
+      int64_t u[32];
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < 32; ++j)
         u[j] = __hip_atomic_load(p + b + j * kMoParts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v += u[j];
+      for (int j = 0; j < 32; ++j) v += u[j];
     }
     for (; b < nb; b += kMoParts)
       v += __hip_atomic_load(p + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1466,9 +1466,8 @@ void launch_moments_refit(PointsView src, const float4* coef, const ModelTest& m
 }
 
 int moments_sp_blocks(int64_t n) {
-  // (2 waves/SIMD at 228 VGPRs: 512 four-wave workgroups are all resident at once, so each wave
-  // walks half as many near super-tiles as with 256; the last workgroup reduces <= 512 partials)
-  return (int)std::max<int64_t>(1, std::min<int64_t>(512, sp_supers(n)));
+  // (512 workgroups measured no faster: the launch is bound by its latency chain and the tail)
+  return (int)std::max<int64_t>(1, std::min<int64_t>(256, sp_supers(n)));
 }
 
 void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers, float margin,
