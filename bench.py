@@ -71,6 +71,8 @@ def parse():
                     help="no HIP timing events in the timed steps (A/B of their host cost)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the C5 (normals + NORMAL_PLANE + post-process) secondary measurement")
+    ap.add_argument("--dry-ranks", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -135,9 +137,56 @@ def c5_secondary(D, ctx, a):
     return out
 
 
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment): start N fresh
+    worker processes of this script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    set as torch.distributed.run sets them, and wait for them.  The parent never imports torch or
+    dialog_amd and makes no HIP call, so nothing is initialised on a GPU before the workers start;
+    rank 0 prints the JSON line, the parent exits with the first non-zero worker status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:  # a free rendezvous port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:  # a failed rank ends the others (they would wait in a collective forever)
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.dry_ranks:  # (test of the launcher: the rank's environment, no GPU)
+        env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                              "MASTER_PORT")}
+        print(json.dumps(env), file=sys.stderr, flush=True)
+        if a.dry_fail_rank >= 0:  # one rank fails, the others would wait (as in a collective)
+            if int(os.environ.get("RANK", "0")) == a.dry_fail_rank:
+                sys.exit(3)
+            time.sleep(60)
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"n_gpus": world, "rank": 0}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_torch = world > 1 or a.torch_dist

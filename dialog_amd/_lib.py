@@ -16,6 +16,7 @@ DLG_SACMODEL_PLANE = 0
 DLG_SACMODEL_NORMAL_PLANE = 11
 DLG_REFIT_PCL = 0
 DLG_REFIT_FAST = 1
+ABI_VERSION = 2  # include/dialog_ransac.h DLG_ABI_VERSION: the structs below match that header
 
 SYMBOLS = [
     "dlg_abi_version", "dlg_status_string", "dlg_sac_params_default", "dlg_ctx_create",
@@ -29,6 +30,7 @@ SYMBOLS = [
     "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
     "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
     "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex", "dlg_cloud_drop_spatial",
+    "dlg_abi_struct_size",
 ]
 
 # context options (include/dialog_ransac.h): equivalent execution paths, identical results
@@ -39,6 +41,7 @@ DLG_OPT_PRUNE_NP = 4
 DLG_OPT_SCORE_KERNEL = 5
 DLG_OPT_PRUNE_STATS = 6
 DLG_OPT_SELECT_TILE = 7
+DLG_OPT_PCL_REFIT_DEVICE = 8
 DLG_SCORE_EXACT = 0
 DLG_SCORE_BF16 = 1
 DLG_SCORE_PRUNED = 2
@@ -79,7 +82,8 @@ class SacStats(C.Structure):
 class ExtractStats(C.Structure):
     _fields_ = [("rounds", C.c_int), ("tests", C.c_int64), ("tests_scored", C.c_int64),
                 ("score_launches", C.c_int), ("score_ms", C.c_double), ("select_ms", C.c_double),
-                ("wall_ms", C.c_double), ("lean_rounds", C.c_int), ("spec_misses", C.c_int)]
+                ("wall_ms", C.c_double), ("lean_rounds", C.c_int), ("spec_misses", C.c_int),
+                ("pcl_host_checks", C.c_int)]
 
 
 _lib = None
@@ -94,12 +98,16 @@ def load():
         from . import build as _b
         _b.build()
     L = C.CDLL(LIB_PATH)
+    if L.dlg_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI version {L.dlg_abi_version()}, binding expects {ABI_VERSION}")
     vp = C.c_void_p
     pp = C.POINTER(C.c_void_p)
     i32p = C.POINTER(C.c_int32)
     i64p = C.POINTER(C.c_int64)
     fp = C.POINTER(C.c_float)
     L.dlg_abi_version.restype = C.c_int
+    L.dlg_abi_struct_size.restype = C.c_int64
+    L.dlg_abi_struct_size.argtypes = [C.c_int]
     L.dlg_status_string.restype = C.c_char_p
     L.dlg_status_string.argtypes = [C.c_int]
     L.dlg_sac_params_default.argtypes = [C.POINTER(SacParams)]
@@ -158,7 +166,7 @@ def load():
                                      C.c_int64, i64p]
     for s in SYMBOLS:
         if s not in ("dlg_abi_version", "dlg_status_string", "dlg_sac_params_default",
-                     "dlg_last_error"):
+                     "dlg_last_error", "dlg_abi_struct_size"):
             getattr(L, s).restype = C.c_int
     _lib = L
     return L

@@ -15,7 +15,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdialog_amd.so")
-SOURCES = ["kernels.hip", "spatial.hip", "normals.hip", "postprocess.hip", "comm.cpp", "driver.cpp", "sac_control.cpp",
+SOURCES = ["kernels.hip", "fsum.hip", "spatial.hip", "normals.hip", "postprocess.hip", "comm.cpp", "driver.cpp", "sac_control.cpp",
            "normals_host.cpp", "postprocess_host.cpp"]
 # every header under csrc/ (a header change rebuilds every object: no per-file dependency scan)
 HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp") or f.endswith(".h"))

@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -36,6 +37,7 @@
 #include "../../include/dialog_ransac.h"
 #include "comm.hpp"
 #include "driver.hpp"
+#include "fsum.hpp"
 #include "host_math.hpp"
 #include "kernels.hpp"
 #include "sac_control.hpp"
@@ -388,10 +390,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // lean-list round: plane model over the Morton copy, single rank, device refit, a list that
   // is pristine or already lean (a list compacted with coordinates stays on the full path)
   const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
+  // PCL's float sums on the device (fsum.hip, one rank: the sums run over the list in global
+  // order); lean rounds take the unrefined inliers in list order from a bitmap over pristine
+  // indices instead of list coordinates
+  const bool pcl_dev = pcl_refit && c->opt.pcl_dev != 0 && c->comm->world() == 1;
   // (any rank count: the fast refit's moments are exact integers, so summing them over the
   // Morton copies of the shards gives the list's bits; every rank decides alike, as the inputs
   // of the decision -- spatial copy present, list lean -- evolve identically on every rank)
-  const bool lean = compact && !np && !pcl_refit && c->opt.lean && cl->sp_valid &&
+  const bool lean = compact && !np && (!pcl_refit || pcl_dev) && c->opt.lean && cl->sp_valid &&
                     cl->n_total < (int64_t(1) << 30) && c->opt.prune != 0 &&
                     (cl->cur < 0 || cl->buf_lean[cl->cur]);
   if (!lean) ensure_list_xyz(c, cl);
@@ -424,7 +430,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                                : pruned_np ? prune_margin(np_lim, cl->amax) : 0.0f;
   if (pruned || pruned_np) ensure_sphere_bounds(c, cl);
   // device slots: winning HypRec (its first float4 is the plane), its 3 samples, refined plane
-  c->small.ensure(8);
+  c->small.ensure(16);
+  c->h_small.ensure(16);
   HypRec* best_dev = reinterpret_cast<HypRec*>(c->small.p);
   SampleRec* best_smp_dev = reinterpret_cast<SampleRec*>(c->small.p + 2);
   float4* rc_dev = c->small.p + 5;
@@ -620,6 +627,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     else HIPCHK(q);
     c->stage_inflight = false;
   };
+  std::function<void(int)> select_round;
   auto refit_select = [&]() {
     // Fast mode (and no optimisation) never leave the device: moments of the unrefined plane's
     // inliers (k_moments, centred on the winning sample), the double eigen33 refit in a
@@ -663,6 +671,47 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         if (prm.optimize) c->comm->allreduce_sum(c->moments.p, kMomDigits, DType::I64, c->stream);
         launch_refit_moments(c->moments.p, cl->qexp, bc_dev, prm.optimize, rc_dev, c->stream);
       }
+    } else if (pcl_dev) {
+      // PCL float refit on the device: the unrefined plane's inliers in list order, PCL's nine
+      // sequential float sums evaluated exactly in parallel (fsum.hip), the float eigen33; the
+      // refined plane stays on the device (no host round trip)
+      if (c->fs_cap < src.n) {
+        const int64_t cap = std::max<int64_t>(src.n, 1);
+        c->fs_scr.ensure(fs_scratch_bytes(cap));
+        c->fs_b = fs_carve(c->fs_scr.p, cap);
+        HIPCHK(hipMemsetAsync(c->fs_b.ticket, 0, sizeof(unsigned), c->stream));
+        c->fs_cap = cap;
+      }
+      int32_t* fs_res = reinterpret_cast<int32_t*>(c->small.p + 8);
+      if (lean) {
+        // inliers stamped into a bitmap over pristine indices from the Morton copy's near tiles,
+        // compacted in ascending pristine order = list order
+        const int64_t nw = (cl->n_total + 31) / 32;
+        if (cl->ubits.cap < (size_t)nw + 16) {
+          cl->ubits.ensure((size_t)nw + 16);
+          HIPCHK(hipMemsetAsync(cl->ubits.p, 0, cl->ubits.cap * sizeof(uint32_t), c->stream));
+        }
+        ensure_sel1(c, std::max<int64_t>(std::max<int64_t>(src.n, cl->sp_n), nw));
+        c->fs_x.ensure((size_t)std::max<int64_t>(src.n, 1));
+        c->fs_y.ensure((size_t)std::max<int64_t>(src.n, 1));
+        c->fs_z.ensure((size_t)std::max<int64_t>(src.n, 1));
+        c->fs_n.ensure(1);
+        const SpatialView sv = spatial_view(cl);
+        launch_ustamp(sp_cur_view(), sv.tiles, sv.supers, pmargin, bc_dev, mt, cl->ubits.p,
+                      c->stream);
+        launch_ucompact(cl->ubits.p, nw, cl->pristine.view(cl->n_total), c->sel1, c->fs_x.p,
+                        c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
+        launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
+                        rc_dev, fs_res, c->num_cus, c->stream);
+      } else {
+        c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
+        stage_wait();
+        launch_select(src, bc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
+                      c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
+        launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
+                        c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream);
+      }
+      HIPCHK(hipGetLastError());
     } else {
       // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
       c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
@@ -684,6 +733,38 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       HIPCHK(hipMemcpyAsync(rc_dev, c->h_small.p + 5, sizeof(float4), hipMemcpyHostToDevice,
                             c->stream));
     }
+    select_round(sk);
+    if (pcl_dev) {
+      // an eigen33 transcendental the device could not round for certain (a double result within
+      // 2^-46 of a float rounding boundary): the host's value from the published sums decides,
+      // and the select is redone when it differs (DLG_OPT_PCL_REFIT_DEVICE 2 / 3: every round)
+      const int32_t* fr = reinterpret_cast<const int32_t*>(c->h_small.p + 8);
+      if (fr[0] != 0 || c->opt.pcl_dev >= 2) {
+        ++c->fs_checks;
+        if (xs) xs->pcl_host_checks++;
+        float a9[9], rh[4];
+        std::memcpy(a9, fr + 2, sizeof(a9));
+        const HypRec* bh = reinterpret_cast<const HypRec*>(c->h_small.p);
+        const float cin[4] = {bh->a, bh->b, bh->c, bh->d};
+        fs_refit_tail_plain(a9, fr[1], cin, rh);
+        const float4 rd = c->h_small.p[5];
+        if (std::memcmp(rh, &rd, sizeof(rh)) != 0 || c->opt.pcl_dev == 3) {
+          ++c->fs_fixes;
+          c->h_small.p[15] = make_float4(rh[0], rh[1], rh[2], rh[3]);
+          HIPCHK(hipMemcpyAsync(rc_dev, c->h_small.p + 15, sizeof(float4), hipMemcpyHostToDevice,
+                                c->stream));
+          // (the first select wrote only spare buffers and stamps under its own tag: redone
+          // outright; its timing is not kept)
+          const bool prof = c->profiling;
+          c->profiling = false;
+          select_round(c->sel_k);
+          c->profiling = prof;
+        }
+      }
+    }
+  };
+  // final selectWithinDistance with the refined plane at rc_dev (+ compaction, publish, wait)
+  select_round = [&](int sk) {
     // final selectWithinDistance with the refined model: the head (counts + scan) makes the
     // round's totals final, they are published right away, and the scatters (inlier ids,
     // survivors of both copies) and the sphere bounds run while the host reads them and draws
@@ -714,7 +795,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     pa.totals = c->totals.p;
     pa.ntot = 4;
     pa.small = c->small.p;
-    pa.nsmall = 6;
+    pa.nsmall = pcl_dev ? 12 : 6;  // (+ the device PCL refit's flag, count and sums: small[8..11])
     pa.rk = W > 1 ? c->rk.p : nullptr;
     pa.nrk = W > 1 ? 2 * W : 0;
     pa.pick = with_counts ? c->pick.p : nullptr;
@@ -805,7 +886,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (trace_on()) c->t_tot = now_ms();
     std::memcpy(c->h_tot.p, c->pub + kPubTot, 16);
     if (c->pub[kPubErr] != 0) sel1_failed(c);  // (this round's or the last list pass's look-back)
-    std::memcpy(c->h_small.p, c->pub + kPubSmall, 6 * sizeof(float4));
+    std::memcpy(c->h_small.p, c->pub + kPubSmall, (size_t)pa.nsmall * sizeof(float4));
     if (W > 1) std::memcpy(c->h_rk.p, c->pub + kPubRk, 8 * (size_t)W);
     check_sp_totals(c, c->h_tot.p + 2);
     if (with_counts) {
@@ -981,6 +1062,18 @@ dlg_status init_ctx(dlg_ctx* c, int device) {
 extern "C" {
 
 int dlg_abi_version(void) { return DLG_ABI_VERSION; }
+
+int64_t dlg_abi_struct_size(int which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(dlg_points);
+    case 1: return (int64_t)sizeof(dlg_sac_params);
+    case 2: return (int64_t)sizeof(dlg_sac_stats);
+    case 3: return (int64_t)sizeof(dlg_extract_stats);
+    case 4: return (int64_t)sizeof(dlg_planes);
+    case 5: return (int64_t)sizeof(dlg_postprocess_params);
+  }
+  return -1;
+}
 
 const char* dlg_status_string(dlg_status s) {
   switch (s) {
@@ -1507,6 +1600,10 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_SELECT_TILE: 4096, 8192 or 16384");
         o.sel1_tile = (int)value;
         break;
+      case DLG_OPT_PCL_REFIT_DEVICE:
+        if (value < 0 || value > 3) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PCL_REFIT_DEVICE: 0..3");
+        o.pcl_dev = (int)value;
+        break;
       default: throw DlgError(DLG_ERR_INVALID, "unknown option");
     }
   });
@@ -1523,6 +1620,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_SCORE_KERNEL: *value = o.score_kernel == kScoreExact ? DLG_SCORE_EXACT : DLG_SCORE_BF16; break;
     case DLG_OPT_PRUNE_STATS: *value = o.prune_stats; break;
     case DLG_OPT_SELECT_TILE: *value = o.sel1_tile; break;
+    case DLG_OPT_PCL_REFIT_DEVICE: *value = o.pcl_dev; break;
     default: return DLG_ERR_INVALID;
   }
   return DLG_OK;

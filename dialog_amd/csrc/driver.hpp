@@ -162,6 +162,11 @@ struct PathOptions {
   int score_kernel = kScoreBf16;  // exhaustive scorer: kScoreBf16 or kScoreExact
   bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
   int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
+  // PCL float refit (DLG_REFIT_PCL, one rank): 1 = the nine sums on the device (fsum.hip,
+  // exact), 0 = gathered to the host and summed there, 2 = device, and the host recomputes the
+  // refit's tail from the published sums every round, 3 = as 2 and the round's select is always
+  // redone with the host's plane (exercises the path an uncertain transcendental takes)
+  int pcl_dev = 1;
 };
 
 struct dlg_ctx {
@@ -237,6 +242,13 @@ struct dlg_ctx {
   int64_t emit_n = 0;
   NormalsWork nw;
   PostWork pw;
+  // PCL float refit on the device (fsum.hip): scratch sized for fs_cap inliers
+  DevBuf<uint8_t> fs_scr;
+  int64_t fs_cap = -1;
+  FsBuffers fs_b;
+  DevBuf<float> fs_x, fs_y, fs_z;  // lean rounds: the unrefined plane's inliers in list order
+  DevBuf<int32_t> fs_n;
+  int64_t fs_checks = 0, fs_fixes = 0;  // host recomputations of the refit tail, and redone selects
 };
 
 struct dlg_cloud {
@@ -278,6 +290,7 @@ struct dlg_cloud {
   // field; x, y, z, normals stale) until a path that reads coordinates materialises it
   bool buf_lean[2] = {false, false};
   bool list_lean() const { return cur >= 0 && buf_lean[cur]; }
+  DevBuf<uint32_t> ubits;  // PCL refit in lean rounds: unrefined inliers by pristine index (zero between rounds)
   DevBuf<uint8_t> tag;  // per pristine point: the stamp of the select that took it
   int tagv = 0;         // last stamp used (tag[] is zeroed when the byte wraps)
 };

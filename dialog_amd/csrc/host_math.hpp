@@ -111,8 +111,19 @@ DLG_HD inline void compute_roots2(S b, S c, S roots[3]) {
   roots[1] = S(0.5f) * (b - sd);
 }
 
-template <typename S>
-DLG_HD inline void compute_roots(const S m[9], S roots[3]) {
+// the transcendental functions of eigen33 (host_math's m_atan2 / m_cos / m_sin by default; the
+// device refit of fsum.hpp substitutes a variant that flags results it cannot round for certain)
+struct PlainTx {
+  template <typename S>
+  DLG_HD S atan2(S y, S x) const { return m_atan2(y, x); }
+  template <typename S>
+  DLG_HD S cos(S x) const { return m_cos(x); }
+  template <typename S>
+  DLG_HD S sin(S x) const { return m_sin(x); }
+};
+
+template <typename S, typename TX = PlainTx>
+DLG_HD inline void compute_roots(const S m[9], S roots[3], const TX& tx = TX()) {
   auto M = [&](int r, int c) { return m[r * 3 + c]; };
   S c0 = M(0, 0) * M(1, 1) * M(2, 2) + S(2) * M(0, 1) * M(0, 2) * M(1, 2) -
          M(0, 0) * M(1, 2) * M(1, 2) - M(1, 1) * M(0, 2) * M(0, 2) - M(2, 2) * M(0, 1) * M(0, 1);
@@ -133,8 +144,8 @@ DLG_HD inline void compute_roots(const S m[9], S roots[3]) {
   S q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
   if (q > S(0)) q = S(0);
   S rho = m_sqrt(-a_over_3);
-  S theta = m_atan2(m_sqrt(-q), half_b) * s_inv3;
-  S ct = m_cos(theta), st = m_sin(theta);
+  S theta = tx.atan2(m_sqrt(-q), half_b) * s_inv3;
+  S ct = tx.cos(theta), st = tx.sin(theta);
   roots[0] = c2_over_3 + S(2) * rho * ct;
   roots[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
   roots[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
@@ -146,15 +157,15 @@ DLG_HD inline void compute_roots(const S m[9], S roots[3]) {
   if (roots[0] <= S(0)) compute_roots2(c2, c1, roots);
 }
 
-template <typename S>
-DLG_HD inline void eigen33(const S mat[9], S* eval, S evec[3]) {
+template <typename S, typename TX>
+DLG_HD inline void eigen33_tx(const S mat[9], S* eval, S evec[3], const TX& tx) {
   S scale = S(0);
   for (int k = 0; k < 9; ++k) scale = m_fabs(mat[k]) > scale ? m_fabs(mat[k]) : scale;
   if (scale <= min_of<S>()) scale = S(1);
   S m[9];
   for (int k = 0; k < 9; ++k) m[k] = mat[k] / scale;
   S roots[3];
-  compute_roots(m, roots);
+  compute_roots(m, roots, tx);
   *eval = roots[0] * scale;
   m[0] -= roots[0]; m[4] -= roots[0]; m[8] -= roots[0];
   auto cross = [](const S* a, const S* b, S* o) {
@@ -176,6 +187,11 @@ DLG_HD inline void eigen33(const S mat[9], S* eval, S evec[3]) {
   else { v = v3; l = l3; }
   S s = m_sqrt(l);
   evec[0] = v[0] / s; evec[1] = v[1] / s; evec[2] = v[2] / s;
+}
+
+template <typename S>
+DLG_HD inline void eigen33(const S mat[9], S* eval, S evec[3]) {
+  eigen33_tx(mat, eval, evec, PlainTx());
 }
 
 // optimizeModelCoefficients, parity mode: computeMeanAndCovarianceMatrix (float, dense branch,

@@ -1099,6 +1099,119 @@ __global__ void k_list_materialize(PointsView pristine, int64_t n, PointsOut io)
   if (io.nrm) io.nrm[e] = pristine.nrm[p];
 }
 
+// ---------------------------------------------------------------------------------------------
+// PCL refit in lean rounds: the unrefined plane's inliers in list order, without list
+// coordinates.  A lean list is the ascending pristine indices of the active points, so "inliers
+// in list order" = the set bits of a bitmap over pristine indices, ascending.
+// k_ustamp: the Morton copy's tiles whose sphere may hold an inlier (k_moments_sp's walk) set the
+// bit of each inlier's pristine index (the copy's gid field).  The bitmap is all-zero on entry
+// (k_ucompact clears every word it reads).
+__global__ __launch_bounds__(kMoBS) void k_ustamp(PointsView src, const float4* __restrict__ tiles,
+                                                  const float4* __restrict__ supers, float margin,
+                                                  const float4* __restrict__ cfp, ModelTest mt,
+                                                  uint32_t* __restrict__ bits) {
+  const float4 cf = *cfp;
+  const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
+  const int64_t nsup = (src.n + kSuperP - 1) / kSuperP, ntile = (src.n + kTileP - 1) / kTileP;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t W = (int64_t)gridDim.x * (kMoBS / kWave);
+  const int64_t wid = (int64_t)blockIdx.x * (kMoBS / kWave) + threadIdx.x / kWave;
+  constexpr int kIt = kSuperP / kWave;
+  for (int64_t s0 = wid; s0 < nsup; s0 += kWave * W) {
+    const int64_t sl = s0 + lane * W;
+    uint64_t near = ballot(sl < nsup && sphere_near(cf, supers[sl], margin));
+    while (near) {
+      const int64_t s = s0 + (int64_t)(__ffsll((unsigned long long)near) - 1) * W;
+      near &= near - 1;
+      const int64_t tl = s * kSuperTiles + (lane & (kSuperTiles - 1));
+      const uint32_t tm = (uint32_t)ballot(lane < kSuperTiles && tl < ntile &&
+                                           sphere_near(cf, tiles[tl], margin));
+      const int64_t base = s * kSuperP;
+      float x[kIt], y[kIt], z[kIt];
+      int32_t g[kIt];
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) {
+        const int64_t e = base + j * kWave + lane;
+        if (((tm >> (2 * j + (lane >> 5))) & 1u) && e < src.n) {
+          x[j] = src.x[e]; y[j] = src.y[e]; z[j] = src.z[e]; g[j] = src.gid[e];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kIt; ++j) {
+        const int64_t e = base + j * kWave + lane;
+        if (((tm >> (2 * j + (lane >> 5))) & 1u) && e < src.n &&
+            model_in<false>(src, e, cf, cn, mt, x[j], y[j], z[j]))
+          atomicOr(bits + (g[j] >> 5), 1u << (g[j] & 31));
+      }
+    }
+  }
+}
+
+// k_ucompact: bitmap -> the inliers' x, y, z in ascending pristine order (= list order), a
+// single pass with decoupled look-back (sel1_scan); each lane owns 16 consecutive words (4 x 16 B
+// loads), clears them, and writes its inliers from its exclusive rank on.  The last tile writes
+// the count to *n_out.
+constexpr int kUcBS = 256;
+constexpr int kUcWords = 16;  // words per lane
+__global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits, int64_t nwords,
+                                                    PointsView pristine, Sel1State L, int ntiles,
+                                                    float* __restrict__ ox, float* __restrict__ oy,
+                                                    float* __restrict__ oz,
+                                                    int32_t* __restrict__ n_out) {
+  constexpr int kSlots = S1<kUcBS>::kSlots;
+  __shared__ int s_cnt[kSlots], s_pre[kSlots], s_base[2];
+  const int tile = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int64_t w0 = ((int64_t)tile * kUcBS + threadIdx.x) * kUcWords;
+  uint32_t word[kUcWords];
+  if (w0 + kUcWords <= nwords) {
+    uint4* p = reinterpret_cast<uint4*>(bits + w0);
+#pragma unroll
+    for (int q = 0; q < kUcWords / 4; ++q) {
+      const uint4 v = p[q];
+      word[4 * q] = v.x; word[4 * q + 1] = v.y; word[4 * q + 2] = v.z; word[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int q = 0; q < kUcWords / 4; ++q) p[q] = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+#pragma unroll
+    for (int j = 0; j < kUcWords; ++j) {
+      word[j] = w0 + j < nwords ? bits[w0 + j] : 0u;
+      if (w0 + j < nwords) bits[w0 + j] = 0u;
+    }
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kUcWords; ++j) cnt += __popc(word[j]);
+  int incl = cnt;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int u = __shfl_up(incl, off, kWave);
+    if (lane >= off) incl += u;
+  }
+  // slot (j = 0, wave w) carries the wave's total: in-tile order is lane-major within a wave
+  for (int t = threadIdx.x; t < kSlots; t += kUcBS) s_cnt[t] = 0;
+  __syncthreads();
+  if (lane == kWave - 1) s_cnt[w] = incl;
+  const int excl = sel1_scan<kUcBS>(L, tile, s_cnt, s_pre, s_base);
+  if (excl < 0) return;  // (look-back failed: *L.err is set; the words are cleared already)
+  int64_t pos = (int64_t)excl + s_pre[w] + (incl - cnt);
+#pragma unroll
+  for (int j = 0; j < kUcWords; ++j) {
+    uint32_t m = word[j];
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      const int64_t pi = (w0 + j) * 32 + b;
+      ox[pos] = pristine.x[pi];
+      oy[pos] = pristine.y[pi];
+      oz[pos] = pristine.z[pi];
+      ++pos;
+    }
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) *n_out = excl + s_base[1];
+}
+
 // k_score_np: counts[h] for SACMODEL_NORMAL_PLANE.
 //
 // Per point the exact prefilter b = (1 - w) d_euclid < thr becomes one float compare: b is
@@ -1356,6 +1469,27 @@ void launch_sel1_list(const int32_t* lidx, int64_t n, const uint8_t* tag, uint8_
 void launch_list_materialize(PointsView pristine, int64_t n, const PointsOut& io, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_list_materialize, dim3(cdiv(n, 256)), dim3(256), 0, s, pristine, n, io);
+}
+
+void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, float margin,
+                   const float4* coef, const ModelTest& mt, uint32_t* bits, hipStream_t s) {
+  if (sp.n <= 0) return;
+  hipLaunchKernelGGL(k_ustamp, dim3(moments_sp_blocks(sp.n)), dim3(kMoBS), 0, s, sp, tiles, supers,
+                     margin, coef, mt, bits);
+}
+
+int ucompact_tiles(int64_t nwords) { return (int)((nwords + kUcBS * kUcWords - 1) / (kUcBS * kUcWords)); }
+
+void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1State& L, float* ox,
+                     float* oy, float* oz, int32_t* n_out, hipStream_t s) {
+  const int nt = ucompact_tiles(nwords);
+  if (nt == 0) {
+    (void)hipMemsetAsync(n_out, 0, sizeof(int32_t), s);
+    return;
+  }
+  sel1_next(L, nt);
+  hipLaunchKernelGGL(k_ucompact, dim3(nt), dim3(kUcBS), 0, s, bits, nwords, pristine, L, nt, ox, oy,
+                     oz, n_out);
 }
 
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,

@@ -86,7 +86,7 @@ void launch_gather_samples(const int32_t* pos, int m, int64_t lo, PointsView src
 // round results into the coherent pinned buffer pub (layout below), then pub[0] = seq (release,
 // system scope)
 // (err: the single-pass selects' sticky look-back error word, or null)
-constexpr int kPubTot = 1, kPubPick = 5, kPubErr = 7, kPubSmall = 8, kPubRk = 32;  // + nrk: counts
+constexpr int kPubTot = 1, kPubPick = 5, kPubErr = 7, kPubSmall = 8, kPubRk = 64;  // + nrk: counts
 struct PubArgs {
   const int32_t* totals = nullptr;
   int ntot = 0;
@@ -185,6 +185,36 @@ int moments_sp_blocks(int64_t n);
 void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers, float margin,
                        const float4* coef, const ModelTest& mt, int qexp, int64_t* partials,
                        unsigned* done, int nblocks, int64_t* out, float4* cout, hipStream_t s);
+// PCL refit in lean rounds (single rank): the unrefined plane's inliers, stamped into a bitmap
+// over pristine indices from the Morton copy's near tiles (launch_ustamp), then compacted in
+// ascending pristine order = list order into x/y/z arrays (launch_ucompact; clears the bitmap,
+// count -> *n_out).  bits: ceil(n_pristine / 32) words, zero on entry.
+void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, float margin,
+                   const float4* coef, const ModelTest& mt, uint32_t* bits, hipStream_t s);
+int ucompact_tiles(int64_t nwords);
+void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1State& L, float* ox,
+                     float* oy, float* oz, int32_t* n_out, hipStream_t s);
+
+// PCL's float refit on the device (fsum.hip): the nine sequential float sums of
+// computeMeanAndCovarianceMatrix evaluated exactly in parallel (fsum.hpp), then the float
+// eigen33.  Inliers px/py/pz with element stride `stride` floats, count *n_dev (<= n_cap).
+// res (16 int32): [0] = 1 when a transcendental of eigen33 could not be rounded for certain
+// (the host then recomputes the plane from the sums), [1] = n, [2..10] = the nine sums' bits.
+struct FsBuffers {
+  double* csum = nullptr;  // [chunks][9]
+  double* usum = nullptr;  // [units][9]
+  double* upre = nullptr;  // [units][9]
+  void* nodes[8] = {};     // FsNode per level (1..), chain-major
+  int64_t cap[8] = {};     // nodes per chain per level
+  unsigned* ticket = nullptr;
+};
+// bytes of scratch for n_cap inliers; carve() lays the buffers out in `base`
+size_t fs_scratch_bytes(int64_t n_cap);
+FsBuffers fs_carve(void* base, int64_t n_cap);
+void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
+                     const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
+                     float4* cout, int32_t* res, int num_cus, hipStream_t s);
+
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers
 void launch_refit_moments(const int64_t* moments, int qexp, const float4* cin, int optimize,

@@ -33,7 +33,10 @@
 extern "C" {
 #endif
 
-#define DLG_ABI_VERSION 1
+/* 2: dlg_extract_stats gained lean_rounds, spec_misses, pcl_host_checks; dlg_score_benchmark's
+ * 4th argument is a DLG_SCORE_* kernel; execution paths are context options, not environment
+ * variables */
+#define DLG_ABI_VERSION 2
 
 typedef enum {
   DLG_OK = 0,
@@ -49,8 +52,13 @@ typedef enum {
 enum { DLG_SACMODEL_PLANE = 0, DLG_SACMODEL_NORMAL_PLANE = 11 };
 /* refit of the winning model (SampleConsensusModelPlane::optimizeModelCoefficients) */
 enum {
-  DLG_REFIT_PCL = 0,   /* PCL float, single pass, index order: bit-exact with PCL (host-sequential) */
-  DLG_REFIT_FAST = 1   /* on-device double moments + double eigen33: within 1e-5 of the exact LS plane */
+  DLG_REFIT_PCL = 0,   /* PCL's float refit: computeMeanAndCovarianceMatrix's single-pass float
+                          sums in list order + float eigen33, bit-exact with PCL.  One rank: the
+                          sums run on the device, exactly (fsum.hpp); multi-rank: on the host */
+  DLG_REFIT_FAST = 1   /* NOT PCL's arithmetic: exact integer moments of the inliers + a double
+                          Jacobi solve (the least-squares plane to within float rounding; order-
+                          and rank-count-independent).  Its planes differ from PCL's by up to
+                          ~1e-4 and can change which plane a later extract round picks */
 };
 
 typedef struct dlg_ctx dlg_ctx;
@@ -101,11 +109,16 @@ typedef struct {
   double wall_ms;              /* host wall time of the call */
   int lean_rounds;             /* rounds that took the single-pass (lean-list) select */
   int spec_misses;             /* speculative device picks the host replay overturned */
+  int pcl_host_checks;         /* device PCL refits whose tail the host recomputed (an eigen33
+                                  transcendental near a float rounding boundary) */
 } dlg_extract_stats;
 
 void dlg_sac_params_default(dlg_sac_params* p);   /* PCL SACSegmentation defaults */
 const char* dlg_status_string(dlg_status s);
 int dlg_abi_version(void);
+/* sizeof of the ABI's structs, for bindings to check their layouts: 0 dlg_points, 1 dlg_sac_params,
+ * 2 dlg_sac_stats, 3 dlg_extract_stats, 4 dlg_planes, 5 dlg_postprocess_params; -1 otherwise */
+int64_t dlg_abi_struct_size(int which);
 
 /* ---- contexts ------------------------------------------------------------------------------ */
 dlg_status dlg_ctx_create(dlg_ctx** out, int device);
@@ -332,15 +345,20 @@ enum {
   DLG_OPT_PRUNE = 1,        /* Morton copy + pruned countWithinDistance: -1 (default) clouds of
                                >= 131072 points, 0 never, 1 every cloud (applies at upload) */
   DLG_OPT_LEAN_ROUNDS = 2,  /* 1 (default): single-pass selects driven by the Morton copy in
-                               fast-refit / no-optimise SACMODEL_PLANE extraction; 0: two-pass */
+                               SACMODEL_PLANE extraction (any refit mode on one rank; fast or no
+                               refit at any rank count); 0: two-pass */
   DLG_OPT_SPEC_PICK = 3,    /* 1 (default): device-side computeModel decision for probability-1
                                rounds (host replay confirms it); 0: host decision only */
   DLG_OPT_PRUNE_NP = 4,     /* 1 (default): pruned SACMODEL_NORMAL_PLANE scoring; 0: exhaustive */
   DLG_OPT_SCORE_KERNEL = 5, /* exhaustive scorer (no Morton copy): DLG_SCORE_BF16 (default) or
                                DLG_SCORE_EXACT */
   DLG_OPT_PRUNE_STATS = 6,  /* 1: count the pruned kernel's work (dlg_prune_stats); 0 (default) */
-  DLG_OPT_SELECT_TILE = 7   /* points per tile of the lean rounds' single-pass selects: 4096,
+  DLG_OPT_SELECT_TILE = 7,  /* points per tile of the lean rounds' single-pass selects: 4096,
                                8192 or 16384 (default) */
+  DLG_OPT_PCL_REFIT_DEVICE = 8 /* DLG_REFIT_PCL on one rank: 1 (default) the float sums on the
+                               device, exact (fsum.hpp); 0 gathered and summed on the host; 2 as 1,
+                               the host recomputing every refit's tail from the sums; 3 as 2 and
+                               every round's select redone with the host's plane (test) */
 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
 dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);

@@ -49,8 +49,19 @@ def test_params_defaults_match_pcl():
     assert d.max_iterations == 50 and d.probability == 0.99 and d.optimize == 1
     assert d.seed == 12345 and d.model == 0 and d.threshold == 0.0
     assert p.max_iterations == 50
-    assert L.dlg_abi_version() == 1
+    assert L.dlg_abi_version() == _lib.ABI_VERSION == 2
     assert L.dlg_status_string(0) == b"ok"
+
+
+def test_struct_layouts_match_the_header():
+    """The ctypes structs have the header's sizes (dlg_abi_struct_size reports sizeof of each): a
+    binding built for another layout would read or write past the caller's struct."""
+    L = _lib.load()
+    pairs = [(0, _lib.Points), (1, _lib.SacParams), (2, _lib.SacStats), (3, _lib.ExtractStats),
+             (4, _lib.Planes), (5, _lib.PostProcessParams)]
+    for which, cls in pairs:
+        assert L.dlg_abi_struct_size(which) == C.sizeof(cls), cls.__name__
+    assert L.dlg_abi_struct_size(99) == -1
 
 
 def test_no_device_fails_loudly(monkeypatch):

@@ -87,8 +87,7 @@ def test_c3_extract(gpu_ctx, mode):
     e = D.extract_planes(cl, params(mode), max_planes=20, min_inliers=500, capacity=p.shape[0])
     cl.close()
     check_extract(e, DB["c3"]["modes"][mode])
-    if mode != "pcl":
-        assert e["stats"]["lean_rounds"] == e["stats"]["rounds"]  # the bench's path
+    assert e["stats"]["lean_rounds"] == e["stats"]["rounds"]  # the bench's path
 
 
 @pytest.mark.skipif("c3" not in DB or "fast" not in DB["c3"]["modes"], reason="no c3/fast")

@@ -178,8 +178,8 @@ def test_pruned_counts_c3_full_size(gpu_ctx):
 def test_lean_list_continue_segment_and_normal_plane(gpu_ctx, optimize):
     """Lean-list rounds (the Morton copy decides the inliers, the list keeps pristine indices)
     run whenever the refit stays on the device: optimize=False here (bit-exact against the
-    oracle's optimize-off extraction) -- optimize=True takes PCL's host refit and the two-pass
-    path, the control.  Extraction continued over several calls equals one call; a plain
+    oracle's optimize-off extraction), and optimize=True with PCL's float refit on the device
+    (the unrefined inliers from the pristine-index bitmap).  Extraction continued over several calls equals one call; a plain
     segment and a SACMODEL_NORMAL_PLANE round afterwards read the materialised list; all
     against the oracle."""
     p, _, _ = plane_cloud(40000, 6, seed=41)
@@ -195,7 +195,7 @@ def test_lean_list_continue_segment_and_normal_plane(gpu_ctx, optimize):
         e = D.extract_planes(cloud, prm, max_planes=k, min_inliers=50)
         got.append(e["inliers"].copy())
         lean += e["stats"]["lean_rounds"]
-    assert lean == (0 if optimize else 5)
+    assert lean == 5
     assert np.array_equal(np.concatenate(got), ref["inliers"])
     taken = np.concatenate(got)
     rem = np.setdiff1d(np.arange(p.shape[0]), taken).astype(np.int32)
@@ -223,7 +223,8 @@ def test_lean_list_continue_segment_and_normal_plane(gpu_ctx, optimize):
 @pytest.mark.parametrize("optimize", [False, True])
 def test_lean_list_indexed_cloud(gpu_ctx, optimize):
     """setIndices clouds: the list's pristine indices differ from the point ids (and from list
-    order of the ids when the indices are unsorted); lean rounds with optimize=False."""
+    order of the ids when the indices are unsorted); lean rounds with or without the (device) PCL
+    refit."""
     p, _, _ = plane_cloud(50000, 5, seed=43)
     rng = np.random.default_rng(9)
     idx = rng.choice(p.shape[0], 30000, replace=False).astype(np.int32)  # unsorted
@@ -232,7 +233,7 @@ def test_lean_list_indexed_cloud(gpu_ctx, optimize):
     cloud.build_spatial()
     e = D.extract_planes(cloud, D.make_params(0.02, **kw), max_planes=4, min_inliers=50)
     ref = O.extract_planes(p[idx], 0.02, max_planes=4, min_inliers=50, **kw)
-    assert e["stats"]["lean_rounds"] == (0 if optimize else e["stats"]["rounds"])
+    assert e["stats"]["lean_rounds"] == e["stats"]["rounds"]
     assert e["n_planes"] == ref["n_planes"] >= 3
     assert np.array_equal(e["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
     assert np.array_equal(e["inliers"], idx[ref["inliers"]])
