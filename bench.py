@@ -3,23 +3,26 @@
 Workload (BASELINE.json configs[2], the 10M-point cloud the metric is quoted on): per GPU a 10M-
 point synthetic cloud with 20 planes (+10 % outliers, BASELINE.md §3 generator), sequential
 extract-and-remove RANSAC: each round scores 4096 hypotheses (max_iterations 4095, probability 1.0
--> k = inf, exactly 4096 PCL iterations) over the remaining points, refits (DLG_REFIT_FAST: the
-exact-moment LS refit, bit-exact with the oracle's restatement), selects and compacts the
-inliers; stop after 20 planes or when a plane has < 500 inliers.  One step = one full
-extraction from the pristine cloud (inputs resident in HBM).
+-> k = inf, exactly 4096 PCL iterations) over the remaining points, refits with PCL's float
+arithmetic (DLG_REFIT_PCL: computeMeanAndCovarianceMatrix's nine sequential float sums, evaluated
+bit-exactly on the device, then PCL's float eigen33), selects and compacts the inliers; stop after
+20 planes or when a plane has < 500 inliers.  One step = one full extraction from the pristine
+cloud (inputs resident in HBM).  The planes and inlier lists equal the oracle's restatement of
+PCL 1.8 bit for bit (tests/test_fullsize_golden.py).
 
-Multi-GPU (torchrun, one process per GPU): weak scaling by default -- rank r holds its own 10M-
-point shard of one global cloud (same 20 planes); --global-points 100000000 runs configs[3] (C4)
-strong-sharded.  Every round all ranks score the same hypotheses on their shards with one RCCL
-allreduce of the int32[4096] counts, and sum the exact refit moments.
+Multi-GPU (one process per GPU: torchrun, or `--gpus N`, which starts the N ranks itself): weak
+scaling by default -- rank r holds its own 10M-point shard of one global cloud (same 20 planes);
+--global-points 100000000 runs configs[3] (C4) strong-sharded.  Every round all ranks score the
+same hypotheses on their shards with one RCCL allreduce of the int32[4096] counts; the refit's
+float sums run over the ranks' inlier segments in global order.
 
 value = useful point-plane tests (PCL iterations x global active points, summed over rounds) / s,
 whole job.  Roofline: the pruned scoring launch against HBM with SURVEY 8(d)'s algorithmic bytes,
 with its PMC traffic, issue view and the work the pruning leaves (pruned_work).  Extra lines in
-the same JSON object: refit_pcl (the PCL-float-refit mode, bit-exact with PCL's arithmetic as
-restated), incl_index_build (the Morton copy + spheres rebuilt every step), secondary (C5).
-cpu_baseline: the PCL-1.8 restatement (oracle) on the box's host cores (16 OpenMP threads for
-countWithinDistance, plus a single-thread sample), rank 0 at N = 1 only.
+the same JSON object: refit_fast (DLG_REFIT_FAST, an exact least-squares refit -- NOT PCL's
+arithmetic: its planes differ from PCL's), incl_index_build (the Morton copy + spheres rebuilt
+every step), secondary (C5).  cpu_baseline: the PCL-1.8 restatement (oracle) on the box's host
+cores (16 OpenMP threads for countWithinDistance, plus a single-thread sample), rank 0 at N = 1.
 """
 from __future__ import annotations
 
@@ -53,15 +56,16 @@ def parse():
     ap.add_argument("--hyps", type=int, default=4096)
     ap.add_argument("--threshold", type=float, default=0.02)
     ap.add_argument("--min-inliers", type=int, default=500)
-    ap.add_argument("--refit", choices=["fast", "pcl"], default="fast")
+    ap.add_argument("--refit", choices=["pcl", "fast"], default="pcl",
+                    help="pcl (default): PCL's float refit, bit-exact; fast: exact LS refit (not PCL)")
     ap.add_argument("--cpu-hyps", type=int, default=1024,
                     help="hypotheses in the single-thread CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the all-core CPU leg (the GPU box's CPU share: 16)")
-    ap.add_argument("--pcl-steps", type=int, default=3,
-                    help="steps of the bit-exact PCL-refit line (0: skip)")
+    ap.add_argument("--alt-steps", type=int, default=3,
+                    help="steps of the other refit mode's line (refit_fast / refit_pcl; 0: skip)")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the PCL-refit, index-build and pruning-work measurements")
+                    help="skip the other-refit, index-build and pruning-work measurements")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--torch-dist", action="store_true",
                     help="rendezvous through torch.distributed even at N=1 (runtime check)")
@@ -245,6 +249,7 @@ def main():
     ctx.barrier()
     ctx.synchronize()
     tests = scored = launches = 0
+    spec_misses = host_checks = 0
     score_ms = select_ms = 0.0
     planes = []
     inliers_local = 0  # this rank's inliers over the timed steps
@@ -260,6 +265,8 @@ def main():
         launches += s["score_launches"]
         score_ms += s["score_ms"]
         select_ms += s["select_ms"]
+        spec_misses += s["spec_misses"]
+        host_checks += s["pcl_host_checks"]
         planes.append(e["n_planes"])
         inliers_local += int(e["offsets"][-1])
     ctx.synchronize()
@@ -283,24 +290,28 @@ def main():
             ctx.barrier()
             return out, ctx.allreduce_max(time.perf_counter() - t) / k
 
-        # (1) the bit-exact mode: PCL's float refit (host-sequential sums, two-pass selects)
-        if a.pcl_steps > 0:
-            prm_pcl = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
-                                    refit_mode=D.DLG_REFIT_PCL, hypotheses_per_launch=a.hyps,
-                                    gather_inliers=False)
+        # (1) the other refit mode's line: DLG_REFIT_FAST beside the PCL headline (or PCL's
+        # beside a --refit fast run)
+        if a.alt_steps > 0:
+            alt = "fast" if a.refit == "pcl" else "pcl"
+            prm_alt = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
+                                    refit_mode=D.DLG_REFIT_FAST if alt == "fast" else D.DLG_REFIT_PCL,
+                                    hypotheses_per_launch=a.hyps, gather_inliers=False)
 
-            def step_pcl():
+            def step_alt():
                 cloud.reset()
-                return D.extract_planes(cloud, prm_pcl, max_planes=a.planes,
+                return D.extract_planes(cloud, prm_alt, max_planes=a.planes,
                                         min_inliers=a.min_inliers, out=inl_buf)
-            step_pcl()
-            outs, sec = timed_steps(step_pcl, a.pcl_steps)
-            t_pcl = sum(o["stats"]["tests"] for o in outs) / len(outs)
-            extras["refit_pcl"] = {
-                "mode": "DLG_REFIT_PCL (PCL's float refit, bit-exact with the oracle; "
-                        "two-pass selects, host-sequential sums between them)",
-                "value": round(t_pcl / sec / 1e9, 3), "unit": "G point-plane tests/s",
-                "ms_per_step": round(sec * 1e3, 3), "steps": a.pcl_steps,
+            step_alt()
+            outs, sec = timed_steps(step_alt, a.alt_steps)
+            t_alt = sum(o["stats"]["tests"] for o in outs) / len(outs)
+            extras["refit_" + alt] = {
+                "mode": ("DLG_REFIT_FAST: exact least-squares refit (integer moments + Jacobi) -- "
+                         "NOT PCL's arithmetic: its planes and inliers differ from PCL's"
+                         if alt == "fast" else
+                         "DLG_REFIT_PCL: PCL's float refit, bit-exact with the oracle"),
+                "value": round(t_alt / sec / 1e9, 3), "unit": "G point-plane tests/s",
+                "ms_per_step": round(sec * 1e3, 3), "steps": a.alt_steps,
                 "planes_extracted": int(outs[-1]["n_planes"])}
 
         # (2) device-side, including the spatial index (Morton sort + sphere bounds) per step
@@ -383,7 +394,8 @@ def main():
     # the memory-bound passes of a round (H_pass = 1), timed with HIP events around the phase
     # (incl. the small reduce/refit kernels between)
     sum_active = per_rank_tests / max(a.hyps, 1)  # sum over rounds of this rank's active points
-    lean = pruned and lean_rounds == rounds_per_step and a.refit == "fast"
+    per_rank_points_total = a.points
+    lean = pruned and lean_rounds == rounds_per_step
     if lean:
         # lean-list rounds, the phase from the scoring's end to the round's end: the speculative
         # pick, the moments over the Morton copy's near tiles (counted as 12 B per inlier: the
@@ -396,14 +408,25 @@ def main():
                      + 16.0 * sum_active + 16.0 * surv + 1.0 * inliers_local
                      + 5.0 * sum_active + 4.0 * surv + 8.0 * inliers_local
                      + 12.0 * surv + 0.5 * surv)
+        if a.refit == "pcl":
+            # PCL refit instead of the moments: the unrefined inliers stamped into a bitmap over
+            # pristine indices and compacted in list order (bitmap written + read, 12 B gathered
+            # + 12 B written per inlier), then the float-sum passes (k_fs_prep, k_fs_inc: 12 B per
+            # inlier each; k_fs_l1: 12 B per inlier per chain; the 64-byte chunk records of the
+            # nine chains written and walked: 2 x 9 B per inlier).  (Approximate: the stamp pass
+            # reads the near tiles like the moments do; the refit's walk is latency-bound.)
+            sel_bytes += (2.0 * per_rank_points_total / 8.0 * rounds_per_step * a.steps
+                          + 24.0 * inliers_local + (12.0 + 12.0 + 9 * 12.0 + 18.0) * inliers_local)
     else:
         n_copies = 2 if pruned else 1
         sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))
                      + 4.0 * inliers_local)
     sel_gbs = sel_bytes / (select_ms / 1e3) / 1e9 if select_ms > 0 else 0.0
     roofline["memory_bound_passes"] = {
-        "phase": "refit moments + selectWithinDistance + compaction (%s)"
-                 % ("lean rounds: single-pass select of the Morton copy + the index list from "
+        "phase": "%s + selectWithinDistance + compaction (%s)"
+                 % ("PCL float refit (inlier bitmap, compaction, exact float sums, eigen33)"
+                    if a.refit == "pcl" else "refit moments",
+                    "lean rounds: single-pass select of the Morton copy + the index list from "
                     "the inlier stamps" if lean else
                     "list-ordered SoA and Morton copy" if pruned else "list-ordered SoA"),
         "bound": "hbm", "achieved": round(sel_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -505,6 +528,10 @@ def main():
             "tests_launched_per_step": scored // max(a.steps, 1),
             "score_ms_per_step_max_rank": round(score_ms_max / a.steps, 3),
             "select_ms_per_step": round(select_ms / a.steps, 3),
+            # speculative computeModel decisions the host replay overturned (each redoes its
+            # round's refit + select), and PCL-refit tails the host had to confirm
+            "spec_misses_per_step": round(spec_misses / a.steps, 3),
+            "pcl_host_checks_per_step": round(host_checks / a.steps, 3),
             "gen_s": round(gen_s, 2),
             # PCIe-inclusive view (never `value`): host xyz -> SoA upload of this rank's shard
             "upload_ms": round(upload_s * 1e3, 2),

@@ -30,7 +30,7 @@ SYMBOLS = [
     "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
     "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
     "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex", "dlg_cloud_drop_spatial",
-    "dlg_abi_struct_size",
+    "dlg_abi_struct_size", "dlg_float_sums",
 ]
 
 # context options (include/dialog_ransac.h): equivalent execution paths, identical results
@@ -139,6 +139,8 @@ def load():
     L.dlg_barrier.argtypes = [vp]
     L.dlg_score_benchmark.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                       C.POINTER(C.c_double), i32p]
+    L.dlg_float_sums.argtypes = [vp, fp, C.c_int64, fp, C.c_int, fp, fp, C.POINTER(C.c_int),
+                                 C.POINTER(C.c_double)]
     L.dlg_ctx_set_option.argtypes = [vp, C.c_int, C.c_int64]
     L.dlg_ctx_get_option.argtypes = [vp, C.c_int, i64p]
     L.dlg_prune_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int]

@@ -395,9 +395,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // indices instead of list coordinates
   const bool pcl_dev = pcl_refit && c->opt.pcl_dev != 0 && c->comm->world() == 1;
   // (any rank count: the fast refit's moments are exact integers, so summing them over the
-  // Morton copies of the shards gives the list's bits; every rank decides alike, as the inputs
-  // of the decision -- spatial copy present, list lean -- evolve identically on every rank)
+  // Morton copies of the shards gives the list's bits.  Every rank decides alike: whether all
+  // ranks hold a spatial copy is agreed once per extraction (c->sp_all), and the other inputs
+  // -- the list lean, NORMAL_PLANE rounds dropping the copy -- evolve identically on every rank)
   const bool lean = compact && !np && (!pcl_refit || pcl_dev) && c->opt.lean && cl->sp_valid &&
+                    c->sp_all &&
                     cl->n_total < (int64_t(1) << 30) && c->opt.prune != 0 &&
                     (cl->cur < 0 || cl->buf_lean[cl->cur]);
   if (!lean) ensure_list_xyz(c, cl);
@@ -679,7 +681,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         const int64_t cap = std::max<int64_t>(src.n, 1);
         c->fs_scr.ensure(fs_scratch_bytes(cap));
         c->fs_b = fs_carve(c->fs_scr.p, cap);
-        HIPCHK(hipMemsetAsync(c->fs_b.ticket, 0, sizeof(unsigned), c->stream));
+        HIPCHK(hipMemsetAsync(c->fs_b.ticket, 0, 2 * sizeof(unsigned), c->stream));
         c->fs_cap = cap;
       }
       int32_t* fs_res = reinterpret_cast<int32_t*>(c->small.p + 8);
@@ -1468,7 +1470,17 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
     const int64_t floor_n = std::max<int64_t>(3, min_inliers);
     // every rank's active count: gathered once, then carried from each round's survivors
     std::vector<int64_t> active;
-    int64_t N = allgather_i64(c, cl->n_active, &active);
+    // (bit 40: this rank holds a valid spatial copy.  Lean rounds change the round's collective
+    // sequence, so they run only when every rank can take them: one agreed decision per call)
+    constexpr int64_t kSpBit = int64_t(1) << 40;
+    int64_t N = allgather_i64(c, cl->n_active | (cl->sp_valid ? kSpBit : 0), &active);
+    c->sp_all = true;
+    N = 0;
+    for (int64_t& v : active) {
+      c->sp_all = c->sp_all && (v & kSpBit) != 0;
+      v &= kSpBit - 1;
+      N += v;
+    }
     for (int p = 0; p < max_planes; ++p) {
       if (N < floor_n) break;
       dlg_sac_stats st;
@@ -1519,6 +1531,50 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
   c->sp_check = false;
   xs->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return s;
+}
+
+dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float cin[4], int reps,
+                          float sums_out[9], float coeff_out[4], int* uncertain,
+                          double* ms_per_call) {
+  if (!c || n < 0 || n > INT32_MAX || (n > 0 && !xyz) || !cin || reps < 1 || !sums_out ||
+      !coeff_out || !uncertain || !ms_per_call)
+    return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    DevBuf<float> dx;
+    DevBuf<float4> dc;
+    DevBuf<int32_t> dn, dres;
+    DevBuf<uint8_t> scr;
+    dx.ensure(3 * (size_t)std::max<int64_t>(n, 1));
+    dc.ensure(2);
+    dn.ensure(1);
+    dres.ensure(16);
+    scr.ensure(fs_scratch_bytes(std::max<int64_t>(n, 1)));
+    const FsBuffers b = fs_carve(scr.p, std::max<int64_t>(n, 1));
+    HIPCHK(hipMemsetAsync(b.ticket, 0, 2 * sizeof(unsigned), c->stream));
+    if (n) HIPCHK(hipMemcpyAsync(dx.p, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    const int32_t n32 = (int32_t)n;
+    const float4 ci = make_float4(cin[0], cin[1], cin[2], cin[3]);
+    HIPCHK(hipMemcpyAsync(dn.p, &n32, 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(dc.p, &ci, 16, hipMemcpyHostToDevice, c->stream));
+    double total = 0.0;
+    for (int r = 0; r < reps; ++r) {
+      HIPCHK(hipEventRecord(c->ev[0], c->stream));
+      launch_fs_refit(dx.p, dx.p + 1, dx.p + 2, 3, dn.p, std::max<int64_t>(n, 1), b, dc.p,
+                      dc.p + 1, dres.p, c->num_cus, c->stream);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(c->ev[1], c->stream));
+      sync(c);
+      total += event_ms(c, 0, 1);
+    }
+    int32_t h[16];
+    float4 co;
+    HIPCHK(hipMemcpy(h, dres.p, sizeof(h), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&co, dc.p + 1, 16, hipMemcpyDeviceToHost));
+    std::memcpy(sums_out, h + 2, 9 * sizeof(float));
+    coeff_out[0] = co.x; coeff_out[1] = co.y; coeff_out[2] = co.z; coeff_out[3] = co.w;
+    *uncertain = h[0];
+    *ms_per_call = total / reps;
+  });
 }
 
 dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int kernel, int reps,

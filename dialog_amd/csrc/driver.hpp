@@ -177,6 +177,7 @@ struct dlg_ctx {
   std::unique_ptr<Comm> comm;
   std::string err;
   bool profiling = false;
+  bool sp_all = true;  // every rank holds a valid spatial copy (agreed per extraction)
   // scratch
   DevBuf<int32_t> pos;
   DevBuf<SampleRec> samples;

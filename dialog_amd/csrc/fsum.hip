@@ -4,17 +4,24 @@
 //
 // Kernels (stream order; the inlier count lives on the device, so every grid is fixed and the
 // kernels loop over the work the count implies):
-//   k_fs_prep   units of 4096 inliers: per-chunk double sums of the nine terms (the guesses),
-//               per-unit sums; the last workgroup scans the units (double prefixes)
-//   k_fs_run    (unit, chain) items: level-1 fan runs of the 64 chunks from their guesses (4
-//               starts each, 256 lanes, elements staged in LDS), then the unit's level-2 record:
-//               one wave per member walks the 64 chunk records (reruns from LDS)
-//   k_fs_level  levels >= 3 (more than 128 nodes at level 2): one wave per member walks 64
-//               children, descending through per-wave LDS windows of the lower levels
-//   k_fs_top    one wave per chain walks the top level from +0 (descents as above); then the
-//               refit (fs_refit_tail) by one thread: refined plane + uncertainty flag + sums
-// Every wave executes its walk uniformly (all lanes the same values): the lanes are only used to
-// load a 64-node window or a chunk's 64 elements at once.
+//   k_fs_prep   units of 4096 inliers (64 chunks): per-chunk double sums of the nine terms, one
+//               thread per chunk (all nine chains in registers), per-unit sums; the last
+//               workgroup scans the units (double prefixes, optionally from a rank's base)
+//   k_fs_inc    units again, thread (chunk, chain group): each chunk run once from its first
+//               guess fl(double prefix) -> its float increment o - g (double); per-unit sums,
+//               the last workgroup scans them.  The prefix of the increments is the refined
+//               guess: exact wherever every earlier chunk's increment is independent of its
+//               start (the common case), so the records below sit at (or a few quanta from)
+//               the value the walk brings, even where the double prefix drifts by thousands of
+//               quanta from the float chain (sums hovering near zero)
+//   k_fs_l1     (unit, chain) items: the chain's terms staged in LDS, the refined guesses, then
+//               lane (chunk, member) runs the chunk from g_k + member q(g_k): the chunk
+//               records, written as coalesced 16-byte rows
+//   k_fs_walk   one wave per chain: the speculative 64-wide walk over the chunk records from
+//               the chain's start value (+0, or the previous rank's end value); a chunk the
+//               lemma does not cover is rerun from its exact start.  The last chain to finish
+//               runs the refit tail (fs_refit_tail) when the caller asks for it.
+// The walk is wave-uniform: every lane holds one record, the carried value is uniform.
 #include "kernels.hpp"
 #include "dev_common.hpp"
 #include "fsum.hpp"
@@ -24,10 +31,9 @@
 namespace dlg {
 namespace {
 
-constexpr int kFsUnit = kFsChunk * kFsArity;  // 4096 inliers per level-2 node
-constexpr int kFsTopMax = 128;                // the top walk's node count bound
+constexpr int kFsUC = 64;                     // chunks per unit
+constexpr int kFsUnit = kFsChunk * kFsUC;     // 4096 inliers per unit
 constexpr int kFsPad = kFsChunk + 1;          // LDS row stride of a chunk (spreads the banks)
-constexpr int kFsWinLevels = 3;               // LDS windows for levels 1..3 per wave
 
 struct FsDev {
   const float* px;
@@ -38,27 +44,52 @@ struct FsDev {
   FsBuffers b;
 };
 
-__device__ __forceinline__ int fs_top_level(int64_t n) {
-  int L = 1;
-  while (fs_nodes(n, L) > kFsTopMax) ++L;
-  return L;
+__device__ __forceinline__ FsNode* fs_rec(const FsBuffers& b, int c, int64_t k) {
+  return b.rec + (int64_t)c * b.cap + k;
 }
 
-__device__ __forceinline__ FsNode* fs_node_ptr(const FsBuffers& b, int L, int c, int64_t k) {
-  return reinterpret_cast<FsNode*>(b.nodes[L]) + (int64_t)c * b.cap[L] + k;
+template <int C>
+__device__ __forceinline__ void fs_acc9(double (&a)[kFsChains], float x, float y, float z) {
+  a[C] += (double)fs_term(C, x, y, z);
+  if constexpr (C + 1 < kFsChains) fs_acc9<C + 1>(a, x, y, z);
 }
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// the last workgroup of a unit pass scans the per-unit sums usum into the exclusive prefixes
+// upre (from base9, or 0); ticket = the pass's ticket word
+__device__ void fs_scan_units(const FsDev& d, int64_t U, const double* base9, unsigned* ticket,
+                              double* blk) {
+  const int t = threadIdx.x;
+  __builtin_amdgcn_s_waitcnt(0);
+  __shared__ unsigned s_ticket;
+  __syncthreads();
+  if (t == 0)
+    s_ticket = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ticket != gridDim.x - 1) return;
+  if (t == 0) *ticket = 0u;
+  double run = t < kFsChains && base9 ? base9[t] : 0.0;
+  for (int64_t ub = 0; ub < U; ub += kFsUC) {
+    const int nb = (int)(U - ub < kFsUC ? U - ub : kFsUC);
+    __syncthreads();
+    for (int p = t; p < nb * kFsChains; p += blockDim.x)
+      blk[p] = __longlong_as_double(__hip_atomic_load(
+          reinterpret_cast<const int64_t*>(d.b.usum) + ub * kFsChains + p, __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    if (t < kFsChains) {
+      for (int q = 0; q < nb; ++q) {
+        d.b.upre[(ub + q) * kFsChains + t] = run;
+        run += blk[q * kFsChains + t];
+      }
+    }
+  }
 }
 
 // ---- k_fs_prep --------------------------------------------------------------------------------
 constexpr int kFpBS = 256;
-__global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d) {
-  __shared__ float sx[kFsArity * kFsPad], sy[kFsArity * kFsPad], sz[kFsArity * kFsPad];
-  __shared__ double scs[kFsArity * kFsChains];
+__global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d, const double* __restrict__ base9) {
+  __shared__ float sx[kFsUC * kFsPad], sy[kFsUC * kFsPad], sz[kFsUC * kFsPad];
+  __shared__ double scs[kFsUC * kFsChains];
   const int64_t n = *d.n_dev;
   const int64_t U = (n + kFsUnit - 1) / kFsUnit;
   const int t = threadIdx.x;
@@ -73,16 +104,18 @@ __global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d) {
       sx[li] = d.px[e]; sy[li] = d.py[e]; sz[li] = d.pz[e];
     }
     __syncthreads();
-    for (int p = t; p < nch * kFsChains; p += kFpBS) {
-      const int k = p / kFsChains, c = p % kFsChains;
-      const int len = cnt - k * kFsChunk < kFsChunk ? cnt - k * kFsChunk : kFsChunk;
-      double s = 0.0;
+    if (t < nch) {  // thread = chunk: the nine double sums together
+      double a[kFsChains] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      const int len = cnt - t * kFsChunk < kFsChunk ? cnt - t * kFsChunk : kFsChunk;
       for (int j = 0; j < len; ++j) {
-        const int li = k * kFsPad + j;
-        s += (double)fs_term(c, sx[li], sy[li], sz[li]);
+        const int li = t * kFsPad + j;
+        fs_acc9<0>(a, sx[li], sy[li], sz[li]);
       }
-      scs[p] = s;
-      d.b.csum[(u * kFsArity + k) * kFsChains + c] = s;
+#pragma unroll
+      for (int c = 0; c < kFsChains; ++c) {
+        scs[t * kFsChains + c] = a[c];
+        d.b.csum[(u * kFsUC + t) * kFsChains + c] = a[c];
+      }
     }
     __syncthreads();
     if (t < kFsChains) {
@@ -94,63 +127,93 @@ __global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d) {
   }
   // the last workgroup scans the unit sums (agent-scope stores acknowledged before the ticket,
   // read back with agent-scope loads: k_moments' pattern)
-  __builtin_amdgcn_s_waitcnt(0);
-  __shared__ unsigned s_ticket;
-  __syncthreads();
-  if (t == 0)
-    s_ticket = __hip_atomic_fetch_add(d.b.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (s_ticket != gridDim.x - 1) return;
-  if (t == 0) *d.b.ticket = 0u;
-  double* blk = scs;  // (reused: 64 units x 9 per block)
-  double run = 0.0;
-  for (int64_t ub = 0; ub < U; ub += kFsArity) {
-    const int nb = (int)(U - ub < kFsArity ? U - ub : kFsArity);
-    __syncthreads();
-    for (int p = t; p < nb * kFsChains; p += kFpBS)
-      blk[p] = __longlong_as_double(__hip_atomic_load(
-          reinterpret_cast<const int64_t*>(d.b.usum) + ub * kFsChains + p, __ATOMIC_RELAXED,
-          __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();
-    if (t < kFsChains) {
-      for (int q = 0; q < nb; ++q) {
-        d.b.upre[(ub + q) * kFsChains + t] = run;
-        run += blk[q * kFsChains + t];
-      }
-    }
-  }
+  fs_scan_units(d, U, base9, d.b.ticket, scs);
 }
 
-// ---- k_fs_run ---------------------------------------------------------------------------------
-// the level-2 walk's store: the unit's chunk records and elements in LDS
-struct FsUnitStore {
-  const FsNode* sn;
-  int64_t k0, K;
-  const float *sx, *sy, *sz;
-  int c, cnt;
-  __device__ const FsNode& node(int, int64_t k) { return sn[k - k0]; }
-  __device__ int64_t nodes(int) const { return K; }
-  __device__ FsRun rerun(int64_t k, float v) {
-    const int kk = (int)(k - k0);
-    const int len = cnt - kk * kFsChunk < kFsChunk ? cnt - kk * kFsChunk : kFsChunk;
-    FsState st = fs_start(v);
-    for (int j = 0; j < len; ++j) {
-      const int li = kk * kFsPad + j;
-      fs_step(st, fs_term(c, sx[li], sy[li], sz[li]));
-    }
-    return fs_finish(st);
-  }
-};
-
-constexpr int kFrBS = kFsArity * kFsFan;  // 64 chunks x 4 members
-__global__ __launch_bounds__(kFrBS) void k_fs_run(FsDev d) {
-  __shared__ float sx[kFsArity * kFsPad], sy[kFsArity * kFsPad], sz[kFsArity * kFsPad];
-  __shared__ FsNode sn[kFsArity];
-  __shared__ float sg[kFsArity];
-  __shared__ double s_cs[kFsArity];
+// ---- k_fs_inc ---------------------------------------------------------------------------------
+// in place: csum (chunk double sums) -> the chunks' float increments, usum -> their unit sums,
+// upre (double prefixes) -> the increments' prefixes.  Each unit is read and rewritten by one
+// workgroup; the scan runs after every workgroup has passed its ticket.
+constexpr int kFiBS = 256;  // 64 chunks x 4 chain groups (chains g, g + 4, g + 8)
+__global__ __launch_bounds__(kFiBS) void k_fs_inc(FsDev d, const double* __restrict__ base9) {
+  __shared__ float sx[kFsUC * kFsPad], sy[kFsUC * kFsPad], sz[kFsUC * kFsPad];
+  __shared__ double scs[kFsUC * kFsChains];
+  __shared__ double spre[kFsChains];
   const int64_t n = *d.n_dev;
-  const int64_t U = (n + kFsUnit - 1) / kFsUnit, K = fs_nodes(n, 1);
-  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  const int64_t U = (n + kFsUnit - 1) / kFsUnit;
+  const int t = threadIdx.x, k = t & 63, cg = t >> 6;
+  for (int64_t u = blockIdx.x; u < U; u += gridDim.x) {
+    const int64_t e0 = u * kFsUnit;
+    const int cnt = (int)(n - e0 < kFsUnit ? n - e0 : kFsUnit);
+    const int nch = (cnt + kFsChunk - 1) / kFsChunk;
+    __syncthreads();
+    for (int j = t; j < cnt; j += kFiBS) {
+      const int64_t e = (e0 + j) * d.stride;
+      const int li = (j >> 6) * kFsPad + (j & 63);
+      sx[li] = d.px[e]; sy[li] = d.py[e]; sz[li] = d.pz[e];
+    }
+    for (int p = t; p < nch * kFsChains; p += kFiBS)
+      scs[p] = d.b.csum[u * kFsUC * kFsChains + p];
+    if (t < kFsChains) spre[t] = d.b.upre[u * kFsChains + t];
+    __syncthreads();
+    double inc[3] = {0.0, 0.0, 0.0};
+    if (k < nch) {
+      const int len = cnt - k * kFsChunk < kFsChunk ? cnt - k * kFsChunk : kFsChunk;
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int c = cg + 4 * m;
+        if (c >= kFsChains) break;
+        double pre = spre[c];
+        for (int q = 0; q < k; ++q) pre += scs[q * kFsChains + c];
+        const float g = (float)pre;
+        float v = g;
+        for (int j = 0; j < len; ++j) {
+          const int li = k * kFsPad + j;
+          v = v + fs_term(c, sx[li], sy[li], sz[li]);
+        }
+        inc[m] = (double)v - (double)g;
+      }
+    }
+    __syncthreads();  // (every thread has read the double sums)
+    if (k < nch) {
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int c = cg + 4 * m;
+        if (c >= kFsChains) break;
+        scs[k * kFsChains + c] = inc[m];
+        d.b.csum[(u * kFsUC + k) * kFsChains + c] = inc[m];
+      }
+    }
+    __syncthreads();
+    if (t < kFsChains) {
+      double s = 0.0;
+      for (int q = 0; q < nch; ++q) s += scs[q * kFsChains + t];
+      __hip_atomic_store(reinterpret_cast<int64_t*>(d.b.usum) + u * kFsChains + t,
+                         __double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  fs_scan_units(d, U, base9, d.b.ticket, scs);
+}
+
+__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const double u = __shfl_up(v, off, kWave);
+    if (lane >= off) v += u;
+  }
+  return v;
+}
+
+// ---- k_fs_l1 ----------------------------------------------------------------------------------
+constexpr int kFlBS = kFsUC * kFsFan;  // 64 chunks x 4 members
+__global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
+  __shared__ float sp[kFsUC * kFsPad];
+  __shared__ float4 sn[kFsUC * 4];  // the unit's records, 4 rows of 16 bytes each
+  __shared__ double s_cs[kFsUC];
+  __shared__ float sg[kFsUC];
+  const int64_t n = *d.n_dev;
+  const int64_t U = (n + kFsUnit - 1) / kFsUnit;
+  const int t = threadIdx.x;
   for (int64_t it = blockIdx.x; it < U * kFsChains; it += gridDim.x) {
     const int64_t u = it / kFsChains;
     const int c = (int)(it % kFsChains);
@@ -158,21 +221,20 @@ __global__ __launch_bounds__(kFrBS) void k_fs_run(FsDev d) {
     const int cnt = (int)(n - e0 < kFsUnit ? n - e0 : kFsUnit);
     const int nch = (cnt + kFsChunk - 1) / kFsChunk;
     __syncthreads();
-    for (int j = t; j < cnt; j += kFrBS) {
+    for (int j = t; j < cnt; j += kFlBS) {
       const int64_t e = (e0 + j) * d.stride;
-      const int li = (j >> 6) * kFsPad + (j & 63);
-      sx[li] = d.px[e]; sy[li] = d.py[e]; sz[li] = d.pz[e];
+      sp[(j >> 6) * kFsPad + (j & 63)] = fs_term(c, d.px[e], d.py[e], d.pz[e]);
     }
-    if (t < nch) s_cs[t] = d.b.csum[(u * kFsArity + t) * kFsChains + c];
+    if (t < nch) s_cs[t] = d.b.csum[(u * kFsUC + t) * kFsChains + c];
     __syncthreads();
     if (t < nch) {
-      // the guess at chunk t: fl(double prefix of the terms), unit prefix + chunks before it
+      // the guess at chunk t: fl(prefix of the increments), unit prefix + chunks before it
       double pre = d.b.upre[u * kFsChains + c];
       for (int k = 0; k < t; ++k) pre += s_cs[k];
       sg[t] = (float)pre;
     }
     __syncthreads();
-    {  // level 1: lane (chunk k, member i) runs the chunk from g_k + i q(g_k)
+    {  // lane (chunk k, member i) runs the chunk from g_k + i q(g_k)
       const int k = t >> 2, i = t & 3;
       if (k < nch) {
         const float g = sg[k];
@@ -180,180 +242,280 @@ __global__ __launch_bounds__(kFrBS) void k_fs_run(FsDev d) {
         const bool ok = fs_member_start(g, i, &a);
         const int len = cnt - k * kFsChunk < kFsChunk ? cnt - k * kFsChunk : kFsChunk;
         FsState st = fs_start(a);
-        for (int j = 0; j < len; ++j) {
-          const int li = k * kFsPad + j;
-          fs_step(st, fs_term(c, sx[li], sy[li], sz[li]));
-        }
+        for (int j = 0; j < len; ++j) fs_step(st, sp[k * kFsPad + j]);
         const FsRun r = fs_finish(st);
-        sn[k].o[i] = ok ? r.o : 0.0f;
-        sn[k].mu[i] = ok ? r.mu : 0.0f;
-        sn[k].qm[i] = ok ? r.qm : __builtin_nanf("");
+        float* row = reinterpret_cast<float*>(&sn[k * 4]);
+        row[4 + i] = ok ? r.o : 0.0f;
+        row[8 + i] = ok ? r.mu : 0.0f;
+        row[12 + i] = ok ? r.qm : __builtin_nanf("");
         if (i == 0) {
-          sn[k].g = g;
-          sn[k].pad0 = sn[k].pad1 = sn[k].pad2 = 0.0f;
+          row[0] = g;
+          row[1] = row[2] = row[3] = 0.0f;
         }
       }
     }
     __syncthreads();
-    // level-1 records out (the top walk's descents read them)
-    for (int p = t; p < nch * 4; p += kFrBS) {
-      const float4* src = reinterpret_cast<const float4*>(&sn[p >> 2]) + (p & 3);
-      reinterpret_cast<float4*>(fs_node_ptr(d.b, 1, c, u * kFsArity + (p >> 2)))[p & 3] = *src;
-    }
-    {  // level 2: wave wv walks member wv of the unit through the chunk records
-      float a;
-      const bool ok = fs_member_start(sg[0], wv, &a);
-      FsUnitStore st{sn, u * kFsArity, K, sx, sy, sz, c, cnt};
-      float mu = INFINITY, qm = 0.0f, o = 0.0f;
-      if (ok) o = fs_walk(st, 1, u * kFsArity, nch, a, &mu, &qm, nullptr);
-      if (lane == 0) {
-        FsNode* nd = fs_node_ptr(d.b, 2, c, u);
-        nd->o[wv] = ok ? o : 0.0f;
-        nd->mu[wv] = ok ? mu : 0.0f;
-        nd->qm[wv] = ok ? qm : __builtin_nanf("");
-        if (wv == 0) {
-          nd->g = sg[0];
-          nd->pad0 = nd->pad1 = nd->pad2 = 0.0f;
+    if (t < kWave) {
+      // the walk's speculation data in the record's spare words: the exclusive prefix (double,
+      // pad0:pad1) of the member-0 increments over the unit's chunks, and pad2 = mu3, the fast
+      // path's margin: when all four members are usable, share one increment and keep their
+      // quanta <= 2 q(g), any start t = g + d q(g) with |t - g| <= min_i mu_i - 3 q(g) is
+      // covered by its member (|D| <= |t - g| + 3 q) and yields t + the increment.  mu3 < 0:
+      // the record needs the full lemma (fs_apply) at every start.
+      float* row = reinterpret_cast<float*>(&sn[t * 4]);
+      double d0 = 0.0;
+      float mu3 = -1.0f;
+      if (t < nch) {
+        const float g = row[0];
+        const double q = (double)fs_quantum(g);
+        bool fast = true;
+        double mum = INFINITY;
+        for (int i = 0; i < kFsFan; ++i) {
+          const float o = row[4 + i], mu = row[8 + i], qm = row[12 + i];
+          if (!(qm >= 0.0f) || !((double)qm <= 2.0 * q)) fast = false;
+          const double di = (double)o - ((double)g + (double)i * q);
+          if (i == 0) d0 = di;
+          else if (di != d0) fast = false;
+          mum = fmin(mum, (double)mu);
+        }
+        if (!(d0 == d0)) {  // (a non-finite run: left to the exact paths)
+          d0 = 0.0;
+          fast = false;
+        }
+        const double m3 = mum - 3.0 * q;
+        if (fast && m3 >= 0.0) {
+          float f = (float)m3;
+          if ((double)f > m3) f = nextafterf(f, 0.0f);  // (rounded down)
+          mu3 = f;
         }
       }
+      const double inc = wave_incl_scan(d0, t);
+      const double ex = inc - d0;
+      // (exclusive prefix: inc - d0 may round; the walk verifies every speculated start anyway)
+      if (t < nch) {
+        const uint64_t eb = (uint64_t)__double_as_longlong(ex);
+        row[1] = __uint_as_float((uint32_t)eb);
+        row[2] = __uint_as_float((uint32_t)(eb >> 32));
+        row[3] = mu3;
+      }
     }
+    __syncthreads();
+    for (int p = t; p < nch * 4; p += kFlBS)
+      reinterpret_cast<float4*>(fs_rec(d.b, c, u * kFsUC + (p >> 2)))[p & 3] = sn[p];
   }
 }
 
-// ---- walks over the global records ---------------------------------------------------------
-// per-wave LDS windows of 64 nodes for levels 1..kFsWinLevels; higher levels through a one-node
-// slot.  Reruns keep the chunk's elements in the lanes' registers (one element per lane) and step
-// through them with readlane.
-struct FsGlobalStore {
-  const FsDev* d;
-  int c;
-  int64_t n;
-  FsNode* win;      // [kFsWinLevels][64] (LDS, this wave's)
-  FsNode* slot;     // one node (LDS, this wave's)
-  int64_t base[kFsWinLevels + 1];
-  int64_t cnt[kFsMaxLevels + 1];
-  __device__ void init(const FsDev* dd, int cc, int64_t nn, FsNode* w, FsNode* s) {
-    d = dd; c = cc; n = nn; win = w; slot = s;
-    for (int l = 0; l <= kFsWinLevels; ++l) base[l] = -1;
-    for (int l = 1; l <= kFsMaxLevels; ++l) cnt[l] = fs_nodes(n, l);
-  }
-  __device__ int64_t nodes(int L) const { return cnt[L]; }
-  __device__ const FsNode& node(int L, int64_t k) {
-    const int lane = threadIdx.x & (kWave - 1);
-    if (L <= kFsWinLevels) {
-      const int64_t b = k & ~(int64_t)(kWave - 1);
-      FsNode* w = win + (L - 1) * kWave;
-      if (base[L] != b) {
-        wave_sync();
-        if (b + lane < cnt[L]) {
-          const float4* src = reinterpret_cast<const float4*>(fs_node_ptr(d->b, L, c, b + lane));
-          float4* dst = reinterpret_cast<float4*>(w + lane);
-          const float4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
-          dst[0] = v0; dst[1] = v1; dst[2] = v2; dst[3] = v3;
-        }
-        wave_sync();
-        base[L] = b;
-      }
-      return w[k - b];
-    }
-    wave_sync();
-    if (lane < 4)
-      reinterpret_cast<float4*>(slot)[lane] =
-          reinterpret_cast<const float4*>(fs_node_ptr(d->b, L, c, k))[lane];
-    wave_sync();
-    return *slot;
-  }
-  __device__ FsRun rerun(int64_t k, float v) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t e = k * kFsChunk + lane;
-    const int len = n - k * kFsChunk < kFsChunk ? (int)(n - k * kFsChunk) : kFsChunk;
-    float x = 0.0f, y = 0.0f, z = 0.0f;
-    if (lane < len) {
-      x = d->px[e * d->stride]; y = d->py[e * d->stride]; z = d->pz[e * d->stride];
-    }
-    FsState st = fs_start(v);
-    for (int j = 0; j < len; ++j) {
-      const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j));
-      const float yj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), j));
-      const float zj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), j));
-      fs_step(st, fs_term(c, xj, yj, zj));
-    }
-    return fs_finish(st);
-  }
-};
+// ---- k_fs_walk --------------------------------------------------------------------------------
+__device__ __forceinline__ float rdl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 
-// ---- k_fs_level: level l >= 3 records (only when level l - 1 has more than kFsTopMax nodes) --
-constexpr int kFlBS = kWave * kFsFan;
-template <int l>
-__global__ __launch_bounds__(kFlBS) void k_fs_level(FsDev d) {
-  __shared__ FsNode s_win[kFsFan][kFsWinLevels * kWave];
-  __shared__ FsNode s_slot[kFsFan];
-  const int64_t n = *d.n_dev;
-  if (fs_top_level(n) < l) return;
-  const int64_t M = fs_nodes(n, l), Mc = fs_nodes(n, l - 1);
-  const int wv = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  for (int64_t it = blockIdx.x; it < M * kFsChains; it += gridDim.x) {
-    const int64_t k = it / kFsChains;
-    const int c = (int)(it % kFsChains);
-    const int64_t c0 = k * kFsArity;
-    const int64_t cc = Mc - c0 < kFsArity ? Mc - c0 : kFsArity;
-    FsGlobalStore st;
-    st.init(&d, c, n, s_win[wv], &s_slot[wv]);
-    const float g = st.node(l - 1, c0).g;  // (the guess at the node's first element)
-    float a;
-    const bool ok = fs_member_start(g, wv, &a);
-    float mu = INFINITY, qm = 0.0f, o = 0.0f;
-    if (ok) o = fs_walk(st, l - 1, c0, cc, a, &mu, &qm, nullptr);
-    if (lane == 0) {
-      FsNode* nd = fs_node_ptr(d.b, l, c, k);
-      nd->o[wv] = ok ? o : 0.0f;
-      nd->mu[wv] = ok ? mu : 0.0f;
-      nd->qm[wv] = ok ? qm : __builtin_nanf("");
-      if (wv == 0) {
-        nd->g = g;
-        nd->pad0 = nd->pad1 = nd->pad2 = 0.0f;
-      }
-    }
-    wave_sync();
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// lane l + 1's value (DPP wave_shl:1; the last lane gets its own)
+__device__ __forceinline__ double dpp_next(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)b, (int)(uint32_t)b,
+                                                            0x130, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(b >> 32),
+                                                            (int)(uint32_t)(b >> 32), 0x130, 0xF,
+                                                            0xF, false);
+  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
+}
+
+// chunk k rerun from v (its exact start): its terms one per lane, summed in order
+__device__ __forceinline__ float fs_rerun(const FsDev& d, int c, int64_t k, int64_t n, float v,
+                                          int lane) {
+  const int64_t e0 = k * kFsChunk;
+  const int len = n - e0 < kFsChunk ? (int)(n - e0) : kFsChunk;
+  const int64_t e = (e0 + (lane < len ? lane : 0)) * d.stride;
+  // (inline asm with its own drain: a compiler-visible load here would make the compiler wait on
+  // the load counter at the top of every walk iteration, i.e. on the ring's prefetches)
+  float x, y, z;
+  asm volatile(
+      "global_load_dword %0, %3, off\n\t"
+      "global_load_dword %1, %4, off\n\t"
+      "global_load_dword %2, %5, off\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(x), "=&v"(y), "=&v"(z)
+      : "v"(d.px + e), "v"(d.py + e), "v"(d.pz + e)
+      : "memory");
+  const float p = fs_term(c, x, y, z);
+  for (int j = 0; j < len; ++j) v = v + rdl(p, j);
+  return v;
+}
+
+// The walk's records stream through an LDS ring of kFsRing windows (4 KB each: 64 records of 64
+// bytes, the global layout): global_load_lds_dwordx4 moves a window with 4 instructions and no
+// registers, kFsRing - 1 windows ahead of the one being walked.  The loads are counted by vmcnt
+// in issue order, so before reading window w the wave waits until at most the 4 (kFsRing - 1)
+// loads of the windows after it are outstanding (a rerun's own loads drain the counter anyway).
+constexpr int kFsRing = 8;
+constexpr int kFsWinBytes = kWave * (int)sizeof(FsNode);
+
+__device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int64_t K,
+                                             __attribute__((address_space(3))) void* slot,
+                                             int lane) {
+  // (past the last record: the last window's loads re-read valid memory, never used)
+  const int64_t w0 = base < K ? base : (K - 1) / kWave * kWave;
+  const char* src = reinterpret_cast<const char*>(R + w0) + 16 * lane;
+  const int64_t lim = K * (int64_t)sizeof(FsNode) - 16 - w0 * (int64_t)sizeof(FsNode);
+  // (inline asm: the compiler neither sees these loads nor drains them before its own LDS and
+  // VMEM instructions; fs_ring_wait accounts for them)
+  const uint32_t lds = (uint32_t)(uintptr_t)slot;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t off = (int64_t)j * 1024 + 16 * lane;
+    const char* p = off <= lim ? src + j * 1024 : reinterpret_cast<const char*>(R + w0);
+    asm volatile("global_load_lds_dwordx4 %0, off" : : "v"(p), "{m0}"(lds + j * 1024) : "memory");
   }
 }
 
-// ---- k_fs_top: the chains' values, then the refit ----------------------------------------------
-constexpr int kFtBS = kWave * kFsChains;
-__global__ __launch_bounds__(kFtBS) void k_fs_top(FsDev d, const float4* __restrict__ cin,
-                                                  float4* __restrict__ cout,
-                                                  int32_t* __restrict__ res) {
-  __shared__ FsNode s_win[kFsChains][kFsWinLevels * kWave];
-  __shared__ FsNode s_slot[kFsChains];
-  __shared__ float s_sum[kFsChains];
+__device__ __forceinline__ void fs_ring_wait() {
+  // vmcnt <= 4 (kFsRing - 1) = 28: lgkmcnt and expcnt left at their maxima (no wait)
+  static_assert(4 * (kFsRing - 1) == 28, "ring depth and the s_waitcnt immediate");
+  asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+}
+
+constexpr int kFwBS = kWave;
+__global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restrict__ start9,
+                                                   const float4* __restrict__ cin,
+                                                   float4* __restrict__ cout,
+                                                   int32_t* __restrict__ res) {
+  __shared__ __attribute__((aligned(16))) char ring[kFsRing * kFsWinBytes];
+  const int c = blockIdx.x, lane = threadIdx.x;
   const int64_t n = *d.n_dev;
-  const int c = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  {
-    FsGlobalStore st;
-    st.init(&d, c, n, s_win[c], &s_slot[c]);
-    const int L = fs_top_level(n);
-    float mu = INFINITY, qm = 0.0f;
-    const float v = fs_walk(st, L, 0, st.nodes(L), 0.0f, &mu, &qm, nullptr);
-    if (lane == 0) s_sum[c] = v;
+  const int64_t K = fs_chunks(n);
+  const FsNode* R = fs_rec(d.b, c, 0);
+  float t = start9 ? start9[c] : 0.0f;
+  auto slot = [&](int64_t w) {
+    return (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)ring +
+                                                       (w % kFsRing) * kFsWinBytes);
+  };
+  if (K > 0)
+    for (int w = 0; w < kFsRing; ++w) fs_ring_load(R, (int64_t)w * kWave, K, slot(w), lane);
+  for (int64_t w = 0, base = 0; base < K; ++w, base += kWave) {
+    fs_ring_wait();
+    // the record from the ring: read by inline asm, since the compiler would otherwise drain
+    // every outstanding load (vmcnt(0)) before an LDS read that may alias an LDS-DMA write
+    f32x4 r0, r1, r2, r3;
+    {
+      const uint32_t la = (uint32_t)(uintptr_t)(
+          (__attribute__((address_space(3))) char*)slot(w) + sizeof(FsNode) * lane);
+      asm volatile(
+          "ds_read_b128 %0, %4\n\t"
+          "ds_read_b128 %1, %4 offset:16\n\t"
+          "ds_read_b128 %2, %4 offset:32\n\t"
+          "ds_read_b128 %3, %4 offset:48\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+          : "v"(la)
+          : "memory");
+    }
+    // (the slot is free once read: the window kFsRing ahead goes into it)
+    fs_ring_load(R, base + (int64_t)kFsRing * kWave, K, slot(w), lane);
+    const int cnt = K - base < kWave ? (int)(K - base) : kWave;
+    FsNode nd;
+    nd.g = r0.x;
+    nd.pad0 = nd.pad1 = nd.pad2 = 0.0f;
+    nd.o[0] = r1.x; nd.o[1] = r1.y; nd.o[2] = r1.z; nd.o[3] = r1.w;
+    nd.mu[0] = r2.x; nd.mu[1] = r2.y; nd.mu[2] = r2.z; nd.mu[3] = r2.w;
+    nd.qm[0] = r3.x; nd.qm[1] = r3.y; nd.qm[2] = r3.z; nd.qm[3] = r3.w;
+    const double P = __longlong_as_double((int64_t)(((uint64_t)__float_as_uint(r0.z) << 32) |
+                                                    __float_as_uint(r0.y)));
+    const float mu3 = r0.w;
+    const bool fastrec = mu3 >= 0.0f;
+    const double gd = (double)nd.g;
+    const double iq = fs_inv_quantum(nd.g);
+    const double d0 = nd.qm[0] >= 0.0f ? (double)nd.o[0] - gd : 0.0;
+    int s = 0;
+    while (s < cnt) {
+      const bool act = lane >= s && lane < cnt;
+      const uint64_t pb = (uint64_t)__double_as_longlong(P);
+      const double Ps = __longlong_as_double((int64_t)(
+          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pb, s) |
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pb >> 32), s) << 32)));
+      // the speculated starts: t + the member-0 increments of lanes s.., corrected where a
+      // chunk's increment depends on its start (its member chosen by the walk's lead on the
+      // guesses at lane s)
+      double corr = 0.0;
+      const uint64_t slowm = ballot(act && !fastrec);
+      if (slowm) {
+        const double off = (double)t - (double)rdl(nd.g, s);
+        const double cl = act && !fastrec ? fs_increment(nd, off) - d0 : 0.0;
+        const double inc = wave_incl_scan(cl, lane);
+        const double up = __shfl_up(inc, 1, kWave);
+        corr = lane == 0 ? 0.0 : up;
+      }
+      const double tl = (double)t + ((P - Ps) + corr);
+      // the next lane's speculated start (DPP wave shift: no LDS instruction on this path)
+      const double tn = dpp_next(tl);
+      const bool last = lane == cnt - 1;
+      // fast path (see k_fs_l1): a float start within mu3 of the guess, on its quantum grid
+      const double dq = (tl - gd) * iq;
+      double out = tl + d0;
+      bool ver = fastrec && (double)(float)tl == tl && fabs(tl - gd) <= (double)mu3 &&
+                 dq == floor(dq) && (double)(float)out == out && (last || out == tn);
+      if (ballot(act && !ver)) {
+        // the full lemma where the fast path does not decide
+        if (act && !ver) {
+          FsApply a;
+          a.out = 0.0f;
+          const float tf = (float)tl;
+          const bool ok = (double)tf == tl && fs_apply(tf, nd, &a);
+          out = (double)a.out;
+          ver = ok && (last || out == tn);
+        }
+      }
+      const uint64_t bad = ballot(act && !ver);
+      if (bad == 0) {
+        t = rdl((float)out, cnt - 1);
+        break;
+      }
+      int f = (int)__builtin_ctzll(bad);
+      // lanes s..f-1 verified: f's start is exact.  Step lane by lane from f while the records
+      // need the full lemma (sums hovering near zero: runs of such chunks), then speculate again.
+      t = f == s ? t : rdl((float)out, f - 1);
+      for (;;) {
+        FsApply a2;
+        a2.out = 0.0f;
+        const bool ok2 = fs_apply(t, nd, &a2);
+        if (__builtin_amdgcn_readlane((int)ok2, f))
+          t = rdl(a2.out, f);
+        else
+          t = fs_rerun(d, c, base + f, n, t, lane);
+        ++f;
+        if (f >= cnt || rdl(mu3, f) >= 0.0f) break;
+      }
+      s = f;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // (the ring's last loads: never read, but drained)
+  __shared__ unsigned s_ticket;
+  if (lane == 0) {
+    __hip_atomic_store(reinterpret_cast<int32_t*>(d.b.sums) + c, __float_as_int(t),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);
+    s_ticket = cout ? __hip_atomic_fetch_add(d.b.ticket + 1, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                    : 0u;
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  if (!cout || s_ticket != gridDim.x - 1 || lane != 0) return;
+  d.b.ticket[1] = 0u;
+  float a9[kFsChains];
+  for (int k = 0; k < kFsChains; ++k)
+    a9[k] = __int_as_float(__hip_atomic_load(reinterpret_cast<const int32_t*>(d.b.sums) + k,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const float4 ci = *cin;
   const float cv[4] = {ci.x, ci.y, ci.z, ci.w};
-  float a[9], co[4];
-  for (int k = 0; k < 9; ++k) a[k] = s_sum[k];
+  float co[4];
   bool unc = false;
-  fs_refit_tail(a, n, cv, co, &unc);
+  fs_refit_tail(a9, n, cv, co, &unc);
   *cout = make_float4(co[0], co[1], co[2], co[3]);
   res[0] = unc ? 1 : 0;
   res[1] = (int32_t)n;
-  for (int k = 0; k < 9; ++k) res[2 + k] = __float_as_int(a[k]);
-}
-
-int fs_levels_host(int64_t n) {
-  int L = 1;
-  while (fs_nodes(n, L) > kFsTopMax) ++L;
-  return L < 2 ? 2 : L;  // (k_fs_run always writes level 2)
+  for (int k = 0; k < kFsChains; ++k) res[2 + k] = __float_as_int(a9[k]);
 }
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -362,16 +524,14 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t fs_scratch_bytes(int64_t n_cap) {
   const int64_t nc = n_cap > 0 ? n_cap : 1;
-  const int64_t K = fs_nodes(nc, 1), U = fs_nodes(nc, 2);
-  size_t b = align256(sizeof(double) * K * kFsChains) + 2 * align256(sizeof(double) * U * kFsChains);
-  const int L = fs_levels_host(nc);
-  for (int l = 1; l <= L; ++l) b += align256(sizeof(FsNode) * fs_nodes(nc, l) * kFsChains);
-  return b + 256;
+  const int64_t K = fs_chunks(nc), U = (K + kFsUC - 1) / kFsUC;
+  return align256(sizeof(double) * K * kFsChains) + 2 * align256(sizeof(double) * U * kFsChains) +
+         align256(sizeof(FsNode) * K * kFsChains) + align256(sizeof(float) * 16) + 256;
 }
 
 FsBuffers fs_carve(void* base, int64_t n_cap) {
   const int64_t nc = n_cap > 0 ? n_cap : 1;
-  const int64_t K = fs_nodes(nc, 1), U = fs_nodes(nc, 2);
+  const int64_t K = fs_chunks(nc), U = (K + kFsUC - 1) / kFsUC;
   uint8_t* p = static_cast<uint8_t*>(base);
   FsBuffers b;
   b.csum = reinterpret_cast<double*>(p);
@@ -380,13 +540,12 @@ FsBuffers fs_carve(void* base, int64_t n_cap) {
   p += align256(sizeof(double) * U * kFsChains);
   b.upre = reinterpret_cast<double*>(p);
   p += align256(sizeof(double) * U * kFsChains);
-  const int L = fs_levels_host(nc);
-  for (int l = 1; l <= L; ++l) {
-    b.nodes[l] = p;
-    b.cap[l] = fs_nodes(nc, l);
-    p += align256(sizeof(FsNode) * fs_nodes(nc, l) * kFsChains);
-  }
-  b.ticket = reinterpret_cast<unsigned*>(p);
+  b.rec = reinterpret_cast<FsNode*>(p);
+  b.cap = K;
+  p += align256(sizeof(FsNode) * K * kFsChains);
+  b.sums = reinterpret_cast<float*>(p);
+  p += align256(sizeof(float) * 16);
+  b.ticket = reinterpret_cast<unsigned*>(p);  // [0]: k_fs_prep, [1]: k_fs_walk
   return b;
 }
 
@@ -395,22 +554,13 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      float4* cout, int32_t* res, int num_cus, hipStream_t s) {
   FsDev d{px, py, pz, stride, n_dev, b};
   const int64_t nc = n_cap > 0 ? n_cap : 1;
-  const int64_t U = fs_nodes(nc, 2);
+  const int64_t U = (fs_chunks(nc) + kFsUC - 1) / kFsUC;
   const int gp = (int)std::min<int64_t>(U, 2 * (int64_t)num_cus);
-  const int gr = (int)std::min<int64_t>(U * kFsChains, 4 * (int64_t)num_cus);
-  hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d);
-  hipLaunchKernelGGL(k_fs_run, dim3(gr), dim3(kFrBS), 0, s, d);
-  const int L = fs_levels_host(nc);
-  for (int l = 3; l <= L; ++l) {
-    const int g = (int)std::min<int64_t>(fs_nodes(nc, l) * kFsChains, 4 * (int64_t)num_cus);
-    switch (l) {
-      case 3: hipLaunchKernelGGL(k_fs_level<3>, dim3(g), dim3(kFlBS), 0, s, d); break;
-      case 4: hipLaunchKernelGGL(k_fs_level<4>, dim3(g), dim3(kFlBS), 0, s, d); break;
-      case 5: hipLaunchKernelGGL(k_fs_level<5>, dim3(g), dim3(kFlBS), 0, s, d); break;
-      default: break;  // (n < 2^31: at most 5 levels)
-    }
-  }
-  hipLaunchKernelGGL(k_fs_top, dim3(1), dim3(kFtBS), 0, s, d, cin, cout, res);
+  const int gl = (int)std::min<int64_t>(U * kFsChains, 8 * (int64_t)num_cus);
+  hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr);
+  hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, nullptr);
+  hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
+  hipLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, d, nullptr, cin, cout, res);
 }
 
 }  // namespace dlg

@@ -21,18 +21,21 @@
 // i = d mod 4, D = (d - i) q(g); the result is o_i + D when qm_i <= 2 q(g) and |D| <= mu_i, or
 // o_i itself when D = 0 (the run is then the computation).
 //
-// Hierarchy.  Level 1: chunks of kFsChunk elements, run from four starts around the guess
-// g = fl(double prefix of the terms), all chunks and chains in parallel.  Level 2..L: a node of
-// kFsArity children is walked from each of its four member starts: a child is applied by the
-// lemma (shift within its margin) or, failing that, evaluated exactly (a level-1 child rerun
-// from the arrival value, a higher child walked through its own children); the walk's output,
-// min(mu_child - |D_child|) and max(qm_child) form the node's record, valid by the same
-// argument.  The top walk starts at +0 (the first node's guess is 0: exact) and descends into any
-// node whose record cannot be applied.  Every value a walk produces is either a literal run of the
-// chain or a shift proven exact, so the result is the sequential sum bit for bit whatever the
-// guesses; the guesses only decide how often a walk has to descend.
+// Records and the walk.  Chunks of kFsChunk elements get a record each: the fan of four runs
+// from the guess g_k = fl(double prefix of the terms before chunk k), all chunks and chains in
+// parallel.  The chain's value is then carried across the chunks from +0: a chunk whose record
+// covers the arriving value is applied (one translation), any other chunk is rerun from that
+// value.  Every value produced is a literal run of the chain or a shift the lemma proves exact,
+// so the result is the sequential sum bit for bit whatever the guesses; the guesses only decide
+// how many chunks have to be rerun.  The device walks 64 records at a time, one per lane
+// (fsum.hip, k_fs_walk): lane l speculates that its chunk starts at the exact value plus the
+// prefix sum of the increments o_m - start_m of the lanes before it, applies its record to that
+// start, and checks the result against the next lane's speculated start.  The lanes before the
+// first failed check are proven exact by induction (each verified lane's output is the exact
+// start of the next); the first failed lane is applied or rerun alone from its start, which is
+// exact, and the speculation restarts after it.
 //
-// Used by fsum.hip (device) and tests/cpp/fsum_host.cpp (host emulation of the same walks, CPU
+// Used by fsum.hip (device) and tests/cpp/fsum_host.cpp (host emulation of the same walk, CPU
 // test against the literal loop).  Build with -ffp-contract=off: p_j = x * y and s + p are
 // separate roundings, as in PCL.
 #pragma once
@@ -45,10 +48,8 @@
 namespace dlg {
 
 constexpr int kFsChains = 9;    // accu[0..8] of computeMeanAndCovarianceMatrix
-constexpr int kFsChunk = 64;    // elements per level-1 node
-constexpr int kFsArity = 64;    // children per node at levels >= 2
-constexpr int kFsFan = 4;       // member starts per node
-constexpr int kFsMaxLevels = 8;
+constexpr int kFsChunk = 64;    // elements per record
+constexpr int kFsFan = 4;       // member starts per record
 
 DLG_HD inline uint32_t fs_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
 DLG_HD inline float fs_float(uint32_t u) { return __builtin_bit_cast(float, u); }
@@ -74,6 +75,15 @@ DLG_HD inline float fs_quantum(float g) {
   if (e == 0xFFu) return fs_float(0x7FC00000u);
   if (e <= 23u) return fs_float(1u << (e == 0u ? 0u : e - 1u));  // 2^(e-150), subnormal
   return fs_float((e - 23u) << 23);
+}
+
+// 1 / fs_quantum(g) as an exact double (the quantum is 2^(max(e, 1) - 150)); NaN when g is not
+// finite.  Multiplying by it is the exact division by the quantum.
+DLG_HD inline double fs_inv_quantum(float g) {
+  const uint32_t e = (fs_bits(g) >> 23) & 0xFFu;
+  if (e == 0xFFu) return __builtin_nan("");
+  const uint64_t be = 1023u + 150u - (e == 0u ? 1u : e);
+  return __builtin_bit_cast(double, be << 52);
 }
 
 // a node's record: guess g (member i starts at g + i q(g)) and per member the run's output, its
@@ -128,29 +138,35 @@ struct FsApply {
   float out, mu, qm;
 };
 
+// a[i] for a runtime i in 0..3 without indexing (keeps a record in registers on the device)
+DLG_HD inline float fs_sel4(const float (&a)[kFsFan], int i) {
+  return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+
 // apply node nd to the arrival t: true (and the exact result) when the lemma covers it
 DLG_HD inline bool fs_apply(float t, const FsNode& nd, FsApply* r) {
   const float q = fs_quantum(nd.g);
   const double qd = (double)q;
-  const double tq = (double)t / qd;  // exact (a power-of-two scaling within double's range)
+  const double iq = fs_inv_quantum(nd.g);
+  const double tq = (double)t * iq;  // exact (a power-of-two scaling within double's range)
   if (!(std::fabs(tq) < 4503599627370496.0) || tq != std::floor(tq)) return false;  // NaN too
-  const double dl = tq - (double)nd.g / qd;                                           // exact
+  const double dl = tq - (double)nd.g * iq;                                           // exact
   const double d4 = std::floor(dl * 0.25);
   const int i = (int)(dl - 4.0 * d4);
   const double D = (dl - (double)i) * qd;
-  const float qm = nd.qm[i];
+  const float qm = fs_sel4(nd.qm, i), oi = fs_sel4(nd.o, i), mui = fs_sel4(nd.mu, i);
   if (!(qm >= 0.0f)) return false;  // member unusable
   if (D == 0.0) {                   // t is member i's start: its run is the computation
-    r->out = nd.o[i];
-    r->mu = nd.mu[i];
+    r->out = oi;
+    r->mu = mui;
     r->qm = qm;
     return true;
   }
   const double aD = std::fabs(D);
-  if (!((double)qm <= 2.0 * qd) || !(aD <= (double)nd.mu[i])) return false;
-  r->out = (float)((double)nd.o[i] + D);  // exact
+  if (!((double)qm <= 2.0 * qd) || !(aD <= (double)mui)) return false;
+  r->out = (float)((double)oi + D);  // exact
   // the margin left for a further shift, rounded down
-  const double rem = (double)nd.mu[i] - aD;
+  const double rem = (double)mui - aD;
   float rf = (float)rem;
   if ((double)rf > rem) rf = std::nextafter(rf, -INFINITY);
   r->mu = rf;
@@ -158,67 +174,25 @@ DLG_HD inline bool fs_apply(float t, const FsNode& nd, FsApply* r) {
   return true;
 }
 
-DLG_HD inline void fs_acc(float* mu, float* qm, float m, float q) {
-  *mu = std::fmin(*mu, m);
-  *qm = std::fmax(*qm, q);
+// the speculative increment of a record for a start `off` above its guess: o_i - start_i of the
+// member i = (off / q) mod 4 that start would select (member 0 when off is not a multiple of
+// q(g), or when i is unusable; exact in double: two floats of nearby binades); NaN when no member
+// is usable.  The walk passes the offset between its exact value and the guess of the first
+// record it speculates on: the refined guesses lag the chain by the same amount until the next
+// chunk whose increment depends on its start.
+DLG_HD inline double fs_increment(const FsNode& nd, double off) {
+  const double qd = (double)fs_quantum(nd.g);
+  const double d = off * fs_inv_quantum(nd.g);
+  int i = 0;
+  if (std::fabs(d) < 4503599627370496.0 && d == std::floor(d)) i = (int)(d - 4.0 * std::floor(d * 0.25));
+  if (!(fs_sel4(nd.qm, i) >= 0.0f))
+    i = nd.qm[0] >= 0.0f ? 0 : nd.qm[1] >= 0.0f ? 1 : nd.qm[2] >= 0.0f ? 2 : 3;
+  if (!(fs_sel4(nd.qm, i) >= 0.0f)) return __builtin_nan("");
+  return (double)fs_sel4(nd.o, i) - ((double)nd.g + (double)i * qd);
 }
 
-// counters of a walk (diagnostics)
-struct FsWalkStats {
-  int64_t applied = 0, reruns = 0, descents = 0;
-};
-
-// Walk nodes [first, first + count) of `level` from the value v, descending into nodes the lemma
-// does not cover.  Store: node(level, k) -> FsNode, nodes(level) -> node count,
-// rerun(k, v) -> FsRun (level-1 node k evaluated from v).  *mu, *qm accumulate the walked path's
-// record.  Returns the exact sequential value after the last node.
-template <class Store>
-DLG_HD inline float fs_walk(Store& st, int level, int64_t first, int64_t count, float v,
-                            float* mu, float* qm, FsWalkStats* ws) {
-  int lv[kFsMaxLevels];
-  int64_t idx[kFsMaxLevels], end[kFsMaxLevels];
-  int sp = 0;
-  lv[0] = level;
-  idx[0] = first;
-  end[0] = first + count;
-  while (sp >= 0) {
-    if (idx[sp] == end[sp]) {
-      --sp;
-      continue;
-    }
-    const int L = lv[sp];
-    const int64_t k = idx[sp]++;
-    FsApply r;
-    if (fs_apply(v, st.node(L, k), &r)) {
-      v = r.out;
-      fs_acc(mu, qm, r.mu, r.qm);
-      if (ws) ws->applied++;
-      continue;
-    }
-    if (L == 1) {
-      const FsRun rr = st.rerun(k, v);
-      v = rr.o;
-      fs_acc(mu, qm, rr.mu, rr.qm);
-      if (ws) ws->reruns++;
-      continue;
-    }
-    if (ws) ws->descents++;
-    const int64_t c0 = k * kFsArity;
-    const int64_t c1 = c0 + kFsArity < st.nodes(L - 1) ? c0 + kFsArity : st.nodes(L - 1);
-    ++sp;
-    lv[sp] = L - 1;
-    idx[sp] = c0;
-    end[sp] = c1;
-  }
-  return v;
-}
-
-// number of nodes at each level for n elements: level 1 = chunks, level l+1 = ceil(level l / 64)
-DLG_HD inline int64_t fs_nodes(int64_t n, int level) {
-  int64_t m = (n + kFsChunk - 1) / kFsChunk;
-  for (int l = 1; l < level; ++l) m = (m + kFsArity - 1) / kFsArity;
-  return m;
-}
+// chunk records for n elements
+DLG_HD inline int64_t fs_chunks(int64_t n) { return (n + kFsChunk - 1) / kFsChunk; }
 
 // the refit's tail (refit_pcl_float after the sums): a = the nine sums, n = inlier count.
 // Float transcendentals of eigen33 are PCL's as restated in host_math.hpp (the double function

@@ -662,7 +662,14 @@ __global__ __launch_bounds__(kPickBS) void k_pick_p1(PickArgs a) { pick_body<kPi
 // select); tot01: the select's own totals[0..1] when the caller has just computed them (the
 // global words may not be visible yet), else null
 __device__ __forceinline__ void publish_body(const PubArgs& a, const int32_t* tot01, int t, int nthr) {
-  if (t == 0) a.pub[kPubErr] = a.err ? *a.err : 0;
+  // (the sticky look-back error word, read coherently at agent scope.  A predecessor tile whose
+  // aggregate the last tile already summed can still give up after this publish: that failure
+  // then surfaces at the next publish or at the extraction's end check, and the extraction throws
+  // -- a round is never consumed silently from a failed compaction.  The relaxed agent-scope
+  // atomics + s_waitcnt(0) handoffs here and in moments_tail / the fused pick rely on gfx9's
+  // in-order L2 write-back at agent scope.)
+  if (t == 0)
+    a.pub[kPubErr] = a.err ? __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   for (int i = t; i < a.ntot; i += nthr)
     a.pub[kPubTot + i] = tot01 && i < 2 ? tot01[i] : a.totals[i];
   for (int i = t; i < 4 * a.nsmall; i += nthr)

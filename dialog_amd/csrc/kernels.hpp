@@ -200,13 +200,15 @@ void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1St
 // eigen33.  Inliers px/py/pz with element stride `stride` floats, count *n_dev (<= n_cap).
 // res (16 int32): [0] = 1 when a transcendental of eigen33 could not be rounded for certain
 // (the host then recomputes the plane from the sums), [1] = n, [2..10] = the nine sums' bits.
+struct FsNode;
 struct FsBuffers {
-  double* csum = nullptr;  // [chunks][9]
+  double* csum = nullptr;  // [chunks][9] double sums of the terms
   double* usum = nullptr;  // [units][9]
-  double* upre = nullptr;  // [units][9]
-  void* nodes[8] = {};     // FsNode per level (1..), chain-major
-  int64_t cap[8] = {};     // nodes per chain per level
-  unsigned* ticket = nullptr;
+  double* upre = nullptr;  // [units][9] exclusive prefixes
+  FsNode* rec = nullptr;   // chunk records, chain-major: rec[c * cap + k]
+  int64_t cap = 0;         // chunks per chain
+  float* sums = nullptr;   // [9] the chains' end values
+  unsigned* ticket = nullptr;  // [2], zero on entry
 };
 // bytes of scratch for n_cap inliers; carve() lays the buffers out in `base`
 size_t fs_scratch_bytes(int64_t n_cap);

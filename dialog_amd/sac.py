@@ -138,6 +138,19 @@ class Context:
     def barrier(self):
         self.check(self._L.dlg_barrier(self.h))
 
+    def float_sums(self, xyz, cin=(0.0, 0.0, 1.0, 0.0), reps=1):
+        """dlg_float_sums: DLG_REFIT_PCL's device sums (fsum.hip) over xyz (n x 3 float32, list
+        order) and the float refit of cin -> (sums[9], coeff[4], uncertain, ms_per_call)."""
+        a = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+        ci = np.ascontiguousarray(cin, np.float32)
+        sums = np.zeros(9, np.float32)
+        co = np.zeros(4, np.float32)
+        unc, ms = C.c_int(), C.c_double()
+        self.check(self._L.dlg_float_sums(self.h, _f32p(a), C.c_int64(a.shape[0]), _f32p(ci),
+                                          int(reps), _f32p(sums), _f32p(co), C.byref(unc),
+                                          C.byref(ms)))
+        return sums, co, bool(unc.value), ms.value
+
     def allreduce_max(self, v: float) -> float:
         x = C.c_double(float(v))
         self.check(self._L.dlg_allreduce_max_f64(self.h, C.byref(x)))

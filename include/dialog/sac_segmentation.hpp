@@ -453,12 +453,13 @@ inline dlg_extract_stats extractPlanes(const pcl::PointCloud<PointT>& cloud, con
 // The plane stage's output for the reference's polyPlanes (PlaneDetect.h:1358-1440): one entry
 // of `plane_clouds` (PlaneDetect.h:100) per RANSAC plane, PlaneT being the reference's struct
 // Plane (HeaderFile.h:81-88: border, points_set, coeff, triangles_headfile).  As the reference's
-// segmentation leaves it (PlaneDetect.h:1094-1096): points_set = copies of the inlier points,
-// border = an empty cloud (polyPlanes builds it; it skips planes whose border is already set,
-// :1364), coeff.values = the 3 components of the plane normal pointing out of the object.  The
-// reference orients by one point's regulated normal (:1086-1093); here by the sign of the sum of
-// n . normal_i over the inliers with a finite normal (the majority vote of the same test).
-// Returns the number of planes appended.
+// segmentation leaves it (PlaneDetect.h:997-999, 1094-1096): points_set = copies of the inlier
+// points, border = null (polyPlanes builds the ConcaveHull border for every plane whose border is
+// still null and skips the others, :1364), coeff.values = the 3 components of the plane normal
+// pointing out of the object.  Orientation as the reference's (:1048-1050, 1086-1093): the
+// regulated normal of the source point nearest plane->points[0] -- the first inlier itself --
+// flips the normal when p_n . n < 0 (float dot in Eigen's Vector3f order; a NaN normal never
+// flips).  Returns the number of planes appended.
 template <typename PlaneT, typename Alloc, typename PointT, typename PointNT>
 inline size_t fillPlaneClouds(const pcl::PointCloud<PointT>& cloud,
                               const pcl::PointCloud<PointNT>& normals,
@@ -471,17 +472,11 @@ inline size_t fillPlaneClouds(const pcl::PointCloud<PointT>& cloud,
     if (pr.indices.empty()) continue;
     PlaneT pl;
     pl.points_set.reset(new pcl::PointCloud<PointT>);
-    pl.border.reset(new pcl::PointCloud<PointT>);
     pl.points_set->points.reserve(pr.indices.size());
-    double s = 0.0;
-    for (int i : pr.indices) {
-      pl.points_set->push_back(cloud.points[(size_t)i]);
-      const PointNT& nr = normals.points[(size_t)i];
-      const double d = (double)pr.coeff[0] * nr.normal_x + (double)pr.coeff[1] * nr.normal_y +
-                       (double)pr.coeff[2] * nr.normal_z;
-      if (d == d) s += d;  // (NaN normals: no vote)
-    }
-    const float sg = s < 0.0 ? -1.0f : 1.0f;
+    for (int i : pr.indices) pl.points_set->push_back(cloud.points[(size_t)i]);
+    const PointNT& nr = normals.points[(size_t)pr.indices[0]];
+    const float dot = (nr.normal_x * pr.coeff[0] + nr.normal_y * pr.coeff[1]) + nr.normal_z * pr.coeff[2];
+    const float sg = dot < 0.0f ? -1.0f : 1.0f;
     pl.coeff.values.assign({sg * pr.coeff[0], sg * pr.coeff[1], sg * pr.coeff[2]});
     plane_clouds.push_back(std::move(pl));
     ++added;

@@ -4,7 +4,9 @@
 // the GPU by tests/test_gpu_parity.py: a closed box (six faces) -> estimateNormal (viewpoint at
 // the box centre, then reversed: every normal outward, what regulateNormal() establishes) ->
 // segmentPlanesRansac() -> the contract polyPlanes relies on (PlaneDetect.h:1364-1373): every
-// plane has points, an empty border, and coeff.values = 3 components pointing out of the box.
+// plane has points, a null border (polyPlanes builds borders only where it is null), and
+// coeff.values = 3 components pointing out of the box.  Orientation follows the reference's rule
+// (PlaneDetect.h:1086-1093): the first inlier's normal decides, even against all the others.
 #include <cmath>
 #include <cstdio>
 #include <memory>
@@ -29,6 +31,7 @@ struct Plane {  // HeaderFile.h:81-88
 PointCloudT::Ptr source_cloud(new PointCloudT);
 pcl::PointCloud<pcl::Normal>::Ptr source_normal(new pcl::PointCloud<pcl::Normal>);
 std::vector<Plane> plane_clouds;
+std::vector<dialog::PlaneResult> found;
 float T_dist_point_plane = 0.02f;   // config.txt:29 (scaled to this cloud)
 int T_num_of_single_plane = 500;    // config.txt:20
 float r_for_estimate_normal = 0.1f; // config.txt:4
@@ -46,7 +49,6 @@ void segmentPlanesRansac() {  // fills plane_clouds
   ep.threshold = T_dist_point_plane;
   ep.min_inliers = T_num_of_single_plane;
   ep.max_iterations = 1000;
-  std::vector<dialog::PlaneResult> found;
   dialog::extractPlanes(*source_cloud, ep, found);
   dialog::fillPlaneClouds(*source_cloud, *source_normal, found, plane_clouds);
 }
@@ -67,18 +69,30 @@ int main() {
     n.normal_x = -n.normal_x; n.normal_y = -n.normal_y; n.normal_z = -n.normal_z;
   }
   segmentPlanesRansac();
-  int bad = 0;
-  for (const Plane& pl : plane_clouds) {
-    if (!pl.points_set || pl.points_set->points.empty() || !pl.border || !pl.border->points.empty() ||
-        pl.coeff.values.size() != 3)
-      ++bad;
+  auto outward = [&](const Plane& pl) {  // the face centroid lies ~h along the outward normal
     double m[3] = {0, 0, 0};
     for (const auto& p : pl.points_set->points) { m[0] += p.x; m[1] += p.y; m[2] += p.z; }
     const double k = (double)pl.points_set->points.size();
-    const double out = pl.coeff.values[0] * (m[0] / k - cx) + pl.coeff.values[1] * (m[1] / k - cy) +
-                       pl.coeff.values[2] * (m[2] / k - cz);
-    if (!(out > 0.5)) ++bad;  // the face centroid lies ~h along the outward normal
+    return pl.coeff.values[0] * (m[0] / k - cx) + pl.coeff.values[1] * (m[1] / k - cy) +
+           pl.coeff.values[2] * (m[2] / k - cz);
+  };
+  int bad = 0;
+  for (const Plane& pl : plane_clouds) {
+    if (!pl.points_set || pl.points_set->points.empty() || pl.border || pl.coeff.values.size() != 3)
+      ++bad;
+    if (!(outward(pl) > 0.5)) ++bad;
   }
+  // the first inlier's normal alone reversed: the reference's rule follows it (a majority vote
+  // over the inliers would not)
+  pcl::PointCloud<pcl::Normal> flipped = *source_normal;
+  for (const auto& pr : found) {
+    pcl::Normal& n = flipped.points[(size_t)pr.indices[0]];
+    n.normal_x = -n.normal_x; n.normal_y = -n.normal_y; n.normal_z = -n.normal_z;
+  }
+  std::vector<Plane> inward;
+  dialog::fillPlaneClouds(*source_cloud, flipped, found, inward);
+  for (const Plane& pl : inward)
+    if (!(outward(pl) < -0.5)) ++bad;
   std::printf("planes %zu bad %d\n", plane_clouds.size(), bad);
-  return bad == 0 && plane_clouds.size() == 6 ? 0 : 1;
+  return bad == 0 && plane_clouds.size() == 6 && inward.size() == 6 ? 0 : 1;
 }

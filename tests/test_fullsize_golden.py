@@ -125,6 +125,44 @@ def test_c3_fast_two_pass_and_sharded(gpu_ctx):
     assert not errs, errs
     for r in range(2):
         check_extract(out[r], g)
+        assert out[r]["stats"]["lean_rounds"] > 0  # (both shards hold a Morton copy)
+
+
+def run_sharded(p, bounds, mode):
+    """extract_planes over in-process loopback ranks, rank r holding p[bounds[r]:bounds[r+1]]."""
+    W = len(bounds) - 1
+    ctxs = D.Context.loopback_group(W, 0)
+    out, errs = [None] * W, []
+
+    def run(r):
+        try:
+            lo, hi = bounds[r], bounds[r + 1]
+            c = D.Cloud(ctxs[r], p[lo:hi], id_base=lo)
+            out[r] = D.extract_planes(c, params(mode), max_planes=20, min_inliers=500,
+                                      capacity=p.shape[0])
+            c.close()
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    return out
+
+
+@pytest.mark.skipif("c3" not in DB, reason="fullsize.json has no c3")
+def test_c3_fast_uneven_shards_agree_on_lean(gpu_ctx):
+    """One shard below the Morton-copy size (131072 points), one above: the ranks agree once per
+    extraction that lean rounds need every rank's spatial copy, so both take the list path, and
+    the planes still equal the one-rank oracle's bit for bit."""
+    p = cloud("c3")
+    out = run_sharded(p, [0, 100_000, p.shape[0]], "fast")
+    for r in range(2):
+        check_extract(out[r], DB["c3"]["modes"]["fast"])
+        assert out[r]["stats"]["lean_rounds"] == 0
 
 
 @pytest.mark.skipif("c4shape" not in DB, reason="fullsize.json has no c4shape")
