@@ -140,7 +140,7 @@ def load():
     L.dlg_score_benchmark.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                       C.POINTER(C.c_double), i32p]
     L.dlg_float_sums.argtypes = [vp, fp, C.c_int64, fp, C.c_int, fp, fp, C.POINTER(C.c_int),
-                                 C.POINTER(C.c_double)]
+                                 C.POINTER(C.c_double), i64p]
     L.dlg_ctx_set_option.argtypes = [vp, C.c_int, C.c_int64]
     L.dlg_ctx_get_option.argtypes = [vp, C.c_int, i64p]
     L.dlg_prune_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int]

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <deque>
 #include <stdexcept>
 
 namespace dlg {
@@ -33,6 +34,13 @@ class SingleComm final : public Comm {
       hip_check(hipMemcpyAsync(recv, send, count * dtype_size(t), hipMemcpyDeviceToDevice, s),
                 "allgather copy");
   }
+  void send(const void*, size_t, DType, int, hipStream_t) override {
+    throw std::runtime_error("send on a single-rank communicator");
+  }
+  void recv(void*, size_t, DType, int, hipStream_t) override {
+    throw std::runtime_error("recv on a single-rank communicator");
+  }
+  void broadcast(void*, size_t, DType, int, hipStream_t) override {}
 };
 
 std::unique_ptr<Comm> make_single_comm() { return std::make_unique<SingleComm>(); }
@@ -48,6 +56,10 @@ struct RcclApi {
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                             hipStream_t) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
                             hipStream_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
   bool load(std::string* err) {
@@ -72,6 +84,9 @@ struct RcclApi {
     DLG_SYM(CommDestroy, "ncclCommDestroy");
     DLG_SYM(AllReduce, "ncclAllReduce");
     DLG_SYM(AllGather, "ncclAllGather");
+    DLG_SYM(Send, "ncclSend");
+    DLG_SYM(Recv, "ncclRecv");
+    DLG_SYM(Broadcast, "ncclBroadcast");
     DLG_SYM(GetErrorString, "ncclGetErrorString");
 #undef DLG_SYM
     return true;
@@ -126,6 +141,18 @@ class RcclComm final : public Comm {
     if (!count) return;
     check(rccl().AllGather(send, recv, count, nccl_type(t), comm_, s), "ncclAllGather");
   }
+  void send(const void* dev, size_t count, DType t, int peer, hipStream_t s) override {
+    if (!count) return;
+    check(rccl().Send(dev, count, nccl_type(t), peer, comm_, s), "ncclSend");
+  }
+  void recv(void* dev, size_t count, DType t, int peer, hipStream_t s) override {
+    if (!count) return;
+    check(rccl().Recv(dev, count, nccl_type(t), peer, comm_, s), "ncclRecv");
+  }
+  void broadcast(void* dev, size_t count, DType t, int root, hipStream_t s) override {
+    if (!count) return;
+    check(rccl().Broadcast(dev, dev, count, nccl_type(t), root, comm_, s), "ncclBroadcast");
+  }
 
  private:
   static void check(ncclResult_t r, const char* what) {
@@ -149,13 +176,15 @@ std::unique_ptr<Comm> make_rccl_comm(int rank, int world, const void* uid128, st
 
 // ---------------------------------------------------------------------------------------------
 struct LoopbackGroup {
-  explicit LoopbackGroup(int w) : world(w), slots(w) {}
+  explicit LoopbackGroup(int w) : world(w), slots(w), mail((size_t)w * w) {}
   int world;
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
   std::vector<std::vector<uint8_t>> slots;
+  std::vector<std::deque<std::vector<uint8_t>>> mail;  // [src * world + dst]: messages in order
+  std::condition_variable mail_cv;
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     const uint64_t g = gen;
@@ -212,6 +241,35 @@ class LoopbackComm final : public Comm {
       if (bytes) std::memcpy(out.data() + r * bytes, g_->slots[r].data(), bytes);
     g_->barrier();
     upload(recv, out.data(), out.size(), s);
+  }
+  void send(const void* dev, size_t count, DType t, int peer, hipStream_t s) override {
+    std::vector<uint8_t> m(count * dtype_size(t));
+    if (!m.empty()) {
+      hip_check(hipMemcpyAsync(m.data(), dev, m.size(), hipMemcpyDeviceToHost, s), "loopback d2h");
+      hip_check(hipStreamSynchronize(s), "loopback sync");
+    }
+    std::lock_guard<std::mutex> lk(g_->mu);
+    g_->mail[(size_t)rank_ * world_ + peer].push_back(std::move(m));
+    g_->mail_cv.notify_all();
+  }
+  void recv(void* dev, size_t count, DType t, int peer, hipStream_t s) override {
+    std::vector<uint8_t> m;
+    {
+      std::unique_lock<std::mutex> lk(g_->mu);
+      auto& q = g_->mail[(size_t)peer * world_ + rank_];
+      g_->mail_cv.wait(lk, [&] { return !q.empty(); });
+      m = std::move(q.front());
+      q.pop_front();
+    }
+    if (m.size() != count * dtype_size(t)) throw std::runtime_error("loopback recv: size mismatch");
+    upload(dev, m.data(), m.size(), s);
+  }
+  void broadcast(void* dev, size_t count, DType t, int root, hipStream_t s) override {
+    const size_t bytes = count * dtype_size(t);
+    exchange(dev, rank_ == root ? bytes : 0, s);
+    std::vector<uint8_t> out(g_->slots[root]);
+    g_->barrier();
+    if (rank_ != root) upload(dev, out.data(), bytes, s);
   }
 
  private:

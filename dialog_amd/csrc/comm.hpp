@@ -6,6 +6,9 @@
 //   * allreduce(sum) of the refit moments            (double[10], fast mode)
 //   * allgather of per-rank totals                    (int64 per rank)
 //   * padded allgather of inlier ids / xyz            (only when inliers are gathered)
+//   * PCL float refit (DLG_REFIT_PCL): allgather of each rank's double term sums (10 doubles),
+//     then the nine float chains handed from rank to rank in list order (send/recv of 9 floats)
+//     and the last rank's sums broadcast
 // All operate in place on device buffers on the caller's stream.  RcclComm runs them over RCCL
 // (xGMI within a node); LoopbackComm runs an in-process group of ranks that share one device
 // (one host thread per rank) for single-GPU rehearsal and tests of the sharded path.
@@ -36,6 +39,11 @@ class Comm {
   virtual void allreduce_max_f64(double* dev, size_t count, hipStream_t s) = 0;
   // recv[r * count + i] = send_of_rank_r[i]   (device buffers; send may alias recv + rank*count)
   virtual void allgather(const void* send, void* recv, size_t count, DType t, hipStream_t s) = 0;
+  // point to point (stream-ordered; every send has its matching recv on the peer) and broadcast
+  // of root's buffer to every rank (in place)
+  virtual void send(const void* dev, size_t count, DType t, int peer, hipStream_t s) = 0;
+  virtual void recv(void* dev, size_t count, DType t, int peer, hipStream_t s) = 0;
+  virtual void broadcast(void* dev, size_t count, DType t, int root, hipStream_t s) = 0;
 
  protected:
   int rank_ = 0;

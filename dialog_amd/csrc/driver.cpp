@@ -390,10 +390,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // lean-list round: plane model over the Morton copy, single rank, device refit, a list that
   // is pristine or already lean (a list compacted with coordinates stays on the full path)
   const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
-  // PCL's float sums on the device (fsum.hip, one rank: the sums run over the list in global
-  // order); lean rounds take the unrefined inliers in list order from a bitmap over pristine
-  // indices instead of list coordinates
-  const bool pcl_dev = pcl_refit && c->opt.pcl_dev != 0 && c->comm->world() == 1;
+  // PCL's float sums on the device (fsum.hip; several ranks: each walks its segment of the list
+  // from the previous rank's end values); lean rounds take the unrefined inliers in list order
+  // from a bitmap over pristine indices instead of list coordinates
+  const bool pcl_dev = pcl_refit && c->opt.pcl_dev != 0;
   // (any rank count: the fast refit's moments are exact integers, so summing them over the
   // Morton copies of the shards gives the list's bits.  Every rank decides alike: whether all
   // ranks hold a spatial copy is agreed once per extraction (c->sp_all), and the other inputs
@@ -679,8 +679,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       // refined plane stays on the device (no host round trip)
       if (c->fs_cap < src.n) {
         const int64_t cap = std::max<int64_t>(src.n, 1);
-        c->fs_scr.ensure(fs_scratch_bytes(cap));
-        c->fs_b = fs_carve(c->fs_scr.p, cap);
+        c->fs_scr.ensure(fs_scratch_bytes(cap, c->comm->world()));
+        c->fs_b = fs_carve(c->fs_scr.p, cap, c->comm->world());
         HIPCHK(hipMemsetAsync(c->fs_b.ticket, 0, 2 * sizeof(unsigned), c->stream));
         c->fs_cap = cap;
       }
@@ -704,14 +704,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         launch_ucompact(cl->ubits.p, nw, cl->pristine.view(cl->n_total), c->sel1, c->fs_x.p,
                         c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
-                        rc_dev, fs_res, c->num_cus, c->stream);
+                        rc_dev, fs_res, c->num_cus, c->stream, c->comm.get());
       } else {
         c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
         stage_wait();
         launch_select(src, bc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
                       c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
         launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
-                        c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream);
+                        c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get());
       }
       HIPCHK(hipGetLastError());
     } else {
@@ -1535,7 +1535,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
 
 dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float cin[4], int reps,
                           float sums_out[9], float coeff_out[4], int* uncertain,
-                          double* ms_per_call) {
+                          double* ms_per_call, int64_t* walk_stats) {
   if (!c || n < 0 || n > INT32_MAX || (n > 0 && !xyz) || !cin || reps < 1 || !sums_out ||
       !coeff_out || !uncertain || !ms_per_call)
     return DLG_ERR_INVALID;
@@ -1548,8 +1548,14 @@ dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float c
     dc.ensure(2);
     dn.ensure(1);
     dres.ensure(16);
-    scr.ensure(fs_scratch_bytes(std::max<int64_t>(n, 1)));
-    const FsBuffers b = fs_carve(scr.p, std::max<int64_t>(n, 1));
+    scr.ensure(fs_scratch_bytes(std::max<int64_t>(n, 1), 1));
+    FsBuffers b = fs_carve(scr.p, std::max<int64_t>(n, 1), 1);
+    DevBuf<int64_t> wst;
+    if (walk_stats) {
+      wst.ensure(72);
+      HIPCHK(hipMemsetAsync(wst.p, 0, 72 * 8, c->stream));
+      b.wst = wst.p;
+    }
     HIPCHK(hipMemsetAsync(b.ticket, 0, 2 * sizeof(unsigned), c->stream));
     if (n) HIPCHK(hipMemcpyAsync(dx.p, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream));
     const int32_t n32 = (int32_t)n;
@@ -1574,6 +1580,7 @@ dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float c
     coeff_out[0] = co.x; coeff_out[1] = co.y; coeff_out[2] = co.z; coeff_out[3] = co.w;
     *uncertain = h[0];
     *ms_per_call = total / reps;
+    if (walk_stats) HIPCHK(hipMemcpy(walk_stats, wst.p, 72 * 8, hipMemcpyDeviceToHost));
   });
 }
 

@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "dev_common.hpp"
 #include "fsum.hpp"
+#include "comm.hpp"
 
 #include <cstdint>
 
@@ -56,8 +57,11 @@ __device__ __forceinline__ void fs_acc9(double (&a)[kFsChains], float x, float y
 
 // the last workgroup of a unit pass scans the per-unit sums usum into the exclusive prefixes
 // upre (from base9, or 0); ticket = the pass's ticket word
+__device__ void fs_scan_body(const FsDev& d, int64_t U, const double* base9, double* blk,
+                             double* tot_out);
+
 __device__ void fs_scan_units(const FsDev& d, int64_t U, const double* base9, unsigned* ticket,
-                              double* blk) {
+                              double* blk, double* tot_out = nullptr) {
   const int t = threadIdx.x;
   __builtin_amdgcn_s_waitcnt(0);
   __shared__ unsigned s_ticket;
@@ -67,6 +71,14 @@ __device__ void fs_scan_units(const FsDev& d, int64_t U, const double* base9, un
   __syncthreads();
   if (s_ticket != gridDim.x - 1) return;
   if (t == 0) *ticket = 0u;
+  fs_scan_body(d, U, base9, blk, tot_out);
+}
+
+// upre = exclusive prefixes of usum from base9 (or 0); tot_out non-null: only the totals (and
+// the count n in tot_out[9]) are written
+__device__ void fs_scan_body(const FsDev& d, int64_t U, const double* base9, double* blk,
+                             double* tot_out) {
+  const int t = threadIdx.x;
   double run = t < kFsChains && base9 ? base9[t] : 0.0;
   for (int64_t ub = 0; ub < U; ub += kFsUC) {
     const int nb = (int)(U - ub < kFsUC ? U - ub : kFsUC);
@@ -78,16 +90,63 @@ __device__ void fs_scan_units(const FsDev& d, int64_t U, const double* base9, un
     __syncthreads();
     if (t < kFsChains) {
       for (int q = 0; q < nb; ++q) {
-        d.b.upre[(ub + q) * kFsChains + t] = run;
+        if (!tot_out) d.b.upre[(ub + q) * kFsChains + t] = run;
         run += blk[q * kFsChains + t];
       }
     }
   }
+  if (tot_out) {
+    if (t < kFsChains) tot_out[t] = run;
+    if (t == 0) tot_out[kFsChains] = (double)*d.n_dev;
+  }
+}
+
+// several ranks: this rank's base = the double totals of the ranks before it (list order), the
+// global inlier count; then the unit scan from that base.  One workgroup.
+__global__ __launch_bounds__(256) void k_fs_base(FsDev d, const double* __restrict__ gath, int rank,
+                                                 int world, double* __restrict__ base9,
+                                                 int64_t* __restrict__ n_global) {
+  __shared__ double blk[64 * kFsChains];
+  __shared__ double sb[kFsChains];
+  const int t = threadIdx.x;
+  if (t < kFsChains) {
+    double b = 0.0;
+    for (int r = 0; r < rank; ++r) b += gath[r * (kFsChains + 1) + t];
+    sb[t] = b;
+    base9[t] = b;
+  }
+  if (t == kFsChains) {
+    int64_t ng = 0;
+    for (int r = 0; r < world; ++r) ng += (int64_t)gath[r * (kFsChains + 1) + kFsChains];
+    *n_global = ng;
+  }
+  __syncthreads();
+  const int64_t n = *d.n_dev;
+  fs_scan_body(d, (n + kFsUnit - 1) / kFsUnit, sb, blk, nullptr);
+}
+
+// several ranks: the refit tail on the broadcast global sums (identical on every rank)
+__global__ void k_fs_tail(const float* __restrict__ sums9, const int64_t* __restrict__ n_global,
+                          const float4* __restrict__ cin, float4* __restrict__ cout,
+                          int32_t* __restrict__ res) {
+  float a9[kFsChains];
+  for (int k = 0; k < kFsChains; ++k) a9[k] = sums9[k];
+  const int64_t n = *n_global;
+  const float4 ci = *cin;
+  const float cv[4] = {ci.x, ci.y, ci.z, ci.w};
+  float co[4];
+  bool unc = false;
+  fs_refit_tail(a9, n, cv, co, &unc);
+  *cout = make_float4(co[0], co[1], co[2], co[3]);
+  res[0] = unc ? 1 : 0;
+  res[1] = (int32_t)n;
+  for (int k = 0; k < kFsChains; ++k) res[2 + k] = __float_as_int(a9[k]);
 }
 
 // ---- k_fs_prep --------------------------------------------------------------------------------
 constexpr int kFpBS = 256;
-__global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d, const double* __restrict__ base9) {
+__global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d, const double* __restrict__ base9,
+                                                   double* __restrict__ tot_out) {
   __shared__ float sx[kFsUC * kFsPad], sy[kFsUC * kFsPad], sz[kFsUC * kFsPad];
   __shared__ double scs[kFsUC * kFsChains];
   const int64_t n = *d.n_dev;
@@ -126,8 +185,9 @@ __global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d, const double* __rest
     }
   }
   // the last workgroup scans the unit sums (agent-scope stores acknowledged before the ticket,
-  // read back with agent-scope loads: k_moments' pattern)
-  fs_scan_units(d, U, base9, d.b.ticket, scs);
+  // read back with agent-scope loads: k_moments' pattern); with tot_out (several ranks) it only
+  // totals them -- the scan waits for the other ranks' totals (k_fs_base)
+  fs_scan_units(d, U, base9, d.b.ticket, scs, tot_out);
 }
 
 // ---- k_fs_inc ---------------------------------------------------------------------------------
@@ -345,12 +405,236 @@ __device__ __forceinline__ float fs_rerun(const FsDev& d, int c, int64_t k, int6
   return v;
 }
 
+// a record unpacked for the walk, with its per-record constants (q = quantum of g, iq = 1/q, gq =
+// g / q, d0 = member 0's increment, P = the in-unit prefix of the member-0 increments, mu3 = the
+// fast path's margin)
+struct FsWalkRec {
+  float g, mu3;
+  float o0, o1, o2, o3, m0, m1, m2, m3, q0, q1, q2, q3;
+  double d0, P;
+  // (derived on use: fewer live registers)
+  __device__ double q() const { return (double)fs_quantum(g); }
+  __device__ double iq() const { return fs_inv_quantum(g); }
+  __device__ double gd() const { return (double)g; }
+};
+
+__device__ __forceinline__ FsWalkRec fs_walk_rec(const f32x4& r0, const f32x4& r1, const f32x4& r2,
+                                                 const f32x4& r3) {
+  FsWalkRec w;
+  w.g = r0.x;
+  w.mu3 = r0.w;
+  w.o0 = r1.x; w.o1 = r1.y; w.o2 = r1.z; w.o3 = r1.w;
+  w.m0 = r2.x; w.m1 = r2.y; w.m2 = r2.z; w.m3 = r2.w;
+  w.q0 = r3.x; w.q1 = r3.y; w.q2 = r3.z; w.q3 = r3.w;
+  w.d0 = w.q0 >= 0.0f ? (double)w.o0 - (double)w.g : 0.0;
+  w.P = __longlong_as_double((int64_t)(((uint64_t)__float_as_uint(r0.z) << 32) |
+                                       __float_as_uint(r0.y)));
+  return w;
+}
+
+// fs_increment (fsum.hpp) on the unpacked record (scalar selects: no indexed record array)
+__device__ __forceinline__ double fs_increment_rec(const FsWalkRec w, double off) {
+  const double qd = w.q();
+  const double dd = off * w.iq();
+  int i = 0;
+  if (fabs(dd) < 4503599627370496.0 && dd == floor(dd)) i = (int)(dd - 4.0 * floor(dd * 0.25));
+  const bool u0 = w.q0 >= 0.0f, u1 = w.q1 >= 0.0f, u2 = w.q2 >= 0.0f, u3 = w.q3 >= 0.0f;
+  const bool ui = i == 0 ? u0 : i == 1 ? u1 : i == 2 ? u2 : u3;
+  if (!ui) i = u0 ? 0 : u1 ? 1 : u2 ? 2 : 3;
+  const bool uf = i == 0 ? u0 : i == 1 ? u1 : i == 2 ? u2 : u3;
+  if (!uf) return __builtin_nan("");
+  const float oi = i == 0 ? w.o0 : i == 1 ? w.o1 : i == 2 ? w.o2 : w.o3;
+  return (double)oi - ((double)w.g + (double)i * qd);
+}
+
+// fs_apply (fsum.hpp) for the walk, branch-free on the unpacked record: the same decisions and the
+// same result bits
+__device__ __forceinline__ bool fs_apply_lean(float t, const FsWalkRec w, float* out) {
+  const double q = w.q(), iq = w.iq();
+  const double tq = (double)t * iq;
+  const bool grid = fabs(tq) < 4503599627370496.0 && tq == floor(tq);
+  const double dl = tq - (double)w.g * iq;
+  const double d4 = floor(dl * 0.25);
+  const double fi = dl - 4.0 * d4;  // 0..3 on the grid
+  const int i = grid ? (int)fi : 0;
+  const double D = (dl - (double)i) * q;
+  const bool b1 = i & 1, b2 = i & 2;
+  const float qm = b2 ? (b1 ? w.q3 : w.q2) : (b1 ? w.q1 : w.q0);
+  const float oi = b2 ? (b1 ? w.o3 : w.o2) : (b1 ? w.o1 : w.o0);
+  const float mui = b2 ? (b1 ? w.m3 : w.m2) : (b1 ? w.m1 : w.m0);
+  const bool ok = grid && qm >= 0.0f &&
+                  (D == 0.0 || ((double)qm <= 2.0 * q && fabs(D) <= (double)mui));
+  *out = D == 0.0 ? oi : (float)((double)oi + D);
+  return ok;
+}
+
+// The lemma on integers, for stepping chunk by chunk (sums hovering near zero: many records
+// whose increment depends on the start's low bits, one after another).  The window's records
+// and the carried value are taken as int64 multiples of qmin = 2^(elo - 150), the smallest
+// quantum among the window's guesses and member outputs (exact when every value lies within 37
+// binades of it); a step is then a few scalar integer operations on the stepped lane's fields:
+// the same decisions as fs_apply (grid, member, margin, quantum) and the exact result.
+struct FsIntWin {
+  bool ok;  // (wave-uniform) the window is representable
+  int elo;  // (wave-uniform)
+  int64_t G, O0, O1, O2, O3;  // per lane: g and the member outputs / qmin
+  int32_t M0, M1, M2, M3;     // floor(mu_i / qmin) clamped to 2^31 - 1; -1 for a negative margin
+  int32_t meta;               // sh = log2(q(g) / qmin) | usable_i << 8 + i | qm_i <= 2 q << 12 + i
+};
+
+__device__ __forceinline__ int fs_exp1(float v) {  // max(biased exponent, 1)
+  const int e = (int)((__float_as_uint(v) >> 23) & 0xFFu);
+  return e == 0 ? 1 : e;
+}
+
+__device__ __forceinline__ int64_t fs_to_int(float v, int elo) {
+  const uint32_t b = __float_as_uint(v);
+  const uint32_t e = (b >> 23) & 0xFFu;
+  const int64_t m = (int64_t)((b & 0x7FFFFFu) | (e ? 0x800000u : 0u));
+  const int64_t x = m << ((e ? (int)e : 1) - elo);
+  return (b >> 31) ? -x : x;
+}
+
+__device__ __forceinline__ float fs_from_int(int64_t x, int elo) {
+  return (float)ldexp((double)x, elo - 150);  // (exact: x holds a float's value)
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+__device__ __forceinline__ int32_t fs_mu_int(float mu, int elo) {
+  const double mq = ldexp((double)mu, 150 - elo);
+  return !(mq >= 0.0) ? -1 : mq >= 2147483647.0 ? 2147483647 : (int32_t)floor(mq);
+}
+
+__device__ __forceinline__ FsIntWin fs_int_win(const FsWalkRec w, bool lane_in) {
+  FsIntWin iw;
+  const bool u0 = w.q0 >= 0.0f, u1 = w.q1 >= 0.0f, u2 = w.q2 >= 0.0f, u3 = w.q3 >= 0.0f;
+  int lo = 255, hi = 0;
+  bool fin = true;
+  if (lane_in) {
+    lo = fs_exp1(w.g);
+    hi = lo;
+    fin = lo < 255;
+    auto acc = [&](bool u, float o) {
+      if (!u) return;
+      const int e = fs_exp1(o);
+      lo = min(lo, e);
+      hi = max(hi, e);
+      fin = fin && e < 255;
+    };
+    acc(u0, w.o0);
+    acc(u1, w.o1);
+    acc(u2, w.o2);
+    acc(u3, w.o3);
+  }
+  iw.elo = wave_min_i(lo);
+  const int ehi = wave_max_i(hi);
+  iw.ok = ballot(!fin) == 0 && ehi - iw.elo <= 37;
+  iw.G = fs_to_int(w.g, iw.elo);
+  iw.O0 = u0 ? fs_to_int(w.o0, iw.elo) : 0;
+  iw.O1 = u1 ? fs_to_int(w.o1, iw.elo) : 0;
+  iw.O2 = u2 ? fs_to_int(w.o2, iw.elo) : 0;
+  iw.O3 = u3 ? fs_to_int(w.o3, iw.elo) : 0;
+  iw.M0 = fs_mu_int(w.m0, iw.elo);
+  iw.M1 = fs_mu_int(w.m1, iw.elo);
+  iw.M2 = fs_mu_int(w.m2, iw.elo);
+  iw.M3 = fs_mu_int(w.m3, iw.elo);
+  const float q2 = 2.0f * fs_quantum(w.g);
+  const int sh = fs_exp1(w.g) - iw.elo;
+  iw.meta = (sh & 0xFF) | (u0 << 8) | (u1 << 9) | (u2 << 10) | (u3 << 11) |
+            ((w.q0 <= q2) << 12) | ((w.q1 <= q2) << 13) | ((w.q2 <= q2) << 14) |
+            ((w.q3 <= q2) << 15);
+  return iw;
+}
+
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
+  const uint64_t u = (uint64_t)v;
+  return (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l)
+                    << 32));
+}
+
+// one step of lane f's record on the integer value T (wave-uniform): true and T advanced, or false
+__device__ __forceinline__ bool fs_int_step(const FsIntWin& iw, int f, int64_t* T) {
+  const int meta = __builtin_amdgcn_readlane(iw.meta, f);
+  const int sh = meta & 0xFF;
+  const int64_t t = *T;
+  if ((t & (((int64_t)1 << sh) - 1)) != 0) return false;  // off the record's quantum grid
+  const int64_t D = t - rl64(iw.G, f);
+  const int i = (int)((D >> sh) & 3);
+  const int64_t Dm = D - ((int64_t)i << sh);
+  if (!((meta >> (8 + i)) & 1)) return false;  // member unusable
+  const int64_t Oi = i == 0 ? rl64(iw.O0, f) : i == 1 ? rl64(iw.O1, f) : i == 2 ? rl64(iw.O2, f)
+                                                                           : rl64(iw.O3, f);
+  if (Dm != 0) {
+    if (!((meta >> (12 + i)) & 1)) return false;  // the run's quantum outgrows 2 q(g)
+    const int32_t Mi = i == 0 ? __builtin_amdgcn_readlane(iw.M0, f)
+                     : i == 1 ? __builtin_amdgcn_readlane(iw.M1, f)
+                     : i == 2 ? __builtin_amdgcn_readlane(iw.M2, f)
+                              : __builtin_amdgcn_readlane(iw.M3, f);
+    if (!((Dm < 0 ? -Dm : Dm) <= (int64_t)Mi)) return false;  // outside the margin
+  }
+  *T = Oi + Dm;
+  return true;
+}
+
+// steps lanes f0 .. (until `stop` says so) from the exact value t; returns the next lane
+template <class Stop>
+__device__ __forceinline__ int fs_step_lanes(const FsDev& d, int c, int64_t base, int64_t n,
+                                             const FsWalkRec wr, int cnt, int f, float* t,
+                                             int lane, Stop stop, int64_t* n_step,
+                                             int64_t* n_rerun) {
+  const FsIntWin iw = fs_int_win(wr, lane < cnt);
+  for (;;) {
+    const int et = fs_exp1(*t);
+    const bool trep = iw.ok && (*t == 0.0f || (et >= iw.elo && et - iw.elo <= 38 &&
+                                              fs_from_int(fs_to_int(*t, iw.elo), iw.elo) == *t));
+    int64_t T = trep ? (*t == 0.0f ? 0 : fs_to_int(*t, iw.elo)) : 0;
+    // integer stepping while it lasts
+    bool ok = trep;
+    while (ok) {
+      ++*n_step;
+      ok = fs_int_step(iw, f, &T);
+      if (!ok) break;
+      ++f;
+      if (f >= cnt || stop(f)) {
+        *t = fs_from_int(T, iw.elo);
+        return f;
+      }
+    }
+    if (trep) *t = fs_from_int(T, iw.elo);
+    // lane f: the full lemma in double (off the integer range), or its rerun
+    float o3;
+    const bool ok2 = fs_apply_lean(*t, wr, &o3);
+    if (!trep) ++*n_step;
+    if (__builtin_amdgcn_readlane((int)ok2, f)) {
+      *t = rdl(o3, f);
+    } else {
+      ++*n_rerun;
+      *t = fs_rerun(d, c, base + f, n, *t, lane);
+    }
+    ++f;
+    if (f >= cnt || stop(f)) return f;
+  }
+}
+
 // The walk's records stream through an LDS ring of kFsRing windows (4 KB each: 64 records of 64
 // bytes, the global layout): global_load_lds_dwordx4 moves a window with 4 instructions and no
 // registers, kFsRing - 1 windows ahead of the one being walked.  The loads are counted by vmcnt
 // in issue order, so before reading window w the wave waits until at most the 4 (kFsRing - 1)
 // loads of the windows after it are outstanding (a rerun's own loads drain the counter anyway).
-constexpr int kFsRing = 8;
+constexpr int kFsStepAll = 6;  // more records needing the full lemma: step through the window
+constexpr int kFsGroup = 4;   // windows per fast-path pass
+constexpr int kFsRing = 16;   // windows in the ring (four groups)
 constexpr int kFsWinBytes = kWave * (int)sizeof(FsNode);
 
 __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int64_t K,
@@ -372,9 +656,95 @@ __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int6
 }
 
 __device__ __forceinline__ void fs_ring_wait() {
-  // vmcnt <= 4 (kFsRing - 1) = 28: lgkmcnt and expcnt left at their maxima (no wait)
-  static_assert(4 * (kFsRing - 1) == 28, "ring depth and the s_waitcnt immediate");
-  asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+  // a group's windows loaded: vmcnt <= 4 (kFsRing - kFsGroup) = 48 (lgkmcnt, expcnt: no wait)
+  static_assert(4 * (kFsRing - kFsGroup) == 48, "ring depth and the s_waitcnt immediate");
+  asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+}
+
+struct FsWalkCounters {
+  int64_t win = 0, pass = 0, slow = 0, step = 0, rerun = 0, clk_step = 0, group_fast = 0;
+};
+
+// one window's walk from the exact value t: speculation passes (fast path, the full lemma where
+// it does not decide), lanes stepped alone from the first failed one; returns the value after the
+// window's last chunk
+__device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t base, int64_t n,
+                                                const FsWalkRec wr, int cnt, float t, int lane,
+                                                FsWalkCounters& ct) {
+  const bool fastrec = wr.mu3 >= 0.0f;
+  ++ct.win;
+  int s = 0;
+  while (s < cnt) {
+    ++ct.pass;
+    const bool act = lane >= s && lane < cnt;
+    const uint64_t pb = (uint64_t)__double_as_longlong(wr.P);
+    const double Ps = __longlong_as_double((int64_t)(
+        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pb, s) |
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pb >> 32), s) << 32)));
+    // the speculated starts: t + the member-0 increments of lanes s.., corrected where a chunk's
+    // increment depends on its start (its member chosen by the walk's lead on the guesses at s)
+    double corr = 0.0;
+    const uint64_t slowm = ballot(act && !fastrec);
+    if (__builtin_popcountll(slowm) > kFsStepAll) {
+      // many chunks whose increment depends on the start's low bits (a sum hovering near zero):
+      // speculation would fail at most of them, so the window is stepped through
+      const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
+      fs_step_lanes(d, c, base, n, wr, cnt, s, &t, lane, [](int) { return false; }, &ct.step,
+                    &ct.rerun);
+      if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
+      break;
+    }
+    if (slowm) {
+      const double off = (double)t - (double)rdl(wr.g, s);
+      const double cl = act && !fastrec ? fs_increment_rec(wr, off) - wr.d0 : 0.0;
+      const double inc = wave_incl_scan(cl, lane);
+      const double up = __shfl_up(inc, 1, kWave);
+      corr = lane == 0 ? 0.0 : up;
+    }
+    const double tl = (double)t + ((wr.P - Ps) + corr);
+    // the next lane's speculated start (DPP wave shift: no LDS instruction on this path)
+    const double tn = dpp_next(tl);
+    const bool last = lane == cnt - 1;
+    // fast path (see k_fs_l1): a float start within mu3 of the guess, on its quantum grid
+    const double dq = tl * wr.iq();
+    double out = tl + wr.d0;
+    bool ver = fastrec && (double)(float)tl == tl && fabs(tl - wr.gd()) <= (double)wr.mu3 &&
+               dq == floor(dq) && (double)(float)out == out && (last || out == tn);
+    if (ballot(act && !ver)) {
+      ++ct.slow;
+      // the full lemma where the fast path does not decide
+      float o2;
+      const float tf = (float)tl;
+      const bool ok = (double)tf == tl && fs_apply_lean(tf, wr, &o2);
+      if (!ver) {
+        out = (double)o2;
+        ver = ok && (last || out == tn);
+      }
+    }
+    const uint64_t bad = ballot(act && !ver);
+    if (bad == 0) {
+      t = rdl((float)out, cnt - 1);
+      break;
+    }
+    int f = (int)__builtin_ctzll(bad);
+    // lanes s..f-1 verified: f's start is exact.  Step lane by lane from f while the records
+    // need the full lemma, then speculate again.
+    t = f == s ? t : rdl((float)out, f - 1);
+    const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
+    const float mu3 = wr.mu3;
+    f = fs_step_lanes(d, c, base, n, wr, cnt, f, &t, lane,
+                      [&](int l) { return rdl(mu3, l) >= 0.0f; }, &ct.step, &ct.rerun);
+    if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
+    s = f;
+  }
+  return t;
+}
+
+__device__ __forceinline__ double rld(double v, int l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return __longlong_as_double((int64_t)(
+      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l) |
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l) << 32)));
 }
 
 constexpr int kFwBS = kWave;
@@ -388,20 +758,27 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   const int64_t K = fs_chunks(n);
   const FsNode* R = fs_rec(d.b, c, 0);
   float t = start9 ? start9[c] : 0.0f;
+  // walk counters (dlg_float_sums' walk_stats): windows walked one by one, speculation passes,
+  // passes with lanes the fast path could not decide, lanes stepped alone, reruns, clocks (all,
+  // stepping), groups passed by the group fast path
+  const int64_t clk0 = d.b.wst ? (int64_t)clock64() : 0;
   auto slot = [&](int64_t w) {
     return (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)ring +
                                                        (w % kFsRing) * kFsWinBytes);
   };
+  FsWalkCounters ct;
   if (K > 0)
     for (int w = 0; w < kFsRing; ++w) fs_ring_load(R, (int64_t)w * kWave, K, slot(w), lane);
-  for (int64_t w = 0, base = 0; base < K; ++w, base += kWave) {
+  for (int64_t w = 0; w * kWave < K; w += kFsGroup) {
     fs_ring_wait();
-    // the record from the ring: read by inline asm, since the compiler would otherwise drain
-    // every outstanding load (vmcnt(0)) before an LDS read that may alias an LDS-DMA write
-    f32x4 r0, r1, r2, r3;
-    {
+    // the group's records from the ring (inline asm: the compiler would otherwise drain every
+    // outstanding load before an LDS read that may alias an LDS-DMA write), then the slots are
+    // refilled with the windows kFsRing ahead
+    // (named records, no array: a runtime index would put them in scratch memory)
+    auto read_rec = [&](int j, int* cnj) {
+      f32x4 r0, r1, r2, r3;
       const uint32_t la = (uint32_t)(uintptr_t)(
-          (__attribute__((address_space(3))) char*)slot(w) + sizeof(FsNode) * lane);
+          (__attribute__((address_space(3))) char*)slot(w + j) + sizeof(FsNode) * lane);
       asm volatile(
           "ds_read_b128 %0, %4\n\t"
           "ds_read_b128 %1, %4 offset:16\n\t"
@@ -411,86 +788,67 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
           : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
           : "v"(la)
           : "memory");
+      const int64_t b0 = (w + j) * kWave;
+      *cnj = b0 >= K ? 0 : K - b0 < kWave ? (int)(K - b0) : kWave;
+      return fs_walk_rec(r0, r1, r2, r3);
+    };
+    static_assert(kFsGroup == 4, "four named records");
+    int c0, c1, c2, c3;
+    const FsWalkRec w0 = read_rec(0, &c0), w1 = read_rec(1, &c1), w2 = read_rec(2, &c2),
+                    w3 = read_rec(3, &c3);
+#pragma unroll
+    for (int j = 0; j < kFsGroup; ++j)
+      fs_ring_load(R, (w + j + kFsRing) * kWave, K, slot(w + j), lane);
+    // group fast path: every record fast, the four windows' starts from the chunk increments'
+    // prefixes, all verified at once (else window by window)
+    auto fastm = [&](const FsWalkRec& x, int cn) {
+      return ballot(lane < cn && !(x.mu3 >= 0.0f)) == 0;
+    };
+    if (fastm(w0, c0) && fastm(w1, c1) && fastm(w2, c2) && fastm(w3, c3)) {
+      double B = 0.0, prev_out = 0.0;
+      bool okg = true;
+      auto win = [&](const FsWalkRec& x, int cn, bool first) {
+        if (cn == 0) return;
+        const double tl = (double)t + (B + x.P);
+        const double tn = dpp_next(tl);
+        const bool last = lane == cn - 1;
+        const double dq = tl * x.iq();
+        const double out = tl + x.d0;
+        const bool ver = (double)(float)tl == tl && fabs(tl - x.gd()) <= (double)x.mu3 &&
+                         dq == floor(dq) && (double)(float)out == out && (last || out == tn);
+        okg = okg && ballot(lane < cn && !ver) == 0;
+        if (!first) okg = okg && rld(tl, 0) == prev_out;  // (the windows' seam)
+        prev_out = rld(out, cn - 1);
+        B = B + rld(x.P + x.d0, cn - 1);
+      };
+      win(w0, c0, true);
+      win(w1, c1, false);
+      win(w2, c2, false);
+      win(w3, c3, false);
+      if (okg) {
+        ++ct.group_fast;
+        t = (float)prev_out;
+        continue;
+      }
     }
-    // (the slot is free once read: the window kFsRing ahead goes into it)
-    fs_ring_load(R, base + (int64_t)kFsRing * kWave, K, slot(w), lane);
-    const int cnt = K - base < kWave ? (int)(K - base) : kWave;
-    FsNode nd;
-    nd.g = r0.x;
-    nd.pad0 = nd.pad1 = nd.pad2 = 0.0f;
-    nd.o[0] = r1.x; nd.o[1] = r1.y; nd.o[2] = r1.z; nd.o[3] = r1.w;
-    nd.mu[0] = r2.x; nd.mu[1] = r2.y; nd.mu[2] = r2.z; nd.mu[3] = r2.w;
-    nd.qm[0] = r3.x; nd.qm[1] = r3.y; nd.qm[2] = r3.z; nd.qm[3] = r3.w;
-    const double P = __longlong_as_double((int64_t)(((uint64_t)__float_as_uint(r0.z) << 32) |
-                                                    __float_as_uint(r0.y)));
-    const float mu3 = r0.w;
-    const bool fastrec = mu3 >= 0.0f;
-    const double gd = (double)nd.g;
-    const double iq = fs_inv_quantum(nd.g);
-    const double d0 = nd.qm[0] >= 0.0f ? (double)nd.o[0] - gd : 0.0;
-    int s = 0;
-    while (s < cnt) {
-      const bool act = lane >= s && lane < cnt;
-      const uint64_t pb = (uint64_t)__double_as_longlong(P);
-      const double Ps = __longlong_as_double((int64_t)(
-          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pb, s) |
-          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pb >> 32), s) << 32)));
-      // the speculated starts: t + the member-0 increments of lanes s.., corrected where a
-      // chunk's increment depends on its start (its member chosen by the walk's lead on the
-      // guesses at lane s)
-      double corr = 0.0;
-      const uint64_t slowm = ballot(act && !fastrec);
-      if (slowm) {
-        const double off = (double)t - (double)rdl(nd.g, s);
-        const double cl = act && !fastrec ? fs_increment(nd, off) - d0 : 0.0;
-        const double inc = wave_incl_scan(cl, lane);
-        const double up = __shfl_up(inc, 1, kWave);
-        corr = lane == 0 ? 0.0 : up;
-      }
-      const double tl = (double)t + ((P - Ps) + corr);
-      // the next lane's speculated start (DPP wave shift: no LDS instruction on this path)
-      const double tn = dpp_next(tl);
-      const bool last = lane == cnt - 1;
-      // fast path (see k_fs_l1): a float start within mu3 of the guess, on its quantum grid
-      const double dq = (tl - gd) * iq;
-      double out = tl + d0;
-      bool ver = fastrec && (double)(float)tl == tl && fabs(tl - gd) <= (double)mu3 &&
-                 dq == floor(dq) && (double)(float)out == out && (last || out == tn);
-      if (ballot(act && !ver)) {
-        // the full lemma where the fast path does not decide
-        if (act && !ver) {
-          FsApply a;
-          a.out = 0.0f;
-          const float tf = (float)tl;
-          const bool ok = (double)tf == tl && fs_apply(tf, nd, &a);
-          out = (double)a.out;
-          ver = ok && (last || out == tn);
-        }
-      }
-      const uint64_t bad = ballot(act && !ver);
-      if (bad == 0) {
-        t = rdl((float)out, cnt - 1);
-        break;
-      }
-      int f = (int)__builtin_ctzll(bad);
-      // lanes s..f-1 verified: f's start is exact.  Step lane by lane from f while the records
-      // need the full lemma (sums hovering near zero: runs of such chunks), then speculate again.
-      t = f == s ? t : rdl((float)out, f - 1);
-      for (;;) {
-        FsApply a2;
-        a2.out = 0.0f;
-        const bool ok2 = fs_apply(t, nd, &a2);
-        if (__builtin_amdgcn_readlane((int)ok2, f))
-          t = rdl(a2.out, f);
-        else
-          t = fs_rerun(d, c, base + f, n, t, lane);
-        ++f;
-        if (f >= cnt || rdl(mu3, f) >= 0.0f) break;
-      }
-      s = f;
+    for (int j = 0; j < kFsGroup; ++j) {
+      const int cn = j == 0 ? c0 : j == 1 ? c1 : j == 2 ? c2 : c3;
+      if (cn == 0) break;
+      FsWalkRec x;  // (field by field: a struct-level select goes through scratch memory)
+#define DLG_SEL(f) x.f = j == 0 ? w0.f : j == 1 ? w1.f : j == 2 ? w2.f : w3.f
+      DLG_SEL(g); DLG_SEL(mu3); DLG_SEL(o0); DLG_SEL(o1); DLG_SEL(o2); DLG_SEL(o3);
+      DLG_SEL(m0); DLG_SEL(m1); DLG_SEL(m2); DLG_SEL(m3); DLG_SEL(q0); DLG_SEL(q1);
+      DLG_SEL(q2); DLG_SEL(q3); DLG_SEL(d0); DLG_SEL(P);
+#undef DLG_SEL
+      t = fs_walk_window(d, c, (w + j) * kWave, n, x, cn, t, lane, ct);
     }
   }
   __builtin_amdgcn_s_waitcnt(0);  // (the ring's last loads: never read, but drained)
+  if (d.b.wst && lane == 0) {
+    int64_t* w = d.b.wst + 8 * c;
+    w[0] = ct.win; w[1] = ct.pass; w[2] = ct.slow; w[3] = ct.step; w[4] = ct.rerun;
+    w[5] = (int64_t)clock64() - clk0; w[6] = ct.clk_step; w[7] = ct.group_fast;
+  }
   __shared__ unsigned s_ticket;
   if (lane == 0) {
     __hip_atomic_store(reinterpret_cast<int32_t*>(d.b.sums) + c, __float_as_int(t),
@@ -522,14 +880,15 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 }  // namespace
 
-size_t fs_scratch_bytes(int64_t n_cap) {
+size_t fs_scratch_bytes(int64_t n_cap, int world) {
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t K = fs_chunks(nc), U = (K + kFsUC - 1) / kFsUC;
   return align256(sizeof(double) * K * kFsChains) + 2 * align256(sizeof(double) * U * kFsChains) +
-         align256(sizeof(FsNode) * K * kFsChains) + align256(sizeof(float) * 16) + 256;
+         align256(sizeof(FsNode) * K * kFsChains) + align256(sizeof(float) * 32) +
+         align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) + 256;
 }
 
-FsBuffers fs_carve(void* base, int64_t n_cap) {
+FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t K = fs_chunks(nc), U = (K + kFsUC - 1) / kFsUC;
   uint8_t* p = static_cast<uint8_t*>(base);
@@ -543,24 +902,49 @@ FsBuffers fs_carve(void* base, int64_t n_cap) {
   b.rec = reinterpret_cast<FsNode*>(p);
   b.cap = K;
   p += align256(sizeof(FsNode) * K * kFsChains);
-  b.sums = reinterpret_cast<float*>(p);
-  p += align256(sizeof(float) * 16);
-  b.ticket = reinterpret_cast<unsigned*>(p);  // [0]: k_fs_prep, [1]: k_fs_walk
+  b.sums = reinterpret_cast<float*>(p);      // [0..8] end values, [16..24] the received starts
+  b.start9 = b.sums + 16;
+  p += align256(sizeof(float) * 32);
+  b.tot = reinterpret_cast<double*>(p);       // [0..9] this rank's totals + count, [16..24] base
+  b.base9 = b.tot + 16;
+  b.n_global = reinterpret_cast<int64_t*>(b.tot + 26);
+  p += align256(sizeof(double) * 32);
+  b.gath = reinterpret_cast<double*>(p);      // [world][10]
+  p += align256(sizeof(double) * (kFsChains + 1) * world);
+  b.ticket = reinterpret_cast<unsigned*>(p);  // [0]: k_fs_prep / k_fs_inc, [1]: k_fs_walk
   return b;
 }
 
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
-                     float4* cout, int32_t* res, int num_cus, hipStream_t s) {
+                     float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm) {
   FsDev d{px, py, pz, stride, n_dev, b};
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t U = (fs_chunks(nc) + kFsUC - 1) / kFsUC;
   const int gp = (int)std::min<int64_t>(U, 2 * (int64_t)num_cus);
   const int gl = (int)std::min<int64_t>(U * kFsChains, 8 * (int64_t)num_cus);
-  hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr);
-  hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, nullptr);
+  const int W = comm ? comm->world() : 1, r = comm ? comm->rank() : 0;
+  if (W == 1) {
+    hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, nullptr);
+    hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, nullptr);
+    hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
+    hipLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, d, nullptr, cin, cout, res);
+    return;
+  }
+  // several ranks (the list is the ranks' segments in order): each rank's guesses start from the
+  // double totals of the ranks before it; the chains' exact values are handed from rank to rank
+  // (rank r walks from rank r - 1's end values) and the last rank's sums are broadcast
+  hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, b.tot);
+  comm->allgather(b.tot, b.gath, kFsChains + 1, DType::F64, s);
+  hipLaunchKernelGGL(k_fs_base, dim3(1), dim3(256), 0, s, d, b.gath, r, W, b.base9, b.n_global);
+  hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, b.base9);
   hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-  hipLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, d, nullptr, cin, cout, res);
+  if (r > 0) comm->recv(b.start9, kFsChains, DType::I32, r - 1, s);
+  hipLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, d, r > 0 ? b.start9 : nullptr,
+                     nullptr, nullptr, nullptr);
+  if (r < W - 1) comm->send(b.sums, kFsChains, DType::I32, r + 1, s);
+  comm->broadcast(b.sums, kFsChains, DType::I32, W - 1, s);
+  hipLaunchKernelGGL(k_fs_tail, dim3(1), dim3(1), 0, s, b.sums, b.n_global, cin, cout, res);
 }
 
 }  // namespace dlg

@@ -197,7 +197,8 @@ void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1St
 
 // PCL's float refit on the device (fsum.hip): the nine sequential float sums of
 // computeMeanAndCovarianceMatrix evaluated exactly in parallel (fsum.hpp), then the float
-// eigen33.  Inliers px/py/pz with element stride `stride` floats, count *n_dev (<= n_cap).
+// eigen33.  Inliers px/py/pz with element stride `stride` floats, count *n_dev (<= n_cap): this
+// rank's segment of the list (the ranks' segments in rank order make up the list).
 // res (16 int32): [0] = 1 when a transcendental of eigen33 could not be rounded for certain
 // (the host then recomputes the plane from the sums), [1] = n, [2..10] = the nine sums' bits.
 struct FsNode;
@@ -208,14 +209,23 @@ struct FsBuffers {
   FsNode* rec = nullptr;   // chunk records, chain-major: rec[c * cap + k]
   int64_t cap = 0;         // chunks per chain
   float* sums = nullptr;   // [9] the chains' end values
+  float* start9 = nullptr; // [9] several ranks: the chains' values at this rank's first inlier
+  double* tot = nullptr;   // [10] several ranks: this rank's double term sums + inlier count
+  double* base9 = nullptr; // [9] several ranks: the totals of the ranks before this one
+  int64_t* n_global = nullptr;  // several ranks: the inliers of all ranks
+  double* gath = nullptr;  // [world][10] several ranks: every rank's tot
   unsigned* ticket = nullptr;  // [2], zero on entry
+  int64_t* wst = nullptr;      // [9][8] walk counters (dlg_float_sums), or null
 };
 // bytes of scratch for n_cap inliers; carve() lays the buffers out in `base`
-size_t fs_scratch_bytes(int64_t n_cap);
-FsBuffers fs_carve(void* base, int64_t n_cap);
+// (world: the ranks of the communicator passed to launch_fs_refit; comm null or one rank: the
+// whole list is here)
+size_t fs_scratch_bytes(int64_t n_cap, int world);
+FsBuffers fs_carve(void* base, int64_t n_cap, int world);
+class Comm;
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
-                     float4* cout, int32_t* res, int num_cus, hipStream_t s);
+                     float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm = nullptr);
 
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers

@@ -138,17 +138,23 @@ class Context:
     def barrier(self):
         self.check(self._L.dlg_barrier(self.h))
 
-    def float_sums(self, xyz, cin=(0.0, 0.0, 1.0, 0.0), reps=1):
+    def float_sums(self, xyz, cin=(0.0, 0.0, 1.0, 0.0), reps=1, walk_stats=False):
         """dlg_float_sums: DLG_REFIT_PCL's device sums (fsum.hip) over xyz (n x 3 float32, list
-        order) and the float refit of cin -> (sums[9], coeff[4], uncertain, ms_per_call)."""
+        order) and the float refit of cin -> (sums[9], coeff[4], uncertain, ms_per_call), plus
+        the walk's per-chain counters [9, 8] when walk_stats."""
         a = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
         ci = np.ascontiguousarray(cin, np.float32)
         sums = np.zeros(9, np.float32)
         co = np.zeros(4, np.float32)
         unc, ms = C.c_int(), C.c_double()
+        ws = np.zeros((9, 8), np.int64) if walk_stats else None
         self.check(self._L.dlg_float_sums(self.h, _f32p(a), C.c_int64(a.shape[0]), _f32p(ci),
                                           int(reps), _f32p(sums), _f32p(co), C.byref(unc),
-                                          C.byref(ms)))
+                                          C.byref(ms),
+                                          ws.ctypes.data_as(C.POINTER(C.c_int64)) if walk_stats
+                                          else None))
+        if walk_stats:
+            return sums, co, bool(unc.value), ms.value, ws
         return sums, co, bool(unc.value), ms.value
 
     def allreduce_max(self, v: float) -> float:

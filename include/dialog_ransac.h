@@ -343,10 +343,12 @@ dlg_status dlg_score_benchmark(dlg_ctx* ctx, dlg_cloud* cloud, int D, int kernel
  * xx, xy, xz, yy, yz, zz, x, y, z in list order) over n points (xyz: 3 floats each), then
  * optimizeModelCoefficients' float eigen33 refit of cin.  sums_out[9] and coeff_out[4] are the
  * device's bits; *uncertain = 1 when an eigen33 transcendental could not be rounded for certain
- * (the extraction then takes the host's value).  reps >= 1 launches are timed: *ms_per_call. */
+ * (the extraction then takes the host's value).  reps >= 1 launches are timed: *ms_per_call.
+ * walk_stats (optional) per chain: windows, speculation passes, passes needing the full lemma,
+ * chunks stepped alone, reruns, shader clocks of the walk, of its stepping, chunk records. */
 dlg_status dlg_float_sums(dlg_ctx* ctx, const float* xyz, int64_t n, const float cin[4], int reps,
                           float sums_out[9], float coeff_out[4], int* uncertain,
-                          double* ms_per_call);
+                          double* ms_per_call, int64_t* walk_stats /* nullable: [9][8] */);
 /* Execution-path options of a context.  Every setting gives identical results (planes, inliers,
  * counts): they only choose among equivalent device paths, for tests and measurement.  There are
  * no environment switches in the library. */

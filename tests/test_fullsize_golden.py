@@ -154,6 +154,20 @@ def run_sharded(p, bounds, mode):
 
 
 @pytest.mark.skipif("c3" not in DB, reason="fullsize.json has no c3")
+@pytest.mark.parametrize("bounds", ["halves", "uneven3"])
+def test_c3_pcl_sharded(gpu_ctx, bounds):
+    """DLG_REFIT_PCL over in-process ranks (halves: lean rounds on both; uneven3: one shard below
+    the Morton-copy size, so the list path): the nine float chains are walked rank after rank in
+    list order, and the planes equal the one-rank oracle's PCL refit bit for bit."""
+    p = cloud("c3")
+    b = [0, p.shape[0] // 2, p.shape[0]] if bounds == "halves" else [0, 100_000, 4_000_000, p.shape[0]]
+    out = run_sharded(p, b, "pcl")
+    for r in range(len(b) - 1):
+        check_extract(out[r], DB["c3"]["modes"]["pcl"])
+        assert (out[r]["stats"]["lean_rounds"] > 0) == (bounds == "halves")
+
+
+@pytest.mark.skipif("c3" not in DB, reason="fullsize.json has no c3")
 def test_c3_fast_uneven_shards_agree_on_lean(gpu_ctx):
     """One shard below the Morton-copy size (131072 points), one above: the ranks agree once per
     extraction that lean rounds need every rank's spatial copy, so both take the list path, and

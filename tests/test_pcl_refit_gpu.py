@@ -106,8 +106,8 @@ def test_extract_pcl_adversarial_sums(case):
 
 
 def test_segment_pcl_three_levels(gpu_ctx):
-    """One segment() with ~1.4M inliers: more than 128 level-2 nodes, so the top walk runs over
-    level-3 records (k_fs_level<3>)."""
+    """One segment() with ~1.4M inliers: more than 64 units of 4096 (the unit scans run over
+    several windows) and ~22k chunk records per chain for the walk."""
     p, _, _ = plane_cloud(1_600_000, 1, seed=515, outlier_frac=0.1)
     kw = dict(max_iterations=255, probability=1.0)
     ref = O.sac_segment(p, 0.02, **kw)
@@ -117,6 +117,43 @@ def test_segment_pcl_three_levels(gpu_ctx):
     assert st["n_unrefined"] == ref["n_unrefined"] > 524288
     assert np.array_equal(bits(coeff), bits(ref["coeff"])), (coeff, ref["coeff"])
     assert np.array_equal(inl, ref["inliers"])
+
+
+@pytest.mark.parametrize("world,lean", [(2, 1), (3, 1), (3, 0)])
+def test_extract_pcl_sharded(world, lean):
+    """The PCL refit over in-process ranks (one shard empty in one case): every rank walks its
+    segment of the list from the previous rank's end values; == the one-rank oracle."""
+    import threading
+    rng = np.random.default_rng(70 + world + lean)
+    n = int(rng.integers(300000, 500000))
+    p, _, _ = plane_cloud(n, 5, seed=world * 10 + lean, outlier_frac=0.15)
+    kw = dict(max_iterations=511, probability=1.0)
+    ref = O.extract_planes(p, 0.02, max_planes=6, min_inliers=200, **kw)
+    cuts = sorted(rng.integers(150000, n - 150000, world - 1).tolist())
+    if world == 3 and not lean:
+        cuts = [cuts[0], cuts[0]]  # (an empty middle shard)
+    b = [0, *cuts, n]
+    ctxs = D.Context.loopback_group(world, 0)
+    out, errs = [None] * world, []
+
+    def run(r):
+        try:
+            ctxs[r].set_option(D.DLG_OPT_LEAN_ROUNDS, lean)
+            c = D.Cloud(ctxs[r], p[b[r]:b[r + 1]], id_base=b[r])
+            out[r] = D.extract_planes(c, D.make_params(0.02, **kw), max_planes=6, min_inliers=200,
+                                      capacity=n)
+            c.close()
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    for r in range(world):
+        check(out[r], ref, (world, lean, r))
 
 
 def test_normal_plane_pcl_refit_device():
