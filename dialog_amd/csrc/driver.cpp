@@ -1058,6 +1058,55 @@ dlg_status init_ctx(dlg_ctx* c, int device) {
 
 }  // namespace
 
+// normals records on the device (raw_dev: stride_f floats per record, curvature at curv_off,
+// indexed by uploaded point (by_pos false) or by pristine position) -> the cloud's normal
+// buffers (normalized, + curvature), the Morton copy's, the curvature range; the cloud is reset
+void dlg::attach_normals(dlg_ctx* c, dlg_cloud* cl, const float* raw_dev, int64_t stride_f,
+                    int curv_off, bool by_pos) {
+  {
+    cl->cur = -1;  // normals attach to the pristine list: the cloud is reset
+    cl->n_active = cl->n_total;
+    cl->pristine.ensure_nrm((size_t)std::max<int64_t>(cl->n_total, 1));
+    if (raw_dev && cl->n_total > 0) {
+      PointsView pv = cl->pristine.view(cl->n_total);
+      if (by_pos) pv.gid = nullptr;
+      launch_pack_point_normals(raw_dev, stride_f, curv_off, pv, cl->id_base, cl->pristine.nrm.p,
+                                c->stream);
+      HIPCHK(hipGetLastError());
+      // the Morton copy carries the normals too (pruned NORMAL_PLANE scoring)
+      if (cl->sp_built) {
+        cl->sp_pristine.ensure_nrm((size_t)std::max<int64_t>(cl->sp_n_pristine, 1));
+        launch_gather_nrm(cl->pristine.nrm.p, cl->sp_order.p, cl->sp_n_pristine,
+                          cl->sp_pristine.nrm.p, c->stream);
+      }
+      // curvature range -> the largest w = lambda (1 - curvature) of the cloud
+      c->small.ensure(8);
+      uint32_t* cr = reinterpret_cast<uint32_t*>(c->small.p + 7);
+      launch_curv_range(cl->pristine.nrm.p, cl->n_total, cr, c->stream);
+      uint32_t h[2] = {0u, 0u};
+      HIPCHK(hipMemcpyAsync(h, cr, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipGetLastError());
+      sync(c);
+      auto ord2f = [](uint32_t o) {
+        const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f;
+      };
+      cl->curv_known = h[0] <= h[1];  // (all NaN: no finite curvature)
+      if (cl->curv_known) {
+        cl->curv_min = ord2f(h[0]);
+        cl->curv_max = ord2f(h[1]);
+      }
+    }
+    cl->has_normals = true;
+    cl->sp_cur = -1;  // (the reset above also resets the Morton copy)
+    cl->sp_n = cl->sp_n_pristine;
+    cl->sp_valid = cl->sp_built;
+    cl->sp_dirty = false;
+  }
+}
+
 // ================================================================================================
 // C ABI
 // ================================================================================================
@@ -1376,49 +1425,15 @@ dlg_status dlg_cloud_set_normals(dlg_ctx* c, dlg_cloud* cl, const float* normals
   if (stride_bytes != 16 && (stride_bytes < 32 || stride_bytes % 4))
     return fail(c, DLG_ERR_INVALID, "stride_bytes must be 16 (nx, ny, nz, curvature) or >= 32 (pcl::Normal)");
   return guarded(c, [&] {
-    cl->cur = -1;  // normals attach to the pristine list: the cloud is reset
-    cl->n_active = cl->n_total;
-    cl->pristine.ensure_nrm((size_t)std::max<int64_t>(cl->n_total, 1));
+    const float* raw_dev = nullptr;
     if (n > 0) {
       DevBuf<uint8_t>& raw = c->nw.raw;  // scratch shared with the normals path
       raw.ensure((size_t)n * (size_t)stride_bytes);
       HIPCHK(hipMemcpyAsync(raw.p, normals, (size_t)n * (size_t)stride_bytes,
                             hipMemcpyHostToDevice, c->stream));
-      launch_pack_point_normals(reinterpret_cast<const float*>(raw.p), stride_bytes / 4,
-                                stride_bytes == 16 ? 3 : 4, cl->pristine.view(cl->n_total),
-                                cl->id_base, cl->pristine.nrm.p, c->stream);
-      HIPCHK(hipGetLastError());
-      // the Morton copy carries the normals too (pruned NORMAL_PLANE scoring)
-      if (cl->sp_built) {
-        cl->sp_pristine.ensure_nrm((size_t)std::max<int64_t>(cl->sp_n_pristine, 1));
-        launch_gather_nrm(cl->pristine.nrm.p, cl->sp_order.p, cl->sp_n_pristine,
-                          cl->sp_pristine.nrm.p, c->stream);
-      }
-      // curvature range -> the largest w = lambda (1 - curvature) of the cloud
-      c->small.ensure(8);
-      uint32_t* cr = reinterpret_cast<uint32_t*>(c->small.p + 7);
-      launch_curv_range(cl->pristine.nrm.p, cl->n_total, cr, c->stream);
-      uint32_t h[2] = {0u, 0u};
-      HIPCHK(hipMemcpyAsync(h, cr, 8, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(hipGetLastError());
-      sync(c);
-      auto ord2f = [](uint32_t o) {
-        const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
-        float f;
-        std::memcpy(&f, &u, 4);
-        return f;
-      };
-      cl->curv_known = h[0] <= h[1];  // (all NaN: no finite curvature)
-      if (cl->curv_known) {
-        cl->curv_min = ord2f(h[0]);
-        cl->curv_max = ord2f(h[1]);
-      }
+      raw_dev = reinterpret_cast<const float*>(raw.p);
     }
-    cl->has_normals = true;
-    cl->sp_cur = -1;  // (the reset above also resets the Morton copy)
-    cl->sp_n = cl->sp_n_pristine;
-    cl->sp_valid = cl->sp_built;
-    cl->sp_dirty = false;
+    attach_normals(c, cl, raw_dev, stride_bytes / 4, stride_bytes == 16 ? 3 : 4, false);
   });
 }
 

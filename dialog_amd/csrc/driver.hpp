@@ -323,4 +323,8 @@ dlg_status guarded(dlg_ctx* c, F&& f) {
   }
 }
 
+// normals on the device -> the cloud (dlg_cloud_set_normals, dlg_cloud_estimate_normals)
+void attach_normals(dlg_ctx* c, dlg_cloud* cl, const float* raw_dev, int64_t stride_f,
+                    int curv_off, bool by_pos);
+
 }  // namespace dlg

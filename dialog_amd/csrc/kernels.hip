@@ -1331,7 +1331,8 @@ __global__ void k_pack_point_normals(const float* __restrict__ raw, int64_t stri
                                      PointsView src, int32_t id_base, float4* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= src.n) return;
-  const float* r = raw + (int64_t)(src.gid[e] - id_base) * stride_f;
+  // (gid null: the records follow the list's positions)
+  const float* r = raw + (src.gid ? (int64_t)(src.gid[e] - id_base) : e) * stride_f;
   out[e] = eigen_normalized3(r[0], r[1], r[2], r[curv_off]);
 }
 

@@ -179,23 +179,43 @@ void check_points(const dlg_points* pts) {
 
 namespace {
 
-void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn, const float* vp_in,
-                      float* out, int64_t out_stride, int mode) {
+void check_normals_args(float radius, int k_nn, int mode) {
   if (mode != DLG_NORMALS_PCL_FLOAT && mode != DLG_NORMALS_CENTRED_DOUBLE)
     throw DlgError(DLG_ERR_INVALID, "mode must be DLG_NORMALS_PCL_FLOAT or DLG_NORMALS_CENTRED_DOUBLE");
-  const bool pclf = mode == DLG_NORMALS_PCL_FLOAT;
+  if (k_nn < 0 || k_nn > kMaxKnn) throw DlgError(DLG_ERR_INVALID, "k_nn must be in 0..64");
+  if (k_nn == 0 && !(radius > 0.0f && std::isfinite(radius)))
+    throw DlgError(DLG_ERR_INVALID, "neither radius nor k set");  // PCL initCompute error
+}
+
+// the normals of the n points in nw.x/y/z (bounding box b) -> nw.nrm (nx, ny, nz, curvature)
+void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, const float* vp_in,
+                  int mode);
+
+void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn, const float* vp_in,
+                      float* out, int64_t out_stride, int mode) {
+  check_normals_args(radius, k_nn, mode);
   check_points(pts);
   if (!out) throw DlgError(DLG_ERR_INVALID, "normals_out is null");
   if (out_stride != 16 && out_stride < 32) throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be 16 or >= 32");
   if (out_stride % 4) throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be a multiple of 4");
-  if (k_nn < 0 || k_nn > kMaxKnn) throw DlgError(DLG_ERR_INVALID, "k_nn must be in 0..64");
-  if (k_nn == 0 && !(radius > 0.0f && std::isfinite(radius)))
-    throw DlgError(DLG_ERR_INVALID, "neither radius nor k set");  // PCL initCompute error
   const int n = (int)pts->n;
   if (n == 0) return;
+  const BBox b = upload_points(c, pts);
+  normals_core(c, n, b, radius, k_nn, vp_in, mode);
+  NormalsWork& w = c->nw;
+  const size_t obytes = (size_t)n * (size_t)out_stride;
+  w.out.ensure(obytes);
+  launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), out_stride / 4,
+                      out_stride == 16 ? 3 : 4, c->stream);
+  HIPCHK(hipMemcpyAsync(out, w.out.p, obytes, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+}
+
+void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, const float* vp_in,
+                  int mode) {
+  const bool pclf = mode == DLG_NORMALS_PCL_FLOAT;
   const float vp[3] = {vp_in ? vp_in[0] : 0.0f, vp_in ? vp_in[1] : 0.0f, vp_in ? vp_in[2] : 0.0f};
   NormalsWork& w = c->nw;
-  const BBox b = upload_points(c, pts);
   w.nrm.ensure(n);
   GridBufs B;
   if (k_nn == 0) {
@@ -257,12 +277,6 @@ void estimate_normals(dlg_ctx* c, const dlg_points* pts, float radius, int k_nn,
     }
   }
   HIPCHK(hipGetLastError());
-  const size_t obytes = (size_t)n * (size_t)out_stride;
-  w.out.ensure(obytes);
-  launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), out_stride / 4,
-                      out_stride == 16 ? 3 : 4, c->stream);
-  HIPCHK(hipMemcpyAsync(out, w.out.p, obytes, hipMemcpyDeviceToHost, c->stream));
-  sync(c);
 }
 
 int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64_t stride,
@@ -495,6 +509,38 @@ dlg_status dlg_estimate_normals_ex(dlg_ctx* c, const dlg_points* pts, float radi
   if (!c) return DLG_ERR_INVALID;
   return guarded(c, [&] {
     estimate_normals(c, pts, radius, k_nn, viewpoint, normals_out, out_stride_bytes, mode);
+  });
+}
+
+dlg_status dlg_cloud_estimate_normals(dlg_ctx* c, dlg_cloud* cl, float radius, int k_nn,
+                                      const float viewpoint[3], int mode, float* normals_out,
+                                      int64_t out_stride_bytes) {
+  if (!c || !cl || cl->ctx != c) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    check_normals_args(radius, k_nn, mode);
+    if (normals_out && (out_stride_bytes % 4 || (out_stride_bytes != 16 && out_stride_bytes < 32)))
+      throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be 16 or >= 32 (multiple of 4)");
+    if (cl->n_total > INT32_MAX / 2) throw DlgError(DLG_ERR_INVALID, "more than 2^30 points");
+    const int n = (int)cl->n_total;
+    NormalsWork& w = c->nw;
+    if (n > 0) {
+      // the cloud's own device copy (upload order) is the point set
+      w.x.ensure(n); w.y.ensure(n); w.z.ensure(n);
+      HIPCHK(hipMemcpyAsync(w.x.p, cl->pristine.x.p, 4 * (size_t)n, hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(w.y.p, cl->pristine.y.p, 4 * (size_t)n, hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(w.z.p, cl->pristine.z.p, 4 * (size_t)n, hipMemcpyDeviceToDevice, c->stream));
+      const BBox b = bbox_of(c, w.x.p, w.y.p, w.z.p, n);
+      normals_core(c, n, b, radius, k_nn, viewpoint, mode);
+    }
+    attach_normals(c, cl, n > 0 ? reinterpret_cast<const float*>(w.nrm.p) : nullptr, 4, 3, true);
+    if (normals_out && n > 0) {
+      const size_t obytes = (size_t)n * (size_t)out_stride_bytes;
+      w.out.ensure(obytes);
+      launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), out_stride_bytes / 4,
+                          out_stride_bytes == 16 ? 3 : 4, c->stream);
+      HIPCHK(hipMemcpyAsync(normals_out, w.out.p, obytes, hipMemcpyDeviceToHost, c->stream));
+    }
+    sync(c);
   });
 }
 

@@ -202,6 +202,21 @@ class Cloud:
         self.ctx.check(self.ctx._L.dlg_cloud_set_normals(self.ctx.h, self.h, _f32p(a), a.shape[0],
                                                          4 * a.shape[1]))
 
+    def estimate_normals(self, radius: float = 0.0, k: int = 0, viewpoint=(0.0, 0.0, 0.0),
+                         mode: str = "pcl", copy_out: bool = False):
+        """dlg_cloud_estimate_normals: estimateNormal() on this cloud's own device copy, the
+        normals attached to the cloud (as set_normals; the cloud is reset) with no host round
+        trip.  mode "pcl" (bit-exact PCL arithmetic) or "double".  copy_out: also return them
+        as float32 [N,4] (nx, ny, nz, curvature)."""
+        m = {"pcl": 0, "double": 1}[mode]
+        vp = np.ascontiguousarray(viewpoint, np.float32)
+        n = self.n
+        out = np.empty((n, 4), np.float32) if copy_out else None
+        self.ctx.check(self.ctx._L.dlg_cloud_estimate_normals(
+            self.ctx.h, self.h, float(radius), int(k), _f32p(vp), m,
+            _f32p(out) if copy_out else None, 16))
+        return out
+
     @property
     def n_active(self):
         v = C.c_int64()

@@ -209,6 +209,14 @@ enum { DLG_NORMALS_PCL_FLOAT = 0, DLG_NORMALS_CENTRED_DOUBLE = 1 };
 dlg_status dlg_estimate_normals_ex(dlg_ctx* ctx, const dlg_points* pts, float radius, int k_nn,
                                    const float viewpoint[3], float* normals_out,
                                    int64_t out_stride_bytes, int mode);
+/* estimateNormal() on a cloud already on the device (the C5 chain: normals fused ahead of the
+ * NORMAL_PLANE segmentation without a host round trip): the normals of dlg_estimate_normals_ex
+ * (same neighbourhoods, same arithmetic for `mode`) over the cloud's uploaded points, attached
+ * to the cloud as dlg_cloud_set_normals would attach them (the cloud is reset).  normals_out
+ * (nullable): also copied out, records of out_stride_bytes as dlg_estimate_normals writes them. */
+dlg_status dlg_cloud_estimate_normals(dlg_ctx* ctx, dlg_cloud* cloud, float radius, int k_nn,
+                                      const float viewpoint[3], int mode, float* normals_out,
+                                      int64_t out_stride_bytes);
 /* regulateNormal() first-round branch (PlaneDetect.h:586-646): flip the seed normal unless
  * seed_is_outward (is_norm_direction_valid), then BFS over radius-`radius` neighbourhoods
  * (r_for_regulate_normal, config.txt:9) in PCL's queue order, flipping each newly reached normal

@@ -271,18 +271,41 @@ def test_gpu_c5_chain_vs_oracle_chain(gpu_ctx, nmode, refit):
     assert np.array_equal(g.view(np.uint32), o.view(np.uint32))
     kw = dict(max_iterations=255, probability=1.0)
     mode = D.DLG_REFIT_PCL if refit == "pcl" else D.DLG_REFIT_FAST
-    cloud = D.Cloud(gpu_ctx, p)
-    cloud.set_normals(g)
     prm = D.make_params(0.05, model=D.SACMODEL_NORMAL_PLANE, normal_distance_weight=0.1,
                         refit_mode=mode, **kw)
-    e = D.extract_planes(cloud, prm, max_planes=6, min_inliers=200)
-    cloud.close()
     r = O.extract_planes(p, 0.05, max_planes=6, min_inliers=200, normals=o,
                          normal_distance_weight=0.1, refit=refit, **kw)
-    assert e["n_planes"] == r["n_planes"] >= 4
-    assert np.array_equal(e["coeffs"].view(np.uint32), r["coeffs"].view(np.uint32))
-    assert np.array_equal(e["offsets"], r["offsets"])
-    assert np.array_equal(e["inliers"], r["inliers"])
+    # host hand-off (normals out, then back in) and the device-resident chain
+    # (dlg_cloud_estimate_normals: the normals never leave the device)
+    for resident in (False, True):
+        cloud = D.Cloud(gpu_ctx, p)
+        if resident:
+            gd = cloud.estimate_normals(radius=0.1 if nmode == "radius" else 0.0,
+                                        k=0 if nmode == "radius" else 20, copy_out=True)
+            assert np.array_equal(gd.view(np.uint32), o.view(np.uint32))
+        else:
+            cloud.set_normals(g)
+        e = D.extract_planes(cloud, prm, max_planes=6, min_inliers=200)
+        cloud.close()
+        assert e["n_planes"] == r["n_planes"] >= 4
+        assert np.array_equal(e["coeffs"].view(np.uint32), r["coeffs"].view(np.uint32))
+        assert np.array_equal(e["offsets"], r["offsets"])
+        assert np.array_equal(e["inliers"], r["inliers"])
+
+
+@pytest.mark.gpu
+def test_gpu_cloud_normals_index_subset(gpu_ctx):
+    """dlg_cloud_estimate_normals on a cloud uploaded with an index subset (and a non-zero id
+    base): the normals of the subset cloud itself, == dlg_estimate_normals on those points."""
+    import dialog_amd as D
+    from dialog_amd.synth import plane_cloud
+    p, _, _ = plane_cloud(40000, 4, outlier_frac=0.1, seed=77, patch=2.0)
+    idx = np.sort(np.random.default_rng(1).choice(p.shape[0], 25000, replace=False)).astype(np.int32)
+    cloud = D.Cloud(gpu_ctx, p, indices=idx, id_base=1000)
+    gd = cloud.estimate_normals(k=12, copy_out=True)
+    cloud.close()
+    ref = D.estimate_normals(p[idx], k=12, ctx=gpu_ctx)
+    assert np.array_equal(gd.view(np.uint32), ref.view(np.uint32))
 
 
 @pytest.mark.gpu
@@ -294,11 +317,9 @@ def test_gpu_c5_full_size_properties(gpu_ctx):
     import dialog_amd as D
     from dialog_amd.synth import SEED_BASE, plane_cloud
     p, _, _ = plane_cloud(10_000_000, 20, seed=SEED_BASE + 5)
-    nrm = D.estimate_normals(p, k=20, ctx=gpu_ctx)
-    assert np.isfinite(nrm).all()
-    # spot-check the normals against the oracle's kNN restatement on a sub-cloud's own kNN
     cloud = D.Cloud(gpu_ctx, p)
-    cloud.set_normals(nrm)
+    nrm = cloud.estimate_normals(k=20, copy_out=True)  # (device-resident: attached on the GPU)
+    assert np.isfinite(nrm).all()
     prm = D.make_params(0.02, max_iterations=4095, probability=1.0, refit_mode=D.DLG_REFIT_FAST,
                         hypotheses_per_launch=4096, model=D.SACMODEL_NORMAL_PLANE,
                         normal_distance_weight=0.1)

@@ -1,0 +1,14 @@
+set -u
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${TAG:-r03k}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 60 ./tools/ubench_lat > $O/ubench.txt 2>&1; cat $O/ubench.txt
+timeout -k 10 400 python -u -m pytest tests/test_fsum_gpu.py tests/test_pcl_refit_gpu.py tests/test_normal_plane.py -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/fs_walk_stats.py 4 $O/ws.json > $O/ws.txt 2>&1
+rc=$?; echo "ws rc=$rc"; cat $O/ws.txt | head -44
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench rc=$rc"; tail -c 1500 $O/bench.json
