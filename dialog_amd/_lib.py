@@ -30,7 +30,7 @@ SYMBOLS = [
     "dlg_sac_control_destroy", "dlg_sac_control_next", "dlg_sac_control_consume",
     "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
     "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex", "dlg_cloud_drop_spatial",
-    "dlg_abi_struct_size", "dlg_float_sums", "dlg_cloud_estimate_normals",
+    "dlg_abi_struct_size", "dlg_float_sums", "dlg_cloud_estimate_normals", "dlg_plane_border",
 ]
 
 # context options (include/dialog_ransac.h): equivalent execution paths, identical results
@@ -151,6 +151,8 @@ def load():
     L.dlg_cloud_set_normals.argtypes = [vp, vp, fp, C.c_int64, C.c_int64]
     L.dlg_cloud_estimate_normals.argtypes = [vp, vp, C.c_float, C.c_int, fp, C.c_int, fp,
                                              C.c_int64]
+    L.dlg_plane_border.argtypes = [C.POINTER(Points), fp, C.c_float, fp, C.c_int64, C.c_int64,
+                                   i64p]
     L.dlg_estimate_normals.argtypes = [vp, C.POINTER(Points), C.c_float, C.c_int, fp, fp, C.c_int64]
     L.dlg_estimate_normals_ex.argtypes = [vp, C.POINTER(Points), C.c_float, C.c_int, fp, fp,
                                           C.c_int64, C.c_int]

@@ -68,6 +68,23 @@ class _PlaneArrays:
                              12, self.boff.ctypes.data_as(C.POINTER(C.c_int64)))
 
 
+def plane_border(points, normal, alpha: float = 0.5) -> np.ndarray:
+    """polyPointCloud (PlaneDetect.h:1376-1440) for one plane: its points projected on their
+    least-squares plane, then a closed concave border of projected points oriented by `normal`
+    (dlg_plane_border; the reference's qhull ConcaveHull is absent: parity unpinned) -> float32
+    [B, 3] (B = 0: fewer than 3 points).  alpha: alpha_poly (config.txt: 0.5)."""
+    a = np.ascontiguousarray(_xyz(points), np.float32)
+    pts = _lib.Points(_f32p(a), a.shape[0], 12)
+    pn = np.ascontiguousarray(normal, np.float32)[:3]
+    L = _lib.load()
+    n = C.c_int64()
+    cap = max(a.shape[0], 16)
+    out = np.zeros((cap, 3), np.float32)
+    _lib.check(L.dlg_plane_border(C.byref(pts), _f32p(pn), float(alpha), _f32p(out), 12, cap,
+                                  C.byref(n)))
+    return out[:n.value].copy()
+
+
 def refit_planes(planes):
     """PlaneDetect.h:1477-1498: computePointNormal of each plane's points, oriented like its
     previous normal -> float32 [P, 4]."""

@@ -276,6 +276,22 @@ typedef struct {
   uint32_t rand_seed;        /* the srand(time(0)) value isPointInPoly reseeds rand() with */
 } dlg_postprocess_params;
 
+/* polyPlanes() -> polyPointCloud() (PlaneDetect.h:1358-1440) for one plane, so the four-file
+ * polygon hand-off (PCLViewer.cpp:1341-1396) can run from RANSAC output alone: the plane's points
+ * (its points_set) projected onto their least-squares plane (pcl::computePointNormal, PCL float
+ * arithmetic) as projPoint2Plane does, then a concave border.  The reference takes polygons[0] of
+ * pcl::ConcaveHull (qhull alpha shape, alpha = alpha_poly, config.txt:28); qhull is absent here,
+ * so the border is the outer boundary of the projected points' alpha occupancy (cells of edge
+ * alpha, the largest 8-connected component, traced once around; per boundary cell its projected
+ * point farthest from the component's centroid): a closed polygon of projected plane points --
+ * the reference's contract, not qhull's facets (parity unpinned).  Orientation as the reference:
+ * reversed when normalize(normalize(p1 - p0) x normalize(p2 - p1)) . pn < 0.  border_out: up to
+ * cap records of out_stride_bytes (>= 12; xyz first); *n_out = vertices (0: fewer than 3 points
+ * or no polygon), also reported with DLG_ERR_CAPACITY.  Host arithmetic; no context. */
+dlg_status dlg_plane_border(const dlg_points* plane_pts, const float pn[3], float alpha,
+                            float* border_out, int64_t out_stride_bytes, int64_t cap,
+                            int64_t* n_out);
+
 /* PlaneDetect.h:1477-1498: coeffs_out[4k..4k+3] = pcl::computePointNormal of plane k's points
  * (float sums in list order, eigen33, d = -n.centroid; NaN with < 3 points), negated when its
  * dot with the previous normal coeffs[4k..4k+2] is < 0.  Host arithmetic (sequential float sums
