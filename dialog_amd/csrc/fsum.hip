@@ -468,155 +468,20 @@ __device__ __forceinline__ bool fs_apply_lean(float t, const FsWalkRec w, float*
   return ok;
 }
 
-// The lemma on integers, for stepping chunk by chunk (sums hovering near zero: many records
-// whose increment depends on the start's low bits, one after another).  The window's records
-// and the carried value are taken as int64 multiples of qmin = 2^(elo - 150), the smallest
-// quantum among the window's guesses and member outputs (exact when every value lies within 37
-// binades of it); a step is then a few scalar integer operations on the stepped lane's fields:
-// the same decisions as fs_apply (grid, member, margin, quantum) and the exact result.
-struct FsIntWin {
-  bool ok;  // (wave-uniform) the window is representable
-  int elo;  // (wave-uniform)
-  int64_t G, O0, O1, O2, O3;  // per lane: g and the member outputs / qmin
-  int32_t M0, M1, M2, M3;     // floor(mu_i / qmin) clamped to 2^31 - 1; -1 for a negative margin
-  int32_t meta;               // sh = log2(q(g) / qmin) | usable_i << 8 + i | qm_i <= 2 q << 12 + i
-};
-
-__device__ __forceinline__ int fs_exp1(float v) {  // max(biased exponent, 1)
-  const int e = (int)((__float_as_uint(v) >> 23) & 0xFFu);
-  return e == 0 ? 1 : e;
-}
-
-__device__ __forceinline__ int64_t fs_to_int(float v, int elo) {
-  const uint32_t b = __float_as_uint(v);
-  const uint32_t e = (b >> 23) & 0xFFu;
-  const int64_t m = (int64_t)((b & 0x7FFFFFu) | (e ? 0x800000u : 0u));
-  const int64_t x = m << ((e ? (int)e : 1) - elo);
-  return (b >> 31) ? -x : x;
-}
-
-__device__ __forceinline__ float fs_from_int(int64_t x, int elo) {
-  return (float)ldexp((double)x, elo - 150);  // (exact: x holds a float's value)
-}
-
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, kWave));
-  return v;
-}
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
-  return v;
-}
-
-__device__ __forceinline__ int32_t fs_mu_int(float mu, int elo) {
-  const double mq = ldexp((double)mu, 150 - elo);
-  return !(mq >= 0.0) ? -1 : mq >= 2147483647.0 ? 2147483647 : (int32_t)floor(mq);
-}
-
-__device__ __forceinline__ FsIntWin fs_int_win(const FsWalkRec w, bool lane_in) {
-  FsIntWin iw;
-  const bool u0 = w.q0 >= 0.0f, u1 = w.q1 >= 0.0f, u2 = w.q2 >= 0.0f, u3 = w.q3 >= 0.0f;
-  int lo = 255, hi = 0;
-  bool fin = true;
-  if (lane_in) {
-    lo = fs_exp1(w.g);
-    hi = lo;
-    fin = lo < 255;
-    auto acc = [&](bool u, float o) {
-      if (!u) return;
-      const int e = fs_exp1(o);
-      lo = min(lo, e);
-      hi = max(hi, e);
-      fin = fin && e < 255;
-    };
-    acc(u0, w.o0);
-    acc(u1, w.o1);
-    acc(u2, w.o2);
-    acc(u3, w.o3);
-  }
-  iw.elo = wave_min_i(lo);
-  const int ehi = wave_max_i(hi);
-  iw.ok = ballot(!fin) == 0 && ehi - iw.elo <= 37;
-  iw.G = fs_to_int(w.g, iw.elo);
-  iw.O0 = u0 ? fs_to_int(w.o0, iw.elo) : 0;
-  iw.O1 = u1 ? fs_to_int(w.o1, iw.elo) : 0;
-  iw.O2 = u2 ? fs_to_int(w.o2, iw.elo) : 0;
-  iw.O3 = u3 ? fs_to_int(w.o3, iw.elo) : 0;
-  iw.M0 = fs_mu_int(w.m0, iw.elo);
-  iw.M1 = fs_mu_int(w.m1, iw.elo);
-  iw.M2 = fs_mu_int(w.m2, iw.elo);
-  iw.M3 = fs_mu_int(w.m3, iw.elo);
-  const float q2 = 2.0f * fs_quantum(w.g);
-  const int sh = fs_exp1(w.g) - iw.elo;
-  iw.meta = (sh & 0xFF) | (u0 << 8) | (u1 << 9) | (u2 << 10) | (u3 << 11) |
-            ((w.q0 <= q2) << 12) | ((w.q1 <= q2) << 13) | ((w.q2 <= q2) << 14) |
-            ((w.q3 <= q2) << 15);
-  return iw;
-}
-
-__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
-  const uint64_t u = (uint64_t)v;
-  return (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l) |
-                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l)
-                    << 32));
-}
-
-// one step of lane f's record on the integer value T (wave-uniform): true and T advanced, or false
-__device__ __forceinline__ bool fs_int_step(const FsIntWin& iw, int f, int64_t* T) {
-  const int meta = __builtin_amdgcn_readlane(iw.meta, f);
-  const int sh = meta & 0xFF;
-  const int64_t t = *T;
-  if ((t & (((int64_t)1 << sh) - 1)) != 0) return false;  // off the record's quantum grid
-  const int64_t D = t - rl64(iw.G, f);
-  const int i = (int)((D >> sh) & 3);
-  const int64_t Dm = D - ((int64_t)i << sh);
-  if (!((meta >> (8 + i)) & 1)) return false;  // member unusable
-  const int64_t Oi = i == 0 ? rl64(iw.O0, f) : i == 1 ? rl64(iw.O1, f) : i == 2 ? rl64(iw.O2, f)
-                                                                           : rl64(iw.O3, f);
-  if (Dm != 0) {
-    if (!((meta >> (12 + i)) & 1)) return false;  // the run's quantum outgrows 2 q(g)
-    const int32_t Mi = i == 0 ? __builtin_amdgcn_readlane(iw.M0, f)
-                     : i == 1 ? __builtin_amdgcn_readlane(iw.M1, f)
-                     : i == 2 ? __builtin_amdgcn_readlane(iw.M2, f)
-                              : __builtin_amdgcn_readlane(iw.M3, f);
-    if (!((Dm < 0 ? -Dm : Dm) <= (int64_t)Mi)) return false;  // outside the margin
-  }
-  *T = Oi + Dm;
-  return true;
-}
-
-// steps lanes f0 .. (until `stop` says so) from the exact value t; returns the next lane
+// steps lanes f, f + 1, ... (until `stop` says so) from the exact value t, each by the full lemma
+// (fs_apply_lean) or a rerun; returns the next lane.  (An integer form of the step, in units of
+// the window's smallest quantum, measured slower on gfx950: its readlanes into scalar registers
+// cost ~50 clocks each.)
 template <class Stop>
 __device__ __forceinline__ int fs_step_lanes(const FsDev& d, int c, int64_t base, int64_t n,
                                              const FsWalkRec wr, int cnt, int f, float* t,
                                              int lane, Stop stop, int64_t* n_step,
                                              int64_t* n_rerun) {
-  const FsIntWin iw = fs_int_win(wr, lane < cnt);
   for (;;) {
-    const int et = fs_exp1(*t);
-    const bool trep = iw.ok && (*t == 0.0f || (et >= iw.elo && et - iw.elo <= 38 &&
-                                              fs_from_int(fs_to_int(*t, iw.elo), iw.elo) == *t));
-    int64_t T = trep ? (*t == 0.0f ? 0 : fs_to_int(*t, iw.elo)) : 0;
-    // integer stepping while it lasts
-    bool ok = trep;
-    while (ok) {
-      ++*n_step;
-      ok = fs_int_step(iw, f, &T);
-      if (!ok) break;
-      ++f;
-      if (f >= cnt || stop(f)) {
-        *t = fs_from_int(T, iw.elo);
-        return f;
-      }
-    }
-    if (trep) *t = fs_from_int(T, iw.elo);
-    // lane f: the full lemma in double (off the integer range), or its rerun
     float o3;
     const bool ok2 = fs_apply_lean(*t, wr, &o3);
-    if (!trep) ++*n_step;
-    if (__builtin_amdgcn_readlane((int)ok2, f)) {
+    ++*n_step;
+    if ((ballot(ok2) >> f) & 1) {  // (a ballot bit: cheaper than a readlane into SALU)
       *t = rdl(o3, f);
     } else {
       ++*n_rerun;
@@ -632,7 +497,7 @@ __device__ __forceinline__ int fs_step_lanes(const FsDev& d, int c, int64_t base
 // registers, kFsRing - 1 windows ahead of the one being walked.  The loads are counted by vmcnt
 // in issue order, so before reading window w the wave waits until at most the 4 (kFsRing - 1)
 // loads of the windows after it are outstanding (a rerun's own loads drain the counter anyway).
-constexpr int kFsStepAll = 6;  // more records needing the full lemma: step through the window
+constexpr int kFsStepAll = 64;  // (step through a whole window: measured slower than speculating)
 constexpr int kFsGroup = 4;   // windows per fast-path pass
 constexpr int kFsRing = 16;   // windows in the ring (four groups)
 constexpr int kFsWinBytes = kWave * (int)sizeof(FsNode);
@@ -731,9 +596,9 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
     // need the full lemma, then speculate again.
     t = f == s ? t : rdl((float)out, f - 1);
     const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
-    const float mu3 = wr.mu3;
+    const uint64_t fastm = ballot(fastrec);
     f = fs_step_lanes(d, c, base, n, wr, cnt, f, &t, lane,
-                      [&](int l) { return rdl(mu3, l) >= 0.0f; }, &ct.step, &ct.rerun);
+                      [&](int l) { return ((fastm >> l) & 1) != 0; }, &ct.step, &ct.rerun);
     if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
     s = f;
   }
@@ -804,11 +669,17 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
     auto fastm = [&](const FsWalkRec& x, int cn) {
       return ballot(lane < cn && !(x.mu3 >= 0.0f)) == 0;
     };
-    if (fastm(w0, c0) && fastm(w1, c1) && fastm(w2, c2) && fastm(w3, c3)) {
+    // the leading windows whose records all take the fast path are verified together (their
+    // starts from the chunk increments' prefixes); the walk goes on window by window from the
+    // first window that fails
+    int jd = 0;
+    {
+      const int nf = !fastm(w0, c0) ? 0 : !fastm(w1, c1) ? 1 : !fastm(w2, c2) ? 2
+                   : !fastm(w3, c3) ? 3 : 4;
       double B = 0.0, prev_out = 0.0;
       bool okg = true;
-      auto win = [&](const FsWalkRec& x, int cn, bool first) {
-        if (cn == 0) return;
+      auto win = [&](const FsWalkRec& x, int cn, int j) {
+        if (cn == 0 || j >= nf || !okg) return;
         const double tl = (double)t + (B + x.P);
         const double tn = dpp_next(tl);
         const bool last = lane == cn - 1;
@@ -816,22 +687,24 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
         const double out = tl + x.d0;
         const bool ver = (double)(float)tl == tl && fabs(tl - x.gd()) <= (double)x.mu3 &&
                          dq == floor(dq) && (double)(float)out == out && (last || out == tn);
-        okg = okg && ballot(lane < cn && !ver) == 0;
-        if (!first) okg = okg && rld(tl, 0) == prev_out;  // (the windows' seam)
+        bool ok = ballot(lane < cn && !ver) == 0;
+        if (j > 0) ok = ok && rld(tl, 0) == prev_out;  // (the windows' seam)
+        if (!ok) {
+          okg = false;
+          return;
+        }
         prev_out = rld(out, cn - 1);
         B = B + rld(x.P + x.d0, cn - 1);
+        jd = j + 1;
       };
-      win(w0, c0, true);
-      win(w1, c1, false);
-      win(w2, c2, false);
-      win(w3, c3, false);
-      if (okg) {
-        ++ct.group_fast;
-        t = (float)prev_out;
-        continue;
-      }
+      win(w0, c0, 0);
+      win(w1, c1, 1);
+      win(w2, c2, 2);
+      win(w3, c3, 3);
+      if (jd > 0) t = (float)prev_out;
+      ct.group_fast += jd;
     }
-    for (int j = 0; j < kFsGroup; ++j) {
+    for (int j = jd; j < kFsGroup; ++j) {
       const int cn = j == 0 ? c0 : j == 1 ? c1 : j == 2 ? c2 : c3;
       if (cn == 0) break;
       FsWalkRec x;  // (field by field: a struct-level select goes through scratch memory)
