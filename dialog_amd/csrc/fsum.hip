@@ -255,12 +255,25 @@ __global__ __launch_bounds__(kFiBS) void k_fs_inc(FsDev d, const double* __restr
   fs_scan_units(d, U, base9, d.b.ticket, scs);
 }
 
-__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const double u = __shfl_up(v, off, kWave);
-    if (lane >= off) v += u;
-  }
+// inclusive prefix sum of a double over the wave, by DPP row shifts and row broadcasts (no LDS
+// instruction: ds_bpermute shuffles cost ~100 clocks each on this path)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ double dpp_dbl(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, kCtrl, kRowMask,
+                                                            0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), kCtrl,
+                                                            kRowMask, 0xF, false);
+  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double wave_incl_scan(double v, int) {
+  v += dpp_dbl<0x111, 0xF>(v);  // row_shr:1 (lanes shifted in from outside the row read 0)
+  v += dpp_dbl<0x112, 0xF>(v);  // row_shr:2
+  v += dpp_dbl<0x114, 0xF>(v);  // row_shr:4
+  v += dpp_dbl<0x118, 0xF>(v);  // row_shr:8
+  v += dpp_dbl<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp_dbl<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
   return v;
 }
 
@@ -563,8 +576,7 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
       const double off = (double)t - (double)rdl(wr.g, s);
       const double cl = act && !fastrec ? fs_increment_rec(wr, off) - wr.d0 : 0.0;
       const double inc = wave_incl_scan(cl, lane);
-      const double up = __shfl_up(inc, 1, kWave);
-      corr = lane == 0 ? 0.0 : up;
+      corr = dpp_dbl<0x138, 0xF>(inc);  // wave_shr:1 (lane 0 reads 0): the exclusive prefix
     }
     const double tl = (double)t + ((wr.P - Ps) + corr);
     // the next lane's speculated start (DPP wave shift: no LDS instruction on this path)
