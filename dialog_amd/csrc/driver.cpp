@@ -334,8 +334,8 @@ void ensure_list_xyz(dlg_ctx* c, dlg_cloud* cl) {
   cl->buf_lean[cl->cur] = false;
 }
 
-void ensure_sel1(dlg_ctx* c, int64_t n) {
-  const size_t nt = (size_t)sel1_tiles(n) + 1;
+void ensure_sel1(dlg_ctx* c, int64_t n, int64_t min_tiles = 0) {
+  const size_t nt = (size_t)std::max<int64_t>(sel1_tiles(n), min_tiles) + 1;
   if (nt > c->sel1_status.cap) {
     c->sel1_status.ensure(nt);
     HIPCHK(hipMemsetAsync(c->sel1_status.p, 0, sizeof(uint64_t) * c->sel1_status.cap, c->stream));
@@ -693,7 +693,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
           cl->ubits.ensure((size_t)nw + 16);
           HIPCHK(hipMemsetAsync(cl->ubits.p, 0, cl->ubits.cap * sizeof(uint32_t), c->stream));
         }
-        ensure_sel1(c, std::max<int64_t>(std::max<int64_t>(src.n, cl->sp_n), nw));
+        ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n), ucompact_tiles(nw));
         c->fs_x.ensure((size_t)std::max<int64_t>(src.n, 1));
         c->fs_y.ensure((size_t)std::max<int64_t>(src.n, 1));
         c->fs_z.ensure((size_t)std::max<int64_t>(src.n, 1));

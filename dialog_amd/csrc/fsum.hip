@@ -55,6 +55,35 @@ __device__ __forceinline__ void fs_acc9(double (&a)[kFsChains], float x, float y
   if constexpr (C + 1 < kFsChains) fs_acc9<C + 1>(a, x, y, z);
 }
 
+// inclusive prefix sum of a double over the wave, by DPP row shifts and row broadcasts (no LDS
+// instruction: ds_bpermute shuffles cost ~100 clocks each on this path)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ double dpp_dbl(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, kCtrl, kRowMask,
+                                                            0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), kCtrl,
+                                                            kRowMask, 0xF, false);
+  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double wave_incl_scan(double v, int) {
+  v += dpp_dbl<0x111, 0xF>(v);  // row_shr:1 (lanes shifted in from outside the row read 0)
+  v += dpp_dbl<0x112, 0xF>(v);  // row_shr:2
+  v += dpp_dbl<0x114, 0xF>(v);  // row_shr:4
+  v += dpp_dbl<0x118, 0xF>(v);  // row_shr:8
+  v += dpp_dbl<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp_dbl<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
+  return v;
+}
+
+__device__ __forceinline__ double rld(double v, int l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return __longlong_as_double((int64_t)(
+      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l) |
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l) << 32)));
+}
+
 // the last workgroup of a unit pass scans the per-unit sums usum into the exclusive prefixes
 // upre (from base9, or 0); ticket = the pass's ticket word
 __device__ void fs_scan_body(const FsDev& d, int64_t U, const double* base9, double* blk,
@@ -75,30 +104,29 @@ __device__ void fs_scan_units(const FsDev& d, int64_t U, const double* base9, un
 }
 
 // upre = exclusive prefixes of usum from base9 (or 0); tot_out non-null: only the totals (and
-// the count n in tot_out[9]) are written
-__device__ void fs_scan_body(const FsDev& d, int64_t U, const double* base9, double* blk,
+// the count n in tot_out[9]) are written.  Wave w scans chains w, w + 4, w + 8, 64 units per
+// DPP wave scan (the prefixes are guesses: any fixed summation order serves).
+__device__ void fs_scan_body(const FsDev& d, int64_t U, const double* base9, double*,
                              double* tot_out) {
-  const int t = threadIdx.x;
-  double run = t < kFsChains && base9 ? base9[t] : 0.0;
-  for (int64_t ub = 0; ub < U; ub += kFsUC) {
-    const int nb = (int)(U - ub < kFsUC ? U - ub : kFsUC);
-    __syncthreads();
-    for (int p = t; p < nb * kFsChains; p += blockDim.x)
-      blk[p] = __longlong_as_double(__hip_atomic_load(
-          reinterpret_cast<const int64_t*>(d.b.usum) + ub * kFsChains + p, __ATOMIC_RELAXED,
-          __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();
-    if (t < kFsChains) {
-      for (int q = 0; q < nb; ++q) {
-        if (!tot_out) d.b.upre[(ub + q) * kFsChains + t] = run;
-        run += blk[q * kFsChains + t];
-      }
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int c = w + 4 * m;
+    if (c >= kFsChains) break;  // (wave-uniform)
+    double run = base9 ? base9[c] : 0.0;
+    for (int64_t ub = 0; ub < U; ub += kWave) {
+      const int64_t uu = ub + l;
+      const double v = uu < U ? __longlong_as_double(__hip_atomic_load(
+                                    reinterpret_cast<const int64_t*>(d.b.usum) + uu * kFsChains + c,
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              : 0.0;
+      const double inc = wave_incl_scan(v, l);
+      if (!tot_out && uu < U) d.b.upre[uu * kFsChains + c] = run + (inc - v);
+      run += rld(inc, kWave - 1);
     }
+    if (tot_out && l == 0) tot_out[c] = run;
   }
-  if (tot_out) {
-    if (t < kFsChains) tot_out[t] = run;
-    if (t == 0) tot_out[kFsChains] = (double)*d.n_dev;
-  }
+  if (tot_out && t == 0) tot_out[kFsChains] = (double)*d.n_dev;
 }
 
 // several ranks: this rank's base = the double totals of the ranks before it (list order), the
@@ -144,14 +172,16 @@ __global__ void k_fs_tail(const float* __restrict__ sums9, const int64_t* __rest
 }
 
 // ---- k_fs_prep --------------------------------------------------------------------------------
+// thread (chunk k, quarter h): the nine double sums of its 16 terms; wave w then adds the four
+// quarters of chains w, w + 4, w + 8 per chunk and reduces them over the unit (DPP)
 constexpr int kFpBS = 256;
 __global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d, const double* __restrict__ base9,
                                                    double* __restrict__ tot_out) {
   __shared__ float sx[kFsUC * kFsPad], sy[kFsUC * kFsPad], sz[kFsUC * kFsPad];
-  __shared__ double scs[kFsUC * kFsChains];
+  __shared__ double sq[4 * kFsChains * kFsUC];  // [quarter][chain][chunk]
   const int64_t n = *d.n_dev;
   const int64_t U = (n + kFsUnit - 1) / kFsUnit;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, k = t & 63, h = t >> 6;
   for (int64_t u = blockIdx.x; u < U; u += gridDim.x) {
     const int64_t e0 = u * kFsUnit;
     const int cnt = (int)(n - e0 < kFsUnit ? n - e0 : kFsUnit);
@@ -163,37 +193,56 @@ __global__ __launch_bounds__(kFpBS) void k_fs_prep(FsDev d, const double* __rest
       sx[li] = d.px[e]; sy[li] = d.py[e]; sz[li] = d.pz[e];
     }
     __syncthreads();
-    if (t < nch) {  // thread = chunk: the nine double sums together
+    {
       double a[kFsChains] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      const int len = cnt - t * kFsChunk < kFsChunk ? cnt - t * kFsChunk : kFsChunk;
-      for (int j = 0; j < len; ++j) {
-        const int li = t * kFsPad + j;
+      const int j0 = k * kFsChunk + h * (kFsChunk / 4);
+      int len = cnt - j0 < kFsChunk / 4 ? cnt - j0 : kFsChunk / 4;
+      if (len < 0) len = 0;
+      for (int i = 0; i < len; ++i) {
+        const int li = k * kFsPad + h * (kFsChunk / 4) + i;
         fs_acc9<0>(a, sx[li], sy[li], sz[li]);
       }
 #pragma unroll
-      for (int c = 0; c < kFsChains; ++c) {
-        scs[t * kFsChains + c] = a[c];
-        d.b.csum[(u * kFsUC + t) * kFsChains + c] = a[c];
-      }
+      for (int c = 0; c < kFsChains; ++c) sq[(h * kFsChains + c) * kFsUC + k] = a[c];
     }
     __syncthreads();
-    if (t < kFsChains) {
-      double s = 0.0;
-      for (int k = 0; k < nch; ++k) s += scs[k * kFsChains + t];
-      __hip_atomic_store(reinterpret_cast<int64_t*>(d.b.usum) + u * kFsChains + t,
-                         __double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int c = h + 4 * m;
+      if (c >= kFsChains) break;  // (wave-uniform)
+      const double v = ((sq[c * kFsUC + k] + sq[(kFsChains + c) * kFsUC + k]) +
+                        sq[(2 * kFsChains + c) * kFsUC + k]) +
+                       sq[(3 * kFsChains + c) * kFsUC + k];
+      if (k < nch) d.b.csum[(u * kFsUC + k) * kFsChains + c] = v;
+      const double s = wave_incl_scan(k < nch ? v : 0.0, k);
+      if (k == kWave - 1)
+        __hip_atomic_store(reinterpret_cast<int64_t*>(d.b.usum) + u * kFsChains + c,
+                           __double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // the last workgroup scans the unit sums (agent-scope stores acknowledged before the ticket,
   // read back with agent-scope loads: k_moments' pattern); with tot_out (several ranks) it only
   // totals them -- the scan waits for the other ranks' totals (k_fs_base)
-  fs_scan_units(d, U, base9, d.b.ticket, scs, tot_out);
+  fs_scan_units(d, U, base9, d.b.ticket, nullptr, tot_out);
 }
 
 // ---- k_fs_inc ---------------------------------------------------------------------------------
 // in place: csum (chunk double sums) -> the chunks' float increments, usum -> their unit sums,
 // upre (double prefixes) -> the increments' prefixes.  Each unit is read and rewritten by one
 // workgroup; the scan runs after every workgroup has passed its ticket.
+// the chunk's float runs of chains CG, CG + 4 (and CG + 8 for CG = 0) from v[], interleaved
+template <int CG>
+__device__ __forceinline__ void fs_inc_run(const float* sx, const float* sy, const float* sz,
+                                           int li0, int len, float (&v)[3]) {
+#pragma unroll 4
+  for (int j = 0; j < len; ++j) {
+    const float x = sx[li0 + j], y = sy[li0 + j], z = sz[li0 + j];
+    v[0] = v[0] + fs_term(CG, x, y, z);
+    v[1] = v[1] + fs_term(CG + 4, x, y, z);
+    if constexpr (CG + 8 < kFsChains) v[2] = v[2] + fs_term(CG + 8, x, y, z);
+  }
+}
+
 constexpr int kFiBS = 256;  // 64 chunks x 4 chain groups (chains g, g + 4, g + 8)
 __global__ __launch_bounds__(kFiBS) void k_fs_inc(FsDev d, const double* __restrict__ base9) {
   __shared__ float sx[kFsUC * kFsPad], sy[kFsUC * kFsPad], sz[kFsUC * kFsPad];
@@ -216,65 +265,42 @@ __global__ __launch_bounds__(kFiBS) void k_fs_inc(FsDev d, const double* __restr
       scs[p] = d.b.csum[u * kFsUC * kFsChains + p];
     if (t < kFsChains) spre[t] = d.b.upre[u * kFsChains + t];
     __syncthreads();
-    double inc[3] = {0.0, 0.0, 0.0};
+    // first guesses at chunk k: the unit's double prefix + the chunks before it (DPP scans of
+    // the sums shifted by one chunk), chains cg, cg + 4, cg + 8
+    float g[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int c = cg + 4 * m < kFsChains ? cg + 4 * m : cg;
+      const double pv = k > 0 && k - 1 < nch ? scs[(k - 1) * kFsChains + c] : 0.0;
+      g[m] = (float)(spre[c] + wave_incl_scan(pv, k));
+    }
+    float v[3] = {g[0], g[1], g[2]};
     if (k < nch) {
       const int len = cnt - k * kFsChunk < kFsChunk ? cnt - k * kFsChunk : kFsChunk;
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        const int c = cg + 4 * m;
-        if (c >= kFsChains) break;
-        double pre = spre[c];
-        for (int q = 0; q < k; ++q) pre += scs[q * kFsChains + c];
-        const float g = (float)pre;
-        float v = g;
-        for (int j = 0; j < len; ++j) {
-          const int li = k * kFsPad + j;
-          v = v + fs_term(c, sx[li], sy[li], sz[li]);
-        }
-        inc[m] = (double)v - (double)g;
+      switch (cg) {  // (wave-uniform: the chains' terms resolved outside the loop)
+        case 0: fs_inc_run<0>(sx, sy, sz, k * kFsPad, len, v); break;
+        case 1: fs_inc_run<1>(sx, sy, sz, k * kFsPad, len, v); break;
+        case 2: fs_inc_run<2>(sx, sy, sz, k * kFsPad, len, v); break;
+        default: fs_inc_run<3>(sx, sy, sz, k * kFsPad, len, v); break;
       }
     }
-    __syncthreads();  // (every thread has read the double sums)
-    if (k < nch) {
 #pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        const int c = cg + 4 * m;
-        if (c >= kFsChains) break;
-        scs[k * kFsChains + c] = inc[m];
-        d.b.csum[(u * kFsUC + k) * kFsChains + c] = inc[m];
-      }
-    }
-    __syncthreads();
-    if (t < kFsChains) {
-      double s = 0.0;
-      for (int q = 0; q < nch; ++q) s += scs[q * kFsChains + t];
-      __hip_atomic_store(reinterpret_cast<int64_t*>(d.b.usum) + u * kFsChains + t,
-                         __double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int m = 0; m < 3; ++m) {
+      const int c = cg + 4 * m;
+      if (c >= kFsChains) break;  // (wave-uniform)
+      const double inc = k < nch ? (double)v[m] - (double)g[m] : 0.0;
+      if (k < nch) d.b.csum[(u * kFsUC + k) * kFsChains + c] = inc;
+      const double s = wave_incl_scan(inc, k);
+      if (k == kWave - 1)
+        __hip_atomic_store(reinterpret_cast<int64_t*>(d.b.usum) + u * kFsChains + c,
+                           __double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  fs_scan_units(d, U, base9, d.b.ticket, scs);
+  fs_scan_units(d, U, base9, d.b.ticket, nullptr);
 }
 
-// inclusive prefix sum of a double over the wave, by DPP row shifts and row broadcasts (no LDS
-// instruction: ds_bpermute shuffles cost ~100 clocks each on this path)
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ double dpp_dbl(double v) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, kCtrl, kRowMask,
-                                                            0xF, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), kCtrl,
-                                                            kRowMask, 0xF, false);
-  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
-}
-
-__device__ __forceinline__ double wave_incl_scan(double v, int) {
-  v += dpp_dbl<0x111, 0xF>(v);  // row_shr:1 (lanes shifted in from outside the row read 0)
-  v += dpp_dbl<0x112, 0xF>(v);  // row_shr:2
-  v += dpp_dbl<0x114, 0xF>(v);  // row_shr:4
-  v += dpp_dbl<0x118, 0xF>(v);  // row_shr:8
-  v += dpp_dbl<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
-  v += dpp_dbl<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
-  return v;
+__device__ __forceinline__ float rdl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
 // ---- k_fs_l1 ----------------------------------------------------------------------------------
@@ -282,7 +308,6 @@ constexpr int kFlBS = kFsUC * kFsFan;  // 64 chunks x 4 members
 __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
   __shared__ float sp[kFsUC * kFsPad];
   __shared__ float4 sn[kFsUC * 4];  // the unit's records, 4 rows of 16 bytes each
-  __shared__ double s_cs[kFsUC];
   __shared__ float sg[kFsUC];
   const int64_t n = *d.n_dev;
   const int64_t U = (n + kFsUnit - 1) / kFsUnit;
@@ -298,13 +323,11 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
       const int64_t e = (e0 + j) * d.stride;
       sp[(j >> 6) * kFsPad + (j & 63)] = fs_term(c, d.px[e], d.py[e], d.pz[e]);
     }
-    if (t < nch) s_cs[t] = d.b.csum[(u * kFsUC + t) * kFsChains + c];
-    __syncthreads();
-    if (t < nch) {
+    if (t < kWave) {
       // the guess at chunk t: fl(prefix of the increments), unit prefix + chunks before it
-      double pre = d.b.upre[u * kFsChains + c];
-      for (int k = 0; k < t; ++k) pre += s_cs[k];
-      sg[t] = (float)pre;
+      const double pv = t > 0 && t - 1 < nch ? d.b.csum[(u * kFsUC + t - 1) * kFsChains + c] : 0.0;
+      const double pre = d.b.upre[u * kFsChains + c] + wave_incl_scan(pv, t);
+      if (t < nch) sg[t] = (float)pre;
     }
     __syncthreads();
     {  // lane (chunk k, member i) runs the chunk from g_k + i q(g_k)
@@ -364,6 +387,33 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
       }
       const double inc = wave_incl_scan(d0, t);
       const double ex = inc - d0;
+      // the window summary (this unit's 64 records: k_fs_walk passes such a window in one step).
+      // Link: member 0's output is the next chunk's guess, bit for bit (past the unit's last
+      // chunk: the walk compares o0_last with the next window's g0).  A start t equal
+      // to the window's first guess then runs through every guess of the window exactly (each
+      // member-0 run is the computation), ending at the last chunk's o0.  A start t = g0 + dl,
+      // dl != 0: every record fast, |dl| <= min mu3 and dl a multiple of every quantum q(g_k)
+      // (the largest) make each start g_k + dl and the end o0_last + dl (the fast path, record
+      // by record, by induction).  Summary: (g0, o0_last, min mu3 or -1 when a record is not
+      // fast, the largest quantum or NaN when a link fails).
+      const float gk = t < nch ? row[0] : 0.0f, o0 = t < nch ? row[4] : 0.0f;
+      bool lk = true;
+      if (t < nch) {
+        const float gn = t + 1 < nch ? reinterpret_cast<const float*>(&sn[(t + 1) * 4])[0] : 0.0f;
+        lk = row[12] >= 0.0f && (t + 1 >= nch || __float_as_uint(o0) == __float_as_uint(gn));
+      }
+      const bool valid = ballot(t < nch && !lk) == 0;
+      const bool fastall = ballot(t < nch && !(mu3 >= 0.0f)) == 0;
+      float mn = t < nch ? mu3 : INFINITY, qx = t < nch ? fs_quantum(gk) : 0.0f;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        mn = fminf(mn, __shfl_xor(mn, off, kWave));
+        qx = fmaxf(qx, __shfl_xor(qx, off, kWave));
+      }
+      const float g0 = rdl(gk, 0), ol = rdl(o0, nch - 1);
+      if (t == 0)
+        d.b.win[c * d.b.wcap + u] =
+            make_float4(g0, ol, fastall ? mn : -1.0f, valid ? qx : __builtin_nanf(""));
       // (exclusive prefix: inc - d0 may round; the walk verifies every speculated start anyway)
       if (t < nch) {
         const uint64_t eb = (uint64_t)__double_as_longlong(ex);
@@ -379,9 +429,6 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
 }
 
 // ---- k_fs_walk --------------------------------------------------------------------------------
-__device__ __forceinline__ float rdl(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -505,14 +552,12 @@ __device__ __forceinline__ int fs_step_lanes(const FsDev& d, int c, int64_t base
   }
 }
 
-// The walk's records stream through an LDS ring of kFsRing windows (4 KB each: 64 records of 64
-// bytes, the global layout): global_load_lds_dwordx4 moves a window with 4 instructions and no
-// registers, kFsRing - 1 windows ahead of the one being walked.  The loads are counted by vmcnt
-// in issue order, so before reading window w the wave waits until at most the 4 (kFsRing - 1)
-// loads of the windows after it are outstanding (a rerun's own loads drain the counter anyway).
+// A window's records (64 records of 64 bytes, the global layout: 4 KB) are moved into LDS by
+// global_load_lds_dwordx4 (4 instructions, no registers); two slots: the window being walked and
+// the next one the summaries cannot skip, prefetched.  The loads are counted by vmcnt in issue
+// order: with the prefetch's 4 loads issued after the current window's, vmcnt(4) waits for the
+// current window (a rerun's own loads drain the counter anyway).
 constexpr int kFsStepAll = 64;  // (step through a whole window: measured slower than speculating)
-constexpr int kFsGroup = 4;   // windows per fast-path pass
-constexpr int kFsRing = 16;   // windows in the ring (four groups)
 constexpr int kFsWinBytes = kWave * (int)sizeof(FsNode);
 
 __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int64_t K,
@@ -523,7 +568,7 @@ __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int6
   const char* src = reinterpret_cast<const char*>(R + w0) + 16 * lane;
   const int64_t lim = K * (int64_t)sizeof(FsNode) - 16 - w0 * (int64_t)sizeof(FsNode);
   // (inline asm: the compiler neither sees these loads nor drains them before its own LDS and
-  // VMEM instructions; fs_ring_wait accounts for them)
+  // VMEM instructions; the walk waits for them explicitly)
   const uint32_t lds = (uint32_t)(uintptr_t)slot;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -531,12 +576,6 @@ __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int6
     const char* p = off <= lim ? src + j * 1024 : reinterpret_cast<const char*>(R + w0);
     asm volatile("global_load_lds_dwordx4 %0, off" : : "v"(p), "{m0}"(lds + j * 1024) : "memory");
   }
-}
-
-__device__ __forceinline__ void fs_ring_wait() {
-  // a group's windows loaded: vmcnt <= 4 (kFsRing - kFsGroup) = 48 (lgkmcnt, expcnt: no wait)
-  static_assert(4 * (kFsRing - kFsGroup) == 48, "ring depth and the s_waitcnt immediate");
-  asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
 }
 
 struct FsWalkCounters {
@@ -617,45 +656,80 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
   return t;
 }
 
-__device__ __forceinline__ double rld(double v, int l) {
-  const uint64_t u = (uint64_t)__double_as_longlong(v);
-  return __longlong_as_double((int64_t)(
-      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l) |
-      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l) << 32)));
-}
-
 constexpr int kFwBS = kWave;
 __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restrict__ start9,
                                                    const float4* __restrict__ cin,
                                                    float4* __restrict__ cout,
                                                    int32_t* __restrict__ res) {
-  __shared__ __attribute__((aligned(16))) char ring[kFsRing * kFsWinBytes];
+  __shared__ __attribute__((aligned(16))) char ring[2 * kFsWinBytes];
   const int c = blockIdx.x, lane = threadIdx.x;
   const int64_t n = *d.n_dev;
   const int64_t K = fs_chunks(n);
+  const int64_t NW = (K + kWave - 1) / kWave;
   const FsNode* R = fs_rec(d.b, c, 0);
+  const float4* S = d.b.win + c * d.b.wcap;
   float t = start9 ? start9[c] : 0.0f;
-  // walk counters (dlg_float_sums' walk_stats): windows walked one by one, speculation passes,
-  // passes with lanes the fast path could not decide, lanes stepped alone, reruns, clocks (all,
-  // stepping), groups passed by the group fast path
+  // walk counters (dlg_float_sums' walk_stats): windows walked record by record, speculation
+  // passes, passes with lanes the fast path could not decide, lanes stepped alone, reruns, clocks
+  // (all, stepping), windows passed by their summaries
   const int64_t clk0 = d.b.wst ? (int64_t)clock64() : 0;
-  auto slot = [&](int64_t w) {
+  auto slot = [&](int j) {
     return (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)ring +
-                                                       (w % kFsRing) * kFsWinBytes);
+                                                       j * kFsWinBytes);
   };
   FsWalkCounters ct;
-  if (K > 0)
-    for (int w = 0; w < kFsRing; ++w) fs_ring_load(R, (int64_t)w * kWave, K, slot(w), lane);
-  for (int64_t w = 0; w * kWave < K; w += kFsGroup) {
-    fs_ring_wait();
-    // the group's records from the ring (inline asm: the compiler would otherwise drain every
-    // outstanding load before an LDS read that may alias an LDS-DMA write), then the slots are
-    // refilled with the windows kFsRing ahead
-    // (named records, no array: a runtime index would put them in scratch memory)
-    auto read_rec = [&](int j, int* cnj) {
+  int64_t pre_w = -1;  // the window prefetched into slot pre_s (or none)
+  int pre_s = 0;
+  for (int64_t wb = 0; wb < NW; wb += kWave) {
+    // the batch's summaries, lane = window; a window is skippable only if its last record also
+    // links to the next window's first guess
+    const int nb = NW - wb < kWave ? (int)(NW - wb) : kWave;
+    float4 sm = make_float4(0.0f, 0.0f, -1.0f, __builtin_nanf(""));
+    float gnx = 0.0f;
+    const bool has_next = wb + lane + 1 < NW;
+    if (lane < nb) sm = S[wb + lane];
+    if (lane < nb && has_next) gnx = S[wb + lane + 1].x;
+    const bool valid = lane < nb && sm.w == sm.w &&
+                       (!has_next || __float_as_uint(sm.y) == __float_as_uint(gnx));
+    const uint64_t stat = ballot(lane < nb && !valid);  // (walked at any lag: prefetch candidates)
+    const double iqx = valid ? 1.0 / (double)sm.w : 0.0;  // (exact: a power of two)
+    int i = 0;
+    while (i < nb) {
+      // windows i.. from the exact value t: lag dl = t - g0_i, the same for every linked window
+      const float g0 = rdl(sm.x, i);
+      const bool zero = __float_as_uint(t) == __float_as_uint(g0);
+      const double dl = (double)t - (double)g0;
+      const double dq = dl * iqx;
+      const bool ok = lane >= i && valid &&
+                      (zero || (fabs(dl) <= (double)sm.z && fabs(dq) < 4503599627370496.0 &&
+                                dq == floor(dq)));
+      const uint64_t nm = ~ballot(ok) & (~0ull << i) & (nb == kWave ? ~0ull : (1ull << nb) - 1);
+      const int f = nm ? (int)__builtin_ctzll(nm) : nb;
+      if (f > i) {
+        const float ol = rdl(sm.y, f - 1);
+        t = zero ? ol : (float)((double)ol + dl);  // (exact: the lemma, record by record)
+        ct.group_fast += f - i;
+      }
+      if (f >= nb) break;
+      // window f record by record
+      const int64_t w = wb + f;
+      const int cur = pre_w == w ? pre_s : pre_s ^ 1;
+      if (pre_w != w) fs_ring_load(R, w * kWave, K, slot(cur), lane);
+      // prefetch the next window the summaries cannot skip at any lag
+      const uint64_t nx = f + 1 < kWave ? stat & (~0ull << (f + 1)) : 0ull;
+      pre_w = nx ? wb + (int64_t)__builtin_ctzll(nx) : -1;
+      pre_s = cur ^ 1;
+      if (pre_w >= 0) {
+        fs_ring_load(R, pre_w * kWave, K, slot(pre_s), lane);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       f32x4 r0, r1, r2, r3;
       const uint32_t la = (uint32_t)(uintptr_t)(
-          (__attribute__((address_space(3))) char*)slot(w + j) + sizeof(FsNode) * lane);
+          (__attribute__((address_space(3))) char*)slot(cur) + sizeof(FsNode) * lane);
+      // (inline asm: the compiler would otherwise drain every outstanding load before an LDS
+      // read that may alias an LDS-DMA write)
       asm volatile(
           "ds_read_b128 %0, %4\n\t"
           "ds_read_b128 %1, %4 offset:16\n\t"
@@ -665,70 +739,13 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
           : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
           : "v"(la)
           : "memory");
-      const int64_t b0 = (w + j) * kWave;
-      *cnj = b0 >= K ? 0 : K - b0 < kWave ? (int)(K - b0) : kWave;
-      return fs_walk_rec(r0, r1, r2, r3);
-    };
-    static_assert(kFsGroup == 4, "four named records");
-    int c0, c1, c2, c3;
-    const FsWalkRec w0 = read_rec(0, &c0), w1 = read_rec(1, &c1), w2 = read_rec(2, &c2),
-                    w3 = read_rec(3, &c3);
-#pragma unroll
-    for (int j = 0; j < kFsGroup; ++j)
-      fs_ring_load(R, (w + j + kFsRing) * kWave, K, slot(w + j), lane);
-    // group fast path: every record fast, the four windows' starts from the chunk increments'
-    // prefixes, all verified at once (else window by window)
-    auto fastm = [&](const FsWalkRec& x, int cn) {
-      return ballot(lane < cn && !(x.mu3 >= 0.0f)) == 0;
-    };
-    // the leading windows whose records all take the fast path are verified together (their
-    // starts from the chunk increments' prefixes); the walk goes on window by window from the
-    // first window that fails
-    int jd = 0;
-    {
-      const int nf = !fastm(w0, c0) ? 0 : !fastm(w1, c1) ? 1 : !fastm(w2, c2) ? 2
-                   : !fastm(w3, c3) ? 3 : 4;
-      double B = 0.0, prev_out = 0.0;
-      bool okg = true;
-      auto win = [&](const FsWalkRec& x, int cn, int j) {
-        if (cn == 0 || j >= nf || !okg) return;
-        const double tl = (double)t + (B + x.P);
-        const double tn = dpp_next(tl);
-        const bool last = lane == cn - 1;
-        const double dq = tl * x.iq();
-        const double out = tl + x.d0;
-        const bool ver = (double)(float)tl == tl && fabs(tl - x.gd()) <= (double)x.mu3 &&
-                         dq == floor(dq) && (double)(float)out == out && (last || out == tn);
-        bool ok = ballot(lane < cn && !ver) == 0;
-        if (j > 0) ok = ok && rld(tl, 0) == prev_out;  // (the windows' seam)
-        if (!ok) {
-          okg = false;
-          return;
-        }
-        prev_out = rld(out, cn - 1);
-        B = B + rld(x.P + x.d0, cn - 1);
-        jd = j + 1;
-      };
-      win(w0, c0, 0);
-      win(w1, c1, 1);
-      win(w2, c2, 2);
-      win(w3, c3, 3);
-      if (jd > 0) t = (float)prev_out;
-      ct.group_fast += jd;
-    }
-    for (int j = jd; j < kFsGroup; ++j) {
-      const int cn = j == 0 ? c0 : j == 1 ? c1 : j == 2 ? c2 : c3;
-      if (cn == 0) break;
-      FsWalkRec x;  // (field by field: a struct-level select goes through scratch memory)
-#define DLG_SEL(f) x.f = j == 0 ? w0.f : j == 1 ? w1.f : j == 2 ? w2.f : w3.f
-      DLG_SEL(g); DLG_SEL(mu3); DLG_SEL(o0); DLG_SEL(o1); DLG_SEL(o2); DLG_SEL(o3);
-      DLG_SEL(m0); DLG_SEL(m1); DLG_SEL(m2); DLG_SEL(m3); DLG_SEL(q0); DLG_SEL(q1);
-      DLG_SEL(q2); DLG_SEL(q3); DLG_SEL(d0); DLG_SEL(P);
-#undef DLG_SEL
-      t = fs_walk_window(d, c, (w + j) * kWave, n, x, cn, t, lane, ct);
+      const int64_t b0 = w * kWave;
+      const int cn = K - b0 < kWave ? (int)(K - b0) : kWave;
+      t = fs_walk_window(d, c, b0, n, fs_walk_rec(r0, r1, r2, r3), cn, t, lane, ct);
+      i = f + 1;
     }
   }
-  __builtin_amdgcn_s_waitcnt(0);  // (the ring's last loads: never read, but drained)
+  __builtin_amdgcn_s_waitcnt(0);  // (a last prefetch: never read, but drained)
   if (d.b.wst && lane == 0) {
     int64_t* w = d.b.wst + 8 * c;
     w[0] = ct.win; w[1] = ct.pass; w[2] = ct.slow; w[3] = ct.step; w[4] = ct.rerun;
@@ -769,7 +786,8 @@ size_t fs_scratch_bytes(int64_t n_cap, int world) {
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t K = fs_chunks(nc), U = (K + kFsUC - 1) / kFsUC;
   return align256(sizeof(double) * K * kFsChains) + 2 * align256(sizeof(double) * U * kFsChains) +
-         align256(sizeof(FsNode) * K * kFsChains) + align256(sizeof(float) * 32) +
+         align256(sizeof(FsNode) * K * kFsChains) + align256(sizeof(float4) * U * kFsChains) +
+         align256(sizeof(float) * 32) +
          align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) + 256;
 }
 
@@ -787,6 +805,9 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   b.rec = reinterpret_cast<FsNode*>(p);
   b.cap = K;
   p += align256(sizeof(FsNode) * K * kFsChains);
+  b.win = reinterpret_cast<float4*>(p);
+  b.wcap = U;
+  p += align256(sizeof(float4) * U * kFsChains);
   b.sums = reinterpret_cast<float*>(p);      // [0..8] end values, [16..24] the received starts
   b.start9 = b.sums + 16;
   p += align256(sizeof(float) * 32);

@@ -1155,11 +1155,17 @@ __global__ __launch_bounds__(kMoBS) void k_ustamp(PointsView src, const float4* 
 }
 
 // k_ucompact: bitmap -> the inliers' x, y, z in ascending pristine order (= list order), a
-// single pass with decoupled look-back (sel1_scan); each lane owns 16 consecutive words (4 x 16 B
-// loads), clears them, and writes its inliers from its exclusive rank on.  The last tile writes
-// the count to *n_out.
+// single pass with decoupled look-back (sel1_scan); each lane owns 2 consecutive words (64
+// points), clears them and ranks its inliers.  The gather is cooperative: the wave walks its 64
+// lanes' words in order, lane i taking point i of each (coalesced, masked 4-byte loads and
+// stores; four words in flight), so dense runs and sparse scatter cost the same.  The last tile
+// writes the count to *n_out.
 constexpr int kUcBS = 256;
-constexpr int kUcWords = 16;  // words per lane
+constexpr int kUcWords = 2;  // words per lane
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+}
 __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits, int64_t nwords,
                                                     PointsView pristine, Sel1State L, int ntiles,
                                                     float* __restrict__ ox, float* __restrict__ oy,
@@ -1170,26 +1176,17 @@ __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits,
   const int tile = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int64_t w0 = ((int64_t)tile * kUcBS + threadIdx.x) * kUcWords;
-  uint32_t word[kUcWords];
+  uint64_t m = 0;
   if (w0 + kUcWords <= nwords) {
-    uint4* p = reinterpret_cast<uint4*>(bits + w0);
-#pragma unroll
-    for (int q = 0; q < kUcWords / 4; ++q) {
-      const uint4 v = p[q];
-      word[4 * q] = v.x; word[4 * q + 1] = v.y; word[4 * q + 2] = v.z; word[4 * q + 3] = v.w;
-    }
-#pragma unroll
-    for (int q = 0; q < kUcWords / 4; ++q) p[q] = make_uint4(0u, 0u, 0u, 0u);
-  } else {
-#pragma unroll
-    for (int j = 0; j < kUcWords; ++j) {
-      word[j] = w0 + j < nwords ? bits[w0 + j] : 0u;
-      if (w0 + j < nwords) bits[w0 + j] = 0u;
-    }
+    uint2* p = reinterpret_cast<uint2*>(bits + w0);
+    const uint2 v = *p;
+    m = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    *p = make_uint2(0u, 0u);
+  } else if (w0 < nwords) {  // (the bitmap's last word)
+    m = bits[w0];
+    bits[w0] = 0u;
   }
-  int cnt = 0;
-#pragma unroll
-  for (int j = 0; j < kUcWords; ++j) cnt += __popc(word[j]);
+  const int cnt = __popcll(m);
   int incl = cnt;
 #pragma unroll
   for (int off = 1; off < kWave; off <<= 1) {
@@ -1202,18 +1199,36 @@ __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits,
   if (lane == kWave - 1) s_cnt[w] = incl;
   const int excl = sel1_scan<kUcBS>(L, tile, s_cnt, s_pre, s_base);
   if (excl < 0) return;  // (look-back failed: *L.err is set; the words are cleared already)
-  int64_t pos = (int64_t)excl + s_pre[w] + (incl - cnt);
+  const int pos = excl + s_pre[w] + (incl - cnt);  // this lane's first output slot
+  const int64_t wbase = ((int64_t)tile * kUcBS + w * kWave) * kUcWords * 32;  // the wave's point 0
+  const uint32_t below_lo = lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu;
+  const uint32_t below_hi = lane < 32 ? 0u : (lane == 32 ? 0u : (1u << (lane - 32)) - 1u);
+  for (int s0 = 0; s0 < kWave; s0 += 4) {
+    uint64_t mk[4];
+    int ps[4];
 #pragma unroll
-  for (int j = 0; j < kUcWords; ++j) {
-    uint32_t m = word[j];
-    while (m) {
-      const int b = __ffs(m) - 1;
-      m &= m - 1;
-      const int64_t pi = (w0 + j) * 32 + b;
-      ox[pos] = pristine.x[pi];
-      oy[pos] = pristine.y[pi];
-      oz[pos] = pristine.z[pi];
-      ++pos;
+    for (int k = 0; k < 4; ++k) {
+      mk[k] = readlane64(m, s0 + k);
+      ps[k] = __builtin_amdgcn_readlane(pos, s0 + k);
+    }
+    if ((mk[0] | mk[1] | mk[2] | mk[3]) == 0) continue;  // (wave-uniform)
+    float x[4], y[4], z[4];
+    bool on[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      on[k] = ((mk[k] >> lane) & 1u) != 0;
+      if (on[k]) {
+        const int64_t pi = wbase + (int64_t)(s0 + k) * 64 + lane;
+        x[k] = pristine.x[pi]; y[k] = pristine.y[pi]; z[k] = pristine.z[pi];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (on[k]) {
+        const int o = ps[k] + __popc((uint32_t)mk[k] & below_lo) +
+                      __popc((uint32_t)(mk[k] >> 32) & below_hi);
+        ox[o] = x[k]; oy[o] = y[k]; oz[o] = z[k];
+      }
     }
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) *n_out = excl + s_base[1];

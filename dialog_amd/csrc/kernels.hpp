@@ -208,6 +208,8 @@ struct FsBuffers {
   double* upre = nullptr;  // [units][9] exclusive prefixes
   FsNode* rec = nullptr;   // chunk records, chain-major: rec[c * cap + k]
   int64_t cap = 0;         // chunks per chain
+  float4* win = nullptr;   // window summaries (64 records each), chain-major: win[c * wcap + w]
+  int64_t wcap = 0;        // windows per chain
   float* sums = nullptr;   // [9] the chains' end values
   float* start9 = nullptr; // [9] several ranks: the chains' values at this rank's first inlier
   double* tot = nullptr;   // [10] several ranks: this rank's double term sums + inlier count
