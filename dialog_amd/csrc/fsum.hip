@@ -557,7 +557,9 @@ __device__ __forceinline__ int fs_step_lanes(const FsDev& d, int c, int64_t base
 // the next one the summaries cannot skip, prefetched.  The loads are counted by vmcnt in issue
 // order: with the prefetch's 4 loads issued after the current window's, vmcnt(4) waits for the
 // current window (a rerun's own loads drain the counter anyway).
-constexpr int kFsStepAll = 64;  // (step through a whole window: measured slower than speculating)
+constexpr int kFsSpecIter = 2;  // rounds of member choice per speculation pass
+constexpr bool kFsSeq = true;   // after a failed pass: integer stepping (fs_seq_window) ...
+constexpr int kFsSeqMin = 4;    // ... in windows with more records than this that are not fast
 constexpr int kFsWinBytes = kWave * (int)sizeof(FsNode);
 
 __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int64_t K,
@@ -582,6 +584,148 @@ struct FsWalkCounters {
   int64_t win = 0, pass = 0, slow = 0, step = 0, rerun = 0, clk_step = 0, group_fast = 0;
 };
 
+// float minimum over the wave by DPP (lane 63 ends with it; no LDS instruction)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ float dpp_min_step(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v),
+                                                              kCtrl, kRowMask, 0xF, false));
+  return fminf(v, o);
+}
+__device__ __forceinline__ float wave_min(float v) {
+  v = dpp_min_step<0x111, 0xF>(v);
+  v = dpp_min_step<0x112, 0xF>(v);
+  v = dpp_min_step<0x114, 0xF>(v);
+  v = dpp_min_step<0x118, 0xF>(v);
+  v = dpp_min_step<0x142, 0xA>(v);
+  v = dpp_min_step<0x143, 0xC>(v);
+  return rdl(v, kWave - 1);
+}
+
+// Exact stepping in integers, lanes f..cnt-1 of a window from the exact value t at lane f.
+// Every value involved (the guesses, the usable members' outputs, the chain's values where a
+// record covers them) is a multiple of Q, the window's smallest quantum of a nonzero guess or
+// output, so the chain is followed as its lead over the guesses, L_k = (t_k - g_k) / Q, an int:
+// record k applied to t_k = g_k + L_k Q selects member i = (L_k >> s_k) & 3 (q(g_k) = 2^s_k Q),
+// and when the lemma covers that start (fs_apply: on the grid, member usable, D = L_k - i 2^s_k
+// zero, or within the margin with the member's quanta <= 2 q(g_k)) the next lead is
+// L_{k+1} = L_k + E_k[i], E_k[i] = (o_i - i q(g_k) - g_{k+1}) / Q.  One step is a few integer
+// operations and a DPP lane shift (|E| < 2^20, |L| < 2^30: 24-bit multiplies, no overflow); the
+// coverage is checked for all lanes afterwards, the first uncovered lane is rerun from its exact
+// start g_u + L_u Q and the stepping resumes after it.  Returns the value after the window.
+__device__ __forceinline__ float fs_seq_window(const FsDev& d, int c, int64_t base, int64_t n,
+                                               const FsWalkRec wr, int cnt, int f, float t,
+                                               int lane, FsWalkCounters& ct) {
+  const bool act = lane < cnt;
+  const bool u0 = wr.q0 >= 0.0f, u1 = wr.q1 >= 0.0f, u2 = wr.q2 >= 0.0f, u3 = wr.q3 >= 0.0f;
+  float qv = INFINITY;
+  auto qmin = [&](float v, bool use) {
+    if (use && v != 0.0f) qv = fminf(qv, fs_quantum(v));  // (NaN quanta of non-finite values: ignored)
+  };
+  if (act) {
+    qmin(wr.g, true);
+    qmin(wr.o0, u0); qmin(wr.o1, u1); qmin(wr.o2, u2); qmin(wr.o3, u3);
+  }
+  float Qf = wave_min(qv);
+  if (!(Qf < INFINITY)) Qf = 1.40129846e-45f;  // (every value zero)
+  const double Q = (double)Qf, iQ = 1.0 / Q;  // (exact: powers of two)
+  const float qk = fs_quantum(wr.g);
+  // s = log2(q(g_k) / Q); a lane whose quantum is below Q (a zero guess) or not finite only takes
+  // its exact start (L = 0, member 0)
+  const bool gfin = fabsf(wr.g) <= 3.40282347e+38f;
+  // (log2 of a power of two from its bits: exponent field, or the bit position when subnormal)
+  auto lg2 = [](float p) {
+    const uint32_t b = __float_as_uint(p), e = (b >> 23) & 0xFFu;
+    return e ? (int)e - 127 : (int)__builtin_ctz(b | 0x80000000u) - 149;
+  };
+  int sh = lg2(qk) - lg2(Qf);
+  const bool exact_only = !gfin || !(qk >= Qf);
+  if (exact_only || sh < 0) sh = 0;
+  if (sh > 30) sh = 30;
+  // E_k[i] (0 past the window's last lane: its end value is taken from the member directly)
+  const float gn = __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(wr.g), 0x130, 0xF, 0xF, false));  // g_{k+1}
+  const bool lastl = lane == cnt - 1;
+  auto emem = [&](float o, int i, bool u, bool* ok) {
+    if (lastl) {
+      *ok = u;
+      return 0;
+    }
+    // (o - g_{k+1}, both multiples of Q, is exact below 2^52 Q; the bound keeps it exact)
+    const double dd = (double)o - (double)gn;
+    const double e = (dd - (double)i * (double)qk) * iQ;
+    *ok = u && fabs(dd * iQ) < 1099511627776.0 && fabs(e) < 1048576.0 && e == floor(e);
+    return *ok ? (int)e : 0;
+  };
+  bool k0, k1, k2, k3;
+  const int E0 = emem(wr.o0, 0, u0, &k0), E1 = emem(wr.o1, 1, u1, &k1),
+            E2 = emem(wr.o2, 2, u2, &k2), E3 = emem(wr.o3, 3, u3, &k3);
+  // (a lane taking only its exact start steps with E0 whatever the lead's bits)
+  const int F1 = exact_only ? E0 : E1, F2 = exact_only ? E0 : E2, F3 = exact_only ? E0 : E3;
+  auto marg = [&](float mu) {  // floor(mu / Q), saturated; -1: no shift tolerated
+    const double m = floor((double)mu * iQ);
+    return m >= 0.0 ? (int64_t)fmin(m, 1073741824.0) : (int64_t)-1;
+  };
+  const int64_t M0 = marg(wr.m0), M1 = marg(wr.m1), M2 = marg(wr.m2), M3 = marg(wr.m3);
+  const double q2 = 2.0 * (double)qk;
+  const bool c0 = (double)wr.q0 <= q2, c1 = (double)wr.q1 <= q2, c2 = (double)wr.q2 <= q2,
+             c3 = (double)wr.q3 <= q2;
+  while (f < cnt) {
+    // the start's lead: t - g_f with its rounding error (TwoSum: the lead must be exact)
+    const double ta = (double)t, gb = -(double)rdl(wr.g, f);
+    const double sd = ta + gb, bv = sd - ta;
+    const double er = (ta - (sd - bv)) + (gb - bv);
+    const double Ld = sd * iQ;
+    if (!(fabs(Ld) < 1073741824.0) || Ld != floor(Ld) || er != 0.0) {
+      // (the start is off the window's grid or far from the guess: no record covers it)
+      ++ct.rerun;
+      t = fs_rerun(d, c, base + f, n, t, lane);
+      ++f;
+      continue;
+    }
+    int cur = (int)Ld, keep = 0;
+#pragma unroll 2
+    for (int j = f; j < cnt; ++j) {
+      keep = lane == j ? cur : keep;
+      // the member's bits as all-ones / zero masks (signed bit-field extracts), the increment
+      // picked by bit-field inserts
+      const unsigned m0 = (unsigned)__builtin_amdgcn_sbfe(cur, sh, 1);
+      const unsigned m1 = (unsigned)__builtin_amdgcn_sbfe(cur, sh + 1, 1);
+      const unsigned lo = (m0 & (unsigned)F1) | (~m0 & (unsigned)E0);
+      const unsigned hi = (m0 & (unsigned)F3) | (~m0 & (unsigned)F2);
+      const int e = (int)((m1 & hi) | (~m1 & lo));
+      cur = __builtin_amdgcn_update_dpp(cur, cur + e, 0x138, 0xF, 0xF, false);  // wave_shr:1
+    }
+    ct.step += cnt - f;
+    // coverage of every lane's start (fs_apply's decisions on the integer lead)
+    const int64_t L = keep;
+    const bool grid = (L & ((1ll << sh) - 1)) == 0;
+    const int i = (int)((L >> sh) & 3);
+    const int64_t D = L - ((int64_t)i << sh);
+    const bool b1 = (i & 2) != 0, b0 = (i & 1) != 0;
+    const bool ki = b1 ? (b0 ? k3 : k2) : (b0 ? k1 : k0);
+    const bool ci = b1 ? (b0 ? c3 : c2) : (b0 ? c1 : c0);
+    const int64_t Mi = b1 ? (b0 ? M3 : M2) : (b0 ? M1 : M0);
+    bool cov = gfin && (L < 1073741824 && L > -1073741824) && grid && ki &&
+               (D == 0 || (ci && (D < 0 ? -D : D) <= Mi));
+    if (exact_only) cov = gfin && L == 0 && k0;
+    const uint64_t bad = ballot(act && lane >= f && !cov);
+    if (bad == 0) {
+      const float oi = b1 ? (b0 ? wr.o3 : wr.o2) : (b0 ? wr.o1 : wr.o0);
+      const float out = (float)((double)oi + (double)D * Q);  // (exact: the lemma)
+      t = rdl(out, cnt - 1);
+      break;
+    }
+    const int u = (int)__builtin_ctzll(bad);
+    // lane u's exact start (a float: g_u + L_u Q is the chain's value), rerun
+    const float tu = (float)((double)rdl(wr.g, u) +
+                             (double)__builtin_amdgcn_readlane((int)keep, u) * Q);
+    ++ct.rerun;
+    t = fs_rerun(d, c, base + u, n, tu, lane);
+    f = u + 1;
+  }
+  return t;
+}
+
 // one window's walk from the exact value t: speculation passes (fast path, the full lemma where
 // it does not decide), lanes stepped alone from the first failed one; returns the value after the
 // window's last chunk
@@ -590,6 +734,10 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
                                                 FsWalkCounters& ct) {
   const bool fastrec = wr.mu3 >= 0.0f;
   ++ct.win;
+  // many records whose increment depends on the start (a sum hovering near zero): after a failed
+  // speculation pass the rest of the window is stepped in integers; with few, speculating again
+  // after the failed lane is cheaper
+  const bool seq = kFsSeq && __builtin_popcountll(ballot(lane < cnt && !fastrec)) > kFsSeqMin;
   int s = 0;
   while (s < cnt) {
     ++ct.pass;
@@ -602,22 +750,23 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
     // increment depends on its start (its member chosen by the walk's lead on the guesses at s)
     double corr = 0.0;
     const uint64_t slowm = ballot(act && !fastrec);
-    if (__builtin_popcountll(slowm) > kFsStepAll) {
-      // many chunks whose increment depends on the start's low bits (a sum hovering near zero):
-      // speculation would fail at most of them, so the window is stepped through
-      const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
-      fs_step_lanes(d, c, base, n, wr, cnt, s, &t, lane, [](int) { return false; }, &ct.step,
-                    &ct.rerun);
-      if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
-      break;
-    }
+    const double tb = (double)t + (wr.P - Ps);  // (the member-0 increments alone)
     if (slowm) {
-      const double off = (double)t - (double)rdl(wr.g, s);
-      const double cl = act && !fastrec ? fs_increment_rec(wr, off) - wr.d0 : 0.0;
-      const double inc = wave_incl_scan(cl, lane);
-      corr = dpp_dbl<0x138, 0xF>(inc);  // wave_shr:1 (lane 0 reads 0): the exclusive prefix
+      // the records whose increment depends on the start (member i = lead / q mod 4): each
+      // lane's lead over its guess from the speculated start, the corrections' prefix from the
+      // members those leads select, repeated while a lead changes (every round settles at least
+      // the first lane whose member changed: a sum hovering near zero has many such records)
+      double off = tb - wr.gd();
+      for (int it = 0; it < kFsSpecIter; ++it) {
+        const double cl = act && !fastrec ? fs_increment_rec(wr, off) - wr.d0 : 0.0;
+        const double inc = wave_incl_scan(cl, lane);
+        corr = dpp_dbl<0x138, 0xF>(inc);  // wave_shr:1 (lane 0 reads 0): the exclusive prefix
+        const double on = (tb + corr) - wr.gd();
+        if (ballot(act && !fastrec && !(on == off)) == 0) break;
+        off = on;
+      }
     }
-    const double tl = (double)t + ((wr.P - Ps) + corr);
+    const double tl = tb + corr;
     // the next lane's speculated start (DPP wave shift: no LDS instruction on this path)
     const double tn = dpp_next(tl);
     const bool last = lane == cnt - 1;
@@ -643,6 +792,14 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
       break;
     }
     int f = (int)__builtin_ctzll(bad);
+    if (seq) {
+      // lanes s..f-1 verified, f's start is exact: the rest of the window in integer steps
+      t = f == s ? t : rdl((float)out, f - 1);
+      const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
+      t = fs_seq_window(d, c, base, n, wr, cnt, f, t, lane, ct);
+      if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
+      break;
+    }
     // lanes s..f-1 verified: f's start is exact.  Step lane by lane from f while the records
     // need the full lemma, then speculate again.
     t = f == s ? t : rdl((float)out, f - 1);
