@@ -53,8 +53,9 @@ enum { DLG_SACMODEL_PLANE = 0, DLG_SACMODEL_NORMAL_PLANE = 11 };
 /* refit of the winning model (SampleConsensusModelPlane::optimizeModelCoefficients) */
 enum {
   DLG_REFIT_PCL = 0,   /* PCL's float refit: computeMeanAndCovarianceMatrix's single-pass float
-                          sums in list order + float eigen33, bit-exact with PCL.  One rank: the
-                          sums run on the device, exactly (fsum.hpp); multi-rank: on the host */
+                          sums in list order + float eigen33, bit-exact with PCL.  The sums run
+                          on the device, exactly (fsum.hpp); several ranks hand the chains'
+                          values from rank to rank in list order (RCCL send/recv) */
   DLG_REFIT_FAST = 1   /* NOT PCL's arithmetic: exact integer moments of the inliers + a double
                           Jacobi solve (the least-squares plane to within float rounding; order-
                           and rank-count-independent).  Its planes differ from PCL's by up to
@@ -390,7 +391,7 @@ enum {
   DLG_OPT_PRUNE_STATS = 6,  /* 1: count the pruned kernel's work (dlg_prune_stats); 0 (default) */
   DLG_OPT_SELECT_TILE = 7,  /* points per tile of the lean rounds' single-pass selects: 4096,
                                8192 or 16384 (default) */
-  DLG_OPT_PCL_REFIT_DEVICE = 8 /* DLG_REFIT_PCL on one rank: 1 (default) the float sums on the
+  DLG_OPT_PCL_REFIT_DEVICE = 8 /* DLG_REFIT_PCL: 1 (default) the float sums on the
                                device, exact (fsum.hpp); 0 gathered and summed on the host; 2 as 1,
                                the host recomputing every refit's tail from the sums; 3 as 2 and
                                every round's select redone with the host's plane (test) */
