@@ -560,6 +560,7 @@ __device__ __forceinline__ int fs_step_lanes(const FsDev& d, int c, int64_t base
 constexpr int kFsSpecIter = 2;  // rounds of member choice per speculation pass
 constexpr bool kFsSeq = true;   // after a failed pass: integer stepping (fs_seq_window) ...
 constexpr int kFsSeqMin = 4;    // ... in windows with more records than this that are not fast
+constexpr bool kFsSeqFirst = true;  // (such windows: no speculation pass first)
 constexpr int kFsWinBytes = kWave * (int)sizeof(FsNode);
 
 __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int64_t K,
@@ -738,6 +739,12 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
   // speculation pass the rest of the window is stepped in integers; with few, speculating again
   // after the failed lane is cheaper
   const bool seq = kFsSeq && __builtin_popcountll(ballot(lane < cnt && !fastrec)) > kFsSeqMin;
+  if (seq && kFsSeqFirst) {
+    const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
+    t = fs_seq_window(d, c, base, n, wr, cnt, 0, t, lane, ct);
+    if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
+    return t;
+  }
   int s = 0;
   while (s < cnt) {
     ++ct.pass;
