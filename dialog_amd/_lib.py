@@ -83,7 +83,7 @@ class ExtractStats(C.Structure):
     _fields_ = [("rounds", C.c_int), ("tests", C.c_int64), ("tests_scored", C.c_int64),
                 ("score_launches", C.c_int), ("score_ms", C.c_double), ("select_ms", C.c_double),
                 ("wall_ms", C.c_double), ("lean_rounds", C.c_int), ("spec_misses", C.c_int),
-                ("pcl_host_checks", C.c_int)]
+                ("pcl_host_checks", C.c_int), ("refit_walk_ms", C.c_double)]
 
 
 _lib = None

@@ -106,6 +106,15 @@ void check_sp_totals(dlg_ctx* c, const int32_t* sp_tot) {
   }
 }
 
+// the PCL refit walk's share of a round's select phase (its events ride k_fs_walk's dispatch)
+void add_walk_ms(dlg_ctx* c, int k) {
+  if (!c->walk_rec[k]) return;
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->ev_walk[k][0], c->ev_walk[k][1]));
+  c->sel_pending->refit_walk_ms += ms;
+  c->walk_rec[k] = false;
+}
+
 // after a stream synchronisation: the last compaction's Morton-copy totals and select timing
 void settle_round(dlg_ctx* c) {
   if (c->sel1_err.p) {
@@ -123,6 +132,7 @@ void settle_round(dlg_ctx* c) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, c->ev_sel[k][0], c->ev_sel[k][1]));
     c->sel_pending->select_ms += ms;
+    add_walk_ms(c, k);
     c->sel_pending = nullptr;
   }
 }
@@ -636,6 +646,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // one-thread kernel, then the select with the refined plane read from device memory.  PCL
     // mode needs the host's sequential float sums in between.
     const int sk = c->sel_k;  // this round's pair of select timing events
+    c->walk_rec[sk] = false;
+    // the PCL refit walk's timing events (profiling only)
+    auto walk_ev = [&](int e) -> hipEvent_t {
+      if (!c->profiling) return nullptr;
+      if (!c->ev_walk[sk][e]) HIPCHK(hipEventCreate(&c->ev_walk[sk][e]));
+      c->walk_rec[sk] = true;
+      return c->ev_walk[sk][e];
+    };
     if (c->profiling) {
       for (auto& ev : c->ev_sel[sk])
         if (!ev) HIPCHK(hipEventCreate(&ev));
@@ -704,14 +722,16 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         launch_ucompact(cl->ubits.p, nw, cl->pristine.view(cl->n_total), c->sel1, c->fs_x.p,
                         c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
-                        rc_dev, fs_res, c->num_cus, c->stream, c->comm.get());
+                        rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
+                        walk_ev(1));
       } else {
         c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
         stage_wait();
         launch_select(src, bc_dev, mt, c->tile_in.p, c->tile_off_in.p, c->tile_off_out.p,
                       c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
         launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
-                        c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get());
+                        c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(),
+                        walk_ev(0), walk_ev(1));
       }
       HIPCHK(hipGetLastError());
     } else {
@@ -900,6 +920,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, c->ev_sel[sk ^ 1][0], c->ev_sel[sk ^ 1][1]));
       c->sel_pending->select_ms += ms;
+      add_walk_ms(c, sk ^ 1);
       c->sel_pending = nullptr;
     }
     if (c->profiling && xs) c->sel_pending = xs;  // this round's: read at the next publish / end
@@ -1251,6 +1272,9 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
     (void)hipStreamDestroy(c->cstream);
   }
   for (auto& pr : c->ev_sel)
+    for (auto& ev : pr)
+      if (ev) (void)hipEventDestroy(ev);
+  for (auto& pr : c->ev_walk)
     for (auto& ev : pr)
       if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : c->ev)

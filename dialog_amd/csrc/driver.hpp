@@ -228,6 +228,8 @@ struct dlg_ctx {
   int64_t sp_expect_in = 0, sp_expect_out = 0;
   dlg_extract_stats* sel_pending = nullptr;  // select_ms of the last round, not yet read
   hipEvent_t ev_sel[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // per-round pairs
+  hipEvent_t ev_walk[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // the PCL refit's walk
+  bool walk_rec[2] = {false, false};  // the pair's walk events were recorded this round
   int sel_k = 0;
   DevBuf<int32_t> rk;     // every rank's (inliers, survivors) of a round
   PinBuf<int32_t> h_rk;

@@ -27,6 +27,8 @@
 #include "fsum.hpp"
 #include "comm.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <cstdint>
 
 namespace dlg {
@@ -987,7 +989,8 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
 
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
-                     float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm) {
+                     float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
+                     hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
   FsDev d{px, py, pz, stride, n_dev, b};
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t U = (fs_chunks(nc) + kFsUC - 1) / kFsUC;
@@ -998,7 +1001,8 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
     hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, nullptr);
     hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, nullptr);
     hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-    hipLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, d, nullptr, cin, cout, res);
+    hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
+                          nullptr, cin, cout, res);
     return;
   }
   // several ranks (the list is the ranks' segments in order): each rank's guesses start from the
@@ -1010,8 +1014,9 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
   hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, b.base9);
   hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
   if (r > 0) comm->recv(b.start9, kFsChains, DType::I32, r - 1, s);
-  hipLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, d, r > 0 ? b.start9 : nullptr,
-                     nullptr, nullptr, nullptr);
+  hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
+                        r > 0 ? b.start9 : (const float*)nullptr, (const float4*)nullptr,
+                        (float4*)nullptr, (int32_t*)nullptr);
   if (r < W - 1) comm->send(b.sums, kFsChains, DType::I32, r + 1, s);
   comm->broadcast(b.sums, kFsChains, DType::I32, W - 1, s);
   hipLaunchKernelGGL(k_fs_tail, dim3(1), dim3(1), 0, s, b.sums, b.n_global, cin, cout, res);

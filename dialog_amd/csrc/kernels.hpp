@@ -225,9 +225,11 @@ struct FsBuffers {
 size_t fs_scratch_bytes(int64_t n_cap, int world);
 FsBuffers fs_carve(void* base, int64_t n_cap, int world);
 class Comm;
+// ev_walk0 / ev_walk1 (optional): timing events riding k_fs_walk's dispatch
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
-                     float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm = nullptr);
+                     float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm = nullptr,
+                     hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr);
 
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers

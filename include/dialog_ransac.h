@@ -112,6 +112,8 @@ typedef struct {
   int spec_misses;             /* speculative device picks the host replay overturned */
   int pcl_host_checks;         /* device PCL refits whose tail the host recomputed (an eigen33
                                   transcendental near a float rounding boundary) */
+  double refit_walk_ms;        /* of select_ms: the device PCL refit's chain walks (k_fs_walk,
+                                  latency-bound sequential chains), lean rounds */
 } dlg_extract_stats;
 
 void dlg_sac_params_default(dlg_sac_params* p);   /* PCL SACSegmentation defaults */
