@@ -587,6 +587,21 @@ struct FsWalkCounters {
   int64_t win = 0, pass = 0, slow = 0, step = 0, rerun = 0, clk_step = 0, group_fast = 0;
 };
 
+// inclusive prefix sum of an int over the wave (DPP, as wave_incl_scan)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, kCtrl, kRowMask, 0xF, false);
+}
+__device__ __forceinline__ int wave_incl_scan_i32(int v) {
+  v += dpp_i32<0x111, 0xF>(v);
+  v += dpp_i32<0x112, 0xF>(v);
+  v += dpp_i32<0x114, 0xF>(v);
+  v += dpp_i32<0x118, 0xF>(v);
+  v += dpp_i32<0x142, 0xA>(v);
+  v += dpp_i32<0x143, 0xC>(v);
+  return v;
+}
+
 // float minimum over the wave by DPP (lane 63 ends with it; no LDS instruction)
 template <int kCtrl, int kRowMask>
 __device__ __forceinline__ float dpp_min_step(float v) {
@@ -669,6 +684,9 @@ __device__ __forceinline__ float fs_seq_window(const FsDev& d, int c, int64_t ba
     return m >= 0.0 ? (int64_t)fmin(m, 1073741824.0) : (int64_t)-1;
   };
   const int64_t M0 = marg(wr.m0), M1 = marg(wr.m1), M2 = marg(wr.m2), M3 = marg(wr.m3);
+  // a translation record: fast (every member's increment the same) with all four E usable
+  const bool tr = act && wr.mu3 >= 0.0f && !exact_only && k0 && k1 && k2 && k3 && E1 == E0 &&
+                  E2 == E0 && E3 == E0;
   const double q2 = 2.0 * (double)qk;
   const bool c0 = (double)wr.q0 <= q2, c1 = (double)wr.q1 <= q2, c2 = (double)wr.q2 <= q2,
              c3 = (double)wr.q3 <= q2;
@@ -685,20 +703,52 @@ __device__ __forceinline__ float fs_seq_window(const FsDev& d, int c, int64_t ba
       ++f;
       continue;
     }
-    int cur = (int)Ld, keep = 0;
+    // the stepping runs over nodes: a record whose increment depends on its start, or a run of
+    // translation records (fast, one increment whatever the member) taken as one step with the
+    // run's summed increment.  Node j's data are compacted into lane j (ds_permute over a
+    // permutation: node starts to their node index, every other lane to a distinct lane >= m).
+    const bool in = act && lane >= f;
+    const int trv = tr ? 1 : 0;
+    const int trprev = __builtin_amdgcn_update_dpp(0, trv, 0x138, 0xF, 0xF, false);  // lane - 1
+    const bool ns = in && (lane == f || !tr || !trprev);
+    const uint64_t nsm = ballot(ns);
+    const int m = (int)__builtin_popcountll(nsm);
+    const int nk = (int)__builtin_popcountll(nsm & ((2ull << lane) - 1ull)) - 1;  // (lane 63: all)
+    const int ev = in && tr ? E0 : 0;
+    const int sxi = wave_incl_scan_i32(ev);
+    const int sx = sxi - ev;  // exclusive prefix of the translation increments
+    const int sx_tot = __builtin_amdgcn_readlane(sxi, kWave - 1);
+    const int dest = in ? (ns ? nk : m + ((lane - f) - (nk + 1))) : lane < f ? (cnt - f) + lane : lane;
+    const int pa = dest * 4;
+    const int sxj = __builtin_amdgcn_ds_permute(pa, sx);
+    const int shj0 = __builtin_amdgcn_ds_permute(pa, sh | (trv << 8));
+    const int e0j = __builtin_amdgcn_ds_permute(pa, E0);
+    const int f1j = __builtin_amdgcn_ds_permute(pa, F1);
+    const int f2j = __builtin_amdgcn_ds_permute(pa, F2);
+    const int f3j = __builtin_amdgcn_ds_permute(pa, F3);
+    const int sxn = __builtin_amdgcn_update_dpp(sxj, sxj, 0x130, 0xF, 0xF, false);  // lane + 1
+    const bool trj = (shj0 >> 8) != 0;
+    const int etot = (lane == m - 1 ? sx_tot : sxn) - sxj;  // a translation run's increment
+    const int shn = trj ? 0 : (shj0 & 0xFF);
+    const int G0 = trj ? etot : e0j, G1 = trj ? etot : f1j, G2 = trj ? etot : f2j,
+              G3 = trj ? etot : f3j;
+    int cur = (int)Ld, keepn = 0;
 #pragma unroll 2
-    for (int j = f; j < cnt; ++j) {
-      keep = lane == j ? cur : keep;
+    for (int j = 0; j < m; ++j) {
+      keepn = lane == j ? cur : keepn;
       // the member's bits as all-ones / zero masks (signed bit-field extracts), the increment
       // picked by bit-field inserts
-      const unsigned m0 = (unsigned)__builtin_amdgcn_sbfe(cur, sh, 1);
-      const unsigned m1 = (unsigned)__builtin_amdgcn_sbfe(cur, sh + 1, 1);
-      const unsigned lo = (m0 & (unsigned)F1) | (~m0 & (unsigned)E0);
-      const unsigned hi = (m0 & (unsigned)F3) | (~m0 & (unsigned)F2);
+      const unsigned m0 = (unsigned)__builtin_amdgcn_sbfe(cur, shn, 1);
+      const unsigned m1 = (unsigned)__builtin_amdgcn_sbfe(cur, shn + 1, 1);
+      const unsigned lo = (m0 & (unsigned)G1) | (~m0 & (unsigned)G0);
+      const unsigned hi = (m0 & (unsigned)G3) | (~m0 & (unsigned)G2);
       const int e = (int)((m1 & hi) | (~m1 & lo));
       cur = __builtin_amdgcn_update_dpp(cur, cur + e, 0x138, 0xF, 0xF, false);  // wave_shr:1
     }
-    ct.step += cnt - f;
+    ct.step += m;
+    // every record's lead: its node's lead plus the translation increments before it in the run
+    const int keep = __builtin_amdgcn_ds_bpermute(nk * 4, keepn) +
+                     (sx - __builtin_amdgcn_ds_bpermute(nk * 4, sxj));
     // coverage of every lane's start (fs_apply's decisions on the integer lead)
     const int64_t L = keep;
     const bool grid = (L & ((1ll << sh) - 1)) == 0;
