@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdialog_amd.so")
+LIB_PATH = os.environ.get("DLG_AB_LIB") or os.path.join(HERE, "libdialog_amd.so")  # (A/B tooling)
 
 DLG_OK = 0
 DLG_ERR_CAPACITY = 5
