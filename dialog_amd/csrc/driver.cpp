@@ -269,10 +269,12 @@ unsigned long long* prune_stats_ptr(dlg_ctx* c) {
 
 void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
   const int64_t n = cl->n_total;
-  DevBuf<uint32_t> k0, k1;
-  DevBuf<int32_t> i0, i1;
-  DevBuf<uint8_t> tmp;
-  try {
+  DevBuf<uint32_t>& k0 = c->mk0;
+  DevBuf<uint32_t>& k1 = c->mk1;
+  DevBuf<int32_t>& i0 = c->mi0;
+  DevBuf<int32_t>& i1 = c->mi1;
+  DevBuf<uint8_t>& tmp = c->msort;
+  {
     k0.ensure(n); k1.ensure(n); i0.ensure(n); i1.ensure(n);
     const size_t tb = morton_sort_temp_bytes(n);
     tmp.ensure(std::max<size_t>(tb, 16));
@@ -299,16 +301,13 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
     launch_sphere_bounds(cl->sp_pristine.x.p, cl->sp_pristine.y.p, cl->sp_pristine.z.p, m, nullptr,
                          cl->sp_tiles_pr.p, cl->sp_supers_pr.p, c->stream);
     HIPCHK(hipGetLastError());
-    sync(c);
+    // (no synchronisation: everything that reads the copy is queued behind it on the stream;
+    // the scratch above is only rewritten by the next build, on the same stream)
     cl->sp_n_pristine = cl->sp_n = m;
     cl->sp_built = cl->sp_valid = true;
     cl->sp_cur = -1;
     cl->sp_dirty = false;
-  } catch (...) {
-    k0.release(); k1.release(); i0.release(); i1.release(); tmp.release();
-    throw;
   }
-  k0.release(); k1.release(); i0.release(); i1.release(); tmp.release();
 }
 
 SpatialView spatial_view(const dlg_cloud* cl) {
@@ -1265,6 +1264,10 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->sel1_err.release();
   c->lp.release();
   c->lp_n.release();
+  c->fs_scr.release();
+  c->fs_x.release(); c->fs_y.release(); c->fs_z.release(); c->fs_n.release();
+  c->mk0.release(); c->mk1.release(); c->mi0.release(); c->mi1.release(); c->msort.release();
+  c->mom_done.release(); c->pick_done.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
   if (c->ev_inl) (void)hipEventDestroy(c->ev_inl);
   if (c->cstream) {
@@ -1401,20 +1404,8 @@ dlg_status dlg_cloud_build_spatial(dlg_ctx* c, dlg_cloud* cl) {
 
 dlg_status dlg_cloud_drop_spatial(dlg_cloud* cl) {
   if (!cl) return DLG_ERR_INVALID;
-  if (cl->ctx) {
-    (void)hipSetDevice(cl->ctx->device);
-    (void)hipStreamSynchronize(cl->ctx->stream);
-  }
-  cl->sp_pristine.release();
-  cl->sp_buf[0].release();
-  cl->sp_buf[1].release();
-  cl->sp_tiles_pr.release();
-  cl->sp_supers_pr.release();
-  cl->sp_order.release();
-  for (int b = 0; b < 2; ++b) {
-    cl->sp_tb[b].release();
-    cl->sp_sb[b].release();
-  }
+  // (the copy's device buffers stay allocated for the next build -- hipFree synchronises the
+  // device and a rebuild would allocate them again; dlg_cloud_destroy frees them)
   cl->sp_built = cl->sp_valid = false;
   cl->sp_n = cl->sp_n_pristine = 0;
   cl->cur = -1;  // (a lean list needs the Morton copy: back to the pristine list)

@@ -247,6 +247,11 @@ struct dlg_ctx {
   PostWork pw;
   // PCL float refit on the device (fsum.hip): scratch sized for fs_cap inliers
   DevBuf<uint8_t> fs_scr;
+  // the spatial index build's sort scratch (Morton keys and orders, ping-pong; radix-sort
+  // temporaries), kept across builds: no allocation per build
+  DevBuf<uint32_t> mk0, mk1;
+  DevBuf<int32_t> mi0, mi1;
+  DevBuf<uint8_t> msort;
   int64_t fs_cap = -1;
   FsBuffers fs_b;
   DevBuf<float> fs_x, fs_y, fs_z;  // lean rounds: the unrefined plane's inliers in list order

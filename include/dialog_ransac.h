@@ -154,9 +154,10 @@ dlg_status dlg_cloud_reset(dlg_cloud* cloud);
  * >= 131072 points (context option DLG_OPT_PRUNE: 0 never, 1 always); this forces it for any cloud
  * (call right after upload or dlg_cloud_reset).  Kept in step by SACMODEL_PLANE extraction. */
 dlg_status dlg_cloud_build_spatial(dlg_ctx* ctx, dlg_cloud* cloud);
-/* release the Morton copy (the exhaustive scoring kernels take over until it is built again);
- * resets the cloud to all points active.  With dlg_cloud_build_spatial it times the index build
- * on device-resident points. */
+/* drop the Morton copy (the exhaustive scoring kernels take over until it is built again; its
+ * device buffers are kept for the next build and freed by dlg_cloud_destroy); resets the cloud to
+ * all points active.  With dlg_cloud_build_spatial it times the index build on device-resident
+ * points. */
 dlg_status dlg_cloud_drop_spatial(dlg_cloud* cloud);
 dlg_status dlg_cloud_active(const dlg_cloud* cloud, int64_t* n_active_local);
 /* SACSegmentationFromNormals::setInputNormals: one normal record per uploaded point (n = the
