@@ -305,6 +305,141 @@ __device__ __forceinline__ float rdl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// a record unpacked for the walk, with its per-record constants (q = quantum of g, iq = 1/q, gq =
+// g / q, d0 = member 0's increment, P = the in-unit prefix of the member-0 increments, mu3 = the
+// fast path's margin)
+struct FsWalkRec {
+  float g, mu3;
+  float o0, o1, o2, o3, m0, m1, m2, m3, q0, q1, q2, q3;
+  double d0, P;
+  // (derived on use: fewer live registers)
+  __device__ double q() const { return (double)fs_quantum(g); }
+  __device__ double iq() const { return fs_inv_quantum(g); }
+  __device__ double gd() const { return (double)g; }
+};
+
+__device__ __forceinline__ FsWalkRec fs_walk_rec(const f32x4& r0, const f32x4& r1, const f32x4& r2,
+                                                 const f32x4& r3) {
+  FsWalkRec w;
+  w.g = r0.x;
+  w.mu3 = r0.w;
+  w.o0 = r1.x; w.o1 = r1.y; w.o2 = r1.z; w.o3 = r1.w;
+  w.m0 = r2.x; w.m1 = r2.y; w.m2 = r2.z; w.m3 = r2.w;
+  w.q0 = r3.x; w.q1 = r3.y; w.q2 = r3.z; w.q3 = r3.w;
+  w.d0 = w.q0 >= 0.0f ? (double)w.o0 - (double)w.g : 0.0;
+  w.P = __longlong_as_double((int64_t)(((uint64_t)__float_as_uint(r0.z) << 32) |
+                                       __float_as_uint(r0.y)));
+  return w;
+}
+
+// inclusive prefix sum of an int over the wave (DPP, as wave_incl_scan)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, kCtrl, kRowMask, 0xF, false);
+}
+__device__ __forceinline__ int wave_incl_scan_i32(int v) {
+  v += dpp_i32<0x111, 0xF>(v);
+  v += dpp_i32<0x112, 0xF>(v);
+  v += dpp_i32<0x114, 0xF>(v);
+  v += dpp_i32<0x118, 0xF>(v);
+  v += dpp_i32<0x142, 0xA>(v);
+  v += dpp_i32<0x143, 0xC>(v);
+  return v;
+}
+
+// float minimum over the wave by DPP (lane 63 ends with it; no LDS instruction)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ float dpp_min_step(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v),
+                                                              kCtrl, kRowMask, 0xF, false));
+  return fminf(v, o);
+}
+__device__ __forceinline__ float wave_min(float v) {
+  v = dpp_min_step<0x111, 0xF>(v);
+  v = dpp_min_step<0x112, 0xF>(v);
+  v = dpp_min_step<0x114, 0xF>(v);
+  v = dpp_min_step<0x118, 0xF>(v);
+  v = dpp_min_step<0x142, 0xA>(v);
+  v = dpp_min_step<0x143, 0xC>(v);
+  return rdl(v, kWave - 1);
+}
+
+// the integer-stepping table of a window's records (fs_seq_window), one record per lane: Q =
+// the window's smallest quantum of a nonzero guess or usable output, per record the member
+// increments E_i = (o_i - i q(g_k) - g_{k+1}) / Q (0 past the last record; F_i = E_0 for a
+// record that takes only its exact start), margins floor(mu_i / Q) (saturated, -1: none), the
+// shift s = log2(q(g_k) / Q) and flags.  Computed once per window in k_fs_l1, in parallel.
+__device__ __forceinline__ void fs_seq_prep(const FsWalkRec wr, int cnt, int lane, uint4* sq0,
+                                            uint4* sq1, uint4* sq2) {
+  const bool act = lane < cnt;
+  const bool u0 = wr.q0 >= 0.0f, u1 = wr.q1 >= 0.0f, u2 = wr.q2 >= 0.0f, u3 = wr.q3 >= 0.0f;
+  float qv = INFINITY;
+  auto qmin = [&](float v, bool use) {
+    if (use && v != 0.0f) qv = fminf(qv, fs_quantum(v));  // (NaN quanta of non-finite values: ignored)
+  };
+  if (act) {
+    qmin(wr.g, true);
+    qmin(wr.o0, u0); qmin(wr.o1, u1); qmin(wr.o2, u2); qmin(wr.o3, u3);
+  }
+  float Qf = wave_min(qv);
+  if (!(Qf < INFINITY)) Qf = 1.40129846e-45f;  // (every value zero)
+  const double iQ = 1.0 / (double)Qf;  // (exact: powers of two)
+  const float qk = fs_quantum(wr.g);
+  // s = log2(q(g_k) / Q); a lane whose quantum is below Q (a zero guess) or not finite only takes
+  // its exact start (L = 0, member 0)
+  const bool gfin = fabsf(wr.g) <= 3.40282347e+38f;
+  // (log2 of a power of two from its bits: exponent field, or the bit position when subnormal)
+  auto lg2 = [](float p) {
+    const uint32_t b = __float_as_uint(p), e = (b >> 23) & 0xFFu;
+    return e ? (int)e - 127 : (int)__builtin_ctz(b | 0x80000000u) - 149;
+  };
+  int sh = lg2(qk) - lg2(Qf);
+  const bool exact_only = !gfin || !(qk >= Qf);
+  if (exact_only || sh < 0) sh = 0;
+  if (sh > 30) sh = 30;
+  // E_k[i] (0 past the window's last lane: its end value is taken from the member directly)
+  const float gn = __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(wr.g), 0x130, 0xF, 0xF, false));  // g_{k+1}
+  const bool lastl = lane == cnt - 1;
+  auto emem = [&](float o, int i, bool u, bool* ok) {
+    if (lastl) {
+      *ok = u;
+      return 0;
+    }
+    // (o - g_{k+1}, both multiples of Q, is exact below 2^52 Q; the bound keeps it exact)
+    const double dd = (double)o - (double)gn;
+    const double e = (dd - (double)i * (double)qk) * iQ;
+    *ok = u && fabs(dd * iQ) < 1099511627776.0 && fabs(e) < 1048576.0 && e == floor(e);
+    return *ok ? (int)e : 0;
+  };
+  bool k0, k1, k2, k3;
+  const int E0 = emem(wr.o0, 0, u0, &k0), E1 = emem(wr.o1, 1, u1, &k1),
+            E2 = emem(wr.o2, 2, u2, &k2), E3 = emem(wr.o3, 3, u3, &k3);
+  // (a lane taking only its exact start steps with E0 whatever the lead's bits)
+  const int F1 = exact_only ? E0 : E1, F2 = exact_only ? E0 : E2, F3 = exact_only ? E0 : E3;
+  auto marg = [&](float mu) {  // floor(mu / Q), saturated; -1: no shift tolerated
+    const double m = floor((double)mu * iQ);
+    return m >= 0.0 ? (int64_t)fmin(m, 1073741824.0) : (int64_t)-1;
+  };
+  const int64_t M0 = marg(wr.m0), M1 = marg(wr.m1), M2 = marg(wr.m2), M3 = marg(wr.m3);
+  // a translation record: fast (every member's increment the same) with all four E usable
+  const bool tr = act && wr.mu3 >= 0.0f && !exact_only && k0 && k1 && k2 && k3 && E1 == E0 &&
+                  E2 == E0 && E3 == E0;
+  const double q2 = 2.0 * (double)qk;
+  const bool c0 = (double)wr.q0 <= q2, c1 = (double)wr.q1 <= q2, c2 = (double)wr.q2 <= q2,
+             c3 = (double)wr.q3 <= q2;
+  *sq0 = make_uint4((uint32_t)E0, (uint32_t)F1, (uint32_t)F2, (uint32_t)F3);
+  *sq1 = make_uint4((uint32_t)(int32_t)M0, (uint32_t)(int32_t)M1, (uint32_t)(int32_t)M2,
+                    (uint32_t)(int32_t)M3);
+  const uint32_t fl = (uint32_t)sh | (uint32_t)exact_only << 8 | (uint32_t)gfin << 9 |
+                      (uint32_t)k0 << 10 | (uint32_t)k1 << 11 | (uint32_t)k2 << 12 |
+                      (uint32_t)k3 << 13 | (uint32_t)c0 << 14 | (uint32_t)c1 << 15 |
+                      (uint32_t)c2 << 16 | (uint32_t)c3 << 17 | (uint32_t)tr << 18;
+  *sq2 = make_uint4(fl, __float_as_uint(Qf), 0u, 0u);
+}
+
 // ---- k_fs_l1 ----------------------------------------------------------------------------------
 constexpr int kFlBS = kFsUC * kFsFan;  // 64 chunks x 4 members
 __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
@@ -423,6 +558,16 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
         row[2] = __uint_as_float((uint32_t)(eb >> 32));
         row[3] = mu3;
       }
+      // the integer-stepping table of the record (lanes past nch: unused)
+      const float4 q0 = sn[t * 4], q1 = sn[t * 4 + 1], q2 = sn[t * 4 + 2], q3 = sn[t * 4 + 3];
+      uint4 s0, s1, s2;
+      fs_seq_prep(fs_walk_rec(f32x4{q0.x, q0.y, q0.z, q0.w}, f32x4{q1.x, q1.y, q1.z, q1.w},
+                              f32x4{q2.x, q2.y, q2.z, q2.w}, f32x4{q3.x, q3.y, q3.z, q3.w}),
+                  nch, t, &s0, &s1, &s2);
+      if (t < nch) {
+        uint4* o = d.b.srec + 3 * ((int64_t)c * d.b.cap + u * kFsUC + t);
+        o[0] = s0; o[1] = s1; o[2] = s2;
+      }
     }
     __syncthreads();
     for (int p = t; p < nch * 4; p += kFlBS)
@@ -431,8 +576,6 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
 }
 
 // ---- k_fs_walk --------------------------------------------------------------------------------
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // lane l + 1's value (DPP wave_shl:1; the last lane gets its own)
 __device__ __forceinline__ double dpp_next(double v) {
@@ -465,33 +608,6 @@ __device__ __forceinline__ float fs_rerun(const FsDev& d, int c, int64_t k, int6
   const float p = fs_term(c, x, y, z);
   for (int j = 0; j < len; ++j) v = v + rdl(p, j);
   return v;
-}
-
-// a record unpacked for the walk, with its per-record constants (q = quantum of g, iq = 1/q, gq =
-// g / q, d0 = member 0's increment, P = the in-unit prefix of the member-0 increments, mu3 = the
-// fast path's margin)
-struct FsWalkRec {
-  float g, mu3;
-  float o0, o1, o2, o3, m0, m1, m2, m3, q0, q1, q2, q3;
-  double d0, P;
-  // (derived on use: fewer live registers)
-  __device__ double q() const { return (double)fs_quantum(g); }
-  __device__ double iq() const { return fs_inv_quantum(g); }
-  __device__ double gd() const { return (double)g; }
-};
-
-__device__ __forceinline__ FsWalkRec fs_walk_rec(const f32x4& r0, const f32x4& r1, const f32x4& r2,
-                                                 const f32x4& r3) {
-  FsWalkRec w;
-  w.g = r0.x;
-  w.mu3 = r0.w;
-  w.o0 = r1.x; w.o1 = r1.y; w.o2 = r1.z; w.o3 = r1.w;
-  w.m0 = r2.x; w.m1 = r2.y; w.m2 = r2.z; w.m3 = r2.w;
-  w.q0 = r3.x; w.q1 = r3.y; w.q2 = r3.z; w.q3 = r3.w;
-  w.d0 = w.q0 >= 0.0f ? (double)w.o0 - (double)w.g : 0.0;
-  w.P = __longlong_as_double((int64_t)(((uint64_t)__float_as_uint(r0.z) << 32) |
-                                       __float_as_uint(r0.y)));
-  return w;
 }
 
 // fs_increment (fsum.hpp) on the unpacked record (scalar selects: no indexed record array)
@@ -564,6 +680,22 @@ constexpr bool kFsSeq = true;   // after a failed pass: integer stepping (fs_seq
 constexpr int kFsSeqMin = 4;    // ... in windows with more records than this that are not fast
 constexpr bool kFsSeqFirst = true;  // (such windows: no speculation pass first)
 constexpr int kFsWinBytes = kWave * (int)sizeof(FsNode);
+constexpr int kFsSeqBytes = kWave * 3 * (int)sizeof(uint4);  // a window's integer-stepping tables
+constexpr int kFsSlotBytes = kFsWinBytes + kFsSeqBytes;
+
+// a window's tables (3 KB: 3 loads of 1 KB) into LDS behind its records
+__device__ __forceinline__ void fs_seq_load(const uint4* T, int64_t base, int64_t K,
+                                            uint32_t lds, int lane) {
+  const int64_t w0 = base < K ? base : (K - 1) / kWave * kWave;
+  const char* src = reinterpret_cast<const char*>(T + 3 * w0) + 16 * lane;
+  const int64_t lim = 3 * K * (int64_t)sizeof(uint4) - 16 - 3 * w0 * (int64_t)sizeof(uint4);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int64_t off = (int64_t)j * 1024 + 16 * lane;
+    const char* p = off <= lim ? src + j * 1024 : reinterpret_cast<const char*>(T + 3 * w0);
+    asm volatile("global_load_lds_dwordx4 %0, off" : : "v"(p), "{m0}"(lds + j * 1024) : "memory");
+  }
+}
 
 __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int64_t K,
                                              __attribute__((address_space(3))) void* slot,
@@ -587,38 +719,6 @@ struct FsWalkCounters {
   int64_t win = 0, pass = 0, slow = 0, step = 0, rerun = 0, clk_step = 0, group_fast = 0;
 };
 
-// inclusive prefix sum of an int over the wave (DPP, as wave_incl_scan)
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ int dpp_i32(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, kCtrl, kRowMask, 0xF, false);
-}
-__device__ __forceinline__ int wave_incl_scan_i32(int v) {
-  v += dpp_i32<0x111, 0xF>(v);
-  v += dpp_i32<0x112, 0xF>(v);
-  v += dpp_i32<0x114, 0xF>(v);
-  v += dpp_i32<0x118, 0xF>(v);
-  v += dpp_i32<0x142, 0xA>(v);
-  v += dpp_i32<0x143, 0xC>(v);
-  return v;
-}
-
-// float minimum over the wave by DPP (lane 63 ends with it; no LDS instruction)
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ float dpp_min_step(float v) {
-  const float o = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v),
-                                                              kCtrl, kRowMask, 0xF, false));
-  return fminf(v, o);
-}
-__device__ __forceinline__ float wave_min(float v) {
-  v = dpp_min_step<0x111, 0xF>(v);
-  v = dpp_min_step<0x112, 0xF>(v);
-  v = dpp_min_step<0x114, 0xF>(v);
-  v = dpp_min_step<0x118, 0xF>(v);
-  v = dpp_min_step<0x142, 0xA>(v);
-  v = dpp_min_step<0x143, 0xC>(v);
-  return rdl(v, kWave - 1);
-}
-
 // Exact stepping in integers, lanes f..cnt-1 of a window from the exact value t at lane f.
 // Every value involved (the guesses, the usable members' outputs, the chain's values where a
 // record covers them) is a multiple of Q, the window's smallest quantum of a nonzero guess or
@@ -631,65 +731,21 @@ __device__ __forceinline__ float wave_min(float v) {
 // coverage is checked for all lanes afterwards, the first uncovered lane is rerun from its exact
 // start g_u + L_u Q and the stepping resumes after it.  Returns the value after the window.
 __device__ __forceinline__ float fs_seq_window(const FsDev& d, int c, int64_t base, int64_t n,
-                                               const FsWalkRec wr, int cnt, int f, float t,
-                                               int lane, FsWalkCounters& ct) {
+                                               const FsWalkRec wr, const uint4 sq0,
+                                               const uint4 sq1, const uint4 sq2, int cnt, int f,
+                                               float t, int lane, FsWalkCounters& ct) {
   const bool act = lane < cnt;
-  const bool u0 = wr.q0 >= 0.0f, u1 = wr.q1 >= 0.0f, u2 = wr.q2 >= 0.0f, u3 = wr.q3 >= 0.0f;
-  float qv = INFINITY;
-  auto qmin = [&](float v, bool use) {
-    if (use && v != 0.0f) qv = fminf(qv, fs_quantum(v));  // (NaN quanta of non-finite values: ignored)
-  };
-  if (act) {
-    qmin(wr.g, true);
-    qmin(wr.o0, u0); qmin(wr.o1, u1); qmin(wr.o2, u2); qmin(wr.o3, u3);
-  }
-  float Qf = wave_min(qv);
-  if (!(Qf < INFINITY)) Qf = 1.40129846e-45f;  // (every value zero)
+  // the record's table (k_fs_l1: fs_seq_prep)
+  const int E0 = (int)sq0.x, F1 = (int)sq0.y, F2 = (int)sq0.z, F3 = (int)sq0.w;
+  const int64_t M0 = (int32_t)sq1.x, M1 = (int32_t)sq1.y, M2 = (int32_t)sq1.z, M3 = (int32_t)sq1.w;
+  const uint32_t fl = sq2.x;
+  const int sh = (int)(fl & 0xFFu);
+  const bool exact_only = (fl >> 8) & 1u, gfin = (fl >> 9) & 1u;
+  const bool k0 = (fl >> 10) & 1u, k1 = (fl >> 11) & 1u, k2 = (fl >> 12) & 1u, k3 = (fl >> 13) & 1u;
+  const bool c0 = (fl >> 14) & 1u, c1 = (fl >> 15) & 1u, c2 = (fl >> 16) & 1u, c3 = (fl >> 17) & 1u;
+  const bool tr = act && ((fl >> 18) & 1u);
+  const float Qf = __uint_as_float(__builtin_amdgcn_readfirstlane(sq2.y));
   const double Q = (double)Qf, iQ = 1.0 / Q;  // (exact: powers of two)
-  const float qk = fs_quantum(wr.g);
-  // s = log2(q(g_k) / Q); a lane whose quantum is below Q (a zero guess) or not finite only takes
-  // its exact start (L = 0, member 0)
-  const bool gfin = fabsf(wr.g) <= 3.40282347e+38f;
-  // (log2 of a power of two from its bits: exponent field, or the bit position when subnormal)
-  auto lg2 = [](float p) {
-    const uint32_t b = __float_as_uint(p), e = (b >> 23) & 0xFFu;
-    return e ? (int)e - 127 : (int)__builtin_ctz(b | 0x80000000u) - 149;
-  };
-  int sh = lg2(qk) - lg2(Qf);
-  const bool exact_only = !gfin || !(qk >= Qf);
-  if (exact_only || sh < 0) sh = 0;
-  if (sh > 30) sh = 30;
-  // E_k[i] (0 past the window's last lane: its end value is taken from the member directly)
-  const float gn = __int_as_float(
-      __builtin_amdgcn_update_dpp(0, __float_as_int(wr.g), 0x130, 0xF, 0xF, false));  // g_{k+1}
-  const bool lastl = lane == cnt - 1;
-  auto emem = [&](float o, int i, bool u, bool* ok) {
-    if (lastl) {
-      *ok = u;
-      return 0;
-    }
-    // (o - g_{k+1}, both multiples of Q, is exact below 2^52 Q; the bound keeps it exact)
-    const double dd = (double)o - (double)gn;
-    const double e = (dd - (double)i * (double)qk) * iQ;
-    *ok = u && fabs(dd * iQ) < 1099511627776.0 && fabs(e) < 1048576.0 && e == floor(e);
-    return *ok ? (int)e : 0;
-  };
-  bool k0, k1, k2, k3;
-  const int E0 = emem(wr.o0, 0, u0, &k0), E1 = emem(wr.o1, 1, u1, &k1),
-            E2 = emem(wr.o2, 2, u2, &k2), E3 = emem(wr.o3, 3, u3, &k3);
-  // (a lane taking only its exact start steps with E0 whatever the lead's bits)
-  const int F1 = exact_only ? E0 : E1, F2 = exact_only ? E0 : E2, F3 = exact_only ? E0 : E3;
-  auto marg = [&](float mu) {  // floor(mu / Q), saturated; -1: no shift tolerated
-    const double m = floor((double)mu * iQ);
-    return m >= 0.0 ? (int64_t)fmin(m, 1073741824.0) : (int64_t)-1;
-  };
-  const int64_t M0 = marg(wr.m0), M1 = marg(wr.m1), M2 = marg(wr.m2), M3 = marg(wr.m3);
-  // a translation record: fast (every member's increment the same) with all four E usable
-  const bool tr = act && wr.mu3 >= 0.0f && !exact_only && k0 && k1 && k2 && k3 && E1 == E0 &&
-                  E2 == E0 && E3 == E0;
-  const double q2 = 2.0 * (double)qk;
-  const bool c0 = (double)wr.q0 <= q2, c1 = (double)wr.q1 <= q2, c2 = (double)wr.q2 <= q2,
-             c3 = (double)wr.q3 <= q2;
   while (f < cnt) {
     // the start's lead: t - g_f with its rounding error (TwoSum: the lead must be exact)
     const double ta = (double)t, gb = -(double)rdl(wr.g, f);
@@ -783,8 +839,9 @@ __device__ __forceinline__ float fs_seq_window(const FsDev& d, int c, int64_t ba
 // it does not decide), lanes stepped alone from the first failed one; returns the value after the
 // window's last chunk
 __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t base, int64_t n,
-                                                const FsWalkRec wr, int cnt, float t, int lane,
-                                                FsWalkCounters& ct) {
+                                                const FsWalkRec wr, const uint4 sq0,
+                                                const uint4 sq1, const uint4 sq2, int cnt, float t,
+                                                int lane, FsWalkCounters& ct) {
   const bool fastrec = wr.mu3 >= 0.0f;
   ++ct.win;
   // many records whose increment depends on the start (a sum hovering near zero): after a failed
@@ -793,7 +850,7 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
   const bool seq = kFsSeq && __builtin_popcountll(ballot(lane < cnt && !fastrec)) > kFsSeqMin;
   if (seq && kFsSeqFirst) {
     const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
-    t = fs_seq_window(d, c, base, n, wr, cnt, 0, t, lane, ct);
+    t = fs_seq_window(d, c, base, n, wr, sq0, sq1, sq2, cnt, 0, t, lane, ct);
     if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
     return t;
   }
@@ -855,7 +912,7 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
       // lanes s..f-1 verified, f's start is exact: the rest of the window in integer steps
       t = f == s ? t : rdl((float)out, f - 1);
       const int64_t clk1 = d.b.wst ? (int64_t)clock64() : 0;
-      t = fs_seq_window(d, c, base, n, wr, cnt, f, t, lane, ct);
+      t = fs_seq_window(d, c, base, n, wr, sq0, sq1, sq2, cnt, f, t, lane, ct);
       if (d.b.wst) ct.clk_step += (int64_t)clock64() - clk1;
       break;
     }
@@ -877,12 +934,13 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
                                                    const float4* __restrict__ cin,
                                                    float4* __restrict__ cout,
                                                    int32_t* __restrict__ res) {
-  __shared__ __attribute__((aligned(16))) char ring[2 * kFsWinBytes];
+  __shared__ __attribute__((aligned(16))) char ring[2 * kFsSlotBytes];
   const int c = blockIdx.x, lane = threadIdx.x;
   const int64_t n = *d.n_dev;
   const int64_t K = fs_chunks(n);
   const int64_t NW = (K + kWave - 1) / kWave;
   const FsNode* R = fs_rec(d.b, c, 0);
+  const uint4* T = d.b.srec + 3 * (int64_t)c * d.b.cap;
   const float4* S = d.b.win + c * d.b.wcap;
   float t = start9 ? start9[c] : 0.0f;
   // walk counters (dlg_float_sums' walk_stats): windows walked record by record, speculation
@@ -891,8 +949,9 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   const int64_t clk0 = d.b.wst ? (int64_t)clock64() : 0;
   auto slot = [&](int j) {
     return (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)ring +
-                                                       j * kFsWinBytes);
+                                                       j * kFsSlotBytes);
   };
+  auto tslot = [&](int j) { return (uint32_t)(uintptr_t)slot(j) + (uint32_t)kFsWinBytes; };
   FsWalkCounters ct;
   int64_t pre_w = -1;  // the window prefetched into slot pre_s (or none)
   int pre_s = 0;
@@ -930,34 +989,43 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
       // window f record by record
       const int64_t w = wb + f;
       const int cur = pre_w == w ? pre_s : pre_s ^ 1;
-      if (pre_w != w) fs_ring_load(R, w * kWave, K, slot(cur), lane);
+      if (pre_w != w) {
+        fs_ring_load(R, w * kWave, K, slot(cur), lane);
+        fs_seq_load(T, w * kWave, K, tslot(cur), lane);
+      }
       // prefetch the next window the summaries cannot skip at any lag
       const uint64_t nx = f + 1 < kWave ? stat & (~0ull << (f + 1)) : 0ull;
       pre_w = nx ? wb + (int64_t)__builtin_ctzll(nx) : -1;
       pre_s = cur ^ 1;
       if (pre_w >= 0) {
         fs_ring_load(R, pre_w * kWave, K, slot(pre_s), lane);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        fs_seq_load(T, pre_w * kWave, K, tslot(pre_s), lane);
+        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       f32x4 r0, r1, r2, r3;
+      uint4 q0, q1, q2;
       const uint32_t la = (uint32_t)(uintptr_t)(
           (__attribute__((address_space(3))) char*)slot(cur) + sizeof(FsNode) * lane);
+      const uint32_t lt = tslot(cur) + 3u * 16u * (uint32_t)lane;
       // (inline asm: the compiler would otherwise drain every outstanding load before an LDS
       // read that may alias an LDS-DMA write)
       asm volatile(
-          "ds_read_b128 %0, %4\n\t"
-          "ds_read_b128 %1, %4 offset:16\n\t"
-          "ds_read_b128 %2, %4 offset:32\n\t"
-          "ds_read_b128 %3, %4 offset:48\n\t"
+          "ds_read_b128 %0, %7\n\t"
+          "ds_read_b128 %1, %7 offset:16\n\t"
+          "ds_read_b128 %2, %7 offset:32\n\t"
+          "ds_read_b128 %3, %7 offset:48\n\t"
+          "ds_read_b128 %4, %8\n\t"
+          "ds_read_b128 %5, %8 offset:16\n\t"
+          "ds_read_b128 %6, %8 offset:32\n\t"
           "s_waitcnt lgkmcnt(0)"
-          : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
-          : "v"(la)
+          : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(q0), "=&v"(q1), "=&v"(q2)
+          : "v"(la), "v"(lt)
           : "memory");
       const int64_t b0 = w * kWave;
       const int cn = K - b0 < kWave ? (int)(K - b0) : kWave;
-      t = fs_walk_window(d, c, b0, n, fs_walk_rec(r0, r1, r2, r3), cn, t, lane, ct);
+      t = fs_walk_window(d, c, b0, n, fs_walk_rec(r0, r1, r2, r3), q0, q1, q2, cn, t, lane, ct);
       i = f + 1;
     }
   }
@@ -1002,7 +1070,8 @@ size_t fs_scratch_bytes(int64_t n_cap, int world) {
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t K = fs_chunks(nc), U = (K + kFsUC - 1) / kFsUC;
   return align256(sizeof(double) * K * kFsChains) + 2 * align256(sizeof(double) * U * kFsChains) +
-         align256(sizeof(FsNode) * K * kFsChains) + align256(sizeof(float4) * U * kFsChains) +
+         align256(sizeof(FsNode) * K * kFsChains) + align256(3 * sizeof(uint4) * K * kFsChains) +
+         align256(sizeof(float4) * U * kFsChains) +
          align256(sizeof(float) * 32) +
          align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) + 256;
 }
@@ -1021,6 +1090,8 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   b.rec = reinterpret_cast<FsNode*>(p);
   b.cap = K;
   p += align256(sizeof(FsNode) * K * kFsChains);
+  b.srec = reinterpret_cast<uint4*>(p);
+  p += align256(3 * sizeof(uint4) * K * kFsChains);
   b.win = reinterpret_cast<float4*>(p);
   b.wcap = U;
   p += align256(sizeof(float4) * U * kFsChains);

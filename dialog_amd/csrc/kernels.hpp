@@ -208,6 +208,7 @@ struct FsBuffers {
   double* upre = nullptr;  // [units][9] exclusive prefixes
   FsNode* rec = nullptr;   // chunk records, chain-major: rec[c * cap + k]
   int64_t cap = 0;         // chunks per chain
+  uint4* srec = nullptr;   // the records' integer-stepping tables (3 x 16 B each): srec[3 (c * cap + k) + j]
   float4* win = nullptr;   // window summaries (64 records each), chain-major: win[c * wcap + w]
   int64_t wcap = 0;        // windows per chain
   float* sums = nullptr;   // [9] the chains' end values
