@@ -49,20 +49,52 @@ __global__ void k(float* out, long long* cyc, int iters) {
     q = __builtin_amdgcn_readlane(q, f2) + lane;
   }
   t1 = clock64(); if (lane == 0) cyc[6] = (t1 - t0) / iters;
-  out[lane] = f + (float)d + (float)s + (float)e + g + tv + q;
+  // (h) int add + DPP wave_shr:1 chain; (i) int add + DPP row_shr:1 chain; (j) v_bfi chain;
+  // (k) dependent SALU chain (s_add + s_lshr through asm)
+  int wv = lane;
+  t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+    wv = __builtin_amdgcn_update_dpp(wv, wv + 3, 0x138, 0xF, 0xF, false);
+    wv = __builtin_amdgcn_update_dpp(wv, wv + 5, 0x138, 0xF, 0xF, false);
+  }
+  t1 = clock64(); if (lane == 0) cyc[7] = (t1 - t0) / (2 * iters);
+  int rv = lane;
+  t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+    rv = __builtin_amdgcn_update_dpp(rv, rv + 3, 0x111, 0xF, 0xF, false);
+    rv = __builtin_amdgcn_update_dpp(rv, rv + 5, 0x111, 0xF, 0xF, false);
+  }
+  t1 = clock64(); if (lane == 0) cyc[8] = (t1 - t0) / (2 * iters);
+  unsigned bv = lane, mk = 0x0F0F0F0Fu + lane;
+  t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+    bv = (mk & bv) | (~mk & (bv + 7u));
+    bv = (mk & (bv + 3u)) | (~mk & bv);
+  }
+  t1 = clock64(); if (lane == 0) cyc[9] = (t1 - t0) / (2 * iters);
+  int sv = iters;
+  t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile("s_add_u32 %0, %0, 7\n\ts_lshr_b32 %0, %0, 1\n\ts_add_u32 %0, %0, 3\n\ts_lshr_b32 %0, %0, 1"
+                 : "+s"(sv));
+  }
+  t1 = clock64(); if (lane == 0) cyc[10] = (t1 - t0) / (4 * iters);
+  out[lane] = f + (float)d + (float)s + (float)e + g + tv + q + (float)wv + (float)rv + (float)bv + (float)sv;
 }
 
 int main() {
   float* o; long long* c;
-  hipMalloc(&o, 256); hipMalloc(&c, 64);
+  hipMalloc(&o, 256); hipMalloc(&c, 128);
   k<<<1, 64>>>(o, c, 1000);
   hipDeviceSynchronize();
   k<<<1, 64>>>(o, c, 10000);
-  long long h[8];
-  hipMemcpy(h, c, 56, hipMemcpyDeviceToHost);
+  long long h[11];
+  hipMemcpy(h, c, 88, hipMemcpyDeviceToHost);
   const char* names[] = {"f32 add", "f64 add", "readlane->salu", "f64 floor+mul+add (x3)",
-                         "cvt f32->f64 mul f64->f32", "readlane(float add) uniform", "ballot->ctz->readlane"};
-  for (int i = 0; i < 7; ++i) printf("%-32s %lld clk\n", names[i], h[i]);
+                         "cvt f32->f64 mul f64->f32", "readlane(float add) uniform", "ballot->ctz->readlane",
+                         "int add + dpp wave_shr:1", "int add + dpp row_shr:1", "bfi-style select",
+                         "salu add/lshr"};
+  for (int i = 0; i < 11; ++i) printf("%-32s %lld clk\n", names[i], h[i]);
   int clk = 0; hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
   printf("clock rate %d kHz\n", clk);
   return 0;
