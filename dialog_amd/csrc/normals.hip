@@ -542,9 +542,35 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
     const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
     const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
-    for (int z = max(cz - 1, 0); z <= min(cz + 1, G.g[2] - 1); ++z)
-      for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
-        for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
+    // The 27 cells nearest first (own cell, faces, edges, corners); a cell is skipped when a
+    // lower bound of its distance to the query reaches the radius, or exceeds the current K-th
+    // distance once K candidates are held (then its candidates could neither count nor enter).
+    // Per axis the bound is the query's distance to the shared cell face in units of the index
+    // map's cell width, less 1e-4 of a cell for the map's rounding, and the squared sum is
+    // scaled by (1 - 1e-5) before the compare (FLANN's d2 rounding): never above a point's d2.
+    const float w = 1.0f / G.inv_cell;
+    const float fx = (qx - G.lo[0]) * G.inv_cell - (float)cx;
+    const float fy = (qy - G.lo[1]) * G.inv_cell - (float)cy;
+    const float fz = (qz - G.lo[2]) * G.inv_cell - (float)cz;
+    auto side = [&](float f, int d) {  // distance bound to the neighbour on side d, cell units
+      const float v = d < 0 ? f : d > 0 ? 1.0f - f : 0.0f;
+      return v > 1e-4f ? (v - 1e-4f) * w : 0.0f;
+    };
+    const float bx0 = side(fx, -1), bx1 = side(fx, 1), by0 = side(fy, -1), by1 = side(fy, 1);
+    const float bz0 = side(fz, -1), bz1 = side(fz, 1);
+    constexpr uint64_t kOrd[3] = {0x904416665151515ull, 0x1a9864a9261058ull, 0x2a2a20a8220ull};
+#pragma unroll 1
+    for (int c3 = 0; c3 < 27; ++c3) {
+      const uint32_t code = (uint32_t)(kOrd[c3 / 10] >> (6 * (c3 % 10))) & 63u;
+      const int dx = (int)(code & 3u) - 1, dy = (int)((code >> 2) & 3u) - 1,
+                dz = (int)((code >> 4) & 3u) - 1;
+      const int x = cx + dx, y = cy + dy, z = cz + dz;
+      if (x < 0 || x >= G.g[0] || y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
+      const float ex = dx < 0 ? bx0 : dx > 0 ? bx1 : 0.0f;
+      const float ey = dy < 0 ? by0 : dy > 0 ? by1 : 0.0f;
+      const float ez = dz < 0 ? bz0 : dz > 0 ? bz1 : 0.0f;
+      const float md = (ex * ex + ey * ey + ez * ez) * (1.0f - 1e-5f);
+      if (md >= lim || md > kd) continue;
           const int2 rg = cell_range(L.tkeys[l], L.trange[l], L.tmask[l], cell_key(G, x, y, z));
           for (int u = rg.x; u < rg.y; ++u) {
             const float d2 = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
