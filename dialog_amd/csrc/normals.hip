@@ -31,6 +31,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "grid_dev.hpp"
 #include "host_math.hpp"
@@ -510,11 +511,14 @@ __global__ __launch_bounds__(kBS) void k_nbr_normals(
   normals[sidx[t]] = finish_normal_pcl(a, k, sx[t], sy[t], sz[t], vpx, vpy, vpz);
 }
 
-template <int KP, bool PCLF>
+constexpr int kKnnCap = 32;  // level 0: buffered candidates per query
+template <int KP, bool PCLF, bool L0>
 __global__ __launch_bounds__(kBS) void k_normals_knn(
     KnnLevels L, int l, const int32_t* __restrict__ qpos, int nq, const float* __restrict__ X,
     const float* __restrict__ Y, const float* __restrict__ Z, int K, float vpx, float vpy,
     float vpz, float4* __restrict__ normals, uint8_t* __restrict__ defer_next) {
+  __shared__ uint32_t s_hist[L0 ? 8 : 1][kBS];        // level 0: 16 d2 buckets (16-bit halves)
+  __shared__ int32_t s_buf[L0 ? kKnnCap : 1][kBS];    // level 0: the candidates of buckets <= B
   const int t = blockIdx.x * kBS + threadIdx.x;
   if (t >= nq) return;
   const int uq = qpos ? qpos[t] : t;
@@ -559,42 +563,91 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     const float bx0 = side(fx, -1), bx1 = side(fx, 1), by0 = side(fy, -1), by1 = side(fy, 1);
     const float bz0 = side(fz, -1), bz1 = side(fz, 1);
     constexpr uint64_t kOrd[3] = {0x904416665151515ull, 0x1a9864a9261058ull, 0x2a2a20a8220ull};
+    // cells nearest first, each skipped when its distance bound md fails keep(md)
+    auto scan = [&](auto&& keep, auto&& visit) {
 #pragma unroll 1
-    for (int c3 = 0; c3 < 27; ++c3) {
-      const uint32_t code = (uint32_t)(kOrd[c3 / 10] >> (6 * (c3 % 10))) & 63u;
-      const int dx = (int)(code & 3u) - 1, dy = (int)((code >> 2) & 3u) - 1,
-                dz = (int)((code >> 4) & 3u) - 1;
-      const int x = cx + dx, y = cy + dy, z = cz + dz;
-      if (x < 0 || x >= G.g[0] || y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
-      const float ex = dx < 0 ? bx0 : dx > 0 ? bx1 : 0.0f;
-      const float ey = dy < 0 ? by0 : dy > 0 ? by1 : 0.0f;
-      const float ez = dz < 0 ? bz0 : dz > 0 ? bz1 : 0.0f;
-      const float md = (ex * ex + ey * ey + ez * ez) * (1.0f - 1e-5f);
-      if (md >= lim || md > kd) continue;
-          const int2 rg = cell_range(L.tkeys[l], L.trange[l], L.tmask[l], cell_key(G, x, y, z));
-          for (int u = rg.x; u < rg.y; ++u) {
-            const float d2 = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
-            if (!(d2 < lim)) continue;
-            ++cnt;
-            if (d2 > kd) continue;
-            int ci = sidx[u];
-            if (d2 == kd && ci > ki) continue;
-            float cd = d2;
+      for (int c3 = 0; c3 < 27; ++c3) {
+        const uint32_t code = (uint32_t)(kOrd[c3 / 10] >> (6 * (c3 % 10))) & 63u;
+        const int dx = (int)(code & 3u) - 1, dy = (int)((code >> 2) & 3u) - 1,
+                  dz = (int)((code >> 4) & 3u) - 1;
+        const int x = cx + dx, y = cy + dy, z = cz + dz;
+        if (x < 0 || x >= G.g[0] || y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
+        const float ex = dx < 0 ? bx0 : dx > 0 ? bx1 : 0.0f;
+        const float ey = dy < 0 ? by0 : dy > 0 ? by1 : 0.0f;
+        const float ez = dz < 0 ? bz0 : dz > 0 ? bz1 : 0.0f;
+        const float md = (ex * ex + ey * ey + ez * ez) * (1.0f - 1e-5f);
+        if (md >= lim || !keep(md)) continue;
+        const int2 rg = cell_range(L.tkeys[l], L.trange[l], L.tmask[l], cell_key(G, x, y, z));
+        for (int u = rg.x; u < rg.y; ++u) visit(u, flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]));
+      }
+    };
+    auto insert = [&](float cd, int ci) {
+      if (cd > kd || (cd == kd && ci > ki)) return;
 #pragma unroll
-            for (int j = 0; j < KP; ++j) {
-              const bool lt = cd < bd[j] || (cd == bd[j] && ci < bi[j]);
-              const float od = bd[j];
-              const int oi = bi[j];
-              bd[j] = lt ? cd : od;
-              bi[j] = lt ? ci : oi;
-              cd = lt ? od : cd;
-              ci = lt ? oi : ci;
-            }
+      for (int j = 0; j < KP; ++j) {
+        const bool lt = cd < bd[j] || (cd == bd[j] && ci < bi[j]);
+        const float od = bd[j];
+        const int oi = bi[j];
+        bd[j] = lt ? cd : od;
+        bi[j] = lt ? ci : oi;
+        cd = lt ? od : cd;
+        ci = lt ? oi : ci;
+      }
 #pragma unroll
-            for (int j = 0; j < KP; ++j)
-              if (j == K - 1) { kd = bd[j]; ki = bi[j]; }
-          }
+      for (int j = 0; j < KP; ++j)
+        if (j == K - 1) { kd = bd[j]; ki = bi[j]; }
+    };
+    bool direct = true;
+    int B = 15;
+    const float inv = L0 ? 16.0f / lim : 0.0f;
+    auto bucket = [&](float d2) { const int bb = (int)(d2 * inv); return bb < 15 ? bb : 15; };
+    if constexpr (L0) {
+      // Level 0 (most queries): inside the scan the insertion network runs whenever any lane of
+      // the wave admits a candidate, i.e. at nearly every one.  Instead (1) count the candidates
+      // inside the radius in 16 buckets of d2 (LDS, 16-bit halves); (2) the first bucket B where
+      // the count reaches K bounds the K-th distance: the candidates of buckets <= B (about K)
+      // are buffered in LDS; (3) the network runs over the buffer only.  A bucket too dense for
+      // the buffer takes the network inside the scan.
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s_hist[q][threadIdx.x] = 0u;
+      scan([](float) { return true; }, [&](int, float d2) {
+        if (!(d2 < lim)) return;
+        ++cnt;
+        const int bb = bucket(d2);
+        atomicAdd(&s_hist[bb >> 1][threadIdx.x], 1u << (16 * (bb & 1)));
+      });
+      direct = false;
+      if (cnt >= K) {
+        int cum = 0;
+        for (int bb = 0; bb < 16; ++bb) {
+          cum += (int)((s_hist[bb >> 1][threadIdx.x] >> (16 * (bb & 1))) & 0xFFFFu);
+          if (cum >= K) { B = bb; break; }
         }
+        // (a cell whose bound puts every candidate past bucket B: skipped)
+        const float bmax = (float)(B + 1) * 1.0001f;
+        int nb = 0;
+        scan([&](float md) { return md * inv < bmax; }, [&](int u, float d2) {
+          if (!(d2 < lim) || bucket(d2) > B) return;
+          if (nb < kKnnCap) s_buf[nb][threadIdx.x] = u;
+          ++nb;
+        });
+        if (nb <= kKnnCap) {
+          for (int e = 0; e < nb; ++e) {
+            const int u = s_buf[e][threadIdx.x];
+            insert(flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]), sidx[u]);
+          }
+        } else {
+          direct = true;
+        }
+      }
+    }
+    if (direct) {
+      scan([&](float md) { return !(md > kd); }, [&](int u, float d2) {
+        if (!(d2 < lim)) return;
+        if (!L0) ++cnt;
+        if (!L0 || bucket(d2) <= B) insert(d2, sidx[u]);
+      });
+    }
     defer = cnt < K && !top;
     if (!defer) {
       const int m = cnt < K ? cnt : K;
@@ -1143,19 +1196,25 @@ void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int 
     hipLaunchKernelGGL(kern, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1], vp[2],
                        normals, defer_next);
   };
-  if (pcl_float) {
-    if (k <= 8) go(k_normals_knn<8, true>);
-    else if (k <= 16) go(k_normals_knn<16, true>);
-    else if (k <= 24) go(k_normals_knn<24, true>);
-    else if (k <= 32) go(k_normals_knn<32, true>);
-    else go(k_normals_knn<64, true>);
-  } else {
-    if (k <= 8) go(k_normals_knn<8, false>);
-    else if (k <= 16) go(k_normals_knn<16, false>);
-    else if (k <= 24) go(k_normals_knn<24, false>);
-    else if (k <= 32) go(k_normals_knn<32, false>);
-    else go(k_normals_knn<64, false>);
-  }
+  // (level 0: the histogram-buffered variant; the deferred levels scan and insert directly)
+  auto pick = [&](auto l0) {
+    constexpr bool Z = decltype(l0)::value;
+    if (pcl_float) {
+      if (k <= 8) go(k_normals_knn<8, true, Z>);
+      else if (k <= 16) go(k_normals_knn<16, true, Z>);
+      else if (k <= 24) go(k_normals_knn<24, true, Z>);
+      else if (k <= 32) go(k_normals_knn<32, true, Z>);
+      else go(k_normals_knn<64, true, Z>);
+    } else {
+      if (k <= 8) go(k_normals_knn<8, false, Z>);
+      else if (k <= 16) go(k_normals_knn<16, false, Z>);
+      else if (k <= 24) go(k_normals_knn<24, false, Z>);
+      else if (k <= 32) go(k_normals_knn<32, false, Z>);
+      else go(k_normals_knn<64, false, Z>);
+    }
+  };
+  if (level == 0 && level != L.levels - 1) pick(std::true_type{});
+  else pick(std::false_type{});
 }
 
 void launch_nbr_count(const GridDesc& G, const GridBufs& B, int q0, int nq, float r2,
