@@ -11,5 +11,7 @@ python3 -c "
 import csv
 r=list(csv.DictReader(open('$O/kt/run_kernel_trace.csv')))
 r.sort(key=lambda x:int(x['Start_Timestamp']))
-print([round((int(x['End_Timestamp'])-int(x['Start_Timestamp']))/1e6,2) for x in r if 'normals_knn' in x['Kernel_Name']], 'VGPR', [x['VGPR_Count'] for x in r if 'normals_knn' in x['Kernel_Name']][:1])
+d=lambda x:(int(x['End_Timestamp'])-int(x['Start_Timestamp']))/1e6
+print('knn', [round(d(x),2) for x in r if 'normals_knn' in x['Kernel_Name']])
+print('cells_build', round(sum(d(x) for x in r if 'k_cells_build' in x['Kernel_Name']),2), 'cells_end', round(sum(d(x) for x in r if 'k_cells_end' in x['Kernel_Name']),2), 'all kernels', round(sum(d(x) for x in r),2), 'span', round((max(int(x['End_Timestamp']) for x in r)-min(int(x['Start_Timestamp']) for x in r))/1e6,2))
 "
