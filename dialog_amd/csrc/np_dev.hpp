@@ -32,6 +32,16 @@ __device__ __forceinline__ bool np_full(float4 cn, float4 nn, double w, double b
   double rad = (double)((nn.x * cn.x + nn.z * cn.z) + (nn.y * cn.y + 0.0f * 0.0f));
   if (rad < -1.0) rad = -1.0;
   else if (rad > 1.0) rad = 1.0;
+  // Fast decision: min(acos(rad), pi - acos(rad)) = acos(|rad|) to within 4e-4 when taken as
+  // float acos of the float |rad| (the float rounding of rad moves acos by <= sqrt(2 * 6e-8)
+  // near |rad| = 1, float acos adds ~1e-6): a result clear of thr by w * 4e-4 (and a few ulps
+  // of the double sum) is PCL's; the band in between takes PCL's double arithmetic below.
+  if (w == w && b == b && w >= 0.0 && w < 1e30) {
+    const double a = (double)acosf((float)fabs(rad));
+    const double v = fabs(w * a + b), e = w * 4e-4 + 1e-12 + 1e-9 * fabs(b);
+    if (v < thr - e) return true;
+    if (v > thr + e) return false;
+  }
   double dn = fabs(acos(rad));
   const double alt = 3.14159265358979323846 - dn;  // M_PI
   if (alt < dn) dn = alt;                          // std::min(dn, M_PI - dn)
