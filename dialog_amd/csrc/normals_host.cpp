@@ -119,7 +119,41 @@ uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B, c
 // level-0 cell guessed from the bounding volume, then resized once from the measured occupancy
 // so an occupied cell holds ~k/2 points (surface-like clouds: occupancy ~ cell^2); levels above
 // grow 2x until one has <= 2 cells per axis
-KnnLevels build_hierarchy(dlg_ctx* c, int n, const BBox& b, int k_nn) {
+// the hierarchy's plan: level 0 built (cell tuned on the occupancy), the coarser cells recorded;
+// build_level() builds a planned level on demand (the k-NN normals build a level only when some
+// query needs it: most clouds resolve every query within a few levels of the planned ~10)
+struct KnnPlan {
+  BBox b;
+  int n = 0;
+  double cell[kMaxLevels] = {};
+  int planned = 0;
+};
+
+void build_level(dlg_ctx* c, const KnnPlan& P, KnnLevels& L, int l, const GridBufs* B0) {
+  GridBufs BL;
+  GridDesc G;
+  if (l == 0) {
+    BL = *B0;
+    G = L.G[0];
+  } else {
+    G = make_grid(P.b, P.cell[l]);
+    build_grid(c, P.n, G, l, &BL);
+  }
+  L.G[l] = G;
+  L.sx[l] = BL.sx; L.sy[l] = BL.sy; L.sz[l] = BL.sz; L.idx[l] = BL.idx_out;
+  c->nw.lv[l].pos.ensure(P.n);
+  launch_inverse_perm(BL.idx_out, P.n, c->nw.lv[l].pos.p, c->stream);
+  L.pos_of[l] = c->nw.lv[l].pos.p;
+  L.tkeys[l] = BL.tkeys; L.trange[l] = BL.trange; L.tmask[l] = BL.tmask;
+}
+
+// grid hierarchy over nw.x/y/z for k-nearest-neighbour queries (normals.hip, k_normals_knn):
+// level-0 cell guessed from the bounding volume, then resized once from the measured occupancy
+// so an occupied cell holds ~k/2 points (surface-like clouds: occupancy ~ cell^2); levels above
+// grow 2x until one has <= 2 cells per axis.  Builds `eager_levels` levels (all: -1); L.levels
+// is the planned count either way.
+KnnLevels build_hierarchy_plan(dlg_ctx* c, int n, const BBox& b, int k_nn, KnnPlan* plan,
+                               int eager_levels) {
   GridBufs B;
   double ext[3], maxe = 0.0;
   for (int k = 0; k < 3; ++k) {
@@ -141,32 +175,31 @@ KnnLevels build_hierarchy(dlg_ctx* c, int n, const BBox& b, int k_nn) {
     cell *= std::sqrt(target / pw);
     G = make_grid(b, cell);
   }
-  KnnLevels L;
-  L.levels = 0;
+  KnnPlan P;
+  P.b = b;
+  P.n = n;
   const double top_cell = maxe * 0.75;  // floor(ext / cell) + 1 <= 2 on every axis
   // 2x per level, more when the hierarchy would not fit kMaxLevels
   const double fac = std::max(2.0, std::pow(top_cell / cell, 1.0 / (kMaxLevels - 1)));
   for (int l = 0; l < kMaxLevels; ++l) {
     const bool last = cell >= top_cell || l == kMaxLevels - 1;
     if (last) cell = std::max(cell, top_cell);
-    GridBufs BL;
-    if (l == 0) {
-      BL = B;
-    } else {
-      G = make_grid(b, cell);
-      build_grid(c, n, G, l, &BL);
-    }
-    L.G[l] = G;
-    L.sx[l] = BL.sx; L.sy[l] = BL.sy; L.sz[l] = BL.sz; L.idx[l] = BL.idx_out;
-    c->nw.lv[l].pos.ensure(n);
-    launch_inverse_perm(BL.idx_out, n, c->nw.lv[l].pos.p, c->stream);
-    L.pos_of[l] = c->nw.lv[l].pos.p;
-    L.tkeys[l] = BL.tkeys; L.trange[l] = BL.trange; L.tmask[l] = BL.tmask;
-    L.levels = l + 1;
+    P.cell[l] = cell;
+    P.planned = l + 1;
     if (last) break;
     cell *= fac;
   }
+  KnnLevels L;
+  L.levels = P.planned;
+  L.G[0] = G;
+  const int eager = eager_levels < 0 ? P.planned : std::min(eager_levels, P.planned);
+  for (int l = 0; l < eager; ++l) build_level(c, P, L, l, &B);
+  if (plan) *plan = P;
   return L;
+}
+
+KnnLevels build_hierarchy(dlg_ctx* c, int n, const BBox& b, int k_nn) {
+  return build_hierarchy_plan(c, n, b, k_nn, nullptr, -1);
 }
 
 void check_points(const dlg_points* pts) {
@@ -255,7 +288,8 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
       }
     }
   } else {
-    const KnnLevels L = build_hierarchy(c, n, b, k_nn);
+    KnnPlan plan;
+    KnnLevels L = build_hierarchy_plan(c, n, b, k_nn, &plan, 1);
     w.queue.ensure(n);
     w.processed.ensure(n);
     w.sort_tmp.ensure(select_tmp_bytes(n));
@@ -263,6 +297,8 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
     int nq = n;
     for (int l = 0; l < L.levels && nq > 0; ++l) {
       const bool top = l == L.levels - 1;
+      // (level l + 1 built only now: level l's deferred queries are marked in its order)
+      if (!top) build_level(c, plan, L, l + 1, nullptr);
       if (!top) HIPCHK(hipMemsetAsync(w.processed.p, 0, n, c->stream));
       launch_normals_knn(L, l, qpos, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, w.processed.p,
                          pclf, c->stream);
