@@ -168,13 +168,20 @@ KnnLevels build_hierarchy_plan(dlg_ctx* c, int n, const BBox& b, int k_nn, KnnPl
   // tune on the point-weighted occupancy (what a typical query sees; sparse outlier cells do
   // not drag it down), assuming surface-like scaling occ ~ cell^2; two corrections at most
   const double target = std::max(2.0, k_nn / 2.0);
+  // large clouds tune on a prefix of 1/8 of the points (a sampled cell's occupancy is ~1/8 of the
+  // full one: pw_full ~ (pw_sample - (1 - f)) / f), then build level 0 once; the cell size only
+  // affects the speed, never the neighbour sets
+  const int ns = n >= (1 << 20) ? n / 8 : n;
+  const double f = (double)ns / (double)n;
   for (int it = 0; it < 3; ++it) {
     double pw = 0.0;
-    build_grid(c, n, G, 0, &B, nullptr, nullptr, nullptr, &pw);
+    build_grid(c, ns, G, 0, &B, nullptr, nullptr, nullptr, &pw);
+    if (ns < n) pw = (pw - (1.0 - f)) / f;
     if (it == 2 || pw <= 0.0 || (pw <= 2.0 * target && pw >= 0.5 * target)) break;
     cell *= std::sqrt(target / pw);
     G = make_grid(b, cell);
   }
+  if (ns < n) build_grid(c, n, G, 0, &B);
   KnnPlan P;
   P.b = b;
   P.n = n;
