@@ -16,7 +16,7 @@ DLG_SACMODEL_PLANE = 0
 DLG_SACMODEL_NORMAL_PLANE = 11
 DLG_REFIT_PCL = 0
 DLG_REFIT_FAST = 1
-ABI_VERSION = 2  # include/dialog_ransac.h DLG_ABI_VERSION: the structs below match that header
+ABI_VERSION = 3  # include/dialog_ransac.h DLG_ABI_VERSION: the structs below match that header
 
 SYMBOLS = [
     "dlg_abi_version", "dlg_status_string", "dlg_sac_params_default", "dlg_ctx_create",

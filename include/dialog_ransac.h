@@ -35,8 +35,9 @@ extern "C" {
 
 /* 2: dlg_extract_stats gained lean_rounds, spec_misses, pcl_host_checks; dlg_score_benchmark's
  * 4th argument is a DLG_SCORE_* kernel; execution paths are context options, not environment
- * variables */
-#define DLG_ABI_VERSION 2
+ * variables.  3: dlg_extract_stats gained refit_walk_ms; dlg_float_sums, dlg_cloud_estimate_normals
+ * and dlg_plane_border were added; dlg_cloud_drop_spatial keeps the copy's buffers */
+#define DLG_ABI_VERSION 3
 
 typedef enum {
   DLG_OK = 0,
