@@ -12,8 +12,8 @@ from .sac import (SAC_RANSAC, SACMODEL_NORMAL_PLANE, SACMODEL_PLANE, Cloud, Cont
 from .normals import (NormalEstimation, estimate_normals, orient_normals_nn,  # noqa: F401
                       regulate_normals)
 from .preprocess import preprocess, remove_redundant_points  # noqa: F401
-from .postprocess import (PostProcessParams, cluster_filter, post_process_planes,  # noqa: F401
-                          refit_planes)
+from .postprocess import (PostProcessParams, cluster_filter, plane_border,  # noqa: F401
+                          post_process_planes, refit_planes)
 from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, LIB_PATH  # noqa: F401
 from ._lib import (DLG_OPT_LEAN_ROUNDS, DLG_OPT_PCL_REFIT_DEVICE, DLG_OPT_PRUNE,  # noqa: F401
                    DLG_OPT_PRUNE_NP,
