@@ -529,7 +529,8 @@ template <int KP, bool PCLF, bool L0>
 __global__ __launch_bounds__(kBS) void k_normals_knn(
     KnnLevels L, int l, const int32_t* __restrict__ qpos, int nq, const float* __restrict__ X,
     const float* __restrict__ Y, const float* __restrict__ Z, int K, float vpx, float vpy,
-    float vpz, float4* __restrict__ normals, uint8_t* __restrict__ defer_next) {
+    float vpz, float4* __restrict__ normals, uint8_t* __restrict__ dflags, int64_t dstride,
+    int lmax) {
   __shared__ uint32_t s_hist[L0 ? 8 : 1][kBS];        // level 0: 16 d2 buckets (16-bit halves)
   __shared__ int32_t s_buf[L0 ? kKnnCap : 1][kBS];    // level 0: the candidates of buckets <= B
   const int t = blockIdx.x * kBS + threadIdx.x;
@@ -540,6 +541,7 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
   const bool active = true;
   Moments M;
   bool defer = false;
+  int jump = 1;  // levels up a deferred query goes
   if (active && finite3(qx, qy, qz)) {
     const GridDesc& G = L.G[l];
     const bool top = l == L.levels - 1;
@@ -662,6 +664,11 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
       });
     }
     defer = cnt < K && !top;
+    // (level 0, fewer than K/4 candidates: the radius holding K is more than twice this level's
+    // on a surface, so level 1 would nearly always defer it again -- it goes to level 2.  Only
+    // from level 0: above it the sparse queries are volume-like outliers, many of which level
+    // l + 1 resolves, and a query scanned a level too coarse costs ~4x the candidates)
+    if (L0 && cnt > 0 && cnt * 4 < K && l + 2 < L.levels - 1) jump = 2;
     if (!defer) {
       const int m = cnt < K ? cnt : K;
       if constexpr (PCLF) {
@@ -684,7 +691,10 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
         }
     }
   }
-  if (defer) defer_next[L.pos_of[l + 1][qi]] = 1;
+  if (defer) {
+    const int tl = l + jump < lmax ? l + jump : lmax;
+    dflags[(int64_t)tl * dstride + qi] = 1;
+  }
   else normals[qi] = PCLF ? finish_normal_pcl(nullptr, 0, qx, qy, qz, vpx, vpy, vpz)
                           : finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
 }
@@ -1202,12 +1212,13 @@ void launch_normals_radius(const GridDesc& G, const GridBufs& B, int n, float r2
 
 void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
-                        float4* normals, uint8_t* defer_next, bool pcl_float, hipStream_t s) {
+                        float4* normals, uint8_t* defer, int64_t defer_stride, int lmax,
+                        bool pcl_float, hipStream_t s) {
   if (nq <= 0) return;
   const dim3 g(cdiv(nq, kBS)), b(kBS);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, g, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1], vp[2],
-                       normals, defer_next);
+                       normals, defer, defer_stride, lmax);
   };
   // (level 0: the histogram-buffered variant; the deferred levels scan and insert directly)
   auto pick = [&](auto l0) {
@@ -1259,6 +1270,19 @@ void launch_nbr_fill_sort_normals(const GridDesc& G, const GridBufs& B, int q0, 
   hipLaunchKernelGGL(k_nbr_sort, dim3(gs), dim3(kBS), 0, s, nq, cnt, off, keys);
   hipLaunchKernelGGL(k_nbr_normals, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, B.sx, B.sy, B.sz,
                      B.idx_out, q0, nq, cnt, off, keys, X, Y, Z, vp[0], vp[1], vp[2], normals);
+}
+
+__global__ __launch_bounds__(kBS) void k_gather_flags(const uint8_t* __restrict__ f,
+                                                      const int32_t* __restrict__ idx, int n,
+                                                      uint8_t* __restrict__ out) {
+  const int u = blockIdx.x * kBS + threadIdx.x;
+  if (u < n) out[u] = f[idx[u]];
+}
+
+void launch_gather_flags(const uint8_t* f, const int32_t* idx, int n, uint8_t* out,
+                         hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_flags, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, f, idx, n, out);
 }
 
 void launch_inverse_perm(const int32_t* idx, int n, int32_t* pos_of, hipStream_t s) {

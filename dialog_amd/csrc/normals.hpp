@@ -78,9 +78,14 @@ struct KnnLevels {
 // defer_next[its sorted position at level + 1]
 // pcl_float: PCL's single-pass float moments over the (d2, index)-ordered list + float eigen33
 // (bit-exact with PCL's arithmetic as restated); else centred double moments + double eigen33
+// defer: per-level flag arrays (level t at defer + t * defer_stride, indexed by point); a
+// deferred query is flagged at level l + 1, or (from level 0) l + 2 when it saw fewer than k / 4
+// candidates (surface-like density: the radius it needs is more than twice this level's), never
+// above level lmax
 void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
-                        float4* normals, uint8_t* defer_next, bool pcl_float, hipStream_t s);
+                        float4* normals, uint8_t* defer, int64_t defer_stride, int lmax,
+                        bool pcl_float, hipStream_t s);
 // PCL-float radius normals in chunks of queries (sorted positions [q0, q0 + nq)):
 // counts -> exclusive scan (int64 offsets) -> (d2, index) keys filled, sorted per query (one
 // wave per query: bitonic in registers up to 1024 keys, heapsort beyond) -> float sums in that
@@ -95,6 +100,8 @@ void launch_nbr_fill_sort_normals(const GridDesc& G, const GridBufs& B, int q0, 
                                   const float* X, const float* Y, const float* Z, const float vp[3],
                                   float4* normals, int num_cus, hipStream_t s);
 void launch_inverse_perm(const int32_t* idx, int n, int32_t* pos_of, hipStream_t s);
+// out[u] = f[idx[u]] (point-indexed flags -> a level's sorted order)
+void launch_gather_flags(const uint8_t* f, const int32_t* idx, int n, uint8_t* out, hipStream_t s);
 
 // nearest neighbour (k = 1, ties -> lowest index) in the hierarchy's cloud of external queries
 // (qx, qy, qz)[qlist or 0..nq); unresolved queries go to next[] for the level above

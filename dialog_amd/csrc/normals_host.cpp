@@ -299,24 +299,38 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
     KnnLevels L = build_hierarchy_plan(c, n, b, k_nn, &plan, 1);
     w.queue.ensure(n);
     w.processed.ensure(n);
+    // deferred-query flags per level, indexed by point: a level is built only once some query
+    // is flagged for it (most clouds resolve every query within a few of the planned levels)
+    w.dflags.ensure((size_t)n * L.levels);
+    if (L.levels > 1)
+      HIPCHK(hipMemsetAsync(w.dflags.p + n, 0, (size_t)n * (L.levels - 1), c->stream));
     w.sort_tmp.ensure(select_tmp_bytes(n));
-    const int32_t* qpos = nullptr;  // level 0: every point
-    int nq = n;
-    for (int l = 0; l < L.levels && nq > 0; ++l) {
-      const bool top = l == L.levels - 1;
-      // (level l + 1 built only now: level l's deferred queries are marked in its order)
-      if (!top) build_level(c, plan, L, l + 1, nullptr);
-      if (!top) HIPCHK(hipMemsetAsync(w.processed.p, 0, n, c->stream));
-      launch_normals_knn(L, l, qpos, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, w.processed.p,
-                         pclf, c->stream);
-      if (top) break;
-      // deferred queries in level l+1's cell order
-      HIPCHK(select_flagged(w.sort_tmp.p, w.sort_tmp.cap, w.processed.p, n, w.queue.p,
-                            w.counters.p, c->stream));
+    bool built[kMaxLevels] = {true};
+    auto count_flags = [&](const uint8_t* f) {
+      HIPCHK(select_flagged(w.sort_tmp.p, w.sort_tmp.cap, f, n, w.queue.p, w.counters.p,
+                            c->stream));
       HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 4, hipMemcpyDeviceToHost, c->stream));
       sync(c);
-      nq = (int)w.h_cnt.p[0];
-      qpos = w.queue.p;
+      return (int)w.h_cnt.p[0];
+    };
+    for (int l = 0; l < L.levels; ++l) {
+      const int32_t* qpos = nullptr;  // level 0: every point
+      int nq = n;
+      if (l > 0) {
+        const uint8_t* f = w.dflags.p + (size_t)l * n;
+        nq = count_flags(f);
+        if (nq == 0) {
+          if (l >= 2) break;  // (queries skip a level only from level 0)
+          continue;
+        }
+        if (!built[l]) build_level(c, plan, L, l, nullptr), built[l] = true;
+        // the flagged queries in this level's cell order
+        launch_gather_flags(f, L.idx[l], n, w.processed.p, c->stream);
+        nq = count_flags(w.processed.p);
+        qpos = w.queue.p;
+      }
+      launch_normals_knn(L, l, qpos, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, w.dflags.p,
+                         (int64_t)n, L.levels - 1, pclf, c->stream);
     }
   }
   HIPCHK(hipGetLastError());
