@@ -102,7 +102,7 @@ struct GridLevelBufs {
 struct NormalsWork {
   static constexpr int kLevels = 12;
   GridLevelBufs lv[kLevels];
-  DevBuf<uint8_t> raw, out, processed, processed_s, sort_tmp, dflags;
+  DevBuf<uint8_t> raw, out, processed, processed_s, sort_tmp, dflags, fs_scr;
   DevBuf<float> x, y, z, qx, qy, qz, partial;
   DevBuf<uint32_t> keys_in, keys_out, counters;
   DevBuf<int32_t> idx_in, queue, cand, ids, ids_alt, pos_of, nn;
@@ -119,6 +119,7 @@ struct NormalsWork {
   void release() {
     for (auto& l : lv) l.release();
     raw.release(); out.release(); processed.release(); processed_s.release(); sort_tmp.release(); dflags.release();
+    fs_scr.release();
     x.release(); y.release(); z.release(); qx.release(); qy.release(); qz.release();
     partial.release(); nn.release();
     keys_in.release(); keys_out.release(); counters.release();

@@ -789,32 +789,11 @@ __global__ __launch_bounds__(kBS) void k_gather3(const int32_t* __restrict__ src
   OZ[i] = Z[j];
 }
 
-// the reference's centroid: sequential float sums in index order, then / float(n).  One block;
-// lanes 0, 1, 2 run the x, y, z chains over LDS-staged chunks (bit-exact with the serial loop).
-__global__ __launch_bounds__(256) void k_seq_centroid(const float* __restrict__ X,
-                                                      const float* __restrict__ Y,
-                                                      const float* __restrict__ Z, int n,
-                                                      float* __restrict__ out) {
-  __shared__ float s[2][3][256];
-  const int lane = threadIdx.x;
-  float acc = 0.0f;
-  int buf = 0;
-  if (lane < n) { s[0][0][lane] = X[lane]; s[0][1][lane] = Y[lane]; s[0][2][lane] = Z[lane]; }
-  for (int base = 0; base < n; base += 256) {
-    __syncthreads();
-    const int nb = base + 256;  // prefetch the next chunk while lanes 0-2 sum this one
-    if (nb + lane < n) {
-      s[buf ^ 1][0][lane] = X[nb + lane];
-      s[buf ^ 1][1][lane] = Y[nb + lane];
-      s[buf ^ 1][2][lane] = Z[nb + lane];
-    }
-    if (lane < 3) {
-      const int m = min(256, n - base);
-      for (int k = 0; k < m; ++k) acc += s[buf][lane][k];
-    }
-    buf ^= 1;
-  }
-  if (lane < 3) out[lane] = acc / (float)n;
+// the reference's centroid (PlaneDetect.h:463-471): the three sequential float sums (fsum's
+// chains 6-8, exact in parallel) divided by float(n), correctly rounded as on the host
+__global__ void k_centroid_div(const float* __restrict__ sums3, int n, float* __restrict__ out) {
+  const int k = threadIdx.x;
+  if (k < 3) out[k] = sums3[k] / (float)n;
 }
 
 __global__ __launch_bounds__(kBS) void k_translate(float* __restrict__ X, float* __restrict__ Y,
@@ -1332,10 +1311,9 @@ void launch_gather3(const int32_t* src, int n, const float* X, const float* Y, c
   hipLaunchKernelGGL(k_gather3, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, src, n, X, Y, Z, OX, OY, OZ);
 }
 
-void launch_seq_centroid(const float* X, const float* Y, const float* Z, int n, float* out,
-                         hipStream_t s) {
+void launch_centroid_div(const float* sums3, int n, float* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_seq_centroid, dim3(1), dim3(256), 0, s, X, Y, Z, n, out);
+  hipLaunchKernelGGL(k_centroid_div, dim3(1), dim3(64), 0, s, sums3, n, out);
 }
 
 void launch_translate(float* X, float* Y, float* Z, int n, const float* p, hipStream_t s) {

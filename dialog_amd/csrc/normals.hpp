@@ -121,9 +121,8 @@ hipError_t select_flagged(void* tmp, size_t tmp_bytes, const uint8_t* flags, int
                           uint32_t* n_out, hipStream_t s);
 void launch_gather3(const int32_t* src, int n, const float* X, const float* Y, const float* Z,
                     float* OX, float* OY, float* OZ, hipStream_t s);
-// out[0..2] = (sequential float sum of X, Y, Z) / float(n), exactly the reference's loop
-void launch_seq_centroid(const float* X, const float* Y, const float* Z, int n, float* out,
-                         hipStream_t s);
+// out[0..2] = sums3[0..2] / float(n) (sums3: fsum's x, y, z chain end values)
+void launch_centroid_div(const float* sums3, int n, float* out, hipStream_t s);
 void launch_translate(float* X, float* Y, float* Z, int n, const float* p, hipStream_t s);
 // index-ordered maximal independent set of the radius graph, one round over the undecided
 // sorted positions (qlist == nullptr: all); state: 0 undecided, 1 kept, 2 removed

@@ -77,6 +77,29 @@ def test_gpu_preprocess_bit_exact(gpu_ctx, n, seed, r, translate, nan_every, qua
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["offset", "centred", "quantised"])
+def test_gpu_preprocess_centroid_large(gpu_ctx, kind):
+    """The translation at sizes past fsum's chunk / unit / window boundaries (PlaneDetect.h:463-471:
+    p.x += x_i in index order, then / float(n)); np.cumsum is the literal sequential float loop.
+    'centred' makes the chains hover around zero (the walk's slow, start-dependent windows)."""
+    import dialog_amd as D
+    rng = np.random.default_rng({"offset": 11, "centred": 12, "quantised": 13}[kind])
+    n = {"offset": 1_000_003, "centred": 2_000_000, "quantised": 1_500_001}[kind]
+    p = rng.normal(0.0, 3.0, (n, 3)).astype(np.float32)
+    if kind == "offset":
+        p += np.float32([120.0, -45.0, 7.5])
+    elif kind == "quantised":
+        p = (np.round(p / 0.001) * 0.001 + 2.0).astype(np.float32)
+    p[rng.choice(n, 97, replace=False), 1] = np.nan  # dropped before the sums
+    _, g_idx, g_tr = D.preprocess(p, 0.0, True, ctx=gpu_ctx)
+    q = p[np.all(np.isfinite(p), axis=1)]
+    assert 0 < len(g_idx) <= len(q)  # (the translation comes before redundancy removal)
+    want = np.array([np.cumsum(q[:, k], dtype=np.float32)[-1] for k in range(3)], np.float32)
+    want = (want / np.float32(len(q))).astype(np.float32)
+    np.testing.assert_array_equal(np.asarray(g_tr, np.float32).view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_gpu_preprocess_edges(gpu_ctx):
     import dialog_amd as D
     # all NaN, empty, PointXYZ stride, capacity error
