@@ -517,7 +517,22 @@ __global__ __launch_bounds__(kBS) void k_nbr_normals(
   const int k = cnt[i];
   float a[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const uint64_t* seg = keys + off[i];
-  for (int e = 0; e < k; ++e) {
+  // eight neighbours' keys, then their 24 coordinate gathers, issued before any is summed (the
+  // gathers are random over the cloud: one key -> coordinates latency per 8 terms, not per term);
+  // the sums still run in list order
+  constexpr int kB = 8;
+  int e = 0;
+  for (; e + kB <= k; e += kB) {
+    int j[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) j[u] = (int)(uint32_t)seg[e + u];
+    float px[kB], py[kB], pz[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) { px[u] = X[j[u]]; py[u] = Y[j[u]]; pz[u] = Z[j[u]]; }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) pcl_accu_add(a, px[u], py[u], pz[u]);
+  }
+  for (; e < k; ++e) {
     const int j = (int)(uint32_t)seg[e];
     pcl_accu_add(a, X[j], Y[j], Z[j]);
   }
