@@ -381,6 +381,7 @@ __global__ __launch_bounds__(kBS) void k_nbr_count(
       for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
         for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
           const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+#pragma unroll 4  // (the cell's loads issued together)
           for (int u = rg.x; u < rg.y; ++u)
             c += flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2 ? 1 : 0;
         }
@@ -409,6 +410,7 @@ __global__ __launch_bounds__(kBS) void k_nbr_fill(
     for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1); ++y)
       for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1); ++x) {
         const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+#pragma unroll 4
         for (int u = rg.x; u < rg.y; ++u) {
           const float d2 = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
           if (d2 < r2)
@@ -517,10 +519,10 @@ __global__ __launch_bounds__(kBS) void k_nbr_normals(
   const int k = cnt[i];
   float a[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const uint64_t* seg = keys + off[i];
-  // eight neighbours' keys, then their 24 coordinate gathers, issued before any is summed (the
-  // gathers are random over the cloud: one key -> coordinates latency per 8 terms, not per term);
+  // sixteen neighbours' keys, then their 48 coordinate gathers, issued before any is summed (the
+  // gathers are random over the cloud: one key -> coordinates latency per 16 terms, not per term);
   // the sums still run in list order
-  constexpr int kB = 8;
+  constexpr int kB = 16;
   int e = 0;
   for (; e + kB <= k; e += kB) {
     int j[kB];
@@ -842,12 +844,25 @@ __global__ __launch_bounds__(kBS) void k_mis_round(
     for (int y = max(cy - 1, 0); y <= min(cy + 1, G.g[1] - 1) && !kept_nb; ++y)
       for (int x = max(cx - 1, 0); x <= min(cx + 1, G.g[0] - 1) && !kept_nb; ++x) {
         const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
-        for (int v = rg.x; v < rg.y; ++v) {
-          if (sidx[v] >= j) continue;
-          if (!(flann_d2(qx, qy, qz, sx[v], sy[v], sz[v]) < r2)) continue;
-          const uint8_t st = __hip_atomic_load(&state[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (st == 1) { kept_nb = true; break; }
-          if (st == 0) all_removed = false;
+        // four cell points' (immutable) index and coordinates loaded together; the state of a
+        // lower-index neighbour is read as before, one candidate at a time
+        for (int v0 = rg.x; v0 < rg.y && !kept_nb; v0 += 4) {
+          int ci[4];
+          float px[4], py[4], pz[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int v = min(v0 + k, rg.y - 1);
+            ci[k] = sidx[v]; px[k] = sx[v]; py[k] = sy[v]; pz[k] = sz[v];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int v = v0 + k;
+            if (kept_nb || v >= rg.y || ci[k] >= j) continue;
+            if (!(flann_d2(qx, qy, qz, px[k], py[k], pz[k]) < r2)) continue;
+            const uint8_t st = __hip_atomic_load(&state[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st == 1) kept_nb = true;
+            else if (st == 0) all_removed = false;
+          }
         }
       }
   if (active && kept_nb) {
@@ -951,14 +966,27 @@ __global__ __launch_bounds__(kBS) void k_bfs2_claim(
     const int z = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]) + c / 9 - 1;
     if (x < 0 || y < 0 || z < 0 || x >= G.g[0] || y >= G.g[1] || z >= G.g[2]) continue;
     const int2 rg = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
-    for (int u = rg.x; u < rg.y; ++u) {
-      if (processed_s[u]) continue;
-      if (!(flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) < r2)) continue;
-      if (claim_s[u] <= mypos) continue;  // claims only decrease
-      if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) {
-        const uint32_t p = atomicAdd(&s_n, 1u);
-        if (p < (uint32_t)kStage) s_buf[p] = u;
-        else cand[atomicAdd((unsigned long long*)&st_w[2], 1ull)] = u;
+    // four cell points' state and coordinates loaded together (processed_s is fixed during the
+    // claim pass; claims are a min, so the order the candidates are met in does not matter)
+    for (int u0 = rg.x; u0 < rg.y; u0 += 4) {
+      uint8_t pr[4];
+      float px[4], py[4], pz[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int u = min(u0 + v, rg.y - 1);
+        pr[v] = processed_s[u]; px[v] = sx[u]; py[v] = sy[u]; pz[v] = sz[u];
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int u = u0 + v;
+        if (u >= rg.y || pr[v]) continue;
+        if (!(flann_d2(qx, qy, qz, px[v], py[v], pz[v]) < r2)) continue;
+        if (claim_s[u] <= mypos) continue;  // claims only decrease
+        if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) {
+          const uint32_t p = atomicAdd(&s_n, 1u);
+          if (p < (uint32_t)kStage) s_buf[p] = u;
+          else cand[atomicAdd((unsigned long long*)&st_w[2], 1ull)] = u;
+        }
       }
     }
   }
