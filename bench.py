@@ -353,23 +353,23 @@ def main():
         extras["pruned_work"] = {
             "pairs_evaluated_per_launch": round(st["pairs"] / nl),
             "pair_fraction": round(st["pairs"] / max(full_pairs, 1.0), 5),
-            "blocks_per_launch": round(st["blocks"] / nl),
-            "block_fill": round(st["pairs"] / max(32.0 * st["blocks"], 1.0), 4),
-            "redecided_block_fraction": round(st["redecided_blocks"] / max(st["blocks"], 1), 4),
+            "passes_per_launch": round(st["blocks"] / nl),
+            "pass_fill": round(st["pairs"] / max(128.0 * st["blocks"], 1.0), 4),
             "tile_list_entries_per_launch": round(st["list_entries"] / nl),
             "evaluated_tests_per_step": int(32 * st["pairs"] * world),
-            "note": "(tile, plane) pairs the bounding spheres could not rule out, each scored as "
-                    "32 point tests in a 32x32 bf16 matrix-core block; `value` counts PCL's "
-                    "tests (iterations x active points), the kernel evaluates pair_fraction of them"}
+            "note": "(tile, plane) pairs the bounding spheres could not rule out, each evaluated "
+                    "as 32 exact PCL-order point tests (k_score_tiles_ex: lanes as planes, two "
+                    "planes of one tile per lane, 64 lanes per pass); `value` counts PCL's tests "
+                    "(iterations x active points), the kernel evaluates pair_fraction of them"}
     ms_per_step = elapsed / a.steps * 1e3
     # dominant kernel: the scoring launch (this rank's launches; tests per rank = scored / world)
     per_rank_tests = scored / world
     avg_launch_ms = score_ms / max(launches, 1)
     ktests_per_s = per_rank_tests / (score_ms / 1e3) if score_ms > 0 else 0.0
     pruned = a.points >= 131072  # (the library builds the Morton copy for such clouds)
-    kname = ("k_prune_supers + k_score_tiles_rl (countWithinDistance over the Morton-ordered copy: "
+    kname = ("k_prune_supers + k_score_tiles_ex (countWithinDistance over the Morton-ordered copy: "
              "super-tile and tile bounding spheres rule out (tile, plane) pairs with no possible "
-             "PCL inlier; the rest as 32x32 bf16 matrix-core blocks + exact band re-decision; "
+             "PCL inlier; the rest evaluated exactly in PCL's f32 op order, lanes as planes; "
              f"{a.hyps} hypotheses/launch)" if pruned else
              "k_score_bf16<8> (countWithinDistance on the bf16 matrix cores + exact band "
              f"re-decision; {a.hyps} hypotheses/launch)")
@@ -469,9 +469,9 @@ def main():
                     roofline["issue_view"] = tj
                     pw = roofline.get("pruned_work")
                     vi = tj.get("per_launch", {}).get("SQ_INSTS_VALU")
-                    if pw and vi and pw["blocks_per_launch"]:
-                        # (wave instructions; blocks from the stats run of the same workload)
-                        tj["valu_insts_per_block"] = round(vi / pw["blocks_per_launch"], 1)
+                    if pw and vi and pw["pairs_evaluated_per_launch"]:
+                        # (wave instructions; pairs from the stats run of the same workload)
+                        tj["valu_insts_per_pair"] = round(vi / pw["pairs_evaluated_per_launch"], 2)
             except Exception:
                 pass
 

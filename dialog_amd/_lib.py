@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("DLG_AB_LIB") or os.path.join(HERE, "libdialog_amd.so")  # (A/B tooling)
+LIB_PATH = os.path.join(HERE, "libdialog_amd.so")  # (A/B tooling rebinds it: tools/with_lib.py)
 
 DLG_OK = 0
 DLG_ERR_CAPACITY = 5
@@ -42,6 +42,9 @@ DLG_OPT_SCORE_KERNEL = 5
 DLG_OPT_PRUNE_STATS = 6
 DLG_OPT_SELECT_TILE = 7
 DLG_OPT_PCL_REFIT_DEVICE = 8
+DLG_OPT_PRUNE_TILE_SCORER = 9
+DLG_TILE_EXACT = 0
+DLG_TILE_BF16 = 1
 DLG_SCORE_EXACT = 0
 DLG_SCORE_BF16 = 1
 DLG_SCORE_PRUNED = 2
@@ -95,6 +98,8 @@ def load():
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
+        if LIB_PATH != os.path.join(HERE, "libdialog_amd.so"):
+            raise RuntimeError(f"{LIB_PATH}: no such library")
         from . import build as _b
         _b.build()
     L = C.CDLL(LIB_PATH)

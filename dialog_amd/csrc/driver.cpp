@@ -541,7 +541,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
                           c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), nullptr,
                           fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
-                          ext_ev ? c->ev[1] : nullptr);
+                          ext_ev ? c->ev[1] : nullptr, c->opt.tile_scorer);
     } else
       launch_score(src, c->hyps.p, D, cthr, c->res.p, c->opt.score_kernel, c->num_cus, c->stream);
     HIPCHK(hipGetLastError());
@@ -1647,7 +1647,8 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int kernel, int
         c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
         unsigned long long* stp = prune_stats_ptr(c);
         launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, prune_margin(cthr, cl->amax),
-                            cl->amax, c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream, stp);
+                            cl->amax, c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream, stp,
+                            nullptr, nullptr, nullptr, nullptr, c->opt.tile_scorer);
       } else {
         launch_score(src, c->hyps.p, D, cthr, c->res.p, variant, c->num_cus, c->stream);
       }
@@ -1697,6 +1698,11 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         if (value < 0 || value > 3) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PCL_REFIT_DEVICE: 0..3");
         o.pcl_dev = (int)value;
         break;
+      case DLG_OPT_PRUNE_TILE_SCORER:
+        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && !(value >= 11 && value <= 14))
+          throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
+        o.tile_scorer = value == DLG_TILE_EXACT ? kTileScorerExact : value == DLG_TILE_BF16 ? kTileScorerBf16 : (int)value;
+        break;
       default: throw DlgError(DLG_ERR_INVALID, "unknown option");
     }
   });
@@ -1714,6 +1720,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_PRUNE_STATS: *value = o.prune_stats; break;
     case DLG_OPT_SELECT_TILE: *value = o.sel1_tile; break;
     case DLG_OPT_PCL_REFIT_DEVICE: *value = o.pcl_dev; break;
+    case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer == kTileScorerExact ? DLG_TILE_EXACT : DLG_TILE_BF16; break;
     default: return DLG_ERR_INVALID;
   }
   return DLG_OK;

@@ -163,6 +163,7 @@ struct PathOptions {
   int score_kernel = kScoreBf16;  // exhaustive scorer: kScoreBf16 or kScoreExact
   bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
   int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
+  int tile_scorer = 0;            // pruned plane scorer: kTileScorerExact or kTileScorerBf16
   // PCL float refit (DLG_REFIT_PCL, one rank): 1 = the nine sums on the device (fsum.hip,
   // exact), 0 = gathered to the host and summed there, 2 = device, and the host recomputes the
   // refit's tail from the published sums every round, 3 = as 2 and the round's select is always

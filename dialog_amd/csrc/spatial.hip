@@ -598,6 +598,236 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_score_tiles_ex (default tile scorer, SACMODEL_PLANE): the near (tile, plane) pairs evaluated
+// exactly in PCL's op order with lanes as planes.  Same items, claims, plane lists and tile-sphere
+// tests as k_score_tiles_rl, but a near pair is queued as (plane | tile slot << 12) and every 64
+// queued pairs form one pass: lane l takes pair l, reads its plane from LDS and walks the 32
+// points of its tile, which every lane reads from the wave's LDS tile slots with uniform (or at
+// most four distinct, bank-disjoint) ds_read_b128 addresses.  Per test: PCL's 3 mul + 3 add, the
+// |d| < cthr compare and the count add; 32 independent tests per lane per pass, no band, no
+// re-decision, no cross-lane traffic.  (k_score_tiles_rl spends ~178 VALU instructions per 32 x 32
+// block on the B split, the two MFMAs' post-processing and the band check, along one dependent
+// chain per block: VALU active 0.28 at 4 waves/SIMD.)  Points past n are stored as NaN (never an
+// inlier: PCL's NaN < thr is false), so the pass has no validity test.
+// The wave's four tile slots hold two items (slot pair = item sequence & 1): a pass may mix the
+// leftover pairs of the previous item with the current item's, and leftovers whose slots are about
+// to be overwritten are flushed first.
+constexpr int kExRing = 1024;  // >= 64 K - 1 queued + 256 appended per list step + K - 1 pad
+constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad (slot bases 0,
+                               // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
+constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
+
+template <int BS, int K>
+__global__ __launch_bounds__(BS) void k_score_tiles_ex(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
+    const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
+    const int32_t* __restrict__ lp_n, int blk_cap, int xcd, const HypRec* __restrict__ hyps,
+    int D, float cthr, float margin, int32_t* __restrict__ counts,
+    unsigned long long* __restrict__ stats, PickArgs pick_args) {
+  static_assert(K == 1 || K == 2 || K == 4, "planes per lane");
+  constexpr int kChunk = 2;  // tiles per item
+  __shared__ float4 s_cf[kMaxHypPerLaunch];
+  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves: <= 65535 points per workgroup
+  __shared__ __attribute__((aligned(8))) uint16_t s_ring[BS / kWave][kExRing];
+  __shared__ __attribute__((aligned(16))) float s_pt[BS / kWave][4 * kExSlotF];
+  __shared__ unsigned long long s_st[6];
+  __shared__ int s_taken;
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  for (int j = threadIdx.x; j < D; j += BS) {
+    const HypRec h = hyps[j];
+    s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
+  }
+  if (threadIdx.x == 0) s_taken = 0;
+  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += BS) s_cnt[j] = 0u;
+  if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
+  __syncthreads();
+  const int ntiles = (n + kTileP - 1) / kTileP;
+  const int nitems = (ntiles + kChunk - 1) / kChunk;
+  uint16_t* ring = s_ring[wv];
+  float* spt = s_pt[wv];
+  const int ips = kSuperTiles / kChunk;
+  auto claim = [&]() -> int {  // as k_score_tiles_rl (XCD-aware or interleaved items)
+    int v = nitems;
+    if (lane == 0) {
+      const int k = atomicAdd(&s_taken, 1);
+      if (k < blk_cap) {
+        if (xcd) {
+          const int64_t l = (int64_t)k * (gridDim.x >> 3) + (blockIdx.x >> 3);
+          const int64_t s = (int64_t)(blockIdx.x & 7) + 8 * (l / ips);
+          v = (int)min((int64_t)nitems, s * ips + l % ips);
+        } else {
+          v = (int)min((int64_t)nitems, (int64_t)blockIdx.x + (int64_t)k * gridDim.x);
+        }
+      }
+    }
+    return __shfl(v, 0);
+  };
+  // lane l holds point l of an item (its two tiles); NaN past n
+  auto fetch = [&](int it, float& px, float& py, float& pz) {
+    const int64_t p = (int64_t)it * (kChunk * kTileP) + lane;
+    px = py = pz = __builtin_nanf("");
+    if (it < nitems && p < n) { px = X[p]; py = Y[p]; pz = Z[p]; }
+  };
+  int nq = 0, head = 0;  // ring positions (multiples of K at every tile segment boundary)
+  // the m (<= 64 K, a multiple of K) oldest queued pairs: lane l takes the K consecutive entries
+  // K l .. K l + K - 1 (one tile, K planes), so each point read from LDS serves K planes
+  auto pass = [&](int m) __attribute__((always_inline)) {
+    if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
+    const bool act = lane * K < m;
+    uint32_t e[K];
+    if constexpr (K == 1) {
+      e[0] = act ? (uint32_t)ring[(head + lane) & (kExRing - 1)] : kExPad;
+    } else if constexpr (K == 2) {
+      const uint32_t w = act ? *reinterpret_cast<const uint32_t*>(ring + ((head + 2 * lane) & (kExRing - 1)))
+                             : (kExPad | kExPad << 16);
+      e[0] = w & 0xFFFFu; e[1] = w >> 16;
+    } else {
+      const uint2 w = act ? *reinterpret_cast<const uint2*>(ring + ((head + 4 * lane) & (kExRing - 1)))
+                          : make_uint2(kExPad | kExPad << 16, kExPad | kExPad << 16);
+      e[0] = w.x & 0xFFFFu; e[1] = w.x >> 16; e[2] = w.y & 0xFFFFu; e[3] = w.y >> 16;
+    }
+    float4 cf[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cf[k] = s_cf[e[k] & 0xFFFu];
+      if (e[k] & kExPad) cf[k] = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);  // never counts
+    }
+    const float* b = spt + ((e[0] >> 12) & 3u) * kExSlotF;
+    uint32_t acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0u;
+    // (partly unrolled: fully unrolled, the compiler hoists all 24 LDS reads, 96 VGPRs, and spills)
+#pragma unroll 2
+    for (int p = 0; p < kTileP; p += 4) {
+      const float4 xs = *reinterpret_cast<const float4*>(b + p);
+      const float4 ys = *reinterpret_cast<const float4*>(b + kTileP + p);
+      const float4 zs = *reinterpret_cast<const float4*>(b + 2 * kTileP + p);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float4 c = cf[k];
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.x, ys.x, zs.x)) < cthr ? 1u : 0u;
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.y, ys.y, zs.y)) < cthr ? 1u : 0u;
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.z, ys.z, zs.z)) < cthr ? 1u : 0u;
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.w, ys.w, zs.w)) < cthr ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = (int)(e[k] & 0xFFFu);
+      if (acc[k]) atomicAdd(&s_cnt[j >> 1], acc[k] << (16 * (j & 1)));  // (pads count 0)
+    }
+    head += m;
+  };
+  // close a tile segment: pad it to a multiple of K entries (one tile per lane item)
+  auto pad = [&](uint32_t tag) {
+    if constexpr (K > 1) {
+      const int r = (K - (nq & (K - 1))) & (K - 1);
+      if (lane < r) ring[(nq + lane) & (kExRing - 1)] = (uint16_t)(tag | kExPad);
+      nq += r;
+      __builtin_amdgcn_wave_barrier();
+      while (nq - head >= K * kWave) pass(K * kWave);
+    }
+  };
+  int it_next = claim();
+  float px, py, pz;
+  fetch(it_next, px, py, pz);
+  for (int seq = 0;; ++seq) {
+    const int it = it_next;
+    if (it >= nitems) break;
+    it_next = claim();
+    const int t0 = it * kChunk, t_end = min(ntiles, t0 + kChunk);
+    const int sidx = t0 / kSuperTiles;  // kSuperTiles % kChunk == 0: one super-tile per item
+    const int slot0 = (seq & 1) * 2;
+    // queued leftovers of the item two back use the slots about to be overwritten: score them
+    if (nq > head && ((int)(ring[head & (kExRing - 1)] >> 13) & 1) == (seq & 1)) pass(nq - head);
+    const float4 tb0 = tiles[t0];
+    const float4 tb1 = t0 + 1 < t_end ? tiles[t0 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int nlp = lp_n[sidx];
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
+    {
+      float* d = spt + (slot0 + (lane >> 5)) * kExSlotF + (lane & 31);
+      __builtin_amdgcn_wave_barrier();
+      d[0] = px; d[kTileP] = py; d[2 * kTileP] = pz;
+      __builtin_amdgcn_wave_barrier();
+    }
+    fetch(it_next, px, py, pz);  // the next item's points, in flight during this one
+#pragma unroll 1
+    for (int lb = 0; lb < nlp; lb += kListCap) {
+      const int le = min(nlp, lb + kListCap);
+      uint32_t L[kListRegs];
+#pragma unroll
+      for (int k = 0; k < kListRegs; ++k) {
+        const int e = lb + 2 * (lane + k * kWave);
+        L[k] = e < le ? lw[(lb >> 1) + lane + k * kWave] : 0u;
+        if (e + 1 >= le) L[k] &= 0xFFFFu;
+      }
+#pragma unroll 1
+      for (int t = t0; t < t_end; ++t) {
+        const float4 tb = t == t0 ? tb0 : tb1;
+        const uint32_t tag = (uint32_t)(slot0 + (t - t0)) << 12;
+        const float tlim = prune_lim(margin, tb.w);
+        if (stats && lane == 0) { atomicAdd(&s_st[2], 1ull); atomicAdd(&s_st[1], (unsigned long long)(le - lb)); }
+        const f32x2 tbx = {tb.x, tb.x}, tby = {tb.y, tb.y}, tbz = {tb.z, tb.z};
+        auto test4 = [&](uint32_t wa, uint32_t wb, int ea) {
+          const int j0 = (int)(wa & 0xFFFFu), j1 = (int)(wa >> 16);
+          const int j2 = (int)(wb & 0xFFFFu), j3 = (int)(wb >> 16);
+          const float4 c0 = s_cf[j0], c1 = s_cf[j1], c2 = s_cf[j2], c3 = s_cf[j3];
+          const f32x2 ax2 = {c0.x, c1.x}, ay2 = {c0.y, c1.y}, az2 = {c0.z, c1.z}, aw2 = {c0.w, c1.w};
+          const f32x2 bx2 = {c2.x, c3.x}, by2 = {c2.y, c3.y}, bz2 = {c2.z, c3.z}, bw2 = {c2.w, c3.w};
+          const f32x2 ha = __builtin_elementwise_fma(ax2, tbx, __builtin_elementwise_fma(ay2, tby,
+                                                     __builtin_elementwise_fma(az2, tbz, aw2)));
+          const f32x2 hb = __builtin_elementwise_fma(bx2, tbx, __builtin_elementwise_fma(by2, tby,
+                                                     __builtin_elementwise_fma(bz2, tbz, bw2)));
+          const int eb = ea + 2 * kWave;
+          const bool n0 = ea < le && fabsf(ha.x) <= tlim;
+          const bool n1 = ea + 1 < le && fabsf(ha.y) <= tlim;
+          const bool n2 = eb < le && fabsf(hb.x) <= tlim;
+          const bool n3 = eb + 1 < le && fabsf(hb.y) <= tlim;
+          const uint64_t m0 = ballot(n0), m1 = ballot(n1), m2 = ballot(n2), m3 = ballot(n3);
+          const int k0 = (int)__popcll(m0), k1 = k0 + (int)__popcll(m1), k2 = k1 + (int)__popcll(m2);
+          if (n0) ring[(nq + lanes_below(m0)) & (kExRing - 1)] = (uint16_t)(tag | (uint32_t)j0);
+          if (n1) ring[(nq + k0 + lanes_below(m1)) & (kExRing - 1)] = (uint16_t)(tag | (uint32_t)j1);
+          if (n2) ring[(nq + k1 + lanes_below(m2)) & (kExRing - 1)] = (uint16_t)(tag | (uint32_t)j2);
+          if (n3) ring[(nq + k2 + lanes_below(m3)) & (kExRing - 1)] = (uint16_t)(tag | (uint32_t)j3);
+          nq += k2 + (int)__popcll(m3);
+          __builtin_amdgcn_wave_barrier();
+          while (nq - head >= K * kWave) pass(K * kWave);
+        };
+        uint32_t R[kListRegs];
+#pragma unroll
+        for (int k = 0; k < kListRegs; ++k) R[k] = L[k];
+#pragma unroll 1
+        for (int k = 0; lb + k * 2 * kWave < le; k += 2) {
+          test4(R[0], R[1], lb + 2 * (lane + k * kWave));
+#pragma unroll
+          for (int q = 0; q + 2 < kListRegs; ++q) R[q] = R[q + 2];
+        }
+        pad(tag);
+      }
+    }
+  }
+  if (nq > head) pass(nq - head);
+  __syncthreads();
+  for (int j = threadIdx.x; j < D; j += BS) {
+    const int c = (int)((s_cnt[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+    if (c) atomicAdd(&counts[j], c);
+  }
+  if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
+  if (pick_args.done) {  // the fused speculative pick, as in k_score_tiles_rl
+    __builtin_amdgcn_s_waitcnt(0);
+    __shared__ unsigned s_ticket;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_ticket = __hip_atomic_fetch_add(pick_args.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_ticket != gridDim.x - 1) return;
+    if (threadIdx.x == 0)
+      __hip_atomic_store(pick_args.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pick_body<BS, true>(pick_args);
+  }
+}
+
 __global__ void k_gather_nrm(const float4* __restrict__ src, const int32_t* __restrict__ order,
                              int64_t n, float4* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -709,7 +939,8 @@ float np_lim_max(double w, double thr) {  // np_de_limit (np_dev.hpp) on the hos
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float cthr, float margin,
                          const float amax[3], int32_t* counts, uint16_t* lp, int32_t* lp_n,
                          int num_cus, hipStream_t s, unsigned long long* stats, const PrunedNp* np,
-                         const PickArgs* pick, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                         const PickArgs* pick, hipEvent_t ev_start, hipEvent_t ev_stop,
+                         int tile_scorer) {
   if (D <= 0 || v.n <= 0 || D > kMaxHypPerLaunch) {
     if (ev_start) (void)hipEventRecord(ev_start, s);
     if (pick) launch_pick_p1(*pick, s);  // (nothing to score: the pick still runs)
@@ -747,6 +978,14 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     while ((per_xcd + gx / 8 - 1) / (gx / 8) > blk_cap) gx += 8;
     g = gx;
     xcd = 1;
+  }
+  if (!np && tile_scorer != kTileScorerBf16) {
+    auto* kex = tile_scorer == 11 ? k_score_tiles_ex<kBS, 1>
+              : tile_scorer == 14 ? k_score_tiles_ex<kBS, 4> : k_score_tiles_ex<kBS, 2>;
+    hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
+                          0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, blk_cap, xcd, hyps, D,
+                          cthr, margin, counts, stats, pick ? *pick : PickArgs{});
+    return;
   }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;
   hipExtLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop, 0u, v.x, v.y,

@@ -73,6 +73,11 @@ float prune_margin(float cthr, const float amax[3]);
 // amax: the cloud's per-axis max |coordinate| (the scoring band's S bound).
 // list stride per super-tile (D rounded up to 64 entries: dword-aligned entry pairs)
 inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
+// the plane model's (tile, plane) scorer: exact PCL-order evaluation with lanes as planes
+// (k_score_tiles_ex, default) or 32 x 32 bf16 matrix-core blocks with band re-decision
+// (k_score_tiles_rl); identical counts
+constexpr int kTileScorerExact = 0;
+constexpr int kTileScorerBf16 = 1;
 // SACMODEL_NORMAL_PLANE scoring over the spatial copy: its (normalised normal, curvature) per
 // point, and the model's lambda / threshold; margin then comes from prune_margin(lim_max, amax)
 struct PrunedNp {
@@ -86,7 +91,8 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
                          const PrunedNp* np = nullptr,
                          const PickArgs* pick = nullptr,  // fused speculative pick (one rank)
                          hipEvent_t ev_start = nullptr,   // timing events of the launch pair
-                         hipEvent_t ev_stop = nullptr);
+                         hipEvent_t ev_stop = nullptr,
+                         int tile_scorer = kTileScorerExact);
 // the NORMAL_PLANE prefilter limit of the largest w (host restatement of np_de_limit): every
 // point's d_euclid limit is <= this when 0 <= w < 1 for all points; +inf otherwise
 float np_lim_max(double w_max, double thr);

@@ -385,8 +385,9 @@ enum {
   DLG_OPT_PRUNE = 1,        /* Morton copy + pruned countWithinDistance: -1 (default) clouds of
                                >= 131072 points, 0 never, 1 every cloud (applies at upload) */
   DLG_OPT_LEAN_ROUNDS = 2,  /* 1 (default): single-pass selects driven by the Morton copy in
-                               SACMODEL_PLANE extraction (any refit mode on one rank; fast or no
-                               refit at any rank count); 0: two-pass */
+                               SACMODEL_PLANE extraction, in every refit mode and at any rank
+                               count (PCL refit on N > 1 ranks: each rank walks its shard's float
+                               chains); 0: two-pass */
   DLG_OPT_SPEC_PICK = 3,    /* 1 (default): device-side computeModel decision for probability-1
                                rounds (host replay confirms it); 0: host decision only */
   DLG_OPT_PRUNE_NP = 4,     /* 1 (default): pruned SACMODEL_NORMAL_PLANE scoring; 0: exhaustive */
@@ -395,17 +396,22 @@ enum {
   DLG_OPT_PRUNE_STATS = 6,  /* 1: count the pruned kernel's work (dlg_prune_stats); 0 (default) */
   DLG_OPT_SELECT_TILE = 7,  /* points per tile of the lean rounds' single-pass selects: 4096,
                                8192 or 16384 (default) */
-  DLG_OPT_PCL_REFIT_DEVICE = 8 /* DLG_REFIT_PCL: 1 (default) the float sums on the
+  DLG_OPT_PCL_REFIT_DEVICE = 8, /* DLG_REFIT_PCL: 1 (default) the float sums on the
                                device, exact (fsum.hpp); 0 gathered and summed on the host; 2 as 1,
                                the host recomputing every refit's tail from the sums; 3 as 2 and
                                every round's select redone with the host's plane (test) */
+  DLG_OPT_PRUNE_TILE_SCORER = 9 /* the pruned plane scorer's (tile, plane) pairs:
+                               DLG_TILE_EXACT (default) PCL-order f32 with lanes as planes, or
+                               DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band re-decision */
 };
+enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
 dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);
 dlg_status dlg_ctx_get_option(const dlg_ctx* ctx, int option, int64_t* value);
 /* the pruned scoring kernel's counters since DLG_OPT_PRUNE_STATS was set (or the last reset):
  * [0] unused, [1] super-tile list entries tested against tile spheres, [2] tiles visited,
- * [3] 32x32 blocks scored, [4] (tile, plane) pairs scored, [5] blocks with a band re-decision */
+ * [3] 32x32 blocks (DLG_TILE_EXACT: 64-pair passes) scored, [4] (tile, plane) pairs scored,
+ * [5] blocks with a band re-decision (DLG_TILE_BF16 only) */
 dlg_status dlg_prune_stats(dlg_ctx* ctx, uint64_t out[6], int reset);
 
 /* max over ranks of a host double (bench timing) and a barrier; no-ops for world == 1 */

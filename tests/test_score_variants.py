@@ -58,5 +58,12 @@ def test_score_variants_bit_identical(gpu_ctx, case):
             for v in VARIANTS[1:]:
                 got = counts(gpu_ctx, cloud, nh, v, thr)
                 assert np.array_equal(got, ref), (case, nh, v, int((got != ref).sum()))
+            # the pruned path's second tile scorer (bf16 blocks + band re-decision)
+            gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_BF16)
+            try:
+                got = counts(gpu_ctx, cloud, nh, 2, thr)
+            finally:
+                gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_EXACT)
+            assert np.array_equal(got, ref), (case, nh, "pruned_bf16", int((got != ref).sum()))
     finally:
         cloud.close()

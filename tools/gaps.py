@@ -15,7 +15,7 @@ def nm(x):
     return m.group(1) if m else x['Kernel_Name'][:30]
 
 
-idx = [i for i, x in enumerate(r) if 'k_score_tiles_rl' in x['Kernel_Name']]
+idx = [i for i, x in enumerate(r) if 'k_score_tiles' in x['Kernel_Name']]
 seg = r[idx[-rounds] - 2:]
 g = collections.defaultdict(list)
 for a, b in zip(seg, seg[1:]):

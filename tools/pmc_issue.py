@@ -4,7 +4,7 @@ SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BU
 GRBM_GUI_ACTIVE).  Per MI355X_MICROARCH.md: WAVE_CYCLES = ACTIVE_INST_ANY + WAIT_ANY +
 WAIT_INST_ANY (disjoint, quad-cycles); SQ_VALU_MFMA_BUSY_CYCLES counts cycles (32 per 32x32x16 bf16
 MFMA).  Writes profiles/score_issue.json (read by bench.py into roofline.issue_view).
-Usage: python tools/pmc_issue.py <counter_collection.csv> [kernel=k_score_tiles_rl] [num_cus=256]"""
+Usage: python tools/pmc_issue.py <counter_collection.csv> [kernel=k_score_tiles_ex] [num_cus=256]"""
 import collections
 import csv
 import json
@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     path = sys.argv[1]
-    kern = sys.argv[2] if len(sys.argv) > 2 else "k_score_tiles_rl"
+    kern = sys.argv[2] if len(sys.argv) > 2 else "k_score_tiles_ex"
     cus = int(sys.argv[3]) if len(sys.argv) > 3 else 256
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):

@@ -1,6 +1,7 @@
 """A/B of the scoring kernels on the GPU (one process, interleaved rounds, counts checked equal
 across kernels).  Usage: python tools/score_ab.py [n_points] [D] [rounds]
-KERNELS=0,1,2 (DLG_SCORE_EXACT, DLG_SCORE_BF16, DLG_SCORE_PRUNED); PRUNE_STATS=1 also prints the
+KERNELS=0,1,2,3 (DLG_SCORE_EXACT, DLG_SCORE_BF16, DLG_SCORE_PRUNED with the exact lanes-as-planes
+tile scorer, DLG_SCORE_PRUNED with the bf16-block tile scorer); PRUNE_STATS=1 also prints the
 pruned kernel's work counters per launch (dlg_prune_stats).  The round-1 A/B of the retired
 variants (FMA prefilters, scalar coefficients, f32 MFMA, lanes-as-planes) is recorded in
 profiles/r01_score_variants_ab.json and DESIGN.md."""
@@ -17,14 +18,16 @@ import dialog_amd as D  # noqa: E402
 from dialog_amd import _lib  # noqa: E402
 from dialog_amd.synth import SEED_BASE, plane_cloud  # noqa: E402
 
-NAMES = {0: "exact_p4", 1: "bf16_t8", 2: "pruned"}
+NAMES = {0: "exact_p4", 1: "bf16_t8", 2: "pruned_ex", 3: "pruned_bf16", 5: "pruned_ex_k1",
+         6: "pruned_ex_k4"}
+TILE_OPT = {3: 1, 5: 11, 6: 14}  # DLG_OPT_PRUNE_TILE_SCORER per variant (A/B-only values 11..14)
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
     nh = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    variants = [int(v) for v in os.environ.get("KERNELS", "2,1").split(",")]
+    variants = [int(v) for v in os.environ.get("KERNELS", "2,3").split(",")]
     want_stats = os.environ.get("PRUNE_STATS") == "1"
     pts, _, _ = plane_cloud(n, 20, seed=SEED_BASE + 3, shard=0)
     ctx = D.Context(0)
@@ -38,7 +41,8 @@ def main():
         for v in variants:
             ms = C.c_double()
             cnt = np.zeros(nh, np.int32)
-            ctx.check(L.dlg_score_benchmark(ctx.h, cloud.h, nh, v, 3, 0.02, C.byref(ms),
+            ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, TILE_OPT.get(v, D.DLG_TILE_EXACT))
+            ctx.check(L.dlg_score_benchmark(ctx.h, cloud.h, nh, min(v, 2), 3, 0.02, C.byref(ms),
                                             cnt.ctypes.data_as(C.POINTER(C.c_int32))))
             res[v].append(ms.value)
             if ref is None:
@@ -53,7 +57,7 @@ def main():
     extra = {}
     if want_stats:
         st = ctx.prune_stats(reset=True)
-        launches = rounds * 3 if 2 in variants else 0
+        launches = rounds * 3 * sum(v >= 2 for v in variants)
         if launches:
             extra["pruned_per_launch"] = {k: v / launches for k, v in st.items()}
             extra["pruned_per_launch"]["pair_fraction"] = st["pairs"] / launches / (n * nh / 32)

@@ -53,7 +53,7 @@ def main():
                      "--warmup 0; reads x calibration (k_absmax: 12 B/point)",
            "kernels": res, "read_calibration_dword_loads": cal}
     # one scoring launch = k_prune_supers + k_score_tiles (pruned, default), else the exhaustive kernel
-    keys = [k for k in ("k_prune_supers", "k_score_tiles_rl", "k_score_tiles") if k in res][:2] or \
+    keys = [k for k in ("k_prune_supers", "k_score_tiles_ex", "k_score_tiles_rl", "k_score_tiles") if k in res][:2] or \
            (["k_score_bf16"] if "k_score_bf16" in res else ["k_score"])
     if all(k in res for k in keys) and cal:
         out["kernel"] = " + ".join(keys)
