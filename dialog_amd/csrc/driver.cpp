@@ -706,9 +706,12 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         // inliers stamped into a bitmap over pristine indices from the Morton copy's near tiles,
         // compacted in ascending pristine order = list order
         const int64_t nw = (cl->n_total + 31) / 32;
-        if (cl->ubits.cap < (size_t)nw + 16) {
+        if (cl->ubits.cap < (size_t)nw + 16 || cl->ubits_dirty) {
+          // (new, or left stamped by an extraction that failed between the stamp and the
+          // compaction, which clears every word it reads)
           cl->ubits.ensure((size_t)nw + 16);
           HIPCHK(hipMemsetAsync(cl->ubits.p, 0, cl->ubits.cap * sizeof(uint32_t), c->stream));
+          cl->ubits_dirty = false;
         }
         ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n), ucompact_tiles(nw));
         c->fs_x.ensure((size_t)std::max<int64_t>(src.n, 1));
@@ -716,10 +719,13 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         c->fs_z.ensure((size_t)std::max<int64_t>(src.n, 1));
         c->fs_n.ensure(1);
         const SpatialView sv = spatial_view(cl);
+        cl->ubits_dirty = true;
         launch_ustamp(sp_cur_view(), sv.tiles, sv.supers, pmargin, bc_dev, mt, cl->ubits.p,
                       c->stream);
         launch_ucompact(cl->ubits.p, nw, cl->pristine.view(cl->n_total), c->sel1, c->fs_x.p,
                         c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
+        HIPCHK(hipGetLastError());
+        cl->ubits_dirty = false;
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
                         rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
                         walk_ev(1));
@@ -1594,6 +1600,7 @@ dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float c
     HIPCHK(hipMemcpyAsync(dc.p, &ci, 16, hipMemcpyHostToDevice, c->stream));
     double total = 0.0;
     for (int r = 0; r < reps; ++r) {
+      if (walk_stats) HIPCHK(hipMemsetAsync(wst.p, 0, 72 * 8, c->stream));  // (the last call's)
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
       launch_fs_refit(dx.p, dx.p + 1, dx.p + 2, 3, dn.p, std::max<int64_t>(n, 1), b, dc.p,
                       dc.p + 1, dres.p, c->num_cus, c->stream);

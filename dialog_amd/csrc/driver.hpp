@@ -164,7 +164,7 @@ struct PathOptions {
   bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
   int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
   int tile_scorer = 0;            // pruned plane scorer: kTileScorerExact or kTileScorerBf16
-  // PCL float refit (DLG_REFIT_PCL, one rank): 1 = the nine sums on the device (fsum.hip,
+  // PCL float refit (DLG_REFIT_PCL, any rank count): 1 = the nine sums on the device (fsum.hip,
   // exact), 0 = gathered to the host and summed there, 2 = device, and the host recomputes the
   // refit's tail from the published sums every round, 3 = as 2 and the round's select is always
   // redone with the host's plane (exercises the path an uncertain transcendental takes)
@@ -301,6 +301,7 @@ struct dlg_cloud {
   bool buf_lean[2] = {false, false};
   bool list_lean() const { return cur >= 0 && buf_lean[cur]; }
   DevBuf<uint32_t> ubits;  // PCL refit in lean rounds: unrefined inliers by pristine index (zero between rounds)
+  bool ubits_dirty = false;  // stamped but not (known to be) compacted: cleared before next use
   DevBuf<uint8_t> tag;  // per pristine point: the stamp of the select that took it
   int tagv = 0;         // last stamp used (tag[] is zeroed when the byte wraps)
 };

@@ -440,12 +440,79 @@ __device__ __forceinline__ void fs_seq_prep(const FsWalkRec wr, int cnt, int lan
   *sq2 = make_uint4(fl, __float_as_uint(Qf), 0u, 0u);
 }
 
+// Window transfer table (the walk's lookup for a window it would walk record by record): the
+// window's records applied to each of the 64 entry leads -kFtLo..63-kFtLo at once, lane = entry
+// lead L (entering at t = g_0 + L Q, Q the window's smallest quantum).  Record k is applied as
+// fs_seq_window applies it: covered by the lemma (member i = (L_k >> s_k) & 3, the grid, margin
+// and quanta conditions) it steps L_{k+1} = L_k + E_k[i]; otherwise the lane reruns the chunk's
+// terms (LDS, in order, a wave-uniform loop) from its exact start g_k + L_k Q and re-expresses
+// the result as a lead on g_{k+1}.  A lane whose start or re-expressed lead is not exact is
+// dropped.  Every lane kept holds the window's exit value -- a literal run or lemma-proven shift
+// of the chain from that entry, the value any exact walk carries out of the window -- and its
+// mask bit.  Chains hovering near zero (many start-dependent records, a few reruns per window)
+// are then walked one lookup per window instead of record by record.
+constexpr int kFtLo = 32;  // entry leads -kFtLo .. 63 - kFtLo
+__device__ __forceinline__ void fs_wtab_build(const FsDev& d, int c, int64_t u, int nch, int cnt,
+                                              const float* sp, const float4* sn,
+                                              const uint4 (*sq)[3], int lane) {
+  const uint32_t qb = sq[0][2].y;  // the window's Q (every record holds it)
+  const double Q = (double)__uint_as_float(qb), iQ = 1.0 / Q;  // (exact: powers of two)
+  int64_t L = lane - kFtLo;
+  bool ok = nch > 0;
+  float out = 0.0f;
+  for (int k = 0; k < nch; ++k) {
+    const uint4 sq0 = sq[k][0], sq1 = sq[k][1], sq2 = sq[k][2];
+    const float* row = reinterpret_cast<const float*>(&sn[k * 4]);
+    const uint32_t fl = sq2.x;
+    const int sh = (int)(fl & 0xFFu);
+    const bool exact_only = (fl >> 8) & 1u, gfin = (fl >> 9) & 1u;
+    const bool grid = (L & ((1ll << sh) - 1)) == 0;
+    const int i = (int)((L >> sh) & 3);
+    const int64_t D = L - ((int64_t)i << sh);
+    const bool ki = (fl >> (10 + i)) & 1u, ci = (fl >> (14 + i)) & 1u;
+    const int64_t Mi = (int32_t)(i == 0 ? sq1.x : i == 1 ? sq1.y : i == 2 ? sq1.z : sq1.w);
+    bool cov = gfin && (L < 1073741824 && L > -1073741824) && grid && ki &&
+               (D == 0 || (ci && (D < 0 ? -D : D) <= Mi));
+    if (exact_only) cov = gfin && L == 0 && ((fl >> 10) & 1u);
+    const bool last = k == nch - 1;
+    if (cov) {
+      const float oi = row[4 + i];
+      if (last) out = (float)((double)oi + (double)D * Q);  // (exact: the lemma)
+      else L += (int32_t)(i == 0 ? sq0.x : i == 1 ? sq0.y : i == 2 ? sq0.z : sq0.w);
+    }
+    if (ballot(ok && !cov)) {  // the uncovered lanes rerun the chunk from their exact start
+      const double tv = (double)row[0] + (double)L * Q;
+      float v = (float)tv;
+      bool run = ok && !cov && (double)v == tv && (L < 1073741824 && L > -1073741824);
+      const int len = cnt - k * kFsChunk < kFsChunk ? cnt - k * kFsChunk : kFsChunk;
+      if (run) {
+        for (int j = 0; j < len; ++j) v = v + sp[k * kFsPad + j];
+        if (last) {
+          out = v;
+        } else {  // the exact lead on the next record's guess (TwoSum: it must be exact)
+          const double ta = (double)v, gb = -(double)reinterpret_cast<const float*>(&sn[(k + 1) * 4])[0];
+          const double sd = ta + gb, bv = sd - ta;
+          const double er = (ta - (sd - bv)) + (gb - bv);
+          const double Ld = sd * iQ;
+          if (er == 0.0 && Ld == floor(Ld) && fabs(Ld) < 1073741824.0) L = (int64_t)Ld;
+          else run = false;
+        }
+      }
+      if (!cov && !run) ok = false;
+    }
+  }
+  const uint64_t m = ballot(ok);
+  d.b.wtab[((int64_t)c * d.b.wcap + u) * kWave + lane] = out;
+  if (lane == 0) d.b.wmeta[(int64_t)c * d.b.wcap + u] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), qb, 0u);
+}
+
 // ---- k_fs_l1 ----------------------------------------------------------------------------------
 constexpr int kFlBS = kFsUC * kFsFan;  // 64 chunks x 4 members
 __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
   __shared__ float sp[kFsUC * kFsPad];
   __shared__ float4 sn[kFsUC * 4];  // the unit's records, 4 rows of 16 bytes each
   __shared__ float sg[kFsUC];
+  __shared__ uint4 ssq[kFsUC][3];  // the unit's integer-stepping tables (the transfer table's input)
   const int64_t n = *d.n_dev;
   const int64_t U = (n + kFsUnit - 1) / kFsUnit;
   const int t = threadIdx.x;
@@ -568,6 +635,9 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
         uint4* o = d.b.srec + 3 * ((int64_t)c * d.b.cap + u * kFsUC + t);
         o[0] = s0; o[1] = s1; o[2] = s2;
       }
+      ssq[t][0] = s0; ssq[t][1] = s1; ssq[t][2] = s2;
+      __builtin_amdgcn_wave_barrier();
+      fs_wtab_build(d, c, u, nch, cnt, sp, sn, ssq, t);
     }
     __syncthreads();
     for (int p = t; p < nch * 4; p += kFlBS)
@@ -716,8 +786,12 @@ __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int6
 }
 
 struct FsWalkCounters {
-  int64_t win = 0, pass = 0, slow = 0, step = 0, rerun = 0, clk_step = 0, group_fast = 0;
+  int64_t win = 0, pass = 0, slow = 0, step = 0, rerun = 0, clk_step = 0, group_fast = 0, table = 0;
 };
+
+__device__ __forceinline__ float g0f(const float4& sm, int f) {  // the first guess of window f
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm.x), f));
+}
 
 // Exact stepping in integers, lanes f..cnt-1 of a window from the exact value t at lane f.
 // Every value involved (the guesses, the usable members' outputs, the chain's values where a
@@ -929,41 +1003,41 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
   return t;
 }
 
-constexpr int kFwBS = kWave;
-__global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restrict__ start9,
-                                                   const float4* __restrict__ cin,
-                                                   float4* __restrict__ cout,
-                                                   int32_t* __restrict__ res) {
-  __shared__ __attribute__((aligned(16))) char ring[2 * kFsSlotBytes];
-  const int c = blockIdx.x, lane = threadIdx.x;
+// Walks windows [w_lo, w_hi) of chain c from the value t (the batch loop of summaries, window
+// walks and the record ring).  kRecord: vw[w] = the value the walk enters window w with.
+// kRepair (t is the exact start of the span, vw holds a walk of the span from another start):
+// stops at the first window whose entry value equals vw[w] bit for bit -- from there both walks
+// are the same computation -- and returns true.  *tp = the value after the last window walked.
+template <bool kRepair, bool kRecord>
+__device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, float* tp,
+                             int lane, __attribute__((address_space(3))) char* ring,
+                             FsWalkCounters& ct) {
   const int64_t n = *d.n_dev;
   const int64_t K = fs_chunks(n);
   const int64_t NW = (K + kWave - 1) / kWave;
   const FsNode* R = fs_rec(d.b, c, 0);
   const uint4* T = d.b.srec + 3 * (int64_t)c * d.b.cap;
   const float4* S = d.b.win + c * d.b.wcap;
-  float t = start9 ? start9[c] : 0.0f;
-  // walk counters (dlg_float_sums' walk_stats): windows walked record by record, speculation
-  // passes, passes with lanes the fast path could not decide, lanes stepped alone, reruns, clocks
-  // (all, stepping), windows passed by their summaries
-  const int64_t clk0 = d.b.wst ? (int64_t)clock64() : 0;
+  float* V = d.b.vw + c * d.b.wcap;
+  float t = *tp;
   auto slot = [&](int j) {
-    return (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) char*)ring +
-                                                       j * kFsSlotBytes);
+    return (__attribute__((address_space(3))) void*)(ring + j * kFsSlotBytes);
   };
   auto tslot = [&](int j) { return (uint32_t)(uintptr_t)slot(j) + (uint32_t)kFsWinBytes; };
-  FsWalkCounters ct;
   int64_t pre_w = -1;  // the window prefetched into slot pre_s (or none)
   int pre_s = 0;
-  for (int64_t wb = 0; wb < NW; wb += kWave) {
+  bool met = false;
+  for (int64_t wb = w_lo; wb < w_hi && !met; wb += kWave) {
     // the batch's summaries, lane = window; a window is skippable only if its last record also
     // links to the next window's first guess
-    const int nb = NW - wb < kWave ? (int)(NW - wb) : kWave;
+    const int nb = w_hi - wb < kWave ? (int)(w_hi - wb) : kWave;
     float4 sm = make_float4(0.0f, 0.0f, -1.0f, __builtin_nanf(""));
     float gnx = 0.0f;
     const bool has_next = wb + lane + 1 < NW;
     if (lane < nb) sm = S[wb + lane];
     if (lane < nb && has_next) gnx = S[wb + lane + 1].x;
+    const float vb = kRepair && lane < nb ? V[wb + lane] : 0.0f;
+    const uint4 tm = lane < nb ? d.b.wmeta[c * d.b.wcap + wb + lane] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = lane < nb && sm.w == sm.w &&
                        (!has_next || __float_as_uint(sm.y) == __float_as_uint(gnx));
     const uint64_t stat = ballot(lane < nb && !valid);  // (walked at any lag: prefetch candidates)
@@ -980,20 +1054,54 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
                                 dq == floor(dq)));
       const uint64_t nm = ~ballot(ok) & (~0ull << i) & (nb == kWave ? ~0ull : (1ull << nb) - 1);
       const int f = nm ? (int)__builtin_ctzll(nm) : nb;
+      // entry values of windows i..f: linked windows passed with lag dl enter at g0 + dl
+      // (exact: the lemma); window f at t after them
+      const float ent = zero ? sm.x : (float)((double)sm.x + dl);
+      if (kRepair) {
+        if (ballot(lane >= i && lane < f && __float_as_uint(ent) == __float_as_uint(vb))) {
+          met = true;
+          break;
+        }
+      }
+      if (kRecord && lane >= i && lane < f) V[wb + lane] = ent;
       if (f > i) {
         const float ol = rdl(sm.y, f - 1);
         t = zero ? ol : (float)((double)ol + dl);  // (exact: the lemma, record by record)
         ct.group_fast += f - i;
       }
       if (f >= nb) break;
-      // window f record by record
+      if (kRepair && __float_as_uint(t) == __float_as_uint(rdl(vb, f))) {
+        met = true;
+        break;
+      }
+      if (kRecord && lane == 0) V[wb + f] = t;
       const int64_t w = wb + f;
+      {  // the window's transfer table (k_fs_wtab): the exit value when the entry lead is in it
+        const uint64_t tmask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)tm.x, f) |
+                               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)tm.y, f) << 32);
+        if (tmask) {
+          const double Q = (double)__uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)tm.z, f));
+          // the lead t - g_0 with its rounding error (TwoSum: it must be exact), in units of Q
+          const double ta = (double)t, gb = -(double)g0f(sm, f);
+          const double sd = ta + gb, bv = sd - ta;
+          const double er = (ta - (sd - bv)) + (gb - bv);
+          const double Ld = sd * (1.0 / Q) + (double)kFtLo;
+          if (er == 0.0 && Ld == floor(Ld) && Ld >= 0.0 && Ld < (double)kWave &&
+              ((tmask >> (int)Ld) & 1)) {
+            t = d.b.wtab[(c * d.b.wcap + w) * kWave + (int)Ld];
+            ++ct.table;
+            i = f + 1;
+            continue;
+          }
+        }
+      }
+      // window f record by record
       const int cur = pre_w == w ? pre_s : pre_s ^ 1;
       if (pre_w != w) {
         fs_ring_load(R, w * kWave, K, slot(cur), lane);
         fs_seq_load(T, w * kWave, K, tslot(cur), lane);
       }
-      // prefetch the next window the summaries cannot skip at any lag
+      // prefetch the next window the summaries cannot skip at any lag (inside the span)
       const uint64_t nx = f + 1 < kWave ? stat & (~0ull << (f + 1)) : 0ull;
       pre_w = nx ? wb + (int64_t)__builtin_ctzll(nx) : -1;
       pre_s = cur ^ 1;
@@ -1030,10 +1138,44 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
     }
   }
   __builtin_amdgcn_s_waitcnt(0);  // (a last prefetch: never read, but drained)
+  *tp = t;
+  return met;
+}
+
+// The walk: one wave per chain over all its windows.  from_guess (several ranks, rank r > 0):
+// the chain starts from the refined guess at the rank's first inlier instead of its exact start,
+// which only the previous rank can supply, and records every window's entry value for
+// k_fs_repair.  (Walking segments of one chain in parallel from the refined guesses at their
+// starts and repairing each from its predecessor's exact end was measured and dropped: in chains
+// whose sums hover near zero the guess at a segment start is off by many quanta of the small
+// binades there, the two walks never meet, and the repairs walked every segment a second time.)
+// The last chain to finish runs the refit tail when asked.
+constexpr int kFwBS = kWave;
+__global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restrict__ start9,
+                                                   int from_guess, const float4* __restrict__ cin,
+                                                   float4* __restrict__ cout,
+                                                   int32_t* __restrict__ res) {
+  __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
+  auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int64_t n = *d.n_dev;
+  const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
+  // walk counters (dlg_float_sums' walk_stats): windows walked record by record, speculation
+  // passes, passes with lanes the fast path could not decide, lanes stepped alone, reruns, clocks
+  // (all, stepping), windows passed by their summaries
+  const int64_t clk0 = d.b.wst ? (int64_t)clock64() : 0;
+  FsWalkCounters ct;
+  float t = start9 ? start9[c] : 0.0f;
+  if (from_guess) {
+    if (NW > 0) t = fs_rec(d.b, c, 0)->g;
+    fs_walk_span<false, true>(d, c, 0, NW, &t, lane, ring, ct);
+  } else {
+    fs_walk_span<false, false>(d, c, 0, NW, &t, lane, ring, ct);
+  }
   if (d.b.wst && lane == 0) {
     int64_t* w = d.b.wst + 8 * c;
     w[0] = ct.win; w[1] = ct.pass; w[2] = ct.slow; w[3] = ct.step; w[4] = ct.rerun;
-    w[5] = (int64_t)clock64() - clk0; w[6] = ct.clk_step; w[7] = ct.group_fast;
+    w[5] = (int64_t)clock64() - clk0; w[6] = ct.clk_step; w[7] = ct.group_fast + (ct.table << 32);
   }
   __shared__ unsigned s_ticket;
   if (lane == 0) {
@@ -1062,6 +1204,28 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   for (int k = 0; k < kFsChains; ++k) res[2 + k] = __float_as_int(a9[k]);
 }
 
+// several ranks, rank > 0: k_fs_walk ran from the rank's guess (from_guess) while the ranks
+// before it walked theirs; with the exact start from the previous rank, the chain is walked again
+// from it only until it enters a window with the value the recorded walk entered it with (from
+// there both are the same computation, so the recorded end is exact).  A chain whose guess was
+// exact is not walked at all; one with a constant lag passes its windows by their summaries.
+__global__ __launch_bounds__(kFwBS) void k_fs_repair(FsDev d, const float* __restrict__ start9) {
+  __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
+  auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int64_t n = *d.n_dev;
+  const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
+  FsWalkCounters ct;
+  float t = start9[c];
+  if (NW == 0) {  // (an empty shard passes its start on)
+    if (lane == 0) d.b.sums[c] = t;
+    return;
+  }
+  if (__float_as_uint(t) == __float_as_uint(fs_rec(d.b, c, 0)->g)) return;  // (sums: exact)
+  const bool met = fs_walk_span<true, false>(d, c, 0, NW, &t, lane, ring, ct);
+  if (!met && lane == 0) d.b.sums[c] = t;  // (met: the recorded walk's end is exact)
+}
+
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -1073,7 +1237,9 @@ size_t fs_scratch_bytes(int64_t n_cap, int world) {
          align256(sizeof(FsNode) * K * kFsChains) + align256(3 * sizeof(uint4) * K * kFsChains) +
          align256(sizeof(float4) * U * kFsChains) +
          align256(sizeof(float) * 32) +
-         align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) + 256;
+         align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) +
+         align256(sizeof(float) * U * kFsChains) + align256(sizeof(float) * U * kFsChains * kWave) +
+         align256(sizeof(uint4) * U * kFsChains) + 256;
 }
 
 FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
@@ -1104,6 +1270,12 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   p += align256(sizeof(double) * 32);
   b.gath = reinterpret_cast<double*>(p);      // [world][10]
   p += align256(sizeof(double) * (kFsChains + 1) * world);
+  b.vw = reinterpret_cast<float*>(p);
+  p += align256(sizeof(float) * U * kFsChains);
+  b.wtab = reinterpret_cast<float*>(p);
+  p += align256(sizeof(float) * U * kFsChains * kWave);
+  b.wmeta = reinterpret_cast<uint4*>(p);
+  p += align256(sizeof(uint4) * U * kFsChains);
   b.ticket = reinterpret_cast<unsigned*>(p);  // [0]: k_fs_prep / k_fs_inc, [1]: k_fs_walk
   return b;
 }
@@ -1122,22 +1294,29 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
     hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, nullptr);
     hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, nullptr);
     hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-    hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
-                          nullptr, cin, cout, res);
+    hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u,
+                          d, nullptr, 0, cin, cout, res);
     return;
   }
   // several ranks (the list is the ranks' segments in order): each rank's guesses start from the
-  // double totals of the ranks before it; the chains' exact values are handed from rank to rank
-  // (rank r walks from rank r - 1's end values) and the last rank's sums are broadcast
+  // double totals of the ranks before it, and every rank walks its shard at once -- rank 0 from
+  // the exact start, rank r > 0 from the refined guess at its first inlier.  Then the exact values
+  // are handed from rank to rank (RCCL send/recv of 9 floats): rank r repairs its walk from rank
+  // r - 1's end values (k_fs_repair: walked again only until it meets the recorded walk) and
+  // passes its exact end on; the last rank's sums are broadcast
   hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, b.tot);
   comm->allgather(b.tot, b.gath, kFsChains + 1, DType::F64, s);
   hipLaunchKernelGGL(k_fs_base, dim3(1), dim3(256), 0, s, d, b.gath, r, W, b.base9, b.n_global);
   hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, b.base9);
   hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-  if (r > 0) comm->recv(b.start9, kFsChains, DType::I32, r - 1, s);
-  hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
-                        r > 0 ? b.start9 : (const float*)nullptr, (const float4*)nullptr,
-                        (float4*)nullptr, (int32_t*)nullptr);
+  hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0,
+                        r > 0 ? nullptr : ev_walk1, 0u, d, (const float*)nullptr, r > 0 ? 1 : 0,
+                        (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
+  if (r > 0) {
+    comm->recv(b.start9, kFsChains, DType::I32, r - 1, s);
+    hipExtLaunchKernelGGL(k_fs_repair, dim3(kFsChains), dim3(kFwBS), 0, s, nullptr, ev_walk1, 0u,
+                          d, (const float*)b.start9);
+  }
   if (r < W - 1) comm->send(b.sums, kFsChains, DType::I32, r + 1, s);
   comm->broadcast(b.sums, kFsChains, DType::I32, W - 1, s);
   hipLaunchKernelGGL(k_fs_tail, dim3(1), dim3(1), 0, s, b.sums, b.n_global, cin, cout, res);

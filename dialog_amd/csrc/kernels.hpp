@@ -185,8 +185,9 @@ int moments_sp_blocks(int64_t n);
 void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers, float margin,
                        const float4* coef, const ModelTest& mt, int qexp, int64_t* partials,
                        unsigned* done, int nblocks, int64_t* out, float4* cout, hipStream_t s);
-// PCL refit in lean rounds (single rank): the unrefined plane's inliers, stamped into a bitmap
-// over pristine indices from the Morton copy's near tiles (launch_ustamp), then compacted in
+// PCL refit in lean rounds (any rank count: each rank its own shard): the unrefined plane's
+// inliers, stamped into a bitmap over pristine indices from the Morton copy's near tiles
+// (launch_ustamp), then compacted in
 // ascending pristine order = list order into x/y/z arrays (launch_ucompact; clears the bitmap,
 // count -> *n_out).  bits: ceil(n_pristine / 32) words, zero on entry.
 void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, float margin,
@@ -219,6 +220,11 @@ struct FsBuffers {
   double* gath = nullptr;  // [world][10] several ranks: every rank's tot
   unsigned* ticket = nullptr;  // [2], zero on entry
   int64_t* wst = nullptr;      // [9][8] walk counters (dlg_float_sums), or null
+  float* vw = nullptr;         // [9][wcap] several ranks: each window's entry value along the
+                               // walk from the rank's guess (k_fs_repair compares against it)
+  float* wtab = nullptr;       // [9][wcap][64] window transfer tables (k_fs_wtab): exit value for
+                               // entry leads -32..31 (in the window's smallest quantum)
+  uint4* wmeta = nullptr;      // [9][wcap] (valid-entry mask lo, hi, Q bits, 0)
 };
 // bytes of scratch for n_cap inliers; carve() lays the buffers out in `base`
 // (world: the ranks of the communicator passed to launch_fs_refit; comm null or one rank: the

@@ -582,6 +582,9 @@ dlg_status dlg_cloud_estimate_normals(dlg_ctx* c, dlg_cloud* cl, float radius, i
                                       int64_t out_stride_bytes) {
   if (!c || !cl || cl->ctx != c) return DLG_ERR_INVALID;
   return guarded(c, [&] {
+    if (c->comm->world() > 1)
+      throw DlgError(DLG_ERR_INVALID, "dlg_cloud_estimate_normals: the cloud is one rank's shard "
+                                      "(world > 1); its normals need the whole cloud");
     check_normals_args(radius, k_nn, mode);
     if (normals_out && (out_stride_bytes % 4 || (out_stride_bytes != 16 && out_stride_bytes < 32)))
       throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be 16 or >= 32 (multiple of 4)");

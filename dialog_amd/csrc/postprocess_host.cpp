@@ -19,6 +19,7 @@
 #include "driver.hpp"
 #include "grid_host.hpp"
 #include "normals.hpp"
+#include "alpha_shape.hpp"
 #include "postprocess.hpp"
 
 namespace dlg {
@@ -467,173 +468,72 @@ int64_t plane_border(const float* pts, int64_t stride_f, int64_t n, const float 
   compute_point_normal(pts, stride_f, n, prm);  // (NaN with < 3 points)
   if (!(prm[0] == prm[0])) return 0;
   // projPoint2Plane (PlaneDetect.h:1437-1444): lambda = 2.0 * (float dot + d), in double, stored
-  // as float; dest = src - lambda / 2.0 * param (double), stored as float
-  std::vector<float> q(3 * (size_t)n);
+  // as float; dest = src - lambda / 2.0 * param (double), stored as float.  (Non-finite points
+  // are left out: the reference's clouds have none after preProcess.)
+  std::vector<float> q;
+  q.reserve(3 * (size_t)n);
   for (int64_t i = 0; i < n; ++i) {
     const float* p = pts + i * stride_f;
     const float lambda =
         (float)(2.0 * (double)(prm[0] * p[0] + prm[1] * p[1] + prm[2] * p[2] + prm[3]));
-    for (int k = 0; k < 3; ++k) q[3 * i + k] = (float)((double)p[k] - lambda / 2.0 * prm[k]);
+    float d[3];
+    for (int k = 0; k < 3; ++k) d[k] = (float)((double)p[k] - lambda / 2.0 * prm[k]);
+    if (std::isfinite(d[0]) && std::isfinite(d[1]) && std::isfinite(d[2])) q.insert(q.end(), d, d + 3);
   }
-  // in-plane coordinates (double): u = a unit vector across the normal, v = n x u
-  const double nz[3] = {prm[0], prm[1], prm[2]};
-  const int ax = std::fabs(nz[0]) <= std::fabs(nz[1]) && std::fabs(nz[0]) <= std::fabs(nz[2]) ? 0
-                 : std::fabs(nz[1]) <= std::fabs(nz[2]) ? 1 : 2;
-  double u[3] = {0, 0, 0};
-  u[ax] = 1.0;
-  const double dt = u[0] * nz[0] + u[1] * nz[1] + u[2] * nz[2];
-  for (int k = 0; k < 3; ++k) u[k] -= dt * nz[k];
-  const double un = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-  for (int k = 0; k < 3; ++k) u[k] /= un;
-  const double v[3] = {nz[1] * u[2] - nz[2] * u[1], nz[2] * u[0] - nz[0] * u[2],
-                       nz[0] * u[1] - nz[1] * u[0]};
-  std::vector<double> cu(n), cv(n);
-  double lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
-  int64_t finite = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const float* p = &q[3 * i];
-    cu[i] = p[0] * u[0] + p[1] * u[1] + p[2] * u[2];
-    cv[i] = p[0] * v[0] + p[1] * v[1] + p[2] * v[2];
-    if (!std::isfinite(cu[i]) || !std::isfinite(cv[i])) continue;
-    ++finite;
-    lo[0] = std::min(lo[0], cu[i]); hi[0] = std::max(hi[0], cu[i]);
-    lo[1] = std::min(lo[1], cv[i]); hi[1] = std::max(hi[1], cv[i]);
-  }
-  if (finite < 3) return 0;
-  // alpha occupancy: cells of edge alpha (grown until the grid has <= 2^24 cells), a one-cell
-  // empty frame around it
-  double cell = alpha;
-  int64_t gx, gy;
-  for (;;) {
-    gx = (int64_t)std::floor((hi[0] - lo[0]) / cell) + 3;
-    gy = (int64_t)std::floor((hi[1] - lo[1]) / cell) + 3;
-    if (gx * gy <= (int64_t(1) << 24)) break;
-    cell *= 1.5;
-  }
-  std::vector<int32_t> rep((size_t)(gx * gy), -1);  // per cell: its point farthest from the
-  std::vector<int32_t> cid(n, -1);                   // centroid (chosen below), cell of a point
-  for (int64_t i = 0; i < n; ++i) {
-    if (!std::isfinite(cu[i]) || !std::isfinite(cv[i])) continue;
-    const int64_t ix = (int64_t)std::floor((cu[i] - lo[0]) / cell) + 1;
-    const int64_t iy = (int64_t)std::floor((cv[i] - lo[1]) / cell) + 1;
-    cid[i] = (int32_t)(iy * gx + ix);
-    rep[(size_t)cid[i]] = 0;
-  }
-  // the largest 8-connected component of occupied cells
-  std::vector<int32_t> comp((size_t)(gx * gy), -1);
-  int32_t best = -1;
-  int64_t best_sz = 0;
-  std::vector<int64_t> stack;
-  for (int64_t c0 = 0; c0 < gx * gy; ++c0) {
-    if (rep[(size_t)c0] < 0 || comp[(size_t)c0] >= 0) continue;
-    const int32_t id = (int32_t)c0;
-    int64_t sz = 0;
-    stack.assign(1, c0);
-    comp[(size_t)c0] = id;
-    while (!stack.empty()) {
-      const int64_t cc = stack.back();
-      stack.pop_back();
-      ++sz;
-      const int64_t x = cc % gx, y = cc / gx;
-      for (int dy = -1; dy <= 1; ++dy)
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int64_t nb = (y + dy) * gx + (x + dx);
-          if ((dx || dy) && rep[(size_t)nb] >= 0 && comp[(size_t)nb] < 0) {
-            comp[(size_t)nb] = id;
-            stack.push_back(nb);
-          }
-        }
+  const int64_t m = (int64_t)q.size() / 3;
+  if (m > INT32_MAX / 4) throw DlgError(DLG_ERR_INVALID, "too many plane points");
+  // pcl::ConcaveHull (setAlpha(alpha_poly), reconstruct(output, polygons)): alpha_shape.hpp
+  const alpha::Hull2 H = alpha::concave_hull_2d(q.data(), m, (double)alpha);
+  if (H.polygons.empty()) return 0;
+  // the reference takes polygons[0]; which polygon qhull's facet order puts first is not
+  // reproducible (alpha_shape.hpp), so the border is the polygon enclosing the largest area --
+  // polygons[0] whenever the plane's alpha shape is one simple polygon
+  size_t best = 0;
+  double best_a = -1.0;
+  for (size_t k = 0; k < H.polygons.size(); ++k) {
+    const auto& pg = H.polygons[k];
+    double ax = 0, ay = 0, az = 0;
+    for (size_t j = 0; j < pg.size(); ++j) {
+      const float* a0 = &H.pts[3 * (size_t)pg[j]];
+      const float* a1 = &H.pts[3 * (size_t)pg[(j + 1) % pg.size()]];
+      ax += (double)a0[1] * a1[2] - (double)a0[2] * a1[1];
+      ay += (double)a0[2] * a1[0] - (double)a0[0] * a1[2];
+      az += (double)a0[0] * a1[1] - (double)a0[1] * a1[0];
     }
-    if (sz > best_sz) {
-      best_sz = sz;
-      best = id;
+    const double ar = std::sqrt(ax * ax + ay * ay + az * az);
+    if (ar > best_a) {
+      best_a = ar;
+      best = k;
     }
   }
-  // each cell's representative: its point farthest from the component's centroid (ties: the
-  // lowest index), i.e. the cell's most outward projected point
-  double mc[2] = {0, 0};
-  int64_t m = 0;
-  for (int64_t i = 0; i < n; ++i)
-    if (cid[i] >= 0 && comp[(size_t)cid[i]] == best) {
-      mc[0] += cu[i]; mc[1] += cv[i]; ++m;
-    }
-  mc[0] /= (double)m; mc[1] /= (double)m;
-  std::vector<double> rd((size_t)(gx * gy), -1.0);
-  for (int64_t i = 0; i < n; ++i) {
-    if (cid[i] < 0 || comp[(size_t)cid[i]] != best) continue;
-    const double dd = (cu[i] - mc[0]) * (cu[i] - mc[0]) + (cv[i] - mc[1]) * (cv[i] - mc[1]);
-    if (dd > rd[(size_t)cid[i]]) {
-      rd[(size_t)cid[i]] = dd;
-      rep[(size_t)cid[i]] = (int32_t)i;
-    }
-  }
-  auto inside = [&](int64_t x, int64_t y) {
-    return x >= 0 && y >= 0 && x < gx && y < gy && comp[(size_t)(y * gx + x)] == best;
-  };
-  // Moore-neighbour trace of the component's outer boundary (Gonzalez & Woods): from its first
-  // cell in row order (its west neighbour is empty), each step scans the current cell's eight
-  // neighbours clockwise from the last empty one examined; stops on the first step repeated.
-  // Each boundary cell is kept once, in the order first reached.
-  int64_t start = -1;
-  for (int64_t cc = 0; cc < gx * gy && start < 0; ++cc)
-    if (comp[(size_t)cc] == best) start = cc;
-  static const int ox[8] = {-1, -1, 0, 1, 1, 1, 0, -1};  // W NW N NE E SE S SW (v up)
-  static const int oy[8] = {0, 1, 1, 1, 0, -1, -1, -1};
-  auto dir_of = [&](int64_t dx, int64_t dy) {
-    for (int k = 0; k < 8; ++k)
-      if (ox[k] == dx && oy[k] == dy) return k;
-    return 0;
-  };
-  std::vector<int64_t> ring;
-  std::vector<uint8_t> seen((size_t)(gx * gy), 0);
-  int64_t bcur = start, bx = start % gx, by = start / gx;
-  int64_t cx = bx - 1, cy = by;  // the empty cell the scan starts after
-  int64_t first_next = -1;
-  const int64_t max_steps = 8 * best_sz + 16;
-  for (int64_t it = 0; it < max_steps; ++it) {
-    if (!seen[(size_t)bcur]) {
-      seen[(size_t)bcur] = 1;
-      ring.push_back(bcur);
-    }
-    const int k0 = dir_of(cx - bx, cy - by);
-    int64_t nx = -1, ny = -1, px = cx, py = cy;
-    for (int m = 1; m <= 8; ++m) {
-      const int k = (k0 + m) % 8;
-      const int64_t tx = bx + ox[k], ty = by + oy[k];
-      if (inside(tx, ty)) {
-        nx = tx;
-        ny = ty;
-        break;
-      }
-      px = tx;
-      py = ty;
-    }
-    if (nx < 0) break;  // a single cell
-    const int64_t nxt = ny * gx + nx;
-    if (bcur == start) {
-      if (first_next < 0) first_next = nxt;
-      else if (nxt == first_next) break;  // (Jacob's stopping criterion)
-    }
-    cx = px; cy = py;
-    bx = nx; by = ny;
-    bcur = nxt;
-  }
-  int64_t nb = (int64_t)ring.size();
-  if (nb < 3) return 0;
+  std::vector<int32_t> bi = H.polygons[best];
+  const int64_t nb = (int64_t)bi.size();
   *n_needed = nb;
   if (nb > cap) throw DlgError(DLG_ERR_CAPACITY, "border buffer too small: need " + std::to_string(nb));
-  std::vector<int32_t> bi(nb);
-  for (int64_t k = 0; k < nb; ++k) bi[k] = rep[(size_t)ring[k]];
-  // start one vertex before the lowest-then-leftmost one (in-plane): the reference orients by the
-  // turn at its second vertex, which is then a convex vertex of the polygon, so the turn's sign
-  // is the polygon's orientation
-  int64_t mk = 0;
-  for (int64_t k = 1; k < nb; ++k)
-    if (cv[bi[k]] < cv[bi[mk]] || (cv[bi[k]] == cv[bi[mk]] && cu[bi[k]] < cu[bi[mk]])) mk = k;
-  std::rotate(bi.begin(), bi.begin() + (mk + nb - 1) % nb, bi.end());
+  // the walk's start is qhull's (unpinned); start one vertex before an extreme vertex in the
+  // plane, a convex one: the reference orients by the turn at the second vertex, whose sign is
+  // then the polygon's orientation (from a reflex second vertex its rule would reverse a
+  // correctly oriented border)
+  {
+    double u[3] = {0, 0, 0};
+    const int ax = std::fabs(pn[0]) <= std::fabs(pn[1]) && std::fabs(pn[0]) <= std::fabs(pn[2]) ? 0
+                   : std::fabs(pn[1]) <= std::fabs(pn[2]) ? 1 : 2;
+    u[ax] = 1.0;
+    const double nn = (double)pn[0] * pn[0] + (double)pn[1] * pn[1] + (double)pn[2] * pn[2];
+    const double dt = ((double)pn[0] * u[0] + (double)pn[1] * u[1] + (double)pn[2] * u[2]) / nn;
+    for (int k = 0; k < 3; ++k) u[k] -= dt * pn[k];
+    int64_t mk = 0;
+    double mv = INFINITY;
+    for (int64_t k = 0; k < nb; ++k) {
+      const float* a = &H.pts[3 * (size_t)bi[k]];
+      const double v = a[0] * u[0] + a[1] * u[1] + a[2] * u[2];
+      if (v < mv) { mv = v; mk = k; }
+    }
+    std::rotate(bi.begin(), bi.begin() + (mk + nb - 1) % nb, bi.end());
+  }
   // the reference's orientation rule (PlaneDetect.h:1415-1434): v01, v12 normalized (float),
-  // v_dir = v01 x v12 normalized; reversed when v_dir . pn < 0
-  auto P = [&](int64_t k) { return &q[3 * (size_t)bi[k]]; };
+  // v_dir = v01 x v12 normalized; the order reversed when v_dir . pn < 0
+  auto P = [&](int64_t k) { return &H.pts[3 * (size_t)bi[k]]; };
   float v01[3], v12[3];
   for (int k = 0; k < 3; ++k) {
     v01[k] = P(1)[k] - P(0)[k];
@@ -641,7 +541,7 @@ int64_t plane_border(const float* pts, int64_t stride_f, int64_t n, const float 
   }
   auto nrm = [](float* w) {
     const float l = std::sqrt((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
-    if (l > 0.0f) for (int k = 0; k < 3; ++k) w[k] = w[k] / l;
+    for (int k = 0; k < 3; ++k) w[k] = w[k] / l;
   };
   nrm(v01);
   nrm(v12);
@@ -650,11 +550,11 @@ int64_t plane_border(const float* pts, int64_t stride_f, int64_t n, const float 
   nrm(vd);
   if ((vd[0] * pn[0] + vd[1] * pn[1]) + vd[2] * pn[2] < 0.0f) {
     std::reverse(bi.begin(), bi.end());
-    // (then the convex vertex second again: the border passes the reference's own test)
+    // (the convex vertex second again: the border passes the reference's own test)
     std::rotate(bi.begin(), bi.begin() + (nb - 3) % nb, bi.end());
   }
   for (int64_t k = 0; k < nb; ++k)
-    for (int j = 0; j < 3; ++j) out[k * out_stride_f + j] = q[3 * (size_t)bi[k] + j];
+    for (int j = 0; j < 3; ++j) out[k * out_stride_f + j] = H.pts[3 * (size_t)bi[k] + j];
   return nb;
 }
 

@@ -218,7 +218,11 @@ dlg_status dlg_estimate_normals_ex(dlg_ctx* ctx, const dlg_points* pts, float ra
  * NORMAL_PLANE segmentation without a host round trip): the normals of dlg_estimate_normals_ex
  * (same neighbourhoods, same arithmetic for `mode`) over the cloud's uploaded points, attached
  * to the cloud as dlg_cloud_set_normals would attach them (the cloud is reset).  normals_out
- * (nullable): also copied out, records of out_stride_bytes as dlg_estimate_normals writes them. */
+ * (nullable): also copied out, records of out_stride_bytes as dlg_estimate_normals writes them.
+ * One rank only: a context of a communicator with world > 1 holds a shard, whose points near the
+ * cut would lose the neighbours on other ranks (PCL's normals are over the whole cloud), so it
+ * gets DLG_ERR_INVALID -- estimate the normals over the whole cloud (dlg_estimate_normals_ex) and
+ * attach each rank's slice with dlg_cloud_set_normals. */
 dlg_status dlg_cloud_estimate_normals(dlg_ctx* ctx, dlg_cloud* cloud, float radius, int k_nn,
                                       const float viewpoint[3], int mode, float* normals_out,
                                       int64_t out_stride_bytes);
@@ -374,7 +378,8 @@ dlg_status dlg_score_benchmark(dlg_ctx* ctx, dlg_cloud* cloud, int D, int kernel
  * device's bits; *uncertain = 1 when an eigen33 transcendental could not be rounded for certain
  * (the extraction then takes the host's value).  reps >= 1 launches are timed: *ms_per_call.
  * walk_stats (optional) per chain: windows, speculation passes, passes needing the full lemma,
- * chunks stepped alone, reruns, shader clocks of the walk, of its stepping, chunk records. */
+ * chunks stepped alone, reruns, shader clocks of the walk, of its stepping, chunk records (the
+ * last call's). */
 dlg_status dlg_float_sums(dlg_ctx* ctx, const float* xyz, int64_t n, const float cin[4], int reps,
                           float sums_out[9], float coeff_out[4], int* uncertain,
                           double* ms_per_call, int64_t* walk_stats /* nullable: [9][8] */);

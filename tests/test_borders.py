@@ -1,24 +1,188 @@
 """Plane borders (dlg_plane_border): polyPlanes / polyPointCloud (Dialog/PlaneDetect.h:1358-1440)
 so the four-file polygon hand-off (PCLViewer.cpp:1341-1396) runs from RANSAC output alone.
 
-The reference's border is polygons[0] of pcl::ConcaveHull (qhull alpha shape, alpha_poly = 0.5,
-config.txt); qhull is absent from this image, so the border here is the outer boundary of the
-projected points' alpha occupancy -- PARITY UNPINNED: these tests check the contract the
-reference's consumers rely on, not qhull's facets:
-  * every vertex is one of the plane's points projected as projPoint2Plane projects it (on the
-    least-squares plane of pcl::computePointNormal, within float rounding);
-  * the polygon is closed, has no repeated vertex, encloses the point set's occupied area (area
-    close to the patch's), and is oriented as the reference orients it: the normal of its first
-    three vertices points along the given outward normal;
-  * an L-shaped plane gets a concave border (area well below its convex hull's).
+The reference's border is polygons[0] of pcl::ConcaveHull (qhull "d QJ" Delaunay + alpha test,
+alpha_poly = 0.5, config.txt).  dialog_amd/csrc/alpha_shape.hpp restates ConcaveHull's steps with
+its own Delaunay triangulation; these tests pin it to qhull itself (scipy.spatial.Delaunay with
+"QJ", committed fixtures tests/golden/alpha_shapes.npz from tests/golden/make_alpha.py):
+  * the triangulation equals qhull's triangle for triangle (points in general position), the
+    alpha filter keeps the same triangles, and the boundary edges and their components (PCL's
+    polygons, as vertex sets) are qhull's;
+  * on 3-D plane patches, dlg_plane_border's vertices are exactly the fixture's outer-boundary
+    vertex set (each vertex mapped back to its plane point);
+  * the contract the reference's consumers rely on: vertices on the least-squares plane, a closed
+    polygon without repeated vertices enclosing the patch's area, the reference's orientation
+    rule, a concave border for an L-shaped patch.
+Parity unpinned: qhull's version and joggle seed, the facet order that decides where PCL's walk
+starts and which polygon is polygons[0] (the border here is the largest polygon), and qhull's
+joggled output coordinates.
 CPU (host arithmetic, no device); the GPU test runs extract -> borders -> write_polygons ->
 read_polygons -> dlg_post_process_planes.
 """
+import ctypes
+import os
+import subprocess
+
 import numpy as np
 import pytest
 
 import dialog_amd as D
 from dialog_amd.postprocess import plane_border
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden", "alpha_shapes.npz")
+VP = ctypes.c_void_p
+
+
+@pytest.fixture(scope="module")
+def ah(tmp_path_factory):
+    so = tmp_path_factory.mktemp("alpha") / "libalpha_host.so"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-shared", "-fPIC",
+                    os.path.join(ROOT, "tests", "cpp", "alpha_host.cpp"), "-o", str(so)], check=True)
+    L = ctypes.CDLL(str(so))
+    L.alpha_delaunay.restype = ctypes.c_int64
+    L.alpha_boundary.restype = ctypes.c_int64
+    return L
+
+
+def delaunay(L, xy):
+    xy = np.ascontiguousarray(xy, np.float64)
+    out = np.zeros((2 * xy.shape[0] + 8, 3), np.int32)
+    nt = L.alpha_delaunay(VP(xy.ctypes.data), ctypes.c_int64(xy.shape[0]), VP(out.ctypes.data),
+                          ctypes.c_int64(out.shape[0]))
+    assert nt <= out.shape[0]
+    return out[:nt]
+
+
+def boundary(L, xy, alpha):
+    xy = np.ascontiguousarray(xy, np.float64)
+    n = xy.shape[0]
+    kept = np.zeros(2 * n + 8, np.uint8)
+    verts, order, poly = (np.zeros(n + 1, np.int32) for _ in range(3))
+    nv = L.alpha_boundary(VP(xy.ctypes.data), ctypes.c_int64(n), ctypes.c_double(alpha),
+                          VP(kept.ctypes.data), ctypes.c_int64(kept.size), VP(verts.ctypes.data),
+                          VP(order.ctypes.data), VP(poly.ctypes.data), ctypes.c_int64(n + 1))
+    nt = delaunay(L, xy).shape[0]
+    polys = {}
+    for v, pid in zip(order[:nv], poly[:nv]):
+        if pid >= 0:
+            polys.setdefault(int(pid), []).append(int(v))
+    return kept[:nt].astype(bool), verts[:nv], [polys[k] for k in sorted(polys)]
+
+
+def sorted_tris(t):
+    t = np.sort(t, axis=1)
+    return t[np.lexsort((t[:, 2], t[:, 1], t[:, 0]))]
+
+
+def names(prefix):
+    z = np.load(GOLD)
+    return [str(x) for x in z["names"] if str(x).startswith(prefix)]
+
+
+@pytest.mark.parametrize("name", names("c2_"))
+def test_alpha_shape_equals_qhull_fixture(ah, name):
+    """Triangles, alpha filter, boundary edges and boundary components equal qhull's (scipy
+    Delaunay "QJ") on the committed fixtures: square, L, annulus (a hole), two blobs, graded
+    density."""
+    z = np.load(GOLD)
+    xy, alpha = z[f"{name}_xy"], float(z[f"{name}_alpha"])
+    tri = delaunay(ah, xy)
+    st = sorted_tris(tri)
+    assert np.array_equal(st, z[f"{name}_tri"])
+    kept, verts, polys = boundary(ah, xy, alpha)
+    order = np.lexsort((np.sort(tri, 1)[:, 2], np.sort(tri, 1)[:, 1], np.sort(tri, 1)[:, 0]))
+    assert np.array_equal(kept[order], z[f"{name}_kept"])
+    # boundary edges: the kept triangles' edges not shared with another kept triangle
+    cnt = {}
+    for t in tri[kept]:
+        for i in range(3):
+            e = tuple(sorted((int(t[i]), int(t[(i + 1) % 3]))))
+            cnt[e] = cnt.get(e, 0) + 1
+    be = sorted(e for e, k in cnt.items() if k == 1)
+    assert be == [tuple(e) for e in z[f"{name}_bedges"].tolist()]
+    sizes, cv = z[f"{name}_comp_sizes"], z[f"{name}_comp_verts"]
+    comps = [frozenset(x.tolist()) for x in np.split(cv, np.cumsum(sizes)[:-1])]
+    assert set(verts.tolist()) == set(cv.tolist())
+    deg = {}
+    for a, b in be:
+        deg[a] = deg.get(a, 0) + 1
+        deg[b] = deg.get(b, 0) + 1
+    if max(deg.values()) == 2:  # simple boundaries: PCL's walk yields exactly the components
+        assert {frozenset(p) for p in polys} == set(comps)
+        for p in polys:  # consecutive walk vertices are boundary edges
+            for k in range(len(p)):
+                assert tuple(sorted((p[k], p[(k + 1) % len(p)]))) in cnt
+
+
+def delaunay_valid(xy, tri):
+    """every triangle counter-clockwise and no point strictly inside its circumcircle"""
+    a, b, c = xy[tri[:, 0]], xy[tri[:, 1]], xy[tri[:, 2]]
+    o = (b[:, 0] - a[:, 0]) * (c[:, 1] - a[:, 1]) - (b[:, 1] - a[:, 1]) * (c[:, 0] - a[:, 0])
+    assert (o > 0).all()
+    for k in range(tri.shape[0]):
+        rows = []
+        for v in (a[k], b[k], c[k]):
+            d = v[None, :] - xy
+            rows.append((d[:, 0], d[:, 1], d[:, 0] ** 2 + d[:, 1] ** 2))
+        (ax, ay, al), (bx, by, bl), (cx, cy, cl) = rows
+        det = ax * (by * cl - bl * cy) - ay * (bx * cl - bl * cx) + al * (bx * cy - by * cx)
+        scale = (np.abs(ax) + np.abs(ay) + 1e-300) ** 4
+        assert (det <= 1e-9 * scale.max()).all(), k
+
+
+@pytest.mark.parametrize("case", ["random", "grid", "collinear", "duplicates", "tiny", "far"])
+def test_delaunay_degenerate_inputs(ah, case):
+    """Degenerate inputs (cocircular grids, collinear sets, duplicates, tiny / offset coordinates)
+    triangulate without error into a valid Delaunay triangulation (for general-position input:
+    qhull's, live through scipy)."""
+    from scipy.spatial import Delaunay
+    rng = np.random.default_rng(11)
+    if case == "random":
+        xy = rng.uniform(-3, 3, (1500, 2))
+    elif case == "grid":
+        g = np.arange(20.0)
+        xy = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2)
+    elif case == "collinear":  # exactly collinear (integer coordinates): no triangle
+        t = rng.permutation(200).astype(np.float64)
+        xy = np.stack([t, 2 * t + 1], 1)
+    elif case == "duplicates":
+        xy = np.repeat(rng.uniform(0, 1, (300, 2)), 3, axis=0)
+    elif case == "tiny":
+        xy = rng.uniform(0, 1e-6, (500, 2))
+    else:
+        xy = rng.uniform(0, 1, (500, 2)) + 1e4
+    tri = delaunay(ah, xy)
+    if case == "collinear":
+        assert tri.shape[0] == 0
+        return
+    delaunay_valid(xy, tri)
+    if case in ("random", "tiny", "far"):
+        # (qhull's joggle scales with the coordinates' magnitude: far from the origin it flips
+        # near-cocircular pairs, so qhull is run on the centred points -- ConcaveHull demeans
+        # before qhull as well)
+        d = Delaunay(xy - xy.mean(0), qhull_options="QJ")
+        assert np.array_equal(sorted_tris(tri), sorted_tris(d.simplices))
+    if case == "duplicates":  # each distinct point used once
+        assert np.unique(xy[np.unique(tri)], axis=0).shape[0] == np.unique(tri).size
+
+
+@pytest.mark.parametrize("name", names("c3_"))
+def test_plane_border_vertex_set_pinned(name):
+    """dlg_plane_border on 3-D plane patches: its vertices, mapped back to the plane points, are
+    exactly the outer boundary of qhull's alpha shape (fixture)."""
+    z = np.load(GOLD)
+    p, nrm, alpha = z[f"{name}_pts"], z[f"{name}_normal"], float(z[f"{name}_alpha"])
+    b = plane_border(p, nrm, alpha)
+    q = p.astype(np.float64)
+    c = q.mean(0)
+    _, V = np.linalg.eigh(np.cov((q - c).T, bias=True))
+    pq, bq = (q - c) @ V[:, [2, 1]], (b.astype(np.float64) - c) @ V[:, [2, 1]]
+    d2 = ((bq[:, None, :] - pq[None, :, :]) ** 2).sum(-1)
+    idx = d2.argmin(1)
+    assert np.sqrt(d2[np.arange(len(idx)), idx]).max() < 1e-4
+    assert len(set(idx.tolist())) == len(idx)
+    assert set(idx.tolist()) == set(z[f"{name}_outer"].tolist())
 
 
 def frame(n):

@@ -252,6 +252,24 @@ def test_gpu_np_loopback_sharded(gpu_ctx, world):
         c.close()
 
 
+@pytest.mark.gpu
+def test_gpu_cloud_normals_refused_on_a_shard():
+    """dlg_cloud_estimate_normals on one rank's shard (world > 1) is refused: points near the
+    cut would lose their neighbours on other ranks.  The whole cloud's normals, attached per
+    shard with set_normals, are the supported path (test_gpu_np_loopback_sharded)."""
+    import dialog_amd as D
+    p, _, _, _ = cloud_with_normals(4000, seed=5)
+    ctxs = D.Context.loopback_group(2, 0)
+    try:
+        c = D.Cloud(ctxs[0], p[:2000], id_base=0)
+        with pytest.raises(D.DialogError):
+            c.estimate_normals(radius=0.1)
+        c.close()
+    finally:
+        for x in ctxs:
+            x.close()
+
+
 # ------------------------------------------------------------------------------------- C5 chain
 @pytest.mark.gpu
 @pytest.mark.parametrize("nmode,refit", [("radius", "pcl"), ("knn", "pcl"), ("knn", "fast")])
