@@ -88,7 +88,8 @@ def c5_secondary(D, ctx, a):
     pts, _, _ = plane_cloud(a.points, a.planes, seed=SEED_BASE + 5)
     out = {"workload": "C5: 10M-pt 20-plane cloud, k=20 normals, NORMAL_PLANE (w=0.1) extract; "
                        "postProcessPlanes on a 10M-pt 20-plane scene (1000-vertex borders); "
-                       "chain_ms = device-resident normals (dlg_cloud_estimate_normals) + extract",
+                       "chain_ms = device-resident normals (dlg_cloud_estimate_normals) + extract; "
+                       "chain_regulate_ms = normals + RegulateNormal + extract",
            "points": a.points}
 
     def timed(f, reps=2):
@@ -111,6 +112,7 @@ def c5_secondary(D, ctx, a):
     # the device-resident chain: k = 20 normals computed from the cloud's device copy and
     # attached to it (dlg_cloud_estimate_normals), then the NORMAL_PLANE extraction
     _, out["cloud_normals_knn20_ms"] = timed(lambda: cloud.estimate_normals(k=20))
+    _, out["cloud_normals_radius0.1_ms"] = timed(lambda: cloud.estimate_normals(radius=0.1))
     prm = D.make_params(a.threshold, max_iterations=a.hyps - 1, probability=1.0,
                         refit_mode=D.DLG_REFIT_PCL if a.refit == "pcl" else D.DLG_REFIT_FAST,
                         hypotheses_per_launch=a.hyps,
@@ -129,7 +131,35 @@ def c5_secondary(D, ctx, a):
 
     _, out["chain_ms"] = timed(chain)
     out["chain_ms"] = round(out["chain_ms"], 2)
+
+    def chain_regulate():
+        # the reference's order: estimateNormal (k = 20, on the cloud's device copy) ->
+        # regulateNormal (BFS, r 0.1, seed 0) -> the NORMAL_PLANE extraction on the regulated
+        # normals (host round trip of the normals: dlg_regulate_normals takes host records)
+        nr = cloud.estimate_normals(k=20, copy_out=True)
+        rg, _, _ = D.regulate_normals(pts, nr, 0, True, 0.1, ctx=ctx)
+        cloud.set_normals(rg)
+        return D.extract_planes(cloud, prm, max_planes=a.planes, min_inliers=a.min_inliers,
+                                capacity=a.points)
+
+    _, out["chain_regulate_ms"] = timed(chain_regulate, 1)
+    out["chain_regulate_ms"] = round(out["chain_regulate_ms"], 2)
     out["cloud_normals_knn20_ms"] = round(out["cloud_normals_knn20_ms"], 2)
+    out["cloud_normals_radius0.1_ms"] = round(out["cloud_normals_radius0.1_ms"], 2)
+    # HBM views of the device-resident stages (SURVEY 8(d) per-point bytes: the point read once,
+    # the (normal, curvature) record written once; RegulateNormal: points + normals read, normals
+    # + processed flag written).  None of them is HBM-bound -- the neighbour search (cell scans,
+    # candidate distances, the k-selection or the BFS frontier) bounds them -- so frac states how
+    # far each stage is from streaming its data once.
+    n = a.points
+    views = {"normals_knn20": (28.0, out["cloud_normals_knn20_ms"]),
+             "normals_radius0.1": (28.0, out["cloud_normals_radius0.1_ms"]),
+             "regulate_r0.1 (host records in and out, PCIe incl.)": (37.0, out["regulate_r0.1_ms"])}
+    out["rooflines"] = {
+        k: {"bound": "latency (neighbour search); hbm view", "alg_bytes_per_point": b,
+            "achieved": round(b * n / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(b * n / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)}
+        for k, (b, ms) in views.items() if ms}
     e, ms = timed(step)
     st = e["stats"]
     out.update({"np_extract_ms": round(ms, 2), "np_planes": e["n_planes"],
@@ -422,15 +452,16 @@ def main():
                      + 5.0 * sum_active + 4.0 * surv + 8.0 * inliers_local
                      + 12.0 * surv + 0.5 * surv)
         if a.refit == "pcl":
-            # PCL refit instead of the moments: the unrefined inliers stamped into a bitmap over
-            # pristine indices and compacted in list order (bitmap written + read, 12 B gathered
-            # + 12 B written per inlier), then the float-sum passes (k_fs_prep, k_fs_inc: 12 B per
-            # inlier each; k_fs_l1: 12 B per inlier per chain + the 64-byte chunk records of the
-            # nine chains written: 9 B per inlier).  The chains' walk (k_fs_walk: sequential,
-            # latency-bound, one wave per chain) is timed on its own and left out of this phase.
-            # (Approximate: the stamp pass reads the near tiles like the moments do.)
+            # PCL refit instead of the moments: the stamp pass visits the same near tiles (the
+            # 12 B per inlier above), the inlier bitmap over pristine indices is written and read
+            # once per round, and the float-sum passes leave nine 64-byte chunk records (9 B per
+            # inlier).  Each inlier's coordinates count once: k_ucompact's gather from the
+            # pristine records and the float-sum passes' re-reads of the compacted list
+            # (k_fs_prep, k_fs_inc, k_fs_l1) are implementation traffic, not algorithmic bytes.
+            # The chains' walk (k_fs_walk: sequential, latency-bound) is timed on its own and
+            # left out of this phase.
             sel_bytes += (2.0 * per_rank_points_total / 8.0 * rounds_per_step * a.steps
-                          + 24.0 * inliers_local + (12.0 + 12.0 + 9 * 12.0 + 9.0) * inliers_local)
+                          + 9.0 * inliers_local)
     else:
         n_copies = 2 if pruned else 1
         sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))
@@ -514,6 +545,11 @@ def main():
                "host_cpu": model, "host_nproc": os.cpu_count()}
 
     if rank == 0:
+        xchg = ("RCCL allreduce of the hypotheses' counts; the PCL refit's nine float chains "
+                "walked over the ranks' inlier segments in global order (each rank from its "
+                "guess, repaired from the previous rank's 9-float end state)"
+                if a.refit == "pcl" else
+                "RCCL allreduce of the hypotheses' counts and of exact refit moments")
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "G point-plane tests/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -523,10 +559,10 @@ def main():
             "config": {"workload": (
                            "C4: 100M-pt 20-plane synthetic cloud sharded over the GPUs "
                            "(BASELINE.json configs[3]), sequential extract-and-remove RANSAC, "
-                           "RCCL allreduce of counts and exact refit moments" if strong else
+                           + xchg if strong else
                            ("C3: sequential extract-and-remove RANSAC, 10M-pt 20-plane synthetic "
                             "cloud per GPU (BASELINE.json configs[2]; N>1: shards of one cloud, "
-                            "RCCL allreduce of counts and exact refit moments)"
+                            + xchg + ")"
                             if a.points == 10_000_000 and a.planes == 20 else
                             f"sequential extract-and-remove RANSAC, {a.points / 1e6:g}M-pt "
                             f"{a.planes}-plane synthetic cloud per GPU (not the C3 size: "

@@ -112,6 +112,8 @@ struct NormalsWork {
   DevBuf<int32_t> ncnt;   // PCL-float radius normals: neighbours per query (chunk)
   DevBuf<int64_t> noff;   //   their offsets
   DevBuf<uint64_t> nkeys; //   (d2, index) keys
+  DevBuf<int32_t> ovfa, ovfb;  // fused radius normals: queries with too many neighbours
+  DevBuf<uint32_t> ovfc;       //   their counts
   DevBuf<long long> bst;
   PinBuf<long long> h_bst;
   DevBuf<unsigned long long> keys64, keys_alt;
@@ -128,6 +130,7 @@ struct NormalsWork {
     keys_alt.release(); h_cnt.release(); ccnt.release(); coffs.release(); ccur.release();
     sd2.release(); bst.release(); h_bst.release(); ctile.release(); cslot.release();
     ncnt.release(); noff.release(); nkeys.release();
+    ovfa.release(); ovfb.release(); ovfc.release();
   }
 };
 
@@ -164,6 +167,8 @@ struct PathOptions {
   bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
   int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
   int tile_scorer = 0;            // pruned plane scorer: kTileScorerExact or kTileScorerBf16
+  bool nbr_fused = true;          // PCL-float radius normals in one fused pass (else chunked)
+  int nbr_xp = 0;                 // (timing experiment: phases skipped, results wrong)
   // PCL float refit (DLG_REFIT_PCL, any rank count): 1 = the nine sums on the device (fsum.hip,
   // exact), 0 = gathered to the host and summed there, 2 = device, and the host recomputes the
   // refit's tail from the published sums every round, 3 = as 2 and the round's select is always
@@ -271,6 +276,7 @@ struct dlg_cloud {
   int64_t n_active = 0;
   int cur = -1;  // -1 pristine, 0 = A, 1 = B
   SoA pristine, buf[2];
+  DevBuf<float4> paos;  // the pristine points as (x, y, z, 0) records (with the Morton copy)
   float amax[3] = {0, 0, 0};
   float fmax = 0.0f;         // largest |coordinate| of the finite points (this rank's)
   bool qexp_known = false;   // fast refit quantum exponent (global over ranks), set lazily

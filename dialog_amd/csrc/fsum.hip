@@ -29,6 +29,7 @@
 
 #include <hip/hip_ext.h>
 
+#include <atomic>
 #include <cstdint>
 
 namespace dlg {
@@ -45,6 +46,7 @@ struct FsDev {
   int stride;
   const int32_t* n_dev;
   FsBuffers b;
+  uint32_t gen;  // this launch's stamp (window transfer tables of older launches are ignored)
 };
 
 __device__ __forceinline__ FsNode* fs_rec(const FsBuffers& b, int c, int64_t k) {
@@ -445,24 +447,48 @@ __device__ __forceinline__ void fs_seq_prep(const FsWalkRec wr, int cnt, int lan
 // lead L (entering at t = g_0 + L Q, Q the window's smallest quantum).  Record k is applied as
 // fs_seq_window applies it: covered by the lemma (member i = (L_k >> s_k) & 3, the grid, margin
 // and quanta conditions) it steps L_{k+1} = L_k + E_k[i]; otherwise the lane reruns the chunk's
-// terms (LDS, in order, a wave-uniform loop) from its exact start g_k + L_k Q and re-expresses
-// the result as a lead on g_{k+1}.  A lane whose start or re-expressed lead is not exact is
-// dropped.  Every lane kept holds the window's exit value -- a literal run or lemma-proven shift
-// of the chain from that entry, the value any exact walk carries out of the window -- and its
-// mask bit.  Chains hovering near zero (many start-dependent records, a few reruns per window)
-// are then walked one lookup per window instead of record by record.
+// terms (staged in LDS, summed in order) from its exact start g_k + L_k Q and re-expresses the
+// result as a lead on g_{k+1}.  A lane whose start or re-expressed lead is not exact is dropped.
+// Every lane kept holds the window's exit value -- a literal run or lemma-proven shift of the
+// chain from that entry, the value any exact walk carries out of the window -- and its mask bit.
+// Chains hovering near zero (many start-dependent records, a few reruns per window) are then
+// walked one lookup per window instead of record by record.  The tables are built by the walk
+// kernel's own builder workgroups while the walkers run (k_fs_walk): a table is published with
+// this launch's stamp (release) and the walker uses it only if the stamp is there when it arrives
+// (acquire); otherwise it walks the window itself -- nobody waits.
 constexpr int kFtLo = 32;  // entry leads -kFtLo .. 63 - kFtLo
-__device__ __forceinline__ void fs_wtab_build(const FsDev& d, int c, int64_t u, int nch, int cnt,
-                                              const float* sp, const float4* sn,
-                                              const uint4 (*sq)[3], int lane) {
-  const uint32_t qb = sq[0][2].y;  // the window's Q (every record holds it)
+struct FsTabLds {
+  uint4 sq[kWave][3];
+  float g[kWave];
+  float4 o[kWave];
+  float term[kWave];
+};
+__device__ __forceinline__ void fs_wtab_item(const FsDev& d, int c, int64_t u, int lane,
+                                             FsTabLds& L_) {
+  const int64_t n = *d.n_dev;
+  const int64_t K = fs_chunks(n);
+  const int64_t base = u * kWave;
+  const int nch = K - base < kWave ? (int)(K - base) : kWave;
+  const int cnt = n - u * kFsUnit < kFsUnit ? (int)(n - u * kFsUnit) : kFsUnit;
+  const float4 sm = d.b.win[(int64_t)c * d.b.wcap + u];
+  if (nch <= 0 || (sm.z >= 0.0f && sm.w == sm.w)) return;  // (fast: the summaries / speculation)
+  __builtin_amdgcn_wave_barrier();
+  if (lane < nch) {
+    const uint4* q = d.b.srec + 3 * ((int64_t)c * d.b.cap + base + lane);
+    L_.sq[lane][0] = q[0]; L_.sq[lane][1] = q[1]; L_.sq[lane][2] = q[2];
+    const FsNode* r = fs_rec(d.b, c, base + lane);
+    L_.g[lane] = r->g;
+    L_.o[lane] = make_float4(r->o[0], r->o[1], r->o[2], r->o[3]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t qb = L_.sq[0][2].y;  // the window's Q (every record holds it)
   const double Q = (double)__uint_as_float(qb), iQ = 1.0 / Q;  // (exact: powers of two)
   int64_t L = lane - kFtLo;
-  bool ok = nch > 0;
+  bool ok = true;
   float out = 0.0f;
   for (int k = 0; k < nch; ++k) {
-    const uint4 sq0 = sq[k][0], sq1 = sq[k][1], sq2 = sq[k][2];
-    const float* row = reinterpret_cast<const float*>(&sn[k * 4]);
+    const uint4 sq0 = L_.sq[k][0], sq1 = L_.sq[k][1], sq2 = L_.sq[k][2];
+    const float4 o4 = L_.o[k];
     const uint32_t fl = sq2.x;
     const int sh = (int)(fl & 0xFFu);
     const bool exact_only = (fl >> 8) & 1u, gfin = (fl >> 9) & 1u;
@@ -476,21 +502,36 @@ __device__ __forceinline__ void fs_wtab_build(const FsDev& d, int c, int64_t u, 
     if (exact_only) cov = gfin && L == 0 && ((fl >> 10) & 1u);
     const bool last = k == nch - 1;
     if (cov) {
-      const float oi = row[4 + i];
+      const float oi = i == 0 ? o4.x : i == 1 ? o4.y : i == 2 ? o4.z : o4.w;
       if (last) out = (float)((double)oi + (double)D * Q);  // (exact: the lemma)
       else L += (int32_t)(i == 0 ? sq0.x : i == 1 ? sq0.y : i == 2 ? sq0.z : sq0.w);
     }
     if (ballot(ok && !cov)) {  // the uncovered lanes rerun the chunk from their exact start
-      const double tv = (double)row[0] + (double)L * Q;
+      const int len = cnt - k * kFsChunk < kFsChunk ? cnt - k * kFsChunk : kFsChunk;
+      {  // the chunk's terms into LDS (one per lane, coalesced)
+        const int64_t e = ((base + k) * kFsChunk + (lane < len ? lane : 0)) * d.stride;
+        const float tv = fs_term(c, d.px[e], d.py[e], d.pz[e]);
+        __builtin_amdgcn_wave_barrier();
+        L_.term[lane] = tv;
+        __builtin_amdgcn_wave_barrier();
+      }
+      const double tv = (double)L_.g[k] + (double)L * Q;
       float v = (float)tv;
       bool run = ok && !cov && (double)v == tv && (L < 1073741824 && L > -1073741824);
-      const int len = cnt - k * kFsChunk < kFsChunk ? cnt - k * kFsChunk : kFsChunk;
       if (run) {
-        for (int j = 0; j < len; ++j) v = v + sp[k * kFsPad + j];
+        if (len == kFsChunk) {  // (the terms read ahead: one LDS latency, 64 adds)
+          float tm[kFsChunk];
+#pragma unroll
+          for (int j = 0; j < kFsChunk; ++j) tm[j] = L_.term[j];
+#pragma unroll
+          for (int j = 0; j < kFsChunk; ++j) v = v + tm[j];
+        } else {
+          for (int j = 0; j < len; ++j) v = v + L_.term[j];
+        }
         if (last) {
           out = v;
         } else {  // the exact lead on the next record's guess (TwoSum: it must be exact)
-          const double ta = (double)v, gb = -(double)reinterpret_cast<const float*>(&sn[(k + 1) * 4])[0];
+          const double ta = (double)v, gb = -(double)L_.g[k + 1];
           const double sd = ta + gb, bv = sd - ta;
           const double er = (ta - (sd - bv)) + (gb - bv);
           const double Ld = sd * iQ;
@@ -502,8 +543,16 @@ __device__ __forceinline__ void fs_wtab_build(const FsDev& d, int c, int64_t u, 
     }
   }
   const uint64_t m = ballot(ok);
+  uint4* meta = d.b.wmeta + (int64_t)c * d.b.wcap + u;
   d.b.wtab[((int64_t)c * d.b.wcap + u) * kWave + lane] = out;
-  if (lane == 0) d.b.wmeta[(int64_t)c * d.b.wcap + u] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), qb, 0u);
+  if (lane == 0) {
+    meta->x = (uint32_t)m;
+    meta->y = (uint32_t)(m >> 32);
+    meta->z = qb;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) __hip_atomic_store(&meta->w, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- k_fs_l1 ----------------------------------------------------------------------------------
@@ -512,7 +561,6 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
   __shared__ float sp[kFsUC * kFsPad];
   __shared__ float4 sn[kFsUC * 4];  // the unit's records, 4 rows of 16 bytes each
   __shared__ float sg[kFsUC];
-  __shared__ uint4 ssq[kFsUC][3];  // the unit's integer-stepping tables (the transfer table's input)
   const int64_t n = *d.n_dev;
   const int64_t U = (n + kFsUnit - 1) / kFsUnit;
   const int t = threadIdx.x;
@@ -635,9 +683,6 @@ __global__ __launch_bounds__(kFlBS) void k_fs_l1(FsDev d) {
         uint4* o = d.b.srec + 3 * ((int64_t)c * d.b.cap + u * kFsUC + t);
         o[0] = s0; o[1] = s1; o[2] = s2;
       }
-      ssq[t][0] = s0; ssq[t][1] = s1; ssq[t][2] = s2;
-      __builtin_amdgcn_wave_barrier();
-      fs_wtab_build(d, c, u, nch, cnt, sp, sn, ssq, t);
     }
     __syncthreads();
     for (int p = t; p < nch * 4; p += kFlBS)
@@ -1037,7 +1082,6 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
     if (lane < nb) sm = S[wb + lane];
     if (lane < nb && has_next) gnx = S[wb + lane + 1].x;
     const float vb = kRepair && lane < nb ? V[wb + lane] : 0.0f;
-    const uint4 tm = lane < nb ? d.b.wmeta[c * d.b.wcap + wb + lane] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = lane < nb && sm.w == sm.w &&
                        (!has_next || __float_as_uint(sm.y) == __float_as_uint(gnx));
     const uint64_t stat = ballot(lane < nb && !valid);  // (walked at any lag: prefetch candidates)
@@ -1076,11 +1120,13 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
       }
       if (kRecord && lane == 0) V[wb + f] = t;
       const int64_t w = wb + f;
-      {  // the window's transfer table (k_fs_wtab): the exit value when the entry lead is in it
-        const uint64_t tmask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)tm.x, f) |
-                               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)tm.y, f) << 32);
+      {  // the window's transfer table, if its builder has published it (fs_wtab_item): the
+         // exit value when the entry lead is in it
+        uint4* meta = d.b.wmeta + c * d.b.wcap + w;
+        const uint32_t stamp = __hip_atomic_load(&meta->w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t tmask = stamp != d.gen ? 0ull : (uint64_t)meta->x | ((uint64_t)meta->y << 32);
         if (tmask) {
-          const double Q = (double)__uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)tm.z, f));
+          const double Q = (double)__uint_as_float(meta->z);
           // the lead t - g_0 with its rounding error (TwoSum: it must be exact), in units of Q
           const double ta = (double)t, gb = -(double)g0f(sm, f);
           const double sd = ta + gb, bv = sd - ta;
@@ -1160,6 +1206,15 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   const int c = blockIdx.x, lane = threadIdx.x;
   const int64_t n = *d.n_dev;
   const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
+  if (c >= kFsChains) {
+    // a table builder: (window, chain) items in window order, so the walkers find the early
+    // windows' tables first
+    FsTabLds& L_ = *reinterpret_cast<FsTabLds*>(ring_raw);
+    static_assert(sizeof(FsTabLds) <= 2 * kFsSlotBytes, "builder state fits the ring's LDS");
+    for (int64_t it = c - kFsChains; it < NW * kFsChains; it += gridDim.x - kFsChains)
+      fs_wtab_item(d, (int)(it % kFsChains), it / kFsChains, lane, L_);
+    return;
+  }
   // walk counters (dlg_float_sums' walk_stats): windows walked record by record, speculation
   // passes, passes with lanes the fast path could not decide, lanes stepped alone, reruns, clocks
   // (all, stepping), windows passed by their summaries
@@ -1187,7 +1242,7 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
                     : 0u;
   }
   __syncthreads();
-  if (!cout || s_ticket != gridDim.x - 1 || lane != 0) return;
+  if (!cout || s_ticket != kFsChains - 1 || lane != 0) return;
   d.b.ticket[1] = 0u;
   float a9[kFsChains];
   for (int k = 0; k < kFsChains; ++k)
@@ -1284,7 +1339,11 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
                      hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
-  FsDev d{px, py, pz, stride, n_dev, b};
+  static std::atomic<uint32_t> s_gen{0};
+  FsDev d{px, py, pz, stride, n_dev, b, ++s_gen};
+  const unsigned gw = (unsigned)(kFsChains +
+      std::max<int64_t>(1, std::min<int64_t>(((n_cap > 0 ? n_cap : 1) + kFsUnit - 1) / kFsUnit * kFsChains,
+                                             4 * (int64_t)num_cus)));
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t U = (fs_chunks(nc) + kFsUC - 1) / kFsUC;
   const int gp = (int)std::min<int64_t>(U, 2 * (int64_t)num_cus);
@@ -1294,8 +1353,8 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
     hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, nullptr);
     hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, nullptr);
     hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-    hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u,
-                          d, nullptr, 0, cin, cout, res);
+    hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
+                          nullptr, 0, cin, cout, res);
     return;
   }
   // several ranks (the list is the ranks' segments in order): each rank's guesses start from the
@@ -1309,7 +1368,7 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
   hipLaunchKernelGGL(k_fs_base, dim3(1), dim3(256), 0, s, d, b.gath, r, W, b.base9, b.n_global);
   hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, b.base9);
   hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-  hipExtLaunchKernelGGL(k_fs_walk, dim3(kFsChains), dim3(kFwBS), 0, s, ev_walk0,
+  hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0,
                         r > 0 ? nullptr : ev_walk1, 0u, d, (const float*)nullptr, r > 0 ? 1 : 0,
                         (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
   if (r > 0) {

@@ -193,7 +193,7 @@ void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers
 void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, float margin,
                    const float4* coef, const ModelTest& mt, uint32_t* bits, hipStream_t s);
 int ucompact_tiles(int64_t nwords);
-void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1State& L, float* ox,
+void launch_ucompact(uint32_t* bits, int64_t nwords, const float4* paos, Sel1State& L, float* ox,
                      float* oy, float* oz, int32_t* n_out, hipStream_t s);
 
 // PCL's float refit on the device (fsum.hip): the nine sequential float sums of

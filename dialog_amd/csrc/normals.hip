@@ -419,35 +419,76 @@ __global__ __launch_bounds__(kBS) void k_nbr_fill(
       }
 }
 
-// bitonic sort of 64 * E keys held E per lane (element e = lane + 64 j), ascending
+// v of lane (lane ^ S), S < 64, without LDS: DPP quad permutes (S = 1, 2), quad reversal then
+// half-row mirror (4: l ^ 3 mirrored in 8 lanes is l ^ 4), row rotate by 8 (8), and gfx950's
+// row / half-wave swaps (16, 32: the swap of v with itself leaves each lane's partner in one of
+// the two results).  The whole wave must be active.
+template <int S>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  if constexpr (S == 1) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (S == 2) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (S == 4) {
+    const uint32_t r = __builtin_amdgcn_update_dpp(0u, v, 0x1B, 0xF, 0xF, false);  // [3,2,1,0]
+    return __builtin_amdgcn_update_dpp(0u, r, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  } else if constexpr (S == 8) {
+    return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (S == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? r[0] : r[1];
+  } else {
+    static_assert(S == 32, "xor_lane: S in 1..32");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
+  }
+}
+
+template <int S>
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v) {
+  return (uint64_t)xor_lane<S>((uint32_t)v) | ((uint64_t)xor_lane<S>((uint32_t)(v >> 32)) << 32);
+}
+
+// one bitonic merge step at in-wave distance S over the E registers (blocks of `size` elements)
+template <int E, int S>
+__device__ __forceinline__ void bitonic_xstep(uint64_t (&v)[E], int size) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = lane + 64 * j;
+    const bool up = (e & size) == 0;  // this element's block sorts ascending
+    const bool take_min = ((lane & S) == 0) == up;  // the lower element keeps the min ascending
+    const uint64_t o = xor_lane64<S>(v[j]);
+    v[j] = (o < v[j]) == take_min ? o : v[j];
+  }
+}
+
+// bitonic sort of 64 * E keys held E per lane (element e = lane + 64 j), ascending; the steps
+// within a wave exchange through DPP / lane swaps (no LDS round trip per step)
 template <int E>
 __device__ __forceinline__ void wave_bitonic(uint64_t (&v)[E]) {
-  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int size = 2; size <= 64 * E; size <<= 1) {
 #pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+    for (int stride = size >> 1; stride >= 64; stride >>= 1) {
+      const int js = stride >> 6;
 #pragma unroll
       for (int j = 0; j < E; ++j) {
-        const int e = lane + 64 * j;
-        const bool up = (e & size) == 0;  // this element's block sorts ascending
-        if (stride >= 64) {
-          const int js = stride >> 6;
-          if ((j & js) == 0) {  // (j, j | js): both in this lane
-            uint64_t& a = v[j];
-            uint64_t& b = v[j | js];
-            const bool sw = up ? (a > b) : (a < b);
-            if (sw) { const uint64_t t = a; a = b; b = t; }
-          }
-        } else {
-          const uint64_t o = __shfl_xor(v[j], stride, 64);
-          const bool lower = (lane & stride) == 0;
-          // lower element keeps min when ascending, max when descending
-          const bool take_min = lower == up;
-          v[j] = take_min ? (o < v[j] ? o : v[j]) : (o > v[j] ? o : v[j]);
+        if ((j & js) == 0) {  // (j, j | js): both in this lane
+          const bool up = ((j * 64) & size) == 0;
+          uint64_t& a = v[j];
+          uint64_t& b = v[j | js];
+          const bool sw = up ? (a > b) : (a < b);
+          if (sw) { const uint64_t t = a; a = b; b = t; }
         }
       }
     }
+    if (size >= 64) bitonic_xstep<E, 32>(v, size);
+    if (size >= 32) bitonic_xstep<E, 16>(v, size);
+    if (size >= 16) bitonic_xstep<E, 8>(v, size);
+    if (size >= 8) bitonic_xstep<E, 4>(v, size);
+    if (size >= 4) bitonic_xstep<E, 2>(v, size);
+    bitonic_xstep<E, 1>(v, size);
   }
 }
 
@@ -539,6 +580,226 @@ __global__ __launch_bounds__(kBS) void k_nbr_normals(
     pcl_accu_add(a, X[j], Y[j], Z[j]);
   }
   normals[sidx[t]] = finish_normal_pcl(a, k, sx[t], sy[t], sz[t], vpx, vpy, vpz);
+}
+
+// ---- fused radius normals (PCL float): search, (d2, index) order and the sums in one pass ----
+// One wave per query at a time, queries taken in runs of kFqRun consecutive sorted positions.
+// Per query: the 27 cells around it are 9 runs of sorted positions (a row's three x cells have
+// consecutive keys, so their ranges are contiguous; looked up once per run cell, lane r < 9
+// holding row r's range), scanned 64 candidates per step with FLANN's d2 and test (the
+// neighbour set is KdTreeFLANN's); the passing ones are compacted into the wave's LDS as keys
+// (d2 bits << 32 | sorted position), sorted in registers (wave bitonic, 64 E keys), reordered by
+// the points' original index where d2 ties (FLANN's (d2, index) order: sorted positions follow
+// the original index only within a cell), and their coordinates staged in LDS in that order;
+// lanes 0..8 then run computeMeanAndCovarianceMatrix's nine float chains in list order (each
+// lane its chain's operand pair, no divergence).  The sums of 64 queries are parked in LDS and
+// finished (eigen33, curvature, viewpoint flip) with one query per lane.  Nothing per neighbour
+// leaves the chip (the chunked pipeline writes, sorts and re-reads 8 bytes per neighbour).  A
+// query with more than 64 E neighbours goes to the overflow list for the next, wider launch.
+constexpr int kFqRun = 16;
+constexpr int kFqB = 4;  // candidate steps whose loads are in flight together
+#define DLG_NBR_FUSED_ARGS                                                                        \
+    const float *__restrict__ sx, const float *__restrict__ sy, const float *__restrict__ sz,     \
+        const int32_t *__restrict__ sidx, int n, const int32_t *__restrict__ qlist,              \
+        const uint32_t *__restrict__ qcount, GridDesc G, const uint32_t *__restrict__ tkeys,     \
+        const int2 *__restrict__ trange, uint32_t tmask, float r2, float vpx, float vpy,         \
+        float vpz, float4 *__restrict__ normals, int32_t *__restrict__ ovf,                      \
+        uint32_t *__restrict__ ovf_count
+template <int E, int XP>
+__device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS);
+
+// the first pass (<= 256 neighbours) held to 128 VGPRs: four waves per SIMD, as many as its LDS
+// allows; the wider passes are LDS-limited to fewer waves anyway
+template <int E, int XP = 0>  // XP: timing experiment (bit 0 no sort, 1 no sum, 2 no scan)
+__global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(4))) void k_nbr_fused(
+    DLG_NBR_FUSED_ARGS) {
+  nbr_fused_body<E, XP>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx, vpy,
+                        vpz, normals, ovf, ovf_count);
+}
+template <int E>
+__global__ __launch_bounds__(kBS) void k_nbr_fused_wide(DLG_NBR_FUSED_ARGS) {
+  nbr_fused_body<E, 0>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx, vpy,
+                       vpz, normals, ovf, ovf_count);
+}
+
+template <int E, int XP>
+__device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
+  constexpr int kCap = 64 * E;
+  constexpr int kW = kBS / 64;
+  __shared__ uint64_t s_key[kW][kCap];
+  __shared__ float4 s_nr[kW][kCap];  // the neighbours in list order: (x, y, z, 1)
+  __shared__ float s_sum[kW][9][64];  // parked sums: [chain][slot]
+  __shared__ float4 s_q[kW][64];      // (query xyz, count) per slot
+  __shared__ int32_t s_dst[kW][64];   // output point index per slot
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t* key = s_key[wv];
+  float4* nr = s_nr[wv];
+  // lane c < 9 runs chain c: term = pa * pb (pb = the record's 1 for the coordinate sums: x * 1
+  // = x exactly), each lane reading its two operands at its own offsets in the record
+  const int sa = lane < 3 ? 0 : lane < 5 ? 1 : lane < 6 ? 2 : lane - 6;
+  const int sb = lane == 0 ? 0 : (lane == 1 || lane == 3) ? 1 : (lane == 2 || lane == 4 || lane == 5) ? 2 : 3;
+  int parked = 0;
+  auto finish = [&]() {  // the parked queries, one per lane
+    __builtin_amdgcn_wave_barrier();
+    if (lane < parked) {
+      float a[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) a[k] = s_sum[wv][k][lane];
+      const float4 q = s_q[wv][lane];
+      normals[s_dst[wv][lane]] = finish_normal_pcl(a, __float_as_int(q.w), q.x, q.y, q.z, vpx, vpy, vpz);
+    }
+    __builtin_amdgcn_wave_barrier();
+    parked = 0;
+  };
+  const int nq = qlist ? (int)*qcount : n;
+  const int nruns = (nq + kFqRun - 1) / kFqRun;
+  const int gw = (int)((blockIdx.x * kBS + threadIdx.x) >> 6), nw = (int)((gridDim.x * kBS) >> 6);
+  for (int run = gw; run < nruns; run += nw) {
+    int pcx = -1, pcy = -1, pcz = -1;
+    int2 rg = make_int2(0, 0);  // lane r < 9: row r's contiguous range around the current cell
+    const int i_end = min(nq, (run + 1) * kFqRun);
+    for (int i = run * kFqRun; i < i_end; ++i) {
+      const int t = qlist ? qlist[i] : i;
+      const float qx = sx[t], qy = sy[t], qz = sz[t];
+      if (!finite3(qx, qy, qz)) {
+        if (lane == 0) {
+          const float qn = __builtin_nanf("");
+          normals[sidx[t]] = make_float4(qn, qn, qn, qn);
+        }
+        continue;
+      }
+      const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+      const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+      const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+      if (cx != pcx || cy != pcy || cz != pcz) {
+        pcx = cx; pcy = cy; pcz = cz;
+        // lanes 0..26 look up one cell each; a row's range is its cells' union (contiguous)
+        int2 c = make_int2(INT_MAX, INT_MIN);
+        if (lane < 27) {
+          const int x = cx + lane % 3 - 1, y = cy + (lane / 3) % 3 - 1, z = cz + lane / 9 - 1;
+          if (x >= 0 && y >= 0 && z >= 0 && x < G.g[0] && y < G.g[1] && z < G.g[2]) {
+            const int2 r = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+            if (r.y > r.x) c = r;
+          }
+        }
+        int lo = c.x, hi = c.y;
+#pragma unroll
+        for (int o = 1; o <= 2; o <<= 1) {  // (min / max over each aligned triple of lanes)
+          const int l2 = __shfl(lo, (lane / 3) * 3 + ((lane % 3 + o) % 3), 64);
+          const int h2 = __shfl(hi, (lane / 3) * 3 + ((lane % 3 + o) % 3), 64);
+          lo = min(lo, l2);
+          hi = max(hi, h2);
+        }
+        const int rl = __shfl(lo, 3 * (lane < 9 ? lane : 0), 64);
+        const int rh = __shfl(hi, 3 * (lane < 9 ? lane : 0), 64);
+        rg = lane < 9 && rl < rh ? make_int2(rl, rh) : make_int2(0, 0);
+      }
+      // the 9 rows as one list of 64-candidate steps (lane r < 9: row r's steps; their starts
+      // scanned), walked kFqB steps at a time with every step's loads issued first: one memory
+      // latency per kFqB steps instead of one per step
+      const int rlen = rg.y - rg.x;
+      const int rs = (rlen + 63) >> 6;
+      int incl = rs;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+      }
+      const int nsteps = __shfl(incl, 8, 64);
+      const int first = incl - rs;  // this row's first step
+      int cnt = 0;
+      for (int k0 = 0; k0 < ((XP & 4) ? 0 : nsteps); k0 += kFqB) {
+        float d2[kFqB];
+        int uu[kFqB];
+#pragma unroll
+        for (int j = 0; j < kFqB; ++j) {
+          const int k = k0 + j;
+          // the row holding step k: the lane r < 9 with first <= k < first + rs (ballot)
+          const uint64_t hit = __ballot(lane < 9 && k >= first && k < first + rs);
+          const int r = hit ? (int)__builtin_ctzll(hit) : 0;
+          const int rb = __builtin_amdgcn_readlane(rg.x, r), re = __builtin_amdgcn_readlane(rg.y, r);
+          const int rf = __builtin_amdgcn_readlane(first, r);
+          const int u = rb + ((k - rf) << 6) + lane;
+          uu[j] = u;
+          d2[j] = INFINITY;
+          if (hit && u < re) d2[j] = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
+        }
+#pragma unroll
+        for (int j = 0; j < kFqB; ++j) {
+          const bool in = d2[j] < r2;
+          const uint64_t m = __ballot(in);
+          const int p = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (in && p < kCap) key[p] = ((uint64_t)__float_as_uint(d2[j]) << 32) | (uint32_t)uu[j];
+          cnt += (int)__popcll(m);
+        }
+      }
+      if (cnt > kCap) {  // (too many neighbours for this instantiation)
+        if (lane == 0) ovf[atomicAdd(ovf_count, 1u)] = t;
+        continue;
+      }
+      __builtin_amdgcn_wave_barrier();
+      uint64_t v[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const int e = lane + 64 * j;
+        v[j] = e < cnt ? key[e] : ~0ull;
+      }
+      if (!(XP & 1)) wave_bitonic<E>(v);
+      // (d2, sorted position) -> FLANN's (d2, original index): only equal-d2 runs can differ
+      bool tie = false;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const uint64_t nxt = __shfl_down(v[j], 1, 64);
+        const uint64_t nxt2 = j + 1 < E ? __shfl(v[j + 1 < E ? j + 1 : j], 0, 64) : ~0ull;
+        const uint64_t w = lane == 63 ? nxt2 : nxt;
+        const int e = lane + 64 * j;
+        tie |= e + 1 < cnt && (v[j] >> 32) == (w >> 32);
+      }
+#pragma unroll
+      for (int j = 0; j < E; ++j) key[lane + 64 * j] = v[j];
+      __builtin_amdgcn_wave_barrier();
+      if (__ballot(tie)) {
+        if (lane == 0) {  // insertion sort by (d2, original index): equal-d2 runs move only
+          for (int e = 1; e < cnt; ++e) {
+            const uint64_t kv = key[e];
+            const int id = sidx[(uint32_t)kv];
+            int f = e - 1;
+            while (f >= 0 && (key[f] >> 32) == (kv >> 32) && sidx[(uint32_t)key[f]] > id) {
+              key[f + 1] = key[f];
+              --f;
+            }
+            key[f + 1] = kv;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+#pragma unroll
+      for (int j = 0; j < E; ++j) {  // (every gather issued before the stores)
+        const int e = lane + 64 * j;
+        if (e < cnt) {
+          const uint32_t u = (uint32_t)key[e];
+          nr[e] = make_float4(sx[u], sy[u], sz[u], 1.0f);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // the nine chains, one per lane, in list order (PCL: accu[k] += term, float)
+      float acc = 0.0f;
+      if (lane < 9) {
+        const float* ra = reinterpret_cast<const float*>(nr) + sa;
+        const float* rb = reinterpret_cast<const float*>(nr) + sb;
+#pragma unroll 8
+        for (int e = 0; e < ((XP & 2) ? 0 : cnt); ++e) acc = acc + ra[4 * e] * rb[4 * e];
+        s_sum[wv][lane][parked] = acc;
+      }
+      if (lane == 0) {
+        s_q[wv][parked] = make_float4(qx, qy, qz, __int_as_float(cnt));
+        s_dst[wv][parked] = sidx[t];
+      }
+      if (++parked == 64) finish();
+    }
+  }
+  if (parked) finish();
 }
 
 constexpr int kKnnCap = 32;  // level 0: buffered candidates per query
@@ -1292,6 +1553,24 @@ void launch_nbr_fill_sort_normals(const GridDesc& G, const GridBufs& B, int q0, 
   hipLaunchKernelGGL(k_nbr_sort, dim3(gs), dim3(kBS), 0, s, nq, cnt, off, keys);
   hipLaunchKernelGGL(k_nbr_normals, dim3(cdiv(nq, kBS)), dim3(kBS), 0, s, B.sx, B.sy, B.sz,
                      B.idx_out, q0, nq, cnt, off, keys, X, Y, Z, vp[0], vp[1], vp[2], normals);
+}
+
+void launch_nbr_fused(const GridDesc& G, const GridBufs& B, int n, const int32_t* qlist,
+                      const uint32_t* qcount, int wide, float r2, const float vp[3],
+                      float4* normals, int32_t* ovf, uint32_t* ovf_count, int num_cus,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t waves = qlist ? (int64_t)num_cus * 16 : cdiv(n, kFqRun);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(waves, kBS / 64),
+                                                                      (int64_t)num_cus * 64));
+  auto* k = wide == 2 ? k_nbr_fused_wide<16> : wide == 1 ? k_nbr_fused_wide<8> : k_nbr_fused<4>;
+  if (wide >= 10) {  // (timing experiments: results wrong)
+    const int xp = wide - 10;
+    k = xp == 1 ? k_nbr_fused<4, 1> : xp == 2 ? k_nbr_fused<4, 2> : xp == 3 ? k_nbr_fused<4, 3>
+      : xp == 4 ? k_nbr_fused<4, 4> : k_nbr_fused<4, 7>;
+  }
+  hipLaunchKernelGGL(k, dim3(g), dim3(kBS), 0, s, B.sx, B.sy, B.sz, B.idx_out, n, qlist, qcount, G,
+                     B.tkeys, B.trange, B.tmask, r2, vp[0], vp[1], vp[2], normals, ovf, ovf_count);
 }
 
 __global__ __launch_bounds__(kBS) void k_gather_flags(const uint8_t* __restrict__ f,

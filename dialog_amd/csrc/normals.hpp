@@ -99,6 +99,13 @@ void launch_nbr_fill_sort_normals(const GridDesc& G, const GridBufs& B, int q0, 
                                   const int32_t* cnt, const int64_t* off, uint64_t* keys,
                                   const float* X, const float* Y, const float* Z, const float vp[3],
                                   float4* normals, int num_cus, hipStream_t s);
+// the same radius normals in one fused pass (k_nbr_fused): all n queries (qlist null) or the
+// *qcount sorted positions of qlist; wide = 0: up to 256 neighbours per query, 1: 512, 2: 1024;
+// queries with more go to ovf (count *ovf_count)
+void launch_nbr_fused(const GridDesc& G, const GridBufs& B, int n, const int32_t* qlist,
+                      const uint32_t* qcount, int wide, float r2, const float vp[3],
+                      float4* normals, int32_t* ovf, uint32_t* ovf_count, int num_cus,
+                      hipStream_t s);
 void launch_inverse_perm(const int32_t* idx, int n, int32_t* pos_of, hipStream_t s);
 // out[u] = f[idx[u]] (point-indexed flags -> a level's sorted order)
 void launch_gather_flags(const uint8_t* f, const int32_t* idx, int n, uint8_t* out, hipStream_t s);

@@ -32,13 +32,16 @@ __device__ __forceinline__ uint32_t quant10(float v, float a) {
   return (uint32_t)fminf(fmaxf(t, 0.0f), 1023.0f);
 }
 
+// (also writes the points as (x, y, z, 0) records: k_gather_order and k_ucompact gather from
+// them, one 16-byte record per point instead of three scattered floats)
 __global__ void k_morton_keys(PointsView src, float ax, float ay, float az,
                               uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
-                              int32_t* __restrict__ n_nonfinite) {
+                              int32_t* __restrict__ n_nonfinite, float4* __restrict__ aos) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool nf = false;
   if (i < src.n) {
     const float x = src.x[i], y = src.y[i], z = src.z[i];
+    aos[i] = make_float4(x, y, z, 0.0f);
     uint32_t k = 0xFFFFFFFFu;
     if (isfinite(x) && isfinite(y) && isfinite(z))
       k = spread10(quant10(x, ax)) | (spread10(quant10(y, ay)) << 1) | (spread10(quant10(z, az)) << 2);
@@ -51,14 +54,15 @@ __global__ void k_morton_keys(PointsView src, float ax, float ay, float az,
   if (m && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(n_nonfinite, (int32_t)__popcll(m));
 }
 
-__global__ void k_gather_order(PointsView src, const int32_t* __restrict__ order, int64_t n,
-                               PointsOut dst) {
+__global__ void k_gather_order(const float4* __restrict__ src, const int32_t* __restrict__ order,
+                               int64_t n, PointsOut dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t k = order[i];
-  dst.x[i] = src.x[k];
-  dst.y[i] = src.y[k];
-  dst.z[i] = src.z[k];
+  const float4 v = src[k];
+  dst.x[i] = v.x;
+  dst.y[i] = v.y;
+  dst.z[i] = v.z;
   dst.gid[i] = k;  // the Morton copy's "gid" is the pristine index (lean-list rounds stamp it)
 }
 
@@ -863,10 +867,10 @@ __global__ void k_curv_range(const float4* __restrict__ nrm, int64_t n, uint32_t
 }  // namespace
 
 void launch_morton_keys(PointsView src, float ax, float ay, float az, uint32_t* keys,
-                        int32_t* idx, int32_t* n_nonfinite, hipStream_t s) {
+                        int32_t* idx, int32_t* n_nonfinite, float4* aos, hipStream_t s) {
   if (src.n <= 0) return;
   hipLaunchKernelGGL(k_morton_keys, dim3((unsigned)((src.n + 255) / 256)), dim3(256), 0, s, src,
-                     ax, ay, az, keys, idx, n_nonfinite);
+                     ax, ay, az, keys, idx, n_nonfinite, aos);
 }
 
 size_t morton_sort_temp_bytes(int64_t n) {
@@ -882,7 +886,7 @@ hipError_t morton_sort(void* tmp, size_t tmp_bytes, uint32_t* keys_in, uint32_t*
                                             (int)n, 0, 32, s);
 }
 
-void launch_gather_order(PointsView src, const int32_t* order, int64_t n, PointsOut dst,
+void launch_gather_order(const float4* src, const int32_t* order, int64_t n, PointsOut dst,
                          hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_gather_order, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src,

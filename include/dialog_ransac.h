@@ -405,9 +405,12 @@ enum {
                                device, exact (fsum.hpp); 0 gathered and summed on the host; 2 as 1,
                                the host recomputing every refit's tail from the sums; 3 as 2 and
                                every round's select redone with the host's plane (test) */
-  DLG_OPT_PRUNE_TILE_SCORER = 9 /* the pruned plane scorer's (tile, plane) pairs:
+  DLG_OPT_PRUNE_TILE_SCORER = 9, /* the pruned plane scorer's (tile, plane) pairs:
                                DLG_TILE_EXACT (default) PCL-order f32 with lanes as planes, or
                                DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band re-decision */
+  DLG_OPT_NORMALS_FUSED = 10 /* PCL-float radius normals: 1 (default) search, (d2, index) order
+                               and sums in one fused pass; 0: the chunked count / fill / sort /
+                               sum pipeline */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };

@@ -3,7 +3,7 @@
 
   c2       1M points, 3 planes, one segment() of 4096 hypotheses (configs[1])   pcl, fast refit
   c3       10M points, 20 planes, extract-and-remove (configs[2], the bench)    fast, pcl, none
-  c4shape  100M points, 20 planes, the same extraction on one GPU (configs[3]) fast (if present)
+  c4shape  100M points, 20 planes, the same extraction on one GPU (configs[3]) fast, pcl
 
 Bit-exact: iterations, best sample, coefficient bit patterns, per-plane inlier counts and the
 SHA-256 of every plane's inlier-id list.  The fast refit (the bench's mode) is also run with the

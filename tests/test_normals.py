@@ -219,6 +219,32 @@ def test_gpu_radius_normals_pcl_bit_exact(gpu_ctx, n, patch, r, seed):
 
 
 @pytest.mark.gpu
+def test_gpu_radius_normals_fused_ties_and_chunked(gpu_ctx):
+    """The fused radius pass (DLG_OPT_NORMALS_FUSED = 1, default) on a quantised cloud, where
+    many neighbours tie in d2 and FLANN's order falls back to the point index: bit-identical to
+    the oracle; and on a larger cloud bit-identical to the chunked pipeline (option 0)."""
+    import dialog_amd as D
+    p, _, _ = small_cloud(8000, seed=21, patch=1.5)
+    q = (np.round(p * 64) / 64).astype(np.float32)
+    g = D.estimate_normals(q, radius=0.12, ctx=gpu_ctx)
+    o = O.estimate_normals(q, 0.12)
+    assert np.array_equal(np.isnan(g), np.isnan(o))
+    ok = ~np.isnan(o[:, 0])
+    assert np.array_equal(g[ok].view(np.uint32), o[ok].view(np.uint32))
+    big, _, _ = small_cloud(200000, seed=22, patch=6.0)
+    ctx = D.Context(0)
+    try:
+        f = D.estimate_normals(big, radius=0.1, ctx=ctx)
+        ctx.set_option(D.DLG_OPT_NORMALS_FUSED, 0)
+        c = D.estimate_normals(big, radius=0.1, ctx=ctx)
+    finally:
+        ctx.close()
+    assert np.array_equal(np.isnan(f), np.isnan(c))
+    ok = ~np.isnan(c[:, 0])
+    assert np.array_equal(f[ok].view(np.uint32), c[ok].view(np.uint32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k", [3, 20, 33, 64])
 def test_gpu_knn_normals_pcl_bit_exact(gpu_ctx, k):
     import dialog_amd as D

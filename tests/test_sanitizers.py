@@ -70,3 +70,46 @@ def test_oracle_under_sanitizers(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, env=ENV, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.startswith("checksum ")
+
+
+def test_alpha_shape_under_sanitizers(tmp_path):
+    """The border's host module (dialog_amd/csrc/alpha_shape.hpp: Delaunay sweep-hull, alpha
+    filter, PCL's polygon walk, ConcaveHull's transform chain) under ASan + UBSan, on random,
+    quantised (duplicates, cocircular), collinear and tiny inputs."""
+    exe = str(tmp_path / "alpha_san")
+    src = tmp_path / "alpha_san.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include <random>
+#include <vector>
+#include "alpha_shape.hpp"
+int main() {
+  std::mt19937 g(7);
+  std::uniform_real_distribution<double> u(0.0, 10.0);
+  long total = 0;
+  for (int c = 0; c < 6; ++c) {
+    const int n = c == 5 ? 3 : 2000;
+    std::vector<double> xy(2 * n);
+    for (int i = 0; i < n; ++i) {
+      double x = u(g), y = u(g);
+      if (c == 1) { x = (int)x; y = (int)y; }          // duplicates, cocircular grid points
+      if (c == 2) { y = 2 * (int)x + 1; x = (int)x; }  // exactly collinear
+      if (c == 3) { x *= 1e-7; y *= 1e-7; }
+      xy[2 * i] = x; xy[2 * i + 1] = y;
+    }
+    const dlg::alpha::Tri2 T = dlg::alpha::Delaunay(xy.data(), n).run();
+    const dlg::alpha::AlphaShape S = dlg::alpha::alpha_shape(xy.data(), T, c == 3 ? 1e-7 : 0.5);
+    std::vector<float> p3(3 * (size_t)n);
+    for (int i = 0; i < n; ++i) { p3[3 * i] = (float)xy[2 * i]; p3[3 * i + 1] = (float)xy[2 * i + 1]; p3[3 * i + 2] = 0.25f * (float)xy[2 * i]; }
+    const dlg::alpha::Hull2 H = dlg::alpha::concave_hull_2d(p3.data(), n, 0.5);
+    total += (long)T.tri.size() + (long)S.av.size() + (long)H.pts.size();
+  }
+  std::printf("%ld\n", total);
+  return 0;
+}
+''')
+    subprocess.run(["g++", "-std=c++17", *SAN, "-I", os.path.join(ROOT, "dialog_amd/csrc"), str(src),
+                    "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, env=ENV, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert int(r.stdout.split()[0]) > 0
