@@ -585,17 +585,20 @@ __global__ __launch_bounds__(kBS) void k_nbr_normals(
 // ---- fused radius normals (PCL float): search, (d2, index) order and the sums in one pass ----
 // One wave per query at a time, queries taken in runs of kFqRun consecutive sorted positions.
 // Per query: the 27 cells around it are 9 runs of sorted positions (a row's three x cells have
-// consecutive keys, so their ranges are contiguous; looked up once per run cell, lane r < 9
-// holding row r's range), scanned 64 candidates per step with FLANN's d2 and test (the
-// neighbour set is KdTreeFLANN's); the passing ones are compacted into the wave's LDS as keys
-// (d2 bits << 32 | sorted position), sorted in registers (wave bitonic, 64 E keys), reordered by
-// the points' original index where d2 ties (FLANN's (d2, index) order: sorted positions follow
-// the original index only within a cell), and their coordinates staged in LDS in that order;
-// lanes 0..8 then run computeMeanAndCovarianceMatrix's nine float chains in list order (each
-// lane its chain's operand pair, no divergence).  The sums of 64 queries are parked in LDS and
-// finished (eigen33, curvature, viewpoint flip) with one query per lane.  Nothing per neighbour
-// leaves the chip (the chunked pipeline writes, sorts and re-reads 8 bytes per neighbour).  A
-// query with more than 64 E neighbours goes to the overflow list for the next, wider launch.
+// consecutive keys, so their ranges are contiguous; looked up when the query's cell changes),
+// packed into one candidate list scanned 64 per step with FLANN's d2 and test (the neighbour
+// set is KdTreeFLANN's); the passing ones are compacted into the wave's LDS buffer as
+// keys (d2 bits << 32 | sorted position), sorted in registers by a wave bitonic sized to the
+// count (64, 128, 256, 512 ... keys), reordered by the points' original index where d2 ties
+// (FLANN's (d2, index) order: sorted positions follow the original index only within a cell),
+// and the neighbours' coordinates gathered from the sorted keys and staged over the same buffer as
+// (x, y, z) triplets in that order; lanes 0..8 then run computeMeanAndCovarianceMatrix's nine
+// float chains in list order (each lane reading its chain's two operands at its own offsets).
+// The sums of 64 queries are parked in LDS and finished (eigen33, curvature, viewpoint flip)
+// with one query per lane.  Nothing per neighbour leaves the chip (the chunked pipeline writes,
+// sorts and re-reads 8 bytes per neighbour).  A query with more than 64 EMAX neighbours goes to
+// the overflow list for the next, wider launch.  Every LDS access of the shared buffer is a
+// 32-bit word access or a memcpy (the keys and the coordinates alias).
 constexpr int kFqRun = 16;
 constexpr int kFqB = 4;  // candidate steps whose loads are in flight together
 #define DLG_NBR_FUSED_ARGS                                                                        \
@@ -605,39 +608,126 @@ constexpr int kFqB = 4;  // candidate steps whose loads are in flight together
         const int2 *__restrict__ trange, uint32_t tmask, float r2, float vpx, float vpy,         \
         float vpz, float4 *__restrict__ normals, int32_t *__restrict__ ovf,                      \
         uint32_t *__restrict__ ovf_count
-template <int E, int XP>
+template <int EMAX, int XP>
 __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS);
 
-// the first pass (<= 256 neighbours) held to 128 VGPRs: four waves per SIMD, as many as its LDS
-// allows; the wider passes are LDS-limited to fewer waves anyway
-template <int E, int XP = 0>  // XP: timing experiment (bit 0 no sort, 1 no sum, 2 no scan)
+// the first pass (<= 512 neighbours) held to 128 VGPRs: four waves per SIMD, as many as its LDS
+// allows; the wider pass (<= 1024) is LDS-limited to fewer waves anyway
+template <int EMAX, int XP = 0>  // XP: timing experiment (bit 0 no sort, 1 no sum, 2 no scan)
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(4))) void k_nbr_fused(
     DLG_NBR_FUSED_ARGS) {
-  nbr_fused_body<E, XP>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx, vpy,
-                        vpz, normals, ovf, ovf_count);
+  nbr_fused_body<EMAX, XP>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx,
+                           vpy, vpz, normals, ovf, ovf_count);
 }
-template <int E>
+template <int EMAX>
 __global__ __launch_bounds__(kBS) void k_nbr_fused_wide(DLG_NBR_FUSED_ARGS) {
-  nbr_fused_body<E, 0>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx, vpy,
-                       vpz, normals, ovf, ovf_count);
+  nbr_fused_body<EMAX, 0>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx,
+                          vpy, vpz, normals, ovf, ovf_count);
 }
 
-template <int E, int XP>
+__device__ __forceinline__ uint64_t lds_key(const uint32_t* buf, int e) {
+  uint64_t k;
+  __builtin_memcpy(&k, buf + 2 * e, 8);
+  return k;
+}
+__device__ __forceinline__ void lds_set_key(uint32_t* buf, int e, uint64_t k) {
+  __builtin_memcpy(buf + 2 * e, &k, 8);
+}
+
+// the wave's cnt (<= 64 E) keys in buf -> FLANN's (d2, original index) order, then the
+// neighbours' (x, y, z) staged over the keys in that order (word 3 e + axis)
+template <int E, bool kSort>
+__device__ __forceinline__ void nbr_order_stage(uint32_t* buf, int cnt,
+                                                const float* __restrict__ sx,
+                                                const float* __restrict__ sy,
+                                                const float* __restrict__ sz,
+                                                const int32_t* __restrict__ sidx) {
+  const int lane = threadIdx.x & 63;
+  uint64_t v[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = lane + 64 * j;
+    v[j] = e < cnt ? lds_key(buf, e) : ~0ull;
+  }
+  if (kSort) wave_bitonic<E>(v);
+  // (d2, sorted position) -> FLANN's (d2, original index): only equal-d2 runs can differ
+  bool tie = false;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const uint64_t nxt = __shfl_down(v[j], 1, 64);
+    const uint64_t nxt2 = j + 1 < E ? __shfl(v[j + 1 < E ? j + 1 : j], 0, 64) : ~0ull;
+    const uint64_t w = lane == 63 ? nxt2 : nxt;
+    const int e = lane + 64 * j;
+    tie |= e + 1 < cnt && (v[j] >> 32) == (w >> 32);
+  }
+  if (__ballot(tie)) {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < E; ++j) lds_set_key(buf, lane + 64 * j, v[j]);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {  // insertion sort by (d2, original index): equal-d2 runs move only
+      for (int e = 1; e < cnt; ++e) {
+        const uint64_t kv = lds_key(buf, e);
+        const int id = sidx[(uint32_t)kv];
+        int f = e - 1;
+        while (f >= 0 && (lds_key(buf, f) >> 32) == (kv >> 32) &&
+               sidx[(uint32_t)lds_key(buf, f)] > id) {
+          lds_set_key(buf, f + 1, lds_key(buf, f));
+          --f;
+        }
+        lds_set_key(buf, f + 1, kv);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int e = lane + 64 * j;
+      v[j] = e < cnt ? lds_key(buf, e) : ~0ull;
+    }
+  }
+  float x[E], y[E], z[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {  // (every gather issued before the stores)
+    const uint32_t u = (uint32_t)v[j];
+    const bool in = lane + 64 * j < cnt;
+    x[j] = in ? sx[u] : 0.0f;
+    y[j] = in ? sy[u] : 0.0f;
+    z[j] = in ? sz[u] : 0.0f;
+  }
+  __builtin_amdgcn_wave_barrier();  // (the keys are read: the triplets overwrite them)
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = lane + 64 * j;
+    if (e < cnt) {
+      buf[3 * e] = __float_as_uint(x[j]);
+      buf[3 * e + 1] = __float_as_uint(y[j]);
+      buf[3 * e + 2] = __float_as_uint(z[j]);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int EMAX, int XP>
 __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
-  constexpr int kCap = 64 * E;
+  constexpr int kCap = 64 * EMAX;
   constexpr int kW = kBS / 64;
-  __shared__ uint64_t s_key[kW][kCap];
-  __shared__ float4 s_nr[kW][kCap];  // the neighbours in list order: (x, y, z, 1)
+  __shared__ __attribute__((aligned(16))) uint32_t s_buf[kW][3 * kCap];  // keys, then (x, y, z)
   __shared__ float s_sum[kW][9][64];  // parked sums: [chain][slot]
   __shared__ float4 s_q[kW][64];      // (query xyz, count) per slot
   __shared__ int32_t s_dst[kW][64];   // output point index per slot
+  // the 27 cells around the current cell as 9 rows of contiguous sorted positions: row r's
+  // start in the packed candidate list [r], its offset to sorted positions [9 + r], the list's
+  // length [18]
+  __shared__ int32_t s_rows[kW][20];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t* key = s_key[wv];
-  float4* nr = s_nr[wv];
-  // lane c < 9 runs chain c: term = pa * pb (pb = the record's 1 for the coordinate sums: x * 1
-  // = x exactly), each lane reading its two operands at its own offsets in the record
+  uint32_t* buf = s_buf[wv];
+  int32_t* rows = s_rows[wv];
+  // lane c < 9 runs chain c: term = pa * pb, the coordinate sums (pb = 1: x * 1 = x exactly)
+  // selecting 1 in place of a second operand
   const int sa = lane < 3 ? 0 : lane < 5 ? 1 : lane < 6 ? 2 : lane - 6;
   const int sb = lane == 0 ? 0 : (lane == 1 || lane == 3) ? 1 : (lane == 2 || lane == 4 || lane == 5) ? 2 : 3;
+  const bool one_b = sb == 3;
+  const int ob = one_b ? 0 : sb;
   int parked = 0;
   auto finish = [&]() {  // the parked queries, one per lane
     __builtin_amdgcn_wave_barrier();
@@ -656,7 +746,6 @@ __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
   const int gw = (int)((blockIdx.x * kBS + threadIdx.x) >> 6), nw = (int)((gridDim.x * kBS) >> 6);
   for (int run = gw; run < nruns; run += nw) {
     int pcx = -1, pcy = -1, pcz = -1;
-    int2 rg = make_int2(0, 0);  // lane r < 9: row r's contiguous range around the current cell
     const int i_end = min(nq, (run + 1) * kFqRun);
     for (int i = run * kFqRun; i < i_end; ++i) {
       const int t = qlist ? qlist[i] : i;
@@ -692,37 +781,48 @@ __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
         }
         const int rl = __shfl(lo, 3 * (lane < 9 ? lane : 0), 64);
         const int rh = __shfl(hi, 3 * (lane < 9 ? lane : 0), 64);
-        rg = lane < 9 && rl < rh ? make_int2(rl, rh) : make_int2(0, 0);
-      }
-      // the 9 rows as one list of 64-candidate steps (lane r < 9: row r's steps; their starts
-      // scanned), walked kFqB steps at a time with every step's loads issued first: one memory
-      // latency per kFqB steps instead of one per step
-      const int rlen = rg.y - rg.x;
-      const int rs = (rlen + 63) >> 6;
-      int incl = rs;
+        const int2 rg = lane < 9 && rl < rh ? make_int2(rl, rh) : make_int2(0, 0);
+        const int rlen = rg.y - rg.x;
+        int incl = rlen;  // (lanes 0..8: inclusive prefix of the row lengths)
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const int v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
+        for (int o = 1; o < 16; o <<= 1) {
+          const int w = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += w;
+        }
+        const int excl = incl - rlen;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 9) {
+          rows[lane] = excl;
+          rows[9 + lane] = rg.x - excl;
+        }
+        if (lane == 8) rows[18] = incl;
+        __builtin_amdgcn_wave_barrier();
       }
-      const int nsteps = __shfl(incl, 8, 64);
-      const int first = incl - rs;  // this row's first step
+      // (re-read per query: live only during the scan)
+      int r_start[9], r_off[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        r_start[q] = rows[q];
+        r_off[q] = rows[9 + q];
+      }
+      const int tot = rows[18];
+      // the 9 rows' candidates as one packed list: position v of the list lies in row r, the
+      // last row whose start P_r <= v, at sorted position v + (begin_r - P_r); row starts and
+      // offsets are wave-uniform (scalars), recomputed when the query's cell changes.  64
+      // positions per step, kFqB steps with their loads in flight together.
       int cnt = 0;
-      for (int k0 = 0; k0 < ((XP & 4) ? 0 : nsteps); k0 += kFqB) {
+      for (int k0 = 0; k0 < ((XP & 4) ? 0 : tot); k0 += 64 * kFqB) {
         float d2[kFqB];
         int uu[kFqB];
 #pragma unroll
         for (int j = 0; j < kFqB; ++j) {
-          const int k = k0 + j;
-          // the row holding step k: the lane r < 9 with first <= k < first + rs (ballot)
-          const uint64_t hit = __ballot(lane < 9 && k >= first && k < first + rs);
-          const int r = hit ? (int)__builtin_ctzll(hit) : 0;
-          const int rb = __builtin_amdgcn_readlane(rg.x, r), re = __builtin_amdgcn_readlane(rg.y, r);
-          const int rf = __builtin_amdgcn_readlane(first, r);
-          const int u = rb + ((k - rf) << 6) + lane;
+          const int v = k0 + 64 * j + lane;
+          int u = v + r_off[0];
+#pragma unroll
+          for (int q = 1; q < 9; ++q) u = v >= r_start[q] ? v + r_off[q] : u;
           uu[j] = u;
           d2[j] = INFINITY;
-          if (hit && u < re) d2[j] = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
+          if (v < tot) d2[j] = flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]);
         }
 #pragma unroll
         for (int j = 0; j < kFqB; ++j) {
@@ -730,7 +830,8 @@ __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
           const uint64_t m = __ballot(in);
           const int p = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          if (in && p < kCap) key[p] = ((uint64_t)__float_as_uint(d2[j]) << 32) | (uint32_t)uu[j];
+          if (in && p < kCap)
+            lds_set_key(buf, p, ((uint64_t)__float_as_uint(d2[j]) << 32) | (uint32_t)uu[j]);
           cnt += (int)__popcll(m);
         }
       }
@@ -739,63 +840,30 @@ __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
         continue;
       }
       __builtin_amdgcn_wave_barrier();
-      uint64_t v[E];
-#pragma unroll
-      for (int j = 0; j < E; ++j) {
-        const int e = lane + 64 * j;
-        v[j] = e < cnt ? key[e] : ~0ull;
-      }
-      if (!(XP & 1)) wave_bitonic<E>(v);
-      // (d2, sorted position) -> FLANN's (d2, original index): only equal-d2 runs can differ
-      bool tie = false;
-#pragma unroll
-      for (int j = 0; j < E; ++j) {
-        const uint64_t nxt = __shfl_down(v[j], 1, 64);
-        const uint64_t nxt2 = j + 1 < E ? __shfl(v[j + 1 < E ? j + 1 : j], 0, 64) : ~0ull;
-        const uint64_t w = lane == 63 ? nxt2 : nxt;
-        const int e = lane + 64 * j;
-        tie |= e + 1 < cnt && (v[j] >> 32) == (w >> 32);
-      }
-#pragma unroll
-      for (int j = 0; j < E; ++j) key[lane + 64 * j] = v[j];
-      __builtin_amdgcn_wave_barrier();
-      if (__ballot(tie)) {
-        if (lane == 0) {  // insertion sort by (d2, original index): equal-d2 runs move only
-          for (int e = 1; e < cnt; ++e) {
-            const uint64_t kv = key[e];
-            const int id = sidx[(uint32_t)kv];
-            int f = e - 1;
-            while (f >= 0 && (key[f] >> 32) == (kv >> 32) && sidx[(uint32_t)key[f]] > id) {
-              key[f + 1] = key[f];
-              --f;
-            }
-            key[f + 1] = kv;
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-#pragma unroll
-      for (int j = 0; j < E; ++j) {  // (every gather issued before the stores)
-        const int e = lane + 64 * j;
-        if (e < cnt) {
-          const uint32_t u = (uint32_t)key[e];
-          nr[e] = make_float4(sx[u], sy[u], sz[u], 1.0f);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
+      constexpr bool kS = !(XP & 1);
+      if (cnt <= 64) nbr_order_stage<1, kS>(buf, cnt, sx, sy, sz, sidx);
+      else if (cnt <= 128) nbr_order_stage<2, kS>(buf, cnt, sx, sy, sz, sidx);
+      else if (cnt <= 256 || EMAX < 8) nbr_order_stage<(EMAX < 4 ? EMAX : 4), kS>(buf, cnt, sx, sy, sz, sidx);
+      else if (cnt <= 512 || EMAX < 16) nbr_order_stage<(EMAX < 8 ? EMAX : 8), kS>(buf, cnt, sx, sy, sz, sidx);
+      else nbr_order_stage<EMAX, kS>(buf, cnt, sx, sy, sz, sidx);
       // the nine chains, one per lane, in list order (PCL: accu[k] += term, float)
       float acc = 0.0f;
       if (lane < 9) {
-        const float* ra = reinterpret_cast<const float*>(nr) + sa;
-        const float* rb = reinterpret_cast<const float*>(nr) + sb;
+        const uint32_t* ra = buf + sa;
+        const uint32_t* rb = buf + ob;
 #pragma unroll 8
-        for (int e = 0; e < ((XP & 2) ? 0 : cnt); ++e) acc = acc + ra[4 * e] * rb[4 * e];
+        for (int e = 0; e < ((XP & 2) ? 0 : cnt); ++e) {
+          const float pa = __uint_as_float(ra[3 * e]);
+          const float pb = one_b ? 1.0f : __uint_as_float(rb[3 * e]);
+          acc = acc + pa * pb;
+        }
         s_sum[wv][lane][parked] = acc;
       }
       if (lane == 0) {
         s_q[wv][parked] = make_float4(qx, qy, qz, __int_as_float(cnt));
         s_dst[wv][parked] = sidx[t];
       }
+      __builtin_amdgcn_wave_barrier();  // (the next query's keys overwrite the triplets)
       if (++parked == 64) finish();
     }
   }
@@ -1563,11 +1631,11 @@ void launch_nbr_fused(const GridDesc& G, const GridBufs& B, int n, const int32_t
   const int64_t waves = qlist ? (int64_t)num_cus * 16 : cdiv(n, kFqRun);
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(waves, kBS / 64),
                                                                       (int64_t)num_cus * 64));
-  auto* k = wide == 2 ? k_nbr_fused_wide<16> : wide == 1 ? k_nbr_fused_wide<8> : k_nbr_fused<4>;
+  auto* k = wide ? k_nbr_fused_wide<16> : k_nbr_fused<8>;
   if (wide >= 10) {  // (timing experiments: results wrong)
     const int xp = wide - 10;
-    k = xp == 1 ? k_nbr_fused<4, 1> : xp == 2 ? k_nbr_fused<4, 2> : xp == 3 ? k_nbr_fused<4, 3>
-      : xp == 4 ? k_nbr_fused<4, 4> : k_nbr_fused<4, 7>;
+    k = xp == 1 ? k_nbr_fused<8, 1> : xp == 2 ? k_nbr_fused<8, 2> : xp == 3 ? k_nbr_fused<8, 3>
+      : xp == 4 ? k_nbr_fused<8, 4> : k_nbr_fused<8, 7>;
   }
   hipLaunchKernelGGL(k, dim3(g), dim3(kBS), 0, s, B.sx, B.sy, B.sz, B.idx_out, n, qlist, qcount, G,
                      B.tkeys, B.trange, B.tmask, r2, vp[0], vp[1], vp[2], normals, ovf, ovf_count);

@@ -100,8 +100,8 @@ void launch_nbr_fill_sort_normals(const GridDesc& G, const GridBufs& B, int q0, 
                                   const float* X, const float* Y, const float* Z, const float vp[3],
                                   float4* normals, int num_cus, hipStream_t s);
 // the same radius normals in one fused pass (k_nbr_fused): all n queries (qlist null) or the
-// *qcount sorted positions of qlist; wide = 0: up to 256 neighbours per query, 1: 512, 2: 1024;
-// queries with more go to ovf (count *ovf_count)
+// *qcount sorted positions of qlist; wide = 0: up to 512 neighbours per query, 1: 1024; queries
+// with more go to ovf (count *ovf_count)
 void launch_nbr_fused(const GridDesc& G, const GridBufs& B, int n, const int32_t* qlist,
                       const uint32_t* qcount, int wide, float r2, const float vp[3],
                       float4* normals, int32_t* ovf, uint32_t* ovf_count, int num_cus,

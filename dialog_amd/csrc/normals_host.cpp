@@ -266,21 +266,18 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
     if (!pclf) {
       launch_normals_radius(G, B, n, r2, vp, w.nrm.p, c->stream);
     } else if (!chunked) {
-      // one fused pass (<= 256 neighbours per query), the overflow in wider ones (<= 512, then
-      // <= 1024); a query beyond that (none at the configs' radii) sends the whole call down the
-      // chunked path
+      // one fused pass (<= 512 neighbours per query), the overflow in a wider one (<= 1024); a
+      // query beyond that (none at the configs' radii) sends the whole call down the chunked path
       w.ovfa.ensure(n);
       w.ovfb.ensure(n);
-      w.ovfc.ensure(3);
+      w.ovfc.ensure(2);
       w.h_cnt.ensure(2);
-      HIPCHK(hipMemsetAsync(w.ovfc.p, 0, 3 * sizeof(uint32_t), c->stream));
+      HIPCHK(hipMemsetAsync(w.ovfc.p, 0, 2 * sizeof(uint32_t), c->stream));
       launch_nbr_fused(G, B, n, nullptr, nullptr, c->opt.nbr_xp ? 10 + c->opt.nbr_xp : 0, r2, vp,
                        w.nrm.p, w.ovfa.p, w.ovfc.p, c->num_cus, c->stream);
       launch_nbr_fused(G, B, n, w.ovfa.p, w.ovfc.p, 1, r2, vp, w.nrm.p, w.ovfb.p, w.ovfc.p + 1,
                        c->num_cus, c->stream);
-      launch_nbr_fused(G, B, n, w.ovfb.p, w.ovfc.p + 1, 2, r2, vp, w.nrm.p, w.ovfa.p, w.ovfc.p + 2,
-                       c->num_cus, c->stream);
-      HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.ovfc.p + 2, sizeof(uint32_t), hipMemcpyDeviceToHost,
+      HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.ovfc.p + 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
                             c->stream));
       sync(c);
       chunked = w.h_cnt.p[0] > 0;

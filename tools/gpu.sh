@@ -15,6 +15,7 @@
 #   pmc                                   FETCH/WRITE/SQ-issue PMC passes of the scoring launch
 #                                         -> traffic.py / pmc_issue.py summaries
 #   c5                                    tools/bench_c5.py (normals, RegulateNormal, chain)
+#   c5prof                                rocprofv3 --kernel-trace --stats over tools/c5_kernels.py
 #   walk                                  tools/fs_walk_stats.py (PCL float-sum walk counters)
 #   py=<script,args...>                   any python script (comma-separated argv)
 set -uo pipefail
@@ -65,6 +66,8 @@ for s in "$@"; do
       python3 tools/pmc_kern.py k_score_tiles $(find "$O/pmcab_a" "$O/pmcab_b" -name '*counter_collection.csv') > "$O/pmcab.json" 2>&1
       cat "$O/pmcab.json" ;;
     c5) run c5 600 python3 -u tools/bench_c5.py ${arg//,/ } ;;
+    c5prof) run c5prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5prof" -o run -- \
+              python3 tools/c5_kernels.py ${arg//,/ } ;;
     walk) run walk 300 python3 -u tools/fs_walk_stats.py ${arg//,/ } ;;
     py) run py_$(basename "${arg%%,*}" .py) 900 python3 -u ${arg//,/ } ;;
     *) echo "unknown step $name"; exit 2 ;;
