@@ -454,8 +454,9 @@ __device__ __forceinline__ void fs_seq_prep(const FsWalkRec wr, int cnt, int lan
 // Chains hovering near zero (many start-dependent records, a few reruns per window) are then
 // walked one lookup per window instead of record by record.  The tables are built by the walk
 // kernel's own builder workgroups while the walkers run (k_fs_walk): a table is published with
-// this launch's stamp (release) and the walker uses it only if the stamp is there when it arrives
-// (acquire); otherwise it walks the window itself -- nobody waits.
+// this launch's stamp (release); the walker polls a batch's stamps at once (relaxed, then one
+// acquire fence) and again at a window whose table was not there yet, and uses a table only if
+// its stamp is there when it arrives; otherwise it walks the window itself -- nobody waits.
 constexpr int kFtLo = 32;  // entry leads -kFtLo .. 63 - kFtLo
 struct FsTabLds {
   uint4 sq[kWave][3];
@@ -1085,6 +1086,23 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
     const bool valid = lane < nb && sm.w == sm.w &&
                        (!has_next || __float_as_uint(sm.y) == __float_as_uint(gnx));
     const uint64_t stat = ballot(lane < nb && !valid);  // (walked at any lag: prefetch candidates)
+    // the batch's transfer tables published so far (lane = window): one relaxed poll of the
+    // stamps and one acquire fence per batch, then the tables' masks and quanta; a window whose
+    // table was not ready at the batch's start is polled again when the walk reaches it
+    // (fs_wtab_item builds tables only for windows without a fast summary)
+    const uint64_t tabled = ballot(lane < nb && !(sm.z >= 0.0f && sm.w == sm.w));
+    uint4 tm = make_uint4(0u, 0u, 0u, 0u);
+    const uint4* metas = d.b.wmeta + c * d.b.wcap + wb;
+    if ((tabled >> lane) & 1)
+      tm.w = __hip_atomic_load(&metas[lane].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t rdy = ballot(((tabled >> lane) & 1) && tm.w == d.gen);
+    if (rdy) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if ((rdy >> lane) & 1) {
+        const uint4 mv = metas[lane];
+        tm.x = mv.x; tm.y = mv.y; tm.z = mv.z;
+      }
+    }
     const double iqx = valid ? 1.0 / (double)sm.w : 0.0;  // (exact: a power of two)
     int i = 0;
     while (i < nb) {
@@ -1122,11 +1140,20 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
       const int64_t w = wb + f;
       {  // the window's transfer table, if its builder has published it (fs_wtab_item): the
          // exit value when the entry lead is in it
-        uint4* meta = d.b.wmeta + c * d.b.wcap + w;
-        const uint32_t stamp = __hip_atomic_load(&meta->w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t tmask = stamp != d.gen ? 0ull : (uint64_t)meta->x | ((uint64_t)meta->y << 32);
+        uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)tm.x, f);
+        uint32_t my = (uint32_t)__builtin_amdgcn_readlane((int)tm.y, f);
+        uint32_t mq = (uint32_t)__builtin_amdgcn_readlane((int)tm.z, f);
+        if (((tabled & ~rdy) >> f) & 1) {  // (not ready at the batch's start: poll again)
+          const uint4* meta = metas + f;
+          if (__hip_atomic_load(&meta->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d.gen) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            const uint4 mv = *meta;
+            mx = mv.x; my = mv.y; mq = mv.z;
+          }
+        }
+        const uint64_t tmask = (uint64_t)mx | ((uint64_t)my << 32);
         if (tmask) {
-          const double Q = (double)__uint_as_float(meta->z);
+          const double Q = (double)__uint_as_float(mq);
           // the lead t - g_0 with its rounding error (TwoSum: it must be exact), in units of Q
           const double ta = (double)t, gb = -(double)g0f(sm, f);
           const double sd = ta + gb, bv = sd - ta;
