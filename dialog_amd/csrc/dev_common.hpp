@@ -37,14 +37,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// pcl_dot of one plane with two points at once (v_pk_mul_f32 / v_pk_add_f32: each half is the
-// same IEEE f32 operation as pcl_dot's, in the same order; -ffp-contract=off keeps them unfused)
-__device__ __forceinline__ f32x2 pcl_dot2(float a, float b, float c, float d, f32x2 x, f32x2 y,
-                                          f32x2 z) {
-  const f32x2 A = {a, a}, B = {b, b}, C = {c, c}, Dd = {d, d};
-  return (A * x + C * z) + (B * y + Dd);
-}
-
 constexpr uint32_t kBf16One = 0x3F80u;
 
 struct Split3 {

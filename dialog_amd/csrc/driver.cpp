@@ -280,16 +280,16 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
     tmp.ensure(std::max<size_t>(tb, 16));
     c->totals.ensure(8);
     HIPCHK(hipMemsetAsync(c->totals.p, 0, 4, c->stream));
-    cl->paos.ensure((size_t)std::max<int64_t>(n, 1));
+    c->mxyz.ensure((size_t)std::max<int64_t>(n, 1));
     launch_morton_keys(cl->pristine.view(n), cl->amax[0], cl->amax[1], cl->amax[2], k0.p, i0.p,
-                       c->totals.p, cl->paos.p, c->stream);
+                       c->totals.p, c->mxyz.p, c->stream);
     HIPCHK(morton_sort(tmp.p, tb, k0.p, k1.p, i0.p, i1.p, n, c->stream));
     int32_t nonfinite = 0;
     HIPCHK(hipMemcpyAsync(&nonfinite, c->totals.p, 4, hipMemcpyDeviceToHost, c->stream));
     sync(c);
     const int64_t m = n - nonfinite;
     cl->sp_pristine.ensure((size_t)std::max<int64_t>(m, 1));
-    launch_gather_order(cl->paos.p, i1.p, m, cl->sp_pristine.out(), c->stream);
+    launch_gather_order(c->mxyz.p, i1.p, m, cl->sp_pristine.out(), c->stream);
     cl->sp_order.ensure((size_t)std::max<int64_t>(m, 1));
     if (m > 0)
       HIPCHK(hipMemcpyAsync(cl->sp_order.p, i1.p, (size_t)m * 4, hipMemcpyDeviceToDevice, c->stream));
@@ -723,8 +723,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         cl->ubits_dirty = true;
         launch_ustamp(sp_cur_view(), sv.tiles, sv.supers, pmargin, bc_dev, mt, cl->ubits.p,
                       c->stream);
-        launch_ucompact(cl->ubits.p, nw, cl->paos.p, c->sel1, c->fs_x.p, c->fs_y.p, c->fs_z.p,
-                        c->fs_n.p, c->stream);
+        launch_ucompact(cl->ubits.p, nw, cl->pristine.view(cl->n_total), c->sel1, c->fs_x.p,
+                        c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
         HIPCHK(hipGetLastError());
         cl->ubits_dirty = false;
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
@@ -1273,7 +1273,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->lp_n.release();
   c->fs_scr.release();
   c->fs_x.release(); c->fs_y.release(); c->fs_z.release(); c->fs_n.release();
-  c->mk0.release(); c->mk1.release(); c->mi0.release(); c->mi1.release(); c->msort.release();
+  c->mk0.release(); c->mk1.release(); c->mi0.release(); c->mi1.release(); c->msort.release(); c->mxyz.release();
   c->mom_done.release(); c->pick_done.release();
   if (c->ev_stage) (void)hipEventDestroy(c->ev_stage);
   if (c->ev_inl) (void)hipEventDestroy(c->ev_inl);
@@ -1373,7 +1373,6 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     cl->sp_pristine.release();
     cl->sp_tiles_pr.release();
     cl->sp_supers_pr.release();
-    cl->paos.release();
     return s;
   }
   *out = cl.release();
@@ -1393,7 +1392,6 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
   cl->sp_tiles_pr.release();
   cl->sp_supers_pr.release();
   cl->sp_order.release();
-  cl->paos.release();
   for (int b = 0; b < 2; ++b) {
     cl->sp_tb[b].release();
     cl->sp_sb[b].release();
@@ -1712,7 +1710,7 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         break;
       case DLG_OPT_NORMALS_FUSED: o.nbr_fused = value != 0; o.nbr_xp = value >= 10 ? (int)value - 10 : 0; break;
       case DLG_OPT_PRUNE_TILE_SCORER:
-        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && !(value >= 11 && value <= 15))
+        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && !(value >= 11 && value <= 14))
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
         o.tile_scorer = value == DLG_TILE_EXACT ? kTileScorerExact : value == DLG_TILE_BF16 ? kTileScorerBf16 : (int)value;
         break;

@@ -259,6 +259,7 @@ struct dlg_ctx {
   DevBuf<uint32_t> mk0, mk1;
   DevBuf<int32_t> mi0, mi1;
   DevBuf<uint8_t> msort;
+  DevBuf<float4> mxyz;  // the points as (x, y, z, 0) records: k_gather_order's source
   int64_t fs_cap = -1;
   FsBuffers fs_b;
   DevBuf<float> fs_x, fs_y, fs_z;  // lean rounds: the unrefined plane's inliers in list order
@@ -276,7 +277,6 @@ struct dlg_cloud {
   int64_t n_active = 0;
   int cur = -1;  // -1 pristine, 0 = A, 1 = B
   SoA pristine, buf[2];
-  DevBuf<float4> paos;  // the pristine points as (x, y, z, 0) records (with the Morton copy)
   float amax[3] = {0, 0, 0};
   float fmax = 0.0f;         // largest |coordinate| of the finite points (this rank's)
   bool qexp_known = false;   // fast refit quantum exponent (global over ranks), set lazily

@@ -443,7 +443,8 @@ __device__ __forceinline__ void fs_seq_prep(const FsWalkRec wr, int cnt, int lan
 }
 
 // Window transfer table (the walk's lookup for a window it would walk record by record): the
-// window's records applied to each of the 64 entry leads -kFtLo..63-kFtLo at once, lane = entry
+// window's records applied to each of the entry leads -kFtLo..kFtW-1-kFtLo, 64 at once (one
+// builder item per half of the table), lane = entry
 // lead L (entering at t = g_0 + L Q, Q the window's smallest quantum).  Record k is applied as
 // fs_seq_window applies it: covered by the lemma (member i = (L_k >> s_k) & 3, the grid, margin
 // and quanta conditions) it steps L_{k+1} = L_k + E_k[i]; otherwise the lane reruns the chunk's
@@ -454,17 +455,22 @@ __device__ __forceinline__ void fs_seq_prep(const FsWalkRec wr, int cnt, int lan
 // Chains hovering near zero (many start-dependent records, a few reruns per window) are then
 // walked one lookup per window instead of record by record.  The tables are built by the walk
 // kernel's own builder workgroups while the walkers run (k_fs_walk): a table is published with
-// this launch's stamp (release); the walker polls a batch's stamps at once (relaxed, then one
-// acquire fence) and again at a window whose table was not there yet, and uses a table only if
-// its stamp is there when it arrives; otherwise it walks the window itself -- nobody waits.
-constexpr int kFtLo = 32;  // entry leads -kFtLo .. 63 - kFtLo
+// this launch's stamp in every 8-byte entry; the walker prefetches the tables of the next 16
+// windows into LDS when it first needs one of them, reads an entry again from memory when its
+// prefetched copy was not there yet, and uses an entry only if it carries the stamp; otherwise
+// it walks the window itself -- nobody waits.
+constexpr int kFtHalves = 2;                // builder items per window (64 leads each)
+constexpr int kFtW = kFtHalves * kWave;      // table width: entry leads -kFtLo .. kFtW - 1 - kFtLo
+constexpr int kFtLo = kFtW / 2;
+constexpr int kFtGroup = 8;  // windows whose tables the walker prefetches at once
+constexpr int kFtLdsWords = kFtGroup * kFtW + kWave;  // (8-byte words: entries, then the quanta)
 struct FsTabLds {
   uint4 sq[kWave][3];
   float g[kWave];
   float4 o[kWave];
   float term[kWave];
 };
-__device__ __forceinline__ void fs_wtab_item(const FsDev& d, int c, int64_t u, int lane,
+__device__ __forceinline__ void fs_wtab_item(const FsDev& d, int c, int64_t u, int half, int lane,
                                              FsTabLds& L_) {
   const int64_t n = *d.n_dev;
   const int64_t K = fs_chunks(n);
@@ -484,7 +490,7 @@ __device__ __forceinline__ void fs_wtab_item(const FsDev& d, int c, int64_t u, i
   __builtin_amdgcn_wave_barrier();
   const uint32_t qb = L_.sq[0][2].y;  // the window's Q (every record holds it)
   const double Q = (double)__uint_as_float(qb), iQ = 1.0 / Q;  // (exact: powers of two)
-  int64_t L = lane - kFtLo;
+  int64_t L = half * kWave + lane - kFtLo;
   bool ok = true;
   float out = 0.0f;
   for (int k = 0; k < nch; ++k) {
@@ -543,17 +549,16 @@ __device__ __forceinline__ void fs_wtab_item(const FsDev& d, int c, int64_t u, i
       if (!cov && !run) ok = false;
     }
   }
-  const uint64_t m = ballot(ok);
-  uint4* meta = d.b.wmeta + (int64_t)c * d.b.wcap + u;
-  d.b.wtab[((int64_t)c * d.b.wcap + u) * kWave + lane] = out;
-  if (lane == 0) {
-    meta->x = (uint32_t)m;
-    meta->y = (uint32_t)(m >> 32);
-    meta->z = qb;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __builtin_amdgcn_wave_barrier();
-  if (lane == 0) __hip_atomic_store(&meta->w, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // every entry and the quantum carry this launch's stamp: each is one 8-byte store, read whole,
+  // so a reader needs no ordering -- an entry is valid iff its stamp is this launch's
+  const uint64_t ev = (uint64_t)__float_as_uint(out) | ((uint64_t)(ok ? d.gen : 0u) << 32);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(d.b.wtab + ((int64_t)c * d.b.wcap + u) * kFtW +
+                                                  half * kWave + lane),
+                     ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0 && half == 0)
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(d.b.wq + (int64_t)c * d.b.wcap + u),
+                       (uint64_t)qb | ((uint64_t)d.gen << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- k_fs_l1 ----------------------------------------------------------------------------------
@@ -833,6 +838,10 @@ __device__ __forceinline__ void fs_ring_load(const FsNode* R, int64_t base, int6
 
 struct FsWalkCounters {
   int64_t win = 0, pass = 0, slow = 0, step = 0, rerun = 0, clk_step = 0, group_fast = 0, table = 0;
+  // windows walked although tabled: no table published yet, lead not exact / out of the
+  // table's range, the lead's lane dropped by the builder
+  int64_t miss_none = 0, miss_range = 0, miss_mask = 0;
+  int64_t lead_hist = 0;  // (diagnostic) 8-bit counts of |lead| < 128, < 512, < 4096, larger, inexact
 };
 
 __device__ __forceinline__ float g0f(const float4& sm, int f) {  // the first guess of window f
@@ -1057,7 +1066,7 @@ __device__ __forceinline__ float fs_walk_window(const FsDev& d, int c, int64_t b
 template <bool kRepair, bool kRecord>
 __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, float* tp,
                              int lane, __attribute__((address_space(3))) char* ring,
-                             FsWalkCounters& ct) {
+                             __attribute__((address_space(3))) uint64_t* tl, FsWalkCounters& ct) {
   const int64_t n = *d.n_dev;
   const int64_t K = fs_chunks(n);
   const int64_t NW = (K + kWave - 1) / kWave;
@@ -1072,6 +1081,7 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
   auto tslot = [&](int j) { return (uint32_t)(uintptr_t)slot(j) + (uint32_t)kFsWinBytes; };
   int64_t pre_w = -1;  // the window prefetched into slot pre_s (or none)
   int pre_s = 0;
+  int64_t tg0 = -(int64_t)kFtGroup - 1;  // the first window of the tables in tl
   bool met = false;
   for (int64_t wb = w_lo; wb < w_hi && !met; wb += kWave) {
     // the batch's summaries, lane = window; a window is skippable only if its last record also
@@ -1086,23 +1096,8 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
     const bool valid = lane < nb && sm.w == sm.w &&
                        (!has_next || __float_as_uint(sm.y) == __float_as_uint(gnx));
     const uint64_t stat = ballot(lane < nb && !valid);  // (walked at any lag: prefetch candidates)
-    // the batch's transfer tables published so far (lane = window): one relaxed poll of the
-    // stamps and one acquire fence per batch, then the tables' masks and quanta; a window whose
-    // table was not ready at the batch's start is polled again when the walk reaches it
     // (fs_wtab_item builds tables only for windows without a fast summary)
     const uint64_t tabled = ballot(lane < nb && !(sm.z >= 0.0f && sm.w == sm.w));
-    uint4 tm = make_uint4(0u, 0u, 0u, 0u);
-    const uint4* metas = d.b.wmeta + c * d.b.wcap + wb;
-    if ((tabled >> lane) & 1)
-      tm.w = __hip_atomic_load(&metas[lane].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t rdy = ballot(((tabled >> lane) & 1) && tm.w == d.gen);
-    if (rdy) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if ((rdy >> lane) & 1) {
-        const uint4 mv = metas[lane];
-        tm.x = mv.x; tm.y = mv.y; tm.z = mv.z;
-      }
-    }
     const double iqx = valid ? 1.0 / (double)sm.w : 0.0;  // (exact: a power of two)
     int i = 0;
     while (i < nb) {
@@ -1138,33 +1133,66 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
       }
       if (kRecord && lane == 0) V[wb + f] = t;
       const int64_t w = wb + f;
-      {  // the window's transfer table, if its builder has published it (fs_wtab_item): the
-         // exit value when the entry lead is in it
-        uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)tm.x, f);
-        uint32_t my = (uint32_t)__builtin_amdgcn_readlane((int)tm.y, f);
-        uint32_t mq = (uint32_t)__builtin_amdgcn_readlane((int)tm.z, f);
-        if (((tabled & ~rdy) >> f) & 1) {  // (not ready at the batch's start: poll again)
-          const uint4* meta = metas + f;
-          if (__hip_atomic_load(&meta->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d.gen) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            const uint4 mv = *meta;
-            mx = mv.x; my = mv.y; mq = mv.z;
-          }
+      if ((tabled >> f) & 1) {  // the window's transfer table (fs_wtab_item): the exit value
+                                // when the entry lead is in it
+        if (w < tg0 || w >= tg0 + kFtGroup) {  // the next kFtGroup windows' tables into LDS
+          tg0 = w;
+          uint64_t e[kFtGroup * kFtHalves];
+#pragma unroll
+          for (int j = 0; j < kFtGroup * kFtHalves; ++j)
+            e[j] = w + j / kFtHalves < NW
+                       ? __hip_atomic_load(reinterpret_cast<const uint64_t*>(
+                                               d.b.wtab + (c * d.b.wcap + w) * kFtW + j * kWave + lane),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : 0ull;
+          const uint64_t qv = lane < kFtGroup && w + lane < NW
+                                  ? __hip_atomic_load(reinterpret_cast<const uint64_t*>(
+                                        d.b.wq + c * d.b.wcap + w + lane),
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0ull;
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int j = 0; j < kFtGroup * kFtHalves; ++j) tl[j * kWave + lane] = e[j];
+          if (lane < kFtGroup) tl[kFtGroup * kFtW + lane] = qv;
+          __builtin_amdgcn_wave_barrier();
         }
-        const uint64_t tmask = (uint64_t)mx | ((uint64_t)my << 32);
-        if (tmask) {
-          const double Q = (double)__uint_as_float(mq);
+        const int gj = (int)(w - tg0);
+        uint64_t qv = tl[kFtGroup * kFtW + gj];
+        if ((uint32_t)(qv >> 32) != d.gen)  // (not built when prefetched: read it again)
+          qv = __hip_atomic_load(reinterpret_cast<const uint64_t*>(d.b.wq + c * d.b.wcap + w),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(qv >> 32) != d.gen) {
+          ++ct.miss_none;
+        } else {
+          const double Q = (double)__uint_as_float((uint32_t)qv);
           // the lead t - g_0 with its rounding error (TwoSum: it must be exact), in units of Q
           const double ta = (double)t, gb = -(double)g0f(sm, f);
           const double sd = ta + gb, bv = sd - ta;
           const double er = (ta - (sd - bv)) + (gb - bv);
           const double Ld = sd * (1.0 / Q) + (double)kFtLo;
-          if (er == 0.0 && Ld == floor(Ld) && Ld >= 0.0 && Ld < (double)kWave &&
-              ((tmask >> (int)Ld) & 1)) {
-            t = d.b.wtab[(c * d.b.wcap + w) * kWave + (int)Ld];
-            ++ct.table;
-            i = f + 1;
-            continue;
+          const bool inr = er == 0.0 && Ld == floor(Ld) && Ld >= 0.0 && Ld < (double)kFtW;
+          if (inr) {
+            const int li = (int)Ld;
+            uint64_t ev = tl[gj * kFtW + li];
+            if ((uint32_t)(ev >> 32) != d.gen)
+              ev = __hip_atomic_load(reinterpret_cast<const uint64_t*>(
+                                         d.b.wtab + (c * d.b.wcap + w) * kFtW + li),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(ev >> 32) == d.gen) {
+              t = __uint_as_float((uint32_t)ev);
+              ++ct.table;
+              i = f + 1;
+              continue;
+            }
+            ++ct.miss_mask;
+          } else {
+            ++ct.miss_range;
+            if (d.b.wst) {
+              const double aL = fabs(Ld - (double)kFtLo);
+              const int bkt = (er != 0.0 || Ld != floor(Ld)) ? 4 : aL < 128 ? 0 : aL < 512 ? 1
+                              : aL < 4096 ? 2 : 3;
+              if (((ct.lead_hist >> (8 * bkt)) & 0xFF) < 0xFF) ct.lead_hist += 1ll << (8 * bkt);
+            }
           }
         }
       }
@@ -1229,7 +1257,9 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
                                                    float4* __restrict__ cout,
                                                    int32_t* __restrict__ res) {
   __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
+  __shared__ uint64_t tl_raw[kFtLdsWords];
   auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
+  auto* tl = (__attribute__((address_space(3))) uint64_t*)tl_raw;
   const int c = blockIdx.x, lane = threadIdx.x;
   const int64_t n = *d.n_dev;
   const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
@@ -1238,8 +1268,9 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
     // windows' tables first
     FsTabLds& L_ = *reinterpret_cast<FsTabLds*>(ring_raw);
     static_assert(sizeof(FsTabLds) <= 2 * kFsSlotBytes, "builder state fits the ring's LDS");
-    for (int64_t it = c - kFsChains; it < NW * kFsChains; it += gridDim.x - kFsChains)
-      fs_wtab_item(d, (int)(it % kFsChains), it / kFsChains, lane, L_);
+    for (int64_t it = c - kFsChains; it < NW * kFsChains * kFtHalves; it += gridDim.x - kFsChains)
+      fs_wtab_item(d, (int)(it % kFsChains), it / (kFsChains * kFtHalves),
+                   (int)((it / kFsChains) % kFtHalves), lane, L_);
     return;
   }
   // walk counters (dlg_float_sums' walk_stats): windows walked record by record, speculation
@@ -1250,13 +1281,14 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   float t = start9 ? start9[c] : 0.0f;
   if (from_guess) {
     if (NW > 0) t = fs_rec(d.b, c, 0)->g;
-    fs_walk_span<false, true>(d, c, 0, NW, &t, lane, ring, ct);
+    fs_walk_span<false, true>(d, c, 0, NW, &t, lane, ring, tl, ct);
   } else {
-    fs_walk_span<false, false>(d, c, 0, NW, &t, lane, ring, ct);
+    fs_walk_span<false, false>(d, c, 0, NW, &t, lane, ring, tl, ct);
   }
   if (d.b.wst && lane == 0) {
     int64_t* w = d.b.wst + 8 * c;
-    w[0] = ct.win; w[1] = ct.pass; w[2] = ct.slow; w[3] = ct.step; w[4] = ct.rerun;
+    w[0] = ct.win; w[1] = ct.pass | (ct.miss_none << 32); w[2] = ct.slow | (ct.miss_range << 32);
+    w[3] = ct.step | (ct.lead_hist << 24); w[4] = ct.rerun | (ct.miss_mask << 32);
     w[5] = (int64_t)clock64() - clk0; w[6] = ct.clk_step; w[7] = ct.group_fast + (ct.table << 32);
   }
   __shared__ unsigned s_ticket;
@@ -1293,7 +1325,9 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
 // exact is not walked at all; one with a constant lag passes its windows by their summaries.
 __global__ __launch_bounds__(kFwBS) void k_fs_repair(FsDev d, const float* __restrict__ start9) {
   __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
+  __shared__ uint64_t tl_raw[kFtLdsWords];
   auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
+  auto* tl = (__attribute__((address_space(3))) uint64_t*)tl_raw;
   const int c = blockIdx.x, lane = threadIdx.x;
   const int64_t n = *d.n_dev;
   const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
@@ -1304,7 +1338,7 @@ __global__ __launch_bounds__(kFwBS) void k_fs_repair(FsDev d, const float* __res
     return;
   }
   if (__float_as_uint(t) == __float_as_uint(fs_rec(d.b, c, 0)->g)) return;  // (sums: exact)
-  const bool met = fs_walk_span<true, false>(d, c, 0, NW, &t, lane, ring, ct);
+  const bool met = fs_walk_span<true, false>(d, c, 0, NW, &t, lane, ring, tl, ct);
   if (!met && lane == 0) d.b.sums[c] = t;  // (met: the recorded walk's end is exact)
 }
 
@@ -1320,8 +1354,8 @@ size_t fs_scratch_bytes(int64_t n_cap, int world) {
          align256(sizeof(float4) * U * kFsChains) +
          align256(sizeof(float) * 32) +
          align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) +
-         align256(sizeof(float) * U * kFsChains) + align256(sizeof(float) * U * kFsChains * kWave) +
-         align256(sizeof(uint4) * U * kFsChains) + 256;
+         align256(sizeof(float) * U * kFsChains) + align256(sizeof(uint2) * U * kFsChains * kFtW) +
+         align256(sizeof(uint2) * U * kFsChains) + 256;
 }
 
 FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
@@ -1354,10 +1388,10 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   p += align256(sizeof(double) * (kFsChains + 1) * world);
   b.vw = reinterpret_cast<float*>(p);
   p += align256(sizeof(float) * U * kFsChains);
-  b.wtab = reinterpret_cast<float*>(p);
-  p += align256(sizeof(float) * U * kFsChains * kWave);
-  b.wmeta = reinterpret_cast<uint4*>(p);
-  p += align256(sizeof(uint4) * U * kFsChains);
+  b.wtab = reinterpret_cast<uint2*>(p);
+  p += align256(sizeof(uint2) * U * kFsChains * kFtW);
+  b.wq = reinterpret_cast<uint2*>(p);
+  p += align256(sizeof(uint2) * U * kFsChains);
   b.ticket = reinterpret_cast<unsigned*>(p);  // [0]: k_fs_prep / k_fs_inc, [1]: k_fs_walk
   return b;
 }
@@ -1367,10 +1401,13 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
                      hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
   static std::atomic<uint32_t> s_gen{0};
-  FsDev d{px, py, pz, stride, n_dev, b, ++s_gen};
+  uint32_t gen = ++s_gen;
+  if (gen == 0) gen = ++s_gen;  // (0 marks a dropped table entry)
+  FsDev d{px, py, pz, stride, n_dev, b, gen};
   const unsigned gw = (unsigned)(kFsChains +
-      std::max<int64_t>(1, std::min<int64_t>(((n_cap > 0 ? n_cap : 1) + kFsUnit - 1) / kFsUnit * kFsChains,
-                                             4 * (int64_t)num_cus)));
+      std::max<int64_t>(1, std::min<int64_t>(((n_cap > 0 ? n_cap : 1) + kFsUnit - 1) / kFsUnit *
+                                                 kFsChains * kFtHalves,
+                                             6 * (int64_t)num_cus)));
   const int64_t nc = n_cap > 0 ? n_cap : 1;
   const int64_t U = (fs_chunks(nc) + kFsUC - 1) / kFsUC;
   const int gp = (int)std::min<int64_t>(U, 2 * (int64_t)num_cus);

@@ -1154,9 +1154,7 @@ __global__ __launch_bounds__(kMoBS) void k_ustamp(PointsView src, const float4* 
   }
 }
 
-// k_ucompact: bitmap -> the inliers' x, y, z in ascending pristine order (= list order), read
-// from the pristine cloud's (x, y, z, 0) records (one 16-byte line share per inlier: with the
-// inliers scattered over a shuffled cloud, the SoA arrays cost three lines each), a
+// k_ucompact: bitmap -> the inliers' x, y, z in ascending pristine order (= list order), a
 // single pass with decoupled look-back (sel1_scan); each lane owns 2 consecutive words (64
 // points), clears them and ranks its inliers.  The gather is cooperative: the wave walks its 64
 // lanes' words in order, lane i taking point i of each (coalesced, masked 4-byte loads and
@@ -1169,8 +1167,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
 }
 __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits, int64_t nwords,
-                                                    const float4* __restrict__ paos, Sel1State L,
-                                                    int ntiles,
+                                                    PointsView pristine, Sel1State L, int ntiles,
                                                     float* __restrict__ ox, float* __restrict__ oy,
                                                     float* __restrict__ oz,
                                                     int32_t* __restrict__ n_out) {
@@ -1222,8 +1219,7 @@ __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits,
       on[k] = ((mk[k] >> lane) & 1u) != 0;
       if (on[k]) {
         const int64_t pi = wbase + (int64_t)(s0 + k) * 64 + lane;
-        const float4 v = paos[pi];  // (one 16-byte record: a third of the SoA's lines)
-        x[k] = v.x; y[k] = v.y; z[k] = v.z;
+        x[k] = pristine.x[pi]; y[k] = pristine.y[pi]; z[k] = pristine.z[pi];
       }
     }
 #pragma unroll
@@ -1507,7 +1503,7 @@ void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, flo
 
 int ucompact_tiles(int64_t nwords) { return (int)((nwords + kUcBS * kUcWords - 1) / (kUcBS * kUcWords)); }
 
-void launch_ucompact(uint32_t* bits, int64_t nwords, const float4* paos, Sel1State& L, float* ox,
+void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1State& L, float* ox,
                      float* oy, float* oz, int32_t* n_out, hipStream_t s) {
   const int nt = ucompact_tiles(nwords);
   if (nt == 0) {
@@ -1515,8 +1511,8 @@ void launch_ucompact(uint32_t* bits, int64_t nwords, const float4* paos, Sel1Sta
     return;
   }
   sel1_next(L, nt);
-  hipLaunchKernelGGL(k_ucompact, dim3(nt), dim3(kUcBS), 0, s, bits, nwords, paos, L, nt, ox, oy,
-                     oz, n_out);
+  hipLaunchKernelGGL(k_ucompact, dim3(nt), dim3(kUcBS), 0, s, bits, nwords, pristine, L, nt, ox,
+                     oy, oz, n_out);
 }
 
 void launch_build_hyps(const SampleRec* samples, int D, float cthr, float ax, float ay, float az,

@@ -193,7 +193,7 @@ void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers
 void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, float margin,
                    const float4* coef, const ModelTest& mt, uint32_t* bits, hipStream_t s);
 int ucompact_tiles(int64_t nwords);
-void launch_ucompact(uint32_t* bits, int64_t nwords, const float4* paos, Sel1State& L, float* ox,
+void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1State& L, float* ox,
                      float* oy, float* oz, int32_t* n_out, hipStream_t s);
 
 // PCL's float refit on the device (fsum.hip): the nine sequential float sums of
@@ -222,9 +222,10 @@ struct FsBuffers {
   int64_t* wst = nullptr;      // [9][8] walk counters (dlg_float_sums), or null
   float* vw = nullptr;         // [9][wcap] several ranks: each window's entry value along the
                                // walk from the rank's guess (k_fs_repair compares against it)
-  float* wtab = nullptr;       // [9][wcap][64] window transfer tables (k_fs_wtab): exit value for
-                               // entry leads -32..31 (in the window's smallest quantum)
-  uint4* wmeta = nullptr;      // [9][wcap] (valid-entry mask lo, hi, Q bits, 0)
+  uint2* wtab = nullptr;       // [9][wcap][128] window transfer tables (fs_wtab_item): (exit value
+                               // bits, launch stamp) for entry leads -64..63 in the window's
+                               // smallest quantum; stamp 0 or stale: no entry
+  uint2* wq = nullptr;         // [9][wcap] (the table's quantum bits, launch stamp)
 };
 // bytes of scratch for n_cap inliers; carve() lays the buffers out in `base`
 // (world: the ranks of the communicator passed to launch_fs_refit; comm null or one rank: the

@@ -604,7 +604,8 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
 
 // ---------------------------------------------------------------------------------------------
 // k_score_tiles_ex (default tile scorer, SACMODEL_PLANE): the near (tile, plane) pairs evaluated
-// exactly in PCL's op order with lanes as planes (two points per packed f32 operation).  Same items, claims, plane lists and tile-sphere
+// exactly in PCL's op order with lanes as planes.  (Two points per packed f32 operation,
+// v_pk_mul_f32 / v_pk_add_f32, measured slower: 0.4485 vs 0.4332 ms per first launch.)  Same items, claims, plane lists and tile-sphere
 // tests as k_score_tiles_rl, but a near pair is queued as (plane | tile slot << 12) and every 64
 // queued pairs form one pass: lane l takes pair l, reads its plane from LDS and walks the 32
 // points of its tile, which every lane reads from the wave's LDS tile slots with uniform (or at
@@ -622,7 +623,7 @@ constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad 
                                // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
 constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
 
-template <int BS, int K, bool PK = true>  // PK: packed f32 pairs (false: A/B-only scalar form)
+template <int BS, int K>
 __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
     const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
@@ -710,21 +711,10 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const float4 c = cf[k];
-        if constexpr (!PK) {
-          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.x, ys.x, zs.x)) < cthr ? 1u : 0u;
-          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.y, ys.y, zs.y)) < cthr ? 1u : 0u;
-          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.z, ys.z, zs.z)) < cthr ? 1u : 0u;
-          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.w, ys.w, zs.w)) < cthr ? 1u : 0u;
-          continue;
-        }
-        const f32x2 d01 = pcl_dot2(c.x, c.y, c.z, c.w, f32x2{xs.x, xs.y}, f32x2{ys.x, ys.y},
-                                   f32x2{zs.x, zs.y});
-        const f32x2 d23 = pcl_dot2(c.x, c.y, c.z, c.w, f32x2{xs.z, xs.w}, f32x2{ys.z, ys.w},
-                                   f32x2{zs.z, zs.w});
-        acc[k] += fabsf(d01.x) < cthr ? 1u : 0u;
-        acc[k] += fabsf(d01.y) < cthr ? 1u : 0u;
-        acc[k] += fabsf(d23.x) < cthr ? 1u : 0u;
-        acc[k] += fabsf(d23.y) < cthr ? 1u : 0u;
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.x, ys.x, zs.x)) < cthr ? 1u : 0u;
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.y, ys.y, zs.y)) < cthr ? 1u : 0u;
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.z, ys.z, zs.z)) < cthr ? 1u : 0u;
+        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.w, ys.w, zs.w)) < cthr ? 1u : 0u;
       }
     }
 #pragma unroll
@@ -996,8 +986,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   }
   if (!np && tile_scorer != kTileScorerBf16) {
     auto* kex = tile_scorer == 11 ? k_score_tiles_ex<kBS, 1>
-              : tile_scorer == 14 ? k_score_tiles_ex<kBS, 4>
-              : tile_scorer == 15 ? k_score_tiles_ex<kBS, 2, false> : k_score_tiles_ex<kBS, 2>;
+              : tile_scorer == 14 ? k_score_tiles_ex<kBS, 4> : k_score_tiles_ex<kBS, 2>;
     hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
                           0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, blk_cap, xcd, hyps, D,
                           cthr, margin, counts, stats, pick ? *pick : PickArgs{});

@@ -17,8 +17,13 @@ for k in range(int(sys.argv[1]) if len(sys.argv) > 1 else 8):
     sums, co, unc, ms, ws = ctx.float_sums(xyz, cin=planes[k], reps=3, walk_stats=True)
     out.append({"plane": k, "n": int(xyz.shape[0]), "ms": round(ms, 4),
                 "chains": ws.tolist()})
-    print(k, xyz.shape[0], round(ms, 4), "win/pass/slow/step/rerun/clk/clk_step/K per chain:",
-          flush=True)
+    print(k, xyz.shape[0], round(ms, 4), "walked/pass/slow/step/rerun/clk/clk_step/summary/"
+          "table/miss_none/miss_range/miss_mask per chain:", flush=True)
     for c in range(9):
-        print("   ", ws[c].tolist(), flush=True)
+        w = [int(v) for v in ws[c].tolist()]
+        lo = [v & 0xFFFFFFFF for v in w]
+        lh = [(w[3] >> (24 + 8 * b)) & 0xFF for b in range(5)]
+        print("   ", [lo[0], lo[1], lo[2], w[3] & 0xFFFFFF, lo[4], w[5], w[6], lo[7], w[7] >> 32,
+                      w[1] >> 32, w[2] >> 32, w[4] >> 32], "|lead| <128/<512/<4096/more/inexact:",
+              lh, flush=True)
 json.dump(out, open(sys.argv[2] if len(sys.argv) > 2 else "/dev/null", "w"))

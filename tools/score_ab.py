@@ -19,9 +19,8 @@ from dialog_amd import _lib  # noqa: E402
 from dialog_amd.synth import SEED_BASE, plane_cloud  # noqa: E402
 
 NAMES = {0: "exact_p4", 1: "bf16_t8", 2: "pruned_ex", 3: "pruned_bf16", 5: "pruned_ex_k1",
-         6: "pruned_ex_k4", 7: "pruned_ex_scalar"}
-# DLG_OPT_PRUNE_TILE_SCORER per variant (A/B-only values 11..15; 15: K = 2 without packed f32)
-TILE_OPT = {3: 1, 5: 11, 6: 14, 7: 15}
+         6: "pruned_ex_k4"}
+TILE_OPT = {3: 1, 5: 11, 6: 14}  # DLG_OPT_PRUNE_TILE_SCORER per variant (A/B-only values 11..14)
 
 
 def main():
