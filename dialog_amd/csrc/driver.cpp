@@ -1708,7 +1708,7 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         if (value < 0 || value > 3) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PCL_REFIT_DEVICE: 0..3");
         o.pcl_dev = (int)value;
         break;
-      case DLG_OPT_NORMALS_FUSED: o.nbr_fused = value != 0; o.nbr_xp = value >= 10 ? (int)value - 10 : 0; break;
+      case DLG_OPT_NORMALS_FUSED: o.nbr_fused = value != 0; break;
       case DLG_OPT_PRUNE_TILE_SCORER:
         if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && !(value >= 11 && value <= 14))
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");

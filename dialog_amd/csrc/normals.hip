@@ -608,20 +608,20 @@ constexpr int kFqB = 4;  // candidate steps whose loads are in flight together
         const int2 *__restrict__ trange, uint32_t tmask, float r2, float vpx, float vpy,         \
         float vpz, float4 *__restrict__ normals, int32_t *__restrict__ ovf,                      \
         uint32_t *__restrict__ ovf_count
-template <int EMAX, int XP>
+template <int EMAX>
 __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS);
 
 // the first pass (<= 512 neighbours) held to 128 VGPRs: four waves per SIMD, as many as its LDS
 // allows; the wider pass (<= 1024) is LDS-limited to fewer waves anyway
-template <int EMAX, int XP = 0>  // XP: timing experiment (bit 0 no sort, 1 no sum, 2 no scan)
+template <int EMAX>
 __global__ __launch_bounds__(kBS) __attribute__((amdgpu_waves_per_eu(4))) void k_nbr_fused(
     DLG_NBR_FUSED_ARGS) {
-  nbr_fused_body<EMAX, XP>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx,
+  nbr_fused_body<EMAX>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx,
                            vpy, vpz, normals, ovf, ovf_count);
 }
 template <int EMAX>
 __global__ __launch_bounds__(kBS) void k_nbr_fused_wide(DLG_NBR_FUSED_ARGS) {
-  nbr_fused_body<EMAX, 0>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx,
+  nbr_fused_body<EMAX>(sx, sy, sz, sidx, n, qlist, qcount, G, tkeys, trange, tmask, r2, vpx,
                           vpy, vpz, normals, ovf, ovf_count);
 }
 
@@ -636,7 +636,7 @@ __device__ __forceinline__ void lds_set_key(uint32_t* buf, int e, uint64_t k) {
 
 // the wave's cnt (<= 64 E) keys in buf -> FLANN's (d2, original index) order, then the
 // neighbours' (x, y, z) staged over the keys in that order (word 3 e + axis)
-template <int E, bool kSort>
+template <int E>
 __device__ __forceinline__ void nbr_order_stage(uint32_t* buf, int cnt,
                                                 const float* __restrict__ sx,
                                                 const float* __restrict__ sy,
@@ -649,7 +649,7 @@ __device__ __forceinline__ void nbr_order_stage(uint32_t* buf, int cnt,
     const int e = lane + 64 * j;
     v[j] = e < cnt ? lds_key(buf, e) : ~0ull;
   }
-  if (kSort) wave_bitonic<E>(v);
+  wave_bitonic<E>(v);
   // (d2, sorted position) -> FLANN's (d2, original index): only equal-d2 runs can differ
   bool tie = false;
 #pragma unroll
@@ -707,7 +707,7 @@ __device__ __forceinline__ void nbr_order_stage(uint32_t* buf, int cnt,
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int EMAX, int XP>
+template <int EMAX>
 __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
   constexpr int kCap = 64 * EMAX;
   constexpr int kW = kBS / 64;
@@ -811,7 +811,7 @@ __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
       // offsets are wave-uniform (scalars), recomputed when the query's cell changes.  64
       // positions per step, kFqB steps with their loads in flight together.
       int cnt = 0;
-      for (int k0 = 0; k0 < ((XP & 4) ? 0 : tot); k0 += 64 * kFqB) {
+      for (int k0 = 0; k0 < tot; k0 += 64 * kFqB) {
         float d2[kFqB];
         int uu[kFqB];
 #pragma unroll
@@ -840,19 +840,18 @@ __device__ __forceinline__ void nbr_fused_body(DLG_NBR_FUSED_ARGS) {
         continue;
       }
       __builtin_amdgcn_wave_barrier();
-      constexpr bool kS = !(XP & 1);
-      if (cnt <= 64) nbr_order_stage<1, kS>(buf, cnt, sx, sy, sz, sidx);
-      else if (cnt <= 128) nbr_order_stage<2, kS>(buf, cnt, sx, sy, sz, sidx);
-      else if (cnt <= 256 || EMAX < 8) nbr_order_stage<(EMAX < 4 ? EMAX : 4), kS>(buf, cnt, sx, sy, sz, sidx);
-      else if (cnt <= 512 || EMAX < 16) nbr_order_stage<(EMAX < 8 ? EMAX : 8), kS>(buf, cnt, sx, sy, sz, sidx);
-      else nbr_order_stage<EMAX, kS>(buf, cnt, sx, sy, sz, sidx);
+      if (cnt <= 64) nbr_order_stage<1>(buf, cnt, sx, sy, sz, sidx);
+      else if (cnt <= 128) nbr_order_stage<2>(buf, cnt, sx, sy, sz, sidx);
+      else if (cnt <= 256 || EMAX < 8) nbr_order_stage<(EMAX < 4 ? EMAX : 4)>(buf, cnt, sx, sy, sz, sidx);
+      else if (cnt <= 512 || EMAX < 16) nbr_order_stage<(EMAX < 8 ? EMAX : 8)>(buf, cnt, sx, sy, sz, sidx);
+      else nbr_order_stage<EMAX>(buf, cnt, sx, sy, sz, sidx);
       // the nine chains, one per lane, in list order (PCL: accu[k] += term, float)
       float acc = 0.0f;
       if (lane < 9) {
         const uint32_t* ra = buf + sa;
         const uint32_t* rb = buf + ob;
 #pragma unroll 8
-        for (int e = 0; e < ((XP & 2) ? 0 : cnt); ++e) {
+        for (int e = 0; e < cnt; ++e) {
           const float pa = __uint_as_float(ra[3 * e]);
           const float pb = one_b ? 1.0f : __uint_as_float(rb[3 * e]);
           acc = acc + pa * pb;
@@ -1632,11 +1631,6 @@ void launch_nbr_fused(const GridDesc& G, const GridBufs& B, int n, const int32_t
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(waves, kBS / 64),
                                                                       (int64_t)num_cus * 64));
   auto* k = wide ? k_nbr_fused_wide<16> : k_nbr_fused<8>;
-  if (wide >= 10) {  // (timing experiments: results wrong)
-    const int xp = wide - 10;
-    k = xp == 1 ? k_nbr_fused<8, 1> : xp == 2 ? k_nbr_fused<8, 2> : xp == 3 ? k_nbr_fused<8, 3>
-      : xp == 4 ? k_nbr_fused<8, 4> : k_nbr_fused<8, 7>;
-  }
   hipLaunchKernelGGL(k, dim3(g), dim3(kBS), 0, s, B.sx, B.sy, B.sz, B.idx_out, n, qlist, qcount, G,
                      B.tkeys, B.trange, B.tmask, r2, vp[0], vp[1], vp[2], normals, ovf, ovf_count);
 }

@@ -273,7 +273,7 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
       w.ovfc.ensure(2);
       w.h_cnt.ensure(2);
       HIPCHK(hipMemsetAsync(w.ovfc.p, 0, 2 * sizeof(uint32_t), c->stream));
-      launch_nbr_fused(G, B, n, nullptr, nullptr, c->opt.nbr_xp ? 10 + c->opt.nbr_xp : 0, r2, vp,
+      launch_nbr_fused(G, B, n, nullptr, nullptr, 0, r2, vp,
                        w.nrm.p, w.ovfa.p, w.ovfc.p, c->num_cus, c->stream);
       launch_nbr_fused(G, B, n, w.ovfa.p, w.ovfc.p, 1, r2, vp, w.nrm.p, w.ovfb.p, w.ovfc.p + 1,
                        c->num_cus, c->stream);
