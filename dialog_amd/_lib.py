@@ -44,6 +44,7 @@ DLG_OPT_SELECT_TILE = 7
 DLG_OPT_PCL_REFIT_DEVICE = 8
 DLG_OPT_PRUNE_TILE_SCORER = 9
 DLG_OPT_NORMALS_FUSED = 10
+DLG_OPT_REGULATE_WAVE = 11
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
 DLG_SCORE_EXACT = 0

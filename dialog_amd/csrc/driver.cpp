@@ -1709,6 +1709,7 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         o.pcl_dev = (int)value;
         break;
       case DLG_OPT_NORMALS_FUSED: o.nbr_fused = value != 0; break;
+      case DLG_OPT_REGULATE_WAVE: o.bfs_wave = value != 0; break;
       case DLG_OPT_PRUNE_TILE_SCORER:
         if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && !(value >= 11 && value <= 14))
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
@@ -1732,6 +1733,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_SELECT_TILE: *value = o.sel1_tile; break;
     case DLG_OPT_PCL_REFIT_DEVICE: *value = o.pcl_dev; break;
     case DLG_OPT_NORMALS_FUSED: *value = o.nbr_fused; break;
+    case DLG_OPT_REGULATE_WAVE: *value = o.bfs_wave; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer == kTileScorerExact ? DLG_TILE_EXACT : DLG_TILE_BF16; break;
     default: return DLG_ERR_INVALID;
   }

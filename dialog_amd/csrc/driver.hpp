@@ -168,6 +168,7 @@ struct PathOptions {
   int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
   int tile_scorer = 0;            // pruned plane scorer: kTileScorerExact or kTileScorerBf16
   bool nbr_fused = true;          // PCL-float radius normals in one fused pass (else chunked)
+  bool bfs_wave = true;           // RegulateNormal's claim pass: one wave per frontier node
   // PCL float refit (DLG_REFIT_PCL, any rank count): 1 = the nine sums on the device (fsum.hip,
   // exact), 0 = gathered to the host and summed there, 2 = device, and the host recomputes the
   // refit's tail from the published sums every round, 3 = as 2 and the round's select is always

@@ -582,6 +582,59 @@ __global__ __launch_bounds__(kBS) void k_nbr_normals(
   normals[sidx[t]] = finish_normal_pcl(a, k, sx[t], sy[t], sz[t], vpx, vpy, vpz);
 }
 
+// The 27 cells around cell (cx, cy, cz) as 9 rows of contiguous sorted positions (a row's three
+// x cells have consecutive keys), packed into one candidate list: rows[r] = row r's start in the
+// list, rows[9 + r] = its offset to sorted positions, rows[18] = the list's length.  The whole
+// wave calls it; rows is the wave's LDS table.
+__device__ __forceinline__ void nbr_rows(const GridDesc& G, const uint32_t* __restrict__ tkeys,
+                                         const int2* __restrict__ trange, uint32_t tmask, int cx,
+                                         int cy, int cz, int32_t* rows) {
+  const int lane = threadIdx.x & 63;
+  // lanes 0..26 look up one cell each; a row's range is its cells' union (contiguous)
+  int2 c = make_int2(INT_MAX, INT_MIN);
+  if (lane < 27) {
+    const int x = cx + lane % 3 - 1, y = cy + (lane / 3) % 3 - 1, z = cz + lane / 9 - 1;
+    if (x >= 0 && y >= 0 && z >= 0 && x < G.g[0] && y < G.g[1] && z < G.g[2]) {
+      const int2 r = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
+      if (r.y > r.x) c = r;
+    }
+  }
+  int lo = c.x, hi = c.y;
+#pragma unroll
+  for (int o = 1; o <= 2; o <<= 1) {  // (min / max over each aligned triple of lanes)
+    const int l2 = __shfl(lo, (lane / 3) * 3 + ((lane % 3 + o) % 3), 64);
+    const int h2 = __shfl(hi, (lane / 3) * 3 + ((lane % 3 + o) % 3), 64);
+    lo = min(lo, l2);
+    hi = max(hi, h2);
+  }
+  const int rl = __shfl(lo, 3 * (lane < 9 ? lane : 0), 64);
+  const int rh = __shfl(hi, 3 * (lane < 9 ? lane : 0), 64);
+  const int2 rg = lane < 9 && rl < rh ? make_int2(rl, rh) : make_int2(0, 0);
+  const int rlen = rg.y - rg.x;
+  int incl = rlen;  // (lanes 0..8: inclusive prefix of the row lengths)
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const int w = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += w;
+  }
+  const int excl = incl - rlen;
+  __builtin_amdgcn_wave_barrier();
+  if (lane < 9) {
+    rows[lane] = excl;
+    rows[9 + lane] = rg.x - excl;
+  }
+  if (lane == 8) rows[18] = incl;
+  __builtin_amdgcn_wave_barrier();
+}
+
+// the sorted position of packed candidate v (row tables read from nbr_rows' LDS table)
+__device__ __forceinline__ int nbr_pos(const int (&r_start)[9], const int (&r_off)[9], int v) {
+  int u = v + r_off[0];
+#pragma unroll
+  for (int q = 1; q < 9; ++q) u = v >= r_start[q] ? v + r_off[q] : u;
+  return u;
+}
+
 // ---- fused radius normals (PCL float): search, (d2, index) order and the sums in one pass ----
 // One wave per query at a time, queries taken in runs of kFqRun consecutive sorted positions.
 // Per query: the 27 cells around it are 9 runs of sorted positions (a row's three x cells have
@@ -1326,6 +1379,91 @@ __global__ __launch_bounds__(kBS) void k_bfs2_claim(
   for (uint32_t i = threadIdx.x; i < m; i += kBS) cand[s_base + i] = s_buf[i];
 }
 
+// The claim pass with one wave per frontier node (default): the node's 27 cells packed into one
+// candidate list (nbr_rows), scanned 64 candidates per step with four steps' loads in flight;
+// waves take runs of kBqRun consecutive frontier nodes (children of consecutive parents: mostly
+// the same cells, looked up once).  Same claims as k_bfs2_claim (a min: the order the candidates
+// are met in does not matter), appended through the workgroup's LDS stage.
+constexpr int kBqRun = 8;
+__global__ __launch_bounds__(kBS) void k_bfs2_claim_w(
+    const int32_t* __restrict__ queue, const long long* __restrict__ st,
+    const int32_t* __restrict__ pos_of, const float* __restrict__ sx, const float* __restrict__ sy,
+    const float* __restrict__ sz, GridDesc G, const uint32_t* __restrict__ tkeys,
+    const int2* __restrict__ trange, uint32_t tmask, float r2,
+    const uint8_t* __restrict__ processed_s, uint32_t* __restrict__ claim_s,
+    int32_t* __restrict__ cand, long long* __restrict__ st_w, uint32_t* __restrict__ child_cnt,
+    uint32_t* __restrict__ cursor) {
+  constexpr int kStage = 2048;
+  constexpr int kW = kBS / 64;
+  __shared__ uint32_t s_n;
+  __shared__ long long s_base;
+  __shared__ int32_t s_buf[kStage];
+  __shared__ int32_t s_rows[kW][20];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t* rows = s_rows[wv];
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const long long fbase = st[0];
+  const int nf = (int)st[1];
+  const int nruns = (nf + kBqRun - 1) / kBqRun;
+  const int gw = (int)((blockIdx.x * kBS + threadIdx.x) >> 6), nw = (int)((gridDim.x * kBS) >> 6);
+  for (int run = gw; run < nruns; run += nw) {
+    int pcx = -1, pcy = -1, pcz = -1;
+    const int f_end = min(nf, (run + 1) * kBqRun);
+    for (int f = run * kBqRun; f < f_end; ++f) {
+      if (lane == 0) { child_cnt[f] = 0; cursor[f] = 0; }
+      const uint32_t mypos = (uint32_t)(fbase + f);
+      const int cu = pos_of[queue[mypos]];
+      const float qx = sx[cu], qy = sy[cu], qz = sz[cu];
+      if (!finite3(qx, qy, qz)) continue;
+      const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+      const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+      const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+      if (cx != pcx || cy != pcy || cz != pcz) {
+        pcx = cx; pcy = cy; pcz = cz;
+        nbr_rows(G, tkeys, trange, tmask, cx, cy, cz, rows);
+      }
+      int r_start[9], r_off[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        r_start[q] = rows[q];
+        r_off[q] = rows[9 + q];
+      }
+      const int tot = rows[18];
+      for (int k0 = 0; k0 < tot; k0 += 64 * kFqB) {
+        int uu[kFqB];
+        uint8_t pr[kFqB];
+        float px[kFqB], py[kFqB], pz[kFqB];
+#pragma unroll
+        for (int j = 0; j < kFqB; ++j) {
+          const int v = k0 + 64 * j + lane;
+          const int u = nbr_pos(r_start, r_off, min(v, tot - 1));
+          uu[j] = v < tot ? u : -1;
+          pr[j] = processed_s[u]; px[j] = sx[u]; py[j] = sy[u]; pz[j] = sz[u];
+        }
+#pragma unroll
+        for (int j = 0; j < kFqB; ++j) {
+          const int u = uu[j];
+          if (u < 0 || pr[j]) continue;
+          if (!(flann_d2(qx, qy, qz, px[j], py[j], pz[j]) < r2)) continue;
+          if (claim_s[u] <= mypos) continue;  // claims only decrease
+          if (atomicMin(&claim_s[u], mypos) == 0xffffffffu) {
+            const uint32_t p = atomicAdd(&s_n, 1u);
+            if (p < (uint32_t)kStage) s_buf[p] = u;
+            else cand[atomicAdd((unsigned long long*)&st_w[2], 1ull)] = u;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t m = min(s_n, (uint32_t)kStage);
+  if (threadIdx.x == 0 && m)
+    s_base = (long long)atomicAdd((unsigned long long*)&st_w[2], (unsigned long long)m);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += kBS) cand[s_base + i] = s_buf[i];
+}
+
 __global__ __launch_bounds__(kBS) void k_bfs2_settle(
     const int32_t* __restrict__ queue, const int32_t* __restrict__ cand,
     const long long* __restrict__ st, const int32_t* __restrict__ pos_of,
@@ -1741,10 +1879,11 @@ void launch_bfs_seed(int32_t seed, int flip, const int32_t* pos_of, float4* nrm_
 
 void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, const GridDesc& G,
                        const GridBufs& B, float r2, uint8_t* processed_s, uint32_t* claim_s,
-                       float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_bfs2_claim, dim3(grid), dim3(kBS), 0, s, queue, st, pos_of, B.sx, B.sy,
-                     B.sz, G, B.tkeys, B.trange, B.tmask, r2, processed_s, claim_s, cand, st,
-                     W.child_cnt, W.cursor);
+                       float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s,
+                       bool wave_claim) {
+  hipLaunchKernelGGL(wave_claim ? k_bfs2_claim_w : k_bfs2_claim, dim3(grid), dim3(kBS), 0, s,
+                     queue, st, pos_of, B.sx, B.sy, B.sz, G, B.tkeys, B.trange, B.tmask, r2,
+                     processed_s, claim_s, cand, st, W.child_cnt, W.cursor);
   hipLaunchKernelGGL(k_bfs2_settle, dim3(grid), dim3(kBS), 0, s, queue, cand, st, pos_of,
                      processed_s, claim_s, nrm_s, W.child_cnt);
   hipLaunchKernelGGL(k_bfs2_scan_tiles, dim3(grid), dim3(kBS), 0, s, st, W.child_cnt, W.offs,

@@ -160,7 +160,8 @@ struct Bfs2Bufs {
 };
 void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, const GridDesc& G,
                        const GridBufs& B, float r2, uint8_t* processed_s, uint32_t* claim_s,
-                       float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s);
+                       float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s,
+                       bool wave_claim = true);  // (false: one thread per (node, cell))
 void launch_bfs_finish(const GridBufs& B, int n, const float4* nrm_s, const uint8_t* processed_s,
                        float4* nrm, uint8_t* processed, hipStream_t s);
 

@@ -407,7 +407,7 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   for (;;) {
     for (int k = 0; k < 16; ++k)
       launch_bfs2_level(w.queue.p, w.bst.p, w.pos_of.p, G, B, r2, w.processed_s.p, w.claim.p,
-                        w.nrm_s.p, w.cand.p, W, grid, c->stream);
+                        w.nrm_s.p, w.cand.p, W, grid, c->stream, c->opt.bfs_wave);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(w.h_bst.p, w.bst.p, 32, hipMemcpyDeviceToHost, c->stream));
     sync(c);

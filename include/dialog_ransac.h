@@ -408,9 +408,12 @@ enum {
   DLG_OPT_PRUNE_TILE_SCORER = 9, /* the pruned plane scorer's (tile, plane) pairs:
                                DLG_TILE_EXACT (default) PCL-order f32 with lanes as planes, or
                                DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band re-decision */
-  DLG_OPT_NORMALS_FUSED = 10 /* PCL-float radius normals: 1 (default) search, (d2, index) order
+  DLG_OPT_NORMALS_FUSED = 10, /* PCL-float radius normals: 1 (default) search, (d2, index) order
                                and sums in one fused pass; 0: the chunked count / fill / sort /
                                sum pipeline */
+  DLG_OPT_REGULATE_WAVE = 11  /* RegulateNormal's claim pass: 1 (default) one wave per frontier
+                               node over its packed candidate cells; 0: one thread per (node,
+                               cell) */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };

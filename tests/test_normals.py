@@ -287,9 +287,12 @@ def test_gpu_normals_pcl_layout_viewpoint_and_edges(gpu_ctx, cloud):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wave", [1, 0])
 @pytest.mark.parametrize("seed_idx,outward,r", [(0, True, 0.08), (123, False, 0.08),
                                                 (4567, True, 0.15), (11000, False, 0.05)])
-def test_gpu_regulate_bit_exact(gpu_ctx, cloud, seed_idx, outward, r):
+def test_gpu_regulate_bit_exact(gpu_ctx, cloud, seed_idx, outward, r, wave):
+    """Both claim passes (DLG_OPT_REGULATE_WAVE 1: a wave per frontier node, default; 0: a
+    thread per (node, cell)) against the oracle's BFS, bit for bit."""
     import dialog_amd as D
     p, _, _ = cloud
     nrm = O.estimate_normals(p, RADIUS)
@@ -297,7 +300,11 @@ def test_gpu_regulate_bit_exact(gpu_ctx, cloud, seed_idx, outward, r):
     rng = np.random.default_rng(seed_idx)
     nrm[:, :3] *= np.where(rng.random(len(p)) < 0.5, -1.0, 1.0).astype(np.float32)[:, None]
     o_reg, o_proc, o_cnt = O.regulate_normals(p, nrm, seed_idx, outward, r)
-    g_reg, g_proc, g_cnt = D.regulate_normals(p, nrm, seed_idx, outward, r, ctx=gpu_ctx)
+    gpu_ctx.set_option(D.DLG_OPT_REGULATE_WAVE, wave)
+    try:
+        g_reg, g_proc, g_cnt = D.regulate_normals(p, nrm, seed_idx, outward, r, ctx=gpu_ctx)
+    finally:
+        gpu_ctx.set_option(D.DLG_OPT_REGULATE_WAVE, 1)
     assert g_cnt == o_cnt
     assert np.array_equal(g_proc, o_proc)
     np.testing.assert_array_equal(g_reg, o_reg)  # NaN-aware, bit-exact
