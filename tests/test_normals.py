@@ -247,10 +247,14 @@ def test_gpu_radius_normals_fused_ties_and_chunked(gpu_ctx):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [3, 20, 33, 64])
 def test_gpu_knn_normals_pcl_bit_exact(gpu_ctx, k):
+    """k-NN normals bit for bit, with sparse outliers that defer to coarser levels."""
     import dialog_amd as D
     p, _, _ = small_cloud(3000, seed=9)
-    g = D.estimate_normals(p, k=k, ctx=gpu_ctx)
+    rng = np.random.default_rng(19)
+    far = rng.uniform(-6.0, 6.0, size=(300, 3)).astype(np.float32)
+    p = np.concatenate([p, far])
     o = O.estimate_normals_knn(p, k)
+    g = D.estimate_normals(p, k=k, ctx=gpu_ctx)
     assert np.array_equal(g.view(np.uint32), o.view(np.uint32)), int((g != o).any(axis=1).sum())
 
 
