@@ -16,7 +16,7 @@ DLG_SACMODEL_PLANE = 0
 DLG_SACMODEL_NORMAL_PLANE = 11
 DLG_REFIT_PCL = 0
 DLG_REFIT_FAST = 1
-ABI_VERSION = 3  # include/dialog_ransac.h DLG_ABI_VERSION: the structs below match that header
+ABI_VERSION = 4  # include/dialog_ransac.h DLG_ABI_VERSION: the structs below match that header
 
 SYMBOLS = [
     "dlg_abi_version", "dlg_status_string", "dlg_sac_params_default", "dlg_ctx_create",
@@ -45,6 +45,7 @@ DLG_OPT_PCL_REFIT_DEVICE = 8
 DLG_OPT_PRUNE_TILE_SCORER = 9
 DLG_OPT_NORMALS_FUSED = 10
 DLG_OPT_REGULATE_WAVE = 11
+DLG_OPT_FS_POISON = 12
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
 DLG_SCORE_EXACT = 0
@@ -88,7 +89,8 @@ class ExtractStats(C.Structure):
     _fields_ = [("rounds", C.c_int), ("tests", C.c_int64), ("tests_scored", C.c_int64),
                 ("score_launches", C.c_int), ("score_ms", C.c_double), ("select_ms", C.c_double),
                 ("wall_ms", C.c_double), ("lean_rounds", C.c_int), ("spec_misses", C.c_int),
-                ("pcl_host_checks", C.c_int), ("refit_walk_ms", C.c_double)]
+                ("pcl_host_checks", C.c_int), ("refit_walk_ms", C.c_double),
+                ("refit_repair_ms", C.c_double)]
 
 
 _lib = None

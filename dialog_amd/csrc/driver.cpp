@@ -113,6 +113,11 @@ void add_walk_ms(dlg_ctx* c, int k) {
   HIPCHK(hipEventElapsedTime(&ms, c->ev_walk[k][0], c->ev_walk[k][1]));
   c->sel_pending->refit_walk_ms += ms;
   c->walk_rec[k] = false;
+  if (c->rep_rec[k]) {
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_walk[k][2], c->ev_walk[k][3]));
+    c->sel_pending->refit_repair_ms += ms;
+    c->rep_rec[k] = false;
+  }
 }
 
 // after a stream synchronisation: the last compaction's Morton-copy totals and select timing
@@ -648,10 +653,13 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     const int sk = c->sel_k;  // this round's pair of select timing events
     c->walk_rec[sk] = false;
     // the PCL refit walk's timing events (profiling only)
+    // (e = 2, 3: k_fs_repair's, which runs on ranks > 0 of a group only)
+    c->rep_rec[sk] = false;
     auto walk_ev = [&](int e) -> hipEvent_t {
       if (!c->profiling) return nullptr;
+      if (e >= 2 && (c->comm->world() == 1 || c->comm->rank() == 0)) return nullptr;
       if (!c->ev_walk[sk][e]) HIPCHK(hipEventCreate(&c->ev_walk[sk][e]));
-      c->walk_rec[sk] = true;
+      (e >= 2 ? c->rep_rec : c->walk_rec)[sk] = true;
       return c->ev_walk[sk][e];
     };
     if (c->profiling) {
@@ -699,7 +707,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         const int64_t cap = std::max<int64_t>(src.n, 1);
         c->fs_scr.ensure(fs_scratch_bytes(cap, c->comm->world()));
         c->fs_b = fs_carve(c->fs_scr.p, cap, c->comm->world());
-        HIPCHK(hipMemsetAsync(c->fs_b.ticket, 0, 2 * sizeof(unsigned), c->stream));
+        HIPCHK(fs_reset(c->fs_b, c->stream, c->opt.fs_poison));
         c->fs_cap = cap;
       }
       int32_t* fs_res = reinterpret_cast<int32_t*>(c->small.p + 8);
@@ -729,7 +737,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         cl->ubits_dirty = false;
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
                         rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
-                        walk_ev(1));
+                        walk_ev(1), walk_ev(2), walk_ev(3));
       } else {
         c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
         stage_wait();
@@ -737,7 +745,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                       c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
         launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
                         c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(),
-                        walk_ev(0), walk_ev(1));
+                        walk_ev(0), walk_ev(1), walk_ev(2), walk_ev(3));
       }
       HIPCHK(hipGetLastError());
     } else {
@@ -1595,7 +1603,7 @@ dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float c
       HIPCHK(hipMemsetAsync(wst.p, 0, 72 * 8, c->stream));
       b.wst = wst.p;
     }
-    HIPCHK(hipMemsetAsync(b.ticket, 0, 2 * sizeof(unsigned), c->stream));
+    HIPCHK(fs_reset(b, c->stream, c->opt.fs_poison));
     if (n) HIPCHK(hipMemcpyAsync(dx.p, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream));
     const int32_t n32 = (int32_t)n;
     const float4 ci = make_float4(cin[0], cin[1], cin[2], cin[3]);
@@ -1710,6 +1718,7 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         break;
       case DLG_OPT_NORMALS_FUSED: o.nbr_fused = value != 0; break;
       case DLG_OPT_REGULATE_WAVE: o.bfs_wave = value != 0; break;
+      case DLG_OPT_FS_POISON: o.fs_poison = value != 0; break;
       case DLG_OPT_PRUNE_TILE_SCORER:
         if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && !(value >= 11 && value <= 14))
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
@@ -1734,6 +1743,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_PCL_REFIT_DEVICE: *value = o.pcl_dev; break;
     case DLG_OPT_NORMALS_FUSED: *value = o.nbr_fused; break;
     case DLG_OPT_REGULATE_WAVE: *value = o.bfs_wave; break;
+    case DLG_OPT_FS_POISON: *value = o.fs_poison; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer == kTileScorerExact ? DLG_TILE_EXACT : DLG_TILE_BF16; break;
     default: return DLG_ERR_INVALID;
   }

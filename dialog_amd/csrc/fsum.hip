@@ -1396,11 +1396,35 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   return b;
 }
 
+namespace {
+std::atomic<uint32_t> s_gen{0};  // launch stamps of the window tables (0: never a valid entry)
+
+__global__ void k_fs_poison(uint2* __restrict__ p, int64_t n, uint32_t stamp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = make_uint2(0x3F800000u + (uint32_t)(i & 0xFFFF), stamp);
+}
+}  // namespace
+
+hipError_t fs_reset(const FsBuffers& b, hipStream_t s, bool poison) {
+  const int64_t nt = (int64_t)kFsChains * b.wcap * kFtW, nq = (int64_t)kFsChains * b.wcap;
+  if (poison) {
+    const uint32_t next = s_gen.load() + 1u;  // (the stamp the next launch will use)
+    hipLaunchKernelGGL(k_fs_poison, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, b.wtab, nt,
+                       next);
+    hipLaunchKernelGGL(k_fs_poison, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, b.wq, nq,
+                       next);
+  }
+  hipError_t e = hipMemsetAsync(b.wtab, 0, sizeof(uint2) * (size_t)nt, s);
+  if (e == hipSuccess) e = hipMemsetAsync(b.wq, 0, sizeof(uint2) * (size_t)nq, s);
+  if (e == hipSuccess) e = hipMemsetAsync(b.ticket, 0, 2 * sizeof(unsigned), s);
+  return e;
+}
+
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
-                     hipEvent_t ev_walk0, hipEvent_t ev_walk1) {
-  static std::atomic<uint32_t> s_gen{0};
+                     hipEvent_t ev_walk0, hipEvent_t ev_walk1, hipEvent_t ev_rep0,
+                     hipEvent_t ev_rep1) {
   uint32_t gen = ++s_gen;
   if (gen == 0) gen = ++s_gen;  // (0 marks a dropped table entry)
   FsDev d{px, py, pz, stride, n_dev, b, gen};
@@ -1432,12 +1456,12 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
   hipLaunchKernelGGL(k_fs_base, dim3(1), dim3(256), 0, s, d, b.gath, r, W, b.base9, b.n_global);
   hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, b.base9);
   hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-  hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0,
-                        r > 0 ? nullptr : ev_walk1, 0u, d, (const float*)nullptr, r > 0 ? 1 : 0,
+  hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
+                        (const float*)nullptr, r > 0 ? 1 : 0,
                         (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
   if (r > 0) {
     comm->recv(b.start9, kFsChains, DType::I32, r - 1, s);
-    hipExtLaunchKernelGGL(k_fs_repair, dim3(kFsChains), dim3(kFwBS), 0, s, nullptr, ev_walk1, 0u,
+    hipExtLaunchKernelGGL(k_fs_repair, dim3(kFsChains), dim3(kFwBS), 0, s, ev_rep0, ev_rep1, 0u,
                           d, (const float*)b.start9);
   }
   if (r < W - 1) comm->send(b.sums, kFsChains, DType::I32, r + 1, s);

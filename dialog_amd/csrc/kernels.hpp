@@ -232,12 +232,20 @@ struct FsBuffers {
 // whole list is here)
 size_t fs_scratch_bytes(int64_t n_cap, int world);
 FsBuffers fs_carve(void* base, int64_t n_cap, int world);
+// after every fs_carve, before the first launch_fs_refit on it: zero the tickets and the window
+// tables (a table entry is valid only with the current launch's stamp, and reused scratch --
+// another layout's records, or a hipMalloc recycling freed memory -- could hold a word with that
+// stamp).  poison (tests only): first fill the tables with garbage entries carrying the next
+// launch's stamp, i.e. exactly what the clear must remove.
+hipError_t fs_reset(const FsBuffers& b, hipStream_t s, bool poison = false);
 class Comm;
-// ev_walk0 / ev_walk1 (optional): timing events riding k_fs_walk's dispatch
+// ev_walk0 / ev_walk1 (optional): timing events riding k_fs_walk's dispatch; ev_rep0 / ev_rep1
+// (several ranks, rank > 0): riding k_fs_repair's
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm = nullptr,
-                     hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr);
+                     hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr,
+                     hipEvent_t ev_rep0 = nullptr, hipEvent_t ev_rep1 = nullptr);
 
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers

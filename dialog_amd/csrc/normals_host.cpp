@@ -517,7 +517,7 @@ int64_t preprocess(dlg_ctx* c, const dlg_points* pts, int translate, float min_d
     // single-wave sequential pass took ~86 ms at 10M points
     w.fs_scr.ensure(fs_scratch_bytes(n, 1));
     const FsBuffers fb = fs_carve(w.fs_scr.p, n, 1);
-    HIPCHK(hipMemsetAsync(fb.ticket, 0, 2 * sizeof(unsigned), c->stream));
+    HIPCHK(fs_reset(fb, c->stream, c->opt.fs_poison));
     launch_fs_refit(w.qx.p, w.qy.p, w.qz.p, 1, reinterpret_cast<const int32_t*>(w.counters.p), n,
                     fb, nullptr, nullptr, nullptr, c->num_cus, c->stream);
     launch_centroid_div(fb.sums + 6, n, w.partial.p, c->stream);

@@ -36,8 +36,10 @@ extern "C" {
 /* 2: dlg_extract_stats gained lean_rounds, spec_misses, pcl_host_checks; dlg_score_benchmark's
  * 4th argument is a DLG_SCORE_* kernel; execution paths are context options, not environment
  * variables.  3: dlg_extract_stats gained refit_walk_ms; dlg_float_sums, dlg_cloud_estimate_normals
- * and dlg_plane_border were added; dlg_cloud_drop_spatial keeps the copy's buffers */
-#define DLG_ABI_VERSION 3
+ * and dlg_plane_border were added; dlg_cloud_drop_spatial keeps the copy's buffers.
+ * 4: dlg_extract_stats gained refit_repair_ms (refit_walk_ms is k_fs_walk alone on every rank);
+ * DLG_OPT_FS_POISON */
+#define DLG_ABI_VERSION 4
 
 typedef enum {
   DLG_OK = 0,
@@ -115,6 +117,9 @@ typedef struct {
                                   transcendental near a float rounding boundary) */
   double refit_walk_ms;        /* of select_ms: the device PCL refit's chain walks (k_fs_walk,
                                   latency-bound sequential chains), lean rounds */
+  double refit_repair_ms;      /* several ranks, rank > 0: the device time of the PCL refit's
+                                  repair walks from the previous rank's exact chain ends
+                                  (k_fs_repair), summed over the rounds */
 } dlg_extract_stats;
 
 void dlg_sac_params_default(dlg_sac_params* p);   /* PCL SACSegmentation defaults */
@@ -411,9 +416,12 @@ enum {
   DLG_OPT_NORMALS_FUSED = 10, /* PCL-float radius normals: 1 (default) search, (d2, index) order
                                and sums in one fused pass; 0: the chunked count / fill / sort /
                                sum pipeline */
-  DLG_OPT_REGULATE_WAVE = 11  /* RegulateNormal's claim pass: 1 (default) one wave per frontier
+  DLG_OPT_REGULATE_WAVE = 11, /* RegulateNormal's claim pass: 1 (default) one wave per frontier
                                node over its packed candidate cells; 0: one thread per (node,
                                cell) */
+  DLG_OPT_FS_POISON = 12    /* tests only: 1 fills the PCL float-sum walk's window tables with
+                               garbage entries stamped for the next launch whenever its scratch
+                               is laid out, before the clear; 0 (default) */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };

@@ -92,3 +92,28 @@ def test_device_refit_on_plane_inliers(gpu_ctx, fs):
     assert same(sums, literal(fs, xyz))
     print(f"\nfloat sums + refit: {np.round(ms, 4).tolist()} ms per ~450k-point plane; "
           f"{t4:.4f} ms at 4M points")
+
+
+def test_device_sums_poisoned_tables(fs):
+    """Window tables are valid only with the current launch's stamp; reused scratch could hold
+    words carrying that stamp (another layout's records, recycled device memory).  With
+    DLG_OPT_FS_POISON every table entry is filled with a garbage value stamped for the next launch
+    before fs_reset clears the tables: the sums must still equal the literal loop.  Hovering sums
+    (planes through the origin) make the walk consult the tables."""
+    ctx = D.Context(0)
+    try:
+        ctx.set_option(D.DLG_OPT_FS_POISON, 1)
+        assert ctx.get_option(D.DLG_OPT_FS_POISON) == 1
+        rng = np.random.default_rng(77)
+        for kind in ("hover", "quant", "alternating"):
+            for n in (4097, 270000, 900000):
+                xyz = np.ascontiguousarray(np.stack(gen(kind, n, rng), axis=1))
+                sums, _, _, _ = ctx.float_sums(xyz)
+                assert same(sums, literal(fs, xyz)), (kind, n)
+        p, lab, planes = plane_cloud(3_000_000, 6, seed=0xD1A106 + 3)
+        for k in range(6):
+            xyz = np.ascontiguousarray(p[lab == k])
+            sums, _, _, _ = ctx.float_sums(xyz)
+            assert same(sums, literal(fs, xyz)), k
+    finally:
+        ctx.close()
