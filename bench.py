@@ -89,7 +89,8 @@ def c5_secondary(D, ctx, a):
     out = {"workload": "C5: 10M-pt 20-plane cloud, k=20 normals, NORMAL_PLANE (w=0.1) extract; "
                        "postProcessPlanes on a 10M-pt 20-plane scene (1000-vertex borders); "
                        "chain_ms = device-resident normals (dlg_cloud_estimate_normals) + extract; "
-                       "chain_regulate_ms = normals + RegulateNormal + extract",
+                       "chain_regulate_ms = normals + RegulateNormal + extract, all on the "
+                       "cloud's device copy (dlg_cloud_regulate_normals)",
            "points": a.points}
 
     def timed(f, reps=2):
@@ -133,15 +134,17 @@ def c5_secondary(D, ctx, a):
     out["chain_ms"] = round(out["chain_ms"], 2)
 
     def chain_regulate():
-        # the reference's order: estimateNormal (k = 20, on the cloud's device copy) ->
-        # regulateNormal (BFS, r 0.1, seed 0) -> the NORMAL_PLANE extraction on the regulated
-        # normals (host round trip of the normals: dlg_regulate_normals takes host records)
-        nr = cloud.estimate_normals(k=20, copy_out=True)
-        rg, _, _ = D.regulate_normals(pts, nr, 0, True, 0.1, ctx=ctx)
-        cloud.set_normals(rg)
+        # the reference's order: estimateNormal (k = 20) -> regulateNormal (BFS, r 0.1, seed 0)
+        # -> the NORMAL_PLANE extraction on the regulated normals, all on the cloud's device copy
+        # (dlg_cloud_estimate_normals, dlg_cloud_regulate_normals: no host round trip)
+        cloud.estimate_normals(k=20)
+        cloud.regulate_normals(0, True, 0.1)
         return D.extract_planes(cloud, prm, max_planes=a.planes, min_inliers=a.min_inliers,
                                 capacity=a.points)
 
+    cloud.estimate_normals(k=20)
+    _, out["cloud_regulate_r0.1_ms"] = timed(lambda: cloud.regulate_normals(0, True, 0.1), 2)
+    out["cloud_regulate_r0.1_ms"] = round(out["cloud_regulate_r0.1_ms"], 2)
     _, out["chain_regulate_ms"] = timed(chain_regulate, 1)
     out["chain_regulate_ms"] = round(out["chain_regulate_ms"], 2)
     out["cloud_normals_knn20_ms"] = round(out["cloud_normals_knn20_ms"], 2)
@@ -380,17 +383,29 @@ def main():
         ctx.set_profiling(not a.no_events)
         nl = max(int(ep["stats"]["score_launches"]), 1)
         full_pairs = ep["stats"]["tests_scored"] / world / 32.0  # (tile, plane) pairs if unpruned
+        sub = st.get("sub_pairs", 0) > 0  # (the default sub-tile scorer)
+        ev_tests = 8 * st["sub_pairs"] if sub else 32 * st["pairs"]
         extras["pruned_work"] = {
-            "pairs_evaluated_per_launch": round(st["pairs"] / nl),
-            "pair_fraction": round(st["pairs"] / max(full_pairs, 1.0), 5),
+            "tile_pairs_per_launch": round(st["pairs"] / nl),
+            "tile_pair_fraction": round(st["pairs"] / max(full_pairs, 1.0), 5),
             "passes_per_launch": round(st["blocks"] / nl),
-            "pass_fill": round(st["pairs"] / max(128.0 * st["blocks"], 1.0), 4),
             "tile_list_entries_per_launch": round(st["list_entries"] / nl),
-            "evaluated_tests_per_step": int(32 * st["pairs"] * world),
-            "note": "(tile, plane) pairs the bounding spheres could not rule out, each evaluated "
-                    "as 32 exact PCL-order point tests (k_score_tiles_ex: lanes as planes, two "
-                    "planes of one tile per lane, 64 lanes per pass); `value` counts PCL's tests "
-                    "(iterations x active points), the kernel evaluates pair_fraction of them"}
+            "evaluated_tests_per_step": int(ev_tests * world),
+            "evaluated_fraction": round(ev_tests / max(32.0 * full_pairs, 1.0), 5),
+            "note": ("(tile, plane) pairs the tile bounding spheres could not rule out, split over "
+                     "the tiles' four 8-point sub-tile spheres; the (sub-tile, plane) pairs left "
+                     "are evaluated as 8 exact PCL-order point tests each (k_score_tiles_sx: lanes "
+                     "as planes, four planes of one sub-tile per lane, 64 lanes per pass)"
+                     if sub else
+                     "(tile, plane) pairs the bounding spheres could not rule out, each evaluated "
+                     "as 32 exact PCL-order point tests (k_score_tiles_ex)")
+                    + "; `value` counts PCL's tests (iterations x active points), the kernel "
+                      "evaluates evaluated_fraction of them"}
+        if sub:
+            extras["pruned_work"]["sub_pairs_per_launch"] = round(st["sub_pairs"] / nl)
+            extras["pruned_work"]["pass_fill"] = round(st["sub_pairs"] / max(256.0 * st["blocks"], 1.0), 4)
+        else:
+            extras["pruned_work"]["pass_fill"] = round(st["pairs"] / max(128.0 * st["blocks"], 1.0), 4)
     ms_per_step = elapsed / a.steps * 1e3
     # dominant kernel: the scoring launch (this rank's launches; tests per rank = scored / world)
     per_rank_tests = scored / world
@@ -516,9 +531,11 @@ def main():
                     roofline["issue_view"] = tj
                     pw = roofline.get("pruned_work")
                     vi = tj.get("per_launch", {}).get("SQ_INSTS_VALU")
-                    if pw and vi and pw["pairs_evaluated_per_launch"]:
-                        # (wave instructions; pairs from the stats run of the same workload)
-                        tj["valu_insts_per_pair"] = round(vi / pw["pairs_evaluated_per_launch"], 2)
+                    if pw and vi and pw.get("evaluated_tests_per_step") and launches:
+                        # (wave instructions; evaluated tests from the stats run of the same
+                        # workload: VALU lane-instructions per evaluated test)
+                        ev = pw["evaluated_tests_per_step"] / world / (launches / a.steps)
+                        tj["valu_lane_insts_per_evaluated_test"] = round(64.0 * vi / ev, 2)
             except Exception:
                 pass
 

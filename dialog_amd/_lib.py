@@ -31,6 +31,7 @@ SYMBOLS = [
     "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
     "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex", "dlg_cloud_drop_spatial",
     "dlg_abi_struct_size", "dlg_float_sums", "dlg_cloud_estimate_normals", "dlg_plane_border",
+    "dlg_cloud_regulate_normals",
 ]
 
 # context options (include/dialog_ransac.h): equivalent execution paths, identical results
@@ -48,6 +49,7 @@ DLG_OPT_REGULATE_WAVE = 11
 DLG_OPT_FS_POISON = 12
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
+DLG_TILE_SUB = 2
 DLG_SCORE_EXACT = 0
 DLG_SCORE_BF16 = 1
 DLG_SCORE_PRUNED = 2
@@ -167,6 +169,8 @@ def load():
                                           C.c_int64, C.c_int]
     L.dlg_regulate_normals.argtypes = [vp, C.POINTER(Points), fp, C.c_int64, C.c_int64, C.c_int,
                                        C.c_float, C.POINTER(C.c_uint8), i64p]
+    L.dlg_cloud_regulate_normals.argtypes = [vp, vp, C.c_int64, C.c_int, C.c_float,
+                                             C.POINTER(C.c_uint8), i64p, fp, C.c_int64]
     L.dlg_refit_planes.argtypes = [C.POINTER(Planes), fp]
     L.dlg_sac_control_create.argtypes = [pp, C.POINTER(SacParams), C.c_int64, C.c_int]
     L.dlg_sac_control_destroy.argtypes = [vp]

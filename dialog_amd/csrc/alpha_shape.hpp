@@ -20,7 +20,11 @@
 //   6. the points go back through transform1's inverse and the centroid.
 // The Delaunay triangulation here is a sweep-hull construction with edge flips (points sorted by
 // distance from a seed triangle's circumcentre, the convex hull grown around them, every new
-// edge legalised by the in-circle test).  For points in general position the triangulation is
+// edge legalised by the in-circle test).  Its structure follows mapbox's Delaunator
+// (https://github.com/mapbox/delaunator, ISC licence, (c) Vladimir Agafonkin / Mapbox: the
+// hullNext / hullPrev / hullTri / hullHash arrays, the pseudo-angle hash key, the legalisation
+// edge stack and the hull-triangle fix-up), restated in C++ with double orientation tests and a
+// long-double fallback near zero.  For points in general position the triangulation is
 // unique, so the kept triangles and the boundary edge SET equal qhull's (checked against
 // scipy.spatial.Delaunay, i.e. qhull, with "QJ": tests/test_borders.py).  What stays unpinned:
 // qhull's version and joggle seed (cocircular inputs triangulate by the joggle), the order qhull

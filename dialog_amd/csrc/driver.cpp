@@ -303,9 +303,10 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
       launch_gather_nrm(cl->pristine.nrm.p, cl->sp_order.p, m, cl->sp_pristine.nrm.p, c->stream);
     }
     cl->sp_tiles_pr.ensure((size_t)std::max<int64_t>(sp_tiles(m), 1));
+    cl->sp_subs_pr.ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(m), 1));
     cl->sp_supers_pr.ensure((size_t)std::max<int64_t>(sp_supers(m), 1));
     launch_sphere_bounds(cl->sp_pristine.x.p, cl->sp_pristine.y.p, cl->sp_pristine.z.p, m, nullptr,
-                         cl->sp_tiles_pr.p, cl->sp_supers_pr.p, c->stream);
+                         cl->sp_tiles_pr.p, cl->sp_supers_pr.p, c->stream, cl->sp_subs_pr.p);
     HIPCHK(hipGetLastError());
     // (no synchronisation: everything that reads the copy is queued behind it on the stream;
     // the scratch above is only rewritten by the next build, on the same stream)
@@ -320,7 +321,8 @@ SpatialView spatial_view(const dlg_cloud* cl) {
   const SoA& s = cl->sp_soa();
   const bool pr = cl->sp_cur < 0;
   return SpatialView{s.x.p, s.y.p, s.z.p, cl->sp_n, pr ? cl->sp_tiles_pr.p : cl->sp_tb[cl->sp_cur].p,
-                     pr ? cl->sp_supers_pr.p : cl->sp_sb[cl->sp_cur].p};
+                     pr ? cl->sp_supers_pr.p : cl->sp_sb[cl->sp_cur].p,
+                     pr ? cl->sp_subs_pr.p : cl->sp_ub[cl->sp_cur].p};
 }
 
 // (re)compute the sphere bounds of the working spatial copy when they are stale
@@ -328,10 +330,11 @@ void ensure_sphere_bounds(dlg_ctx* c, dlg_cloud* cl) {
   if (cl->sp_dirty && cl->sp_cur >= 0 && cl->sp_n > 0) {
     const int b = cl->sp_cur;
     cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+    cl->sp_ub[b].ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(cl->sp_n), 1));
     cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
     const SoA& s = cl->sp_soa();
     launch_sphere_bounds(s.x.p, s.y.p, s.z.p, cl->sp_n, nullptr, cl->sp_tb[b].p, cl->sp_sb[b].p,
-                         c->stream);
+                         c->stream, cl->sp_ub[b].p);
   }
   cl->sp_dirty = false;
 }
@@ -402,8 +405,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   if (prm.threshold == DBL_MAX) return out;  // PCL: "No threshold set!" -> computeModel false
   if (N < 3) return out;                      // getSamples: cannot select 3 unique points
 
-  // lean-list round: plane model over the Morton copy, single rank, device refit, a list that
-  // is pristine or already lean (a list compacted with coordinates stays on the full path)
+  // lean-list round: plane model over the Morton copy, device refit, a list that is pristine or
+  // already lean (a list compacted with coordinates stays on the full path); any rank count
+  // (below)
   const bool pcl_refit = prm.optimize && prm.refit_mode != DLG_REFIT_FAST;
   // PCL's float sums on the device (fsum.hip; several ranks: each walks its segment of the list
   // from the previous rank's end values); lean rounds take the unrefined inliers in list order
@@ -879,9 +883,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       const int b = cl->sp_spare();
       SoA& sd = cl->sp_buf[b];
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+      cl->sp_ub[b].ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(cl->sp_n), 1));
       cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
       launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
-                           cl->sp_sb[b].p, c->stream);
+                           cl->sp_sb[b].p, c->stream, cl->sp_ub[b].p);
     } else {
       stage_wait();
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
@@ -905,9 +910,10 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       // totals[3]), so a round whose plane is rejected leaves the current bounds intact
       const int b = cl->sp_spare();
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+      cl->sp_ub[b].ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(cl->sp_n), 1));
       cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
       launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 3, cl->sp_tb[b].p,
-                           cl->sp_sb[b].p, c->stream);
+                           cl->sp_sb[b].p, c->stream, cl->sp_ub[b].p);
     }
     HIPCHK(hipGetLastError());
     // one marker at the end of the round's work: inl_gid is final there (flush_emit's copy waits
@@ -1102,11 +1108,18 @@ void dlg::attach_normals(dlg_ctx* c, dlg_cloud* cl, const float* raw_dev, int64_
     cl->cur = -1;  // normals attach to the pristine list: the cloud is reset
     cl->n_active = cl->n_total;
     cl->pristine.ensure_nrm((size_t)std::max<int64_t>(cl->n_total, 1));
+    cl->raw_nrm.ensure((size_t)std::max<int64_t>(cl->n_total, 1));
     if (raw_dev && cl->n_total > 0) {
       PointsView pv = cl->pristine.view(cl->n_total);
       if (by_pos) pv.gid = nullptr;
-      launch_pack_point_normals(raw_dev, stride_f, curv_off, pv, cl->id_base, cl->pristine.nrm.p,
-                                c->stream);
+      // the records as given, in pristine order (unless they are that buffer already), then the
+      // normalised copy the NORMAL_PLANE model reads
+      if (raw_dev != reinterpret_cast<const float*>(cl->raw_nrm.p))
+        launch_pack_point_normals(raw_dev, stride_f, curv_off, pv, cl->id_base, cl->raw_nrm.p,
+                                  c->stream, false);
+      pv.gid = nullptr;
+      launch_pack_point_normals(reinterpret_cast<const float*>(cl->raw_nrm.p), 4, 3, pv,
+                                cl->id_base, cl->pristine.nrm.p, c->stream, true);
       HIPCHK(hipGetLastError());
       // the Morton copy carries the normals too (pruned NORMAL_PLANE scoring)
       if (cl->sp_built) {
@@ -1381,6 +1394,7 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     cl->sp_pristine.release();
     cl->sp_tiles_pr.release();
     cl->sp_supers_pr.release();
+    cl->sp_subs_pr.release();
     return s;
   }
   *out = cl.release();
@@ -1392,6 +1406,7 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
   if (cl->ctx) (void)hipSetDevice(cl->ctx->device);
   if (cl->ctx && cl->ctx->stream) (void)hipStreamSynchronize(cl->ctx->stream);
   cl->pristine.release();
+  cl->raw_nrm.release();
   cl->buf[0].release();
   cl->buf[1].release();
   cl->sp_pristine.release();
@@ -1399,10 +1414,12 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
   cl->sp_buf[1].release();
   cl->sp_tiles_pr.release();
   cl->sp_supers_pr.release();
+  cl->sp_subs_pr.release();
   cl->sp_order.release();
   for (int b = 0; b < 2; ++b) {
     cl->sp_tb[b].release();
     cl->sp_sb[b].release();
+    cl->sp_ub[b].release();
   }
   cl->ubits.release();
   cl->tag.release();
@@ -1720,9 +1737,12 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
       case DLG_OPT_REGULATE_WAVE: o.bfs_wave = value != 0; break;
       case DLG_OPT_FS_POISON: o.fs_poison = value != 0; break;
       case DLG_OPT_PRUNE_TILE_SCORER:
-        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && !(value >= 11 && value <= 14))
-          throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
-        o.tile_scorer = value == DLG_TILE_EXACT ? kTileScorerExact : value == DLG_TILE_BF16 ? kTileScorerBf16 : (int)value;
+        // (DLG_TILE_* values, and the A/B-only kernel variants kTileScorerExK1/ExK4/SubK2)
+        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != DLG_TILE_SUB &&
+            value != kTileScorerExK1 && value != kTileScorerExK4 && value != kTileScorerSubK2)
+          throw DlgError(DLG_ERR_INVALID,
+                         "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_SUB, DLG_TILE_EXACT or DLG_TILE_BF16");
+        o.tile_scorer = (int)value;
         break;
       default: throw DlgError(DLG_ERR_INVALID, "unknown option");
     }
@@ -1744,7 +1764,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_NORMALS_FUSED: *value = o.nbr_fused; break;
     case DLG_OPT_REGULATE_WAVE: *value = o.bfs_wave; break;
     case DLG_OPT_FS_POISON: *value = o.fs_poison; break;
-    case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer == kTileScorerExact ? DLG_TILE_EXACT : DLG_TILE_BF16; break;
+    case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;
     default: return DLG_ERR_INVALID;
   }
   return DLG_OK;

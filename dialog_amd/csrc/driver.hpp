@@ -166,7 +166,7 @@ struct PathOptions {
   int score_kernel = kScoreBf16;  // exhaustive scorer: kScoreBf16 or kScoreExact
   bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
   int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
-  int tile_scorer = 0;            // pruned plane scorer: kTileScorerExact or kTileScorerBf16
+  int tile_scorer = DLG_TILE_SUB;  // pruned plane scorer (spatial.hpp kTileScorer*)
   bool nbr_fused = true;          // PCL-float radius normals in one fused pass (else chunked)
   bool bfs_wave = true;           // RegulateNormal's claim pass: one wave per frontier node
   // PCL float refit (DLG_REFIT_PCL, any rank count): 1 = the nine sums on the device (fsum.hip,
@@ -276,6 +276,9 @@ struct dlg_cloud {
   int32_t id_base = 0;
   bool gid_ident = false;  // pristine gid[i] == id_base + i (uploaded without setIndices)
   bool has_normals = false;
+  // the attached normals as given (PCL's normal_x/y/z and curvature, pristine order): RegulateNormal
+  // on the device copy (dlg_cloud_regulate_normals) flips these and re-derives the normalised ones
+  DevBuf<float4> raw_nrm;
   int64_t n_total = 0;
   int64_t n_active = 0;
   int cur = -1;  // -1 pristine, 0 = A, 1 = B
@@ -298,6 +301,7 @@ struct dlg_cloud {
   SoA sp_pristine, sp_buf[2];
   // sphere bounds of the pristine copy and of each ping-pong buffer sp_buf[i]
   DevBuf<float4> sp_tiles_pr, sp_supers_pr, sp_tb[2], sp_sb[2];
+  DevBuf<float4> sp_subs_pr, sp_ub[2];  // 8-point sub-tile spheres (4 per tile) of each copy
   const SoA& sp_soa() const { return sp_cur < 0 ? sp_pristine : sp_buf[sp_cur]; }
   int sp_spare() const { return sp_cur == 0 ? 1 : 0; }
   PointsView view() const {

@@ -1343,12 +1343,14 @@ __global__ __launch_bounds__(kNpBS) void k_score_np(PointsView src, const HypRec
 }
 
 __global__ void k_pack_point_normals(const float* __restrict__ raw, int64_t stride_f, int curv_off,
-                                     PointsView src, int32_t id_base, float4* __restrict__ out) {
+                                     PointsView src, int32_t id_base, float4* __restrict__ out,
+                                     int normalize) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= src.n) return;
   // (gid null: the records follow the list's positions)
   const float* r = raw + (src.gid ? (int64_t)(src.gid[e] - id_base) : e) * stride_f;
-  out[e] = eigen_normalized3(r[0], r[1], r[2], r[curv_off]);
+  out[e] = normalize ? eigen_normalized3(r[0], r[1], r[2], r[curv_off])
+                     : make_float4(r[0], r[1], r[2], r[curv_off]);
 }
 
 // dlg_cloud_upload: caller records (stride_f floats, xyz first) -> SoA + global ids
@@ -1718,10 +1720,10 @@ void launch_score_np(PointsView src, const HypRec* hyps, int D, const ModelTest&
 }
 
 void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,
-                               int32_t id_base, float4* out, hipStream_t s) {
+                               int32_t id_base, float4* out, hipStream_t s, bool normalize) {
   if (src.n <= 0) return;
   hipLaunchKernelGGL(k_pack_point_normals, dim3(cdiv(src.n, 256)), dim3(256), 0, s, raw, stride_f,
-                     curv_off, src, id_base, out);
+                     curv_off, src, id_base, out, normalize ? 1 : 0);
 }
 
 void launch_upload_gather(const float* raw, int64_t stride_f, const int32_t* idx, int64_t n,

@@ -266,9 +266,10 @@ void launch_select_tail(PointsView src, const float4* coef, const ModelTest& mt,
                         const int32_t* tile_off_in, const int32_t* tile_off_out, int32_t* inl_gid,
                         float* inl_xyz, const PointsOut* dst, hipStream_t s);
 // raw caller normals (n records of stride_f floats, curvature at curv_off) gathered by the
-// cloud's local point index (gid - id_base) -> (normalized normal, curvature)
+// cloud's local point index (gid - id_base) -> (normalized normal, curvature), or the raw
+// (normal, curvature) when normalize is false
 void launch_pack_point_normals(const float* raw, int64_t stride_f, int curv_off, PointsView src,
-                               int32_t id_base, float4* out, hipStream_t s);
+                               int32_t id_base, float4* out, hipStream_t s, bool normalize = true);
 // cloud upload: records of stride_f floats (xyz first), optional index list -> SoA + ids
 void launch_upload_gather(const float* raw, int64_t stride_f, const int32_t* idx, int64_t n,
                           int32_t id_base, PointsOut out, hipStream_t s);

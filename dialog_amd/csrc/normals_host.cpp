@@ -354,6 +354,9 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
   HIPCHK(hipGetLastError());
 }
 
+int64_t regulate_core(dlg_ctx* c, int n, const float* X, const float* Y, const float* Z,
+                      const BBox& b, int64_t seed, int seed_is_outward, float radius);
+
 int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64_t stride,
                          int64_t seed, int seed_is_outward, float radius, uint8_t* processed_out) {
   check_points(pts);
@@ -368,16 +371,30 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   if (seed >= n) throw DlgError(DLG_ERR_INVALID, "seed index out of range");
   NormalsWork& w = c->nw;
   const BBox b = upload_points(c, pts);
-  const GridDesc G = make_grid(b, (double)radius);
-  GridBufs B;
-  build_grid(c, n, G, 0, &B);
-  const float r2 = (float)((double)radius * (double)radius);
-
   const size_t nbytes = (size_t)n * (size_t)stride;
   w.out.ensure(nbytes);
   w.nrm.ensure(n);
   HIPCHK(hipMemcpyAsync(w.out.p, nrm_io, nbytes, hipMemcpyHostToDevice, c->stream));
   launch_unpack_normals(reinterpret_cast<const float*>(w.out.p), n, stride / 4, w.nrm.p, c->stream);
+  const int64_t qt = regulate_core(c, n, w.x.p, w.y.p, w.z.p, b, seed, seed_is_outward, radius);
+  launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), stride / 4, -1, c->stream);
+  HIPCHK(hipMemcpyAsync(nrm_io, w.out.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+  if (processed_out)
+    HIPCHK(hipMemcpyAsync(processed_out, w.processed.p, n, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  return qt;
+}
+
+// the BFS of regulateNormal over the n points X/Y/Z (bounding box b) and the normals in nw.nrm
+// (x, y, z; .w carried through): nw.nrm flipped in place (PCL's queue order, float dots),
+// nw.processed = isProcessed; returns the queue length (points reached)
+int64_t regulate_core(dlg_ctx* c, int n, const float* X, const float* Y, const float* Z,
+                      const BBox& b, int64_t seed, int seed_is_outward, float radius) {
+  NormalsWork& w = c->nw;
+  const GridDesc G = make_grid(b, (double)radius);
+  GridBufs B;
+  build_grid(c, n, G, 0, &B, X, Y, Z);
+  const float r2 = (float)((double)radius * (double)radius);
   w.nrm_s.ensure(n);
   w.pos_of.ensure(n);
   w.processed.ensure(n);
@@ -416,8 +433,47 @@ int64_t regulate_normals(dlg_ctx* c, const dlg_points* pts, float* nrm_io, int64
   }
   const int64_t qt = w.h_bst.p[3];
   launch_bfs_finish(B, n, w.nrm_s.p, w.processed_s.p, w.nrm.p, w.processed.p, c->stream);
-  launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), stride / 4, -1, c->stream);
-  HIPCHK(hipMemcpyAsync(nrm_io, w.out.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipGetLastError());
+  return qt;
+}
+
+// regulateNormal on the cloud's device copy and its attached normals (no host round trip): the
+// flipped normals replace the attached ones (raw and normalised, the Morton copy's too)
+int64_t cloud_regulate_normals(dlg_ctx* c, dlg_cloud* cl, int64_t seed, int seed_is_outward,
+                               float radius, uint8_t* processed_out, float* normals_out,
+                               int64_t out_stride) {
+  if (c->comm->world() > 1)
+    throw DlgError(DLG_ERR_INVALID, "dlg_cloud_regulate_normals: the cloud is one rank's shard "
+                                    "(world > 1); the BFS needs the whole cloud");
+  if (!cl->has_normals) throw DlgError(DLG_ERR_INVALID, "the cloud has no normals attached");
+  if (!(radius > 0.0f && std::isfinite(radius))) throw DlgError(DLG_ERR_INVALID, "radius must be > 0");
+  if (normals_out && (out_stride % 4 || (out_stride != 16 && out_stride < 32)))
+    throw DlgError(DLG_ERR_INVALID, "out_stride_bytes must be 16 or >= 32 (multiple of 4)");
+  if (cl->n_total > INT32_MAX / 2) throw DlgError(DLG_ERR_INVALID, "more than 2^30 points");
+  const int n = (int)cl->n_total;
+  if (seed < 0 || n == 0) {  // PlaneDetect.h:592-596: "invalid point index", return
+    if (processed_out && n) std::memset(processed_out, 0, (size_t)n);
+    if (seed >= 0 && n == 0) throw DlgError(DLG_ERR_INVALID, "seed index out of range");
+    return 0;
+  }
+  if (seed >= n) throw DlgError(DLG_ERR_INVALID, "seed index out of range");
+  NormalsWork& w = c->nw;
+  w.nrm.ensure(n);
+  HIPCHK(hipMemcpyAsync(w.nrm.p, cl->raw_nrm.p, 16 * (size_t)n, hipMemcpyDeviceToDevice, c->stream));
+  const float* X = cl->pristine.x.p;
+  const float* Y = cl->pristine.y.p;
+  const float* Z = cl->pristine.z.p;
+  const BBox b = bbox_of(c, X, Y, Z, n);
+  const int64_t qt = regulate_core(c, n, X, Y, Z, b, seed, seed_is_outward, radius);
+  HIPCHK(hipMemcpyAsync(cl->raw_nrm.p, w.nrm.p, 16 * (size_t)n, hipMemcpyDeviceToDevice, c->stream));
+  attach_normals(c, cl, reinterpret_cast<const float*>(cl->raw_nrm.p), 4, 3, true);
+  if (normals_out) {
+    const size_t obytes = (size_t)n * (size_t)out_stride;
+    w.out.ensure(obytes);
+    launch_pack_normals(w.nrm.p, n, reinterpret_cast<float*>(w.out.p), out_stride / 4,
+                        out_stride == 16 ? 3 : 4, c->stream);
+    HIPCHK(hipMemcpyAsync(normals_out, w.out.p, obytes, hipMemcpyDeviceToHost, c->stream));
+  }
   if (processed_out)
     HIPCHK(hipMemcpyAsync(processed_out, w.processed.p, n, hipMemcpyDeviceToHost, c->stream));
   sync(c);
@@ -637,6 +693,18 @@ dlg_status dlg_regulate_normals(dlg_ctx* c, const dlg_points* pts, float* normal
   return guarded(c, [&] {
     const int64_t k = regulate_normals(c, pts, normals_inout, stride_bytes, seed_idx,
                                        seed_is_outward, radius, processed_out);
+    if (n_processed) *n_processed = k;
+  });
+}
+
+dlg_status dlg_cloud_regulate_normals(dlg_ctx* c, dlg_cloud* cl, int64_t seed_idx,
+                                      int seed_is_outward, float radius, uint8_t* processed_out,
+                                      int64_t* n_processed, float* normals_out,
+                                      int64_t out_stride_bytes) {
+  if (!c || !cl || cl->ctx != c) return DLG_ERR_INVALID;
+  return guarded(c, [&] {
+    const int64_t k = cloud_regulate_normals(c, cl, seed_idx, seed_is_outward, radius,
+                                             processed_out, normals_out, out_stride_bytes);
     if (n_processed) *n_processed = k;
   });
 }

@@ -522,12 +522,19 @@ int64_t plane_border(const float* pts, int64_t stride_f, int64_t n, const float 
     const double nn = (double)pn[0] * pn[0] + (double)pn[1] * pn[1] + (double)pn[2] * pn[2];
     const double dt = ((double)pn[0] * u[0] + (double)pn[1] * u[1] + (double)pn[2] * u[2]) / nn;
     for (int k = 0; k < 3; ++k) u[k] -= dt * pn[k];
+    // ties along u (a straight edge perpendicular to u) broken by the smallest coordinate along
+    // w = n x u: the lexicographic minimum is always a strictly convex vertex (never a collinear
+    // middle one, whose turn the reference's rule cannot read)
+    const double w[3] = {(double)pn[1] * u[2] - (double)pn[2] * u[1],
+                         (double)pn[2] * u[0] - (double)pn[0] * u[2],
+                         (double)pn[0] * u[1] - (double)pn[1] * u[0]};
     int64_t mk = 0;
-    double mv = INFINITY;
+    double mv = INFINITY, mw = INFINITY;
     for (int64_t k = 0; k < nb; ++k) {
       const float* a = &H.pts[3 * (size_t)bi[k]];
       const double v = a[0] * u[0] + a[1] * u[1] + a[2] * u[2];
-      if (v < mv) { mv = v; mk = k; }
+      const double vw = a[0] * w[0] + a[1] * w[1] + a[2] * w[2];
+      if (v < mv || (v == mv && vw < mw)) { mv = v; mw = vw; mk = k; }
     }
     std::rotate(bi.begin(), bi.begin() + (mk + nb - 1) % nb, bi.end());
   }

@@ -126,8 +126,8 @@ class Context:
         """The pruned scoring kernel's work counters (needs DLG_OPT_PRUNE_STATS = 1)."""
         a = (C.c_uint64 * 6)()
         self.check(self._L.dlg_prune_stats(self.h, a, int(bool(reset))))
-        return {"list_entries": a[1], "tiles": a[2], "blocks": a[3], "pairs": a[4],
-                "redecided_blocks": a[5]}
+        return {"sub_pairs": a[0], "list_entries": a[1], "tiles": a[2], "blocks": a[3],
+                "pairs": a[4], "redecided_blocks": a[5]}
 
     def set_profiling(self, on=True):
         self.check(self._L.dlg_set_profiling(self.h, int(bool(on))))
@@ -216,6 +216,22 @@ class Cloud:
             self.ctx.h, self.h, float(radius), int(k), _f32p(vp), m,
             _f32p(out) if copy_out else None, 16))
         return out
+
+    def regulate_normals(self, seed_idx: int, seed_is_outward: bool, radius: float,
+                         copy_out: bool = False):
+        """dlg_cloud_regulate_normals: regulateNormal() (PlaneDetect.h:586-646) on this cloud's
+        device copy and its attached normals, no host round trip; the regulated normals replace
+        the attached ones (the cloud is reset).  -> (processed bool[N], number processed,
+        normals float32 [N,4] when copy_out else None)."""
+        n = self.n
+        proc = np.zeros(max(n, 1), np.uint8)
+        cnt = C.c_int64(0)
+        out = np.empty((n, 4), np.float32) if copy_out else None
+        self.ctx.check(self.ctx._L.dlg_cloud_regulate_normals(
+            self.ctx.h, self.h, int(seed_idx), int(bool(seed_is_outward)), float(radius),
+            proc.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(cnt),
+            _f32p(out) if copy_out else None, 16))
+        return proc[:n].astype(bool), int(cnt.value), out
 
     @property
     def n_active(self):

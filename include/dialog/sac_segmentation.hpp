@@ -22,11 +22,13 @@
 // dialog::Error (there is no CPU fallback).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../dialog_ransac.h"
@@ -482,6 +484,52 @@ inline size_t fillPlaneClouds(const pcl::PointCloud<PointT>& cloud,
     ++added;
   }
   return added;
+}
+
+// polyPointCloud() (PlaneDetect.h:1376-1440) on dlg_plane_border: the plane's points projected
+// onto their least-squares plane (pcl::computePointNormal + projPoint2Plane), the concave border
+// of pcl::ConcaveHull (alpha shape of the projected points, alpha = alpha_poly, config.txt:28;
+// the reference takes polygons[0], here the boundary polygon of largest area) appended to
+// `border` in the reference's orientation (reversed when normalize(normalize(p1 - p0) x
+// normalize(p2 - p1)) . pn < 0).  pn: any type with pn[0..2] (float[3], Eigen::Vector3f).  The
+// input cloud is not modified (the reference projects a copy, :1367-1368).  A plane of fewer than
+// 3 points gets no border.  Host arithmetic: replaces pcl::ConcaveHull (qhull) in polyPlanes.
+template <typename PointT, typename Vec3>
+inline void polyPointCloud(const pcl::PointCloud<PointT>& cloud, pcl::PointCloud<PointT>& border,
+                           const Vec3& pn, float alpha_poly) {
+  const int64_t n = (int64_t)cloud.points.size();
+  static_assert(sizeof(PointT) >= 12, "PointT must start with float x, y, z");
+  dlg_points pts{reinterpret_cast<const float*>(cloud.points.data()), n, (int64_t)sizeof(PointT)};
+  const float v[3] = {(float)pn[0], (float)pn[1], (float)pn[2]};
+  std::vector<PointT> out((size_t)std::max<int64_t>(n, 1));
+  int64_t nb = 0;
+  const dlg_status s = dlg_plane_border(&pts, v, alpha_poly, reinterpret_cast<float*>(out.data()),
+                                        (int64_t)sizeof(PointT), n, &nb);
+  if (s != DLG_OK) throw Error(s, std::string("dlg_plane_border: ") + dlg_status_string(s));
+  for (int64_t i = 0; i < nb; ++i) {
+    PointT q = PointT();
+    q.x = out[(size_t)i].x; q.y = out[(size_t)i].y; q.z = out[(size_t)i].z;
+    border.push_back(q);
+  }
+}
+
+// polyPlanes() (PlaneDetect.h:1357-1374): every plane whose border is still null gets one from
+// polyPointCloud over its points_set, oriented by its coeff.values[0..2] (the outward normal
+// fillPlaneClouds stored); planes with a border are skipped, as in the reference.  PlaneT: the
+// reference's struct Plane (HeaderFile.h:81-88).  Returns the number of borders built.
+template <typename PlaneT, typename Alloc>
+inline size_t polyPlanes(std::vector<PlaneT, Alloc>& plane_clouds, float alpha_poly) {
+  size_t built = 0;
+  for (PlaneT& pl : plane_clouds) {
+    if (pl.border) continue;
+    typedef typename std::remove_reference<decltype(*pl.points_set)>::type CloudT;
+    pl.border.reset(new CloudT);
+    if (!pl.points_set || pl.coeff.values.size() < 3) continue;
+    const float pn[3] = {pl.coeff.values[0], pl.coeff.values[1], pl.coeff.values[2]};
+    polyPointCloud(*pl.points_set, *pl.border, pn, alpha_poly);
+    ++built;
+  }
+  return built;
 }
 
 }  // namespace dialog

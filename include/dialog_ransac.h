@@ -38,7 +38,7 @@ extern "C" {
  * variables.  3: dlg_extract_stats gained refit_walk_ms; dlg_float_sums, dlg_cloud_estimate_normals
  * and dlg_plane_border were added; dlg_cloud_drop_spatial keeps the copy's buffers.
  * 4: dlg_extract_stats gained refit_repair_ms (refit_walk_ms is k_fs_walk alone on every rank);
- * DLG_OPT_FS_POISON */
+ * DLG_OPT_FS_POISON; DLG_TILE_SUB (the default tile scorer); dlg_cloud_regulate_normals */
 #define DLG_ABI_VERSION 4
 
 typedef enum {
@@ -242,6 +242,18 @@ dlg_status dlg_regulate_normals(dlg_ctx* ctx, const dlg_points* pts, float* norm
                                 int64_t stride_bytes, int64_t seed_idx, int seed_is_outward,
                                 float radius, uint8_t* processed_out, int64_t* n_processed);
 
+/* regulateNormal() first-round branch on a cloud's device copy and the normals attached to it
+ * (dlg_cloud_estimate_normals or dlg_cloud_set_normals): the same BFS as dlg_regulate_normals
+ * over the cloud's uploaded points, with no host round trip; the flipped normals replace the
+ * attached ones (so a following SACMODEL_NORMAL_PLANE extraction uses them) and the cloud is
+ * reset.  seed_idx indexes the cloud's points (upload order; with setIndices, the index list's
+ * order).  processed_out (nullable): one byte per point; normals_out (nullable): the regulated
+ * normals, stride 16 (x, y, z, curvature) or >= 32 (pcl::Normal).  One rank only. */
+dlg_status dlg_cloud_regulate_normals(dlg_ctx* ctx, dlg_cloud* cloud, int64_t seed_idx,
+                                      int seed_is_outward, float radius, uint8_t* processed_out,
+                                      int64_t* n_processed, float* normals_out,
+                                      int64_t out_stride_bytes);
+
 /* regulateNormal() later-round branch (PlaneDetect.h:553-584, !isFirstPostProcess): each point
  * of pts takes the orientation of its nearest neighbour in the backup cloud ref_pts
  * (KdTreeFLANN::nearestKSearch k = 1; equidistant neighbours -> lowest index): its normal flips
@@ -293,15 +305,16 @@ typedef struct {
 /* polyPlanes() -> polyPointCloud() (PlaneDetect.h:1358-1440) for one plane, so the four-file
  * polygon hand-off (PCLViewer.cpp:1341-1396) can run from RANSAC output alone: the plane's points
  * (its points_set) projected onto their least-squares plane (pcl::computePointNormal, PCL float
- * arithmetic) as projPoint2Plane does, then a concave border.  The reference takes polygons[0] of
- * pcl::ConcaveHull (qhull alpha shape, alpha = alpha_poly, config.txt:28); qhull is absent here,
- * so the border is the outer boundary of the projected points' alpha occupancy (cells of edge
- * alpha, the largest 8-connected component, traced once around; per boundary cell its projected
- * point farthest from the component's centroid): a closed polygon of projected plane points --
- * the reference's contract, not qhull's facets (parity unpinned).  Orientation as the reference:
- * reversed when normalize(normalize(p1 - p0) x normalize(p2 - p1)) . pn < 0.  border_out: up to
- * cap records of out_stride_bytes (>= 12; xyz first); *n_out = vertices (0: fewer than 3 points
- * or no polygon), also reported with DLG_ERR_CAPACITY.  Host arithmetic; no context. */
+ * arithmetic) as projPoint2Plane does, then pcl::ConcaveHull's alpha shape (alpha = alpha_poly,
+ * config.txt:28) restated step by step (PCA frame, Delaunay triangulation, circumradius filter,
+ * boundary edges, PCL's polygon walk; dialog_amd/csrc/alpha_shape.hpp): the triangles, the alpha
+ * filter and the boundary are qhull's ("QJ") on the committed fixtures.  The reference takes
+ * polygons[0]; qhull's facet order, which decides that, is unpinned, so the border is the
+ * boundary polygon of largest area.  Orientation as the reference: reversed when
+ * normalize(normalize(p1 - p0) x normalize(p2 - p1)) . pn < 0.  border_out: up to cap records of
+ * out_stride_bytes (>= 12; xyz first); *n_out = vertices (0: fewer than 3 points or no polygon),
+ * also reported with DLG_ERR_CAPACITY.  Host arithmetic; no context.  The C++ shim's
+ * dialog::polyPointCloud / dialog::polyPlanes wrap it (include/dialog/sac_segmentation.hpp). */
 dlg_status dlg_plane_border(const dlg_points* plane_pts, const float pn[3], float alpha,
                             float* border_out, int64_t out_stride_bytes, int64_t cap,
                             int64_t* n_out);
@@ -382,9 +395,16 @@ dlg_status dlg_score_benchmark(dlg_ctx* ctx, dlg_cloud* cloud, int D, int kernel
  * optimizeModelCoefficients' float eigen33 refit of cin.  sums_out[9] and coeff_out[4] are the
  * device's bits; *uncertain = 1 when an eigen33 transcendental could not be rounded for certain
  * (the extraction then takes the host's value).  reps >= 1 launches are timed: *ms_per_call.
- * walk_stats (optional) per chain: windows, speculation passes, passes needing the full lemma,
- * chunks stepped alone, reruns, shader clocks of the walk, of its stepping, chunk records (the
- * last call's). */
+ * walk_stats (optional, the last call's; 8 int64 per chain, several counters packed):
+ *   [0] windows walked record by record;
+ *   [1] bits 0-31 speculation passes, bits 32-63 table lookups missed: no table built yet;
+ *   [2] bits 0-31 passes needing the full lemma, bits 32-63 table lookups missed: lead out of
+ *       the table's range;
+ *   [3] bits 0-23 chunks stepped alone, bits 24-63 five 8-bit saturating buckets of the missed
+ *       leads (|lead| < 128, < 512, < 4096, larger, not an exact multiple of the quantum);
+ *   [4] bits 0-31 reruns, bits 32-63 table lookups missed: entry dropped by the builder;
+ *   [5] shader clocks of the walk; [6] shader clocks of its integer stepping;
+ *   [7] bits 0-31 windows passed by their summaries, bits 32-63 windows passed by a table. */
 dlg_status dlg_float_sums(dlg_ctx* ctx, const float* xyz, int64_t n, const float cin[4], int reps,
                           float sums_out[9], float coeff_out[4], int* uncertain,
                           double* ms_per_call, int64_t* walk_stats /* nullable: [9][8] */);
@@ -411,8 +431,11 @@ enum {
                                the host recomputing every refit's tail from the sums; 3 as 2 and
                                every round's select redone with the host's plane (test) */
   DLG_OPT_PRUNE_TILE_SCORER = 9, /* the pruned plane scorer's (tile, plane) pairs:
-                               DLG_TILE_EXACT (default) PCL-order f32 with lanes as planes, or
-                               DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band re-decision */
+                               DLG_TILE_SUB (default) 8-point sub-tile spheres, then PCL-order f32
+                               with lanes as planes; DLG_TILE_EXACT the same over whole 32-point
+                               tiles; DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band
+                               re-decision.  (11, 14, 22: A/B-only variants of the first two with
+                               1, 4, 2 planes per lane; same counts) */
   DLG_OPT_NORMALS_FUSED = 10, /* PCL-float radius normals: 1 (default) search, (d2, index) order
                                and sums in one fused pass; 0: the chunked count / fill / sort /
                                sum pipeline */
@@ -423,13 +446,14 @@ enum {
                                garbage entries stamped for the next launch whenever its scratch
                                is laid out, before the clear; 0 (default) */
 };
-enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
+enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1, DLG_TILE_SUB = 2 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
 dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);
 dlg_status dlg_ctx_get_option(const dlg_ctx* ctx, int option, int64_t* value);
 /* the pruned scoring kernel's counters since DLG_OPT_PRUNE_STATS was set (or the last reset):
- * [0] unused, [1] super-tile list entries tested against tile spheres, [2] tiles visited,
- * [3] 32x32 blocks (DLG_TILE_EXACT: 64-pair passes) scored, [4] (tile, plane) pairs scored,
+ * [0] (8-point sub-tile, plane) pairs evaluated (DLG_TILE_SUB), [1] super-tile list entries tested
+ * against tile spheres, [2] tiles visited, [3] 32x32 blocks (DLG_TILE_EXACT / SUB: passes)
+ * scored, [4] (tile, plane) pairs near the tile sphere (scored whole except with DLG_TILE_SUB),
  * [5] blocks with a band re-decision (DLG_TILE_BF16 only) */
 dlg_status dlg_prune_stats(dlg_ctx* ctx, uint64_t out[6], int reset);
 

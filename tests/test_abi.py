@@ -85,7 +85,7 @@ def test_no_device_fails_loudly(monkeypatch):
         seg.segment()
 
 
-@pytest.mark.parametrize("prog", ["shim_smoke", "plane_clouds_glue"])
+@pytest.mark.parametrize("prog", ["shim_smoke", "plane_clouds_glue", "poly_planes_glue"])
 def test_cpp_shim_compiles_and_links(tmp_path, prog):
     """The PCL-compatible C++ host shim compiles with g++ against the header and links the .so
     (shim_smoke: every shim entry; plane_clouds_glue: INTEGRATION.md §3's PlaneDetect.h adapter

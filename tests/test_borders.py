@@ -295,3 +295,73 @@ def test_gpu_extract_borders_polygon_files_post_process(gpu_ctx, tmp_path):
         assert np.dot(co[k][:3], rn[k]) > 0.99
         got = np.intersect1d(absorbed[k], rest[k]).size
         assert got >= 0.9 * rest[k].size, (k, got, rest[k].size)
+
+
+def _outer_vertex_set(pts, alpha):
+    """The fixture logic of make_alpha.py for one plane: ConcaveHull's PCA frame in float64, qhull
+    ("QJ") Delaunay, the alpha filter, the largest boundary component's vertex set."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_alpha import alpha_complex
+    q = pts.astype(np.float64)
+    c = q.mean(0)
+    _, V = np.linalg.eigh(np.cov((q - c).T, bias=True))
+    xy = (q - c) @ V[:, [2, 1]]
+    _, _, _, comps, near = alpha_complex(xy, alpha)
+    return set(max(comps, key=len)), near, xy, c, V
+
+
+def _patch_cloud():
+    """Two plane patches of the fixtures' kinds (a square and an L), far enough from each other's
+    planes that RANSAC's inliers of one never reach into the other, plus sparse outliers."""
+    rng = np.random.default_rng(2024)
+    a, na, _, _ = patch(rng, 6000, (0.3, -0.5, 0.8), 2.0, "square")
+    b, nb, _, _ = patch(rng, 8000, (1, 2, -0.5), 0.5, "L")
+    b = b + (20.0 * na).astype(np.float32)  # (B's plane stays B's: shifted along A's normal)
+    out = rng.uniform(-15, 25, (100, 3)).astype(np.float32)
+    return np.vstack([a, b, out]).astype(np.float32)
+
+
+@pytest.mark.gpu
+def test_cpp_poly_planes_on_ransac_planes(tmp_path):
+    """the reference's polyPlanes() with dialog::polyPlanes (the shim's
+    polyPointCloud over dlg_plane_border) in place of pcl::ConcaveHull, compiled as a C++ adapter
+    with the reference's struct Plane, on planes RANSAC extracted on the GPU.  Every border's
+    vertices are distinct points of its plane's projected points_set, and they are exactly the
+    outer boundary of qhull's alpha shape of those points (test_plane_border_vertex_set_pinned's
+    fixture logic, computed here with scipy's qhull); a second polyPlanes() call keeps them."""
+    lib = os.path.dirname(D.LIB_PATH)
+    exe = tmp_path / "poly_planes_glue"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "poly_planes_glue.cpp"), "-o", str(exe),
+                    "-L", lib, "-ldialog_amd", f"-Wl,-rpath,{lib}"], check=True)
+    cloud = _patch_cloud()
+    fin, fout = tmp_path / "cloud.bin", tmp_path / "planes.bin"
+    cloud.tofile(fin)
+    r = subprocess.run([str(exe), str(fin), str(fout)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    assert r.stdout.strip() == "planes 2 built 2 again 0", r.stdout
+    raw = fout.read_bytes()
+    off = 0
+
+    def take():
+        nonlocal off
+        k = int(np.frombuffer(raw, np.int64, 1, off)[0])
+        off += 8
+        a = np.frombuffer(raw, np.float32, 3 * k, off).reshape(k, 3)
+        off += 12 * k
+        return a
+
+    assert int(np.frombuffer(raw, np.int64, 1, 0)[0]) == 2
+    off = 8
+    for _ in range(2):
+        pts, border = take(), take()
+        assert pts.shape[0] > 5000 and border.shape[0] >= 8
+        want, near, xy, c, V = _outer_vertex_set(pts, 0.5)
+        assert not near  # (no circumradius within 1e-9 of alpha: the filter is decided)
+        bq = (border.astype(np.float64) - c) @ V[:, [2, 1]]
+        d2 = ((bq[:, None, :] - xy[None, :, :]) ** 2).sum(-1)
+        idx = d2.argmin(1)
+        assert np.sqrt(d2[np.arange(len(idx)), idx]).max() < 1e-4
+        assert len(set(idx.tolist())) == len(idx)
+        assert set(idx.tolist()) == want

@@ -312,6 +312,39 @@ def test_gpu_c5_chain_vs_oracle_chain(gpu_ctx, nmode, refit):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("refit", ["pcl", "fast"])
+def test_gpu_c5_regulate_chain_vs_oracle_chain(gpu_ctx, refit):
+    """The reference's order end to end at test size, all on the device copy: k = 20 normals
+    (dlg_cloud_estimate_normals) -> RegulateNormal (dlg_cloud_regulate_normals, BFS r 0.1 from
+    point 0) -> SACMODEL_NORMAL_PLANE extract-and-remove, equal to the oracle's chain (k-NN
+    normals -> regulate_normals -> extract) bit for bit."""
+    import dialog_amd as D
+    from dialog_amd.synth import plane_cloud
+    p, _, _ = plane_cloud(30000, 5, outlier_frac=0.1, seed=56, patch=2.0)
+    o = O.estimate_normals_knn(p, 20)
+    o_reg, _, o_cnt = O.regulate_normals(p, o, 0, False, 0.1)
+    kw = dict(max_iterations=255, probability=1.0)
+    mode = D.DLG_REFIT_PCL if refit == "pcl" else D.DLG_REFIT_FAST
+    prm = D.make_params(0.05, model=D.SACMODEL_NORMAL_PLANE, normal_distance_weight=0.1,
+                        refit_mode=mode, **kw)
+    r = O.extract_planes(p, 0.05, max_planes=6, min_inliers=200, normals=o_reg,
+                         normal_distance_weight=0.1, refit=refit, **kw)
+    cloud = D.Cloud(gpu_ctx, p)
+    try:
+        cloud.estimate_normals(k=20)
+        _, cnt, g_reg = cloud.regulate_normals(0, False, 0.1, copy_out=True)
+        assert cnt == o_cnt
+        assert np.array_equal(g_reg.view(np.uint32), o_reg.view(np.uint32))
+        e = D.extract_planes(cloud, prm, max_planes=6, min_inliers=200)
+    finally:
+        cloud.close()
+    assert e["n_planes"] == r["n_planes"] >= 4
+    assert np.array_equal(e["coeffs"].view(np.uint32), r["coeffs"].view(np.uint32))
+    assert np.array_equal(e["offsets"], r["offsets"])
+    assert np.array_equal(e["inliers"], r["inliers"])
+
+
+@pytest.mark.gpu
 def test_gpu_cloud_normals_index_subset(gpu_ctx):
     """dlg_cloud_estimate_normals on a cloud uploaded with an index subset (and a non-zero id
     base): the normals of the subset cloud itself, == dlg_estimate_normals on those points."""

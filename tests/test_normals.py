@@ -317,6 +317,47 @@ def test_gpu_regulate_bit_exact(gpu_ctx, cloud, seed_idx, outward, r, wave):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed_idx,outward,r", [(0, True, 0.08), (4567, False, 0.15)])
+def test_gpu_cloud_regulate_bit_exact(gpu_ctx, cloud, seed_idx, outward, r):
+    """dlg_cloud_regulate_normals: the BFS on the cloud's device copy and its attached normals
+    (no host round trip) equals the oracle's BFS bit for bit; the regulated normals replace the
+    attached ones (raw, as read back, and the curvature untouched)."""
+    import dialog_amd as D
+    p, _, _ = cloud
+    nrm = O.estimate_normals(p, RADIUS)
+    rng = np.random.default_rng(seed_idx + 7)
+    nrm[:, :3] *= np.where(rng.random(len(p)) < 0.5, -1.0, 1.0).astype(np.float32)[:, None]
+    o_reg, o_proc, o_cnt = O.regulate_normals(p, nrm, seed_idx, outward, r)
+    cl = D.Cloud(gpu_ctx, p)
+    try:
+        cl.set_normals(nrm)
+        g_proc, g_cnt, g_reg = cl.regulate_normals(seed_idx, outward, r, copy_out=True)
+        assert g_cnt == o_cnt
+        assert np.array_equal(g_proc, o_proc)
+        np.testing.assert_array_equal(g_reg[:, :3], o_reg[:, :3])  # NaN-aware, bit-exact
+        np.testing.assert_array_equal(g_reg[:, 3], nrm[:, 3])
+        # a second call sees the regulated normals (they replaced the attached ones): with the
+        # seed confirmed outward nothing flips any more
+        g2_proc, g2_cnt, g2_reg = cl.regulate_normals(seed_idx, True, r, copy_out=True)
+        o2_reg, o2_proc, o2_cnt = O.regulate_normals(p, o_reg, seed_idx, True, r)
+        assert g2_cnt == o2_cnt and np.array_equal(g2_proc, o2_proc)
+        np.testing.assert_array_equal(g2_reg[:, :3], o2_reg[:, :3])
+        # invalid seed: nothing changes; out of range / no normals: errors
+        pr, cnt, _ = cl.regulate_normals(-1, True, r)
+        assert cnt == 0 and not pr.any()
+        with pytest.raises(D.DialogError):
+            cl.regulate_normals(len(p), True, r)
+    finally:
+        cl.close()
+    bare = D.Cloud(gpu_ctx, p)
+    try:
+        with pytest.raises(D.DialogError):
+            bare.regulate_normals(0, True, r)
+    finally:
+        bare.close()
+
+
+@pytest.mark.gpu
 def test_gpu_regulate_edges(gpu_ctx, cloud):
     import dialog_amd as D
     p, _, _ = cloud

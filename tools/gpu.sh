@@ -16,7 +16,10 @@
 #                                         -> traffic.py / pmc_issue.py summaries
 #   c5                                    tools/bench_c5.py (normals, RegulateNormal, chain)
 #   c5prof                                rocprofv3 --kernel-trace --stats over tools/c5_kernels.py
+#   c5pmc                                 SQ issue counters (one PMC pass) over tools/bench_c5.py
 #   walk                                  tools/fs_walk_stats.py (PCL float-sum walk counters)
+#   walkab=<a.so,b.so>                    walk counters under two library builds, alternated
+#                                         (tools/with_lib.py; A/B of walk variants)
 #   py=<script,args...>                   any python script (comma-separated argv)
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -69,6 +72,12 @@ for s in "$@"; do
     c5prof) run c5prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5prof" -o run -- \
               python3 tools/c5_kernels.py ${arg//,/ } ;;
     walk) run walk 300 python3 -u tools/fs_walk_stats.py ${arg//,/ } ;;
+    c5pmc) run c5pmc 220 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d "$O/c5pmc" -o run -- python3 tools/bench_c5.py 10000000 1 ;;
+    walkab)
+      a=${arg%%,*}; b=${arg#*,}
+      for v in "$a" "$b" "$a" "$b"; do
+        run walkab_$(basename "$v" .so) 150 python3 -u tools/with_lib.py "$v" tools/fs_walk_stats.py 4
+      done ;;
     py) run py_$(basename "${arg%%,*}" .py) 900 python3 -u ${arg//,/ } ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
