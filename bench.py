@@ -383,29 +383,17 @@ def main():
         ctx.set_profiling(not a.no_events)
         nl = max(int(ep["stats"]["score_launches"]), 1)
         full_pairs = ep["stats"]["tests_scored"] / world / 32.0  # (tile, plane) pairs if unpruned
-        sub = st.get("sub_pairs", 0) > 0  # (the default sub-tile scorer)
-        ev_tests = 8 * st["sub_pairs"] if sub else 32 * st["pairs"]
         extras["pruned_work"] = {
-            "tile_pairs_per_launch": round(st["pairs"] / nl),
-            "tile_pair_fraction": round(st["pairs"] / max(full_pairs, 1.0), 5),
+            "pairs_evaluated_per_launch": round(st["pairs"] / nl),
+            "pair_fraction": round(st["pairs"] / max(full_pairs, 1.0), 5),
             "passes_per_launch": round(st["blocks"] / nl),
+            "pass_fill": round(st["pairs"] / max(128.0 * st["blocks"], 1.0), 4),
             "tile_list_entries_per_launch": round(st["list_entries"] / nl),
-            "evaluated_tests_per_step": int(ev_tests * world),
-            "evaluated_fraction": round(ev_tests / max(32.0 * full_pairs, 1.0), 5),
-            "note": ("(tile, plane) pairs the tile bounding spheres could not rule out, split over "
-                     "the tiles' four 8-point sub-tile spheres; the (sub-tile, plane) pairs left "
-                     "are evaluated as 8 exact PCL-order point tests each (k_score_tiles_sx: lanes "
-                     "as planes, four planes of one sub-tile per lane, 64 lanes per pass)"
-                     if sub else
-                     "(tile, plane) pairs the bounding spheres could not rule out, each evaluated "
-                     "as 32 exact PCL-order point tests (k_score_tiles_ex)")
-                    + "; `value` counts PCL's tests (iterations x active points), the kernel "
-                      "evaluates evaluated_fraction of them"}
-        if sub:
-            extras["pruned_work"]["sub_pairs_per_launch"] = round(st["sub_pairs"] / nl)
-            extras["pruned_work"]["pass_fill"] = round(st["sub_pairs"] / max(256.0 * st["blocks"], 1.0), 4)
-        else:
-            extras["pruned_work"]["pass_fill"] = round(st["pairs"] / max(128.0 * st["blocks"], 1.0), 4)
+            "evaluated_tests_per_step": int(32 * st["pairs"] * world),
+            "note": "(tile, plane) pairs the bounding spheres could not rule out, each evaluated "
+                    "as 32 exact PCL-order point tests (k_score_tiles_ex: lanes as planes, two "
+                    "planes of one tile per lane, 64 lanes per pass); `value` counts PCL's tests "
+                    "(iterations x active points), the kernel evaluates pair_fraction of them"}
     ms_per_step = elapsed / a.steps * 1e3
     # dominant kernel: the scoring launch (this rank's launches; tests per rank = scored / world)
     per_rank_tests = scored / world

@@ -47,9 +47,9 @@ DLG_OPT_PRUNE_TILE_SCORER = 9
 DLG_OPT_NORMALS_FUSED = 10
 DLG_OPT_REGULATE_WAVE = 11
 DLG_OPT_FS_POISON = 12
+DLG_OPT_HYP_SHARD = 13
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
-DLG_TILE_SUB = 2
 DLG_SCORE_EXACT = 0
 DLG_SCORE_BF16 = 1
 DLG_SCORE_PRUNED = 2

@@ -303,10 +303,9 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
       launch_gather_nrm(cl->pristine.nrm.p, cl->sp_order.p, m, cl->sp_pristine.nrm.p, c->stream);
     }
     cl->sp_tiles_pr.ensure((size_t)std::max<int64_t>(sp_tiles(m), 1));
-    cl->sp_subs_pr.ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(m), 1));
     cl->sp_supers_pr.ensure((size_t)std::max<int64_t>(sp_supers(m), 1));
     launch_sphere_bounds(cl->sp_pristine.x.p, cl->sp_pristine.y.p, cl->sp_pristine.z.p, m, nullptr,
-                         cl->sp_tiles_pr.p, cl->sp_supers_pr.p, c->stream, cl->sp_subs_pr.p);
+                         cl->sp_tiles_pr.p, cl->sp_supers_pr.p, c->stream);
     HIPCHK(hipGetLastError());
     // (no synchronisation: everything that reads the copy is queued behind it on the stream;
     // the scratch above is only rewritten by the next build, on the same stream)
@@ -321,8 +320,7 @@ SpatialView spatial_view(const dlg_cloud* cl) {
   const SoA& s = cl->sp_soa();
   const bool pr = cl->sp_cur < 0;
   return SpatialView{s.x.p, s.y.p, s.z.p, cl->sp_n, pr ? cl->sp_tiles_pr.p : cl->sp_tb[cl->sp_cur].p,
-                     pr ? cl->sp_supers_pr.p : cl->sp_sb[cl->sp_cur].p,
-                     pr ? cl->sp_subs_pr.p : cl->sp_ub[cl->sp_cur].p};
+                     pr ? cl->sp_supers_pr.p : cl->sp_sb[cl->sp_cur].p};
 }
 
 // (re)compute the sphere bounds of the working spatial copy when they are stale
@@ -330,11 +328,10 @@ void ensure_sphere_bounds(dlg_ctx* c, dlg_cloud* cl) {
   if (cl->sp_dirty && cl->sp_cur >= 0 && cl->sp_n > 0) {
     const int b = cl->sp_cur;
     cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
-    cl->sp_ub[b].ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(cl->sp_n), 1));
     cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
     const SoA& s = cl->sp_soa();
     launch_sphere_bounds(s.x.p, s.y.p, s.z.p, cl->sp_n, nullptr, cl->sp_tb[b].p, cl->sp_sb[b].p,
-                         c->stream, cl->sp_ub[b].p);
+                         c->stream);
   }
   cl->sp_dirty = false;
 }
@@ -510,6 +507,18 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                         c->res.p + Dp, c->stream);
       HIPCHK(hipMemsetAsync(c->res.p, 0, 4 * (size_t)Dp, c->stream));
     }
+    // hypothesis sharding: this rank scores hypotheses [h_lo, h_hi) only (slices in whole
+    // 64-hypothesis groups, so an exhaustive kernel's padded group never reaches into another
+    // rank's slice), the other counts stay zero until the allreduce below
+    int h_lo = 0, h_hi = D;
+    if (c->hcomm) {
+      const int64_t U = Dp / 64, R = c->hcomm->world(), r = c->hcomm->rank();
+      h_lo = (int)std::min<int64_t>(D, 64 * (U * r / R));
+      h_hi = (int)std::min<int64_t>(D, 64 * (U * (r + 1) / R));
+    }
+    const int Ds = h_hi - h_lo;
+    const HypRec* hyps_s = c->hyps.p + h_lo;
+    int32_t* counts_s = c->res.p + h_lo;
     // the pruned scorer records its timing events on its own dispatches (no marker packets)
     const bool ext_ev = c->profiling && (pruned_np || (!np && pruned));
     if (c->profiling && !ext_ev) HIPCHK(hipEventRecord(c->ev[0], c->stream));
@@ -527,7 +536,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       pk.best_smp = best_smp_dev;
       pk.out = c->pick.p;
     }
-    const bool fuse_pick = speculate && (pruned_np || (!np && pruned)) && c->comm->world() == 1;
+    const bool fuse_pick = speculate && (pruned_np || (!np && pruned)) && c->comm->world() == 1 &&
+                           !c->hcomm;
     if (fuse_pick) {
       if (!c->pick_done.p) {
         c->pick_done.ensure(1);
@@ -539,24 +549,26 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
       const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold};
-      launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
+      launch_score_pruned(spatial_view(cl), hyps_s, Ds, cthr, pmargin, cl->amax, counts_s,
                           c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), &npp,
                           fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
                           ext_ev ? c->ev[1] : nullptr);
-    } else if (np)
-      launch_score_np(src, c->hyps.p, D, mt, c->res.p, c->num_cus, c->stream);
-    else if (pruned) {
+    } else if (np) {
+      if (Ds > 0) launch_score_np(src, hyps_s, Ds, mt, counts_s, c->num_cus, c->stream);
+    } else if (pruned) {
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
-      launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, pmargin, cl->amax, c->res.p,
+      launch_score_pruned(spatial_view(cl), hyps_s, Ds, cthr, pmargin, cl->amax, counts_s,
                           c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), nullptr,
                           fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
                           ext_ev ? c->ev[1] : nullptr, c->opt.tile_scorer);
-    } else
-      launch_score(src, c->hyps.p, D, cthr, c->res.p, c->opt.score_kernel, c->num_cus, c->stream);
+    } else if (Ds > 0) {
+      launch_score(src, hyps_s, Ds, cthr, counts_s, c->opt.score_kernel, c->num_cus, c->stream);
+    }
     HIPCHK(hipGetLastError());
     if (c->profiling && !ext_ev) HIPCHK(hipEventRecord(c->ev[1], c->stream));
     if (c->comm->world() > 1) c->comm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
+    if (c->hcomm) c->hcomm->allreduce_sum(c->res.p, D, DType::I32, c->stream);
     c->h_res.ensure((size_t)Dp + D);
     ++launches;
     st->tests_scored += (int64_t)D * N;
@@ -883,10 +895,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       const int b = cl->sp_spare();
       SoA& sd = cl->sp_buf[b];
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
-      cl->sp_ub[b].ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(cl->sp_n), 1));
       cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
       launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
-                           cl->sp_sb[b].p, c->stream, cl->sp_ub[b].p);
+                           cl->sp_sb[b].p, c->stream);
     } else {
       stage_wait();
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
@@ -910,10 +921,9 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       // totals[3]), so a round whose plane is rejected leaves the current bounds intact
       const int b = cl->sp_spare();
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
-      cl->sp_ub[b].ensure((size_t)std::max<int64_t>(kTileSubs * sp_tiles(cl->sp_n), 1));
       cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
       launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 3, cl->sp_tb[b].p,
-                           cl->sp_sb[b].p, c->stream, cl->sp_ub[b].p);
+                           cl->sp_sb[b].p, c->stream);
     }
     HIPCHK(hipGetLastError());
     // one marker at the end of the round's work: inl_gid is final there (flush_emit's copy waits
@@ -1394,7 +1404,6 @@ dlg_status dlg_cloud_upload(dlg_ctx* c, const dlg_points* pts, const int32_t* in
     cl->sp_pristine.release();
     cl->sp_tiles_pr.release();
     cl->sp_supers_pr.release();
-    cl->sp_subs_pr.release();
     return s;
   }
   *out = cl.release();
@@ -1414,12 +1423,10 @@ dlg_status dlg_cloud_destroy(dlg_cloud* cl) {
   cl->sp_buf[1].release();
   cl->sp_tiles_pr.release();
   cl->sp_supers_pr.release();
-  cl->sp_subs_pr.release();
   cl->sp_order.release();
   for (int b = 0; b < 2; ++b) {
     cl->sp_tb[b].release();
     cl->sp_sb[b].release();
-    cl->sp_ub[b].release();
   }
   cl->ubits.release();
   cl->tag.release();
@@ -1486,6 +1493,27 @@ dlg_status dlg_cloud_set_normals(dlg_ctx* c, dlg_cloud* cl, const float* normals
   });
 }
 
+namespace {
+// DLG_OPT_HYP_SHARD on a multi-rank context: for the call, the context runs as one rank (every
+// rank holds the whole cloud and computes the same round) and only the scoring is split by
+// hypotheses over the real communicator (one_batch: slices + an allreduce of the counts)
+struct HypShardScope {
+  dlg_ctx* c;
+  bool on;
+  explicit HypShardScope(dlg_ctx* ctx) : c(ctx), on(ctx->opt.hyp_shard && ctx->comm->world() > 1) {
+    if (!on) return;
+    if (!c->solo) c->solo = make_single_comm();
+    std::swap(c->comm, c->solo);
+    c->hcomm = c->solo.get();
+  }
+  ~HypShardScope() {
+    if (!on) return;
+    std::swap(c->comm, c->solo);
+    c->hcomm = nullptr;
+  }
+};
+}  // namespace
+
 dlg_status dlg_sac_segment(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* prm, float coeff_out[4],
                            int32_t* inliers_out, int64_t cap, int64_t* n_inliers,
                            dlg_sac_stats* stats) {
@@ -1493,6 +1521,7 @@ dlg_status dlg_sac_segment(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* prm,
   if (!inliers_out && cap > 0) return DLG_ERR_INVALID;
   dlg_sac_stats local;
   dlg_sac_stats* st = stats ? stats : &local;
+  HypShardScope hs(c);
   return guarded(c, [&] {
     std::memset(coeff_out, 0, 4 * sizeof(float));
     *n_inliers = 0;
@@ -1527,6 +1556,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
   dlg_extract_stats* xs = stats ? stats : &local;
   std::memset(xs, 0, sizeof(*xs));
   auto t0 = std::chrono::steady_clock::now();
+  HypShardScope hs(c);
   dlg_status s = guarded(c, [&] {
     *n_planes = 0;
     if (max_planes > 0) offsets_out[0] = 0;
@@ -1736,12 +1766,12 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
       case DLG_OPT_NORMALS_FUSED: o.nbr_fused = value != 0; break;
       case DLG_OPT_REGULATE_WAVE: o.bfs_wave = value != 0; break;
       case DLG_OPT_FS_POISON: o.fs_poison = value != 0; break;
+      case DLG_OPT_HYP_SHARD: o.hyp_shard = value != 0; break;
       case DLG_OPT_PRUNE_TILE_SCORER:
-        // (DLG_TILE_* values, and the A/B-only kernel variants kTileScorerExK1/ExK4/SubK2)
-        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != DLG_TILE_SUB &&
-            value != kTileScorerExK1 && value != kTileScorerExK4 && value != kTileScorerSubK2)
-          throw DlgError(DLG_ERR_INVALID,
-                         "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_SUB, DLG_TILE_EXACT or DLG_TILE_BF16");
+        // (DLG_TILE_* values, and the A/B-only kernel variants kTileScorerExK1/ExK4)
+        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != kTileScorerExK1 &&
+            value != kTileScorerExK4)
+          throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
         o.tile_scorer = (int)value;
         break;
       default: throw DlgError(DLG_ERR_INVALID, "unknown option");
@@ -1764,6 +1794,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_NORMALS_FUSED: *value = o.nbr_fused; break;
     case DLG_OPT_REGULATE_WAVE: *value = o.bfs_wave; break;
     case DLG_OPT_FS_POISON: *value = o.fs_poison; break;
+    case DLG_OPT_HYP_SHARD: *value = o.hyp_shard; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;
     default: return DLG_ERR_INVALID;
   }

@@ -166,7 +166,7 @@ struct PathOptions {
   int score_kernel = kScoreBf16;  // exhaustive scorer: kScoreBf16 or kScoreExact
   bool prune_stats = false;       // accumulate the pruned kernel's work counters (dlg_prune_stats)
   int sel1_tile = 16384;          // points per single-pass select tile (kSel1Points)
-  int tile_scorer = DLG_TILE_SUB;  // pruned plane scorer (spatial.hpp kTileScorer*)
+  int tile_scorer = DLG_TILE_EXACT;  // pruned plane scorer (spatial.hpp kTileScorer*)
   bool nbr_fused = true;          // PCL-float radius normals in one fused pass (else chunked)
   bool bfs_wave = true;           // RegulateNormal's claim pass: one wave per frontier node
   // PCL float refit (DLG_REFIT_PCL, any rank count): 1 = the nine sums on the device (fsum.hip,
@@ -174,6 +174,8 @@ struct PathOptions {
   // refit's tail from the published sums every round, 3 = as 2 and the round's select is always
   // redone with the host's plane (exercises the path an uncertain transcendental takes)
   int pcl_dev = 1;
+  bool hyp_shard = false;  // every rank holds the whole cloud; rank r scores its slice of each
+                           // batch's hypotheses, the counts are allreduced (DLG_OPT_HYP_SHARD)
   bool fs_poison = false;  // tests only: fill the float-sum walk's window tables with garbage
                            // entries stamped for the next launch before the clear (fs_reset)
 };
@@ -184,6 +186,11 @@ struct dlg_ctx {
   int num_cus = 256;
   hipStream_t stream = nullptr;
   std::unique_ptr<Comm> comm;
+  // hypothesis sharding (DLG_OPT_HYP_SHARD, SURVEY 8(e)'s small-N fallback): while a call on a
+  // replicated cloud runs, `comm` is a one-rank communicator (every rank computes the whole
+  // round), `solo` holds the real one and `hcomm` points at it for the scoring's split
+  std::unique_ptr<Comm> solo;
+  Comm* hcomm = nullptr;
   std::string err;
   bool profiling = false;
   bool sp_all = true;  // every rank holds a valid spatial copy (agreed per extraction)
@@ -301,7 +308,6 @@ struct dlg_cloud {
   SoA sp_pristine, sp_buf[2];
   // sphere bounds of the pristine copy and of each ping-pong buffer sp_buf[i]
   DevBuf<float4> sp_tiles_pr, sp_supers_pr, sp_tb[2], sp_sb[2];
-  DevBuf<float4> sp_subs_pr, sp_ub[2];  // 8-point sub-tile spheres (4 per tile) of each copy
   const SoA& sp_soa() const { return sp_cur < 0 ? sp_pristine : sp_buf[sp_cur]; }
   int sp_spare() const { return sp_cur == 0 ? 1 : 0; }
   PointsView view() const {

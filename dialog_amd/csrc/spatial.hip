@@ -81,8 +81,7 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
                                                        const float* __restrict__ Z, int64_t n_arg,
                                                        const int32_t* __restrict__ n_dev,
                                                        float4* __restrict__ tiles,
-                                                       float4* __restrict__ supers,
-                                                       float4* __restrict__ subs) {
+                                                       float4* __restrict__ supers) {
   __shared__ float s_p[3][kSb2Pts + kSb2Pts / kTileP];  // row t: 33 floats
   const int64_t n = n_dev ? (int64_t)*n_dev : n_arg;
   const int lane = threadIdx.x;
@@ -123,26 +122,6 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
   const float rt = d * (1.0f + 0x1p-18f) + 1e-30f;
   const int64_t t = (int64_t)blockIdx.x * (kSb2Pts / kTileP) + lane;
   if (np > 0) tiles[t] = make_float4(cx, cy, cz, rt);
-  if (subs && np > 0) {
-    // the tile's 8-point sub-tiles, built the same way (an empty one: radius -inf, never near)
-#pragma unroll
-    for (int g = 0; g < kTileSubs; ++g) {
-      const int i0 = g * kSubP, i1 = min(np, i0 + kSubP);
-      float a0 = INFINITY, b0 = INFINITY, c0 = INFINITY, a1 = -INFINITY, b1 = -INFINITY, c1 = -INFINITY;
-      for (int i = i0; i < i1; ++i) {
-        a0 = fminf(a0, px[i]); b0 = fminf(b0, py[i]); c0 = fminf(c0, pz[i]);
-        a1 = fmaxf(a1, px[i]); b1 = fmaxf(b1, py[i]); c1 = fmaxf(c1, pz[i]);
-      }
-      const float gx = 0.5f * (a0 + a1), gy = 0.5f * (b0 + b1), gz = 0.5f * (c0 + c1);
-      float dg = 0.0f;
-      for (int i = i0; i < i1; ++i) {
-        const float dx = px[i] - gx, dy = py[i] - gy, dz = pz[i] - gz;
-        dg = fmaxf(dg, sqrtf(dx * dx + dy * dy + dz * dz));
-      }
-      subs[kTileSubs * t + g] = i1 > i0 ? make_float4(gx, gy, gz, dg * (1.0f + 0x1p-18f) + 1e-30f)
-                                        : make_float4(0.f, 0.f, 0.f, -INFINITY);
-    }
-  }
   // super-tile of each kSuperTiles lanes: box over its tiles, then max |c_t - C| + r_t
   float bx0 = x0, by0 = y0, bz0 = z0, bx1 = x1, by1 = y1, bz1 = z1;
 #pragma unroll
@@ -350,7 +329,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
         }
       }
     }
-    return __shfl(v, 0);
+    return __builtin_amdgcn_readfirstlane(__shfl(v, 0));  // (uniform: scalar control flow)
   };
   (void)work;
   int it_next = claim();
@@ -360,7 +339,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_rl(
     it_next = claim();
     const int t0 = it * chunk, t_end = min(ntiles, t0 + chunk);
     const int sidx = t0 / kSuperTiles;  // kSuperTiles % chunk == 0: one super-tile per item
-    const int nlp = lp_n[sidx];
+    const int nlp = __builtin_amdgcn_readfirstlane(lp_n[sidx]);
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
     // the item's tiles take the list kListCap entries at a time (one pass unless it is long)
 #pragma unroll 1
@@ -687,7 +666,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
         }
       }
     }
-    return __shfl(v, 0);
+    return __builtin_amdgcn_readfirstlane(__shfl(v, 0));  // (uniform: scalar control flow)
   };
   // lane l holds point l of an item (its two tiles); NaN past n
   auto fetch = [&](int it, float& px, float& py, float& pz) {
@@ -769,7 +748,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     if (nq > head && ((int)(ring[head & (kExRing - 1)] >> 13) & 1) == (seq & 1)) pass(nq - head);
     const float4 tb0 = tiles[t0];
     const float4 tb1 = t0 + 1 < t_end ? tiles[t0 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const int nlp = lp_n[sidx];
+    const int nlp = __builtin_amdgcn_readfirstlane(lp_n[sidx]);
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
     {
       float* d = spt + (slot0 + (lane >> 5)) * kExSlotF + (lane & 31);
@@ -854,266 +833,6 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_score_tiles_sx (default tile scorer, SACMODEL_PLANE): k_score_tiles_ex with an 8-point
-// sub-tile level between the tile spheres and the exact tests.  Same items, claims, plane lists
-// and tile-sphere tests; a plane near the tile sphere goes to the wave's tile ring (ring 1, the
-// current tile's near planes).  Every 64 of them (and the tile's remainder) are split: lane l
-// takes one near plane and tests it against the tile's four sub-tile spheres (LDS), and each
-// sub-tile's near planes are appended to ring 2 as (plane | sub-tile slot << 13), the run padded
-// to a multiple of K with the NaN plane kSxPad (never counts).  Every 64 K queued (plane,
-// sub-tile) pairs form one pass: lane l takes K consecutive entries -- one sub-tile, K planes --
-// reads the sub-tile's 8 points from the wave's LDS tile slots (wave-uniform or few distinct
-// ds_read_b128 addresses) and evaluates the 8 K tests in PCL's op order.  On C3's clouds the
-// sub-tile spheres leave 0.53 of the tile-level tests (CPU simulation of the Morton copy,
-// DESIGN.md 5), at the price of 4 sphere tests per tile-level pair.
-constexpr int kSxR1 = 320;                          // ring 1 entries per wave and tile (>= 63 + 256)
-constexpr int kSxR2 = 512;                          // ring 2 entries per wave (>= 64 K - 1 + 64 + K - 1)
-constexpr uint32_t kSxPad = kMaxHypPerLaunch;       // s_cf[kSxPad]: the NaN plane (padding)
-
-template <int BS, int K>
-__global__ __launch_bounds__(BS) void k_score_tiles_sx(
-    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
-    const float4* __restrict__ tiles, const float4* __restrict__ subs,
-    const uint16_t* __restrict__ lp, int ls, const int32_t* __restrict__ lp_n, int blk_cap,
-    int xcd, const HypRec* __restrict__ hyps, int D, float cthr, float margin,
-    int32_t* __restrict__ counts, unsigned long long* __restrict__ stats, PickArgs pick_args) {
-  static_assert(K == 2 || K == 4, "planes per lane");
-  static_assert(kSxR2 >= 64 * K + 64 + K - 1, "ring 2 holds a pass's backlog + one split run");
-  constexpr int kChunk = 2;  // tiles per item
-  __shared__ float4 s_cf[kMaxHypPerLaunch + 1];
-  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves: <= 65535 points per workgroup
-  __shared__ uint16_t s_r1[BS / kWave][2][kSxR1];  // one ring per tile of the item
-  __shared__ __attribute__((aligned(16))) uint32_t s_r2[BS / kWave][kSxR2];
-  __shared__ __attribute__((aligned(16))) float s_pt[BS / kWave][4 * kExSlotF];
-  __shared__ float4 s_sub[BS / kWave][4 * kTileSubs];  // the four tile slots' sub-tile spheres
-  __shared__ unsigned long long s_st[6];
-  __shared__ int s_taken;
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  for (int j = threadIdx.x; j < D; j += BS) {
-    const HypRec h = hyps[j];
-    s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
-  }
-  if (threadIdx.x == 0) {
-    s_taken = 0;
-    s_cf[kSxPad] = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
-  }
-  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += BS) s_cnt[j] = 0u;
-  if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
-  __syncthreads();
-  const int ntiles = (n + kTileP - 1) / kTileP;
-  const int nitems = (ntiles + kChunk - 1) / kChunk;
-  uint32_t* r2 = s_r2[wv];
-  float* spt = s_pt[wv];
-  float4* ssub = s_sub[wv];
-  const int ips = kSuperTiles / kChunk;
-  auto claim = [&]() -> int {  // as k_score_tiles_rl (XCD-aware or interleaved items)
-    int v = nitems;
-    if (lane == 0) {
-      const int k = atomicAdd(&s_taken, 1);
-      if (k < blk_cap) {
-        if (xcd) {
-          const int64_t l = (int64_t)k * (gridDim.x >> 3) + (blockIdx.x >> 3);
-          const int64_t s = (int64_t)(blockIdx.x & 7) + 8 * (l / ips);
-          v = (int)min((int64_t)nitems, s * ips + l % ips);
-        } else {
-          v = (int)min((int64_t)nitems, (int64_t)blockIdx.x + (int64_t)k * gridDim.x);
-        }
-      }
-    }
-    return __shfl(v, 0);
-  };
-  // lane l holds point l of an item (its two tiles), NaN past n; lanes 0-7 its sub-tile spheres
-  auto fetch = [&](int it, float& px, float& py, float& pz, float4& sb) {
-    const int64_t p = (int64_t)it * (kChunk * kTileP) + lane;
-    px = py = pz = __builtin_nanf("");
-    sb = make_float4(0.f, 0.f, 0.f, -INFINITY);
-    if (it < nitems && p < n) { px = X[p]; py = Y[p]; pz = Z[p]; }
-    const int64_t q = (int64_t)it * (kChunk * kTileSubs) + lane;
-    if (it < nitems && lane < kChunk * kTileSubs && q < (int64_t)ntiles * kTileSubs) sb = subs[q];
-  };
-  int n1[2] = {0, 0}, h1[2] = {0, 0}, n2 = 0, h2 = 0;  // ring positions (ring 1: mod kSxR1)
-  // ring 2's m (a multiple of K, <= 64 K) oldest pairs: lane l takes entries K l .. K l + K - 1
-  // (one sub-tile, K planes)
-  auto pass = [&](int m) __attribute__((always_inline)) {
-    if (stats && lane == 0) atomicAdd(&s_st[3], 1ull);
-    const bool act = lane * K < m;
-    uint32_t e[K];
-    if constexpr (K == 2) {
-      const uint2 w = act ? *reinterpret_cast<const uint2*>(r2 + ((h2 + 2 * lane) & (kSxR2 - 1)))
-                          : make_uint2(kSxPad, kSxPad);
-      e[0] = w.x; e[1] = w.y;
-    } else {
-      const uint4 w = act ? *reinterpret_cast<const uint4*>(r2 + ((h2 + 4 * lane) & (kSxR2 - 1)))
-                          : make_uint4(kSxPad, kSxPad, kSxPad, kSxPad);
-      e[0] = w.x; e[1] = w.y; e[2] = w.z; e[3] = w.w;
-    }
-    float4 cf[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) cf[k] = s_cf[e[k] & 0x1FFFu];
-    const uint32_t q = (e[0] >> 13) & 15u;  // sub-tile slot: tile slot q >> 2, sub-tile q & 3
-    const float* b = spt + (q >> 2) * kExSlotF + (q & 3u) * kSubP;
-    const float4 x0 = *reinterpret_cast<const float4*>(b);
-    const float4 x1 = *reinterpret_cast<const float4*>(b + 4);
-    const float4 y0 = *reinterpret_cast<const float4*>(b + kTileP);
-    const float4 y1 = *reinterpret_cast<const float4*>(b + kTileP + 4);
-    const float4 z0 = *reinterpret_cast<const float4*>(b + 2 * kTileP);
-    const float4 z1 = *reinterpret_cast<const float4*>(b + 2 * kTileP + 4);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float4 c = cf[k];
-      uint32_t acc = 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x0.x, y0.x, z0.x)) < cthr ? 1u : 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x0.y, y0.y, z0.y)) < cthr ? 1u : 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x0.z, y0.z, z0.z)) < cthr ? 1u : 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x0.w, y0.w, z0.w)) < cthr ? 1u : 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x1.x, y1.x, z1.x)) < cthr ? 1u : 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x1.y, y1.y, z1.y)) < cthr ? 1u : 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x1.z, y1.z, z1.z)) < cthr ? 1u : 0u;
-      acc += fabsf(pcl_dot(c.x, c.y, c.z, c.w, x1.w, y1.w, z1.w)) < cthr ? 1u : 0u;
-      const uint32_t j = e[k] & 0x1FFFu;
-      if (acc) atomicAdd(&s_cnt[j >> 1], acc << (16 * (j & 1)));  // (the pad plane counts 0)
-    }
-    h2 += m;
-  };
-  // ring 1's m (<= 64) oldest planes, all near tile slot ts: each against the tile's four
-  // sub-tile spheres; the near (plane, sub-tile) pairs go to ring 2, one K-padded run per sub-tile
-  auto split = [&](int u, int m, uint32_t ts) __attribute__((always_inline)) {
-    const bool act = lane < m;
-    const uint32_t j = act ? (uint32_t)s_r1[wv][u][(h1[u] + lane) % kSxR1] : 0u;
-    const float4 cf = s_cf[j];
-    bool nr[kTileSubs];
-#pragma unroll
-    for (int g = 0; g < kTileSubs; ++g) nr[g] = act && sphere_near(cf, ssub[ts * kTileSubs + g], margin);
-#pragma unroll
-    for (int g = 0; g < kTileSubs; ++g) {
-      const uint64_t mk = ballot(nr[g]);
-      const int c = (int)__popcll(mk);
-      const uint32_t tag = ((ts << 2) | (uint32_t)g) << 13;
-      if (nr[g]) r2[(n2 + lanes_below(mk)) & (kSxR2 - 1)] = j | tag;
-      const int pad = (K - (c & (K - 1))) & (K - 1);
-      if (lane < pad) r2[(n2 + c + lane) & (kSxR2 - 1)] = kSxPad | tag;
-      n2 += c + pad;
-      if (stats && lane == 0) atomicAdd(&s_st[0], (unsigned long long)c);
-      __builtin_amdgcn_wave_barrier();
-      while (n2 - h2 >= K * kWave) pass(K * kWave);
-    }
-    if (stats && lane == 0) atomicAdd(&s_st[4], (unsigned long long)m);
-    h1[u] += m;
-  };
-  int it_next = claim();
-  float px, py, pz;
-  float4 sbv;
-  fetch(it_next, px, py, pz, sbv);
-  for (int seq = 0;; ++seq) {
-    const int it = it_next;
-    if (it >= nitems) break;
-    it_next = claim();
-    const int t0 = it * kChunk, t_end = min(ntiles, t0 + kChunk);
-    const int sidx = t0 / kSuperTiles;  // kSuperTiles % kChunk == 0: one super-tile per item
-    const int slot0 = (seq & 1) * 2;
-    // queued pairs of the item two back use the slots about to be overwritten: score them
-    if (n2 > h2 && ((r2[h2 & (kSxR2 - 1)] >> 16) & 1u) == (uint32_t)(seq & 1)) {
-      while (n2 - h2 > 0) pass(min(n2 - h2, K * kWave));
-    }
-    const float4 tb0 = tiles[t0];
-    const float4 tb1 = t0 + 1 < t_end ? tiles[t0 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const int nlp = lp_n[sidx];
-    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
-    {
-      float* d = spt + (slot0 + (lane >> 5)) * kExSlotF + (lane & 31);
-      __builtin_amdgcn_wave_barrier();
-      d[0] = px; d[kTileP] = py; d[2 * kTileP] = pz;
-      if (lane < kChunk * kTileSubs) ssub[slot0 * kTileSubs + lane] = sbv;
-      __builtin_amdgcn_wave_barrier();
-    }
-    fetch(it_next, px, py, pz, sbv);  // the next item's points, in flight during this one
-    // the list against both tiles' spheres at once (one coefficient read per entry); a tile's
-    // near planes go to its own ring 1, split 64 at a time
-    const float tlim0 = prune_lim(margin, tb0.w);
-    const float tlim1 = t0 + 1 < t_end ? prune_lim(margin, tb1.w) : -INFINITY;
-    const uint32_t ts0 = (uint32_t)slot0, ts1 = (uint32_t)slot0 + 1u;
-    const f32x2 tax = {tb0.x, tb0.x}, tay = {tb0.y, tb0.y}, taz = {tb0.z, tb0.z};
-    const f32x2 tbx = {tb1.x, tb1.x}, tby = {tb1.y, tb1.y}, tbz = {tb1.z, tb1.z};
-#pragma unroll 1
-    for (int lb = 0; lb < nlp; lb += kListCap) {
-      const int le = min(nlp, lb + kListCap);
-      uint32_t L[kListRegs];
-#pragma unroll
-      for (int k = 0; k < kListRegs; ++k) {
-        const int e = lb + 2 * (lane + k * kWave);
-        L[k] = e < le ? lw[(lb >> 1) + lane + k * kWave] : 0u;
-        if (e + 1 >= le) L[k] &= 0xFFFFu;
-      }
-      if (stats && lane == 0) {
-        atomicAdd(&s_st[2], (unsigned long long)(t_end - t0));
-        atomicAdd(&s_st[1], (unsigned long long)((le - lb) * (t_end - t0)));
-      }
-      // four list entries per lane against both tiles
-      auto test4 = [&](uint32_t wa, uint32_t wb, int ea) {
-        const int j0 = (int)(wa & 0xFFFFu), j1 = (int)(wa >> 16);
-        const int j2 = (int)(wb & 0xFFFFu), j3 = (int)(wb >> 16);
-        const float4 c0 = s_cf[j0], c1 = s_cf[j1], c2 = s_cf[j2], c3 = s_cf[j3];
-        const f32x2 ax2 = {c0.x, c1.x}, ay2 = {c0.y, c1.y}, az2 = {c0.z, c1.z}, aw2 = {c0.w, c1.w};
-        const f32x2 bx2 = {c2.x, c3.x}, by2 = {c2.y, c3.y}, bz2 = {c2.z, c3.z}, bw2 = {c2.w, c3.w};
-        const int eb = ea + 2 * kWave;
-        const bool v0 = ea < le, v1 = ea + 1 < le, v2 = eb < le, v3 = eb + 1 < le;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const f32x2 cx = u ? tbx : tax, cy = u ? tby : tay, cz = u ? tbz : taz;
-          const float tl = u ? tlim1 : tlim0;
-          const f32x2 ha = __builtin_elementwise_fma(ax2, cx, __builtin_elementwise_fma(ay2, cy,
-                                                     __builtin_elementwise_fma(az2, cz, aw2)));
-          const f32x2 hb = __builtin_elementwise_fma(bx2, cx, __builtin_elementwise_fma(by2, cy,
-                                                     __builtin_elementwise_fma(bz2, cz, bw2)));
-          const bool q0 = v0 && fabsf(ha.x) <= tl, q1 = v1 && fabsf(ha.y) <= tl;
-          const bool q2 = v2 && fabsf(hb.x) <= tl, q3 = v3 && fabsf(hb.y) <= tl;
-          const uint64_t m0 = ballot(q0), m1 = ballot(q1), m2 = ballot(q2), m3 = ballot(q3);
-          const int k0 = (int)__popcll(m0), k1 = k0 + (int)__popcll(m1), k2 = k1 + (int)__popcll(m2);
-          uint16_t* r1 = s_r1[wv][u];
-          const int nb = n1[u];
-          if (q0) r1[(nb + lanes_below(m0)) % kSxR1] = (uint16_t)j0;
-          if (q1) r1[(nb + k0 + lanes_below(m1)) % kSxR1] = (uint16_t)j1;
-          if (q2) r1[(nb + k1 + lanes_below(m2)) % kSxR1] = (uint16_t)j2;
-          if (q3) r1[(nb + k2 + lanes_below(m3)) % kSxR1] = (uint16_t)j3;
-          n1[u] = nb + k2 + (int)__popcll(m3);
-        }
-        __builtin_amdgcn_wave_barrier();
-        while (n1[0] - h1[0] >= kWave) split(0, kWave, ts0);
-        while (n1[1] - h1[1] >= kWave) split(1, kWave, ts1);
-      };
-#pragma unroll 1
-      for (int k = 0; lb + k * 2 * kWave < le; k += 2) {
-        test4(L[0], L[1], lb + 2 * (lane + k * kWave));
-#pragma unroll
-        for (int q = 0; q + 2 < kListRegs; ++q) L[q] = L[q + 2];
-      }
-    }
-    // (ring 1 never holds another item's planes)
-    if (n1[0] > h1[0]) split(0, n1[0] - h1[0], ts0);
-    if (n1[1] > h1[1]) split(1, n1[1] - h1[1], ts1);
-  }
-  while (n2 > h2) pass(min(n2 - h2, K * kWave));
-  __syncthreads();
-  for (int j = threadIdx.x; j < D; j += BS) {
-    const int c = (int)((s_cnt[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
-    if (c) atomicAdd(&counts[j], c);
-  }
-  if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
-  if (pick_args.done) {  // the fused speculative pick, as in k_score_tiles_rl
-    __builtin_amdgcn_s_waitcnt(0);
-    __shared__ unsigned s_ticket;
-    __syncthreads();
-    if (threadIdx.x == 0)
-      s_ticket = __hip_atomic_fetch_add(pick_args.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (s_ticket != gridDim.x - 1) return;
-    if (threadIdx.x == 0)
-      __hip_atomic_store(pick_args.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pick_body<BS, true>(pick_args);
-  }
-}
-
 __global__ void k_gather_nrm(const float4* __restrict__ src, const int32_t* __restrict__ order,
                              int64_t n, float4* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1176,11 +895,10 @@ void launch_gather_order(const float4* src, const int32_t* order, int64_t n, Poi
 }
 
 void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_t n,
-                          const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s,
-                          float4* subs) {
+                          const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_sphere_bounds2, dim3((unsigned)((n + kSb2Pts - 1) / kSb2Pts)), dim3(64), 0, s,
-                     x, y, z, n, n_dev, tiles, supers, subs);
+                     x, y, z, n, n_dev, tiles, supers);
 }
 
 float prune_margin(float cthr, const float amax[3]) {
@@ -1265,13 +983,6 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     while ((per_xcd + gx / 8 - 1) / (gx / 8) > blk_cap) gx += 8;
     g = gx;
     xcd = 1;
-  }
-  if (!np && (tile_scorer == kTileScorerSub || tile_scorer == kTileScorerSubK2)) {
-    auto* ksx = tile_scorer == kTileScorerSubK2 ? k_score_tiles_sx<kBS, 2> : k_score_tiles_sx<kBS, 4>;
-    hipExtLaunchKernelGGL(ksx, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
-                          0u, v.x, v.y, v.z, (int)v.n, v.tiles, v.subs, lp, ls, lp_n, blk_cap, xcd,
-                          hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{});
-    return;
   }
   if (!np && tile_scorer != kTileScorerBf16) {
     auto* kex = tile_scorer == kTileScorerExK1 ? k_score_tiles_ex<kBS, 1>

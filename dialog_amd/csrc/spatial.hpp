@@ -28,8 +28,6 @@ namespace dlg {
 constexpr int kTileP = 32;       // points per tile (the 32 rows of one MFMA block)
 constexpr int kSuperTiles = 16;  // tiles per super-tile (a power of two <= 32)
 constexpr int kSuperP = kTileP * kSuperTiles;
-constexpr int kSubP = 8;                      // points per sub-tile (k_score_tiles_sx)
-constexpr int kTileSubs = kTileP / kSubP;     // sub-tiles per tile
 
 inline int64_t sp_tiles(int64_t n) { return (n + kTileP - 1) / kTileP; }
 inline int64_t sp_supers(int64_t n) { return (n + kSuperP - 1) / kSuperP; }
@@ -41,8 +39,6 @@ struct SpatialView {
   int64_t n;
   const float4* tiles;   // [sp_tiles(n)]  (cx, cy, cz, r): every point of the tile within r of c
   const float4* supers;  // [sp_supers(n)]
-  const float4* subs;    // [kTileSubs * sp_tiles(n)]: the 8-point sub-tiles' spheres (sub s of
-                         // tile t at kTileSubs t + s; an empty sub-tile has radius -inf)
 };
 
 // the pruning test: may the sphere sp = (c, r) hold a point that passes PCL's test for the plane
@@ -69,8 +65,7 @@ void launch_gather_order(const float4* src, const int32_t* order, int64_t n, Poi
 // tile and super-tile bounding spheres of n points; with n_dev the count is read on the device
 // (*n_dev <= n, the grid is sized for n)
 void launch_sphere_bounds(const float* x, const float* y, const float* z, int64_t n,
-                          const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s,
-                          float4* subs = nullptr);
+                          const int32_t* n_dev, float4* tiles, float4* supers, hipStream_t s);
 // margin = smallest float >= (cthr + 2 e_max)(1 + 2^-19), e_max = 64 u 2.0001 (ax + ay + az)
 float prune_margin(float cthr, const float amax[3]);
 // pruned countWithinDistance of D plane hypotheses over the spatial points (k_prune_supers +
@@ -79,14 +74,13 @@ float prune_margin(float cthr, const float amax[3]);
 // amax: the cloud's per-axis max |coordinate| (the scoring band's S bound).
 // list stride per super-tile (D rounded up to 64 entries: dword-aligned entry pairs)
 inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
-// the plane model's (tile, plane) scorer: exact PCL-order evaluation with lanes as planes over
-// 8-point sub-tiles (k_score_tiles_sx, default) or whole tiles (k_score_tiles_ex), or 32 x 32
-// bf16 matrix-core blocks with band re-decision (k_score_tiles_rl); identical counts
-constexpr int kTileScorerExact = 0;   // k_score_tiles_ex<2>
+// the plane model's (tile, plane) scorer: exact PCL-order evaluation with lanes as planes
+// (k_score_tiles_ex, default) or 32 x 32 bf16 matrix-core blocks with band re-decision
+// (k_score_tiles_rl); identical counts
+constexpr int kTileScorerExact = 0;   // k_score_tiles_ex<2> (default)
 constexpr int kTileScorerBf16 = 1;    // k_score_tiles_rl
-constexpr int kTileScorerSub = 2;     // k_score_tiles_sx<4>: 8-point sub-tiles (default)
 // A/B-only variants (same counts; tests/test_score_variants.py runs each)
-constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14, kTileScorerSubK2 = 22;
+constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14;
 // SACMODEL_NORMAL_PLANE scoring over the spatial copy: its (normalised normal, curvature) per
 // point, and the model's lambda / threshold; margin then comes from prune_margin(lim_max, amax)
 struct PrunedNp {
@@ -101,7 +95,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
                          const PickArgs* pick = nullptr,  // fused speculative pick (one rank)
                          hipEvent_t ev_start = nullptr,   // timing events of the launch pair
                          hipEvent_t ev_stop = nullptr,
-                         int tile_scorer = kTileScorerSub);
+                         int tile_scorer = kTileScorerExact);
 // the NORMAL_PLANE prefilter limit of the largest w (host restatement of np_de_limit): every
 // point's d_euclid limit is <= this when 0 <= w < 1 for all points; +inf otherwise
 float np_lim_max(double w_max, double thr);

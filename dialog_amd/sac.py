@@ -126,8 +126,8 @@ class Context:
         """The pruned scoring kernel's work counters (needs DLG_OPT_PRUNE_STATS = 1)."""
         a = (C.c_uint64 * 6)()
         self.check(self._L.dlg_prune_stats(self.h, a, int(bool(reset))))
-        return {"sub_pairs": a[0], "list_entries": a[1], "tiles": a[2], "blocks": a[3],
-                "pairs": a[4], "redecided_blocks": a[5]}
+        return {"list_entries": a[1], "tiles": a[2], "blocks": a[3], "pairs": a[4],
+                "redecided_blocks": a[5]}
 
     def set_profiling(self, on=True):
         self.check(self._L.dlg_set_profiling(self.h, int(bool(on))))

@@ -38,7 +38,8 @@ extern "C" {
  * variables.  3: dlg_extract_stats gained refit_walk_ms; dlg_float_sums, dlg_cloud_estimate_normals
  * and dlg_plane_border were added; dlg_cloud_drop_spatial keeps the copy's buffers.
  * 4: dlg_extract_stats gained refit_repair_ms (refit_walk_ms is k_fs_walk alone on every rank);
- * DLG_OPT_FS_POISON; DLG_TILE_SUB (the default tile scorer); dlg_cloud_regulate_normals */
+ * DLG_OPT_FS_POISON; dlg_cloud_regulate_normals; DLG_OPT_HYP_SHARD; the tile-scorer option's
+ * getter returns the value set */
 #define DLG_ABI_VERSION 4
 
 typedef enum {
@@ -431,29 +432,33 @@ enum {
                                the host recomputing every refit's tail from the sums; 3 as 2 and
                                every round's select redone with the host's plane (test) */
   DLG_OPT_PRUNE_TILE_SCORER = 9, /* the pruned plane scorer's (tile, plane) pairs:
-                               DLG_TILE_SUB (default) 8-point sub-tile spheres, then PCL-order f32
-                               with lanes as planes; DLG_TILE_EXACT the same over whole 32-point
-                               tiles; DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band
-                               re-decision.  (11, 14, 22: A/B-only variants of the first two with
-                               1, 4, 2 planes per lane; same counts) */
+                               DLG_TILE_EXACT (default) PCL-order f32 with lanes as planes, or
+                               DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band re-decision.
+                               (11, 14: A/B-only variants of the first with 1, 4 planes per lane;
+                               same counts; the getter returns the value set) */
   DLG_OPT_NORMALS_FUSED = 10, /* PCL-float radius normals: 1 (default) search, (d2, index) order
                                and sums in one fused pass; 0: the chunked count / fill / sort /
                                sum pipeline */
   DLG_OPT_REGULATE_WAVE = 11, /* RegulateNormal's claim pass: 1 (default) one wave per frontier
                                node over its packed candidate cells; 0: one thread per (node,
                                cell) */
-  DLG_OPT_FS_POISON = 12    /* tests only: 1 fills the PCL float-sum walk's window tables with
+  DLG_OPT_FS_POISON = 12,   /* tests only: 1 fills the PCL float-sum walk's window tables with
                                garbage entries stamped for the next launch whenever its scratch
                                is laid out, before the clear; 0 (default) */
+  DLG_OPT_HYP_SHARD = 13    /* several ranks, small clouds (SURVEY 8(e)'s fallback): 1 = every
+                               rank uploads the WHOLE cloud (id_base 0) and dlg_sac_segment /
+                               dlg_extract_planes split each batch's hypotheses over the ranks
+                               (rank r scores its slice, the counts are allreduced; the rest of
+                               the round runs on every rank alike: same results as one rank).
+                               0 (default): point sharding (each rank uploads its shard) */
 };
-enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1, DLG_TILE_SUB = 2 };
+enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
 dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);
 dlg_status dlg_ctx_get_option(const dlg_ctx* ctx, int option, int64_t* value);
 /* the pruned scoring kernel's counters since DLG_OPT_PRUNE_STATS was set (or the last reset):
- * [0] (8-point sub-tile, plane) pairs evaluated (DLG_TILE_SUB), [1] super-tile list entries tested
- * against tile spheres, [2] tiles visited, [3] 32x32 blocks (DLG_TILE_EXACT / SUB: passes)
- * scored, [4] (tile, plane) pairs near the tile sphere (scored whole except with DLG_TILE_SUB),
+ * [0] unused, [1] super-tile list entries tested against tile spheres, [2] tiles visited,
+ * [3] 32x32 blocks (DLG_TILE_EXACT: 64-lane passes) scored, [4] (tile, plane) pairs scored,
  * [5] blocks with a band re-decision (DLG_TILE_BF16 only) */
 dlg_status dlg_prune_stats(dlg_ctx* ctx, uint64_t out[6], int reset);
 

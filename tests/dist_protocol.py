@@ -26,6 +26,12 @@ infrastructure):
 
 Each rank logs (op, dtype, count) of every collective; the test checks the logs are identical
 across ranks and that the result equals the single-process restatement bit for bit.
+
+hyp_shard (DLG_OPT_HYP_SHARD, SURVEY 8(e)'s small-N fallback): every rank holds the whole cloud
+and runs the whole round; per batch of D draws rank r scores only its slice of the hypotheses
+(whole 64-hypothesis groups: groups [U r / R, U (r + 1) / R) of U = ceil(D / 64)) and the counts
+are allreduced -- the only collective:
+    allreduce-sum int32[D]        per batch
 """
 from __future__ import annotations
 
@@ -86,8 +92,14 @@ def _pcl_refit(O, xyz, coeff):
     return np.array([v[0], v[1], v[2], f(-1.0) * dot], np.float32)
 
 
+def hyp_slice(D, rank, world):
+    """driver.cpp one_batch: this rank's hypotheses [lo, hi) under DLG_OPT_HYP_SHARD"""
+    U = (D + 63) // 64
+    return min(D, 64 * (U * rank // world)), min(D, 64 * (U * (rank + 1) // world))
+
+
 def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, min_inliers,
-        max_iterations, probability, batch, sizes, refit="pcl", gather=True):
+        max_iterations, probability, batch, sizes, refit="pcl", gather=True, hyp_shard=False):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -103,21 +115,23 @@ def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, m
     cc = Coll(dist, torch)
     pts, _, _ = plane_cloud(n_points, n_planes, seed=913)   # the global cloud (host copy)
     bounds = np.concatenate([[0], np.cumsum(sizes)])
-    mine_ids = np.arange(bounds[rank], bounds[rank + 1], dtype=np.int32)
+    mine_ids = (np.arange(n_points, dtype=np.int32) if hyp_shard else
+                np.arange(bounds[rank], bounds[rank + 1], dtype=np.int32))
     local = mine_ids.copy()                                  # active global ids, list order
     prm = D.make_params(threshold, max_iterations=max_iterations, probability=probability,
                         hypotheses_per_launch=batch,
                         refit_mode=D.DLG_REFIT_FAST if refit == "fast" else D.DLG_REFIT_PCL)
     coeffs, inliers, offsets, decisions = [], [], [0], []
     floor_n = max(3, min_inliers)
-    active = cc.allgather(np.array([local.shape[0]], np.int64))[:, 0]
+    active = (np.array([local.shape[0]], np.int64) if hyp_shard else
+              cc.allgather(np.array([local.shape[0]], np.int64))[:, 0])
     qexp = None
     while len(coeffs) < max_planes:
         N = int(active.sum())
-        offset = int(active[:rank].sum())
+        offset = 0 if hyp_shard else int(active[:rank].sum())
         if N < floor_n:
             break
-        if refit == "fast" and qexp is None and world > 1:
+        if refit == "fast" and qexp is None and world > 1 and not hyp_shard:
             # the cloud's global quantum, before the first round's draws (driver.cpp segment_impl)
             fin_pts = pts[mine_ids][np.isfinite(pts[mine_ids]).all(axis=1)]
             f = float(np.abs(fin_pts).max()) if fin_pts.size else 0.0
@@ -136,17 +150,19 @@ def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, m
             g = local[pos[mine] - offset]
             rec[mine, 0] = g
             rec[mine, 1:] = pts[g].view(np.int32)
-            rec = cc.allreduce_sum(rec.reshape(-1)).reshape(Dn, 3, 4)
+            if not hyp_shard:
+                rec = cc.allreduce_sum(rec.reshape(-1)).reshape(Dn, 3, 4)
             smp = np.ascontiguousarray(rec[:, :, 1:]).view(np.float32)
             # k_build_hyps + k_score on the local shard, allreduce of the counts
             good = np.zeros(Dn, np.int32)
             cnt = np.zeros(Dn, np.int32)
             hyp = np.zeros((Dn, 4), np.float32)
+            lo, hi = hyp_slice(Dn, rank, world) if hyp_shard else (0, Dn)
             for d in range(Dn):
                 ok, c = O.plane_coefficients(smp[d, 0], smp[d, 1], smp[d, 2])
                 good[d] = int(ok)
                 hyp[d] = c
-                if ok:
+                if ok and lo <= d < hi:
                     cnt[d] = O.count_within(shard, c, threshold) if shard.shape[0] else 0
             cnt = cc.allreduce_sum(cnt)
             b, fin = ctl.consume(cnt, good)
@@ -160,7 +176,15 @@ def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, m
             break
         decisions.append((res["iterations"], res["draws"], res["n_unrefined"], res["best_draw"]))
         sel = T.within(best_coeff, shard, threshold) if shard.shape[0] else np.zeros(0, bool)
-        if refit == "pcl":
+        if hyp_shard and refit == "pcl":
+            refined = _pcl_refit(O, shard[sel], best_coeff)
+        elif hyp_shard:
+            if qexp is None:
+                fin_pts = pts[np.isfinite(pts).all(axis=1)]
+                qexp = int(np.frexp(float(np.abs(fin_pts).max()) if fin_pts.size else 0.0)[1])
+            dig = O.mom_digits(pts, local[sel], qexp) if sel.any() else np.zeros(25, np.int64)
+            refined = O.refit_digits(dig, best_coeff, qexp)
+        elif refit == "pcl":
             xyz = cc.gather_lists(shard[sel].reshape(-1).view(np.int32).copy(), 3)
             refined = _pcl_refit(O, xyz.view(np.float32).reshape(-1, 3), best_coeff)
         else:
@@ -168,11 +192,13 @@ def run(rank, world, port, out_dir, n_points, n_planes, threshold, max_planes, m
             dig = cc.allreduce_sum(dig)
             refined = O.refit_digits(dig, best_coeff, qexp)
         sel = T.within(refined, shard, threshold) if shard.shape[0] else np.zeros(0, bool)
-        rk = cc.allgather(np.array([int(sel.sum()), int((~sel).sum())], np.int32))
+        rk = (np.array([[int(sel.sum()), int((~sel).sum())]], np.int32) if hyp_shard else
+              cc.allgather(np.array([int(sel.sum()), int((~sel).sum())], np.int32)))
         n_in = int(rk[:, 0].sum())
         if n_in == 0 or n_in < min_inliers:
             break
-        ids = cc.gather_lists(local[sel].copy(), 1) if gather else local[sel].copy()
+        ids = (local[sel].copy() if (hyp_shard or not gather) else
+               cc.gather_lists(local[sel].copy(), 1))
         coeffs.append(refined)
         inliers.append(ids)
         offsets.append(offsets[-1] + n_in)

@@ -125,3 +125,47 @@ def test_control_matches_oracle_single_rank():
                         max_iterations=0, probability=1.0)
     assert ctl.next().shape[0] == 0 and not ctl.result()["has_model"] and not ref["ok"]
     assert ref["draws"] == 0
+
+
+@pytest.mark.parametrize("world,refit,batch", [(2, "pcl", 64), (3, "fast", 200), (4, "pcl", 100)],
+                         ids=["ws2-pcl", "ws3-fast", "ws4-pcl-few-groups"])
+def test_hyp_sharded_extract_gloo(tmp_path, world, refit, batch):
+    """DLG_OPT_HYP_SHARD (SURVEY 8(e)'s small-N fallback) over gloo: every rank holds the whole
+    cloud, scores its slice of each batch's hypotheses (whole 64-hypothesis groups; with fewer
+    groups than ranks some ranks score none) and the counts are allreduced -- the only
+    collective, once per batch.  Every rank's planes equal the single-process oracle's."""
+    n = 6000
+    kw = dict(n_points=n, n_planes=3, threshold=0.02, max_planes=4, min_inliers=50,
+              max_iterations=120, probability=0.99, batch=batch, sizes=[n] * world, refit=refit,
+              hyp_shard=True)
+    mp.start_processes(_entry, args=(world, _port(), str(tmp_path), kw), nprocs=world,
+                       join=True, start_method="spawn")
+    outs = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    for o in outs[1:]:
+        for k in ("coeffs", "inliers", "offsets", "decisions", "log"):
+            assert np.array_equal(o[k], outs[0][k]), k
+    log = [tuple(e.split(":")) for e in outs[0]["log"]]
+    assert log and all(e[:2] == ("allreduce_sum", "int32") and 0 < int(e[2]) <= batch for e in log)
+    from dialog_amd.synth import plane_cloud
+    pts, _, _ = plane_cloud(n, 3, seed=913)
+    ref = O.extract_planes(pts, 0.02, max_planes=4, min_inliers=50, max_iterations=120,
+                           probability=0.99, refit=refit)
+    got = outs[0]
+    assert ref["n_planes"] >= 3 and got["coeffs"].shape[0] == ref["n_planes"]
+    assert np.array_equal(got["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
+    assert np.array_equal(got["offsets"], ref["offsets"])
+    assert np.array_equal(got["inliers"], ref["inliers"])
+
+
+def test_hyp_slices_partition():
+    """The slices of driver.cpp one_batch / dist_protocol.hyp_slice partition [0, D) into whole
+    64-hypothesis groups (an exhaustive kernel's padded group stays inside its rank's slice)."""
+    from dist_protocol import hyp_slice
+    for D in (1, 63, 64, 65, 100, 511, 4096, 4000):
+        for R in (1, 2, 3, 5, 8, 16):
+            sl = [hyp_slice(D, r, R) for r in range(R)]
+            assert sl[0][0] == 0 and sl[-1][1] == D
+            for (a, b), (c, d) in zip(sl, sl[1:]):
+                assert b == c and a <= b
+            for a, b in sl:
+                assert a % 64 == 0 and (b % 64 == 0 or b == D)

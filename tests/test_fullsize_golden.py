@@ -226,3 +226,39 @@ def test_c4shape_sharded_loopback(gpu_ctx, mode):
     if os.environ.get("DLG_REPORT"):
         with open(os.environ["DLG_REPORT"], "a") as f:
             f.write(json.dumps(rep) + "\n")
+
+
+@pytest.mark.skipif("c2" not in DB, reason="fullsize.json has no c2")
+@pytest.mark.parametrize("mode", modes_of("c2"))
+def test_c2_hyp_sharded_loopback(gpu_ctx, mode):
+    """configs[1]'s 1M-point cloud on 8 ranks the way SURVEY 8(e) falls back for small N: point
+    shards would leave 125k points per rank, under the 131072-point Morton-copy cut-off, so every
+    rank holds the whole cloud (its own pruned scorer) and scores 512 of the 4096 hypotheses
+    (DLG_OPT_HYP_SHARD); the allreduced counts give the golden iterations, best sample and bits."""
+    g = DB["c2"]["modes"][mode]
+    p = cloud("c2")
+    W = 8
+    ctxs = D.Context.loopback_group(W, 0)
+    out, errs = [None] * W, []
+
+    def run(r):
+        try:
+            ctxs[r].set_option(D.DLG_OPT_HYP_SHARD, 1)
+            c = D.Cloud(ctxs[r], p)
+            out[r] = D.segment_cloud(c, params(mode), capacity=p.shape[0])
+            c.close()
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    for r in range(W):
+        inl, coeff, st = out[r]
+        assert st["iterations"] == g["iterations"] and st["draws"] == g["draws"]
+        assert [int(v) for v in st["best_sample"]] == g["best_sample"]
+        assert [int(v) for v in coeff.view(np.uint32)] == g["coeff_bits"]
+        assert inl.size == g["n_inliers"] and sha(inl) == g["inliers_sha256"]

@@ -197,6 +197,51 @@ def test_loopback_sharded_equals_single(gpu_ctx, world):
         c.close()
 
 
+@pytest.mark.parametrize("world,n,refit", [(2, 40000, "pcl"), (3, 300000, "fast"),
+                                           (5, 200000, "pcl")])
+def test_loopback_hyp_sharded_equals_oracle(gpu_ctx, world, n, refit):
+    """DLG_OPT_HYP_SHARD (SURVEY 8(e)'s small-N fallback): every in-process rank uploads the whole
+    cloud and scores its slice of each batch's hypotheses (exhaustive kernels below the Morton
+    copy's size, the pruned scorer above it), the counts are allreduced; every rank's segment()
+    and extract-and-remove equal the oracle's bit for bit."""
+    p, _, _ = plane_cloud(n, 6, seed=98 + world)
+    mode = D.DLG_REFIT_PCL if refit == "pcl" else D.DLG_REFIT_FAST
+    prm = D.make_params(0.02, max_iterations=511, probability=1.0, refit_mode=mode)
+    ref = O.extract_planes(p, 0.02, max_planes=6, min_inliers=200, max_iterations=511,
+                           probability=1.0, refit=refit)
+    seg = O.sac_segment(p, 0.02, max_iterations=99, probability=0.99)
+    prm_s = D.make_params(0.02, max_iterations=99, probability=0.99, refit_mode=D.DLG_REFIT_PCL)
+    ctxs = D.Context.loopback_group(world, 0)
+    out, sout, errs = [None] * world, [None] * world, []
+
+    def run(r):
+        try:
+            ctxs[r].set_option(D.DLG_OPT_HYP_SHARD, 1)
+            c = D.Cloud(ctxs[r], p)
+            out[r] = D.extract_planes(c, prm, max_planes=6, min_inliers=200, capacity=p.shape[0])
+            c.reset()
+            sout[r] = D.segment_cloud(c, prm_s, capacity=p.shape[0])
+            c.close()
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    for r in range(world):
+        assert out[r]["n_planes"] == ref["n_planes"] >= 4
+        assert np.array_equal(out[r]["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32))
+        assert np.array_equal(out[r]["offsets"], ref["offsets"])
+        assert np.array_equal(out[r]["inliers"], ref["inliers"])
+        inl, coeff, st = sout[r]
+        assert list(st["best_sample"]) == list(seg["best_sample"])
+        assert np.array_equal(coeff.view(np.uint32), seg["coeff"].view(np.uint32))
+        assert np.array_equal(inl, seg["inliers"])
+
+
 @pytest.mark.slow
 def test_large_cloud_properties(gpu_ctx):
     """1M-point C2 cloud: bit parity with the oracle on a bounded hypothesis budget, and

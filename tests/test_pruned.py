@@ -257,8 +257,7 @@ def test_path_options_identical(gpu_ctx, seed):
               {D.DLG_OPT_PRUNE: 0}, {D.DLG_OPT_PRUNE: 0, D.DLG_OPT_SCORE_KERNEL: D.DLG_SCORE_EXACT},
               {D.DLG_OPT_SELECT_TILE: 4096}, {D.DLG_OPT_SELECT_TILE: 8192},
               {D.DLG_OPT_SELECT_TILE: 16384},
-              {D.DLG_OPT_PRUNE_TILE_SCORER: D.DLG_TILE_BF16},
-              {D.DLG_OPT_PRUNE_TILE_SCORER: D.DLG_TILE_EXACT}]
+              {D.DLG_OPT_PRUNE_TILE_SCORER: D.DLG_TILE_BF16}]
     for opts in combos:
         ctx = D.Context(0)
         try:

@@ -13,10 +13,9 @@ import numpy as np
 import pytest
 
 VARIANTS = (0, 1, 2)  # DLG_SCORE_EXACT (PCL op order), DLG_SCORE_BF16 (matrix cores), DLG_SCORE_PRUNED
-# DLG_OPT_PRUNE_TILE_SCORER values besides the default DLG_TILE_SUB: DLG_TILE_EXACT,
-# DLG_TILE_BF16, and the A/B-only variants 11, 14 (whole tiles, 1 / 4 planes per lane) and 22
-# (sub-tiles, 2 planes per lane)
-TILE_SCORERS = (0, 1, 11, 14, 22)
+# DLG_OPT_PRUNE_TILE_SCORER values besides the default DLG_TILE_EXACT: DLG_TILE_BF16 and the
+# A/B-only variants 11, 14 (1 / 4 planes per lane)
+TILE_SCORERS = (1, 11, 14)
 
 
 def counts(ctx, cloud, D, v, thr):
@@ -62,15 +61,15 @@ def test_score_variants_bit_identical(gpu_ctx, case):
             for v in VARIANTS[1:]:
                 got = counts(gpu_ctx, cloud, nh, v, thr)
                 assert np.array_equal(got, ref), (case, nh, v, int((got != ref).sum()))
-            # the pruned path's other tile scorers: whole tiles (and its 1- and 4-plane-per-lane
-            # A/B variants), bf16 blocks + band re-decision, the sub-tile scorer's 2-plane variant
+            # the pruned path's other tile scorers: bf16 blocks + band re-decision, the exact
+            # scorer's 1- and 4-plane-per-lane A/B variants
             for ts in TILE_SCORERS:
                 gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, ts)
                 try:
                     assert gpu_ctx.get_option(D.DLG_OPT_PRUNE_TILE_SCORER) == ts
                     got = counts(gpu_ctx, cloud, nh, 2, thr)
                 finally:
-                    gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_SUB)
+                    gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_EXACT)
                 assert np.array_equal(got, ref), (case, nh, "pruned tile scorer", ts,
                                                   int((got != ref).sum()))
     finally:

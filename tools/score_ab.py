@@ -1,7 +1,7 @@
 """A/B of the scoring kernels on the GPU (one process, interleaved rounds, counts checked equal
 across kernels).  Usage: python tools/score_ab.py [n_points] [D] [rounds]
 KERNELS=0,1,2,... (DLG_SCORE_EXACT, DLG_SCORE_BF16, DLG_SCORE_PRUNED with the tile scorer of
-TILE_OPT: 2 sub-tiles (default), 3 bf16 blocks, 4 whole tiles, 5-7 A/B variants); PRUNE_STATS=1 also prints the
+TILE_OPT: 2 lanes-as-planes exact (default), 3 bf16 blocks, 5-6 A/B variants); PRUNE_STATS=1 also prints the
 pruned kernel's work counters per launch (dlg_prune_stats).  The round-1 A/B of the retired
 variants (FMA prefilters, scalar coefficients, f32 MFMA, lanes-as-planes) is recorded in
 profiles/r01_score_variants_ab.json and DESIGN.md."""
@@ -18,10 +18,10 @@ import dialog_amd as D  # noqa: E402
 from dialog_amd import _lib  # noqa: E402
 from dialog_amd.synth import SEED_BASE, plane_cloud  # noqa: E402
 
-NAMES = {0: "exact_p4", 1: "bf16_t8", 2: "pruned_sub_k4", 3: "pruned_bf16", 4: "pruned_ex_k2",
-         5: "pruned_ex_k1", 6: "pruned_ex_k4", 7: "pruned_sub_k2"}
-# DLG_OPT_PRUNE_TILE_SCORER per pruned variant (2: DLG_TILE_SUB, the default; 11, 14, 22: A/B-only)
-TILE_OPT = {2: 2, 3: 1, 4: 0, 5: 11, 6: 14, 7: 22}
+NAMES = {0: "exact_p4", 1: "bf16_t8", 2: "pruned_ex", 3: "pruned_bf16", 5: "pruned_ex_k1",
+         6: "pruned_ex_k4"}
+# DLG_OPT_PRUNE_TILE_SCORER per pruned variant (2: DLG_TILE_EXACT, the default; 11, 14: A/B-only)
+TILE_OPT = {2: 0, 3: 1, 5: 11, 6: 14}
 
 
 def main():
@@ -42,7 +42,7 @@ def main():
         for v in variants:
             ms = C.c_double()
             cnt = np.zeros(nh, np.int32)
-            ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, TILE_OPT.get(v, D.DLG_TILE_SUB))
+            ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, TILE_OPT.get(v, D.DLG_TILE_EXACT))
             ctx.check(L.dlg_score_benchmark(ctx.h, cloud.h, nh, min(v, 2), 3, 0.02, C.byref(ms),
                                             cnt.ctypes.data_as(C.POINTER(C.c_int32))))
             res[v].append(ms.value)
