@@ -48,6 +48,7 @@ DLG_OPT_NORMALS_FUSED = 10
 DLG_OPT_REGULATE_WAVE = 11
 DLG_OPT_FS_POISON = 12
 DLG_OPT_HYP_SHARD = 13
+DLG_OPT_FS_ONE_WALK = 14
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
 DLG_SCORE_EXACT = 0
@@ -92,7 +93,7 @@ class ExtractStats(C.Structure):
                 ("score_launches", C.c_int), ("score_ms", C.c_double), ("select_ms", C.c_double),
                 ("wall_ms", C.c_double), ("lean_rounds", C.c_int), ("spec_misses", C.c_int),
                 ("pcl_host_checks", C.c_int), ("refit_walk_ms", C.c_double),
-                ("refit_repair_ms", C.c_double)]
+                ("refit_repair_ms", C.c_double), ("refit_repairs", C.c_int)]
 
 
 _lib = None

@@ -7,8 +7,9 @@
 //   * allgather of per-rank totals                    (int64 per rank)
 //   * padded allgather of inlier ids / xyz            (only when inliers are gathered)
 //   * PCL float refit (DLG_REFIT_PCL): allgather of each rank's double term sums (10 doubles),
-//     then the nine float chains handed from rank to rank in list order (send/recv of 9 floats)
-//     and the last rank's sums broadcast
+//     an allgather of every rank's first-walk (ends, starts) (18 floats), then the nine float
+//     chains handed from rank to rank in list order (send/recv of 9 floats) and the last
+//     rank's sums broadcast
 // All operate in place on device buffers on the caller's stream.  RcclComm runs them over RCCL
 // (xGMI within a node); LoopbackComm runs an in-process group of ranks that share one device
 // (one host thread per rank) for single-GPU rehearsal and tests of the sharded path.

@@ -727,6 +727,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         c->fs_cap = cap;
       }
       int32_t* fs_res = reinterpret_cast<int32_t*>(c->small.p + 8);
+      int repairs = 0;
       if (lean) {
         // inliers stamped into a bitmap over pristine indices from the Morton copy's near tiles,
         // compacted in ascending pristine order = list order
@@ -753,7 +754,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         cl->ubits_dirty = false;
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
                         rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
-                        walk_ev(1), walk_ev(2), walk_ev(3));
+                        walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol, &repairs);
       } else {
         c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
         stage_wait();
@@ -761,9 +762,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
                       c->totals.p, c->inl_gid.p, c->inl_xyz.p, nullptr, c->stream);
         launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
                         c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(),
-                        walk_ev(0), walk_ev(1), walk_ev(2), walk_ev(3));
+                        walk_ev(0), walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol,
+                        &repairs);
       }
       HIPCHK(hipGetLastError());
+      if (xs) xs->refit_repairs += repairs;
     } else {
       // PCL float refit: inlier xyz in global list order -> sequential float sums on the host
       c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
@@ -1767,10 +1770,14 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
       case DLG_OPT_REGULATE_WAVE: o.bfs_wave = value != 0; break;
       case DLG_OPT_FS_POISON: o.fs_poison = value != 0; break;
       case DLG_OPT_HYP_SHARD: o.hyp_shard = value != 0; break;
+      case DLG_OPT_FS_ONE_WALK:
+        if (value < 0 || value > 2) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_ONE_WALK: 0..2");
+        o.fs_protocol = (int)value;
+        break;
       case DLG_OPT_PRUNE_TILE_SCORER:
         // (DLG_TILE_* values, and the A/B-only kernel variants kTileScorerExK1/ExK4)
         if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != kTileScorerExK1 &&
-            value != kTileScorerExK4)
+            value != kTileScorerExK4 && value != kTileScorerExPk)
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
         o.tile_scorer = (int)value;
         break;
@@ -1795,6 +1802,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_REGULATE_WAVE: *value = o.bfs_wave; break;
     case DLG_OPT_FS_POISON: *value = o.fs_poison; break;
     case DLG_OPT_HYP_SHARD: *value = o.hyp_shard; break;
+    case DLG_OPT_FS_ONE_WALK: *value = o.fs_protocol; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;
     default: return DLG_ERR_INVALID;
   }

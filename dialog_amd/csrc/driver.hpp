@@ -176,6 +176,7 @@ struct PathOptions {
   int pcl_dev = 1;
   bool hyp_shard = false;  // every rank holds the whole cloud; rank r scores its slice of each
                            // batch's hypotheses, the counts are allreduced (DLG_OPT_HYP_SHARD)
+  int fs_protocol = 0;  // several ranks: the PCL refit's protocol (DLG_OPT_FS_ONE_WALK, 0..2)
   bool fs_poison = false;  // tests only: fill the float-sum walk's window tables with garbage
                            // entries stamped for the next launch before the clear (fs_reset)
 };

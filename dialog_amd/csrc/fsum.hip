@@ -31,6 +31,19 @@
 
 #include <atomic>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#define HIPCHK_FS(expr)                                                                       \
+  do {                                                                                        \
+    const hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                                     \
+      throw std::runtime_error(std::string(#expr) + " -> " + hipGetErrorString(e_));          \
+  } while (0)
 
 namespace dlg {
 namespace {
@@ -135,15 +148,20 @@ __device__ void fs_scan_body(const FsDev& d, int64_t U, const double* base9, dou
 
 // several ranks: this rank's base = the double totals of the ranks before it (list order), the
 // global inlier count; then the unit scan from that base.  One workgroup.
+// shift (the rebase, several ranks): every chain's base moved by g2 - (the first walk's start),
+// so that the refined guesses follow the chain from the propagated guess g2
 __global__ __launch_bounds__(256) void k_fs_base(FsDev d, const double* __restrict__ gath, int rank,
                                                  int world, double* __restrict__ base9,
-                                                 int64_t* __restrict__ n_global) {
+                                                 int64_t* __restrict__ n_global,
+                                                 const float* __restrict__ gath2,
+                                                 const float* __restrict__ g2) {
   __shared__ double blk[64 * kFsChains];
   __shared__ double sb[kFsChains];
   const int t = threadIdx.x;
   if (t < kFsChains) {
     double b = 0.0;
     for (int r = 0; r < rank; ++r) b += gath[r * (kFsChains + 1) + t];
+    if (g2) b += (double)g2[t] - (double)gath2[(rank * 2 + 1) * kFsChains + t];
     sb[t] = b;
     base9[t] = b;
   }
@@ -1243,17 +1261,18 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
   return met;
 }
 
-// The walk: one wave per chain over all its windows.  from_guess (several ranks, rank r > 0):
-// the chain starts from the refined guess at the rank's first inlier instead of its exact start,
-// which only the previous rank can supply, and records every window's entry value for
-// k_fs_repair.  (Walking segments of one chain in parallel from the refined guesses at their
-// starts and repairing each from its predecessor's exact end was measured and dropped: in chains
-// whose sums hover near zero the guess at a segment start is off by many quanta of the small
-// binades there, the two walks never meet, and the repairs walked every segment a second time.)
+// The walk: one wave per chain over all its windows, from the exact start (start9, or zero) or,
+// kFwGuess (several ranks, rank r > 0), from the refined guess at the rank's first inlier; it
+// stores the start it took after the end values (sums[9 + c]) and, kFwRecord, every window's entry
+// value for k_fs_repair.  Several ranks walk twice (launch_fs_refit): a segment walked from its
+// double-prefix guess alone hovers near zero in some chains, its start is off by many quanta of
+// the small binades there, a walk from the exact start never meets it and the repairs walked
+// every segment a second time, one rank after another (round 4).
 // The last chain to finish runs the refit tail when asked.
 constexpr int kFwBS = kWave;
+constexpr int kFwGuess = 1, kFwRecord = 2;  // k_fs_walk's mode bits
 __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restrict__ start9,
-                                                   int from_guess, const float4* __restrict__ cin,
+                                                   int mode, const float4* __restrict__ cin,
                                                    float4* __restrict__ cout,
                                                    int32_t* __restrict__ res) {
   __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
@@ -1279,12 +1298,12 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   const int64_t clk0 = d.b.wst ? (int64_t)clock64() : 0;
   FsWalkCounters ct;
   float t = start9 ? start9[c] : 0.0f;
-  if (from_guess) {
-    if (NW > 0) t = fs_rec(d.b, c, 0)->g;
+  if ((mode & kFwGuess) && NW > 0) t = fs_rec(d.b, c, 0)->g;
+  if (lane == 0) d.b.sums[kFsChains + c] = t;  // (the start taken; k_fs_guess2 reads it)
+  if (mode & kFwRecord)
     fs_walk_span<false, true>(d, c, 0, NW, &t, lane, ring, tl, ct);
-  } else {
+  else
     fs_walk_span<false, false>(d, c, 0, NW, &t, lane, ring, tl, ct);
-  }
   if (d.b.wst && lane == 0) {
     int64_t* w = d.b.wst + 8 * c;
     w[0] = ct.win; w[1] = ct.pass | (ct.miss_none << 32); w[2] = ct.slow | (ct.miss_range << 32);
@@ -1333,13 +1352,34 @@ __global__ __launch_bounds__(kFwBS) void k_fs_repair(FsDev d, const float* __res
   const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
   FsWalkCounters ct;
   float t = start9[c];
+  if (lane == 0) d.b.sums[kFsChains + c] = t;
   if (NW == 0) {  // (an empty shard passes its start on)
     if (lane == 0) d.b.sums[c] = t;
     return;
   }
-  if (__float_as_uint(t) == __float_as_uint(fs_rec(d.b, c, 0)->g)) return;  // (sums: exact)
-  const bool met = fs_walk_span<true, false>(d, c, 0, NW, &t, lane, ring, tl, ct);
+  if (__float_as_uint(t) == __float_as_uint(d.b.vw[c * d.b.wcap])) return;  // (sums: exact)
+  // (recording: a later repair compares with this walk; windows left with an older walk's entry
+  // are ones both walks enter alike or lie past a meeting point -- every walk recorded there
+  // ends at the same value)
+  const bool met = fs_walk_span<true, true>(d, c, 0, NW, &t, lane, ring, tl, ct);
   if (!met && lane == 0) d.b.sums[c] = t;  // (met: the recorded walk's end is exact)
+}
+
+// several ranks, between the two walks: rank r's propagated guess.  gath2[j] holds rank j's first
+// walk (ends, then the starts it took); rank 0's walk was exact, and every chain behaves like a
+// translation over a small shift of its start, so rank j's guess moved by the rank before's
+// error-so-far:  G''_j = End_{j-1} + (G''_{j-1} - G_{j-1})  (in double, rounded each step;
+// G''_0 = G_0 = 0).  Measured on C3's inlier list in 8 shards: within 2 quanta of the exact
+// start, where the double-prefix guesses G_j were off by up to ~1400.
+__global__ void k_fs_guess2(const float* __restrict__ gath2, int rank, float* __restrict__ g2) {
+  const int c = threadIdx.x;
+  if (c >= kFsChains) return;
+  float gc = 0.0f;
+  for (int j = 1; j <= rank; ++j) {
+    const float* pj = gath2 + (j - 1) * 2 * kFsChains;
+    gc = (float)((double)pj[c] + ((double)gc - (double)pj[kFsChains + c]));
+  }
+  g2[c] = gc;
 }
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -1352,8 +1392,9 @@ size_t fs_scratch_bytes(int64_t n_cap, int world) {
   return align256(sizeof(double) * K * kFsChains) + 2 * align256(sizeof(double) * U * kFsChains) +
          align256(sizeof(FsNode) * K * kFsChains) + align256(3 * sizeof(uint4) * K * kFsChains) +
          align256(sizeof(float4) * U * kFsChains) +
-         align256(sizeof(float) * 32) +
+         align256(sizeof(float) * 64) +
          align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) +
+         align256(sizeof(float) * 2 * kFsChains * world) +
          align256(sizeof(float) * U * kFsChains) + align256(sizeof(uint2) * U * kFsChains * kFtW) +
          align256(sizeof(uint2) * U * kFsChains) + 256;
 }
@@ -1377,15 +1418,18 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   b.win = reinterpret_cast<float4*>(p);
   b.wcap = U;
   p += align256(sizeof(float4) * U * kFsChains);
-  b.sums = reinterpret_cast<float*>(p);      // [0..8] end values, [16..24] the received starts
-  b.start9 = b.sums + 16;
-  p += align256(sizeof(float) * 32);
+  b.sums = reinterpret_cast<float*>(p);  // [0..8] end values, [9..17] starts, [32..40] the
+  b.start9 = b.sums + 32;                 // received starts, [48..56] the propagated guesses
+  b.g2 = b.sums + 48;
+  p += align256(sizeof(float) * 64);
   b.tot = reinterpret_cast<double*>(p);       // [0..9] this rank's totals + count, [16..24] base
   b.base9 = b.tot + 16;
   b.n_global = reinterpret_cast<int64_t*>(b.tot + 26);
   p += align256(sizeof(double) * 32);
   b.gath = reinterpret_cast<double*>(p);      // [world][10]
   p += align256(sizeof(double) * (kFsChains + 1) * world);
+  b.gath2 = reinterpret_cast<float*>(p);      // [world][18]
+  p += align256(sizeof(float) * 2 * kFsChains * world);
   b.vw = reinterpret_cast<float*>(p);
   p += align256(sizeof(float) * U * kFsChains);
   b.wtab = reinterpret_cast<uint2*>(p);
@@ -1424,7 +1468,7 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
                      hipEvent_t ev_walk0, hipEvent_t ev_walk1, hipEvent_t ev_rep0,
-                     hipEvent_t ev_rep1) {
+                     hipEvent_t ev_rep1, int protocol, int* repairs) {
   uint32_t gen = ++s_gen;
   if (gen == 0) gen = ++s_gen;  // (0 marks a dropped table entry)
   FsDev d{px, py, pz, stride, n_dev, b, gen};
@@ -1447,26 +1491,98 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
   }
   // several ranks (the list is the ranks' segments in order): each rank's guesses start from the
   // double totals of the ranks before it, and every rank walks its shard at once -- rank 0 from
-  // the exact start, rank r > 0 from the refined guess at its first inlier.  Then the exact values
-  // are handed from rank to rank (RCCL send/recv of 9 floats): rank r repairs its walk from rank
-  // r - 1's end values (k_fs_repair: walked again only until it meets the recorded walk) and
-  // passes its exact end on; the last rank's sums are broadcast
+  // the exact start, rank r > 0 from the refined guess at its first inlier.  The (start, end)
+  // pairs are allgathered; rank r > 0 moves its base to the guess they propagate (k_fs_guess2:
+  // within a few dozen floats of the exact start, where the double totals can be ~1000 quanta
+  // off), rebuilds its records and walks again from that guess, recording its window entries.
+  // Then the exact values are handed from rank to rank (RCCL send/recv of 9 floats): rank r
+  // repairs its walk from rank r - 1's end values (k_fs_repair: walked again only until it meets
+  // the recorded walk -- after the rebase a few windows) and passes its exact end on; the last
+  // rank's sums are broadcast.  protocol 1 (round 4, A/B only): no rebase, the first walk records
+  // and the repairs start ~1000 quanta off.  protocol 2 (A/B only): parallel repair iterations
+  // with a host check instead of the hand-over chain (below).
   hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, b.tot);
   comm->allgather(b.tot, b.gath, kFsChains + 1, DType::F64, s);
-  hipLaunchKernelGGL(k_fs_base, dim3(1), dim3(256), 0, s, d, b.gath, r, W, b.base9, b.n_global);
+  hipLaunchKernelGGL(k_fs_base, dim3(1), dim3(256), 0, s, d, b.gath, r, W, b.base9, b.n_global,
+                     (const float*)nullptr, (const float*)nullptr);
   hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, b.base9);
   hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
-  hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
-                        (const float*)nullptr, r > 0 ? 1 : 0,
-                        (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
+  FsDev dw = d;  // the launch the recorded walk (and its window tables) belongs to
+  if (protocol == 1) {
+    hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
+                          (const float*)nullptr, r > 0 ? kFwGuess | kFwRecord : 0,
+                          (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
+  } else {
+    hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0,
+                          r > 0 ? nullptr : ev_walk1, 0u, d, (const float*)nullptr,
+                          r > 0 ? kFwGuess : 0, (const float4*)nullptr, (float4*)nullptr,
+                          (int32_t*)nullptr);
+    comm->allgather(b.sums, b.gath2, 2 * kFsChains, DType::I32, s);
+    if (r > 0) {
+      // the rebase: the records again, from the base moved to the propagated guess (new stamp:
+      // the first walk's window tables are stale), and the walk from that guess
+      uint32_t gen2 = ++s_gen;
+      if (gen2 == 0) gen2 = ++s_gen;
+      dw.gen = gen2;
+      hipLaunchKernelGGL(k_fs_guess2, dim3(1), dim3(kWave), 0, s, b.gath2, r, b.g2);
+      hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, dw, nullptr, b.tot);
+      hipLaunchKernelGGL(k_fs_base, dim3(1), dim3(256), 0, s, dw, b.gath, r, W, b.base9,
+                         b.n_global, (const float*)b.gath2, (const float*)b.g2);
+      hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, dw, b.base9);
+      hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, dw);
+      hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, nullptr, ev_walk1, 0u, dw,
+                            (const float*)b.g2, kFwRecord, (const float4*)nullptr,
+                            (float4*)nullptr, (int32_t*)nullptr);
+    }
+  }
+  if (protocol == 2) {
+    // every rank's (end, start): when each rank's start equals the end of the rank before (rank
+    // 0 starts exactly), every walk was exact and the last rank's end is the sum.  Otherwise
+    // each rank repairs its walk from the guess the pairs now propagate, at once (k_fs_repair
+    // from k_fs_guess2's value: the exact start wherever the rank before was exact, so every
+    // iteration extends the exact prefix of ranks by at least one), and checks again.  (A host
+    // check per iteration: one stream sync each.  Measured at C4 on 8 loopback ranks: ~5
+    // iterations a round -- chains crossing a binade inside a shard leave the propagated guess
+    // 5-40 floats off.)
+    if (ev_rep0) HIPCHK_FS(hipEventRecord(ev_rep0, s));
+    std::vector<uint32_t> h((size_t)2 * kFsChains * W);
+    for (int it = 0;; ++it) {
+      comm->allgather(b.sums, b.gath2, 2 * kFsChains, DType::I32, s);
+      HIPCHK_FS(hipMemcpyAsync(h.data(), b.gath2, 4 * h.size(), hipMemcpyDeviceToHost, s));
+      HIPCHK_FS(hipStreamSynchronize(s));
+      bool exact = true;
+      for (int q = 1; q < W && exact; ++q)
+        for (int c = 0; c < kFsChains; ++c)
+          if (h[(size_t)(2 * q + 1) * kFsChains + c] != h[(size_t)2 * (q - 1) * kFsChains + c]) {
+            exact = false;
+            break;
+          }
+      if (exact) {
+        if (repairs) *repairs = it;
+        break;
+      }
+      if (it >= W - 1) throw std::logic_error("PCL refit: rank walks did not converge");
+      if (r > 0) {
+        hipLaunchKernelGGL(k_fs_guess2, dim3(1), dim3(kWave), 0, s, b.gath2, r, b.g2);
+        hipLaunchKernelGGL(k_fs_repair, dim3(kFsChains), dim3(kFwBS), 0, s, dw,
+                           (const float*)b.g2);
+      }
+    }
+    if (ev_rep1) HIPCHK_FS(hipEventRecord(ev_rep1, s));
+    HIPCHK_FS(hipMemcpyAsync(b.sums, b.gath2 + (size_t)2 * kFsChains * (W - 1),
+                             sizeof(float) * kFsChains, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_fs_tail, dim3(1), dim3(1), 0, s, b.sums, b.n_global, cin, cout, res);
+    return;
+  }
   if (r > 0) {
     comm->recv(b.start9, kFsChains, DType::I32, r - 1, s);
     hipExtLaunchKernelGGL(k_fs_repair, dim3(kFsChains), dim3(kFwBS), 0, s, ev_rep0, ev_rep1, 0u,
-                          d, (const float*)b.start9);
+                          dw, (const float*)b.start9);
   }
   if (r < W - 1) comm->send(b.sums, kFsChains, DType::I32, r + 1, s);
   comm->broadcast(b.sums, kFsChains, DType::I32, W - 1, s);
   hipLaunchKernelGGL(k_fs_tail, dim3(1), dim3(1), 0, s, b.sums, b.n_global, cin, cout, res);
+  if (repairs) *repairs = W - 1;
 }
 
 }  // namespace dlg

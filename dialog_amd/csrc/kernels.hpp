@@ -212,8 +212,10 @@ struct FsBuffers {
   uint4* srec = nullptr;   // the records' integer-stepping tables (3 x 16 B each): srec[3 (c * cap + k) + j]
   float4* win = nullptr;   // window summaries (64 records each), chain-major: win[c * wcap + w]
   int64_t wcap = 0;        // windows per chain
-  float* sums = nullptr;   // [9] the chains' end values
+  float* sums = nullptr;   // [18] the chains' end values, then the starts the walk took
   float* start9 = nullptr; // [9] several ranks: the chains' values at this rank's first inlier
+  float* g2 = nullptr;     // [9] several ranks: the propagated guesses (k_fs_guess2)
+  float* gath2 = nullptr;  // [world][18] several ranks: every rank's first-walk sums
   double* tot = nullptr;   // [10] several ranks: this rank's double term sums + inlier count
   double* base9 = nullptr; // [9] several ranks: the totals of the ranks before this one
   int64_t* n_global = nullptr;  // several ranks: the inliers of all ranks
@@ -239,13 +241,19 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world);
 // launch's stamp, i.e. exactly what the clear must remove.
 hipError_t fs_reset(const FsBuffers& b, hipStream_t s, bool poison = false);
 class Comm;
-// ev_walk0 / ev_walk1 (optional): timing events riding k_fs_walk's dispatch; ev_rep0 / ev_rep1
-// (several ranks, rank > 0): riding k_fs_repair's
+// ev_walk0 / ev_walk1 (optional): timing events around the walks (several ranks: from the first
+// walk's dispatch to the second's end); ev_rep0 / ev_rep1 (several ranks, rank > 0): riding
+// k_fs_repair's.  protocol (several ranks, DLG_OPT_FS_ONE_WALK): 0 = walk, rebase on the
+// propagated guess, walk again, hand the exact chain ends rank to rank (repairs of a few windows);
+// 1 = round 4's: no rebase (repairs from ~1000 quanta off); 2 = as 0 with parallel repair
+// iterations and host checks instead of the hand-over (A/B and tests only).  *repairs (optional)
+// = the repair steps the round took (0 and 1: the W - 1 hops; 2: the iterations)
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm = nullptr,
                      hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr,
-                     hipEvent_t ev_rep0 = nullptr, hipEvent_t ev_rep1 = nullptr);
+                     hipEvent_t ev_rep0 = nullptr, hipEvent_t ev_rep1 = nullptr,
+                     int protocol = 0, int* repairs = nullptr);
 
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers

@@ -623,7 +623,7 @@ constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad 
                                // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
 constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
 
-template <int BS, int K>
+template <int BS, int K, bool PK = false>
 __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
     const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
@@ -711,10 +711,24 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const float4 c = cf[k];
-        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.x, ys.x, zs.x)) < cthr ? 1u : 0u;
-        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.y, ys.y, zs.y)) < cthr ? 1u : 0u;
-        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.z, ys.z, zs.z)) < cthr ? 1u : 0u;
-        acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.w, ys.w, zs.w)) < cthr ? 1u : 0u;
+        if constexpr (PK) {
+          // two points per packed op (v_pk_mul_f32 / v_pk_add_f32, the coefficient broadcast by
+          // op_sel): the same IEEE products and sums in PCL's order, 3 instead of 6 per test
+          const f32x2 A = {c.x, c.x}, B = {c.y, c.y}, C = {c.z, c.z}, Dd = {c.w, c.w};
+          const f32x2 x01 = {xs.x, xs.y}, x23 = {xs.z, xs.w}, y01 = {ys.x, ys.y};
+          const f32x2 y23 = {ys.z, ys.w}, z01 = {zs.x, zs.y}, z23 = {zs.z, zs.w};
+          const f32x2 d01 = (A * x01 + C * z01) + (B * y01 + Dd);
+          const f32x2 d23 = (A * x23 + C * z23) + (B * y23 + Dd);
+          acc[k] += fabsf(d01.x) < cthr ? 1u : 0u;
+          acc[k] += fabsf(d01.y) < cthr ? 1u : 0u;
+          acc[k] += fabsf(d23.x) < cthr ? 1u : 0u;
+          acc[k] += fabsf(d23.y) < cthr ? 1u : 0u;
+        } else {
+          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.x, ys.x, zs.x)) < cthr ? 1u : 0u;
+          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.y, ys.y, zs.y)) < cthr ? 1u : 0u;
+          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.z, ys.z, zs.z)) < cthr ? 1u : 0u;
+          acc[k] += fabsf(pcl_dot(c.x, c.y, c.z, c.w, xs.w, ys.w, zs.w)) < cthr ? 1u : 0u;
+        }
       }
     }
 #pragma unroll
@@ -745,7 +759,10 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const int sidx = t0 / kSuperTiles;  // kSuperTiles % kChunk == 0: one super-tile per item
     const int slot0 = (seq & 1) * 2;
     // queued leftovers of the item two back use the slots about to be overwritten: score them
-    if (nq > head && ((int)(ring[head & (kExRing - 1)] >> 13) & 1) == (seq & 1)) pass(nq - head);
+    // (the tag read is uniform: readfirstlane keeps head, and every pass loop, scalar)
+    if (nq > head &&
+        ((__builtin_amdgcn_readfirstlane((int)ring[head & (kExRing - 1)]) >> 13) & 1) == (seq & 1))
+      pass(nq - head);
     const float4 tb0 = tiles[t0];
     const float4 tb1 = t0 + 1 < t_end ? tiles[t0 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
     const int nlp = __builtin_amdgcn_readfirstlane(lp_n[sidx]);
@@ -986,7 +1003,9 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   }
   if (!np && tile_scorer != kTileScorerBf16) {
     auto* kex = tile_scorer == kTileScorerExK1 ? k_score_tiles_ex<kBS, 1>
-              : tile_scorer == kTileScorerExK4 ? k_score_tiles_ex<kBS, 4> : k_score_tiles_ex<kBS, 2>;
+              : tile_scorer == kTileScorerExK4 ? k_score_tiles_ex<kBS, 4>
+              : tile_scorer == kTileScorerExPk ? k_score_tiles_ex<kBS, 2, true>
+                                               : k_score_tiles_ex<kBS, 2>;
     hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
                           0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, blk_cap, xcd, hyps, D,
                           cthr, margin, counts, stats, pick ? *pick : PickArgs{});

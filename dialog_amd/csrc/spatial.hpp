@@ -81,6 +81,7 @@ constexpr int kTileScorerExact = 0;   // k_score_tiles_ex<2> (default)
 constexpr int kTileScorerBf16 = 1;    // k_score_tiles_rl
 // A/B-only variants (same counts; tests/test_score_variants.py runs each)
 constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14;
+constexpr int kTileScorerExPk = 12;  // k_score_tiles_ex<2> with packed f32 tests (A/B)
 // SACMODEL_NORMAL_PLANE scoring over the spatial copy: its (normalised normal, curvature) per
 // point, and the model's lambda / threshold; margin then comes from prune_margin(lim_max, amax)
 struct PrunedNp {

@@ -38,8 +38,8 @@ extern "C" {
  * variables.  3: dlg_extract_stats gained refit_walk_ms; dlg_float_sums, dlg_cloud_estimate_normals
  * and dlg_plane_border were added; dlg_cloud_drop_spatial keeps the copy's buffers.
  * 4: dlg_extract_stats gained refit_repair_ms (refit_walk_ms is k_fs_walk alone on every rank);
- * DLG_OPT_FS_POISON; dlg_cloud_regulate_normals; DLG_OPT_HYP_SHARD; the tile-scorer option's
- * getter returns the value set */
+ * DLG_OPT_FS_POISON; dlg_cloud_regulate_normals; DLG_OPT_HYP_SHARD; DLG_OPT_FS_ONE_WALK;
+ * dlg_extract_stats gained refit_repairs; the tile-scorer option's getter returns the value set */
 #define DLG_ABI_VERSION 4
 
 typedef enum {
@@ -118,9 +118,12 @@ typedef struct {
                                   transcendental near a float rounding boundary) */
   double refit_walk_ms;        /* of select_ms: the device PCL refit's chain walks (k_fs_walk,
                                   latency-bound sequential chains), lean rounds */
-  double refit_repair_ms;      /* several ranks, rank > 0: the device time of the PCL refit's
-                                  repair walks from the previous rank's exact chain ends
-                                  (k_fs_repair), summed over the rounds */
+  double refit_repair_ms;      /* several ranks: the PCL refit's repair phase on the stream (the
+                                  exactness checks and the repair walks, k_fs_repair), summed
+                                  over the rounds */
+  int refit_repairs;           /* several ranks: the PCL refit's repair steps summed over the
+                                  rounds (hand-over: W - 1 a round; DLG_OPT_FS_ONE_WALK 2: the
+                                  parallel repair iterations) */
 } dlg_extract_stats;
 
 void dlg_sac_params_default(dlg_sac_params* p);   /* PCL SACSegmentation defaults */
@@ -445,12 +448,19 @@ enum {
   DLG_OPT_FS_POISON = 12,   /* tests only: 1 fills the PCL float-sum walk's window tables with
                                garbage entries stamped for the next launch whenever its scratch
                                is laid out, before the clear; 0 (default) */
-  DLG_OPT_HYP_SHARD = 13    /* several ranks, small clouds (SURVEY 8(e)'s fallback): 1 = every
+  DLG_OPT_HYP_SHARD = 13,   /* several ranks, small clouds (SURVEY 8(e)'s fallback): 1 = every
                                rank uploads the WHOLE cloud (id_base 0) and dlg_sac_segment /
                                dlg_extract_planes split each batch's hypotheses over the ranks
                                (rank r scores its slice, the counts are allreduced; the rest of
                                the round runs on every rank alike: same results as one rank).
                                0 (default): point sharding (each rank uploads its shard) */
+  DLG_OPT_FS_ONE_WALK = 14  /* several ranks, PCL float refit (same sums every way): 0 (default)
+                               = walk, rebase every rank on the guess the walks propagate, walk
+                               again, then hand the exact chain ends rank to rank (each repair a
+                               few windows long); 1 = no rebase: the repairs start from the
+                               double-prefix guesses (the round-4 protocol, A/B only); 2 = 0 with
+                               parallel repair iterations and host checks instead of the
+                               hand-over (tests and A/B only) */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };

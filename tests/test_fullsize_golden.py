@@ -128,8 +128,9 @@ def test_c3_fast_two_pass_and_sharded(gpu_ctx):
         assert out[r]["stats"]["lean_rounds"] > 0  # (both shards hold a Morton copy)
 
 
-def run_sharded(p, bounds, mode, profile=False):
-    """extract_planes over in-process loopback ranks, rank r holding p[bounds[r]:bounds[r+1]]."""
+def run_sharded(p, bounds, mode, profile=False, options=()):
+    """extract_planes over in-process loopback ranks, rank r holding p[bounds[r]:bounds[r+1]]
+    (options: (option, value) pairs set on every rank's context)."""
     W = len(bounds) - 1
     ctxs = D.Context.loopback_group(W, 0)
     out, errs = [None] * W, []
@@ -138,6 +139,8 @@ def run_sharded(p, bounds, mode, profile=False):
         try:
             if profile:
                 ctxs[r].set_profiling(True)
+            for o, v in options:
+                ctxs[r].set_option(o, v)
             lo, hi = bounds[r], bounds[r + 1]
             c = D.Cloud(ctxs[r], p[lo:hi], id_base=lo)
             out[r] = D.extract_planes(c, params(mode), max_planes=20, min_inliers=500,
@@ -192,21 +195,29 @@ def test_c4shape_extract_one_gpu(gpu_ctx, mode):
     check_extract(e, DB["c4shape"]["modes"][mode])
 
 
+C4_PROTOCOLS = [(m, 0) for m in modes_of("c4shape")] + \
+    ([("pcl", 1), ("pcl", 2)] if "pcl" in modes_of("c4shape") else [])
+
+
 @pytest.mark.skipif("c4shape" not in DB, reason="fullsize.json has no c4shape")
-@pytest.mark.parametrize("mode", modes_of("c4shape"))
-def test_c4shape_sharded_loopback(gpu_ctx, mode):
+@pytest.mark.parametrize("mode,proto", C4_PROTOCOLS)
+def test_c4shape_sharded_loopback(gpu_ctx, mode, proto):
     """configs[3] as BASELINE states it: the 100M-point cloud sharded over 8 ranks (12.5M points
     each: every shard is far above the 131072-point Morton-copy cut-off, so every rank scores
     with the pruned kernel and every round is a lean round).  An in-process loopback group on one
     GPU stands in for the 8 RCCL ranks (the same driver code; host-relayed collectives).  PCL
-    mode: every rank walks its shard's nine float chains from its refined guesses at once, then
-    the exact chain values travel rank to rank through k_fs_repair (7 hops per round).  Every
-    rank's planes and inlier lists equal the one-rank oracle's bit for bit.  The per-rank walk and
-    repair device times are printed (and written to $DLG_REPORT if set)."""
+    mode (DLG_OPT_FS_ONE_WALK = proto): every rank walks its shard's nine float chains from its
+    refined guesses at once; 0: rebases on the guess the first walks propagate, walks again, and
+    the exact chain values travel rank to rank through k_fs_repair (7 hops per round, each
+    repair a few windows); 1 (round 4): no rebase, the repairs start ~1000 quanta off; 2: as 0
+    with parallel repair iterations and host checks instead of the hand-over.  Every rank's planes and inlier lists equal the one-rank oracle's bit for
+    bit.  The per-rank walk and repair device times are printed (and written to $DLG_REPORT if
+    set)."""
     p = cloud("c4shape")
     n, W = p.shape[0], 8
     b = [n * r // W for r in range(W + 1)]
-    out = run_sharded(p, b, mode, profile=True)
+    out = run_sharded(p, b, mode, profile=True,
+                      options=[(D.DLG_OPT_FS_ONE_WALK, proto)])
     g = DB["c4shape"]["modes"][mode]
     rows = []
     for r in range(W):
@@ -216,12 +227,17 @@ def test_c4shape_sharded_loopback(gpu_ctx, mode):
         rows.append(dict(rank=r, points=b[r + 1] - b[r], rounds=st["rounds"],
                          walk_ms=round(st["refit_walk_ms"], 4),
                          repair_ms=round(st["refit_repair_ms"], 4),
+                         repairs=st["refit_repairs"],
                          score_ms=round(st["score_ms"], 4), select_ms=round(st["select_ms"], 4),
                          wall_ms=round(st["wall_ms"], 2)))
     if mode == "pcl":
         assert all(rw["walk_ms"] > 0 for rw in rows)
         assert rows[0]["repair_ms"] == 0 and all(rw["repair_ms"] >= 0 for rw in rows[1:])
-    rep = dict(mode=mode, ranks=W, rows=rows)
+        # (every rank takes the same branches: the exactness checks read allgathered values)
+        assert len({rw["repairs"] for rw in rows}) == 1
+        assert rows[0]["repairs"] == (W - 1) * rows[0]["rounds"] if proto != 2 else \
+            rows[0]["repairs"] <= (W - 1) * rows[0]["rounds"]
+    rep = dict(mode=mode, proto=proto, ranks=W, rows=rows)
     print("\n" + json.dumps(rep))
     if os.environ.get("DLG_REPORT"):
         with open(os.environ["DLG_REPORT"], "a") as f:

@@ -121,10 +121,13 @@ def test_segment_pcl_three_levels(gpu_ctx):
     assert np.array_equal(inl, ref["inliers"])
 
 
-@pytest.mark.parametrize("world,lean", [(2, 1), (3, 1), (3, 0)])
-def test_extract_pcl_sharded(world, lean):
-    """The PCL refit over in-process ranks (one shard empty in one case): every rank walks its
-    segment of the list from the previous rank's end values; == the one-rank oracle."""
+@pytest.mark.parametrize("world,lean,proto", [(2, 1, 0), (3, 1, 0), (3, 0, 0), (3, 1, 1),
+                                              (3, 0, 1), (3, 1, 2), (3, 0, 2)])
+def test_extract_pcl_sharded(world, lean, proto):
+    """The PCL refit over in-process ranks (one shard empty in one case), every protocol of
+    DLG_OPT_FS_ONE_WALK: 0 = walk from the guess, rebase on the propagated guess, walk again,
+    repairs rank after rank; 1 = round 4's (no rebase); 2 = 0 with parallel repair iterations
+    and host checks.  == the one-rank oracle."""
     import threading
     rng = np.random.default_rng(70 + world + lean)
     n = int(rng.integers(300000, 500000))
@@ -141,6 +144,7 @@ def test_extract_pcl_sharded(world, lean):
     def run(r):
         try:
             ctxs[r].set_option(D.DLG_OPT_LEAN_ROUNDS, lean)
+            ctxs[r].set_option(D.DLG_OPT_FS_ONE_WALK, proto)
             c = D.Cloud(ctxs[r], p[b[r]:b[r + 1]], id_base=b[r])
             out[r] = D.extract_planes(c, D.make_params(0.02, **kw), max_planes=6, min_inliers=200,
                                       capacity=n)
@@ -155,7 +159,7 @@ def test_extract_pcl_sharded(world, lean):
         c.close()
     assert not errs, errs
     for r in range(world):
-        check(out[r], ref, (world, lean, r))
+        check(out[r], ref, (world, lean, proto, r))
 
 
 def test_normal_plane_pcl_refit_device():
