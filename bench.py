@@ -389,6 +389,9 @@ def main():
             "passes_per_launch": round(st["blocks"] / nl),
             "pass_fill": round(st["pairs"] / max(128.0 * st["blocks"], 1.0), 4),
             "tile_list_entries_per_launch": round(st["list_entries"] / nl),
+            # load balance: the workgroups' mean span against the longest one (100 MHz ticks)
+            "workgroup_span_us_mean": round(st["wg_ticks_sum"] / max(st["workgroups"], 1) / 100.0, 2),
+            "workgroup_span_us_max": round(st["wg_ticks_max"] / 100.0, 2),
             "evaluated_tests_per_step": int(32 * st["pairs"] * world),
             "note": "(tile, plane) pairs the bounding spheres could not rule out, each evaluated "
                     "as 32 exact PCL-order point tests (k_score_tiles_ex: lanes as planes, two "

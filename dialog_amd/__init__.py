@@ -18,7 +18,7 @@ from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, LIB_PATH  # noqa: F401
 from ._lib import (DLG_OPT_LEAN_ROUNDS, DLG_OPT_PCL_REFIT_DEVICE, DLG_OPT_PRUNE,  # noqa: F401
                    DLG_OPT_NORMALS_FUSED, DLG_OPT_PRUNE_NP, DLG_OPT_PRUNE_TILE_SCORER, DLG_TILE_BF16, DLG_TILE_EXACT,
                    DLG_OPT_PRUNE_STATS, DLG_OPT_SCORE_KERNEL, DLG_OPT_SELECT_TILE,
-                   DLG_OPT_REGULATE_WAVE, DLG_OPT_SPEC_PICK, DLG_OPT_FS_POISON, DLG_OPT_HYP_SHARD, DLG_OPT_FS_ONE_WALK, DLG_SCORE_BF16,
+                   DLG_OPT_REGULATE_WAVE, DLG_OPT_SPEC_PICK, DLG_OPT_FS_POISON, DLG_OPT_HYP_SHARD, DLG_OPT_FS_ONE_WALK, DLG_OPT_FS_SEGMENTS, DLG_SCORE_BF16,
                    DLG_SCORE_EXACT, DLG_SCORE_PRUNED)
 
 __all__ = ["Context", "Cloud", "SACSegmentation", "extract_planes", "segment_cloud", "make_params",

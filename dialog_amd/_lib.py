@@ -49,6 +49,7 @@ DLG_OPT_REGULATE_WAVE = 11
 DLG_OPT_FS_POISON = 12
 DLG_OPT_HYP_SHARD = 13
 DLG_OPT_FS_ONE_WALK = 14
+DLG_OPT_FS_SEGMENTS = 15
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
 DLG_SCORE_EXACT = 0

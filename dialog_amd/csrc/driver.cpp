@@ -268,6 +268,14 @@ struct SegOut {
 constexpr int64_t kPruneMinPoints = 131072;
 
 // the pruned kernel's work counters (DLG_OPT_PRUNE_STATS), accumulated over its launches
+// the list lengths + the scorers' work area (spatial.hpp); a new allocation starts with zeroed
+// counters (afterwards the scorer's last workgroup leaves them zero)
+void ensure_prune_work(dlg_ctx* c, int64_t ns) {
+  int32_t* old = c->lp_n.p;
+  c->lp_n.ensure((size_t)prune_work_words(ns));
+  if (c->lp_n.p != old) HIPCHK(hipMemsetAsync(c->lp_n.p, 0, sizeof(int32_t) * c->lp_n.cap, c->stream));
+}
+
 unsigned long long* prune_stats_ptr(dlg_ctx* c) {
   return c->opt.prune_stats ? c->pstats.p : nullptr;
 }
@@ -547,19 +555,19 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     }
     if (pruned_np) {
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
-      c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
+      ensure_prune_work(c, sp_supers(cl->sp_n));
       const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold};
       launch_score_pruned(spatial_view(cl), hyps_s, Ds, cthr, pmargin, cl->amax, counts_s,
-                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), &npp,
+                          c->lp.p, c->lp_n.p + kPwHeader, c->num_cus, c->stream, prune_stats_ptr(c), &npp,
                           fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
                           ext_ev ? c->ev[1] : nullptr);
     } else if (np) {
       if (Ds > 0) launch_score_np(src, hyps_s, Ds, mt, counts_s, c->num_cus, c->stream);
     } else if (pruned) {
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
-      c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
+      ensure_prune_work(c, sp_supers(cl->sp_n));
       launch_score_pruned(spatial_view(cl), hyps_s, Ds, cthr, pmargin, cl->amax, counts_s,
-                          c->lp.p, c->lp_n.p, c->num_cus, c->stream, prune_stats_ptr(c), nullptr,
+                          c->lp.p, c->lp_n.p + kPwHeader, c->num_cus, c->stream, prune_stats_ptr(c), nullptr,
                           fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
                           ext_ev ? c->ev[1] : nullptr, c->opt.tile_scorer);
     } else if (Ds > 0) {
@@ -754,7 +762,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         cl->ubits_dirty = false;
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
                         rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
-                        walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol, &repairs);
+                        walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol, &repairs, c->opt.fs_segments);
       } else {
         c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
         stage_wait();
@@ -763,7 +771,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
                         c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(),
                         walk_ev(0), walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol,
-                        &repairs);
+                        &repairs, c->opt.fs_segments);
       }
       HIPCHK(hipGetLastError());
       if (xs) xs->refit_repairs += repairs;
@@ -889,18 +897,23 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     HIPCHK(hipGetLastError());
     spec_pending = false;
     if (lean) {
-      // the list from the stamps (ids in list order; survivors' pristine indices), then the
-      // sphere bounds of the Morton survivors (count in totals[4])
-      stage_wait();
-      launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv,
-                       cl->gid_ident ? nullptr : cl->pristine.gid.p, cl->id_base, c->sel1,
-                       c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream, c->opt.sel1_tile);
+      // the sphere bounds of the Morton survivors (count in totals[4]) on the side stream, beside
+      // the list from the stamps (ids in list order; survivors' pristine indices): independent
+      // passes over different buffers
       const int b = cl->sp_spare();
       SoA& sd = cl->sp_buf[b];
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
       cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+      HIPCHK(hipEventRecord(c->ev_fork, c->stream));
+      HIPCHK(hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
       launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
-                           cl->sp_sb[b].p, c->stream);
+                           cl->sp_sb[b].p, c->sstream);
+      HIPCHK(hipEventRecord(c->ev_join, c->sstream));
+      stage_wait();
+      launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv,
+                       cl->gid_ident ? nullptr : cl->pristine.gid.p, cl->id_base, c->sel1,
+                       c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream, c->opt.sel1_tile);
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
       stage_wait();
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
@@ -1105,7 +1118,10 @@ dlg_status init_ctx(dlg_ctx* c, int device) {
   return guarded(c, [&] {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_inl, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
   });
 }
@@ -1315,6 +1331,12 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
     (void)hipStreamSynchronize(c->cstream);
     (void)hipStreamDestroy(c->cstream);
   }
+  if (c->sstream) {
+    (void)hipStreamSynchronize(c->sstream);
+    (void)hipStreamDestroy(c->sstream);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (auto& pr : c->ev_sel)
     for (auto& ev : pr)
       if (ev) (void)hipEventDestroy(ev);
@@ -1664,7 +1686,8 @@ dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float c
       if (walk_stats) HIPCHK(hipMemsetAsync(wst.p, 0, 72 * 8, c->stream));  // (the last call's)
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
       launch_fs_refit(dx.p, dx.p + 1, dx.p + 2, 3, dn.p, std::max<int64_t>(n, 1), b, dc.p,
-                      dc.p + 1, dres.p, c->num_cus, c->stream);
+                      dc.p + 1, dres.p, c->num_cus, c->stream, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, 0, nullptr, c->opt.fs_segments);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev[1], c->stream));
       sync(c);
@@ -1712,10 +1735,10 @@ dlg_status dlg_score_benchmark(dlg_ctx* c, dlg_cloud* cl, int D, int kernel, int
       if (variant == kScorePruned) {
         if (!cl->sp_valid) throw DlgError(DLG_ERR_INVALID, "cloud has no spatial copy");
         c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
-        c->lp_n.ensure((size_t)sp_supers(cl->sp_n) + 1);
+        ensure_prune_work(c, sp_supers(cl->sp_n));
         unsigned long long* stp = prune_stats_ptr(c);
         launch_score_pruned(spatial_view(cl), c->hyps.p, D, cthr, prune_margin(cthr, cl->amax),
-                            cl->amax, c->res.p, c->lp.p, c->lp_n.p, c->num_cus, c->stream, stp,
+                            cl->amax, c->res.p, c->lp.p, c->lp_n.p + kPwHeader, c->num_cus, c->stream, stp,
                             nullptr, nullptr, nullptr, nullptr, c->opt.tile_scorer);
       } else {
         launch_score(src, c->hyps.p, D, cthr, c->res.p, variant, c->num_cus, c->stream);
@@ -1770,6 +1793,10 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
       case DLG_OPT_REGULATE_WAVE: o.bfs_wave = value != 0; break;
       case DLG_OPT_FS_POISON: o.fs_poison = value != 0; break;
       case DLG_OPT_HYP_SHARD: o.hyp_shard = value != 0; break;
+      case DLG_OPT_FS_SEGMENTS:
+        if (value < 1 || value > kFsSegMax) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_SEGMENTS: 1..16");
+        o.fs_segments = (int)value;
+        break;
       case DLG_OPT_FS_ONE_WALK:
         if (value < 0 || value > 2) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_ONE_WALK: 0..2");
         o.fs_protocol = (int)value;
@@ -1803,18 +1830,19 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_FS_POISON: *value = o.fs_poison; break;
     case DLG_OPT_HYP_SHARD: *value = o.hyp_shard; break;
     case DLG_OPT_FS_ONE_WALK: *value = o.fs_protocol; break;
+    case DLG_OPT_FS_SEGMENTS: *value = o.fs_segments; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;
     default: return DLG_ERR_INVALID;
   }
   return DLG_OK;
 }
 
-dlg_status dlg_prune_stats(dlg_ctx* c, uint64_t out[6], int reset) {
+dlg_status dlg_prune_stats(dlg_ctx* c, uint64_t out[8], int reset) {
   if (!c || !out) return DLG_ERR_INVALID;
   return guarded(c, [&] {
-    std::memset(out, 0, 6 * sizeof(uint64_t));
+    std::memset(out, 0, 8 * sizeof(uint64_t));
     if (!c->opt.prune_stats) return;
-    HIPCHK(hipMemcpyAsync(out, c->pstats.p, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out, c->pstats.p, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     if (reset) HIPCHK(hipMemsetAsync(c->pstats.p, 0, 8 * sizeof(unsigned long long), c->stream));
     sync(c);
   });

@@ -177,6 +177,7 @@ struct PathOptions {
   bool hyp_shard = false;  // every rank holds the whole cloud; rank r scores its slice of each
                            // batch's hypotheses, the counts are allreduced (DLG_OPT_HYP_SHARD)
   int fs_protocol = 0;  // several ranks: the PCL refit's protocol (DLG_OPT_FS_ONE_WALK, 0..2)
+  int fs_segments = 8;  // one rank: walkers per float chain (DLG_OPT_FS_SEGMENTS)
   bool fs_poison = false;  // tests only: fill the float-sum walk's window tables with garbage
                            // entries stamped for the next launch before the clear (fs_reset)
 };
@@ -231,6 +232,10 @@ struct dlg_ctx {
   // the deferred inlier copy runs on its own stream, off the rounds' critical path: it waits for
   // ev_inl (the round's select on the main stream); the next select waits for ev_stage
   hipStream_t cstream = nullptr;
+  // lean rounds: the survivors' sphere bounds run on sstream beside the list pass (forked and
+  // joined by ev_fork / ev_join on the main stream)
+  hipStream_t sstream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_inl = nullptr;
   hipEvent_t ev_inl_cur = nullptr;    // the marker the copy waits for (ev_inl, or the round's
                                       // end-of-select timing event when profiling)

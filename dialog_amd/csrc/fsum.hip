@@ -1271,6 +1271,26 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
 // The last chain to finish runs the refit tail when asked.
 constexpr int kFwBS = kWave;
 constexpr int kFwGuess = 1, kFwRecord = 2;  // k_fs_walk's mode bits
+constexpr int kFwSegShift = 8;               // mode >> kFwSegShift: segments per chain (> 1)
+// segments a chain's NW windows are walked in (at most S, at least kFsSegWin windows each)
+__device__ __forceinline__ int fs_seg_count(int64_t NW, int S) {
+  const int64_t m = NW / kFsSegWin;
+  return (int)(m < 1 ? 1 : m < S ? m : S);
+}
+__device__ void fs_walk_finish(const FsDev& d, int c, float t, int lane, int64_t n,
+                               const float4* __restrict__ cin, float4* __restrict__ cout,
+                               int32_t* __restrict__ res);
+__device__ __forceinline__ void fs_put_counters(const FsDev& d, int c, const FsWalkCounters& ct,
+                                                int64_t clk0, bool add) {
+  int64_t* w = d.b.wst + 8 * c;
+  const int64_t v[8] = {ct.win, ct.pass | (ct.miss_none << 32), ct.slow | (ct.miss_range << 32),
+                        ct.step | (ct.lead_hist << 24), ct.rerun | (ct.miss_mask << 32),
+                        (int64_t)clock64() - clk0, ct.clk_step, ct.group_fast + (ct.table << 32)};
+  for (int k = 0; k < 8; ++k) {
+    if (add) atomicAdd(reinterpret_cast<unsigned long long*>(w + k), (unsigned long long)v[k]);
+    else w[k] = v[k];
+  }
+}
 __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restrict__ start9,
                                                    int mode, const float4* __restrict__ cin,
                                                    float4* __restrict__ cout,
@@ -1279,15 +1299,19 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   __shared__ uint64_t tl_raw[kFtLdsWords];
   auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
   auto* tl = (__attribute__((address_space(3))) uint64_t*)tl_raw;
-  const int c = blockIdx.x, lane = threadIdx.x;
+  const int S = mode >> kFwSegShift;  // (segmented walk: S segments per chain)
+  const bool segmented = S > 1;
+  const int nwalk = kFsChains * (segmented ? S : 1);
+  const int c = (int)blockIdx.x % kFsChains, sg = (int)blockIdx.x / kFsChains;
+  const int lane = threadIdx.x;
   const int64_t n = *d.n_dev;
   const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
-  if (c >= kFsChains) {
+  if ((int)blockIdx.x >= nwalk) {
     // a table builder: (window, chain) items in window order, so the walkers find the early
     // windows' tables first
     FsTabLds& L_ = *reinterpret_cast<FsTabLds*>(ring_raw);
     static_assert(sizeof(FsTabLds) <= 2 * kFsSlotBytes, "builder state fits the ring's LDS");
-    for (int64_t it = c - kFsChains; it < NW * kFsChains * kFtHalves; it += gridDim.x - kFsChains)
+    for (int64_t it = blockIdx.x - nwalk; it < NW * kFsChains * kFtHalves; it += gridDim.x - nwalk)
       fs_wtab_item(d, (int)(it % kFsChains), it / (kFsChains * kFtHalves),
                    (int)((it / kFsChains) % kFtHalves), lane, L_);
     return;
@@ -1298,18 +1322,39 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
   const int64_t clk0 = d.b.wst ? (int64_t)clock64() : 0;
   FsWalkCounters ct;
   float t = start9 ? start9[c] : 0.0f;
-  if ((mode & kFwGuess) && NW > 0) t = fs_rec(d.b, c, 0)->g;
-  if (lane == 0) d.b.sums[kFsChains + c] = t;  // (the start taken; k_fs_guess2 reads it)
-  if (mode & kFwRecord)
-    fs_walk_span<false, true>(d, c, 0, NW, &t, lane, ring, tl, ct);
-  else
-    fs_walk_span<false, false>(d, c, 0, NW, &t, lane, ring, tl, ct);
-  if (d.b.wst && lane == 0) {
-    int64_t* w = d.b.wst + 8 * c;
-    w[0] = ct.win; w[1] = ct.pass | (ct.miss_none << 32); w[2] = ct.slow | (ct.miss_range << 32);
-    w[3] = ct.step | (ct.lead_hist << 24); w[4] = ct.rerun | (ct.miss_mask << 32);
-    w[5] = (int64_t)clock64() - clk0; w[6] = ct.clk_step; w[7] = ct.group_fast + (ct.table << 32);
+  float t0 = t;
+  if (segmented) {
+    // segment sg of the chain's windows, from the refined guess at its first record (segment 0:
+    // the exact start), recording the windows' entries for k_fs_segfix
+    const int Se = fs_seg_count(NW, S);
+    if (sg >= Se) return;
+    const int64_t w_lo = NW * sg / Se, w_hi = NW * (sg + 1) / Se;
+    if (sg > 0) t = fs_rec(d.b, c, w_lo * kWave)->g;
+    t0 = t;
+    fs_walk_span<false, true>(d, c, w_lo, w_hi, &t, lane, ring, tl, ct);
+  } else {
+    if ((mode & kFwGuess) && NW > 0) t = fs_rec(d.b, c, 0)->g;
+    if (lane == 0) d.b.sums[kFsChains + c] = t;  // (the start taken; k_fs_guess2 reads it)
+    if (mode & kFwRecord)
+      fs_walk_span<false, true>(d, c, 0, NW, &t, lane, ring, tl, ct);
+    else
+      fs_walk_span<false, false>(d, c, 0, NW, &t, lane, ring, tl, ct);
   }
+  if (d.b.wst && lane == 0) fs_put_counters(d, c, ct, clk0, segmented);
+  if (segmented) {
+    if (lane == 0) {
+      d.b.seg[(c * kFsSegMax + sg) * 2] = t0;
+      d.b.seg[(c * kFsSegMax + sg) * 2 + 1] = t;
+    }
+    return;
+  }
+  fs_walk_finish(d, c, t, lane, n, cin, cout, res);
+}
+
+// the chain's end value into sums; with cout, the last chain to finish runs the refit tail
+__device__ void fs_walk_finish(const FsDev& d, int c, float t, int lane, int64_t n,
+                               const float4* __restrict__ cin, float4* __restrict__ cout,
+                               int32_t* __restrict__ res) {
   __shared__ unsigned s_ticket;
   if (lane == 0) {
     __hip_atomic_store(reinterpret_cast<int32_t*>(d.b.sums) + c, __float_as_int(t),
@@ -1382,6 +1427,39 @@ __global__ void k_fs_guess2(const float* __restrict__ gath2, int rank, float* __
   g2[c] = gc;
 }
 
+// one rank, segmented walk: chain c's segments joined in order.  Segment 0 started exactly; a
+// later segment whose recorded start equals the exact end of the one before was exact itself,
+// else it is walked again from that end until it meets its recorded walk (k_fs_repair's rule).
+// Then as k_fs_walk's end: sums, and the last chain to finish runs the refit tail.
+__global__ __launch_bounds__(kFwBS) void k_fs_segfix(FsDev d, const float* __restrict__ start9,
+                                                     int S, const float4* __restrict__ cin,
+                                                     float4* __restrict__ cout,
+                                                     int32_t* __restrict__ res) {
+  __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
+  __shared__ uint64_t tl_raw[kFtLdsWords];
+  auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
+  auto* tl = (__attribute__((address_space(3))) uint64_t*)tl_raw;
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int64_t n = *d.n_dev;
+  const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
+  const float* sg = d.b.seg + c * kFsSegMax * 2;
+  float t = start9 ? start9[c] : 0.0f;
+  if (NW > 0) {
+    const int Se = fs_seg_count(NW, S);
+    t = sg[1];
+    FsWalkCounters ct;
+    for (int s = 1; s < Se; ++s) {
+      const float s0 = sg[2 * s], e0 = sg[2 * s + 1];
+      if (__float_as_uint(t) != __float_as_uint(s0)) {
+        const int64_t w_lo = NW * s / Se, w_hi = NW * (s + 1) / Se;
+        if (!fs_walk_span<true, false>(d, c, w_lo, w_hi, &t, lane, ring, tl, ct)) continue;
+      }
+      t = e0;
+    }
+  }
+  fs_walk_finish(d, c, t, lane, n, cin, cout, res);
+}
+
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -1395,6 +1473,7 @@ size_t fs_scratch_bytes(int64_t n_cap, int world) {
          align256(sizeof(float) * 64) +
          align256(sizeof(double) * 32) + align256(sizeof(double) * (kFsChains + 1) * world) +
          align256(sizeof(float) * 2 * kFsChains * world) +
+         align256(sizeof(float) * 2 * kFsChains * kFsSegMax) +
          align256(sizeof(float) * U * kFsChains) + align256(sizeof(uint2) * U * kFsChains * kFtW) +
          align256(sizeof(uint2) * U * kFsChains) + 256;
 }
@@ -1430,6 +1509,8 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   p += align256(sizeof(double) * (kFsChains + 1) * world);
   b.gath2 = reinterpret_cast<float*>(p);      // [world][18]
   p += align256(sizeof(float) * 2 * kFsChains * world);
+  b.seg = reinterpret_cast<float*>(p);        // [9][kFsSegMax][2]
+  p += align256(sizeof(float) * 2 * kFsChains * kFsSegMax);
   b.vw = reinterpret_cast<float*>(p);
   p += align256(sizeof(float) * U * kFsChains);
   b.wtab = reinterpret_cast<uint2*>(p);
@@ -1468,7 +1549,7 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
                      hipEvent_t ev_walk0, hipEvent_t ev_walk1, hipEvent_t ev_rep0,
-                     hipEvent_t ev_rep1, int protocol, int* repairs) {
+                     hipEvent_t ev_rep1, int protocol, int* repairs, int segments) {
   uint32_t gen = ++s_gen;
   if (gen == 0) gen = ++s_gen;  // (0 marks a dropped table entry)
   FsDev d{px, py, pz, stride, n_dev, b, gen};
@@ -1485,6 +1566,16 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
     hipLaunchKernelGGL(k_fs_prep, dim3(gp), dim3(kFpBS), 0, s, d, nullptr, nullptr);
     hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, d, nullptr);
     hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
+    const int S = std::min(std::max(segments, 1), kFsSegMax);
+    if (S > 1) {
+      // segmented: kFsChains x S walkers (+ the table builders), then the joins
+      hipExtLaunchKernelGGL(k_fs_walk, dim3(gw + kFsChains * (S - 1)), dim3(kFwBS), 0, s, ev_walk0,
+                            nullptr, 0u, d, (const float*)nullptr, S << kFwSegShift,
+                            (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
+      hipExtLaunchKernelGGL(k_fs_segfix, dim3(kFsChains), dim3(kFwBS), 0, s, nullptr, ev_walk1, 0u,
+                            d, (const float*)nullptr, S, cin, cout, res);
+      return;
+    }
     hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
                           nullptr, 0, cin, cout, res);
     return;

@@ -203,6 +203,10 @@ void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1St
 // res (16 int32): [0] = 1 when a transcendental of eigen33 could not be rounded for certain
 // (the host then recomputes the plane from the sums), [1] = n, [2..10] = the nine sums' bits.
 struct FsNode;
+// one rank: the float-sum walk splits each chain into at most kFsSegMax segments of at least
+// kFsSegWin windows (64 records each), walked at once from the refined guesses and joined by
+// k_fs_segfix (segments = 1: one walker per chain)
+constexpr int kFsSegMax = 16, kFsSegWin = 8;
 struct FsBuffers {
   double* csum = nullptr;  // [chunks][9] double sums of the terms
   double* usum = nullptr;  // [units][9]
@@ -216,6 +220,7 @@ struct FsBuffers {
   float* start9 = nullptr; // [9] several ranks: the chains' values at this rank's first inlier
   float* g2 = nullptr;     // [9] several ranks: the propagated guesses (k_fs_guess2)
   float* gath2 = nullptr;  // [world][18] several ranks: every rank's first-walk sums
+  float* seg = nullptr;    // [9][kFsSegMax][2] one rank, segmented walk: each segment's start, end
   double* tot = nullptr;   // [10] several ranks: this rank's double term sums + inlier count
   double* base9 = nullptr; // [9] several ranks: the totals of the ranks before this one
   int64_t* n_global = nullptr;  // several ranks: the inliers of all ranks
@@ -247,13 +252,14 @@ class Comm;
 // propagated guess, walk again, hand the exact chain ends rank to rank (repairs of a few windows);
 // 1 = round 4's: no rebase (repairs from ~1000 quanta off); 2 = as 0 with parallel repair
 // iterations and host checks instead of the hand-over (A/B and tests only).  *repairs (optional)
-// = the repair steps the round took (0 and 1: the W - 1 hops; 2: the iterations)
+// = the repair steps the round took (0 and 1: the W - 1 hops; 2: the iterations).  segments (one
+// rank): walkers per chain (1..kFsSegMax; see kFsSegMax)
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm = nullptr,
                      hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr,
                      hipEvent_t ev_rep0 = nullptr, hipEvent_t ev_rep1 = nullptr,
-                     int protocol = 0, int* repairs = nullptr);
+                     int protocol = 0, int* repairs = nullptr, int segments = 1);
 
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers

@@ -714,28 +714,36 @@ __device__ __forceinline__ void nbr_order_stage(uint32_t* buf, int cnt,
     tie |= e + 1 < cnt && (v[j] >> 32) == (w >> 32);
   }
   if (__ballot(tie)) {
+    // in registers: the entries re-sorted by (their equal-d2 run's first entry, original index,
+    // entry) -- 10 + 32 + 10 bits -- and the entry index then finds each one's (d2, sorted
+    // position) key, parked in LDS by entry
+    static_assert(E <= 16, "entry indices fit 10 bits");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int j = 0; j < E; ++j) lds_set_key(buf, lane + 64 * j, v[j]);
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {  // insertion sort by (d2, original index): equal-d2 runs move only
-      for (int e = 1; e < cnt; ++e) {
-        const uint64_t kv = lds_key(buf, e);
-        const int id = sidx[(uint32_t)kv];
-        int f = e - 1;
-        while (f >= 0 && (lds_key(buf, f) >> 32) == (kv >> 32) &&
-               sidx[(uint32_t)lds_key(buf, f)] > id) {
-          lds_set_key(buf, f + 1, lds_key(buf, f));
-          --f;
-        }
-        lds_set_key(buf, f + 1, kv);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
+    uint64_t nk[E];
+    int carry = 0;
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       const int e = lane + 64 * j;
-      v[j] = e < cnt ? lds_key(buf, e) : ~0ull;
+      const uint64_t prev = e > 0 ? lds_key(buf, e - 1) : ~0ull;
+      int rs = (e == 0 || (prev >> 32) != (v[j] >> 32)) ? e : 0;  // (a run starts here)
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {  // inclusive max-scan over the lanes: the run's start
+        const int t = __shfl_up(rs, o, 64);
+        if (lane >= o) rs = max(rs, t);
+      }
+      rs = max(rs, carry);
+      carry = __shfl(rs, 63, 64);
+      const uint32_t oi = e < cnt ? (uint32_t)sidx[(uint32_t)v[j]] : 0u;
+      nk[j] = e < cnt ? ((uint64_t)rs << 42) | ((uint64_t)oi << 10) | (uint64_t)e : ~0ull;
+    }
+    wave_bitonic<E>(nk);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int e = lane + 64 * j;
+      v[j] = e < cnt ? lds_key(buf, (int)(nk[j] & 1023u)) : ~0ull;
     }
   }
   float x[E], y[E], z[E];
@@ -1067,6 +1075,9 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     // from level 0: above it the sparse queries are volume-like outliers, many of which level
     // l + 1 resolves, and a query scanned a level too coarse costs ~4x the candidates)
     if (L0 && cnt > 0 && cnt * 4 < K && l + 2 < L.levels - 1) jump = 2;
+    // (level 0, no candidate at all: volume-like outliers, which C5's clouds resolve three levels
+    // up -- the levels between would scan them only to defer them again)
+    if (L0 && cnt == 0 && l + 3 < L.levels - 1) jump = 3;
     if (!defer) {
       const int m = cnt < K ? cnt : K;
       if constexpr (PCLF) {
@@ -1095,6 +1106,119 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
   }
   else normals[qi] = PCLF ? finish_normal_pcl(nullptr, 0, qx, qy, qz, vpx, vpy, vpz)
                           : finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+}
+
+// The deferred levels (l > 0: mostly outliers, whose coarse cells can hold a plane's thousands of
+// points): one WAVE per query instead of one lane.  The 27 cells are visited in k_normals_knn's
+// order with its bounds; lanes take a cell's candidates 64 at a time (coalesced loads), and the
+// admitted ones -- d2 < the level's radius and (d2, index) below the current K-th -- are merged
+// into the wave's best keys (d2 bits << 32 | original index, lane j = the j-th) by a 128-key
+// bitonic sort.  Same counts, same (d2, index) order, same K-th bound for skipping cells, so the
+// same neighbour lists, deferrals and sums as the one-lane scan, whose wave waited for the lane
+// with the densest cells.
+template <int KP, bool PCLF>
+__global__ __launch_bounds__(kBS) void k_normals_knn_wave(
+    KnnLevels L, int l, const int32_t* __restrict__ qpos, int nq, const float* __restrict__ X,
+    const float* __restrict__ Y, const float* __restrict__ Z, int K, float vpx, float vpy,
+    float vpz, float4* __restrict__ normals, uint8_t* __restrict__ dflags, int64_t dstride,
+    int lmax) {
+  static_assert(KP <= 64, "the K best live one per lane");
+  const int lane = threadIdx.x & 63;
+  const int wq = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * kBS + threadIdx.x) >> 6));
+  if (wq >= nq) return;
+  const int uq = qpos ? qpos[wq] : wq;
+  const int qi = L.idx[l][uq];
+  const float qx = L.sx[l][uq], qy = L.sy[l][uq], qz = L.sz[l][uq];
+  if (!finite3(qx, qy, qz)) {
+    if (lane == 0) {
+      Moments M;
+      normals[qi] = PCLF ? finish_normal_pcl(nullptr, 0, qx, qy, qz, vpx, vpy, vpz)
+                         : finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+    }
+    return;
+  }
+  const GridDesc& G = L.G[l];
+  const bool top = l == L.levels - 1;
+  const float lim = top ? INFINITY : G.cell * G.cell;
+  const float* __restrict__ sx = L.sx[l];
+  const float* __restrict__ sy = L.sy[l];
+  const float* __restrict__ sz = L.sz[l];
+  const int32_t* __restrict__ sidx = L.idx[l];
+  uint64_t best = ~0ull;  // lane j: the j-th smallest key so far
+  uint64_t kth = ~0ull;   // (uniform) the K-th smallest: the admission bound
+  int cnt = 0;            // (uniform) candidates inside the level's guaranteed radius
+  const int cx = cell_of(qx, G.lo[0], G.inv_cell, G.g[0]);
+  const int cy = cell_of(qy, G.lo[1], G.inv_cell, G.g[1]);
+  const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
+  const float w = 1.0f / G.inv_cell;
+  const float fx = (qx - G.lo[0]) * G.inv_cell - (float)cx;
+  const float fy = (qy - G.lo[1]) * G.inv_cell - (float)cy;
+  const float fz = (qz - G.lo[2]) * G.inv_cell - (float)cz;
+  auto side = [&](float f, int d) {
+    const float v = d < 0 ? f : d > 0 ? 1.0f - f : 0.0f;
+    return v > 1e-4f ? (v - 1e-4f) * w : 0.0f;
+  };
+  const float bx0 = side(fx, -1), bx1 = side(fx, 1), by0 = side(fy, -1), by1 = side(fy, 1);
+  const float bz0 = side(fz, -1), bz1 = side(fz, 1);
+  constexpr uint64_t kOrd[3] = {0x904416665151515ull, 0x1a9864a9261058ull, 0x2a2a20a8220ull};
+#pragma unroll 1
+  for (int c3 = 0; c3 < 27; ++c3) {
+    const uint32_t code = (uint32_t)(kOrd[c3 / 10] >> (6 * (c3 % 10))) & 63u;
+    const int dx = (int)(code & 3u) - 1, dy = (int)((code >> 2) & 3u) - 1,
+              dz = (int)((code >> 4) & 3u) - 1;
+    const int x = cx + dx, y = cy + dy, z = cz + dz;
+    if (x < 0 || x >= G.g[0] || y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
+    const float ex = dx < 0 ? bx0 : dx > 0 ? bx1 : 0.0f;
+    const float ey = dy < 0 ? by0 : dy > 0 ? by1 : 0.0f;
+    const float ez = dz < 0 ? bz0 : dz > 0 ? bz1 : 0.0f;
+    const float md = (ex * ex + ey * ey + ez * ez) * (1.0f - 1e-5f);
+    const float kd = __uint_as_float((uint32_t)(kth >> 32));  // (+inf bits... NaN until K held)
+    if (md >= lim || (kth != ~0ull && md > kd)) continue;
+    const int2 rg = cell_range(L.tkeys[l], L.trange[l], L.tmask[l], cell_key(G, x, y, z));
+    const int a = __builtin_amdgcn_readfirstlane(rg.x), b = __builtin_amdgcn_readfirstlane(rg.y);
+#pragma unroll 1
+    for (int u0 = a; u0 < b; u0 += 64) {
+      const int u = u0 + lane;
+      const bool valid = u < b;
+      const float d2 = valid ? flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) : INFINITY;
+      const bool in = valid && d2 < lim;
+      cnt += (int)__popcll(__ballot(in));
+      const uint64_t key = in ? ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)sidx[u] : ~0ull;
+      const bool adm = key < kth;
+      if (__ballot(adm)) {
+        uint64_t v[2] = {best, adm ? key : ~0ull};
+        wave_bitonic<2>(v);
+        best = v[0];
+        const uint64_t kb = __shfl(best, K - 1, 64);
+        kth = kb;
+      }
+    }
+  }
+  const bool defer = cnt < K && !top;
+  if (defer) {
+    const int tl = l + 1 < lmax ? l + 1 : lmax;
+    if (lane == 0) dflags[(int64_t)tl * dstride + qi] = 1;
+    return;
+  }
+  const int m = cnt < K ? cnt : K;
+  // the sums over the list in (d2, index) order, uniform in every lane (broadcast loads)
+  if constexpr (PCLF) {
+    float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int j = 0; j < m; ++j) {
+      const int i = __builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl(best, j, 64));
+      pcl_accu_add(acc, X[i], Y[i], Z[i]);
+    }
+    if (lane == 0) normals[qi] = finish_normal_pcl(acc, m, qx, qy, qz, vpx, vpy, vpz);
+  } else {
+    Moments M;
+#pragma unroll 1
+    for (int j = 0; j < m; ++j) {
+      const int i = __builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl(best, j, 64));
+      M.add(X[i], Y[i], Z[i], qx, qy, qz);
+    }
+    if (lane == 0) normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+  }
 }
 
 __global__ __launch_bounds__(kBS) void k_inverse_perm(const int32_t* __restrict__ idx, int n,
@@ -1725,8 +1849,25 @@ void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int 
       else go(k_normals_knn<64, false, Z>);
     }
   };
-  if (level == 0 && level != L.levels - 1) pick(std::true_type{});
-  else pick(std::false_type{});
+  if (level == 0 && level != L.levels - 1) {
+    pick(std::true_type{});
+  } else if (level > 0 && k <= 64) {
+    // (the deferred levels: one wave per query, k_normals_knn_wave)
+    const dim3 gw((unsigned)cdiv((int64_t)nq * 64, kBS));
+    auto gow = [&](auto kern) {
+      hipLaunchKernelGGL(kern, gw, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1], vp[2],
+                         normals, defer, defer_stride, lmax);
+    };
+    if (pcl_float) {
+      if (k <= 24) gow(k_normals_knn_wave<24, true>);
+      else gow(k_normals_knn_wave<64, true>);
+    } else {
+      if (k <= 24) gow(k_normals_knn_wave<24, false>);
+      else gow(k_normals_knn_wave<64, false>);
+    }
+  } else {
+    pick(std::false_type{});
+  }
 }
 
 void launch_nbr_count(const GridDesc& G, const GridBufs& B, int q0, int nq, float r2,

@@ -338,7 +338,7 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
         const uint8_t* f = w.dflags.p + (size_t)l * n;
         nq = count_flags(f);
         if (nq == 0) {
-          if (l >= 2) break;  // (queries skip a level only from level 0)
+          if (l >= 4) break;  // (queries skip levels only from level 0, at most to level 3)
           continue;
         }
         if (!built[l]) build_level(c, plan, L, l, nullptr), built[l] = true;
@@ -575,7 +575,8 @@ int64_t preprocess(dlg_ctx* c, const dlg_points* pts, int translate, float min_d
     const FsBuffers fb = fs_carve(w.fs_scr.p, n, 1);
     HIPCHK(fs_reset(fb, c->stream, c->opt.fs_poison));
     launch_fs_refit(w.qx.p, w.qy.p, w.qz.p, 1, reinterpret_cast<const int32_t*>(w.counters.p), n,
-                    fb, nullptr, nullptr, nullptr, c->num_cus, c->stream);
+                    fb, nullptr, nullptr, nullptr, c->num_cus, c->stream, nullptr, nullptr, nullptr,
+                    nullptr, nullptr, 0, nullptr, c->opt.fs_segments);
     launch_centroid_div(fb.sums + 6, n, w.partial.p, c->stream);
     launch_translate(w.qx.p, w.qy.p, w.qz.p, n, w.partial.p, c->stream);
     float p[3];

@@ -163,6 +163,11 @@ __global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__
 // cores then add small terms, so |D - pcl_dot| is dominated by PCL's own rounding (4.1 u S)
 // and the re-decision band is ~15x narrower than k_score_bf16's 64 u S.
 constexpr int kPrBS = 1024;
+// XCD x's super-tiles of list-length class b (spatial.hpp: the work area after the lengths)
+__device__ __forceinline__ int32_t* ord_of(const int32_t* lp_n, int64_t nsup, int x, int b) {
+  const int64_t cap = (nsup + 7) / 8;
+  return const_cast<int32_t*>(lp_n) + nsup + ((int64_t)x * kPwBuckets + b) * cap;
+}
 constexpr int kPrWaves = kPrBS / kWave;
 
 // One workgroup per "hyper" of H consecutive super-tiles (a compact region in Morton order): the
@@ -175,14 +180,14 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
                                                         int D, int ls, float margin, int H,
                                                         uint16_t* __restrict__ lp,
                                                         int32_t* __restrict__ lp_n,
-                                                        int32_t* __restrict__ work) {
+                                                        int32_t* __restrict__ work, int order) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ uint16_t s_hl[kMaxHypPerLaunch];  // the planes near this hyper's sphere
   __shared__ float4 s_sp[kWave];
   __shared__ float4 s_hyp;
   __shared__ int s_nh;
   const int t = threadIdx.x, lane = t & (kWave - 1);
-  if (blockIdx.x == 0 && t == 0) *work = 0;  // k_score_tiles_rl's item counter
+  if (blockIdx.x == 0 && t < 8) work[t * kPruneWorkStride] = 0;  // the scorers' item counters
   for (int j = t; j < D; j += kPrBS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
@@ -245,7 +250,16 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
         if (near) out[cnt + lanes_below(m)] = (uint16_t)j;
         cnt += (int)__popcll(m);
       }
-      if (lane == 0) lp_n[h0 + k] = cnt;
+      if (lane == 0) {
+        lp_n[h0 + k] = cnt;
+        if (order) {  // (k_score_tiles_ex's claim order: the longest lists' class first)
+          const int64_t s = h0 + k, cap = ((int64_t)nsup + 7) / 8;
+          const int x = (int)(s & 7), b = pw_class(cnt);
+          ord_of(lp_n, nsup, x, b)[atomicAdd(&work[kPwBucket + x * kPruneWorkStride + b], 1)] =
+              (int32_t)s;
+          (void)cap;
+        }
+      }
     }
   }
 }
@@ -622,12 +636,14 @@ constexpr int kExRing = 1024;  // >= 64 K - 1 queued + 256 appended per list ste
 constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad (slot bases 0,
                                // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
 constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
+constexpr int kStaticNum = 7, kStaticDen = 8;  // k_score_tiles_ex: items dealt before the tail
 
 template <int BS, int K, bool PK = false>
 __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
     const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
-    const int32_t* __restrict__ lp_n, int blk_cap, int xcd, const HypRec* __restrict__ hyps,
+    const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int xcd,
+    int order, const HypRec* __restrict__ hyps,
     int D, float cthr, float margin, int32_t* __restrict__ counts,
     unsigned long long* __restrict__ stats, PickArgs pick_args) {
   static_assert(K == 1 || K == 2 || K == 4, "planes per lane");
@@ -639,6 +655,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   __shared__ unsigned long long s_st[6];
   __shared__ int s_taken;
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const uint64_t wg_t0 = stats ? wall_clock64() : 0;  // (stats: the workgroup's span, RTC ticks)
   for (int j = threadIdx.x; j < D; j += BS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
@@ -652,18 +669,57 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   uint16_t* ring = s_ring[wv];
   float* spt = s_pt[wv];
   const int ips = kSuperTiles / kChunk;
-  auto claim = [&]() -> int {  // as k_score_tiles_rl (XCD-aware or interleaved items)
+  // XCD-aware items (workgroup b takes XCD b & 7's: super-tiles s = b & 7 (mod 8), so the 8 items
+  // of a super-tile share its plane list in one L2).  order: the XCD's super-tiles by list-length
+  // class (pw_class), the longest lists first.  The first kStaticFrac of an XCD's items are dealt
+  // round-robin to its workgroups (claimed through the workgroup's LDS counter: cheap), the rest
+  // from one global counter per XCD (a device atomic per claim, ~1 us, worth it only where it
+  // evens out the workgroups' ends); each workgroup is capped at blk_cap items, and the caps of
+  // an XCD's workgroups cover its items, so every item is claimed.
+  const int xw = xcd ? (int)(blockIdx.x & 7) : 0;
+  const int64_t nsup = ((int64_t)ntiles + kSuperTiles - 1) / kSuperTiles;
+  int o_cnt[kPwBuckets];  // (uniform: this XCD's super-tiles per class)
+  int64_t nx_st = 0;      // (uniform: this XCD's super-tiles)
+#pragma unroll
+  for (int b = 0; b < kPwBuckets; ++b) {
+    o_cnt[b] = order ? __builtin_amdgcn_readfirstlane(work[kPwBucket + xw * kPruneWorkStride + b]) : 0;
+    nx_st += o_cnt[b];
+  }
+  if (!order) nx_st = xcd ? (nsup - xw + 7) / 8 : nsup;
+  const int64_t gx = xcd ? (int64_t)(gridDim.x >> 3) : (int64_t)gridDim.x;  // this XCD's workgroups
+  const int64_t bx = xcd ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
+  const int64_t n_static = (nx_st * ips * kStaticNum / kStaticDen) / gx * gx;
+  // the XCD's l-th item (-1: the last super-tile's missing items; nitems: past the end)
+  auto item_of = [&](int64_t l) -> int64_t {
+    int64_t i = l / ips;
+    int64_t st;
+    if (order) {
+      int b = kPwBuckets;
+#pragma unroll
+      for (int q = 0; q < kPwBuckets; ++q)  // (unrolled: o_cnt stays in registers)
+        if (b == kPwBuckets) {
+          if (i < o_cnt[q]) b = q;
+          else i -= o_cnt[q];
+        }
+      if (b == kPwBuckets) return nitems;
+      st = ord_of(lp_n, nsup, xw, b)[i];
+    } else {
+      st = xcd ? (int64_t)xw + 8 * i : i;
+      if (st >= nsup) return nitems;
+    }
+    const int64_t itm = st * ips + l % ips;
+    return itm < nitems ? itm : -1;
+  };
+  auto claim = [&]() -> int {
     int v = nitems;
     if (lane == 0) {
       const int k = atomicAdd(&s_taken, 1);
       if (k < blk_cap) {
-        if (xcd) {
-          const int64_t l = (int64_t)k * (gridDim.x >> 3) + (blockIdx.x >> 3);
-          const int64_t s = (int64_t)(blockIdx.x & 7) + 8 * (l / ips);
-          v = (int)min((int64_t)nitems, s * ips + l % ips);
-        } else {
-          v = (int)min((int64_t)nitems, (int64_t)blockIdx.x + (int64_t)k * gridDim.x);
-        }
+        const int64_t ls = (int64_t)k * gx + bx;
+        int64_t itm = ls < n_static ? item_of(ls) : -1;
+        while (itm < 0)  // (the global tail; claim again past a missing item)
+          itm = item_of(n_static + atomicAdd(&work[xw * kPruneWorkStride], 1));
+        v = (int)itm;
       }
     }
     return __builtin_amdgcn_readfirstlane(__shfl(v, 0));  // (uniform: scalar control flow)
@@ -751,8 +807,23 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   int it_next = claim();
   float px, py, pz;
   fetch(it_next, px, py, pz);
+#ifdef DLG_WG_TRACE
+  uint64_t tr_t = wall_clock64();
+  int tr_it = -1, tr_head = 0;
+#endif
   for (int seq = 0;; ++seq) {
     const int it = it_next;
+#ifdef DLG_WG_TRACE
+    {
+      const uint64_t now = wall_clock64();
+      if (tr_it >= 0 && now - tr_t > 1500 && lane == 0)
+        printf("ITM %u %d %d %llu %llu %d\n", blockIdx.x, wv, tr_it, (unsigned long long)tr_t,
+               (unsigned long long)(now - tr_t), head - tr_head);
+      tr_t = now;
+      tr_it = it;
+      tr_head = head;
+    }
+#endif
     if (it >= nitems) break;
     it_next = claim();
     const int t0 = it * kChunk, t_end = min(ntiles, t0 + kChunk);
@@ -836,6 +907,25 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     if (c) atomicAdd(&counts[j], c);
   }
   if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
+  if (stats && threadIdx.x == 0) {
+    const unsigned long long dt = wall_clock64() - wg_t0;
+    atomicAdd(&stats[6], dt);
+    atomicMax(&stats[7], dt);
+    atomicAdd(&stats[0], 1ull);
+#ifdef DLG_WG_TRACE  // (A/B build only: every workgroup's span and claims)
+    printf("WGT %u %llu %llu %d\n", blockIdx.x, (unsigned long long)wg_t0,
+           (unsigned long long)(wg_t0 + dt), s_taken);
+#endif
+  }
+  if (order) {  // the last workgroup leaves the super-tile counts zero for the next launch
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&work[kPwTicket], 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (s_last && threadIdx.x < 8 * kPwBuckets)
+      work[kPwBucket + (threadIdx.x / kPwBuckets) * kPruneWorkStride + threadIdx.x % kPwBuckets] = 0;
+    if (s_last && threadIdx.x == 0) work[kPwTicket] = 0;
+  }
   if (pick_args.done) {  // the fused speculative pick, as in k_score_tiles_rl
     __builtin_amdgcn_s_waitcnt(0);
     __shared__ unsigned s_ticket;
@@ -975,11 +1065,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   int H = 1;
   while (H < 32 && ns / (2 * H) >= 2 * (int64_t)num_cus) H *= 2;
   const unsigned ga = (unsigned)std::max<int64_t>(1, (ns + H - 1) / H);
-  int32_t* work = lp_n + ns;  // (lp_n holds sp_supers(n) + 1 entries)
-  // (timing events, when given, ride the two dispatches themselves: no marker packets, so no
-  // launch gaps around the scoring)
-  hipExtLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, ev_start, nullptr, 0u, v.supers,
-                        (int)ns, hyps, D, ls, margin, H, lp, lp_n, work);
+  int32_t* work = lp_n - kPwHeader;  // (the buffer's header: spatial.hpp)
   // one 1024-thread workgroup per CU (LDS + VGPRs); its waves claim 2-tile items dynamically,
   // each workgroup capped at blk_cap items (16-bit LDS counters: <= 65535 points per
   // workgroup), and enough workgroups that the caps cover every item
@@ -1001,14 +1087,20 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     g = gx;
     xcd = 1;
   }
+  const bool ex = !np && tile_scorer != kTileScorerBf16;
+  const int order = ex && xcd ? 1 : 0;  // (k_score_tiles_ex claims heavy super-tiles first)
+  // (timing events, when given, ride the two dispatches themselves: no marker packets, so no
+  // launch gaps around the scoring)
+  hipExtLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, ev_start, nullptr, 0u, v.supers,
+                        (int)ns, hyps, D, ls, margin, H, lp, lp_n, work, order);
   if (!np && tile_scorer != kTileScorerBf16) {
     auto* kex = tile_scorer == kTileScorerExK1 ? k_score_tiles_ex<kBS, 1>
               : tile_scorer == kTileScorerExK4 ? k_score_tiles_ex<kBS, 4>
               : tile_scorer == kTileScorerExPk ? k_score_tiles_ex<kBS, 2, true>
                                                : k_score_tiles_ex<kBS, 2>;
     hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
-                          0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, blk_cap, xcd, hyps, D,
-                          cthr, margin, counts, stats, pick ? *pick : PickArgs{});
+                          0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, xcd,
+                          order, hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{});
     return;
   }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;

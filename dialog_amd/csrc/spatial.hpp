@@ -82,6 +82,23 @@ constexpr int kTileScorerBf16 = 1;    // k_score_tiles_rl
 // A/B-only variants (same counts; tests/test_score_variants.py runs each)
 constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14;
 constexpr int kTileScorerExPk = 12;  // k_score_tiles_ex<2> with packed f32 tests (A/B)
+// the pruned scorer's int32 buffer: a fixed header of kPwHeader words -- the item counters (one
+// per XCD, each on its own 128-byte line, kPruneWorkStride words apart), per XCD the counts of its
+// super-tiles in each of kPwBuckets list-length classes (k_prune_supers appends them,
+// k_score_tiles_ex's last workgroup zeroes them again) and that workgroup's ticket -- then the
+// sp_supers(n) list lengths (the launches' lp_n points there), then per XCD and class the
+// super-tiles (claimed longest-list class first)
+constexpr int kPruneWorkStride = 32, kPwBuckets = 8;
+constexpr int kPwBucket = 8 * kPruneWorkStride, kPwTicket = 16 * kPruneWorkStride;
+constexpr int kPwHeader = 17 * kPruneWorkStride;
+// list-length class of a super-tile: 0 (>= 2048 near planes) .. 7 (< 128)
+__host__ __device__ inline int pw_class(int cnt) {
+  return cnt >= 2048 ? 0 : cnt >= 1024 ? 1 : cnt >= 768 ? 2 : cnt >= 512 ? 3 : cnt >= 384 ? 4
+       : cnt >= 256 ? 5 : cnt >= 128 ? 6 : 7;
+}
+inline int64_t prune_work_words(int64_t ns) {
+  return kPwHeader + ns + (int64_t)kPwBuckets * 8 * ((ns + 7) / 8);
+}
 // SACMODEL_NORMAL_PLANE scoring over the spatial copy: its (normalised normal, curvature) per
 // point, and the model's lambda / threshold; margin then comes from prune_margin(lim_max, amax)
 struct PrunedNp {

@@ -124,10 +124,10 @@ class Context:
 
     def prune_stats(self, reset: bool = False) -> dict:
         """The pruned scoring kernel's work counters (needs DLG_OPT_PRUNE_STATS = 1)."""
-        a = (C.c_uint64 * 6)()
+        a = (C.c_uint64 * 8)()
         self.check(self._L.dlg_prune_stats(self.h, a, int(bool(reset))))
-        return {"list_entries": a[1], "tiles": a[2], "blocks": a[3], "pairs": a[4],
-                "redecided_blocks": a[5]}
+        return {"workgroups": a[0], "list_entries": a[1], "tiles": a[2], "blocks": a[3], "pairs": a[4],
+                "redecided_blocks": a[5], "wg_ticks_sum": a[6], "wg_ticks_max": a[7]}
 
     def set_profiling(self, on=True):
         self.check(self._L.dlg_set_profiling(self.h, int(bool(on))))

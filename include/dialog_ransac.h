@@ -39,7 +39,8 @@ extern "C" {
  * and dlg_plane_border were added; dlg_cloud_drop_spatial keeps the copy's buffers.
  * 4: dlg_extract_stats gained refit_repair_ms (refit_walk_ms is k_fs_walk alone on every rank);
  * DLG_OPT_FS_POISON; dlg_cloud_regulate_normals; DLG_OPT_HYP_SHARD; DLG_OPT_FS_ONE_WALK;
- * dlg_extract_stats gained refit_repairs; the tile-scorer option's getter returns the value set */
+ * dlg_extract_stats gained refit_repairs; dlg_prune_stats fills 8 counters; DLG_OPT_FS_SEGMENTS;
+ * the tile-scorer option's getter returns the value set */
 #define DLG_ABI_VERSION 4
 
 typedef enum {
@@ -454,23 +455,29 @@ enum {
                                (rank r scores its slice, the counts are allreduced; the rest of
                                the round runs on every rank alike: same results as one rank).
                                0 (default): point sharding (each rank uploads its shard) */
-  DLG_OPT_FS_ONE_WALK = 14  /* several ranks, PCL float refit (same sums every way): 0 (default)
+  DLG_OPT_FS_ONE_WALK = 14, /* several ranks, PCL float refit (same sums every way): 0 (default)
                                = walk, rebase every rank on the guess the walks propagate, walk
                                again, then hand the exact chain ends rank to rank (each repair a
                                few windows long); 1 = no rebase: the repairs start from the
                                double-prefix guesses (the round-4 protocol, A/B only); 2 = 0 with
                                parallel repair iterations and host checks instead of the
                                hand-over (tests and A/B only) */
+  DLG_OPT_FS_SEGMENTS = 15  /* one rank, PCL float refit: walkers per float chain, 1..16 (default
+                               8): the chain's windows in segments walked at once from the refined
+                               guesses, then joined in order (a segment whose guess was not its
+                               exact start is walked again until it meets its recorded walk); 1 =
+                               one walker per chain.  Same sums every way */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
 dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);
 dlg_status dlg_ctx_get_option(const dlg_ctx* ctx, int option, int64_t* value);
 /* the pruned scoring kernel's counters since DLG_OPT_PRUNE_STATS was set (or the last reset):
- * [0] unused, [1] super-tile list entries tested against tile spheres, [2] tiles visited,
+ * [0] workgroups (DLG_TILE_EXACT), [1] super-tile list entries tested against tile spheres, [2] tiles visited,
  * [3] 32x32 blocks (DLG_TILE_EXACT: 64-lane passes) scored, [4] (tile, plane) pairs scored,
- * [5] blocks with a band re-decision (DLG_TILE_BF16 only) */
-dlg_status dlg_prune_stats(dlg_ctx* ctx, uint64_t out[6], int reset);
+ * [5] blocks with a band re-decision (DLG_TILE_BF16 only), [6] / [7] (DLG_TILE_EXACT) the sum
+ * and the maximum of the workgroups' spans in 100 MHz clock ticks (load balance) */
+dlg_status dlg_prune_stats(dlg_ctx* ctx, uint64_t out[8], int reset);
 
 /* max over ranks of a host double (bench timing) and a barrier; no-ops for world == 1 */
 dlg_status dlg_allreduce_max_f64(dlg_ctx* ctx, double* value);

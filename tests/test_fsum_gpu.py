@@ -117,3 +117,31 @@ def test_device_sums_poisoned_tables(fs):
             assert same(sums, literal(fs, xyz)), k
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("segments", [1, 2, 5, 16])
+def test_device_sums_segments(fs, segments):
+    """DLG_OPT_FS_SEGMENTS (one rank): each chain's windows in that many segments, walked at once
+    from the refined guesses and joined in order by k_fs_segfix (a segment whose guess missed its
+    exact start is walked again until it meets its recorded walk).  Every segmentation gives the
+    literal loop's sums: hovering and quantised sequences (the guesses miss) and C3's planes."""
+    ctx = D.Context(0)
+    try:
+        ctx.set_option(D.DLG_OPT_FS_SEGMENTS, segments)
+        assert ctx.get_option(D.DLG_OPT_FS_SEGMENTS) == segments
+        rng = np.random.default_rng(500 + segments)
+        for kind in ("hover", "quant", "alternating", "mags", "drift"):
+            for n in (4097, 70000, 600000):
+                xyz = np.ascontiguousarray(np.stack(gen(kind, n, rng), axis=1))
+                sums, _, _, _ = ctx.float_sums(xyz)
+                assert same(sums, literal(fs, xyz)), (kind, n)
+        p, lab, planes = plane_cloud(4_000_000, 8, seed=0xD1A106 + 3)
+        for k in range(8):
+            xyz = np.ascontiguousarray(p[lab == k])
+            cin = np.float32([planes[k, 0], planes[k, 1], planes[k, 2], planes[k, 3]])
+            sums, co, unc, _ = ctx.float_sums(xyz, cin=cin)
+            assert same(sums, literal(fs, xyz)), k
+            if not unc:
+                assert same(co, host_refit(fs, xyz, cin)), k
+    finally:
+        ctx.close()

@@ -16,6 +16,8 @@
 #                                         -> traffic.py / pmc_issue.py summaries
 #   c5                                    tools/bench_c5.py (normals, RegulateNormal, chain)
 #   c5prof                                rocprofv3 --kernel-trace --stats over tools/c5_kernels.py
+#   knnprof                               rocprofv3 --kernel-trace --stats over tools/knn_probe.py
+#                                         (one k = 20 estimation: per-level dispatches)
 #   c5pmc                                 SQ issue counters (one PMC pass) over tools/bench_c5.py
 #   walk                                  tools/fs_walk_stats.py (PCL float-sum walk counters)
 #   walkab=<a.so,b.so>                    walk counters under two library builds, alternated
@@ -71,6 +73,8 @@ for s in "$@"; do
     c5) run c5 600 python3 -u tools/bench_c5.py ${arg//,/ } ;;
     c5prof) run c5prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5prof" -o run -- \
               python3 tools/c5_kernels.py ${arg//,/ } ;;
+    knnprof) run knnprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/knnprof" -o run -- \
+              python3 tools/knn_probe.py ;;
     walk) run walk 300 python3 -u tools/fs_walk_stats.py ${arg//,/ } ;;
     c5pmc) run c5pmc 220 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d "$O/c5pmc" -o run -- python3 tools/bench_c5.py 10000000 1 ;;
     walkab)

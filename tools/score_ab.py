@@ -63,6 +63,9 @@ def main():
         if launches:
             extra["pruned_per_launch"] = {k: v / launches for k, v in st.items()}
             extra["pruned_per_launch"]["pair_fraction"] = st["pairs"] / launches / (n * nh / 32)
+            if st["workgroups"]:  # (100 MHz ticks: the workgroups' spans against the longest)
+                extra["wg_span_us_mean"] = st["wg_ticks_sum"] / st["workgroups"] / 100.0
+                extra["wg_span_us_max"] = st["wg_ticks_max"] / 100.0
     print(json.dumps(dict(n=n, D=nh, rounds=rounds, counts_equal=True, total_inliers=int(ref.sum()),
                           kernels=out, **extra), indent=1))
 
