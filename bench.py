@@ -71,6 +71,8 @@ def parse():
                     help="rendezvous through torch.distributed even at N=1 (runtime check)")
     ap.add_argument("--select-tile", type=int, default=0,
                     help="points per single-pass select tile (DLG_OPT_SELECT_TILE; 0: library default)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B only: a context option, e.g. FS_SEGMENTS=1 (DLG_OPT_FS_SEGMENTS)")
     ap.add_argument("--no-events", action="store_true",
                     help="no HIP timing events in the timed steps (A/B of their host cost)")
     ap.add_argument("--no-secondary", action="store_true",
@@ -260,6 +262,9 @@ def main():
     ctx.set_profiling(not a.no_events)
     if a.select_tile:
         ctx.set_option(D.DLG_OPT_SELECT_TILE, a.select_tile)
+    for o in a.opt:
+        name, val = o.split("=", 1)
+        ctx.set_option(getattr(D, "DLG_OPT_" + name), int(val))
 
     strong = a.global_points > 0
     if strong:  # C4: one global cloud sharded over the ranks (last rank takes the remainder)

@@ -1075,9 +1075,9 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     // from level 0: above it the sparse queries are volume-like outliers, many of which level
     // l + 1 resolves, and a query scanned a level too coarse costs ~4x the candidates)
     if (L0 && cnt > 0 && cnt * 4 < K && l + 2 < L.levels - 1) jump = 2;
-    // (level 0, no candidate at all: volume-like outliers, which C5's clouds resolve three levels
-    // up -- the levels between would scan them only to defer them again)
-    if (L0 && cnt == 0 && l + 3 < L.levels - 1) jump = 3;
+    // (level 0, at most two candidates: volume-like outliers, which C5's clouds resolve three
+    // levels up -- level 2 deferred 86 % of the queries sent there, to level 3)
+    if (L0 && cnt * 10 <= K && l + 3 < L.levels - 1) jump = 3;
     if (!defer) {
       const int m = cnt < K ? cnt : K;
       if constexpr (PCLF) {
@@ -1116,6 +1116,63 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
 // bitonic sort.  Same counts, same (d2, index) order, same K-th bound for skipping cells, so the
 // same neighbour lists, deferrals and sums as the one-lane scan, whose wave waited for the lane
 // with the densest cells.
+// the normal from the wave's m best keys: lane j loads neighbour j (all at once), then the sums
+// run over the list in (d2, index) order from registers (readlane), uniform in every lane; lane
+// 0 stores
+template <bool PCLF>
+__device__ __forceinline__ void knn_finish(uint64_t best, int m, const float* __restrict__ X,
+                                           const float* __restrict__ Y,
+                                           const float* __restrict__ Z, float qx, float qy,
+                                           float qz, float vpx, float vpy, float vpz,
+                                           float4* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane < m ? (int)(uint32_t)best : 0;
+  const float x = X[i], y = Y[i], z = Z[i];
+  auto rl = [](float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+  };
+  if constexpr (PCLF) {
+    float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int j = 0; j < m; ++j) pcl_accu_add(acc, rl(x, j), rl(y, j), rl(z, j));
+    if (lane == 0) *out = finish_normal_pcl(acc, m, qx, qy, qz, vpx, vpy, vpz);
+  } else {
+    Moments M;
+#pragma unroll 1
+    for (int j = 0; j < m; ++j) M.add(rl(x, j), rl(y, j), rl(z, j), qx, qy, qz);
+    if (lane == 0) *out = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
+  }
+}
+
+constexpr int kKwB = 4;    // k_normals_knn_wave: candidate batches in flight
+constexpr int kKwIns = 6;  // ... admitted candidates of a batch inserted one by one (more: a merge)
+
+// one batch of 64 candidate keys (d2 bits << 32 | original index; ~0: none) into the wave's
+// ascending best keys (lane j: the j-th) under the bound kth (the K-th best so far)
+__device__ __forceinline__ void knn_admit(uint64_t key, int K, uint64_t& best, uint64_t& kth) {
+  const int lane = threadIdx.x & 63;
+  const bool adm = key < kth;
+  uint64_t am = __ballot(adm);
+  if (__popcll(am) > kKwIns) {  // many: one 128-key bitonic merge
+    uint64_t v[2] = {best, adm ? key : ~0ull};
+    wave_bitonic<2>(v);
+    best = v[0];
+    kth = __shfl(best, K - 1, 64);
+  } else {
+    while (am) {  // few: each inserted in place (rank by ballot, lanes above shift up)
+      const int src = __builtin_ctzll(am);
+      am &= am - 1;
+      const uint64_t kv =
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), src) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, src);
+      if (!(kv < kth)) continue;  // (uniform: the earlier insertions raised the bar)
+      const int pos = (int)__popcll(__ballot(best < kv));
+      const uint64_t up = __shfl_up(best, 1, 64);
+      best = lane < pos ? best : lane == pos ? kv : up;
+      kth = __shfl(best, K - 1, 64);
+    }
+  }
+}
 template <int KP, bool PCLF>
 __global__ __launch_bounds__(kBS) void k_normals_knn_wave(
     KnnLevels L, int l, const int32_t* __restrict__ qpos, int nq, const float* __restrict__ X,
@@ -1176,21 +1233,28 @@ __global__ __launch_bounds__(kBS) void k_normals_knn_wave(
     if (md >= lim || (kth != ~0ull && md > kd)) continue;
     const int2 rg = cell_range(L.tkeys[l], L.trange[l], L.tmask[l], cell_key(G, x, y, z));
     const int a = __builtin_amdgcn_readfirstlane(rg.x), b = __builtin_amdgcn_readfirstlane(rg.y);
+    // kKwB batches of 64 candidates per step, every load issued before the first d2 (a cell of
+    // a coarse level holds hundreds of a plane's points: the steps are latency-bound)
 #pragma unroll 1
-    for (int u0 = a; u0 < b; u0 += 64) {
-      const int u = u0 + lane;
-      const bool valid = u < b;
-      const float d2 = valid ? flann_d2(qx, qy, qz, sx[u], sy[u], sz[u]) : INFINITY;
-      const bool in = valid && d2 < lim;
-      cnt += (int)__popcll(__ballot(in));
-      const uint64_t key = in ? ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)sidx[u] : ~0ull;
-      const bool adm = key < kth;
-      if (__ballot(adm)) {
-        uint64_t v[2] = {best, adm ? key : ~0ull};
-        wave_bitonic<2>(v);
-        best = v[0];
-        const uint64_t kb = __shfl(best, K - 1, 64);
-        kth = kb;
+    for (int u0 = a; u0 < b; u0 += 64 * kKwB) {
+      float px[kKwB], py[kKwB], pz[kKwB];
+      int32_t pi[kKwB];
+#pragma unroll
+      for (int j = 0; j < kKwB; ++j) {
+        const int u = u0 + 64 * j + lane;
+        const bool valid = u < b;
+        px[j] = valid ? sx[u] : INFINITY;
+        py[j] = valid ? sy[u] : 0.0f;
+        pz[j] = valid ? sz[u] : 0.0f;
+        pi[j] = valid ? sidx[u] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < kKwB; ++j) {
+        const float d2 = flann_d2(qx, qy, qz, px[j], py[j], pz[j]);  // (+inf past the end)
+        const bool in = d2 < lim;
+        cnt += (int)__popcll(__ballot(in));
+        const uint64_t key = in ? ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)pi[j] : ~0ull;
+        knn_admit(key, K, best, kth);
       }
     }
   }
@@ -1200,25 +1264,7 @@ __global__ __launch_bounds__(kBS) void k_normals_knn_wave(
     if (lane == 0) dflags[(int64_t)tl * dstride + qi] = 1;
     return;
   }
-  const int m = cnt < K ? cnt : K;
-  // the sums over the list in (d2, index) order, uniform in every lane (broadcast loads)
-  if constexpr (PCLF) {
-    float acc[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int j = 0; j < m; ++j) {
-      const int i = __builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl(best, j, 64));
-      pcl_accu_add(acc, X[i], Y[i], Z[i]);
-    }
-    if (lane == 0) normals[qi] = finish_normal_pcl(acc, m, qx, qy, qz, vpx, vpy, vpz);
-  } else {
-    Moments M;
-#pragma unroll 1
-    for (int j = 0; j < m; ++j) {
-      const int i = __builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl(best, j, 64));
-      M.add(X[i], Y[i], Z[i], qx, qy, qz);
-    }
-    if (lane == 0) normals[qi] = finish_normal(M, qx, qy, qz, vpx, vpy, vpz);
-  }
+  knn_finish<PCLF>(best, cnt < K ? cnt : K, X, Y, Z, qx, qy, qz, vpx, vpy, vpz, normals + qi);
 }
 
 __global__ __launch_bounds__(kBS) void k_inverse_perm(const int32_t* __restrict__ idx, int n,
