@@ -1075,9 +1075,10 @@ __global__ __launch_bounds__(kBS) void k_normals_knn(
     // from level 0: above it the sparse queries are volume-like outliers, many of which level
     // l + 1 resolves, and a query scanned a level too coarse costs ~4x the candidates)
     if (L0 && cnt > 0 && cnt * 4 < K && l + 2 < L.levels - 1) jump = 2;
-    // (level 0, at most two candidates: volume-like outliers, which C5's clouds resolve three
-    // levels up -- level 2 deferred 86 % of the queries sent there, to level 3)
-    if (L0 && cnt * 10 <= K && l + 3 < L.levels - 1) jump = 3;
+    // (level 0, fewer than K / 4 candidates: volume-like outliers, which C5's clouds resolve
+    // three levels up -- level 2 deferred 86 % of the queries sent there to level 3, and the few
+    // it kept cost a level build of ~1.1 ms)
+    if (L0 && cnt * 4 < K && l + 3 < L.levels - 1) jump = 3;
     if (!defer) {
       const int m = cnt < K ? cnt : K;
       if constexpr (PCLF) {
@@ -1260,7 +1261,7 @@ __global__ __launch_bounds__(kBS) void k_normals_knn_wave(
   }
   const bool defer = cnt < K && !top;
   if (defer) {
-    const int tl = l + 1 < lmax ? l + 1 : lmax;
+    const int tl = lmax;  // (the launch passes the level deferrals go to)
     if (lane == 0) dflags[(int64_t)tl * dstride + qi] = 1;
     return;
   }
@@ -1871,7 +1872,7 @@ void launch_normals_radius(const GridDesc& G, const GridBufs& B, int n, float r2
 void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
                         float4* normals, uint8_t* defer, int64_t defer_stride, int lmax,
-                        bool pcl_float, hipStream_t s) {
+                        bool pcl_float, hipStream_t s, int tnext) {
   if (nq <= 0) return;
   const dim3 g(cdiv(nq, kBS)), b(kBS);
   auto go = [&](auto kern) {
@@ -1900,9 +1901,10 @@ void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int 
   } else if (level > 0 && k <= 64) {
     // (the deferred levels: one wave per query, k_normals_knn_wave)
     const dim3 gw((unsigned)cdiv((int64_t)nq * 64, kBS));
+    const int tl = std::min(tnext >= 0 ? tnext : level + 1, lmax);
     auto gow = [&](auto kern) {
       hipLaunchKernelGGL(kern, gw, b, 0, s, L, level, qpos, nq, X, Y, Z, k, vp[0], vp[1], vp[2],
-                         normals, defer, defer_stride, lmax);
+                         normals, defer, defer_stride, tl);
     };
     if (pcl_float) {
       if (k <= 24) gow(k_normals_knn_wave<24, true>);

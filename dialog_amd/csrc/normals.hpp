@@ -85,7 +85,8 @@ struct KnnLevels {
 void launch_normals_knn(const KnnLevels& L, int level, const int32_t* qpos, int nq,
                         const float* X, const float* Y, const float* Z, int k, const float vp[3],
                         float4* normals, uint8_t* defer, int64_t defer_stride, int lmax,
-                        bool pcl_float, hipStream_t s);
+                        bool pcl_float, hipStream_t s, int tnext = -1);
+// (tnext, levels > 0: the level a deferred query goes to; -1: the next one)
 // PCL-float radius normals in chunks of queries (sorted positions [q0, q0 + nq)):
 // counts -> exclusive scan (int64 offsets) -> (d2, index) keys filled, sorted per query (one
 // wave per query: bitonic in registers up to 1024 keys, heapsort beyond) -> float sums in that

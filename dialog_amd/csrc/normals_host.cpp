@@ -334,6 +334,15 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
     for (int l = 0; l < L.levels; ++l) {
       const int32_t* qpos = nullptr;  // level 0: every point
       int nq = n;
+      int tnext = -1;
+      if (l > 0 && l + 2 < L.levels && !built[l + 1]) {
+        // a level nothing has been sent to yet is skipped by this level's deferrals when the
+        // level above it has queries already (it will be built anyway; C5: level 0 sends its
+        // sparse queries to level 3, so level 1's few deferrals need no level 2)
+        if (count_flags(w.dflags.p + (size_t)(l + 1) * n) == 0 &&
+            count_flags(w.dflags.p + (size_t)(l + 2) * n) > 0)
+          tnext = l + 2;
+      }
       if (l > 0) {
         const uint8_t* f = w.dflags.p + (size_t)l * n;
         nq = count_flags(f);
@@ -348,7 +357,7 @@ void normals_core(dlg_ctx* c, int n, const BBox& b, float radius, int k_nn, cons
         qpos = w.queue.p;
       }
       launch_normals_knn(L, l, qpos, nq, w.x.p, w.y.p, w.z.p, k_nn, vp, w.nrm.p, w.dflags.p,
-                         (int64_t)n, L.levels - 1, pclf, c->stream);
+                         (int64_t)n, L.levels - 1, pclf, c->stream, tnext);
     }
   }
   HIPCHK(hipGetLastError());
