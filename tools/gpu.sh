@@ -12,6 +12,8 @@
 #   bench[=extra args, comma-separated]   bench.py --steps 10 --warmup 3 (+ args)
 #   benchfull                             bench.py as the driver runs it (defaults)
 #   prof[=extra bench args]               rocprofv3 --kernel-trace --stats over a short bench
+#   pmclds                                LDS counters (instructions, bank conflicts, LDS-busy and
+#                                         LDS-issue-stall cycles) of the scoring launch, one pass
 #   pmc                                   FETCH/WRITE/SQ-issue PMC passes of the scoring launch
 #                                         -> traffic.py / pmc_issue.py summaries
 #   c5                                    tools/bench_c5.py (normals, RegulateNormal, chain)
@@ -71,6 +73,10 @@ for s in "$@"; do
       python3 tools/pmc_kern.py k_score_tiles $(find "$O/pmcab_a" "$O/pmcab_b" -name '*counter_collection.csv') > "$O/pmcab.json" 2>&1
       cat "$O/pmcab.json" ;;
     c5) run c5 600 python3 -u tools/bench_c5.py ${arg//,/ } ;;
+    pmclds)  # LDS-side counters of the scoring launch (one pass: 8 SQ + 1 GRBM)
+      run pmc_lds 180 timeout -s KILL 170 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc_lds" -o run -- $B1
+      L=$(find "$O/pmc_lds" -name '*counter_collection.csv' -print -quit)
+      python3 tools/pmc_kern.py k_score_tiles_ex,k_prune_supers "$L" > "$O/pmc_lds_summary.log" 2>&1 ;;
     c5prof) run c5prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5prof" -o run -- \
               python3 tools/c5_kernels.py ${arg//,/ } ;;
     knnprof) run knnprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/knnprof" -o run -- \
