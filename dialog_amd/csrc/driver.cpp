@@ -897,23 +897,20 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     HIPCHK(hipGetLastError());
     spec_pending = false;
     if (lean) {
-      // the sphere bounds of the Morton survivors (count in totals[4]) on the side stream, beside
-      // the list from the stamps (ids in list order; survivors' pristine indices): independent
-      // passes over different buffers
-      const int b = cl->sp_spare();
-      SoA& sd = cl->sp_buf[b];
-      cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
-      cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
-      HIPCHK(hipEventRecord(c->ev_fork, c->stream));
-      HIPCHK(hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
-      launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
-                           cl->sp_sb[b].p, c->sstream);
-      HIPCHK(hipEventRecord(c->ev_join, c->sstream));
+      // the list from the stamps (ids in list order; survivors' pristine indices), then the
+      // sphere bounds of the Morton survivors (count in totals[4]).  (Running the bounds on a
+      // second stream beside the list pass was tried and dropped: with 8 loopback contexts in
+      // one process, 24 streams on 4 hardware queues, a run hung.)
       stage_wait();
       launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv,
                        cl->gid_ident ? nullptr : cl->pristine.gid.p, cl->id_base, c->sel1,
                        c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream, c->opt.sel1_tile);
-      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      const int b = cl->sp_spare();
+      SoA& sd = cl->sp_buf[b];
+      cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
+      cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
+      launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
+                           cl->sp_sb[b].p, c->stream);
     } else {
       stage_wait();
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
@@ -1118,10 +1115,7 @@ dlg_status init_ctx(dlg_ctx* c, int device) {
   return guarded(c, [&] {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_inl, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
   });
 }
@@ -1331,12 +1325,6 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
     (void)hipStreamSynchronize(c->cstream);
     (void)hipStreamDestroy(c->cstream);
   }
-  if (c->sstream) {
-    (void)hipStreamSynchronize(c->sstream);
-    (void)hipStreamDestroy(c->sstream);
-  }
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (auto& pr : c->ev_sel)
     for (auto& ev : pr)
       if (ev) (void)hipEventDestroy(ev);

@@ -232,10 +232,6 @@ struct dlg_ctx {
   // the deferred inlier copy runs on its own stream, off the rounds' critical path: it waits for
   // ev_inl (the round's select on the main stream); the next select waits for ev_stage
   hipStream_t cstream = nullptr;
-  // lean rounds: the survivors' sphere bounds run on sstream beside the list pass (forked and
-  // joined by ev_fork / ev_join on the main stream)
-  hipStream_t sstream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_inl = nullptr;
   hipEvent_t ev_inl_cur = nullptr;    // the marker the copy waits for (ev_inl, or the round's
                                       // end-of-select timing event when profiling)

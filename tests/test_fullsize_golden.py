@@ -147,6 +147,7 @@ def run_sharded(p, bounds, mode, profile=False, options=()):
                                       capacity=p.shape[0])
             c.close()
         except Exception as ex:  # pragma: no cover
+            print(f"rank {r}: {ex!r}", flush=True)  # (the other ranks may now wait forever)
             errs.append(ex)
 
     th = [threading.Thread(target=run, args=(r,)) for r in range(W)]

@@ -31,6 +31,10 @@ export TMPDIR=/tmp
 TAG="${TAG:-run}"
 O=gpurun_out/$TAG
 mkdir -p "$O"
+# a line a minute under gpurun_out/ while a long step (the full-size tests) runs silently
+( while true; do date +%T >> "$O/heartbeat.log"; sleep 60; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 B1="python3 bench.py --steps 1 --warmup 0 --no-secondary --no-extras --no-cpu-baseline"
 
 run() {  # run <name> <seconds> <cmd...>: output to $O/<name>.log, stop the session on failure
@@ -47,7 +51,7 @@ for s in "$@"; do
   case $name in
     tests) run tests_$(echo "$arg" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40) 900 \
              python3 -u -m pytest ${arg//,/ } -m gpu -x -v --timeout 240 --timeout-method thread ;;
-    gputests) run gputests 1100 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    gputests) run gputests 1100 python3 -u -m pytest tests -m gpu -x -v --durations=15 --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     ab) run ab 300 env PRUNE_STATS=1 python3 -u tools/score_ab.py ${arg//,/ } ;;
     bench) run bench_$(echo "$arg" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40)_$(echo "$arg" | md5sum | cut -c1-6) 900 \
