@@ -560,7 +560,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       launch_score_pruned(spatial_view(cl), hyps_s, Ds, cthr, pmargin, cl->amax, counts_s,
                           c->lp.p, c->lp_n.p + kPwHeader, c->num_cus, c->stream, prune_stats_ptr(c), &npp,
                           fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,
-                          ext_ev ? c->ev[1] : nullptr);
+                          ext_ev ? c->ev[1] : nullptr, c->opt.tile_scorer);
     } else if (np) {
       if (Ds > 0) launch_score_np(src, hyps_s, Ds, mt, counts_s, c->num_cus, c->stream);
     } else if (pruned) {
@@ -680,7 +680,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // (e = 2, 3: k_fs_repair's, which runs on ranks > 0 of a group only)
     c->rep_rec[sk] = false;
     auto walk_ev = [&](int e) -> hipEvent_t {
-      if (!c->profiling) return nullptr;
+      if (!c->profiling || !c->walk_events) return nullptr;
       if (e >= 2 && (c->comm->world() == 1 || c->comm->rank() == 0)) return nullptr;
       if (!c->ev_walk[sk][e]) HIPCHK(hipEventCreate(&c->ev_walk[sk][e]));
       (e >= 2 ? c->rep_rec : c->walk_rec)[sk] = true;
@@ -1838,7 +1838,9 @@ dlg_status dlg_prune_stats(dlg_ctx* c, uint64_t out[8], int reset) {
 
 dlg_status dlg_set_profiling(dlg_ctx* c, int enable) {
   if (!c) return DLG_ERR_INVALID;
+  if (enable < 0 || enable > 2) return DLG_ERR_INVALID;
   c->profiling = enable != 0;
+  c->walk_events = enable == 1;
   return DLG_OK;
 }
 

@@ -195,6 +195,7 @@ struct dlg_ctx {
   Comm* hcomm = nullptr;
   std::string err;
   bool profiling = false;
+  bool walk_events = false;  // (profiling level 1: the PCL refit walk's events too)
   bool sp_all = true;  // every rank holds a valid spatial copy (agreed per extraction)
   // scratch
   DevBuf<int32_t> pos;

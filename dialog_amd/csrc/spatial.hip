@@ -6,6 +6,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 
@@ -637,21 +638,91 @@ constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad 
                                // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
 constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
 constexpr int kStaticNum = 7, kStaticDen = 8;  // k_score_tiles_ex: items dealt before the tail
+// NORMAL_PLANE slots: x[32] y[32] z[32] lim[32] + pad (bases 0, 132, 264, 396 dwords: banks 0,
+// 4, 8, 12, disjoint for b128)
+constexpr int kExSlotNp = 132;
 
-template <int BS, int K, bool PK = false>
+// inclusive max over the wave (DPP; lanes a step does not reach keep their own value)
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int dpp_max_step(int v) {
+  return max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, kCtrl, kRowMask, 0xF, false));
+}
+__device__ __forceinline__ int wave_incl_max_i32(int v) {
+  v = dpp_max_step<0x111, 0xF>(v);
+  v = dpp_max_step<0x112, 0xF>(v);
+  v = dpp_max_step<0x114, 0xF>(v);
+  v = dpp_max_step<0x118, 0xF>(v);
+  v = dpp_max_step<0x142, 0xA>(v);
+  v = dpp_max_step<0x143, 0xC>(v);
+  return v;
+}
+__device__ __forceinline__ int wave_incl_sum_i32(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+  return v;
+}
+// v * 16 + the four bits (m0 first) of this lane in the compare masks m0..m3: four v_addc with
+// the masks as carry-ins (the s_nop: two wait states between a VALU's mask write and its use)
+__device__ __forceinline__ uint32_t shl4_add(uint32_t v, uint64_t m0, uint64_t m1, uint64_t m2,
+                                             uint64_t m3) {
+  uint64_t co;
+  asm("s_nop 1\n\t"
+      "v_addc_co_u32_e64 %0, %1, %0, %0, %2\n\t"
+      "v_addc_co_u32_e64 %0, %1, %0, %0, %3\n\t"
+      "v_addc_co_u32_e64 %0, %1, %0, %0, %4\n\t"
+      "v_addc_co_u32_e64 %0, %1, %0, %0, %5"
+      : "+v"(v), "=&s"(co)
+      : "s"(m0), "s"(m1), "s"(m2), "s"(m3));
+  return v;
+}
+// np_deuclid's |d_euclid| without its "+ 0 * 0" term: that add changes only the sign of a zero,
+// which the final fabsf drops (the same float)
+__device__ __forceinline__ float np_de_abs(float4 c, float x, float y, float z) {
+  return fabsf(((c.x * x + c.z * z) + c.y * y) + c.w);
+}
+// position (LSB = 0) of the r-th set bit (r counted from 0) of v; r < popcount(v)
+__device__ __forceinline__ int nth_set_bit(uint32_t v, int r) {
+  int pos = 0, t = __popc(v & 0xFFFFu);
+  if (r >= t) { r -= t; v >>= 16; pos += 16; }
+  t = __popc(v & 0xFFu);
+  if (r >= t) { r -= t; v >>= 8; pos += 8; }
+  t = __popc(v & 0xFu);
+  if (r >= t) { r -= t; v >>= 4; pos += 4; }
+  t = __popc(v & 0x3u);
+  if (r >= t) { r -= t; v >>= 2; pos += 2; }
+  return pos + (r >= (int)(v & 1u) ? 1 : 0);
+}
+
+// NPM (SACMODEL_NORMAL_PLANE, K = 2): the pass evaluates PCL's prefilter b = (1 - w) d_euclid <
+// thr as the float compare d_euclid < lim with the point's lim (np_de_limit, computed once when
+// the point is fetched, stored in its slot), each lane collecting its 2 x 32 verdicts as bits;
+// the passing (point, plane) pairs of the pass are then dealt 64 at a time to the lanes
+// (prefix sum of the lanes' bit counts, owner lane by a DPP max-scan of the chunk's first
+// positions) and decided with PCL's double arithmetic (np_full, as k_score_np), the normal read
+// from global memory.  Same counts as k_score_tiles_rl<NPM> and k_score_np.
+template <int BS, int K, bool PK = false, bool NPM = false>
 __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
     const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
     const int32_t* __restrict__ lp_n, int32_t* __restrict__ work, int blk_cap, int xcd,
     int order, const HypRec* __restrict__ hyps,
     int D, float cthr, float margin, int32_t* __restrict__ counts,
-    unsigned long long* __restrict__ stats, PickArgs pick_args) {
+    unsigned long long* __restrict__ stats, PickArgs pick_args,
+    const float4* __restrict__ NRM = nullptr, double lambda = 0.0, double thr = 0.0) {
   static_assert(K == 1 || K == 2 || K == 4, "planes per lane");
+  static_assert(!NPM || (K == 2 && !PK), "NORMAL_PLANE: two planes per lane");
   constexpr int kChunk = 2;  // tiles per item
+  constexpr int kSlotF = NPM ? kExSlotNp : kExSlotF;
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves: <= 65535 points per workgroup
   __shared__ __attribute__((aligned(8))) uint16_t s_ring[BS / kWave][kExRing];
-  __shared__ __attribute__((aligned(16))) float s_pt[BS / kWave][4 * kExSlotF];
+  __shared__ __attribute__((aligned(16))) float s_pt[BS / kWave][4 * kSlotF];
+  __shared__ int s_own[NPM ? BS / kWave : 1][NPM ? kWave : 1];   // NPM: chunk owners
+  __shared__ int s_stile[NPM ? BS / kWave : 1][4];                // NPM: each slot's tile
   __shared__ unsigned long long s_st[6];
   __shared__ int s_taken;
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -724,11 +795,19 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     }
     return __builtin_amdgcn_readfirstlane(__shfl(v, 0));  // (uniform: scalar control flow)
   };
-  // lane l holds point l of an item (its two tiles); NaN past n
-  auto fetch = [&](int it, float& px, float& py, float& pz) {
+  // lane l holds point l of an item (its two tiles); NaN past n.  NPM: and its prefilter limit
+  // (-inf: never passes; a NaN w leaves the exact test NaN < thr, never an inlier)
+  auto fetch = [&](int it, float& px, float& py, float& pz, float& pl) {
     const int64_t p = (int64_t)it * (kChunk * kTileP) + lane;
     px = py = pz = __builtin_nanf("");
-    if (it < nitems && p < n) { px = X[p]; py = Y[p]; pz = Z[p]; }
+    pl = -INFINITY;
+    if (it < nitems && p < n) {
+      px = X[p]; py = Y[p]; pz = Z[p];
+      if constexpr (NPM) {
+        const double w = lambda * (1.0 - (double)NRM[p].w);
+        pl = w == w ? np_de_limit(w, thr) : -INFINITY;
+      }
+    }
   };
   int nq = 0, head = 0;  // ring positions (multiples of K at every tile segment boundary)
   // the m (<= 64 K, a multiple of K) oldest queued pairs: lane l takes the K consecutive entries
@@ -754,7 +833,68 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
       cf[k] = s_cf[e[k] & 0xFFFu];
       if (e[k] & kExPad) cf[k] = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);  // never counts
     }
-    const float* b = spt + ((e[0] >> 12) & 3u) * kExSlotF;
+    const float* b = spt + ((e[0] >> 12) & 3u) * kSlotF;
+    if constexpr (NPM) {
+      // prefilter verdicts: bit 31 - p of nm[k] for point p of the lane's tile, plane k
+      uint32_t nm[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) nm[k] = 0u;
+#pragma unroll 2
+      for (int p = 0; p < kTileP; p += 4) {
+        const float4 xs = *reinterpret_cast<const float4*>(b + p);
+        const float4 ys = *reinterpret_cast<const float4*>(b + kTileP + p);
+        const float4 zs = *reinterpret_cast<const float4*>(b + 2 * kTileP + p);
+        const float4 lm = *reinterpret_cast<const float4*>(b + 3 * kTileP + p);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float4 c = cf[k];
+          nm[k] = shl4_add(nm[k], ballot(np_de_abs(c, xs.x, ys.x, zs.x) < lm.x),
+                           ballot(np_de_abs(c, xs.y, ys.y, zs.y) < lm.y),
+                           ballot(np_de_abs(c, xs.z, ys.z, zs.z) < lm.z),
+                           ballot(np_de_abs(c, xs.w, ys.w, zs.w) < lm.w));
+        }
+      }
+      // the passing pairs, 64 per step: pair g belongs to the lane whose [excl, incl) holds it
+      const int c0 = __popc(nm[0]), cnt = c0 + __popc(nm[1]);
+      const int incl = wave_incl_sum_i32(cnt), excl = incl - cnt;
+      const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+      const uint32_t ew = e[0] | e[1] << 16;
+      int* own = s_own[wv];
+#pragma unroll 1
+      for (int base = 0; base < total; base += kWave) {
+        const uint64_t om = ballot(cnt > 0 && excl <= base);  // (non-empty: total > base)
+        const int own0 = 63 - (int)__builtin_clzll(om);
+        own[lane] = -1;
+        __builtin_amdgcn_wave_barrier();
+        if (cnt > 0 && excl > base && excl < base + kWave) own[excl - base] = lane;
+        __builtin_amdgcn_wave_barrier();
+        int L = lane == 0 ? own0 : own[lane];
+        L = wave_incl_max_i32(L);
+        __builtin_amdgcn_wave_barrier();  // (own is rewritten by the next step)
+        const int g = base + lane;
+        const int exL = __shfl(excl, L), c0L = __shfl(c0, L);
+        const uint32_t m0 = (uint32_t)__shfl((int)nm[0], L), m1 = (uint32_t)__shfl((int)nm[1], L);
+        const uint32_t eL = (uint32_t)__shfl((int)ew, L);
+        if (g < total) {
+          int r = g - exL;
+          const bool second = r >= c0L;
+          if (second) r -= c0L;
+          const int pt = 31 - nth_set_bit(second ? m1 : m0, r);
+          const int jj = (int)((second ? eL >> 16 : eL) & 0xFFFu);
+          const int slot = (int)((eL >> 12) & 3u);
+          const float* bs = spt + slot * kSlotF;
+          const float4 cq = s_cf[jj];
+          const float de = np_deuclid(cq, bs[pt], bs[kTileP + pt], bs[2 * kTileP + pt]);
+          const float4 nn = NRM[(int64_t)s_stile[wv][slot] * kTileP + pt];
+          const double w = lambda * (1.0 - (double)nn.w);
+          const float4 cn = eigen_normalized3(cq.x, cq.y, cq.z, 0.0f);
+          if (np_full(cn, nn, w, (1.0 - w) * (double)de, thr))
+            atomicAdd(&s_cnt[jj >> 1], 1u << (16 * (jj & 1)));
+        }
+      }
+      head += m;
+      return;
+    }
     uint32_t acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0u;
@@ -805,8 +945,8 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     }
   };
   int it_next = claim();
-  float px, py, pz;
-  fetch(it_next, px, py, pz);
+  float px, py, pz, pl;
+  fetch(it_next, px, py, pz, pl);
 #ifdef DLG_WG_TRACE
   uint64_t tr_t = wall_clock64();
   int tr_it = -1, tr_head = 0;
@@ -839,12 +979,16 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const int nlp = __builtin_amdgcn_readfirstlane(lp_n[sidx]);
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lp + (int64_t)sidx * ls);
     {
-      float* d = spt + (slot0 + (lane >> 5)) * kExSlotF + (lane & 31);
+      float* d = spt + (slot0 + (lane >> 5)) * kSlotF + (lane & 31);
       __builtin_amdgcn_wave_barrier();
       d[0] = px; d[kTileP] = py; d[2 * kTileP] = pz;
+      if constexpr (NPM) {
+        d[3 * kTileP] = pl;
+        if (lane < kChunk) s_stile[wv][slot0 + lane] = t0 + lane;
+      }
       __builtin_amdgcn_wave_barrier();
     }
-    fetch(it_next, px, py, pz);  // the next item's points, in flight during this one
+    fetch(it_next, px, py, pz, pl);  // the next item's points, in flight during this one
 #pragma unroll 1
     for (int lb = 0; lb < nlp; lb += kListCap) {
       const int le = min(nlp, lb + kListCap);
@@ -1087,20 +1231,29 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     g = gx;
     xcd = 1;
   }
-  const bool ex = !np && tile_scorer != kTileScorerBf16;
+  // (NORMAL_PLANE: DLG_TILE_BF16 selects round 4's k_score_tiles_rl<NPM>, lanes as points)
+  const bool ex = tile_scorer != kTileScorerBf16;
   const int order = ex && xcd ? 1 : 0;  // (k_score_tiles_ex claims heavy super-tiles first)
   // (timing events, when given, ride the two dispatches themselves: no marker packets, so no
   // launch gaps around the scoring)
   hipExtLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, ev_start, nullptr, 0u, v.supers,
                         (int)ns, hyps, D, ls, margin, H, lp, lp_n, work, order);
-  if (!np && tile_scorer != kTileScorerBf16) {
+  if (np && ex) {
+    hipExtLaunchKernelGGL((k_score_tiles_ex<kBS, 2, false, true>), dim3((unsigned)g), dim3(kBS), 0, s,
+                          nullptr, ev_stop, 0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work,
+                          blk_cap, xcd, order, hyps, D, cthr, margin, counts, stats,
+                          pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr);
+    return;
+  }
+  if (ex) {
     auto* kex = tile_scorer == kTileScorerExK1 ? k_score_tiles_ex<kBS, 1>
               : tile_scorer == kTileScorerExK4 ? k_score_tiles_ex<kBS, 4>
               : tile_scorer == kTileScorerExPk ? k_score_tiles_ex<kBS, 2, true>
                                                : k_score_tiles_ex<kBS, 2>;
     hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
                           0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, xcd,
-                          order, hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{});
+                          order, hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{},
+                          (const float4*)nullptr, 0.0, 0.0);
     return;
   }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;

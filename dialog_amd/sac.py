@@ -130,7 +130,8 @@ class Context:
                 "redecided_blocks": a[5], "wg_ticks_sum": a[6], "wg_ticks_max": a[7]}
 
     def set_profiling(self, on=True):
-        self.check(self._L.dlg_set_profiling(self.h, int(bool(on))))
+        """on: True / 1 = all timing events, 2 = without the PCL refit walk's, False / 0 = none."""
+        self.check(self._L.dlg_set_profiling(self.h, int(on)))
 
     def synchronize(self):
         self.check(self._L.dlg_synchronize(self.h))

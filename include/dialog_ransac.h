@@ -385,7 +385,9 @@ dlg_status dlg_sac_control_result(const dlg_sac_control* ctl, dlg_sac_stats* st,
                                   int64_t* best_draw);
 
 /* ---- profiling ------------------------------------------------------------------------------ */
-/* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default. */
+/* Kernel-level HIP-event timing on the context's stream (bench roofline); off by default.
+ * enable 1: the scoring launches, the select phase and the PCL refit walk; 2: without the walk's
+ * events (each timing event on a dispatch costs the stream a few microseconds). */
 dlg_status dlg_set_profiling(dlg_ctx* ctx, int enable);
 dlg_status dlg_synchronize(dlg_ctx* ctx);
 /* Scoring-kernel micro-benchmark (kernel A/B on the device): D random plane hypotheses through

@@ -149,10 +149,12 @@ def test_gpu_np_extract_golden(gpu_ctx, pruned):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pruned", [False, True])
+@pytest.mark.parametrize("pruned", [False, True, "rl"])
 @pytest.mark.parametrize("seed,lam,thr", [(1, 0.1, 0.05), (2, 0.5, 0.1), (3, 0.0, 0.02),
                                           (4, 1.0, 0.3), (5, 0.2, 0.05)])
 def test_gpu_np_random_vs_oracle(gpu_ctx, seed, lam, thr, pruned):
+    """pruned: the Morton copy with the default tile scorer (lanes as planes), or "rl" with
+    DLG_TILE_BF16 (round 4's lanes-as-points NORMAL_PLANE scorer)."""
     import dialog_amd as D
     p, nrm, _, _ = cloud_with_normals(int(2000 + 3000 * seed), seed=seed, outliers=0.2)
     if seed == 5:  # NaN normals (isolated points) and a zero normal
@@ -169,7 +171,12 @@ def test_gpu_np_random_vs_oracle(gpu_ctx, seed, lam, thr, pruned):
     cloud.set_normals(nrm)
     prm = D.make_params(thr, max_iterations=300, model=D.SACMODEL_NORMAL_PLANE,
                         normal_distance_weight=lam)
-    inl, coeff, st = D.segment_cloud(cloud, prm)
+    if pruned == "rl":
+        gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_BF16)
+    try:
+        inl, coeff, st = D.segment_cloud(cloud, prm)
+    finally:
+        gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_EXACT)
     assert st["has_model"] == r["ok"]
     assert st["iterations"] == r["iterations"]
     assert np.array_equal(st["best_sample"], r["best_sample"])
@@ -390,3 +397,50 @@ def test_gpu_c5_full_size_properties(gpu_ctx):
         s = ids[rng.choice(ids.size, min(2000, ids.size), replace=False)]
         d = np_twin_dist(e["coeffs"][k], p[s], nrm[s], 0.1)
         assert np.all(d < 0.02)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lam", [0.1, 0.7])
+def test_gpu_np_tile_scorers_agree(gpu_ctx, lam):
+    """The pruned NORMAL_PLANE scorers (default: lanes as planes with the prefilter verdicts as
+    bits, spatial.hip k_score_tiles_ex<NPM>; DLG_TILE_BF16: k_score_tiles_rl<NPM>, lanes as
+    points) and the exhaustive kernel (DLG_OPT_PRUNE_NP 0) extract the same planes bit for bit
+    from a 300k-point cloud with synthetic normals (tilted, NaN, zero and high-curvature ones)."""
+    import dialog_amd as D
+    from dialog_amd.synth import plane_cloud
+    p, lab, pl = plane_cloud(300_000, 6, outlier_frac=0.15, seed=31)
+    rng = np.random.default_rng(31)
+    nrm = np.zeros((p.shape[0], 4), np.float32)
+    for k in range(len(pl)):
+        nrm[lab == k, :3] = np.asarray(pl[k][:3], np.float32)
+    out = lab < 0
+    nrm[out, :3] = rng.normal(size=(int(out.sum()), 3)).astype(np.float32)
+    nrm[:, :3] += rng.normal(scale=0.05, size=(p.shape[0], 3)).astype(np.float32)
+    nrm[:, :3] /= np.linalg.norm(nrm[:, :3], axis=1, keepdims=True)
+    nrm[:, 3] = rng.uniform(0.0, 0.3, p.shape[0]).astype(np.float32)
+    nrm[::101] = np.nan
+    nrm[7::997, :3] = 0.0
+    nrm[11::503, 3] = 1.5  # (w < 0: the prefilter does not apply)
+    prm = D.make_params(0.03, max_iterations=1023, probability=1.0,
+                        model=D.SACMODEL_NORMAL_PLANE, normal_distance_weight=lam)
+    res = {}
+    for name, opts in (("ex", {}), ("rl", {D.DLG_OPT_PRUNE_TILE_SCORER: D.DLG_TILE_BF16}),
+                       ("exhaustive", {D.DLG_OPT_PRUNE_NP: 0})):
+        for k, v in opts.items():
+            gpu_ctx.set_option(k, v)
+        try:
+            cloud = D.Cloud(gpu_ctx, p)
+            cloud.set_normals(nrm)
+            if name != "exhaustive":
+                cloud.build_spatial()
+            res[name] = D.extract_planes(cloud, prm, max_planes=6, min_inliers=500)
+            cloud.close()
+        finally:
+            gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_EXACT)
+            gpu_ctx.set_option(D.DLG_OPT_PRUNE_NP, 1)
+    ref = res["exhaustive"]
+    assert len(ref["offsets"]) > 2
+    for name in ("ex", "rl"):
+        assert np.array_equal(res[name]["offsets"], ref["offsets"]), name
+        assert np.array_equal(res[name]["coeffs"].view(np.uint32), ref["coeffs"].view(np.uint32)), name
+        assert np.array_equal(res[name]["inliers"], ref["inliers"]), name
