@@ -556,7 +556,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     if (pruned_np) {
       c->lp.ensure((size_t)sp_supers(cl->sp_n) * prune_list_stride(D) + 1);
       ensure_prune_work(c, sp_supers(cl->sp_n));
-      const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold};
+      c->np_cn.ensure(kMaxHypPerLaunch);
+      const PrunedNp npp{cl->sp_soa().nrm.p, prm.normal_distance_weight, prm.threshold, c->np_cn.p};
       launch_score_pruned(spatial_view(cl), hyps_s, Ds, cthr, pmargin, cl->amax, counts_s,
                           c->lp.p, c->lp_n.p + kPwHeader, c->num_cus, c->stream, prune_stats_ptr(c), &npp,
                           fuse_pick ? &pk : nullptr, ext_ev ? c->ev[0] : nullptr,

@@ -218,6 +218,7 @@ struct dlg_ctx {
   PinBuf<double> h_mom;
   PinBuf<int64_t> h_g64;
   DevBuf<float4> small;    // winning plane + samples + refined plane (segment_impl)
+  DevBuf<float4> np_cn;    // NORMAL_PLANE pruned scoring: the hypotheses' normalized normals
   DevBuf<uint16_t> lp;     // pruned scoring: per super-tile lists of near planes
   DevBuf<int32_t> lp_n;
   DevBuf<unsigned long long> pstats;  // pruned-kernel work counters (DLG_OPT_PRUNE_STATS)

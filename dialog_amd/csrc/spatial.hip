@@ -181,7 +181,8 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
                                                         int D, int ls, float margin, int H,
                                                         uint16_t* __restrict__ lp,
                                                         int32_t* __restrict__ lp_n,
-                                                        int32_t* __restrict__ work, int order) {
+                                                        int32_t* __restrict__ work, int order,
+                                                        float4* __restrict__ cn) {
   __shared__ float4 s_cf[kMaxHypPerLaunch];
   __shared__ uint16_t s_hl[kMaxHypPerLaunch];  // the planes near this hyper's sphere
   __shared__ float4 s_sp[kWave];
@@ -189,6 +190,11 @@ __global__ __launch_bounds__(kPrBS) void k_prune_supers(const float4* __restrict
   __shared__ int s_nh;
   const int t = threadIdx.x, lane = t & (kWave - 1);
   if (blockIdx.x == 0 && t < 8) work[t * kPruneWorkStride] = 0;  // the scorers' item counters
+  if (cn && blockIdx.x == gridDim.x - 1)  // (NORMAL_PLANE: Eigen's normalized() of each plane)
+    for (int j = t; j < D; j += kPrBS) {
+      const HypRec h = hyps[j];
+      cn[j] = eigen_normalized3(h.a, h.b, h.c, 0.0f);
+    }
   for (int j = t; j < D; j += kPrBS) {
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
@@ -712,7 +718,8 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     int order, const HypRec* __restrict__ hyps,
     int D, float cthr, float margin, int32_t* __restrict__ counts,
     unsigned long long* __restrict__ stats, PickArgs pick_args,
-    const float4* __restrict__ NRM = nullptr, double lambda = 0.0, double thr = 0.0) {
+    const float4* __restrict__ NRM = nullptr, double lambda = 0.0, double thr = 0.0,
+    const float4* __restrict__ CN = nullptr) {
   static_assert(K == 1 || K == 2 || K == 4, "planes per lane");
   static_assert(!NPM || (K == 2 && !PK), "NORMAL_PLANE: two planes per lane");
   constexpr int kChunk = 2;  // tiles per item
@@ -887,8 +894,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
           const float de = np_deuclid(cq, bs[pt], bs[kTileP + pt], bs[2 * kTileP + pt]);
           const float4 nn = NRM[(int64_t)s_stile[wv][slot] * kTileP + pt];
           const double w = lambda * (1.0 - (double)nn.w);
-          const float4 cn = eigen_normalized3(cq.x, cq.y, cq.z, 0.0f);
-          if (np_full(cn, nn, w, (1.0 - w) * (double)de, thr))
+          if (np_full(CN[jj], nn, w, (1.0 - w) * (double)de, thr))
             atomicAdd(&s_cnt[jj >> 1], 1u << (16 * (jj & 1)));
         }
       }
@@ -1237,12 +1243,13 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   // (timing events, when given, ride the two dispatches themselves: no marker packets, so no
   // launch gaps around the scoring)
   hipExtLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, ev_start, nullptr, 0u, v.supers,
-                        (int)ns, hyps, D, ls, margin, H, lp, lp_n, work, order);
+                        (int)ns, hyps, D, ls, margin, H, lp, lp_n, work, order,
+                        np && ex ? np->cn : nullptr);
   if (np && ex) {
     hipExtLaunchKernelGGL((k_score_tiles_ex<kBS, 2, false, true>), dim3((unsigned)g), dim3(kBS), 0, s,
                           nullptr, ev_stop, 0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work,
                           blk_cap, xcd, order, hyps, D, cthr, margin, counts, stats,
-                          pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr);
+                          pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr, np->cn);
     return;
   }
   if (ex) {
@@ -1253,7 +1260,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
                           0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, xcd,
                           order, hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{},
-                          (const float4*)nullptr, 0.0, 0.0);
+                          (const float4*)nullptr, 0.0, 0.0, (const float4*)nullptr);
     return;
   }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;

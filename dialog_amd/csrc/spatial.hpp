@@ -104,6 +104,7 @@ inline int64_t prune_work_words(int64_t ns) {
 struct PrunedNp {
   const float4* nrm;
   double lambda, thr;
+  float4* cn = nullptr;  // [D] scratch: the hypotheses' normalized (a, b, c) (k_prune_supers)
 };
 void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float cthr, float margin,
                          const float amax[3], int32_t* counts, uint16_t* lp, int32_t* lp_n,
