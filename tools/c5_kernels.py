@@ -1,5 +1,6 @@
 """The C5 stages once each, warm, for a kernel-trace profile (tools/gpu.sh c5prof): k = 20 and
-radius 0.1 normals on a cloud's device copy, RegulateNormal (r 0.1, seed 0) from host records.
+radius 0.1 normals on a cloud's device copy, RegulateNormal on the device copy (after the k = 20
+normals) and (r 0.1, seed 0) from host records.
 Prints the stage wall times as one JSON line.
 
 usage: python tools/c5_kernels.py [points]
@@ -32,6 +33,7 @@ def timed(name, f):
 
 
 timed("cloud_normals_knn20_ms", lambda: cloud.estimate_normals(k=20))
+timed("cloud_regulate_r0.1_ms", lambda: cloud.regulate_normals(0, True, 0.1))
 rn = timed("cloud_normals_radius0.1_ms", lambda: cloud.estimate_normals(radius=0.1, copy_out=True))
 res["regulate_reached"] = timed("regulate_r0.1_ms",
                                 lambda: D.regulate_normals(p, rn, 0, True, 0.1, ctx=ctx))[2]
