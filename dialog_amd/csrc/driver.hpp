@@ -107,7 +107,7 @@ struct NormalsWork {
   DevBuf<uint32_t> keys_in, keys_out, counters;
   DevBuf<int32_t> idx_in, queue, cand, ids, ids_alt, pos_of, nn;
   DevBuf<float4> nrm, nrm_s;
-  DevBuf<uint32_t> claim, ccnt, coffs, ccur, ctile, cslot;
+  DevBuf<uint32_t> claim, ccnt, coffs, ccur, ctile, cslot, cdone;
   DevBuf<float> sd2;
   DevBuf<int32_t> ncnt;   // PCL-float radius normals: neighbours per query (chunk)
   DevBuf<int64_t> noff;   //   their offsets
@@ -127,7 +127,7 @@ struct NormalsWork {
     keys_in.release(); keys_out.release(); counters.release();
     idx_in.release(); queue.release(); cand.release(); ids.release(); ids_alt.release();
     pos_of.release(); nrm.release(); nrm_s.release(); claim.release(); keys64.release();
-    keys_alt.release(); h_cnt.release(); ccnt.release(); coffs.release(); ccur.release();
+    keys_alt.release(); h_cnt.release(); ccnt.release(); coffs.release(); ccur.release(); cdone.release();
     sd2.release(); bst.release(); h_bst.release(); ctile.release(); cslot.release();
     ncnt.release(); noff.release(); nkeys.release();
     ovfa.release(); ovfb.release(); ovfc.release();

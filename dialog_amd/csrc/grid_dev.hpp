@@ -51,5 +51,17 @@ __device__ __forceinline__ int2 cell_range(const uint32_t* __restrict__ tkeys,
   }
 }
 
+// the table slot of cell key k (-1 if unoccupied)
+__device__ __forceinline__ int cell_slot(const uint32_t* __restrict__ tkeys, uint32_t tmask,
+                                         uint32_t k) {
+  uint32_t h = hash_key(k) & tmask;
+  while (true) {
+    const uint32_t tk = tkeys[h];
+    if (tk == k) return (int)h;
+    if (tk == kEmpty) return -1;
+    h = (h + 1) & tmask;
+  }
+}
+
 }  // namespace grid
 }  // namespace dlg

@@ -586,17 +586,23 @@ __global__ __launch_bounds__(kBS) void k_nbr_normals(
 // x cells have consecutive keys), packed into one candidate list: rows[r] = row r's start in the
 // list, rows[9 + r] = its offset to sorted positions, rows[18] = the list's length.  The whole
 // wave calls it; rows is the wave's LDS table.
+// cell_done (RegulateNormal's claim pass): cells whose points are all settled are left out (a
+// row keeps the union of its other cells; a settled middle cell stays inside it)
 __device__ __forceinline__ void nbr_rows(const GridDesc& G, const uint32_t* __restrict__ tkeys,
                                          const int2* __restrict__ trange, uint32_t tmask, int cx,
-                                         int cy, int cz, int32_t* rows) {
+                                         int cy, int cz, int32_t* rows,
+                                         const uint32_t* __restrict__ cell_done = nullptr) {
   const int lane = threadIdx.x & 63;
   // lanes 0..26 look up one cell each; a row's range is its cells' union (contiguous)
   int2 c = make_int2(INT_MAX, INT_MIN);
   if (lane < 27) {
     const int x = cx + lane % 3 - 1, y = cy + (lane / 3) % 3 - 1, z = cz + lane / 9 - 1;
     if (x >= 0 && y >= 0 && z >= 0 && x < G.g[0] && y < G.g[1] && z < G.g[2]) {
-      const int2 r = cell_range(tkeys, trange, tmask, cell_key(G, x, y, z));
-      if (r.y > r.x) c = r;
+      const int h = cell_slot(tkeys, tmask, cell_key(G, x, y, z));
+      if (h >= 0) {
+        const int2 r = trange[h];
+        if (r.y > r.x && !(cell_done && cell_done[h] >= (uint32_t)(r.y - r.x))) c = r;
+      }
     }
   }
   int lo = c.x, hi = c.y;
@@ -1495,7 +1501,8 @@ __global__ __launch_bounds__(kBS) void k_bfs2_claim(
     const int2* __restrict__ trange, uint32_t tmask, float r2,
     const uint8_t* __restrict__ processed_s, uint32_t* __restrict__ claim_s,
     int32_t* __restrict__ cand, long long* __restrict__ st_w, uint32_t* __restrict__ child_cnt,
-    uint32_t* __restrict__ cursor) {
+    uint32_t* __restrict__ cursor, const uint32_t* __restrict__ cell_done) {
+  (void)cell_done;
   constexpr int kStage = 2048;
   __shared__ uint32_t s_n;
   __shared__ long long s_base;
@@ -1563,7 +1570,7 @@ __global__ __launch_bounds__(kBS) void k_bfs2_claim_w(
     const int2* __restrict__ trange, uint32_t tmask, float r2,
     const uint8_t* __restrict__ processed_s, uint32_t* __restrict__ claim_s,
     int32_t* __restrict__ cand, long long* __restrict__ st_w, uint32_t* __restrict__ child_cnt,
-    uint32_t* __restrict__ cursor) {
+    uint32_t* __restrict__ cursor, const uint32_t* __restrict__ cell_done) {
   constexpr int kStage = 2048;
   constexpr int kW = kBS / 64;
   __shared__ uint32_t s_n;
@@ -1592,7 +1599,7 @@ __global__ __launch_bounds__(kBS) void k_bfs2_claim_w(
       const int cz = cell_of(qz, G.lo[2], G.inv_cell, G.g[2]);
       if (cx != pcx || cy != pcy || cz != pcz) {
         pcx = cx; pcy = cy; pcz = cz;
-        nbr_rows(G, tkeys, trange, tmask, cx, cy, cz, rows);
+        nbr_rows(G, tkeys, trange, tmask, cx, cy, cz, rows, cell_done);
       }
       int r_start[9], r_off[9];
 #pragma unroll
@@ -1639,7 +1646,9 @@ __global__ __launch_bounds__(kBS) void k_bfs2_settle(
     const int32_t* __restrict__ queue, const int32_t* __restrict__ cand,
     const long long* __restrict__ st, const int32_t* __restrict__ pos_of,
     uint8_t* __restrict__ processed_s, const uint32_t* __restrict__ claim_s,
-    float4* __restrict__ nrm_s, uint32_t* __restrict__ child_cnt) {
+    float4* __restrict__ nrm_s, uint32_t* __restrict__ child_cnt, const float* __restrict__ sx,
+    const float* __restrict__ sy, const float* __restrict__ sz, GridDesc G,
+    const uint32_t* __restrict__ tkeys, uint32_t tmask, uint32_t* __restrict__ cell_done) {
   const long long fbase = st[0], nc = st[2];
   for (long long t = (long long)blockIdx.x * kBS + threadIdx.x; t < nc;
        t += (long long)gridDim.x * kBS) {
@@ -1655,6 +1664,12 @@ __global__ __launch_bounds__(kBS) void k_bfs2_settle(
     }
     processed_s[u] = 1;
     atomicAdd(&child_cnt[ppos - fbase], 1u);
+    // (u is finite: it passed the radius test; its cell is the one the grid binned it in)
+    const int h = cell_slot(tkeys, tmask,
+                            cell_key(G, cell_of(sx[u], G.lo[0], G.inv_cell, G.g[0]),
+                                     cell_of(sy[u], G.lo[1], G.inv_cell, G.g[1]),
+                                     cell_of(sz[u], G.lo[2], G.inv_cell, G.g[2])));
+    if (h >= 0) atomicAdd(&cell_done[h], 1u);
   }
 }
 
@@ -2072,9 +2087,10 @@ void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, con
                        bool wave_claim) {
   hipLaunchKernelGGL(wave_claim ? k_bfs2_claim_w : k_bfs2_claim, dim3(grid), dim3(kBS), 0, s,
                      queue, st, pos_of, B.sx, B.sy, B.sz, G, B.tkeys, B.trange, B.tmask, r2,
-                     processed_s, claim_s, cand, st, W.child_cnt, W.cursor);
+                     processed_s, claim_s, cand, st, W.child_cnt, W.cursor, W.cell_done);
   hipLaunchKernelGGL(k_bfs2_settle, dim3(grid), dim3(kBS), 0, s, queue, cand, st, pos_of,
-                     processed_s, claim_s, nrm_s, W.child_cnt);
+                     processed_s, claim_s, nrm_s, W.child_cnt, B.sx, B.sy, B.sz, G, B.tkeys,
+                     B.tmask, W.cell_done);
   hipLaunchKernelGGL(k_bfs2_scan_tiles, dim3(grid), dim3(kBS), 0, s, st, W.child_cnt, W.offs,
                      W.tile_tot);
   hipLaunchKernelGGL(k_bfs2_scan_top, dim3(1), dim3(1024), 0, s, st, W.tile_tot);

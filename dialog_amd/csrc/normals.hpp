@@ -158,6 +158,7 @@ struct Bfs2Bufs {
   uint32_t* slot_of;
   float* slot_d2;
   int32_t* slot_id;
+  uint32_t* cell_done;  // [tmask + 1] points of each grid cell the BFS has settled (zeroed)
 };
 void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, const GridDesc& G,
                        const GridBufs& B, float r2, uint8_t* processed_s, uint32_t* claim_s,

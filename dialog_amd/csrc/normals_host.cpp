@@ -425,7 +425,9 @@ int64_t regulate_core(dlg_ctx* c, int n, const float* X, const float* Y, const f
   w.bst.ensure(4);
   w.ccnt.ensure(n); w.coffs.ensure(n); w.ccur.ensure(n); w.sd2.ensure(n);
   w.ctile.ensure(n / 1024 + 2); w.cslot.ensure(n);
-  const Bfs2Bufs W{w.ccnt.p, w.ccur.p, w.coffs.p, w.ctile.p, w.cslot.p, w.sd2.p, w.ids.p};
+  w.cdone.ensure((size_t)B.tmask + 1);
+  HIPCHK(hipMemsetAsync(w.cdone.p, 0, ((size_t)B.tmask + 1) * 4, c->stream));
+  const Bfs2Bufs W{w.ccnt.p, w.ccur.p, w.coffs.p, w.ctile.p, w.cslot.p, w.sd2.p, w.ids.p, w.cdone.p};
   w.h_bst.ensure(4);
   w.h_bst.p[0] = 0; w.h_bst.p[1] = 1; w.h_bst.p[2] = 0; w.h_bst.p[3] = 1;
   HIPCHK(hipMemcpyAsync(w.bst.p, w.h_bst.p, 32, hipMemcpyHostToDevice, c->stream));
