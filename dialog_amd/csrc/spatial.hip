@@ -644,6 +644,7 @@ constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad 
                                // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
 constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
 constexpr int kStaticNum = 7, kStaticDen = 8;  // k_score_tiles_ex: items dealt before the tail
+constexpr int64_t kOrderMaxSupers = 65536;      // class-ordered claims up to this many super-tiles
 // NORMAL_PLANE slots: x[32] y[32] z[32] lim[32] + pad (bases 0, 132, 264, 396 dwords: banks 0,
 // 4, 8, 12, disjoint for b128)
 constexpr int kExSlotNp = 132;
@@ -719,7 +720,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     int D, float cthr, float margin, int32_t* __restrict__ counts,
     unsigned long long* __restrict__ stats, PickArgs pick_args,
     const float4* __restrict__ NRM = nullptr, double lambda = 0.0, double thr = 0.0,
-    const float4* __restrict__ CN = nullptr) {
+    const float4* __restrict__ CN = nullptr, int tail = 1) {
   static_assert(K == 1 || K == 2 || K == 4, "planes per lane");
   static_assert(!NPM || (K == 2 && !PK), "NORMAL_PLANE: two planes per lane");
   constexpr int kChunk = 2;  // tiles per item
@@ -766,7 +767,8 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   if (!order) nx_st = xcd ? (nsup - xw + 7) / 8 : nsup;
   const int64_t gx = xcd ? (int64_t)(gridDim.x >> 3) : (int64_t)gridDim.x;  // this XCD's workgroups
   const int64_t bx = xcd ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
-  const int64_t n_static = (nx_st * ips * kStaticNum / kStaticDen) / gx * gx;
+  // (tail 0: every item dealt round-robin, round 4's claim)
+  const int64_t n_static = tail ? (nx_st * ips * kStaticNum / kStaticDen) / gx * gx : nx_st * ips;
   // the XCD's l-th item (-1: the last super-tile's missing items; nitems: past the end)
   auto item_of = [&](int64_t l) -> int64_t {
     int64_t i = l / ips;
@@ -1239,7 +1241,15 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   }
   // (NORMAL_PLANE: DLG_TILE_BF16 selects round 4's k_score_tiles_rl<NPM>, lanes as points)
   const bool ex = tile_scorer != kTileScorerBf16;
-  const int order = ex && xcd ? 1 : 0;  // (k_score_tiles_ex claims heavy super-tiles first)
+  // (A/B only: 15 = round 4's claim, XCD round-robin without classes or tail; 16 = classes
+  // without the tail; 17 = the tail without classes)
+  const bool claim_ab = tile_scorer >= kTileScorerClaimR4 && tile_scorer <= kTileScorerClaimTail;
+  // the class order only up to kOrderMaxSupers super-tiles: at C3 (19.5k) it takes the first
+  // launch 0.418 -> 0.409 ms, at C4's 100M points on one GPU (195k) it costs the prune launch 97
+  // -> 187 us (the bucket appends' atomics) and the scoring 1465 -> 1610 us (r05j4-j7)
+  const int order = ex && xcd && ns <= kOrderMaxSupers && tile_scorer != kTileScorerClaimR4 &&
+                            tile_scorer != kTileScorerClaimTail ? 1 : 0;
+  const int tail = claim_ab && tile_scorer != kTileScorerClaimTail ? 0 : 1;
   // (timing events, when given, ride the two dispatches themselves: no marker packets, so no
   // launch gaps around the scoring)
   hipExtLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, ev_start, nullptr, 0u, v.supers,
@@ -1249,7 +1259,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     hipExtLaunchKernelGGL((k_score_tiles_ex<kBS, 2, false, true>), dim3((unsigned)g), dim3(kBS), 0, s,
                           nullptr, ev_stop, 0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work,
                           blk_cap, xcd, order, hyps, D, cthr, margin, counts, stats,
-                          pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr, np->cn);
+                          pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr, np->cn, tail);
     return;
   }
   if (ex) {
@@ -1260,7 +1270,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
                           0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, xcd,
                           order, hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{},
-                          (const float4*)nullptr, 0.0, 0.0, (const float4*)nullptr);
+                          (const float4*)nullptr, 0.0, 0.0, (const float4*)nullptr, tail);
     return;
   }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;

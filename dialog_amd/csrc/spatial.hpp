@@ -81,7 +81,8 @@ constexpr int kTileScorerExact = 0;   // k_score_tiles_ex<2> (default)
 constexpr int kTileScorerBf16 = 1;    // k_score_tiles_rl
 // A/B-only variants (same counts; tests/test_score_variants.py runs each)
 constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14;
-constexpr int kTileScorerExPk = 12;  // k_score_tiles_ex<2> with packed f32 tests (A/B)
+constexpr int kTileScorerExPk = 12;
+constexpr int kTileScorerClaimR4 = 15, kTileScorerClaimClass = 16, kTileScorerClaimTail = 17;  // A/B  // k_score_tiles_ex<2> with packed f32 tests (A/B)
 // the pruned scorer's int32 buffer: a fixed header of kPwHeader words -- the item counters (one
 // per XCD, each on its own 128-byte line, kPruneWorkStride words apart), per XCD the counts of its
 // super-tiles in each of kPwBuckets list-length classes (k_prune_supers appends them,
