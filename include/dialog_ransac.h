@@ -439,9 +439,12 @@ enum {
                                every round's select redone with the host's plane (test) */
   DLG_OPT_PRUNE_TILE_SCORER = 9, /* the pruned plane scorer's (tile, plane) pairs:
                                DLG_TILE_EXACT (default) PCL-order f32 with lanes as planes, or
-                               DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band re-decision.
-                               (11, 14: A/B-only variants of the first with 1, 4 planes per lane;
-                               same counts; the getter returns the value set) */
+                               DLG_TILE_BF16 32x32 bf16 matrix-core blocks + band re-decision
+                               (NORMAL_PLANE: DLG_TILE_EXACT lanes as planes with the prefilter
+                               verdicts as bits, DLG_TILE_BF16 round 4's lanes-as-points scorer).
+                               (A/B-only variants of the first, same counts: 11, 14 with 1, 4
+                               planes per lane, 12 packed f32 tests, 15..17 item-claim orders;
+                               the getter returns the value set) */
   DLG_OPT_NORMALS_FUSED = 10, /* PCL-float radius normals: 1 (default) search, (d2, index) order
                                and sums in one fused pass; 0: the chunked count / fill / sort /
                                sum pipeline */
