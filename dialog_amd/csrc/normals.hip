@@ -2085,7 +2085,10 @@ void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, con
                        const GridBufs& B, float r2, uint8_t* processed_s, uint32_t* claim_s,
                        float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s,
                        bool wave_claim) {
-  hipLaunchKernelGGL(wave_claim ? k_bfs2_claim_w : k_bfs2_claim, dim3(grid), dim3(kBS), 0, s,
+  // (the wave claim: 4x the workgroups, about one run of frontier nodes per wave -- more
+  // dependent candidate loads in flight per CU)
+  hipLaunchKernelGGL(wave_claim ? k_bfs2_claim_w : k_bfs2_claim, dim3(wave_claim ? 4 * grid : grid),
+                     dim3(kBS), 0, s,
                      queue, st, pos_of, B.sx, B.sy, B.sz, G, B.tkeys, B.trange, B.tmask, r2,
                      processed_s, claim_s, cand, st, W.child_cnt, W.cursor, W.cell_done);
   hipLaunchKernelGGL(k_bfs2_settle, dim3(grid), dim3(kBS), 0, s, queue, cand, st, pos_of,
