@@ -1562,7 +1562,7 @@ __global__ __launch_bounds__(kBS) void k_bfs2_claim(
 // waves take runs of kBqRun consecutive frontier nodes (children of consecutive parents: mostly
 // the same cells, looked up once).  Same claims as k_bfs2_claim (a min: the order the candidates
 // are met in does not matter), appended through the workgroup's LDS stage.
-constexpr int kBqRun = 4;
+constexpr int kBqRun = 2;
 __global__ __launch_bounds__(kBS) void k_bfs2_claim_w(
     const int32_t* __restrict__ queue, const long long* __restrict__ st,
     const int32_t* __restrict__ pos_of, const float* __restrict__ sx, const float* __restrict__ sy,
@@ -2087,7 +2087,7 @@ void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, con
                        bool wave_claim) {
   // (the wave claim: 4x the workgroups, about one run of frontier nodes per wave -- more
   // dependent candidate loads in flight per CU)
-  hipLaunchKernelGGL(wave_claim ? k_bfs2_claim_w : k_bfs2_claim, dim3(wave_claim ? 8 * grid : grid),
+  hipLaunchKernelGGL(wave_claim ? k_bfs2_claim_w : k_bfs2_claim, dim3(wave_claim ? 16 * grid : grid),
                      dim3(kBS), 0, s,
                      queue, st, pos_of, B.sx, B.sy, B.sz, G, B.tkeys, B.trange, B.tmask, r2,
                      processed_s, claim_s, cand, st, W.child_cnt, W.cursor, W.cell_done);
