@@ -2085,8 +2085,9 @@ void launch_bfs2_level(int32_t* queue, long long* st, const int32_t* pos_of, con
                        const GridBufs& B, float r2, uint8_t* processed_s, uint32_t* claim_s,
                        float4* nrm_s, int32_t* cand, const Bfs2Bufs& W, int grid, hipStream_t s,
                        bool wave_claim) {
-  // (the wave claim: 4x the workgroups, about one run of frontier nodes per wave -- more
-  // dependent candidate loads in flight per CU)
+  // (the wave claim: 16x the workgroups, about one run of kBqRun = 2 frontier nodes per wave --
+  // more dependent candidate loads in flight per CU: claim 171 -> 118 us per level at C5; runs
+  // of 8 / 4 / 1 with 4x / 8x / 32x: 146 / 131 / 139 us)
   hipLaunchKernelGGL(wave_claim ? k_bfs2_claim_w : k_bfs2_claim, dim3(wave_claim ? 16 * grid : grid),
                      dim3(kBS), 0, s,
                      queue, st, pos_of, B.sx, B.sy, B.sz, G, B.tkeys, B.trange, B.tmask, r2,
