@@ -1499,7 +1499,8 @@ void launch_list_materialize(PointsView pristine, int64_t n, const PointsOut& io
 void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, float margin,
                    const float4* coef, const ModelTest& mt, uint32_t* bits, hipStream_t s) {
   if (sp.n <= 0) return;
-  hipLaunchKernelGGL(k_ustamp, dim3(moments_sp_blocks(sp.n)), dim3(kMoBS), 0, s, sp, tiles, supers,
+  const int g = (int)std::max<int64_t>(1, std::min<int64_t>(4 * 256, sp_supers(sp.n)));
+  hipLaunchKernelGGL(k_ustamp, dim3(g), dim3(kMoBS), 0, s, sp, tiles, supers,
                      margin, coef, mt, bits);
 }
 
