@@ -107,6 +107,7 @@ struct NormalsWork {
   DevBuf<uint32_t> keys_in, keys_out, counters;
   DevBuf<int32_t> idx_in, queue, cand, ids, ids_alt, pos_of, nn;
   DevBuf<float4> nrm, nrm_s;
+  DevBuf<float4> rec;  // grid builds: the points as (x, y, z, 0) records for the sorted gather
   DevBuf<uint32_t> claim, ccnt, coffs, ccur, ctile, cslot, cdone;
   DevBuf<float> sd2;
   DevBuf<int32_t> ncnt;   // PCL-float radius normals: neighbours per query (chunk)
@@ -130,7 +131,7 @@ struct NormalsWork {
     keys_alt.release(); h_cnt.release(); ccnt.release(); coffs.release(); ccur.release(); cdone.release();
     sd2.release(); bst.release(); h_bst.release(); ctile.release(); cslot.release();
     ncnt.release(); noff.release(); nkeys.release();
-    ovfa.release(); ovfb.release(); ovfc.release();
+    ovfa.release(); ovfb.release(); ovfc.release(); rec.release();
   }
 };
 

@@ -104,10 +104,12 @@ __global__ __launch_bounds__(kBS) void k_cell_keys(const float* __restrict__ X,
                                                    const float* __restrict__ Y,
                                                    const float* __restrict__ Z, int n, GridDesc G,
                                                    uint32_t* __restrict__ keys,
-                                                   int32_t* __restrict__ idx) {
+                                                   int32_t* __restrict__ idx,
+                                                   float4* __restrict__ rec) {
   const int i = blockIdx.x * kBS + threadIdx.x;
   if (i >= n) return;
   const float x = X[i], y = Y[i], z = Z[i];
+  if (rec) rec[i] = make_float4(x, y, z, 0.0f);  // (k_cells_build's gather source)
   uint32_t k = G.ncells;  // non-finite: sorted last, never inserted
   if (finite3(x, y, z))
     k = cell_key(G, cell_of(x, G.lo[0], G.inv_cell, G.g[0]), cell_of(y, G.lo[1], G.inv_cell, G.g[1]),
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(kBS) void k_cells_build(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     uint32_t* __restrict__ tkeys, int2* __restrict__ trange, uint32_t tmask,
     float* __restrict__ sx, float* __restrict__ sy, float* __restrict__ sz,
-    uint32_t* __restrict__ n_occupied) {
+    uint32_t* __restrict__ n_occupied, const float4* __restrict__ rec) {
   __shared__ uint32_t s_occ;
   const int t = blockIdx.x * kBS + threadIdx.x;
   if (threadIdx.x == 0) s_occ = 0u;
@@ -138,9 +140,16 @@ __global__ __launch_bounds__(kBS) void k_cells_build(
   if (threadIdx.x == 0 && s_occ) atomicAdd(n_occupied, s_occ);
   if (!in) return;
   const int i = sidx[t];
-  sx[t] = X[i];
-  sy[t] = Y[i];
-  sz[t] = Z[i];
+  if (rec) {  // (one 16-byte record per point instead of three scattered floats)
+    const float4 v = rec[i];
+    sx[t] = v.x;
+    sy[t] = v.y;
+    sz[t] = v.z;
+  } else {
+    sx[t] = X[i];
+    sy[t] = Y[i];
+    sz[t] = Z[i];
+  }
   if (!first) return;
   uint32_t h = hash_key(k) & tmask;
   while (true) {
@@ -1857,19 +1866,20 @@ size_t sort_tmp_bytes(int n, int key_bits) {
 }
 
 hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, const GridDesc& G,
-                      GridBufs& B, uint32_t* n_occupied, hipStream_t s) {
+                      GridBufs& B, uint32_t* n_occupied, hipStream_t s, float4* rec) {
   hipError_t e = hipMemsetAsync(B.tkeys, 0xff, (size_t)(B.tmask + 1) * 4, s);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(n_occupied, 0, 16, s);  // [0] occupied cells, [2..3] sum of occupancy^2
   if (e != hipSuccess || n <= 0) return e;
   hipLaunchKernelGGL(k_cell_keys, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, X, Y, Z, n, G, B.keys_in,
-                     B.idx_in);
+                     B.idx_in, rec);
   size_t tmp = B.sort_tmp_bytes;
   e = hipcub::DeviceRadixSort::SortPairs(B.sort_tmp, tmp, B.keys_in, B.keys_out, B.idx_in,
                                          B.idx_out, n, 0, G.key_bits, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_cells_build, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.keys_out, B.idx_out, n,
-                     G.ncells, X, Y, Z, B.tkeys, B.trange, B.tmask, B.sx, B.sy, B.sz, n_occupied);
+                     G.ncells, X, Y, Z, B.tkeys, B.trange, B.tmask, B.sx, B.sy, B.sz, n_occupied,
+                     (const float4*)rec);
   hipLaunchKernelGGL(k_cells_end, dim3(cdiv(n, kBS)), dim3(kBS), 0, s, B.keys_out, n, G.ncells,
                      B.tkeys, B.trange, B.tmask,
                      reinterpret_cast<unsigned long long*>(n_occupied + 2));

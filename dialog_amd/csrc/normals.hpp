@@ -47,8 +47,10 @@ void launch_bbox(const float* X, const float* Y, const float* Z, int n, float* p
 size_t sort_tmp_bytes(int n, int key_bits);
 // sort by cell, fill the cell table; n_occupied (device, 16 B): [0] = occupied cells,
 // [2..3] = uint64 sum over cells of occupancy^2
+// rec (optional, n records of scratch): the points are first packed as (x, y, z, 0) records so
+// the sorted gather reads one 16-byte record per point instead of three scattered floats
 hipError_t grid_build(const float* X, const float* Y, const float* Z, int n, const GridDesc& G,
-                      GridBufs& B, uint32_t* n_occupied, hipStream_t s);
+                      GridBufs& B, uint32_t* n_occupied, hipStream_t s, float4* rec = nullptr);
 // strided host-layout xyz records (uploaded raw) -> SoA
 void launch_deinterleave(const float* raw, int n, int64_t stride_floats, float* X, float* Y,
                          float* Z, hipStream_t s);

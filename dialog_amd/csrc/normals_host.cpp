@@ -83,6 +83,8 @@ GridDesc make_grid(const BBox& b, double cell) {
 
 // builds grid level `lv` over (X, Y, Z) (default nw.x/y/z); returns the number of occupied cells
 // (and the point-weighted mean occupancy sum(occ^2) / n in *pw_occ)
+// (clouds from this size gather their sorted coordinates from packed records)
+constexpr int kGridRecMin = 1 << 16;
 uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B, const float* X,
                     const float* Y, const float* Z, double* pw_occ) {
   NormalsWork& w = c->nw;
@@ -103,8 +105,13 @@ uint32_t build_grid(dlg_ctx* c, int n, const GridDesc& G, int lv, GridBufs* B, c
   B->sx = L.sx.p; B->sy = L.sy.p; B->sz = L.sz.p;
   B->tkeys = L.tkeys.p; B->trange = L.trange.p; B->tmask = tcap - 1;
   B->sort_tmp = w.sort_tmp.p; B->sort_tmp_bytes = w.sort_tmp.cap;
+  float4* rec = nullptr;
+  if (n >= kGridRecMin) {
+    w.rec.ensure(n);
+    rec = w.rec.p;
+  }
   HIPCHK(grid_build(X ? X : w.x.p, Y ? Y : w.y.p, Z ? Z : w.z.p, n, G, *B, w.counters.p,
-                    c->stream));
+                    c->stream, rec));
   HIPCHK(hipMemcpyAsync(w.h_cnt.p, w.counters.p, 16, hipMemcpyDeviceToHost, c->stream));
   sync(c);
   if (pw_occ) {
