@@ -1155,17 +1155,14 @@ __global__ __launch_bounds__(kMoBS) void k_ustamp(PointsView src, const float4* 
 }
 
 // k_ucompact: bitmap -> the inliers' x, y, z in ascending pristine order (= list order), a
-// single pass with decoupled look-back (sel1_scan); each lane owns 2 consecutive words (64
-// points), clears them and ranks its inliers.  The gather is cooperative: the wave walks its 64
-// lanes' words in order, lane i taking point i of each (coalesced, masked 4-byte loads and
-// stores; four words in flight), so dense runs and sparse scatter cost the same.  The last tile
-// writes the count to *n_out.
+// single pass with decoupled look-back (sel1_scan); each lane owns one word (32 points), clears
+// it and ranks its inliers.  The gather is cooperative: the wave walks its lanes' words two at a
+// time (64 consecutive points), lane i taking point i of each pair (coalesced, masked 4-byte
+// loads and stores; four pairs in flight), so dense runs and sparse scatter cost the same.  (One
+// word per lane: twice the workgroups of round 4's two, 35.4 -> 31.5 us per round at C3.)  The
+// last tile writes the count to *n_out.
 constexpr int kUcBS = 256;
-constexpr int kUcWords = 2;  // words per lane
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
-         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
-}
+constexpr int kUcWords = 1;  // words per lane (two lanes' words form one 64-point gather step)
 __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits, int64_t nwords,
                                                     PointsView pristine, Sel1State L, int ntiles,
                                                     float* __restrict__ ox, float* __restrict__ oy,
@@ -1176,17 +1173,12 @@ __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits,
   const int tile = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int64_t w0 = ((int64_t)tile * kUcBS + threadIdx.x) * kUcWords;
-  uint64_t m = 0;
-  if (w0 + kUcWords <= nwords) {
-    uint2* p = reinterpret_cast<uint2*>(bits + w0);
-    const uint2 v = *p;
-    m = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    *p = make_uint2(0u, 0u);
-  } else if (w0 < nwords) {  // (the bitmap's last word)
+  uint32_t m = 0;
+  if (w0 < nwords) {
     m = bits[w0];
     bits[w0] = 0u;
   }
-  const int cnt = __popcll(m);
+  const int cnt = __popc(m);
   int incl = cnt;
 #pragma unroll
   for (int off = 1; off < kWave; off <<= 1) {
@@ -1203,13 +1195,16 @@ __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits,
   const int64_t wbase = ((int64_t)tile * kUcBS + w * kWave) * kUcWords * 32;  // the wave's point 0
   const uint32_t below_lo = lane < 32 ? (1u << lane) - 1u : 0xFFFFFFFFu;
   const uint32_t below_hi = lane < 32 ? 0u : (lane == 32 ? 0u : (1u << (lane - 32)) - 1u);
-  for (int s0 = 0; s0 < kWave; s0 += 4) {
+  // step k: the words of lanes s0 + 2k and s0 + 2k + 1 (64 consecutive points, the first
+  // lane's output position)
+  for (int s0 = 0; s0 < kWave; s0 += 8) {
     uint64_t mk[4];
     int ps[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      mk[k] = readlane64(m, s0 + k);
-      ps[k] = __builtin_amdgcn_readlane(pos, s0 + k);
+      mk[k] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m, s0 + 2 * k) |
+              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)m, s0 + 2 * k + 1) << 32);
+      ps[k] = __builtin_amdgcn_readlane(pos, s0 + 2 * k);
     }
     if ((mk[0] | mk[1] | mk[2] | mk[3]) == 0) continue;  // (wave-uniform)
     float x[4], y[4], z[4];
@@ -1218,7 +1213,7 @@ __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits,
     for (int k = 0; k < 4; ++k) {
       on[k] = ((mk[k] >> lane) & 1u) != 0;
       if (on[k]) {
-        const int64_t pi = wbase + (int64_t)(s0 + k) * 64 + lane;
+        const int64_t pi = wbase + (int64_t)(s0 + 2 * k) * 32 + lane;
         x[k] = pristine.x[pi]; y[k] = pristine.y[pi]; z[k] = pristine.z[pi];
       }
     }
