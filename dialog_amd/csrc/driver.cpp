@@ -422,7 +422,19 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   // Morton copies of the shards gives the list's bits.  Every rank decides alike: whether all
   // ranks hold a spatial copy is agreed once per extraction (c->sp_all), and the other inputs
   // -- the list lean, NORMAL_PLANE rounds dropping the copy -- evolve identically on every rank)
-  const bool lean = compact && !np && (!pcl_refit || pcl_dev) && c->opt.lean && cl->sp_valid &&
+  // NORMAL_PLANE over the Morton copy: the prefilter d_euclid < lim(w) holds for the cloud's
+  // largest w = lambda (1 - min curvature) when every w lies in [0, 1) (then lim is finite and
+  // monotone in w); NaN curvatures never pass PCL's test.  Otherwise the exhaustive kernel.
+  float np_lim = INFINITY;
+  if (np && cl->curv_known) {
+    const double w_max = prm.normal_distance_weight * (1.0 - (double)cl->curv_min);
+    const double w_min = prm.normal_distance_weight * (1.0 - (double)cl->curv_max);
+    if (w_min >= 0.0 && w_max < 1.0) np_lim = np_lim_max(w_max, prm.threshold);
+  }
+  // (NORMAL_PLANE: only with the pruned NP scorer -- every w in [0, 1), the copy carrying normals)
+  const bool np_lean_ok = !np || (cl->sp_valid && cl->sp_soa().with_nrm && c->opt.prune_np &&
+                                  np_lim < INFINITY);
+  const bool lean = compact && np_lean_ok && (!pcl_refit || pcl_dev) && c->opt.lean && cl->sp_valid &&
                     c->sp_all &&
                     cl->n_total < (int64_t(1) << 30) && c->opt.prune != 0 &&
                     (cl->cur < 0 || cl->buf_lean[cl->cur]);
@@ -441,15 +453,6 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   if (trace_on()) std::fprintf(stderr, "[dlg] segment start %.3fms ctl %.3fms\n", t_ctl0 - c->t_tot, now_ms() - t_ctl0);
   // pruned scoring over the spatial copy (plane model, default kernel, spatial copy in step)
   const bool pruned = !np && cl->sp_valid && c->opt.prune != 0;
-  // NORMAL_PLANE over the Morton copy: the prefilter d_euclid < lim(w) holds for the cloud's
-  // largest w = lambda (1 - min curvature) when every w lies in [0, 1) (then lim is finite and
-  // monotone in w); NaN curvatures never pass PCL's test.  Otherwise the exhaustive kernel.
-  float np_lim = INFINITY;
-  if (np && cl->curv_known) {
-    const double w_max = prm.normal_distance_weight * (1.0 - (double)cl->curv_min);
-    const double w_min = prm.normal_distance_weight * (1.0 - (double)cl->curv_max);
-    if (w_min >= 0.0 && w_max < 1.0) np_lim = np_lim_max(w_max, prm.threshold);
-  }
   const bool pruned_np = np && cl->sp_valid && cl->sp_soa().with_nrm && c->opt.prune != 0 &&
                          c->opt.prune_np && np_lim < INFINITY;
   const float pmargin = pruned ? prune_margin(cthr, cl->amax)
@@ -651,7 +654,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
   const bool sp_compact = compact && cl->sp_valid && (!np || cl->sp_soa().with_nrm);
   auto sp_cur_view = [&]() {
     const SoA& ss = cl->sp_soa();
-    return PointsView{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n, nullptr};
+    return PointsView{ss.x.p, ss.y.p, ss.z.p, ss.gid.p, cl->sp_n,
+                      np && ss.with_nrm ? ss.nrm.p : nullptr};
   };
   if (lean && cl->tag.cap < (size_t)cl->n_total) {
     cl->tag.ensure((size_t)std::max<int64_t>(cl->n_total, 1));

@@ -571,7 +571,7 @@ __global__ __launch_bounds__(kMoBS) void k_moments(PointsView src, const float4*
 // lean rounds (plane model over the Morton copy): only the tiles whose bounding sphere may hold an
 // inlier of cf are read -- k_prune_supers' test (a ruled-out sphere holds no point that passes
 // PCL's test), first per super-tile, then per tile.  The same digits as k_moments (integer sums).
-template <int MODE>
+template <int MODE, bool NP = false>
 __global__ __launch_bounds__(kMoBS) void k_moments_sp(PointsView src,
                                                       const float4* __restrict__ tiles,
                                                       const float4* __restrict__ supers,
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(kMoBS) void k_moments_sp(PointsView src,
       for (int j = 0; j < kIt; ++j) {
         const int64_t e = base + j * kWave + lane;
         if (((tm >> (2 * j + (lane >> 5))) & 1u) && e < src.n &&
-            model_in<false>(src, e, cf, cn, mt, x[j], y[j], z[j]))
+            model_in<NP>(src, e, cf, cn, mt, x[j], y[j], z[j]))
           mom_point(m, fast_q(x[j], qscale), fast_q(y[j], qscale), fast_q(z[j], qscale));
       }
       if (m.n != 0.0) mom_flush(acc, m);  // (kIt = kMomFlush points per lane per super-tile)
@@ -1113,6 +1113,7 @@ __global__ void k_list_materialize(PointsView pristine, int64_t n, PointsOut io)
 // k_ustamp: the Morton copy's tiles whose sphere may hold an inlier (k_moments_sp's walk) set the
 // bit of each inlier's pristine index (the copy's gid field).  The bitmap is all-zero on entry
 // (k_ucompact clears every word it reads).
+template <bool NP>
 __global__ __launch_bounds__(kMoBS) void k_ustamp(PointsView src, const float4* __restrict__ tiles,
                                                   const float4* __restrict__ supers, float margin,
                                                   const float4* __restrict__ cfp, ModelTest mt,
@@ -1147,7 +1148,7 @@ __global__ __launch_bounds__(kMoBS) void k_ustamp(PointsView src, const float4* 
       for (int j = 0; j < kIt; ++j) {
         const int64_t e = base + j * kWave + lane;
         if (((tm >> (2 * j + (lane >> 5))) & 1u) && e < src.n &&
-            model_in<false>(src, e, cf, cn, mt, x[j], y[j], z[j]))
+            model_in<NP>(src, e, cf, cn, mt, x[j], y[j], z[j]))
           atomicOr(bits + (g[j] >> 5), 1u << (g[j] & 31));
       }
     }
@@ -1495,8 +1496,9 @@ void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, flo
                    const float4* coef, const ModelTest& mt, uint32_t* bits, hipStream_t s) {
   if (sp.n <= 0) return;
   const int g = (int)std::max<int64_t>(1, std::min<int64_t>(4 * 256, sp_supers(sp.n)));
-  hipLaunchKernelGGL(k_ustamp, dim3(g), dim3(kMoBS), 0, s, sp, tiles, supers,
-                     margin, coef, mt, bits);
+  // (NORMAL_PLANE: the model test reads the copy's normals, sp.nrm; margin = the NP prune margin)
+  hipLaunchKernelGGL(mt.normal_plane ? k_ustamp<true> : k_ustamp<false>, dim3(g), dim3(kMoBS), 0, s,
+                     sp, tiles, supers, margin, coef, mt, bits);
 }
 
 int ucompact_tiles(int64_t nwords) { return (int)((nwords + kUcBS * kUcWords - 1) / (kUcBS * kUcWords)); }
@@ -1629,12 +1631,11 @@ void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers
                        const float4* coef, const ModelTest& mt, int qexp, int64_t* partials,
                        unsigned* done, int nblocks, int64_t* out, float4* cout, hipStream_t s) {
   const double qs = pow2d(kFastBits - qexp);
-  if (cout)
-    hipLaunchKernelGGL(k_moments_sp<1>, dim3(nblocks), dim3(kMoBS), 0, s, src, tiles, supers,
-                       margin, coef, mt, qs, partials, done, out, qexp, cout);
-  else
-    hipLaunchKernelGGL(k_moments_sp<0>, dim3(nblocks), dim3(kMoBS), 0, s, src, tiles, supers,
-                       margin, coef, mt, qs, partials, done, out, qexp, nullptr);
+  // (NORMAL_PLANE: the model test reads the copy's normals, src.nrm; margin = the NP prune margin)
+  auto* k = mt.normal_plane ? (cout ? k_moments_sp<1, true> : k_moments_sp<0, true>)
+                            : (cout ? k_moments_sp<1, false> : k_moments_sp<0, false>);
+  hipLaunchKernelGGL(k, dim3(nblocks), dim3(kMoBS), 0, s, src, tiles, supers, margin, coef, mt,
+                     qs, partials, done, out, qexp, cout);
 }
 
 void launch_moments(PointsView src, const float4* coef, const ModelTest& mt, int qexp,

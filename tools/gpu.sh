@@ -83,6 +83,8 @@ for s in "$@"; do
       python3 tools/pmc_kern.py k_score_tiles_ex,k_prune_supers "$L" > "$O/pmc_lds_summary.log" 2>&1 ;;
     c5prof) run c5prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5prof" -o run -- \
               python3 tools/c5_kernels.py ${arg//,/ } ;;
+    c5xprof) run c5xprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5xprof" -o run -- \
+              python3 tools/bench_c5.py 10000000 1 ;;
     knnprof) run knnprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/knnprof" -o run -- \
               python3 tools/knn_probe.py ;;
     walk) run walk 300 python3 -u tools/fs_walk_stats.py ${arg//,/ } ;;
