@@ -212,7 +212,9 @@ def test_lean_list_continue_segment_and_normal_plane(gpu_ctx, optimize):
     npp = D.make_params(0.05, max_iterations=100, model=D.SACMODEL_NORMAL_PLANE,
                         normal_distance_weight=0.1, optimize=optimize)
     e2 = D.extract_planes(cloud, npp, max_planes=1, min_inliers=10)
-    assert e2["stats"]["lean_rounds"] == 0  # (NORMAL_PLANE rounds read the list's coordinates)
+    # (round 5: a NORMAL_PLANE round is lean too when the pruned NP scorer applies and the list is
+    # still lean; either way its inliers are the oracle's)
+    assert e2["stats"]["lean_rounds"] in (0, 1)
     rem2 = np.setdiff1d(np.arange(p.shape[0]), e["inliers"]).astype(np.int32)
     r2 = O.sac_segment(p, 0.05, indices=rem2, max_iterations=100, normals=nrm,
                        normal_distance_weight=0.1, optimize=optimize)
