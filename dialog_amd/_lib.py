@@ -11,12 +11,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdialog_amd.so")  # (A/B tooling rebinds it: tools/with_lib.py)
 
 DLG_OK = 0
+DLG_ERR_INTERNAL = 6
+DLG_ERR_COMM = 4
 DLG_ERR_CAPACITY = 5
 DLG_SACMODEL_PLANE = 0
 DLG_SACMODEL_NORMAL_PLANE = 11
 DLG_REFIT_PCL = 0
 DLG_REFIT_FAST = 1
-ABI_VERSION = 4  # include/dialog_ransac.h DLG_ABI_VERSION: the structs below match that header
+ABI_VERSION = 5  # include/dialog_ransac.h DLG_ABI_VERSION: the structs below match that header
 
 SYMBOLS = [
     "dlg_abi_version", "dlg_status_string", "dlg_sac_params_default", "dlg_ctx_create",
@@ -31,7 +33,7 @@ SYMBOLS = [
     "dlg_sac_control_result", "dlg_cloud_build_spatial", "dlg_ctx_set_option",
     "dlg_ctx_get_option", "dlg_prune_stats", "dlg_estimate_normals_ex", "dlg_cloud_drop_spatial",
     "dlg_abi_struct_size", "dlg_float_sums", "dlg_cloud_estimate_normals", "dlg_plane_border",
-    "dlg_cloud_regulate_normals",
+    "dlg_cloud_regulate_normals", "dlg_shard_range",
 ]
 
 # context options (include/dialog_ransac.h): equivalent execution paths, identical results
@@ -50,6 +52,11 @@ DLG_OPT_FS_POISON = 12
 DLG_OPT_HYP_SHARD = 13
 DLG_OPT_FS_ONE_WALK = 14
 DLG_OPT_FS_SEGMENTS = 15
+DLG_OPT_FAULT_INJECT = 16
+DLG_OPT_SYNC_CHECK = 17
+DLG_OPT_COMM_TIMEOUT_MS = 18
+DLG_OPT_SEL1_TICKET = 19
+DLG_OPT_BOUNDS_STREAM = 20
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
 DLG_SCORE_EXACT = 0
@@ -174,6 +181,7 @@ def load():
     L.dlg_cloud_regulate_normals.argtypes = [vp, vp, C.c_int64, C.c_int, C.c_float,
                                              C.POINTER(C.c_uint8), i64p, fp, C.c_int64]
     L.dlg_refit_planes.argtypes = [C.POINTER(Planes), fp]
+    L.dlg_shard_range.argtypes = [C.c_int64, C.c_int, C.c_int, i64p, i64p, C.POINTER(C.c_int)]
     L.dlg_sac_control_create.argtypes = [pp, C.POINTER(SacParams), C.c_int64, C.c_int]
     L.dlg_sac_control_destroy.argtypes = [vp]
     L.dlg_sac_control_next.argtypes = [vp, i32p, C.c_int64, C.POINTER(C.c_int)]

@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -30,25 +31,80 @@ namespace dlg {
 enum class DType { I32, I64, F64, U8 };
 size_t dtype_size(DType t);
 
+// The group was aborted (a rank failed, or a collective timed out): thrown by every later
+// collective and wait of every rank of the group.  The group stays aborted -- its contexts can
+// only be destroyed -- like an RCCL communicator after ncclCommAbort.
+struct CommAborted : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 class Comm {
  public:
   virtual ~Comm() = default;
   int rank() const { return rank_; }
   int world() const { return world_; }
+  // collectives issued so far (the divergence check compares it over ranks)
+  uint64_t ops() const { return ops_; }
   // in-place elementwise sum over ranks (device buffer)
-  virtual void allreduce_sum(void* dev, size_t count, DType t, hipStream_t s) = 0;
-  virtual void allreduce_max_f64(double* dev, size_t count, hipStream_t s) = 0;
+  void allreduce_sum(void* dev, size_t count, DType t, hipStream_t s) {
+    enter();
+    do_allreduce_sum(dev, count, t, s);
+  }
+  void allreduce_max_f64(double* dev, size_t count, hipStream_t s) {
+    enter();
+    do_allreduce_max_f64(dev, count, s);
+  }
   // recv[r * count + i] = send_of_rank_r[i]   (device buffers; send may alias recv + rank*count)
-  virtual void allgather(const void* send, void* recv, size_t count, DType t, hipStream_t s) = 0;
+  void allgather(const void* send, void* recv, size_t count, DType t, hipStream_t s) {
+    enter();
+    do_allgather(send, recv, count, t, s);
+  }
   // point to point (stream-ordered; every send has its matching recv on the peer) and broadcast
   // of root's buffer to every rank (in place)
-  virtual void send(const void* dev, size_t count, DType t, int peer, hipStream_t s) = 0;
-  virtual void recv(void* dev, size_t count, DType t, int peer, hipStream_t s) = 0;
-  virtual void broadcast(void* dev, size_t count, DType t, int root, hipStream_t s) = 0;
+  void send(const void* dev, size_t count, DType t, int peer, hipStream_t s) {
+    enter();
+    do_send(dev, count, t, peer, s);
+  }
+  void recv(void* dev, size_t count, DType t, int peer, hipStream_t s) {
+    enter();
+    do_recv(dev, count, t, peer, s);
+  }
+  void broadcast(void* dev, size_t count, DType t, int root, hipStream_t s) {
+    enter();
+    do_broadcast(dev, count, t, root, s);
+  }
+
+  // Failure propagation (every rank returns a status).  abort(): this rank failed
+  // (why = its error); every peer blocked in, or entering, a collective or a host wait of the
+  // group gets CommAborted within milliseconds (loopback: the group's condition variables;
+  // RCCL: a poison word in a node-local shared-memory page named after the unique id, then
+  // ncclCommAbort so the device-side waits of the collectives end).  Idempotent.
+  virtual void abort(const std::string& why) { (void)why; }
+  // throws CommAborted if the group was aborted (by any rank) or the communicator reported an
+  // asynchronous error; host wait loops poll it
+  virtual void check() {}
+  // true when a collective makes the device wait for the peers (RCCL): host waits on a stream
+  // holding one must poll check() (sync_stream) instead of blocking in the HIP runtime
+  virtual bool device_waits() const { return false; }
+  // hipStreamSynchronize, or (device_waits) a polling wait that throws CommAborted when the group
+  // is aborted and aborts the group after timeout_ms without progress (0: no limit)
+  void sync_stream(hipStream_t s);
+  int64_t timeout_ms = 600000;
 
  protected:
+  virtual void do_allreduce_sum(void* dev, size_t count, DType t, hipStream_t s) = 0;
+  virtual void do_allreduce_max_f64(double* dev, size_t count, hipStream_t s) = 0;
+  virtual void do_allgather(const void* send, void* recv, size_t count, DType t, hipStream_t s) = 0;
+  virtual void do_send(const void* dev, size_t count, DType t, int peer, hipStream_t s) = 0;
+  virtual void do_recv(void* dev, size_t count, DType t, int peer, hipStream_t s) = 0;
+  virtual void do_broadcast(void* dev, size_t count, DType t, int root, hipStream_t s) = 0;
+  void enter() {
+    check();
+    ++ops_;
+  }
   int rank_ = 0;
   int world_ = 1;
+  uint64_t ops_ = 0;
 };
 
 std::unique_ptr<Comm> make_single_comm();

@@ -70,8 +70,25 @@ double now_ms() {
 void pump_pending(dlg_ctx* c, int64_t ids);
 
 void wait_published(dlg_ctx* c, int32_t seq) {
+  Comm* g = c->group();
+  const bool poll = g->world() > 1;
+  const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t k = 1;; ++k) {
     if (__atomic_load_n(c->pub, __ATOMIC_ACQUIRE) == seq) return;
+    // (several ranks: a failed peer's poison, or no progress within the group's timeout, ends
+    // the wait -- the round's collectives may be waiting for that peer on the device)
+    if (poll && (k & 255u) == 0) {
+      g->check();
+      if (g->timeout_ms > 0 && (k & 65535u) == 0) {
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                            std::chrono::steady_clock::now() - t0).count();
+        if (ms > g->timeout_ms) {
+          g->abort("rank " + std::to_string(g->rank()) + ": round not published after " +
+                   std::to_string(ms) + " ms (DLG_OPT_COMM_TIMEOUT_MS)");
+          g->check();
+        }
+      }
+    }
     // the staged ids go to the caller while we wait; until their copy has landed, its event is
     // queried only every 16th spin (a HIP API call takes the runtime lock)
     if (c->stage_ready || (k & 15u) == 0) pump_pending(c, 16384);
@@ -92,6 +109,10 @@ void wait_published(dlg_ctx* c, int32_t seq) {
 // a single-pass select's look-back failed (sticky word set): clear it and fail the call
 [[noreturn]] void sel1_failed(dlg_ctx* c) {
   (void)hipMemsetAsync(c->sel1_err.p, 0, sizeof(int32_t), c->stream);
+  if (c->sel1_tk.p) {  // (a failed launch may have left tickets untaken)
+    (void)hipMemsetAsync(c->sel1_tk.p, 0, sizeof(uint64_t), c->stream);
+    c->sel1.issued = 0;
+  }
   (void)hipStreamSynchronize(c->stream);
   throw DlgError(DLG_ERR_INTERNAL, "single-pass select did not complete (look-back gave up)");
 }
@@ -367,8 +388,14 @@ void ensure_sel1(dlg_ctx* c, int64_t n, int64_t min_tiles = 0) {
     c->sel1_err.ensure(1);
     HIPCHK(hipMemsetAsync(c->sel1_err.p, 0, sizeof(int32_t), c->stream));
   }
+  if (!c->sel1_tk.p) {
+    c->sel1_tk.ensure(1);
+    HIPCHK(hipMemsetAsync(c->sel1_tk.p, 0, sizeof(uint64_t), c->stream));
+    c->sel1.issued = 0;
+  }
   c->sel1.status = c->sel1_status.p;
   c->sel1.err = c->sel1_err.p;
+  c->sel1.ticket = c->opt.sel1_ticket ? reinterpret_cast<unsigned long long*>(c->sel1_tk.p) : nullptr;
 }
 
 void ensure_mom_done(dlg_ctx* c) {
@@ -679,6 +706,11 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // inliers (k_moments, centred on the winning sample), the double eigen33 refit in a
     // one-thread kernel, then the select with the refined plane read from device memory.  PCL
     // mode needs the host's sequential float sums in between.
+    // (tests: DLG_OPT_FAULT_INJECT -- this rank fails here, after the round's scoring
+    // collectives, while its peers go on into the refit's and the select's)
+    if (xs && c->opt.fault_round > 0 && xs->rounds == c->opt.fault_round - 1)
+      throw DlgError(DLG_ERR_INTERNAL, "injected fault (DLG_OPT_FAULT_INJECT) in extract round " +
+                                           std::to_string(xs->rounds));
     const int sk = c->sel_k;  // this round's pair of select timing events
     c->walk_rec[sk] = false;
     // the PCL refit walk's timing events (profiling only)
@@ -903,19 +935,36 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     spec_pending = false;
     if (lean) {
       // the list from the stamps (ids in list order; survivors' pristine indices), then the
-      // sphere bounds of the Morton survivors (count in totals[4]).  (Running the bounds on a
-      // second stream beside the list pass was tried and dropped: with 8 loopback contexts in
-      // one process, 24 streams on 4 hardware queues, a run hung.)
-      stage_wait();
-      launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv,
-                       cl->gid_ident ? nullptr : cl->pristine.gid.p, cl->id_base, c->sel1,
-                       c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream, c->opt.sel1_tile);
+      // sphere bounds of the Morton survivors (count in totals[4]).  DLG_OPT_BOUNDS_STREAM: the
+      // bounds on a second stream beside the list pass (independent passes over different
+      // buffers; forked after the Morton select, joined before anything later on the stream).
+      // (Round 5 dropped it after an 8-context loopback run hung; the cause was the single-pass
+      // selects' look-back, not the stream: DESIGN.md §6.)
       const int b = cl->sp_spare();
       SoA& sd = cl->sp_buf[b];
       cl->sp_tb[b].ensure((size_t)std::max<int64_t>(sp_tiles(cl->sp_n), 1));
       cl->sp_sb[b].ensure((size_t)std::max<int64_t>(sp_supers(cl->sp_n), 1));
-      launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
-                           cl->sp_sb[b].p, c->stream);
+      const bool side = c->opt.bounds_stream;
+      if (side) {
+        if (!c->sstream) {
+          HIPCHK(hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking));
+          HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+          HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(c->ev_fork, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->sstream, c->ev_fork, 0));
+        launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
+                             cl->sp_sb[b].p, c->sstream);
+        HIPCHK(hipEventRecord(c->ev_join, c->sstream));
+      }
+      stage_wait();
+      launch_sel1_list(lidx, src.n, cl->tag.p, (uint8_t)cl->tagv,
+                       cl->gid_ident ? nullptr : cl->pristine.gid.p, cl->id_base, c->sel1,
+                       c->inl_gid.p, dst.gid, c->totals.p + 2, c->stream, c->opt.sel1_tile);
+      if (side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      else
+        launch_sphere_bounds(sd.x.p, sd.y.p, sd.z.p, cl->sp_n, c->totals.p + 4, cl->sp_tb[b].p,
+                             cl->sp_sb[b].p, c->stream);
     } else {
       stage_wait();
       launch_select_tail(src, rc_dev, mt, c->tile_off_in.p, c->tile_off_out.p, c->inl_gid.p,
@@ -1066,6 +1115,41 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     std::fprintf(stderr, "[dlg] refit+select=%.3fms n_in=%lld\n", now_ms() - t_ref0,
                  (long long)out.n_in_local);
   return out;
+}
+
+// DLG_OPT_SYNC_CHECK: every rank's view of the round just run -- (round, model, global inliers,
+// coefficient bits, collectives issued so far) -- allgathered and compared; the first rank that
+// differs from rank 0 fails the call on every rank (and, through guarded_group, nothing waits)
+void check_in_step(dlg_ctx* c, int round, const SegOut& so) {
+  Comm* g = c->group();
+  const int W = g->world();
+  if (W == 1) return;
+  constexpr int K = 5;
+  int64_t mine[K];
+  uint32_t cb[4];
+  std::memcpy(cb, so.coeff, sizeof(cb));
+  mine[0] = round;
+  mine[1] = so.has_model ? so.n_in_global : -1;
+  mine[2] = (int64_t)(((uint64_t)cb[0] << 32) | cb[1]);
+  mine[3] = (int64_t)(((uint64_t)cb[2] << 32) | cb[3]);
+  mine[4] = (int64_t)g->ops();
+  c->gath64.ensure((size_t)K * (W + 1));
+  c->h_g64.ensure((size_t)K * W);
+  HIPCHK(hipMemcpyAsync(c->gath64.p + (size_t)K * W, mine, sizeof(mine), hipMemcpyHostToDevice,
+                        c->stream));
+  g->allgather(c->gath64.p + (size_t)K * W, c->gath64.p, K, DType::I64, c->stream);
+  HIPCHK(hipMemcpyAsync(c->h_g64.p, c->gath64.p, sizeof(mine) * W, hipMemcpyDeviceToHost,
+                        c->stream));
+  sync(c);
+  static const char* what[K] = {"round", "inliers", "coefficients", "coefficients", "collectives"};
+  for (int r = 1; r < W; ++r)
+    for (int k = 0; k < K; ++k)
+      if (c->h_g64.p[(size_t)K * r + k] != c->h_g64.p[k])
+        throw DlgError(DLG_ERR_INTERNAL,
+                       "ranks diverged in extract round " + std::to_string(round) + ": rank " +
+                           std::to_string(r) + "'s " + what[k] + " " +
+                           std::to_string(c->h_g64.p[(size_t)K * r + k]) + " vs rank 0's " +
+                           std::to_string(c->h_g64.p[k]));
 }
 
 // copy this rank's (or every rank's) refined inliers to the caller buffer
@@ -1318,6 +1402,7 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   c->pstats.release();
   c->sel1_status.release();
   c->sel1_err.release();
+  c->sel1_tk.release();
   c->lp.release();
   c->lp_n.release();
   c->fs_scr.release();
@@ -1330,6 +1415,12 @@ dlg_status dlg_ctx_destroy(dlg_ctx* c) {
     (void)hipStreamSynchronize(c->cstream);
     (void)hipStreamDestroy(c->cstream);
   }
+  if (c->sstream) {
+    (void)hipStreamSynchronize(c->sstream);
+    (void)hipStreamDestroy(c->sstream);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (auto& pr : c->ev_sel)
     for (auto& ev : pr)
       if (ev) (void)hipEventDestroy(ev);
@@ -1518,7 +1609,7 @@ namespace {
 struct HypShardScope {
   dlg_ctx* c;
   bool on;
-  explicit HypShardScope(dlg_ctx* ctx) : c(ctx), on(ctx->opt.hyp_shard && ctx->comm->world() > 1) {
+  HypShardScope(dlg_ctx* ctx, bool enable) : c(ctx), on(enable) {
     if (!on) return;
     if (!c->solo) c->solo = make_single_comm();
     std::swap(c->comm, c->solo);
@@ -1530,6 +1621,36 @@ struct HypShardScope {
     c->hcomm = nullptr;
   }
 };
+
+// whether a call on this cloud runs hypothesis-sharded.  DLG_OPT_HYP_SHARD -1 (default): when
+// every rank holds the same cloud -- the same ids (id_base, count, identity) and the same extent --
+// which is how SURVEY 8(e)'s small-N fallback is set up (dlg_shard_range hands every rank the
+// whole cloud when point shards would fall below the Morton-copy cut-off); point-sharding such a
+// replicated cloud would count every point once per rank.  Decided once per cloud (one allgather
+// of a signature; every rank decides alike).
+bool hyp_shard_on(dlg_ctx* c, dlg_cloud* cl) {
+  if (c->comm->world() == 1) return false;
+  if (c->opt.hyp_shard >= 0) return c->opt.hyp_shard == 1;
+  if (!cl->repl_known) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) {
+      for (int k = 0; k < 8; ++k) h = (h ^ ((v >> (8 * k)) & 0xFFu)) * 1099511628211ull;
+    };
+    mix((uint64_t)cl->n_points);
+    mix((uint64_t)cl->n_total);
+    mix((uint64_t)(uint32_t)cl->id_base);
+    mix(cl->gid_ident ? 1u : 0u);
+    uint32_t b[4];
+    std::memcpy(b, cl->amax, 12);
+    std::memcpy(b + 3, &cl->fmax, 4);
+    for (uint32_t v : b) mix(v);
+    std::vector<int64_t> all;
+    allgather_i64(c, (int64_t)(h >> 1), &all);
+    cl->repl = std::all_of(all.begin(), all.end(), [&](int64_t v) { return v == all[0]; });
+    cl->repl_known = true;
+  }
+  return cl->repl;
+}
 }  // namespace
 
 dlg_status dlg_sac_segment(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* prm, float coeff_out[4],
@@ -1539,8 +1660,8 @@ dlg_status dlg_sac_segment(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* prm,
   if (!inliers_out && cap > 0) return DLG_ERR_INVALID;
   dlg_sac_stats local;
   dlg_sac_stats* st = stats ? stats : &local;
-  HypShardScope hs(c);
-  return guarded(c, [&] {
+  return guarded_group(c, [&] {
+    HypShardScope hs(c, hyp_shard_on(c, cl));
     std::memset(coeff_out, 0, 4 * sizeof(float));
     *n_inliers = 0;
     SegOut so = segment_impl(c, cl, *prm, false, st, nullptr);
@@ -1574,8 +1695,8 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
   dlg_extract_stats* xs = stats ? stats : &local;
   std::memset(xs, 0, sizeof(*xs));
   auto t0 = std::chrono::steady_clock::now();
-  HypShardScope hs(c);
-  dlg_status s = guarded(c, [&] {
+  dlg_status s = guarded_group(c, [&] {
+    HypShardScope hs(c, hyp_shard_on(c, cl));
     *n_planes = 0;
     if (max_planes > 0) offsets_out[0] = 0;
     int64_t written = 0;
@@ -1597,6 +1718,7 @@ dlg_status dlg_extract_planes(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params* p
       if (N < floor_n) break;
       dlg_sac_stats st;
       SegOut so = segment_impl(c, cl, *prm, true, &st, xs, &active);
+      if (c->opt.sync_check) check_in_step(c, p, so);
       xs->rounds++;
       if (!so.has_model) break;
       if (so.lean) xs->lean_rounds++;
@@ -1785,7 +1907,22 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
       case DLG_OPT_NORMALS_FUSED: o.nbr_fused = value != 0; break;
       case DLG_OPT_REGULATE_WAVE: o.bfs_wave = value != 0; break;
       case DLG_OPT_FS_POISON: o.fs_poison = value != 0; break;
-      case DLG_OPT_HYP_SHARD: o.hyp_shard = value != 0; break;
+      case DLG_OPT_HYP_SHARD:
+        if (value < -1 || value > 1) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_HYP_SHARD: -1, 0 or 1");
+        o.hyp_shard = (int)value;
+        break;
+      case DLG_OPT_FAULT_INJECT:
+        if (value < 0) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FAULT_INJECT: >= 0");
+        o.fault_round = (int)value;
+        break;
+      case DLG_OPT_SYNC_CHECK: o.sync_check = value != 0; break;
+      case DLG_OPT_COMM_TIMEOUT_MS:
+        if (value < 0) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_COMM_TIMEOUT_MS: >= 0");
+        c->comm->timeout_ms = value;
+        if (c->solo) c->solo->timeout_ms = value;
+        break;
+      case DLG_OPT_SEL1_TICKET: o.sel1_ticket = value != 0; break;
+      case DLG_OPT_BOUNDS_STREAM: o.bounds_stream = value != 0; break;
       case DLG_OPT_FS_SEGMENTS:
         if (value < 1 || value > kFsSegMax) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_SEGMENTS: 1..16");
         o.fs_segments = (int)value;
@@ -1824,6 +1961,11 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_REGULATE_WAVE: *value = o.bfs_wave; break;
     case DLG_OPT_FS_POISON: *value = o.fs_poison; break;
     case DLG_OPT_HYP_SHARD: *value = o.hyp_shard; break;
+    case DLG_OPT_FAULT_INJECT: *value = o.fault_round; break;
+    case DLG_OPT_SYNC_CHECK: *value = o.sync_check; break;
+    case DLG_OPT_COMM_TIMEOUT_MS: *value = c->comm->timeout_ms; break;
+    case DLG_OPT_SEL1_TICKET: *value = o.sel1_ticket; break;
+    case DLG_OPT_BOUNDS_STREAM: *value = o.bounds_stream; break;
     case DLG_OPT_FS_ONE_WALK: *value = o.fs_protocol; break;
     case DLG_OPT_FS_SEGMENTS: *value = o.fs_segments; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;
@@ -1859,13 +2001,28 @@ dlg_status dlg_synchronize(dlg_ctx* c) {
 dlg_status dlg_allreduce_max_f64(dlg_ctx* c, double* v) {
   if (!c || !v) return DLG_ERR_INVALID;
   if (c->comm->world() == 1) return DLG_OK;
-  return guarded(c, [&] {
+  return guarded_group(c, [&] {
     c->scratch_f64.ensure(1);
     HIPCHK(hipMemcpyAsync(c->scratch_f64.p, v, 8, hipMemcpyHostToDevice, c->stream));
     c->comm->allreduce_max_f64(c->scratch_f64.p, 1, c->stream);
     HIPCHK(hipMemcpyAsync(v, c->scratch_f64.p, 8, hipMemcpyDeviceToHost, c->stream));
     sync(c);
   });
+}
+
+dlg_status dlg_shard_range(int64_t n_global, int rank, int world, int64_t* lo, int64_t* hi,
+                           int* replicated) {
+  if (n_global < 0 || world < 1 || rank < 0 || rank >= world || !lo || !hi) return DLG_ERR_INVALID;
+  const bool repl = world > 1 && n_global / world < kPruneMinPoints;
+  if (replicated) *replicated = repl ? 1 : 0;
+  if (repl) {
+    *lo = 0;
+    *hi = n_global;
+  } else {
+    *lo = n_global * rank / world;
+    *hi = n_global * (rank + 1) / world;
+  }
+  return DLG_OK;
 }
 
 dlg_status dlg_barrier(dlg_ctx* c) {

@@ -175,12 +175,21 @@ struct PathOptions {
   // refit's tail from the published sums every round, 3 = as 2 and the round's select is always
   // redone with the host's plane (exercises the path an uncertain transcendental takes)
   int pcl_dev = 1;
-  bool hyp_shard = false;  // every rank holds the whole cloud; rank r scores its slice of each
-                           // batch's hypotheses, the counts are allreduced (DLG_OPT_HYP_SHARD)
+  int hyp_shard = -1;  // every rank holds the whole cloud; rank r scores its slice of each
+                       // batch's hypotheses, the counts are allreduced (DLG_OPT_HYP_SHARD: 1 on,
+                       // 0 off, -1 = on when every rank holds the same cloud, ids included)
   int fs_protocol = 0;  // several ranks: the PCL refit's protocol (DLG_OPT_FS_ONE_WALK, 0..2)
   int fs_segments = 8;  // one rank: walkers per float chain (DLG_OPT_FS_SEGMENTS)
   bool fs_poison = false;  // tests only: fill the float-sum walk's window tables with garbage
                            // entries stamped for the next launch before the clear (fs_reset)
+  int fault_round = 0;     // tests only (DLG_OPT_FAULT_INJECT): > 0 = this rank throws in the
+                           // middle of extract round fault_round - 1 (after the round's scoring)
+  bool sync_check = false; // DLG_OPT_SYNC_CHECK: per-round allgather of (round, inliers,
+                           // coefficient bits, collectives issued), mismatch fails the call
+  bool sel1_ticket = true; // DLG_OPT_SEL1_TICKET: single-pass select tiles numbered by an atomic
+                           // ticket (dispatch order) instead of the workgroup index
+  bool bounds_stream = false;  // DLG_OPT_BOUNDS_STREAM: lean rounds' survivor sphere bounds on a
+                               // second stream beside the list pass (event-ordered)
 };
 
 struct dlg_ctx {
@@ -194,6 +203,8 @@ struct dlg_ctx {
   // round), `solo` holds the real one and `hcomm` points at it for the scoring's split
   std::unique_ptr<Comm> solo;
   Comm* hcomm = nullptr;
+  // the real communicator of the group (the one a failure must abort)
+  Comm* group() const { return hcomm ? hcomm : comm.get(); }
   std::string err;
   bool profiling = false;
   bool walk_events = false;  // (profiling level 1: the PCL refit walk's events too)
@@ -207,6 +218,8 @@ struct dlg_ctx {
   dlg::Sel1State sel1;  // single-pass selects: tile status words + launch epoch
   DevBuf<uint64_t> sel1_status;
   DevBuf<int32_t> sel1_err;  // sticky look-back failure word of the single-pass selects
+  DevBuf<uint64_t> sel1_tk;  // their tile ticket counter (DLG_OPT_SEL1_TICKET; never reset:
+                             // each launch's tickets start at the count issued before it)
   DevBuf<int64_t> partials, moments;  // fast refit: exact moment digits (exact_refit.hpp)
   DevBuf<unsigned> pick_done;          // the fused pick's workgroup ticket (zero between launches)
   DevBuf<unsigned> mom_done;           // k_moments' last-workgroup counter (zero between launches)
@@ -235,6 +248,10 @@ struct dlg_ctx {
   // the deferred inlier copy runs on its own stream, off the rounds' critical path: it waits for
   // ev_inl (the round's select on the main stream); the next select waits for ev_stage
   hipStream_t cstream = nullptr;
+  // DLG_OPT_BOUNDS_STREAM: the lean rounds' survivor sphere bounds on sstream beside the list
+  // pass (forked by ev_fork, joined by ev_join on the main stream); created on first use
+  hipStream_t sstream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_inl = nullptr;
   hipEvent_t ev_inl_cur = nullptr;    // the marker the copy waits for (ev_inl, or the round's
                                       // end-of-select timing event when profiling)
@@ -287,6 +304,8 @@ struct dlg_cloud {
   int64_t n_points = 0;  // records of the uploaded dlg_points (normals must match)
   int32_t id_base = 0;
   bool gid_ident = false;  // pristine gid[i] == id_base + i (uploaded without setIndices)
+  bool repl_known = false, repl = false;  // several ranks: every rank holds this same cloud
+                                          // (decided at the first call, hyp_shard_on)
   bool has_normals = false;
   // the attached normals as given (PCL's normal_x/y/z and curvature, pristine order): RegulateNormal
   // on the device copy (dlg_cloud_regulate_normals) flips these and re-derives the normalised ones
@@ -333,7 +352,8 @@ struct dlg_cloud {
 namespace dlg {
 
 inline void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
-inline void sync(dlg_ctx* c) { HIPCHK(hipStreamSynchronize(c->stream)); }
+// (several ranks over RCCL: a polling wait that ends when the group is aborted, comm.hpp)
+inline void sync(dlg_ctx* c) { c->group()->sync_stream(c->stream); }
 
 inline dlg_status fail(dlg_ctx* c, dlg_status code, const std::string& msg) {
   if (c) c->err = msg;
@@ -348,6 +368,8 @@ dlg_status guarded(dlg_ctx* c, F&& f) {
     f();
     if (c) c->err.clear();
     return DLG_OK;
+  } catch (const CommAborted& e) {
+    return fail(c, DLG_ERR_COMM, e.what());
   } catch (const DlgError& e) {
     return fail(c, e.code, e.what());
   } catch (const std::exception& e) {
@@ -355,6 +377,18 @@ dlg_status guarded(dlg_ctx* c, F&& f) {
   } catch (...) {
     return fail(c, DLG_ERR_INTERNAL, "unknown error");
   }
+}
+
+// guarded for the entry points whose ranks run collectives together: a rank that fails aborts
+// its group, so every peer returns DLG_ERR_COMM (naming this rank and its error) instead of
+// waiting in the next collective forever (the reference's convention: every caller gets a
+// status back, PlaneDetect.h:371-375, 592-596).  A failed group stays aborted.
+template <typename F>
+dlg_status guarded_group(dlg_ctx* c, F&& f) {
+  const dlg_status s = guarded(c, f);
+  if (s != DLG_OK && s != DLG_ERR_COMM && c && c->group()->world() > 1)
+    c->group()->abort("rank " + std::to_string(c->group()->rank()) + " failed: " + c->err);
+  return s;
 }
 
 // normals on the device -> the cloud (dlg_cloud_set_normals, dlg_cloud_estimate_normals)

@@ -1640,7 +1640,7 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
     for (int it = 0;; ++it) {
       comm->allgather(b.sums, b.gath2, 2 * kFsChains, DType::I32, s);
       HIPCHK_FS(hipMemcpyAsync(h.data(), b.gath2, 4 * h.size(), hipMemcpyDeviceToHost, s));
-      HIPCHK_FS(hipStreamSynchronize(s));
+      comm->sync_stream(s);
       bool exact = true;
       for (int q = 1; q < W && exact; ++q)
         for (int c = 0; c < kFsChains; ++c)

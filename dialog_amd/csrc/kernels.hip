@@ -840,16 +840,30 @@ struct S1 {
   static_assert(kSlots % kWave == 0 && kSlots <= BS, "slot scan layout");
 };
 
-// tile = workgroup index: workgroups are dispatched in index order on each XCD, so the lowest
-// unfinished tile has every predecessor done and always completes (a claim counter would be
-// one same-address device atomic per tile, measured slower).  The look-back still carries an
-// exit: after kS1Spin empty polls the tile gives up, scatters nothing, publishes flag 3 (failed)
-// and sets the sticky error word *L.err, which the last tile never writes; a tile whose
-// look-back meets a failed tile fails the same way.  (A successor may already have summed a
-// failed tile's aggregate and completed: only the sticky word is reliable, so the host checks
-// it -- in the round's publish for k_sel1_morton, at the next publish / the end of the
-// extraction for k_sel1_list.)
+// Tile numbering (sel1_tile_of).  With L.ticket (the default) a workgroup's tile is the ticket
+// it takes when it starts, so a tile's predecessors have all started -- they are resident or done
+// -- and the lowest unfinished tile of the launch can always finish, whatever else occupies the
+// device.  Numbering by workgroup index is only safe while the launch has the device to itself:
+// workgroups are dispatched in index order per XCD, not across XCDs, so beside another spinning
+// kernel (another context's select on the same device: the loopback groups of the tests) tile t
+// can spin on tile t - 1 whose XCD is full of the other kernel's spinning tiles, which wait in
+// turn on theirs -- a circular wait that only the spin limit below ends (measured: the round-5
+// 8-context hang).  The look-back still carries that exit: after kS1Spin empty
+// polls the tile gives up, scatters nothing, publishes flag 3 (failed) and sets the sticky error
+// word *L.err, which the last tile never writes; a tile whose look-back meets a failed tile fails
+// the same way.  (A successor may already have summed a failed tile's aggregate and completed:
+// only the sticky word is reliable, so the host checks it -- in the round's publish for
+// k_sel1_morton, at the next publish / the end of the extraction for k_sel1_list.)
 constexpr int kS1Spin = 1 << 20;
+
+__device__ __forceinline__ int sel1_tile_of(const Sel1State& L, int* s_tile) {
+  if (!L.ticket) return blockIdx.x;
+  if (threadIdx.x == 0)
+    *s_tile = (int)(__hip_atomic_fetch_add(L.ticket, 1ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) - L.base);
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(*s_tile);
+}
 
 // in-tile exclusive ranks from the (j, wave) counts in s_cnt, the tile's exclusive prefix by
 // look-back; returns the prefix (workgroup-uniform), s_pre[] = in-tile exclusive offsets
@@ -978,7 +992,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const flo
                                                        int32_t* __restrict__ totals, PubArgs pa) {
   constexpr int kS1Slots = S1<kS1BS>::kSlots, kS1Tile = S1<kS1BS>::kTile;
   __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
-  const int tile = blockIdx.x;
+  const int tile = sel1_tile_of(L, s_base);
   const float4 cf = *cfp;
   const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
   const int w = threadIdx.x / kWave;
@@ -1042,7 +1056,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__
                                                      int32_t* __restrict__ totals) {
   constexpr int kS1Slots = S1<kS1BS>::kSlots, kS1Tile = S1<kS1BS>::kTile;
   __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
-  const int tile = blockIdx.x;
+  const int tile = sel1_tile_of(L, s_base);
   const int w = threadIdx.x / kWave;
   const int64_t base = (int64_t)tile * kS1Tile;
   int32_t p[kS1It];
@@ -1171,7 +1185,7 @@ __global__ __launch_bounds__(kUcBS) void k_ucompact(uint32_t* __restrict__ bits,
                                                     int32_t* __restrict__ n_out) {
   constexpr int kSlots = S1<kUcBS>::kSlots;
   __shared__ int s_cnt[kSlots], s_pre[kSlots], s_base[2];
-  const int tile = blockIdx.x;
+  const int tile = sel1_tile_of(L, s_base);
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int64_t w0 = ((int64_t)tile * kUcBS + threadIdx.x) * kUcWords;
   uint32_t m = 0;
@@ -1407,7 +1421,14 @@ void launch_gather_build(const int32_t* pos_host, int D, PointsView src, SampleR
 int sel1_tiles(int64_t n) { return (int)((n + kSel1Points[0] - 1) / kSel1Points[0]); }
 
 // single-pass selects (lean-list rounds): every launch stamps its status words with a fresh epoch
-static void sel1_next(Sel1State& L, int) { ++L.epoch; }
+// and (tickets) the first ticket of the launch
+static void sel1_next(Sel1State& L, int nt) {
+  ++L.epoch;
+  if (L.ticket) {
+    L.base = L.issued;
+    L.issued += (uint64_t)nt;
+  }
+}
 
 template <bool NP, int BS>
 static void sel1_morton_bs(PointsView sp, const float4* coef, const ModelTest& mt, Sel1State& L,

@@ -130,6 +130,11 @@ struct Sel1State {
   uint64_t* status = nullptr;
   uint32_t epoch = 0;
   int32_t* err = nullptr;  // sticky: != 0 once a tile's look-back failed (host checks and clears)
+  // tile tickets (null: tile = workgroup index): a launch's workgroups take tickets base ..
+  // base + ntiles - 1 from *ticket in dispatch order; issued = the host's running total
+  unsigned long long* ticket = nullptr;
+  uint64_t base = 0;
+  uint64_t issued = 0;
 };
 // tiles (status words) a single-pass select over n points may use (the smallest tile size: an
 // upper bound for every kSel1Points choice)

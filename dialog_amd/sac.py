@@ -253,6 +253,17 @@ class Cloud:
             pass
 
 
+def shard_range(n_global: int, rank: int, world: int):
+    """dlg_shard_range: the part [lo, hi) of an n_global-point cloud rank `rank` uploads (its
+    contiguous shard; the whole cloud on every rank when shards would fall below the Morton-copy
+    cut-off -- those clouds then run hypothesis-sharded by default) -> (lo, hi, replicated)."""
+    L = _lib.load()
+    lo, hi, rep = C.c_int64(), C.c_int64(), C.c_int()
+    _lib.check(L.dlg_shard_range(int(n_global), int(rank), int(world), C.byref(lo), C.byref(hi),
+                                 C.byref(rep)))
+    return lo.value, hi.value, bool(rep.value)
+
+
 def make_params(threshold=0.0, max_iterations=50, probability=0.99, optimize=True, seed=12345,
                 refit_mode=DLG_REFIT_PCL, hypotheses_per_launch=0, gather_inliers=True,
                 model=SACMODEL_PLANE, normal_distance_weight=0.1):

@@ -40,15 +40,21 @@ extern "C" {
  * 4: dlg_extract_stats gained refit_repair_ms (refit_walk_ms is k_fs_walk alone on every rank);
  * DLG_OPT_FS_POISON; dlg_cloud_regulate_normals; DLG_OPT_HYP_SHARD; DLG_OPT_FS_ONE_WALK;
  * dlg_extract_stats gained refit_repairs; dlg_prune_stats fills 8 counters; DLG_OPT_FS_SEGMENTS;
- * the tile-scorer option's getter returns the value set */
-#define DLG_ABI_VERSION 4
+ * the tile-scorer option's getter returns the value set.
+ * 5: a failing rank aborts its group (peers return DLG_ERR_COMM); DLG_OPT_FAULT_INJECT,
+ * DLG_OPT_SYNC_CHECK, DLG_OPT_COMM_TIMEOUT_MS, DLG_OPT_SEL1_TICKET, DLG_OPT_BOUNDS_STREAM;
+ * DLG_OPT_HYP_SHARD defaults to -1 (automatic); dlg_shard_range */
+#define DLG_ABI_VERSION 5
 
 typedef enum {
   DLG_OK = 0,
   DLG_ERR_INVALID = 1,    /* bad argument */
   DLG_ERR_HIP = 2,        /* HIP runtime error */
   DLG_ERR_NO_DEVICE = 3,  /* no usable gfx950 device */
-  DLG_ERR_COMM = 4,       /* RCCL / communicator error */
+  DLG_ERR_COMM = 4,       /* RCCL / communicator error; several ranks: the group was aborted
+                             (a peer's call failed -- dlg_last_error names the rank and its
+                             error -- or a wait timed out).  An aborted group stays aborted:
+                             destroy its contexts */
   DLG_ERR_CAPACITY = 5,   /* output buffer too small; required size reported */
   DLG_ERR_INTERNAL = 6
 } dlg_status;
@@ -459,7 +465,10 @@ enum {
                                dlg_extract_planes split each batch's hypotheses over the ranks
                                (rank r scores its slice, the counts are allreduced; the rest of
                                the round runs on every rank alike: same results as one rank).
-                               0 (default): point sharding (each rank uploads its shard) */
+                               0: point sharding (each rank uploads its shard).  -1 (default):
+                               hypothesis sharding exactly when every rank holds the same cloud
+                               (same ids and extent), decided once per cloud -- the layout
+                               dlg_shard_range hands out when point shards would be too small */
   DLG_OPT_FS_ONE_WALK = 14, /* several ranks, PCL float refit (same sums every way): 0 (default)
                                = walk, rebase every rank on the guess the walks propagate, walk
                                again, then hand the exact chain ends rank to rank (each repair a
@@ -467,11 +476,28 @@ enum {
                                double-prefix guesses (the round-4 protocol, A/B only); 2 = 0 with
                                parallel repair iterations and host checks instead of the
                                hand-over (tests and A/B only) */
-  DLG_OPT_FS_SEGMENTS = 15  /* one rank, PCL float refit: walkers per float chain, 1..16 (default
+  DLG_OPT_FS_SEGMENTS = 15, /* one rank, PCL float refit: walkers per float chain, 1..16 (default
                                8): the chain's windows in segments walked at once from the refined
                                guesses, then joined in order (a segment whose guess was not its
                                exact start is walked again until it meets its recorded walk); 1 =
                                one walker per chain.  Same sums every way */
+  DLG_OPT_FAULT_INJECT = 16, /* tests only: k > 0 = this rank fails (DLG_ERR_INTERNAL) in the
+                               middle of extract round k - 1, after the round's scoring; 0
+                               (default).  Exercises the group abort: every peer returns
+                               DLG_ERR_COMM naming the failed rank */
+  DLG_OPT_SYNC_CHECK = 17,  /* several ranks, debug: 1 = after every extract round the ranks
+                               allgather (round, inliers, coefficient bits, collectives issued)
+                               and fail the call (aborting the group) on any mismatch; 0 (default) */
+  DLG_OPT_COMM_TIMEOUT_MS = 18, /* several ranks: a host wait on the group (a stream holding an
+                               RCCL collective, a round's results) that makes no progress for this
+                               long aborts the group (DLG_ERR_COMM on every rank); 0 = no limit;
+                               default 600000 */
+  DLG_OPT_SEL1_TICKET = 19, /* single-pass select tiles: 1 (default) numbered by an atomic ticket
+                               taken at dispatch (a tile's predecessors are always resident, so
+                               the look-back completes even beside other contexts' kernels on the
+                               same device); 0 = the workgroup index (A/B only) */
+  DLG_OPT_BOUNDS_STREAM = 20 /* lean rounds: 1 = the survivors' sphere bounds on a second stream
+                               beside the list pass (event-ordered both ways); 0 (default) */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
@@ -483,6 +509,14 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* ctx, int option, int64_t* value);
  * [5] blocks with a band re-decision (DLG_TILE_BF16 only), [6] / [7] (DLG_TILE_EXACT) the sum
  * and the maximum of the workgroups' spans in 100 MHz clock ticks (load balance) */
 dlg_status dlg_prune_stats(dlg_ctx* ctx, uint64_t out[8], int reset);
+
+/* The shard of an n_global-point cloud rank `rank` of `world` should upload:
+ * the contiguous range [*lo, *hi) of the global order, or -- when a shard would fall below the
+ * 131072-point Morton-copy cut-off (the pruned scorer's minimum) and world > 1 -- the whole cloud
+ * [0, n_global) on every rank, which DLG_OPT_HYP_SHARD's default (-1) then runs hypothesis-
+ * sharded.  *replicated = 1 in that case.  Host arithmetic; no context. */
+dlg_status dlg_shard_range(int64_t n_global, int rank, int world, int64_t* lo, int64_t* hi,
+                           int* replicated);
 
 /* max over ranks of a host double (bench timing) and a barrier; no-ops for world == 1 */
 dlg_status dlg_allreduce_max_f64(dlg_ctx* ctx, double* value);

@@ -49,7 +49,7 @@ def test_params_defaults_match_pcl():
     assert d.max_iterations == 50 and d.probability == 0.99 and d.optimize == 1
     assert d.seed == 12345 and d.model == 0 and d.threshold == 0.0
     assert p.max_iterations == 50
-    assert L.dlg_abi_version() == _lib.ABI_VERSION == 4
+    assert L.dlg_abi_version() == _lib.ABI_VERSION == 5
     assert L.dlg_status_string(0) == b"ok"
 
 

@@ -248,10 +248,12 @@ def test_c4shape_sharded_loopback(gpu_ctx, mode, proto):
 @pytest.mark.skipif("c2" not in DB, reason="fullsize.json has no c2")
 @pytest.mark.parametrize("mode", modes_of("c2"))
 def test_c2_hyp_sharded_loopback(gpu_ctx, mode):
-    """configs[1]'s 1M-point cloud on 8 ranks the way SURVEY 8(e) falls back for small N: point
-    shards would leave 125k points per rank, under the 131072-point Morton-copy cut-off, so every
-    rank holds the whole cloud (its own pruned scorer) and scores 512 of the 4096 hypotheses
-    (DLG_OPT_HYP_SHARD); the allreduced counts give the golden iterations, best sample and bits."""
+    """configs[1]'s 1M-point cloud on 8 ranks the way SURVEY 8(e) falls back for small N, with
+    default options: point shards would leave 125k points per rank, under the 131072-point
+    Morton-copy cut-off, so dlg_shard_range hands every rank the whole cloud (its own pruned
+    scorer), and DLG_OPT_HYP_SHARD's default sees the replicated cloud and splits the 4096
+    hypotheses 512 per rank; the allreduced counts give the golden iterations, best sample and
+    bits."""
     g = DB["c2"]["modes"][mode]
     p = cloud("c2")
     W = 8
@@ -260,8 +262,10 @@ def test_c2_hyp_sharded_loopback(gpu_ctx, mode):
 
     def run(r):
         try:
-            ctxs[r].set_option(D.DLG_OPT_HYP_SHARD, 1)
-            c = D.Cloud(ctxs[r], p)
+            lo, hi, rep = D.shard_range(p.shape[0], r, W)
+            assert rep and (lo, hi) == (0, p.shape[0])
+            assert ctxs[r].get_option(D.DLG_OPT_HYP_SHARD) == -1
+            c = D.Cloud(ctxs[r], p[lo:hi], id_base=lo)
             out[r] = D.segment_cloud(c, params(mode), capacity=p.shape[0])
             c.close()
         except Exception as ex:  # pragma: no cover

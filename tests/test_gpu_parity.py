@@ -197,13 +197,15 @@ def test_loopback_sharded_equals_single(gpu_ctx, world):
         c.close()
 
 
-@pytest.mark.parametrize("world,n,refit", [(2, 40000, "pcl"), (3, 300000, "fast"),
-                                           (5, 200000, "pcl")])
-def test_loopback_hyp_sharded_equals_oracle(gpu_ctx, world, n, refit):
+@pytest.mark.parametrize("world,n,refit,opt", [(2, 40000, "pcl", 1), (3, 300000, "fast", -1),
+                                               (5, 200000, "pcl", None)])
+def test_loopback_hyp_sharded_equals_oracle(gpu_ctx, world, n, refit, opt):
     """DLG_OPT_HYP_SHARD (SURVEY 8(e)'s small-N fallback): every in-process rank uploads the whole
     cloud and scores its slice of each batch's hypotheses (exhaustive kernels below the Morton
     copy's size, the pruned scorer above it), the counts are allreduced; every rank's segment()
-    and extract-and-remove equal the oracle's bit for bit."""
+    and extract-and-remove equal the oracle's bit for bit.  opt 1: set explicitly; -1 / None
+    (the default): chosen by the library because every rank holds the same cloud (a point-
+    sharded run would count each point once per rank and miss the oracle's counts)."""
     p, _, _ = plane_cloud(n, 6, seed=98 + world)
     mode = D.DLG_REFIT_PCL if refit == "pcl" else D.DLG_REFIT_FAST
     prm = D.make_params(0.02, max_iterations=511, probability=1.0, refit_mode=mode)
@@ -216,7 +218,8 @@ def test_loopback_hyp_sharded_equals_oracle(gpu_ctx, world, n, refit):
 
     def run(r):
         try:
-            ctxs[r].set_option(D.DLG_OPT_HYP_SHARD, 1)
+            if opt is not None:
+                ctxs[r].set_option(D.DLG_OPT_HYP_SHARD, opt)
             c = D.Cloud(ctxs[r], p)
             out[r] = D.extract_planes(c, prm, max_planes=6, min_inliers=200, capacity=p.shape[0])
             c.reset()
