@@ -22,7 +22,8 @@ with its PMC traffic, issue view and the work the pruning leaves (pruned_work). 
 the same JSON object: refit_fast (DLG_REFIT_FAST, an exact least-squares refit -- NOT PCL's
 arithmetic: its planes differ from PCL's), incl_index_build (the Morton copy + spheres rebuilt
 every step), secondary (C5).  cpu_baseline: the PCL-1.8 restatement (oracle) on the box's host
-cores (16 OpenMP threads for countWithinDistance, plus a single-thread sample), rank 0 at N = 1.
+cores (every CPU of the process's affinity mask for countWithinDistance; the box's 16-CPU share
+and a single-thread sample beside it), rank 0 at N = 1.
 """
 from __future__ import annotations
 
@@ -567,28 +568,54 @@ def main():
                     break
         except OSError:
             pass
-        # the all-core leg: the oracle's countWithinDistance over cpu_threads OpenMP threads
-        # (integer sums: the same counts), one full first round of 4096 hypotheses
-        thr = max(1, min(a.cpu_threads, os.cpu_count() or 1))
-        O.set_threads(thr)
-        t0 = time.perf_counter()
-        r = O.sac_segment(pts, a.threshold, max_iterations=a.hyps - 1, probability=1.0)
-        cdt = time.perf_counter() - t0
+        # three legs of the oracle's segment() (countWithinDistance over OpenMP threads; integer
+        # sums: the same counts): every host CPU the process may run on (the headline cpu leg),
+        # the box's CPU share (--cpu-threads, 16 on the GPU box), and one thread (PCL 1.8's
+        # RANSAC is serial)
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except AttributeError:
+            affinity = os.cpu_count() or 1
+        quota = None  # the cgroup's CPU limit (cpu.max "quota period"), in CPUs
+        try:
+            q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
+        try:
+            numa = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node")])
+        except OSError:
+            numa = None
+
+        def seg_leg(threads, hyps):
+            O.set_threads(threads)
+            t0 = time.perf_counter()
+            r = O.sac_segment(pts, a.threshold, max_iterations=hyps - 1, probability=1.0)
+            dt = time.perf_counter() - t0
+            return r["iterations"] * pts.shape[0] / dt / 1e9, dt
+
+        v_all, dt_all = seg_leg(affinity, a.hyps)
+        thr = max(1, min(a.cpu_threads, affinity))
+        v_share, dt_share = seg_leg(thr, a.hyps)
+        v_one, dt_one = seg_leg(1, a.cpu_hyps)
         O.set_threads(1)
-        t1 = time.perf_counter()
-        r1 = O.sac_segment(pts, a.threshold, max_iterations=a.cpu_hyps - 1, probability=1.0)
-        cdt1 = time.perf_counter() - t1
-        cpu = {"value": round(r["iterations"] * pts.shape[0] / cdt / 1e9, 4),
-               "unit": "G point-plane tests/s", "cores": thr, "kind": "port",
+        cpu = {"value": round(v_all, 4),
+               "unit": "G point-plane tests/s", "cores": affinity, "kind": "port",
                "sample": f"one PCL SACSegmentation::segment (the first extraction round) on the "
                          f"same {pts.shape[0]}-pt cloud with {a.hyps} hypotheses + refit + select, "
-                         f"oracle/pcl_oracle.c with countWithinDistance over {thr} OpenMP threads, "
-                         f"{cdt:.1f} s",
+                         f"oracle/pcl_oracle.c with countWithinDistance over {affinity} OpenMP "
+                         f"threads (every CPU in the process's affinity mask; OpenMP static "
+                         f"schedule, threads placed by the OS over {numa} NUMA node(s); cgroup CPU "
+                         f"quota {quota if quota is not None else 'none'}), {dt_all:.1f} s",
+               "share": {"value": round(v_share, 4), "cores": thr,
+                         "sample": f"the same segment() over {thr} threads (the GPU box's CPU "
+                                   f"share per GPU), {dt_share:.1f} s"},
                "single_thread": {
-                   "value": round(r1["iterations"] * pts.shape[0] / cdt1 / 1e9, 4), "cores": 1,
+                   "value": round(v_one, 4), "cores": 1,
                    "sample": f"the same segment() with {a.cpu_hyps} hypotheses, one thread (PCL "
-                             f"1.8's RANSAC is serial), {cdt1:.1f} s"},
-               "host_cpu": model, "host_nproc": os.cpu_count()}
+                             f"1.8's RANSAC is serial), {dt_one:.1f} s"},
+               "host_cpu": model, "host_nproc": os.cpu_count(), "affinity_cpus": affinity,
+               "cgroup_cpu_quota": quota, "numa_nodes": numa}
 
     if rank == 0:
         xchg = ("RCCL allreduce of the hypotheses' counts; the PCL refit's nine float chains "

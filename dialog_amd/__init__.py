@@ -16,7 +16,7 @@ from .postprocess import (PostProcessParams, cluster_filter, plane_border,  # no
                           post_process_planes, refit_planes)
 from ._lib import DLG_REFIT_FAST, DLG_REFIT_PCL, LIB_PATH  # noqa: F401
 from ._lib import (DLG_OPT_LEAN_ROUNDS, DLG_OPT_PCL_REFIT_DEVICE, DLG_OPT_PRUNE,  # noqa: F401
-                   DLG_OPT_NORMALS_FUSED, DLG_OPT_PRUNE_NP, DLG_OPT_PRUNE_TILE_SCORER, DLG_TILE_BF16, DLG_TILE_EXACT,
+                   DLG_OPT_NORMALS_FUSED, DLG_OPT_PRUNE_NP, DLG_OPT_PRUNE_TILE_SCORER, DLG_TILE_BF16, DLG_TILE_EXACT, DLG_TILE_MFMA,
                    DLG_OPT_PRUNE_STATS, DLG_OPT_SCORE_KERNEL, DLG_OPT_SELECT_TILE,
                    DLG_OPT_REGULATE_WAVE, DLG_OPT_SPEC_PICK, DLG_OPT_FS_POISON, DLG_OPT_HYP_SHARD, DLG_OPT_FS_ONE_WALK, DLG_OPT_FS_SEGMENTS,
                    DLG_OPT_FAULT_INJECT, DLG_OPT_SYNC_CHECK, DLG_OPT_COMM_TIMEOUT_MS, DLG_OPT_SEL1_TICKET,

@@ -59,6 +59,7 @@ DLG_OPT_SEL1_TICKET = 19
 DLG_OPT_BOUNDS_STREAM = 20
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
+DLG_TILE_MFMA = 2
 DLG_SCORE_EXACT = 0
 DLG_SCORE_BF16 = 1
 DLG_SCORE_PRUNED = 2

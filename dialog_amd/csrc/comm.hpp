@@ -43,7 +43,8 @@ class Comm {
   virtual ~Comm() = default;
   int rank() const { return rank_; }
   int world() const { return world_; }
-  // collectives issued so far (the divergence check compares it over ranks)
+  // collectives (not point-to-point ops) issued so far: the divergence check compares it over
+  // ranks (sends and receives differ by rank position in the PCL refit's hand-over chain)
   uint64_t ops() const { return ops_; }
   // in-place elementwise sum over ranks (device buffer)
   void allreduce_sum(void* dev, size_t count, DType t, hipStream_t s) {
@@ -62,11 +63,11 @@ class Comm {
   // point to point (stream-ordered; every send has its matching recv on the peer) and broadcast
   // of root's buffer to every rank (in place)
   void send(const void* dev, size_t count, DType t, int peer, hipStream_t s) {
-    enter();
+    check();
     do_send(dev, count, t, peer, s);
   }
   void recv(void* dev, size_t count, DType t, int peer, hipStream_t s) {
-    enter();
+    check();
     do_recv(dev, count, t, peer, s);
   }
   void broadcast(void* dev, size_t count, DType t, int root, hipStream_t s) {

@@ -1934,7 +1934,8 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
       case DLG_OPT_PRUNE_TILE_SCORER:
         // (DLG_TILE_* values, and the A/B-only kernel variants kTileScorerExK1/ExK4/ExPk and
         // claim variants 15..17)
-        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != kTileScorerExK1 &&
+        if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != DLG_TILE_MFMA &&
+            value != kTileScorerExK1 &&
             value != kTileScorerExK4 && value != kTileScorerExPk &&
             !(value >= kTileScorerClaimR4 && value <= kTileScorerClaimTail))
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");

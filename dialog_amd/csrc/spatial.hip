@@ -704,6 +704,102 @@ __device__ __forceinline__ int nth_set_bit(uint32_t v, int r) {
   return pos + (r >= (int)(v & 1u) ? 1 : 0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// MFMA tile scorer (DLG_TILE_MFMA): a tile's near planes in groups of 16 (its ring segment padded
+// to a multiple of 16 with "far" planes), each group scored against the tile's 32 points by two
+// v_mfma_f32_16x16x4_f32 (A = 16 points x (x, y, z, 1), B = (a, b, c, d) x 16 planes; lane l
+// supplies A[l & 15][l >> 4] and B[l >> 4][l & 15] and receives D[4 (l >> 4) + r][l & 15], i.e.
+// four points of its own plane per MFMA; tools/mfma_f32_probe.hip checks the maps).  The matrix
+// core evaluates each dot as an f32 fma chain, not in PCL's order ((a x + c z) + (b y + d), six
+// roundings): |D - pcl| <= (4 + 4.25) u S with S = |a| ax + |b| ay + |c| az + |d| (u = 2^-24,
+// ax.. the cloud's largest |coordinate|; each order's error <= the sum of its partial sums'
+// roundings).  With band = 12 u S (+ 2^-100), |D| < cthr - band is a PCL inlier and |D| >=
+// cthr + band is not; the rest (a few in 10^4 tests, and NaN: points past n) are re-decided with
+// PCL's own arithmetic from the LDS tile slot, so the counts equal the exact scorer's.  Per
+// 256 tests: one MFMA on the matrix pipe and ~3 VALU per result (two compares, one add) instead
+// of 8 VALU per test.  (Up to 4 groups per pass, their 8 MFMAs issued before any result is read.)
+constexpr int kMfG = 16;
+constexpr int kMfPass = 2;  // groups per pass (their MFMAs issued before any result is read)
+__device__ __forceinline__ void mf_pass(int m, const uint16_t* ring, int head, const float* spt,
+                                        const float4* s_cf, uint32_t* s_cnt, int lane, float cthr,
+                                        float ax, float ay, float az) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  constexpr int G = kMfPass;
+  const int ng = m >> 4;  // groups (m: a multiple of 16, <= 16 G)
+  const int k = lane >> 4, c = lane & 15;
+  f32x4v d0[G], d1[G];
+  float band[G];
+  int jj[G], sb[G];  // the lane's plane (pad: bit 12 set) and tile-slot base, per group
+  const f32x4v zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (g < ng) {
+      const uint32_t e = ring[(head + kMfG * g + c) & (kExRing - 1)];
+      jj[g] = (int)(e & 0xFFFu) | (e & kExPad ? 0x1000 : 0);
+      float4 q = s_cf[e & 0xFFFu];
+      // a pad: a plane 2^100 away (never near, never ambiguous, counts nothing)
+      if (e & kExPad) q = make_float4(0.f, 0.f, 0.f, 0x1p100f);
+      const float S = ((fabsf(q.x) * ax + fabsf(q.y) * ay) + fabsf(q.z) * az) + fabsf(q.w);
+      band[g] = S * (12.0f * 0x1p-24f * (1.0f + 0x1p-16f)) + 0x1p-100f;
+      const float b = k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
+      sb[g] = (int)((e >> 12) & 3u) * kExSlotF;
+      const float* sl = spt + sb[g];
+      const int kk = k < 3 ? k : 2;  // (lanes of k = 3 supply the 1 of (x, y, z, 1))
+      const float a0 = k < 3 ? sl[kk * kTileP + c] : 1.0f;
+      const float a1 = k < 3 ? sl[kk * kTileP + 16 + c] : 1.0f;
+      d0[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, zero, 0, 0, 0);
+      d1[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, zero, 0, 0, 0);
+    }
+  }
+  // per result t = |D| - cthr: a sure inlier when t < -band; the group is ambiguous on this lane
+  // when the smallest |t| is below band (NaN results -- points past n -- compare false and are
+  // skipped by the min: never counted, as PCL's NaN < thr)
+  uint32_t cnt[G];
+  bool amb[G];
+  bool any = false;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    cnt[g] = 0u;
+    amb[g] = false;
+    if (g < ng) {
+      float mn = INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t0 = fabsf(d0[g][r]) - cthr, t1 = fabsf(d1[g][r]) - cthr;
+        cnt[g] += t0 < -band[g] ? 1u : 0u;
+        cnt[g] += t1 < -band[g] ? 1u : 0u;
+        mn = fminf(mn, fminf(fabsf(t0), fabsf(t1)));
+      }
+      amb[g] = mn < band[g];
+      any = any || amb[g];
+    }
+  }
+  if (ballot(any) != 0ull) {
+    // re-decide the lane's 8 results of an ambiguous group with PCL's arithmetic (points from
+    // the LDS slot, the plane from LDS)
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (amb[g]) {
+        const float4 q = s_cf[jj[g] & 0xFFF];  // (never a pad: a pad is never ambiguous)
+        const float* sl = spt + sb[g];
+        uint32_t e = 0u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pt = 16 * h + 4 * k + r;
+            const float dd = pcl_dot(q.x, q.y, q.z, q.w, sl[pt], sl[kTileP + pt], sl[2 * kTileP + pt]);
+            e += fabsf(dd) < cthr ? 1u : 0u;
+          }
+        cnt[g] = e;
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    if (g < ng && cnt[g]) atomicAdd(&s_cnt[(jj[g] & 0xFFF) >> 1], cnt[g] << (16 * (jj[g] & 1)));
+}
+
 // NPM (SACMODEL_NORMAL_PLANE, K = 2): the pass evaluates PCL's prefilter b = (1 - w) d_euclid <
 // thr as the float compare d_euclid < lim with the point's lim (np_de_limit, computed once when
 // the point is fetched, stored in its slot), each lane collecting its 2 x 32 verdicts as bits;
@@ -711,7 +807,7 @@ __device__ __forceinline__ int nth_set_bit(uint32_t v, int r) {
 // (prefix sum of the lanes' bit counts, owner lane by a DPP max-scan of the chunk's first
 // positions) and decided with PCL's double arithmetic (np_full, as k_score_np), the normal read
 // from global memory.  Same counts as k_score_tiles_rl<NPM> and k_score_np.
-template <int BS, int K, bool PK = false, bool NPM = false>
+template <int BS, int K, bool PK = false, bool NPM = false, bool MF = false>
 __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
     const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
@@ -720,9 +816,14 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     int D, float cthr, float margin, int32_t* __restrict__ counts,
     unsigned long long* __restrict__ stats, PickArgs pick_args,
     const float4* __restrict__ NRM = nullptr, double lambda = 0.0, double thr = 0.0,
-    const float4* __restrict__ CN = nullptr, int tail = 1) {
+    const float4* __restrict__ CN = nullptr, int tail = 1, float ax = 0.f, float ay = 0.f,
+    float az = 0.f) {
   static_assert(K == 1 || K == 2 || K == 4, "planes per lane");
   static_assert(!NPM || (K == 2 && !PK), "NORMAL_PLANE: two planes per lane");
+  static_assert(!MF || (K == 2 && !PK && !NPM), "MFMA groups: plane model");
+  // ring segment granularity: K entries (lanes as planes), or 16 planes of one tile (MFMA)
+  constexpr int kSeg = MF ? kMfG : K;
+  constexpr int kPassN = MF ? kMfPass * kMfG : K * kWave;  // queued entries one pass takes
   constexpr int kChunk = 2;  // tiles per item
   constexpr int kSlotF = NPM ? kExSlotNp : kExSlotF;
   __shared__ float4 s_cf[kMaxHypPerLaunch];
@@ -823,6 +924,11 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   // K l .. K l + K - 1 (one tile, K planes), so each point read from LDS serves K planes
   auto pass = [&](int m) __attribute__((always_inline)) {
     if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
+    if constexpr (MF) {
+      mf_pass(m, ring, head, spt, s_cf, s_cnt, lane, cthr, ax, ay, az);
+      head += m;
+      return;
+    }
     const bool act = lane * K < m;
     uint32_t e[K];
     if constexpr (K == 1) {
@@ -944,12 +1050,12 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   };
   // close a tile segment: pad it to a multiple of K entries (one tile per lane item)
   auto pad = [&](uint32_t tag) {
-    if constexpr (K > 1) {
-      const int r = (K - (nq & (K - 1))) & (K - 1);
+    if constexpr (kSeg > 1) {
+      const int r = (kSeg - (nq & (kSeg - 1))) & (kSeg - 1);
       if (lane < r) ring[(nq + lane) & (kExRing - 1)] = (uint16_t)(tag | kExPad);
       nq += r;
       __builtin_amdgcn_wave_barrier();
-      while (nq - head >= K * kWave) pass(K * kWave);
+      while (nq - head >= kPassN) pass(kPassN);
     }
   };
   int it_next = claim();
@@ -1037,7 +1143,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
           if (n3) ring[(nq + k2 + lanes_below(m3)) & (kExRing - 1)] = (uint16_t)(tag | (uint32_t)j3);
           nq += k2 + (int)__popcll(m3);
           __builtin_amdgcn_wave_barrier();
-          while (nq - head >= K * kWave) pass(K * kWave);
+          while (nq - head >= kPassN) pass(kPassN);
         };
         uint32_t R[kListRegs];
 #pragma unroll
@@ -1259,7 +1365,18 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     hipExtLaunchKernelGGL((k_score_tiles_ex<kBS, 2, false, true>), dim3((unsigned)g), dim3(kBS), 0, s,
                           nullptr, ev_stop, 0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work,
                           blk_cap, xcd, order, hyps, D, cthr, margin, counts, stats,
-                          pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr, np->cn, tail);
+                          pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr, np->cn, tail,
+                          0.f, 0.f, 0.f);
+    return;
+  }
+  // (the MFMA scorer's rounding band is S x 12 u with S up to (ax + ay + az) + |d|: clouds whose
+  // coordinates would overflow it take the exact scorer)
+  if (ex && tile_scorer == kTileScorerMfma && (double)amax[0] + amax[1] + amax[2] < 1e30) {
+    hipExtLaunchKernelGGL((k_score_tiles_ex<kBS, 2, false, false, true>), dim3((unsigned)g),
+                          dim3(kBS), 0, s, nullptr, ev_stop, 0u, v.x, v.y, v.z, (int)v.n, v.tiles,
+                          lp, ls, lp_n, work, blk_cap, xcd, order, hyps, D, cthr, margin, counts,
+                          stats, pick ? *pick : PickArgs{}, (const float4*)nullptr, 0.0, 0.0,
+                          (const float4*)nullptr, tail, amax[0], amax[1], amax[2]);
     return;
   }
   if (ex) {
@@ -1270,7 +1387,8 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
     hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
                           0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, xcd,
                           order, hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{},
-                          (const float4*)nullptr, 0.0, 0.0, (const float4*)nullptr, tail);
+                          (const float4*)nullptr, 0.0, 0.0, (const float4*)nullptr, tail, 0.f, 0.f,
+                          0.f);
     return;
   }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;

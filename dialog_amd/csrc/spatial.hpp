@@ -79,6 +79,7 @@ inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
 // (k_score_tiles_rl); identical counts
 constexpr int kTileScorerExact = 0;   // k_score_tiles_ex<2> (default)
 constexpr int kTileScorerBf16 = 1;    // k_score_tiles_rl
+constexpr int kTileScorerMfma = 2;    // k_score_tiles_ex<2, MF>: 16-plane groups on f32 MFMA
 // A/B-only variants (same counts; tests/test_score_variants.py runs each)
 constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14;
 constexpr int kTileScorerExPk = 12;

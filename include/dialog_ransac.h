@@ -499,7 +499,7 @@ enum {
   DLG_OPT_BOUNDS_STREAM = 20 /* lean rounds: 1 = the survivors' sphere bounds on a second stream
                                beside the list pass (event-ordered both ways); 0 (default) */
 };
-enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1 };
+enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1, DLG_TILE_MFMA = 2 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };
 dlg_status dlg_ctx_set_option(dlg_ctx* ctx, int option, int64_t value);
 dlg_status dlg_ctx_get_option(const dlg_ctx* ctx, int option, int64_t* value);

@@ -90,6 +90,7 @@ def lib():
         L.orc_normal_plane_dist.restype = C.c_double
         L.orc_estimate_normals.argtypes = [fp, C.c_int64, C.c_int64, C.c_float, fp, fp]
         L.orc_estimate_normals_knn.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, fp, fp]
+        L.orc_estimate_normals_knn_brute.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, fp, fp]
         L.orc_orient_normals_nn.argtypes = [fp, C.c_int64, C.c_int64, fp, fp, C.c_int64,
                                             C.c_int64, fp]
         L.orc_preprocess.argtypes = [fp, C.c_int64, C.c_int64, C.c_int, C.c_float, fp, i32p, fp]
@@ -316,11 +317,13 @@ def estimate_normals(points, radius, viewpoint=(0.0, 0.0, 0.0)):
     return out
 
 
-def estimate_normals_knn(points, k, viewpoint=(0.0, 0.0, 0.0)):
+def estimate_normals_knn(points, k, viewpoint=(0.0, 0.0, 0.0), brute=False):
+    """k-NN normals (grid search; brute=True: the O(n^2) definition it is checked against)."""
     p, stride = _xyz(points)
     out = np.zeros((p.shape[0], 4), np.float32)
     vp = np.array(viewpoint, np.float32)
-    lib().orc_estimate_normals_knn(_f(p), p.shape[0], stride, int(k), _f(vp), _f(out))
+    f = lib().orc_estimate_normals_knn_brute if brute else lib().orc_estimate_normals_knn
+    f(_f(p), p.shape[0], stride, int(k), _f(vp), _f(out))
     return out
 
 

@@ -149,8 +149,17 @@ double orc_normal_plane_dist(const float c[4], const float p[3], const float nrm
 static int orc_within(const orc_sac_params* prm, const float* xyz, int64_t stride, int32_t g,
                       const float c[4], double thr) {
   const float* p = xyz + (int64_t)g * stride;
-  if (prm && prm->model == ORC_SACMODEL_NORMAL_PLANE)
-    return orc_normal_plane_dist(c, p, prm->normals + (int64_t)g * 4, prm->normal_distance_weight) < thr;
+  if (prm && prm->model == ORC_SACMODEL_NORMAL_PLANE) {
+    /* (exact shortcut, same verdicts: with w in [0, 1] the sum w*theta + (1-w)*d rounds to at
+     * least (1-w)*d, so (1-w)*d >= thr already decides "out" without the acos) */
+    const float* nrm = prm->normals + (int64_t)g * 4;
+    const double w = prm->normal_distance_weight * (1.0 - (double)nrm[3]);
+    if (w >= 0.0 && w <= 1.0) {
+      const double de = (double)fabsf(((c[0] * p[0] + c[2] * p[2]) + (c[1] * p[1] + 0.0f * 0.0f)) + c[3]);
+      if ((1.0 - w) * de >= thr) return 0;
+    }
+    return orc_normal_plane_dist(c, p, nrm, prm->normal_distance_weight) < thr;
+  }
   return (double)orc_plane_abs_dist(c, p[0], p[1], p[2]) < thr;
 }
 
@@ -862,11 +871,26 @@ void orc_estimate_normals(const float* xyz, int64_t n, int64_t stride, float rad
 }
 
 /* k-nearest-neighbour variant: NormalEstimation with setKSearch(k) (PCLViewer.cpp:507-522,
- * TriangularMeshing.h:28-35, k = 20).  Brute force over all points: neighbours = the k smallest
- * (dist2, index) pairs, FLANN's sorted kNN result (the query itself has dist2 0).  O(n^2): for
- * test-sized clouds only. */
-void orc_estimate_normals_knn(const float* xyz, int64_t n, int64_t stride, int k_nn,
-                              const float vp[3], float* out) {
+ * TriangularMeshing.h:28-35, k = 20).  Neighbours = the k smallest (dist2, index) pairs, FLANN's
+ * sorted kNN result (the query itself has dist2 0), NaN distances never taken.  The brute-force
+ * form is the definition; the grid form below finds the same pairs (checked against it on
+ * tie-heavy clouds, tests/test_oracle.py) and is what clouds of any size use when every
+ * coordinate is finite. */
+static void orc_normal_from_ids(const float* xyz, int64_t stride, const float* p, const int32_t* ids,
+                                int64_t k, const float vp[3], float* o) {
+  float cov[9], cen[4], ev, v[3];
+  orc_mean_cov(xyz, stride, ids, k, cov, cen);
+  orc_eigen33(cov, &ev, v);
+  float eig_sum = cov[0] + cov[4] + cov[8];
+  float curv = eig_sum != 0.0f ? fabsf(ev / eig_sum) : 0.0f;
+  float vx = vp[0] - p[0], vy = vp[1] - p[1], vz = vp[2] - p[2];
+  float cos_theta = vx * v[0] + vy * v[1] + vz * v[2];
+  if (cos_theta < 0.0f) { v[0] *= -1.0f; v[1] *= -1.0f; v[2] *= -1.0f; }
+  o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = curv;
+}
+
+void orc_estimate_normals_knn_brute(const float* xyz, int64_t n, int64_t stride, int k_nn,
+                                    const float vp[3], float* out) {
   orc_nb* all = (orc_nb*)malloc((size_t)(n > 0 ? n : 1) * sizeof(orc_nb));
   int32_t* ids = (int32_t*)malloc((size_t)(k_nn > 0 ? k_nn : 1) * sizeof(int32_t));
   for (int64_t i = 0; i < n; ++i) {
@@ -887,17 +911,131 @@ void orc_estimate_normals_knn(const float* xyz, int64_t n, int64_t stride, int k
       continue;
     }
     for (int64_t t = 0; t < k; ++t) ids[t] = all[t].j;
-    float cov[9], cen[4], ev, v[3];
-    orc_mean_cov(xyz, stride, ids, k, cov, cen);
-    orc_eigen33(cov, &ev, v);
-    float eig_sum = cov[0] + cov[4] + cov[8];
-    float curv = eig_sum != 0.0f ? fabsf(ev / eig_sum) : 0.0f;
-    float vx = vp[0] - p[0], vy = vp[1] - p[1], vz = vp[2] - p[2];
-    float cos_theta = vx * v[0] + vy * v[1] + vz * v[2];
-    if (cos_theta < 0.0f) { v[0] *= -1.0f; v[1] *= -1.0f; v[2] *= -1.0f; }
-    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = curv;
+    orc_normal_from_ids(xyz, stride, p, ids, k, vp, o);
   }
   free(all); free(ids);
+}
+
+/* (d, j) lexicographic: a before b */
+static int orc_nb_less(orc_nb a, orc_nb b) { return a.d < b.d || (a.d == b.d && a.j < b.j); }
+/* max-heap on (d, j) of at most K entries: the K best so far, worst on top */
+static void orc_heap_push(orc_nb* h, int* sz, int K, orc_nb v) {
+  if (*sz < K) {
+    int i = (*sz)++;
+    h[i] = v;
+    while (i > 0) {
+      int p = (i - 1) / 2;
+      if (!orc_nb_less(h[p], h[i])) break;
+      orc_nb t = h[p]; h[p] = h[i]; h[i] = t;
+      i = p;
+    }
+    return;
+  }
+  if (!orc_nb_less(v, h[0])) return;
+  h[0] = v;
+  int i = 0;
+  for (;;) {
+    int l = 2 * i + 1, r = l + 1, m = i;
+    if (l < K && orc_nb_less(h[m], h[l])) m = l;
+    if (r < K && orc_nb_less(h[m], h[r])) m = r;
+    if (m == i) break;
+    orc_nb t = h[m]; h[m] = h[i]; h[i] = t;
+    i = m;
+  }
+}
+
+/* Grid form: cells of about 16 points per occupied cell layer, searched in Chebyshev shells
+ * around the query's cell; after shell R every point not yet seen lies outside the box of
+ * shells 0..R, so its distance is at least the distance lb from the query to that box's nearest
+ * open face.  The search stops once the K-th best dist2 is below lb^2 with a relative margin of
+ * 1e-5 (the float dist2 of a farther point is within a few ulps of its true value, far inside
+ * the margin), so neither a nearer point nor an equally near point of lower index can be
+ * missing. */
+static void orc_knn_grid(const float* xyz, int64_t n, int64_t stride, int k_nn, const float vp[3],
+                         float* out) {
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) {
+      float v = xyz[i * stride + k];
+      if (v < mn[k]) mn[k] = v;
+      if (v > mx[k]) mx[k] = v;
+    }
+  double ext = 0.0;
+  for (int k = 0; k < 3; ++k) ext = fmax(ext, (double)mx[k] - (double)mn[k]);
+  /* cell edge: the cube root of the volume per 8 points if the cloud filled its box (a lower
+   * bound of the spacing on surfaces), at least ext / 255 */
+  double vol = 1.0;
+  for (int k = 0; k < 3; ++k) vol *= fmax((double)mx[k] - (double)mn[k], ext * 1e-3 + 1e-30);
+  double h = cbrt(vol * 8.0 / (double)(n > 0 ? n : 1));
+  if (h < ext / 255.0) h = ext / 255.0;
+  if (!(h > 0.0)) h = 1.0;
+  orc_grid G;
+  orc_grid_build(&G, xyz, n, stride, (float)h);
+  const double cell = (double)G.cell;
+  const int K = k_nn;
+#pragma omp parallel num_threads(orc_threads)
+  {
+    orc_nb* heap = (orc_nb*)malloc((size_t)(K > 0 ? K : 1) * sizeof(orc_nb));
+    int32_t* ids = (int32_t*)malloc((size_t)(K > 0 ? K : 1) * sizeof(int32_t));
+#pragma omp for schedule(dynamic, 4096)
+    for (int64_t i = 0; i < n; ++i) {
+      const float* p = xyz + i * stride;
+      float* o = out + 4 * i;
+      const int64_t c[3] = {orc_cell_of(&G, p[0], G.minx, G.gx), orc_cell_of(&G, p[1], G.miny, G.gy),
+                            orc_cell_of(&G, p[2], G.minz, G.gz)};
+      const int64_t dim[3] = {G.gx, G.gy, G.gz};
+      const double lo[3] = {G.minx, G.miny, G.minz};
+      int sz = 0;
+      for (int64_t R = 0;; ++R) {
+        for (int64_t z = c[2] - R; z <= c[2] + R; ++z) {
+          if (z < 0 || z >= G.gz) continue;
+          for (int64_t y = c[1] - R; y <= c[1] + R; ++y) {
+            if (y < 0 || y >= G.gy) continue;
+            const int shell_zy = (z == c[2] - R || z == c[2] + R || y == c[1] - R || y == c[1] + R);
+            for (int64_t x = c[0] - R; x <= c[0] + R; x += (shell_zy || R == 0) ? 1 : 2 * R) {
+              if (x < 0 || x >= G.gx) continue;
+              int64_t cc = (z * G.gy + y) * G.gx + x;
+              for (int64_t t = G.start[cc]; t < G.start[cc + 1]; ++t) {
+                int32_t j = G.order[t];
+                const float* q = xyz + (int64_t)j * stride;
+                float ex = p[0] - q[0], ey = p[1] - q[1], ez = p[2] - q[2];
+                orc_nb v;
+                v.d = ((0.0f + ex * ex) + ey * ey) + ez * ez;
+                v.j = j;
+                orc_heap_push(heap, &sz, K, v);
+              }
+            }
+          }
+        }
+        /* the nearest face of the searched box that still has cells beyond it */
+        double lb = INFINITY;
+        int open = 0;
+        for (int k = 0; k < 3; ++k) {
+          if (c[k] - R > 0) { lb = fmin(lb, (double)p[k] - (lo[k] + (double)(c[k] - R) * cell)); open = 1; }
+          if (c[k] + R < dim[k] - 1) { lb = fmin(lb, (lo[k] + (double)(c[k] + R + 1) * cell) - (double)p[k]); open = 1; }
+        }
+        if (!open) break;                                 /* every cell searched */
+        if (sz == K && lb > 0.0 && (double)heap[0].d < lb * lb * (1.0 - 1e-5)) break;
+      }
+      int k = sz;
+      if (k < 3) { o[0] = o[1] = o[2] = o[3] = NAN; continue; }
+      qsort(heap, (size_t)k, sizeof(orc_nb), orc_nb_cmp);
+      for (int t = 0; t < k; ++t) ids[t] = heap[t].j;
+      orc_normal_from_ids(xyz, stride, p, ids, k, vp, o);
+    }
+    free(heap); free(ids);
+  }
+  orc_grid_free(&G);
+}
+
+void orc_estimate_normals_knn(const float* xyz, int64_t n, int64_t stride, int k_nn,
+                              const float vp[3], float* out) {
+  int finite = 1;
+  for (int64_t i = 0; i < n && finite; ++i)
+    for (int k = 0; k < 3; ++k)
+      if (!isfinite(xyz[i * stride + k])) { finite = 0; break; }
+  if (finite && k_nn > 0) orc_knn_grid(xyz, n, stride, k_nn, vp, out);
+  else orc_estimate_normals_knn_brute(xyz, n, stride, k_nn, vp, out);
 }
 
 /* Dialog/PlaneDetect.h:547-665 (first-round branch; the second-round 1-NN branch at :553-584

@@ -127,6 +127,8 @@ int64_t orc_count_within(const float* xyz, int64_t stride, const int32_t* idx, i
 void orc_estimate_normals(const float* xyz, int64_t n, int64_t stride, float radius,
                           const float vp[3], float* normals_out);
 /* PlaneDetect.h:547-665 first-round branch: seed flip, BFS over radius neighbours (sorted). */
+void orc_estimate_normals_knn_brute(const float* xyz, int64_t n, int64_t stride, int k_nn,
+                                    const float vp[3], float* out);
 void orc_estimate_normals_knn(const float* xyz, int64_t n, int64_t stride, int k_nn,
                               const float vp[3], float* out);
 int64_t orc_regulate_normals(const float* xyz, int64_t n, int64_t stride, float* normals,

@@ -9,6 +9,10 @@ and the SHA-256 of every plane's inlier-id list (int32 little-endian, list order
   c2        1M points, 3 planes (+10 % outliers), 4096 hypotheses, one segment()  [configs[1]]
   c3        10M points, 20 planes, extract-and-remove, 4096 hypotheses per round [configs[2]]
   c4shape   100M points, 20 planes, the same extraction (C4 on one GPU)          [configs[3]]
+  c5        10M points, 20 planes: k = 20 normals -> RegulateNormal (seed point 0, outward,
+            r 0.1) -> SACMODEL_NORMAL_PLANE (w 0.1) extract-and-remove               [configs[4]]
+            (the SHA-256 of the normals' and the regulated normals' float32 bits, the number
+            of points the BFS reached, then the extraction as above)
 
 Modes: "pcl" (PCL's float refit, DLG_REFIT_PCL), "fast" (the product's exact-moment refit,
 DLG_REFIT_FAST -- the bench's mode), "none" (optimize off: lean rounds without a refit).
@@ -42,6 +46,9 @@ WORKLOADS = {
                modes=["fast", "pcl", "none"]),
     "c4shape": dict(n=100_000_000, planes=20, seed=SEED_BASE + 4, kind="extract",
                     modes=["fast", "pcl"]),
+    "c5": dict(n=10_000_000, planes=20, seed=SEED_BASE + 5, kind="np_chain",
+               modes=["pcl", "fast"], k=20, reg_seed=0, reg_outward=True, reg_radius=0.1,
+               weight=0.1),
 }
 
 
@@ -54,8 +61,32 @@ def cloud(w):
     return p
 
 
+_NORMALS = {}
+
+
+def np_chain_normals(w, p):
+    """k-NN normals -> RegulateNormal (oracle), cached per workload; -> (normals, regulated,
+    reached, summary)"""
+    if "c5" not in _NORMALS:
+        t0 = time.time()
+        nrm = O.estimate_normals_knn(p, w["k"])
+        t1 = time.time()
+        reg, _, reached = O.regulate_normals(p, nrm, w["reg_seed"], w["reg_outward"], w["reg_radius"])
+        t2 = time.time()
+        print(f"c5 normals {t1 - t0:.1f} s, regulate {t2 - t1:.1f} s", flush=True)
+        _NORMALS["c5"] = (reg, dict(k=w["k"], normals_sha256=sha(nrm), reg_seed=w["reg_seed"],
+                                    reg_outward=w["reg_outward"], reg_radius=w["reg_radius"],
+                                    reached=int(reached), regulated_sha256=sha(reg),
+                                    weight=w["weight"], oracle_normals_s=round(t1 - t0, 1),
+                                    oracle_regulate_s=round(t2 - t1, 1)))
+    return _NORMALS["c5"]
+
+
 def run(name, w, p, mode):
     kw = dict(max_iterations=4095, probability=1.0)
+    if w["kind"] == "np_chain":
+        kw["normals"] = np_chain_normals(w, p)[0]
+        kw["normal_distance_weight"] = w["weight"]
     if mode == "none":
         kw["optimize"] = False
     else:
@@ -101,6 +132,8 @@ def main():
         ent = dict(n_points=w["n"], planes=w["planes"], seed=w["seed"], kind=w["kind"],
                    shares=w.get("shares"), threshold=THR, cloud_sha256=sha(p),
                    modes=db.get(name, {}).get("modes", {}))
+        if w["kind"] == "np_chain":
+            ent["chain"] = np_chain_normals(w, p)[1]
         if db.get(name, {}).get("cloud_sha256", ent["cloud_sha256"]) != ent["cloud_sha256"]:
             ent["modes"] = {}
         for mode in (ms.split(",") if ms else w["modes"]):

@@ -4,6 +4,8 @@
   c2       1M points, 3 planes, one segment() of 4096 hypotheses (configs[1])   pcl, fast refit
   c3       10M points, 20 planes, extract-and-remove (configs[2], the bench)    fast, pcl, none
   c4shape  100M points, 20 planes, the same extraction on one GPU (configs[3]) fast, pcl
+  c5       10M points, 20 planes: k = 20 normals -> RegulateNormal -> NORMAL_PLANE extraction,
+           all on the cloud's device copy (configs[4])                          pcl, fast
 
 Bit-exact: iterations, best sample, coefficient bit patterns, per-plane inlier counts and the
 SHA-256 of every plane's inlier-id list.  The fast refit (the bench's mode) is also run with the
@@ -283,3 +285,34 @@ def test_c2_hyp_sharded_loopback(gpu_ctx, mode):
         assert [int(v) for v in st["best_sample"]] == g["best_sample"]
         assert [int(v) for v in coeff.view(np.uint32)] == g["coeff_bits"]
         assert inl.size == g["n_inliers"] and sha(inl) == g["inliers_sha256"]
+
+
+@pytest.mark.skipif("c5" not in DB, reason="fullsize.json has no c5")
+@pytest.mark.parametrize("mode", modes_of("c5"))
+def test_c5_fullsize(gpu_ctx, mode):
+    """configs[4] at its quoted size, the reference's order (estimateNormal PlaneDetect.h:515-545,
+    regulateNormal :547-665, then the plane stage) on the cloud's device copy, as the bench's
+    chain_regulate times it: k = 20 normals (dlg_cloud_estimate_normals; the float32 bits of all
+    10M (normal, curvature) records against the oracle's SHA-256), RegulateNormal (BFS r 0.1 from
+    point 0, outward; reached count and the regulated records' SHA-256), then SACMODEL_NORMAL_PLANE
+    (w 0.1) extract-and-remove over the regulated normals: coefficient bits, counts and inlier
+    SHA-256s.  The extraction's rounds run lean (the Morton copy's NORMAL_PLANE rounds)."""
+    w = DB["c5"]
+    ch = w["chain"]
+    p = cloud("c5")
+    cl = D.Cloud(gpu_ctx, p)
+    try:
+        nrm = cl.estimate_normals(k=ch["k"], copy_out=True)
+        assert sha(nrm) == ch["normals_sha256"]
+        del nrm
+        _, reached, reg = cl.regulate_normals(ch["reg_seed"], ch["reg_outward"], ch["reg_radius"],
+                                              copy_out=True)
+        assert reached == ch["reached"]
+        assert sha(reg) == ch["regulated_sha256"]
+        del reg
+        prm = params(mode, model=D.SACMODEL_NORMAL_PLANE, normal_distance_weight=ch["weight"])
+        e = D.extract_planes(cl, prm, max_planes=20, min_inliers=500, capacity=p.shape[0])
+    finally:
+        cl.close()
+    check_extract(e, w["modes"][mode])
+    assert e["stats"]["lean_rounds"] > 0, e["stats"]

@@ -72,6 +72,28 @@ def test_oracle_np_distance_matches_numpy_twin():
             assert O.count_within_np(p, nrm, c, thr, lam) == int((twin < thr).sum())
 
 
+def test_oracle_np_prefilter_any_curvature():
+    """The oracle's countWithinDistance shortcut ((1 - w) d >= threshold decides "out" without the
+    acos, for w in [0, 1]) gives the twin's counts also for weights outside [0, 1] (curvature
+    above 1 or below 0), NaN curvature and NaN / zero normals, where it must not apply."""
+    p, nrm, _, _ = cloud_with_normals(4000, seed=9)
+    rng = np.random.default_rng(9)
+    nrm = nrm.copy()
+    nrm[:, 3] = rng.uniform(-0.5, 1.5, len(nrm)).astype(np.float32)
+    nrm[::37, 3] = np.nan
+    nrm[5::53, :3] = np.nan
+    nrm[7::61, :3] = 0.0
+    for t in range(12):
+        i = rng.choice(len(p), 3, replace=False)
+        nn = np.cross((p[i[1]] - p[i[0]]).astype(np.float64), (p[i[2]] - p[i[0]]).astype(np.float64))
+        nn /= np.linalg.norm(nn)
+        c = np.array([*nn, -np.dot(nn, p[i[0]])], np.float32)
+        lam = [0.1, 0.7, 1.0, 2.0][t % 4]
+        twin = np_twin_dist(c, p, nrm, lam)
+        for thr in (0.01, 0.05, 0.3):
+            assert O.count_within_np(p, nrm, c, thr, lam) == int((twin < thr).sum())
+
+
 def test_oracle_np_segment_properties():
     p, nrm, lab, pl = cloud_with_normals()
     r = O.sac_segment(p, 0.05, max_iterations=200, normals=nrm, normal_distance_weight=0.1)

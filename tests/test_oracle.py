@@ -155,3 +155,26 @@ def test_normals_and_regulate_on_planes():
     m = proc & (lab == 0) & ok
     # after BFS every processed normal of the seed's plane agrees in sign with the seed
     assert np.all(reg[m, :3] @ reg[seed_idx, :3] > 0)
+
+
+@pytest.mark.parametrize("kind", ["planes", "quantized", "lattice", "duplicates", "line"])
+def test_knn_grid_equals_brute_force(kind):
+    """The oracle's k-NN normals search a uniform grid in Chebyshev shells (what full-size clouds
+    use); the O(n^2) brute-force form is the definition (k smallest (dist2, index) pairs).  Equal
+    bits on clouds built for ties: quantised coordinates, a lattice, duplicated points, a line."""
+    rng = np.random.default_rng(0)
+    if kind == "planes":
+        p, _, _ = plane_cloud(5000, 4, seed=3, patch=2.0)
+    elif kind == "quantized":
+        p = (np.round(rng.uniform(0, 1, (3000, 3)) * 20) / 20).astype(np.float32)
+    elif kind == "lattice":
+        p = (np.stack(np.meshgrid(*[np.arange(11)] * 3), -1).reshape(-1, 3) * 0.5).astype(np.float32)
+    elif kind == "duplicates":
+        p = np.repeat(rng.uniform(0, 1, (400, 3)), 5, axis=0).astype(np.float32)
+    else:
+        p = np.zeros((2000, 3), np.float32)
+        p[:, 0] = np.arange(2000) * 0.01
+    for k in (3, 8, 20):
+        a = O.estimate_normals_knn(p, k)
+        b = O.estimate_normals_knn(p, k, brute=True)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k

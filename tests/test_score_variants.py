@@ -15,8 +15,9 @@ import pytest
 VARIANTS = (0, 1, 2)  # DLG_SCORE_EXACT (PCL op order), DLG_SCORE_BF16 (matrix cores), DLG_SCORE_PRUNED
 # DLG_OPT_PRUNE_TILE_SCORER values besides the default DLG_TILE_EXACT: DLG_TILE_BF16 and the
 # A/B-only variants 11, 14 (1 / 4 planes per lane), 12 (packed f32 tests) and the claim variants
-# 15 (round 4's round-robin), 16 (list-length classes, no tail), 17 (tail, no classes)
-TILE_SCORERS = (1, 11, 12, 14, 15, 16, 17)
+# 15 (round 4's round-robin), 16 (list-length classes, no tail), 17 (tail, no classes), and
+# DLG_TILE_MFMA (2: f32 matrix-core groups of 16 planes + band re-decision)
+TILE_SCORERS = (1, 2, 11, 12, 14, 15, 16, 17)
 
 
 def counts(ctx, cloud, D, v, thr):

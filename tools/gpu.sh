@@ -94,7 +94,7 @@ for s in "$@"; do
       for v in "$a" "$b" "$a" "$b"; do
         run walkab_$(basename "$v" .so) 150 python3 -u tools/with_lib.py "$v" tools/fs_walk_stats.py 4
       done ;;
-    py) run py_$(basename "${arg%%,*}" .py) 900 python3 -u ${arg//,/ } ;;
+    py) run py_$(basename "${arg%%,*}" .py)_$(echo "$arg" | md5sum | cut -c1-6) 900 python3 -u ${arg//,/ } ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done
