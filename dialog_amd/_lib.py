@@ -102,7 +102,8 @@ class ExtractStats(C.Structure):
                 ("score_launches", C.c_int), ("score_ms", C.c_double), ("select_ms", C.c_double),
                 ("wall_ms", C.c_double), ("lean_rounds", C.c_int), ("spec_misses", C.c_int),
                 ("pcl_host_checks", C.c_int), ("refit_walk_ms", C.c_double),
-                ("refit_repair_ms", C.c_double), ("refit_repairs", C.c_int)]
+                ("refit_repair_ms", C.c_double), ("refit_repairs", C.c_int),
+                ("refit_rebase_ms", C.c_double)]
 
 
 _lib = None

@@ -131,7 +131,18 @@ void check_sp_totals(dlg_ctx* c, const int32_t* sp_tot) {
 void add_walk_ms(dlg_ctx* c, int k) {
   if (!c->walk_rec[k]) return;
   float ms = 0.f;
-  HIPCHK(hipEventElapsedTime(&ms, c->ev_walk[k][0], c->ev_walk[k][1]));
+  if (c->mid_rec[k]) {
+    // several ranks, rank > 0: the two walks apart from the exchange and rebase between them
+    float a = 0.f, b = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, c->ev_walk[k][0], c->ev_walk[k][4]));
+    HIPCHK(hipEventElapsedTime(&b, c->ev_walk[k][5], c->ev_walk[k][1]));
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_walk[k][4], c->ev_walk[k][5]));
+    c->sel_pending->refit_rebase_ms += ms;
+    ms = a + b;
+    c->mid_rec[k] = false;
+  } else {
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_walk[k][0], c->ev_walk[k][1]));
+  }
   c->sel_pending->refit_walk_ms += ms;
   c->walk_rec[k] = false;
   if (c->rep_rec[k]) {
@@ -716,11 +727,14 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
     // the PCL refit walk's timing events (profiling only)
     // (e = 2, 3: k_fs_repair's, which runs on ranks > 0 of a group only)
     c->rep_rec[sk] = false;
+    c->mid_rec[sk] = false;
+    // (e = 4, 5: the first walk's end and the second's start, ranks > 0 under protocols 0, 2)
     auto walk_ev = [&](int e) -> hipEvent_t {
       if (!c->profiling || !c->walk_events) return nullptr;
       if (e >= 2 && (c->comm->world() == 1 || c->comm->rank() == 0)) return nullptr;
+      if (e >= 4 && c->opt.fs_protocol == 1) return nullptr;
       if (!c->ev_walk[sk][e]) HIPCHK(hipEventCreate(&c->ev_walk[sk][e]));
-      (e >= 2 ? c->rep_rec : c->walk_rec)[sk] = true;
+      (e >= 4 ? c->mid_rec : e >= 2 ? c->rep_rec : c->walk_rec)[sk] = true;
       return c->ev_walk[sk][e];
     };
     if (c->profiling) {
@@ -799,7 +813,8 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         cl->ubits_dirty = false;
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
                         rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
-                        walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol, &repairs, c->opt.fs_segments);
+                        walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol, &repairs,
+                        c->opt.fs_segments, walk_ev(4), walk_ev(5));
       } else {
         c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
         stage_wait();
@@ -808,7 +823,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
                         c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(),
                         walk_ev(0), walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol,
-                        &repairs, c->opt.fs_segments);
+                        &repairs, c->opt.fs_segments, walk_ev(4), walk_ev(5));
       }
       HIPCHK(hipGetLastError());
       if (xs) xs->refit_repairs += repairs;
@@ -1935,7 +1950,7 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         // (DLG_TILE_* values, and the A/B-only kernel variants kTileScorerExK1/ExK4/ExPk and
         // claim variants 15..17)
         if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != DLG_TILE_MFMA &&
-            value != kTileScorerExK1 &&
+            value != kTileScorerExK1 && value != kTileScorerMfmaX && value != kTileScorerMfmaW &&
             value != kTileScorerExK4 && value != kTileScorerExPk &&
             !(value >= kTileScorerClaimR4 && value <= kTileScorerClaimTail))
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");

@@ -266,9 +266,10 @@ struct dlg_ctx {
   int64_t sp_expect_in = 0, sp_expect_out = 0;
   dlg_extract_stats* sel_pending = nullptr;  // select_ms of the last round, not yet read
   hipEvent_t ev_sel[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // per-round pairs
-  hipEvent_t ev_walk[2][4] = {};  // [pair][walk start, walk end, repair start, repair end]:   // the PCL refit's walk
+  hipEvent_t ev_walk[2][6] = {};  // [pair][walk start, walk end, repair start, repair end]:   // the PCL refit's walk
   bool walk_rec[2] = {false, false};  // the pair's walk events were recorded this round
   bool rep_rec[2] = {false, false};   // ... and its repair events (several ranks, rank > 0)
+  bool mid_rec[2] = {false, false};   // ... and the two walks' inner events (protocols 0, 2)
   int sel_k = 0;
   DevBuf<int32_t> rk;     // every rank's (inliers, survivors) of a round
   PinBuf<int32_t> h_rk;

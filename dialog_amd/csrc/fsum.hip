@@ -1549,7 +1549,8 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
                      hipEvent_t ev_walk0, hipEvent_t ev_walk1, hipEvent_t ev_rep0,
-                     hipEvent_t ev_rep1, int protocol, int* repairs, int segments) {
+                     hipEvent_t ev_rep1, int protocol, int* repairs, int segments,
+                     hipEvent_t ev_mid0, hipEvent_t ev_mid1) {
   uint32_t gen = ++s_gen;
   if (gen == 0) gen = ++s_gen;  // (0 marks a dropped table entry)
   FsDev d{px, py, pz, stride, n_dev, b, gen};
@@ -1569,14 +1570,14 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
     const int S = std::min(std::max(segments, 1), kFsSegMax);
     if (S > 1) {
       // segmented: kFsChains x S walkers (+ the table builders), then the joins
-      hipExtLaunchKernelGGL(k_fs_walk, dim3(gw + kFsChains * (S - 1)), dim3(kFwBS), 0, s, ev_walk0,
-                            nullptr, 0u, d, (const float*)nullptr, S << kFwSegShift,
+      DLG_LAUNCH_EV(k_fs_walk, dim3(gw + kFsChains * (S - 1)), dim3(kFwBS), 0, s, ev_walk0,
+                            nullptr, d, (const float*)nullptr, S << kFwSegShift,
                             (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
-      hipExtLaunchKernelGGL(k_fs_segfix, dim3(kFsChains), dim3(kFwBS), 0, s, nullptr, ev_walk1, 0u,
+      DLG_LAUNCH_EV(k_fs_segfix, dim3(kFsChains), dim3(kFwBS), 0, s, nullptr, ev_walk1,
                             d, (const float*)nullptr, S, cin, cout, res);
       return;
     }
-    hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
+    DLG_LAUNCH_EV(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, d,
                           nullptr, 0, cin, cout, res);
     return;
   }
@@ -1600,12 +1601,12 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
   hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
   FsDev dw = d;  // the launch the recorded walk (and its window tables) belongs to
   if (protocol == 1) {
-    hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, 0u, d,
+    DLG_LAUNCH_EV(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0, ev_walk1, d,
                           (const float*)nullptr, r > 0 ? kFwGuess | kFwRecord : 0,
                           (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);
   } else {
-    hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0,
-                          r > 0 ? nullptr : ev_walk1, 0u, d, (const float*)nullptr,
+    DLG_LAUNCH_EV(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_walk0,
+                          r > 0 ? ev_mid0 : ev_walk1, d, (const float*)nullptr,
                           r > 0 ? kFwGuess : 0, (const float4*)nullptr, (float4*)nullptr,
                           (int32_t*)nullptr);
     comm->allgather(b.sums, b.gath2, 2 * kFsChains, DType::I32, s);
@@ -1621,7 +1622,7 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                          b.n_global, (const float*)b.gath2, (const float*)b.g2);
       hipLaunchKernelGGL(k_fs_inc, dim3(gp), dim3(kFiBS), 0, s, dw, b.base9);
       hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, dw);
-      hipExtLaunchKernelGGL(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, nullptr, ev_walk1, 0u, dw,
+      DLG_LAUNCH_EV(k_fs_walk, dim3(gw), dim3(kFwBS), 0, s, ev_mid1, ev_walk1, dw,
                             (const float*)b.g2, kFwRecord, (const float4*)nullptr,
                             (float4*)nullptr, (int32_t*)nullptr);
     }
@@ -1667,7 +1668,7 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
   }
   if (r > 0) {
     comm->recv(b.start9, kFsChains, DType::I32, r - 1, s);
-    hipExtLaunchKernelGGL(k_fs_repair, dim3(kFsChains), dim3(kFwBS), 0, s, ev_rep0, ev_rep1, 0u,
+    DLG_LAUNCH_EV(k_fs_repair, dim3(kFsChains), dim3(kFwBS), 0, s, ev_rep0, ev_rep1,
                           dw, (const float*)b.start9);
   }
   if (r < W - 1) comm->send(b.sums, kFsChains, DType::I32, r + 1, s);

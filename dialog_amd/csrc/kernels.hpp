@@ -258,13 +258,16 @@ class Comm;
 // 1 = round 4's: no rebase (repairs from ~1000 quanta off); 2 = as 0 with parallel repair
 // iterations and host checks instead of the hand-over (A/B and tests only).  *repairs (optional)
 // = the repair steps the round took (0 and 1: the W - 1 hops; 2: the iterations).  segments (one
-// rank): walkers per chain (1..kFsSegMax; see kFsSegMax)
+// rank): walkers per chain (1..kFsSegMax; see kFsSegMax).  ev_mid0 / ev_mid1 (several ranks,
+// protocols 0 and 2, rank > 0): the first walk's end and the second walk's start, so the two walks
+// are timed apart from the exchange and the rebase between them
 void launch_fs_refit(const float* px, const float* py, const float* pz, int stride,
                      const int32_t* n_dev, int64_t n_cap, const FsBuffers& b, const float4* cin,
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm = nullptr,
                      hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr,
                      hipEvent_t ev_rep0 = nullptr, hipEvent_t ev_rep1 = nullptr,
-                     int protocol = 0, int* repairs = nullptr, int segments = 1);
+                     int protocol = 0, int* repairs = nullptr, int segments = 1,
+                     hipEvent_t ev_mid0 = nullptr, hipEvent_t ev_mid1 = nullptr);
 
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers

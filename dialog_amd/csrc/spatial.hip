@@ -720,6 +720,7 @@ __device__ __forceinline__ int nth_set_bit(uint32_t v, int r) {
 // of 8 VALU per test.  (Up to 4 groups per pass, their 8 MFMAs issued before any result is read.)
 constexpr int kMfG = 16;
 constexpr int kMfPass = 2;  // groups per pass (their MFMAs issued before any result is read)
+template <int MODE>  // 0: band 12 u S; A/B checks: 1 every result re-decided, 2 band 64 u S
 __device__ __forceinline__ void mf_pass(int m, const uint16_t* ring, int head, const float* spt,
                                         const float4* s_cf, uint32_t* s_cnt, int lane, float cthr,
                                         float ax, float ay, float az) {
@@ -740,7 +741,7 @@ __device__ __forceinline__ void mf_pass(int m, const uint16_t* ring, int head, c
       // a pad: a plane 2^100 away (never near, never ambiguous, counts nothing)
       if (e & kExPad) q = make_float4(0.f, 0.f, 0.f, 0x1p100f);
       const float S = ((fabsf(q.x) * ax + fabsf(q.y) * ay) + fabsf(q.z) * az) + fabsf(q.w);
-      band[g] = S * (12.0f * 0x1p-24f * (1.0f + 0x1p-16f)) + 0x1p-100f;
+      band[g] = S * ((MODE == 2 ? 64.0f : 12.0f) * 0x1p-24f * (1.0f + 0x1p-16f)) + 0x1p-100f;
       const float b = k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
       sb[g] = (int)((e >> 12) & 3u) * kExSlotF;
       const float* sl = spt + sb[g];
@@ -751,9 +752,9 @@ __device__ __forceinline__ void mf_pass(int m, const uint16_t* ring, int head, c
       d1[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, zero, 0, 0, 0);
     }
   }
-  // per result t = |D| - cthr: a sure inlier when t < -band; the group is ambiguous on this lane
-  // when the smallest |t| is below band (NaN results -- points past n -- compare false and are
-  // skipped by the min: never counted, as PCL's NaN < thr)
+  // per result t = |D| - cthr: a sure inlier when t < -band, a sure outlier when t > band; the
+  // group is ambiguous on this lane when the smallest |t| is not above band (NaN results -- points
+  // past n -- compare false and are skipped by the min: never counted, as PCL's NaN < thr)
   uint32_t cnt[G];
   bool amb[G];
   bool any = false;
@@ -770,7 +771,8 @@ __device__ __forceinline__ void mf_pass(int m, const uint16_t* ring, int head, c
         cnt[g] += t1 < -band[g] ? 1u : 0u;
         mn = fminf(mn, fminf(fabsf(t0), fabsf(t1)));
       }
-      amb[g] = mn < band[g];
+      // (|t| = band exactly is ambiguous: t = -band is an inlier the count above left out)
+      amb[g] = (MODE == 1 && !(jj[g] & 0x1000)) || !(mn > band[g]);
       any = any || amb[g];
     }
   }
@@ -807,7 +809,7 @@ __device__ __forceinline__ void mf_pass(int m, const uint16_t* ring, int head, c
 // (prefix sum of the lanes' bit counts, owner lane by a DPP max-scan of the chunk's first
 // positions) and decided with PCL's double arithmetic (np_full, as k_score_np), the normal read
 // from global memory.  Same counts as k_score_tiles_rl<NPM> and k_score_np.
-template <int BS, int K, bool PK = false, bool NPM = false, bool MF = false>
+template <int BS, int K, bool PK = false, bool NPM = false, bool MF = false, int MFX = 0>
 __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z, int n,
     const float4* __restrict__ tiles, const uint16_t* __restrict__ lp, int ls,
@@ -925,7 +927,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   auto pass = [&](int m) __attribute__((always_inline)) {
     if (stats && lane == 0) { atomicAdd(&s_st[3], 1ull); atomicAdd(&s_st[4], (unsigned long long)m); }
     if constexpr (MF) {
-      mf_pass(m, ring, head, spt, s_cf, s_cnt, lane, cthr, ax, ay, az);
+      mf_pass<MFX>(m, ring, head, spt, s_cf, s_cnt, lane, cthr, ax, ay, az);
       head += m;
       return;
     }
@@ -1358,12 +1360,12 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   const int tail = claim_ab && tile_scorer != kTileScorerClaimTail ? 0 : 1;
   // (timing events, when given, ride the two dispatches themselves: no marker packets, so no
   // launch gaps around the scoring)
-  hipExtLaunchKernelGGL(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, ev_start, nullptr, 0u, v.supers,
+  DLG_LAUNCH_EV(k_prune_supers, dim3(ga), dim3(kPrBS), 0, s, ev_start, nullptr, v.supers,
                         (int)ns, hyps, D, ls, margin, H, lp, lp_n, work, order,
                         np && ex ? np->cn : nullptr);
   if (np && ex) {
-    hipExtLaunchKernelGGL((k_score_tiles_ex<kBS, 2, false, true>), dim3((unsigned)g), dim3(kBS), 0, s,
-                          nullptr, ev_stop, 0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work,
+    DLG_LAUNCH_EV((k_score_tiles_ex<kBS, 2, false, true>), dim3((unsigned)g), dim3(kBS), 0, s,
+                          nullptr, ev_stop, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work,
                           blk_cap, xcd, order, hyps, D, cthr, margin, counts, stats,
                           pick ? *pick : PickArgs{}, np->nrm, np->lambda, np->thr, np->cn, tail,
                           0.f, 0.f, 0.f);
@@ -1371,9 +1373,14 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   }
   // (the MFMA scorer's rounding band is S x 12 u with S up to (ax + ay + az) + |d|: clouds whose
   // coordinates would overflow it take the exact scorer)
-  if (ex && tile_scorer == kTileScorerMfma && (double)amax[0] + amax[1] + amax[2] < 1e30) {
-    hipExtLaunchKernelGGL((k_score_tiles_ex<kBS, 2, false, false, true>), dim3((unsigned)g),
-                          dim3(kBS), 0, s, nullptr, ev_stop, 0u, v.x, v.y, v.z, (int)v.n, v.tiles,
+  if (ex && (tile_scorer == kTileScorerMfma || tile_scorer == kTileScorerMfmaX ||
+             tile_scorer == kTileScorerMfmaW) &&
+      (double)amax[0] + amax[1] + amax[2] < 1e30) {
+    auto* kmf = tile_scorer == kTileScorerMfmaX ? k_score_tiles_ex<kBS, 2, false, false, true, 1>
+              : tile_scorer == kTileScorerMfmaW ? k_score_tiles_ex<kBS, 2, false, false, true, 2>
+                                                : k_score_tiles_ex<kBS, 2, false, false, true>;
+    DLG_LAUNCH_EV(kmf, dim3((unsigned)g),
+                          dim3(kBS), 0, s, nullptr, ev_stop, v.x, v.y, v.z, (int)v.n, v.tiles,
                           lp, ls, lp_n, work, blk_cap, xcd, order, hyps, D, cthr, margin, counts,
                           stats, pick ? *pick : PickArgs{}, (const float4*)nullptr, 0.0, 0.0,
                           (const float4*)nullptr, tail, amax[0], amax[1], amax[2]);
@@ -1384,15 +1391,15 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
               : tile_scorer == kTileScorerExK4 ? k_score_tiles_ex<kBS, 4>
               : tile_scorer == kTileScorerExPk ? k_score_tiles_ex<kBS, 2, true>
                                                : k_score_tiles_ex<kBS, 2>;
-    hipExtLaunchKernelGGL(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
-                          0u, v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, xcd,
+    DLG_LAUNCH_EV(kex, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop,
+                          v.x, v.y, v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, xcd,
                           order, hyps, D, cthr, margin, counts, stats, pick ? *pick : PickArgs{},
                           (const float4*)nullptr, 0.0, 0.0, (const float4*)nullptr, tail, 0.f, 0.f,
                           0.f);
     return;
   }
   auto* kfn = np ? k_score_tiles_rl<kBS, true> : k_score_tiles_rl<kBS, false>;
-  hipExtLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop, 0u, v.x, v.y,
+  DLG_LAUNCH_EV(kfn, dim3((unsigned)g), dim3(kBS), 0, s, nullptr, ev_stop, v.x, v.y,
                         v.z, (int)v.n, v.tiles, lp, ls, lp_n, work, blk_cap, kChunkTiles, xcd, hyps, D,
                         cthr, margin, amax[0], amax[1], amax[2], counts, stats,
                         np ? np->nrm : nullptr, np ? np->lambda : 0.0, np ? np->thr : 0.0,

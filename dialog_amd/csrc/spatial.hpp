@@ -80,6 +80,8 @@ inline int prune_list_stride(int D) { return (D + 63) / 64 * 64; }
 constexpr int kTileScorerExact = 0;   // k_score_tiles_ex<2> (default)
 constexpr int kTileScorerBf16 = 1;    // k_score_tiles_rl
 constexpr int kTileScorerMfma = 2;    // k_score_tiles_ex<2, MF>: 16-plane groups on f32 MFMA
+constexpr int kTileScorerMfmaX = 18;  // A/B check: the same, every result re-decided exactly
+constexpr int kTileScorerMfmaW = 19;  // A/B check: the same with a band of 64 u S
 // A/B-only variants (same counts; tests/test_score_variants.py runs each)
 constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14;
 constexpr int kTileScorerExPk = 12;

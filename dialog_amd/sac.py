@@ -331,7 +331,8 @@ def extract_planes(cloud: Cloud, params, max_planes=20, min_inliers=0, capacity=
                  score_launches=xs.score_launches, score_ms=xs.score_ms, select_ms=xs.select_ms,
                  wall_ms=xs.wall_ms, lean_rounds=xs.lean_rounds, spec_misses=xs.spec_misses,
                  pcl_host_checks=xs.pcl_host_checks, refit_walk_ms=xs.refit_walk_ms,
-                 refit_repair_ms=xs.refit_repair_ms, refit_repairs=xs.refit_repairs)
+                 refit_repair_ms=xs.refit_repair_ms, refit_repairs=xs.refit_repairs,
+                 refit_rebase_ms=xs.refit_rebase_ms)
     return dict(coeffs=coeffs[:k].copy(), offsets=offs[:k + 1].copy(),
                 inliers=inl[:offs[k]], n_planes=k, stats=stats)
 

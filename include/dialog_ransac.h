@@ -131,6 +131,10 @@ typedef struct {
   int refit_repairs;           /* several ranks: the PCL refit's repair steps summed over the
                                   rounds (hand-over: W - 1 a round; DLG_OPT_FS_ONE_WALK 2: the
                                   parallel repair iterations) */
+  double refit_rebase_ms;      /* several ranks, rank > 0, DLG_OPT_FS_ONE_WALK 0 / 2: the time
+                                  between the first walk's end and the second walk's start (the
+                                  allgather of the walks' ends + the rebase kernels); refit_walk_ms
+                                  then holds the two walks alone */
 } dlg_extract_stats;
 
 void dlg_sac_params_default(dlg_sac_params* p);   /* PCL SACSegmentation defaults */

@@ -230,6 +230,7 @@ def test_c4shape_sharded_loopback(gpu_ctx, mode, proto):
         rows.append(dict(rank=r, points=b[r + 1] - b[r], rounds=st["rounds"],
                          walk_ms=round(st["refit_walk_ms"], 4),
                          repair_ms=round(st["refit_repair_ms"], 4),
+                         rebase_ms=round(st["refit_rebase_ms"], 4),
                          repairs=st["refit_repairs"],
                          score_ms=round(st["score_ms"], 4), select_ms=round(st["select_ms"], 4),
                          wall_ms=round(st["wall_ms"], 2)))

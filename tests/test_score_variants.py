@@ -16,8 +16,9 @@ VARIANTS = (0, 1, 2)  # DLG_SCORE_EXACT (PCL op order), DLG_SCORE_BF16 (matrix c
 # DLG_OPT_PRUNE_TILE_SCORER values besides the default DLG_TILE_EXACT: DLG_TILE_BF16 and the
 # A/B-only variants 11, 14 (1 / 4 planes per lane), 12 (packed f32 tests) and the claim variants
 # 15 (round 4's round-robin), 16 (list-length classes, no tail), 17 (tail, no classes), and
-# DLG_TILE_MFMA (2: f32 matrix-core groups of 16 planes + band re-decision)
-TILE_SCORERS = (1, 2, 11, 12, 14, 15, 16, 17)
+# DLG_TILE_MFMA (2: f32 matrix-core groups of 16 planes + band re-decision; 18: the same with
+# every result re-decided, 19: a 64 u S band -- A/B checks of the band)
+TILE_SCORERS = (2, 18, 19, 1, 11, 12, 14, 15, 16, 17)
 
 
 def counts(ctx, cloud, D, v, thr):
@@ -56,6 +57,7 @@ def test_score_variants_bit_identical(gpu_ctx, case):
     p, thr = make(case)
     cloud = D.Cloud(gpu_ctx, p)
     cloud.build_spatial()
+    bad = []
     try:
         for nh in (1, 100, 257, 4096):
             ref = counts(gpu_ctx, cloud, nh, VARIANTS[0], thr)
@@ -72,7 +74,9 @@ def test_score_variants_bit_identical(gpu_ctx, case):
                     got = counts(gpu_ctx, cloud, nh, 2, thr)
                 finally:
                     gpu_ctx.set_option(D.DLG_OPT_PRUNE_TILE_SCORER, D.DLG_TILE_EXACT)
-                assert np.array_equal(got, ref), (case, nh, "pruned tile scorer", ts,
-                                                  int((got != ref).sum()))
+                if not np.array_equal(got, ref):
+                    bad.append((case, nh, ts, int((got != ref).sum()),
+                                [(int(i), int(got[i]), int(ref[i])) for i in np.flatnonzero(got != ref)[:4]]))
+        assert not bad, bad
     finally:
         cloud.close()

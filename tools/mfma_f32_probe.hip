@@ -40,9 +40,9 @@ int main() {
   CK(hipMalloc(&dD, sizeof(hD)));
   // exact integers, asymmetric: the maps
   for (int i = 0; i < 16; ++i)
-    for (int k = 0; k < 4; ++k) hA[i * 4 + k] = (float)(i + 1) * (k == 0 ? 1 : k == 1 ? 100 : k == 2 ? 10000 : 1000000);
+    for (int k = 0; k < 4; ++k) hA[i * 4 + k] = (float)(i + 1) * (k == 0 ? 1 : k == 1 ? 32 : k == 2 ? 1024 : 32768);
   for (int k = 0; k < 4; ++k)
-    for (int j = 0; j < 16; ++j) hB[k * 16 + j] = (float)((k + 1) * (j + 3) % 7 + 1);
+    for (int j = 0; j < 16; ++j) hB[k * 16 + j] = (float)((k + 1) * (j + 3) % 7 + 1);  // < 32: exact sums
   CK(hipMemcpy(dA, hA, sizeof(hA), hipMemcpyHostToDevice));
   CK(hipMemcpy(dB, hB, sizeof(hB), hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, 0, dA, dB, dD);
