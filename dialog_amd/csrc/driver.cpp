@@ -29,7 +29,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -406,7 +408,10 @@ void ensure_sel1(dlg_ctx* c, int64_t n, int64_t min_tiles = 0) {
   }
   c->sel1.status = c->sel1_status.p;
   c->sel1.err = c->sel1_err.p;
-  c->sel1.ticket = c->opt.sel1_ticket ? reinterpret_cast<unsigned long long*>(c->sel1_tk.p) : nullptr;
+  // (tickets whenever another context of this process may run its selects on the same device
+  // at once: with the device to itself a launch's tiles complete in workgroup-index order)
+  const bool tk = c->opt.sel1_ticket == 1 || (c->opt.sel1_ticket == -1 && ctx_shared(c->device));
+  c->sel1.ticket = tk ? reinterpret_cast<unsigned long long*>(c->sel1_tk.p) : nullptr;
 }
 
 void ensure_mom_done(dlg_ctx* c) {
@@ -1203,6 +1208,9 @@ int64_t emit_inliers(dlg_ctx* c, const SegOut& so, bool gather, int32_t* dst, in
 
 std::string g_last_create_error;
 
+std::mutex g_ctx_mu;
+std::map<int, int> g_ctx_count;  // live contexts per device
+
 dlg_status init_ctx(dlg_ctx* c, int device) {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
@@ -1221,10 +1229,22 @@ dlg_status init_ctx(dlg_ctx* c, int device) {
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_inl, hipEventDisableTiming));
     for (auto& ev : c->ev) HIPCHK(hipEventCreate(&ev));
+    ctx_count_add(device, 1);  // (last: a failed init is not counted)
+    c->counted = true;
   });
 }
 
 }  // namespace
+
+void dlg::ctx_count_add(int device, int delta) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  g_ctx_count[device] += delta;
+}
+bool dlg::ctx_shared(int device) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto it = g_ctx_count.find(device);
+  return it != g_ctx_count.end() && it->second > 1;
+}
 
 // normals records on the device (raw_dev: stride_f floats per record, curvature at curv_off,
 // indexed by uploaded point (by_pos false) or by pristine position) -> the cloud's normal
@@ -1370,6 +1390,7 @@ dlg_status dlg_ctx_create_dist(dlg_ctx** out, int device, int rank, int world, c
     c->comm = make_rccl_comm(rank, world, uid, &err);
     if (!c->comm) {
       g_last_create_error = err;
+      dlg_ctx_destroy(c.release());  // (its streams, events and device count)
       return DLG_ERR_COMM;
     }
   }
@@ -1398,6 +1419,7 @@ dlg_status dlg_ctx_create_loopback_group(dlg_ctx** out_array, int world, int dev
 
 dlg_status dlg_ctx_destroy(dlg_ctx* c) {
   if (!c) return DLG_OK;
+  if (c->counted) ctx_count_add(c->device, -1);
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->comm.reset();
@@ -1936,7 +1958,10 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         c->comm->timeout_ms = value;
         if (c->solo) c->solo->timeout_ms = value;
         break;
-      case DLG_OPT_SEL1_TICKET: o.sel1_ticket = value != 0; break;
+      case DLG_OPT_SEL1_TICKET:
+        if (value < -1 || value > 1) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_SEL1_TICKET: -1, 0 or 1");
+        o.sel1_ticket = (int)value;
+        break;
       case DLG_OPT_BOUNDS_STREAM: o.bounds_stream = value != 0; break;
       case DLG_OPT_FS_SEGMENTS:
         if (value < 1 || value > kFsSegMax) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_SEGMENTS: 1..16");

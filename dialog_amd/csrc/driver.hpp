@@ -186,14 +186,16 @@ struct PathOptions {
                            // middle of extract round fault_round - 1 (after the round's scoring)
   bool sync_check = false; // DLG_OPT_SYNC_CHECK: per-round allgather of (round, inliers,
                            // coefficient bits, collectives issued), mismatch fails the call
-  bool sel1_ticket = true; // DLG_OPT_SEL1_TICKET: single-pass select tiles numbered by an atomic
-                           // ticket (dispatch order) instead of the workgroup index
+  int sel1_ticket = -1;    // DLG_OPT_SEL1_TICKET: single-pass select tiles numbered by an atomic
+                           // ticket (dispatch order) instead of the workgroup index: 1 always,
+                           // 0 never, -1 while another context of this process shares the device
   bool bounds_stream = false;  // DLG_OPT_BOUNDS_STREAM: lean rounds' survivor sphere bounds on a
                                // second stream beside the list pass (event-ordered)
 };
 
 struct dlg_ctx {
   int device = 0;
+  bool counted = false;  // registered in the per-device context count (ctx_shared)
   PathOptions opt;
   int num_cus = 256;
   hipStream_t stream = nullptr;
@@ -353,6 +355,9 @@ struct dlg_cloud {
 namespace dlg {
 
 inline void set_device(dlg_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
+// live contexts of this process per device (the look-back selects' tile numbering: ctx_shared)
+void ctx_count_add(int device, int delta);
+bool ctx_shared(int device);
 // (several ranks over RCCL: a polling wait that ends when the group is aborted, comm.hpp)
 inline void sync(dlg_ctx* c) { c->group()->sync_stream(c->stream); }
 

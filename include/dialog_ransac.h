@@ -496,10 +496,13 @@ enum {
                                RCCL collective, a round's results) that makes no progress for this
                                long aborts the group (DLG_ERR_COMM on every rank); 0 = no limit;
                                default 600000 */
-  DLG_OPT_SEL1_TICKET = 19, /* single-pass select tiles: 1 (default) numbered by an atomic ticket
-                               taken at dispatch (a tile's predecessors are always resident, so
-                               the look-back completes even beside other contexts' kernels on the
-                               same device); 0 = the workgroup index (A/B only) */
+  DLG_OPT_SEL1_TICKET = 19, /* single-pass select tiles numbered by an atomic ticket taken at
+                               dispatch (a tile's predecessors are then always resident, so the
+                               look-back completes even beside other contexts' spinning selects on
+                               the same device) or by workgroup index (complete in index order
+                               while the launch has the device to itself): -1 (default) tickets
+                               while another context of this process uses the same device, 1
+                               always, 0 never */
   DLG_OPT_BOUNDS_STREAM = 20 /* lean rounds: 1 = the survivors' sphere bounds on a second stream
                                beside the list pass (event-ordered both ways); 0 (default) */
 };

@@ -125,8 +125,9 @@ def test_sync_check_and_side_stream_match_one_rank(gpu_ctx):
 @pytest.mark.gpu
 @pytest.mark.parametrize("ticket,side", [(0, 0), (1, 1), (0, 1)])
 def test_select_tile_numbering_and_side_stream_one_rank(gpu_ctx, ticket, side):
-    """The single-pass selects' tile numbering (DLG_OPT_SEL1_TICKET: 1 ticket, the default; 0
-    workgroup index) and the side-stream bounds give the default path's bits on one rank."""
+    """The single-pass selects' tile numbering (DLG_OPT_SEL1_TICKET: 1 tickets, 0 workgroup index;
+    the default -1 takes tickets while another context shares the device) and the side-stream
+    bounds give the default path's bits on one rank."""
     ctx = D.Context(0)
     ctx.set_option(D.DLG_OPT_SEL1_TICKET, ticket)
     ctx.set_option(D.DLG_OPT_BOUNDS_STREAM, side)
@@ -141,7 +142,7 @@ def test_select_tile_numbering_and_side_stream_one_rank(gpu_ctx, ticket, side):
 @pytest.mark.gpu
 def test_options_reported(gpu_ctx):
     ctx = D.Context(0)
-    assert ctx.get_option(D.DLG_OPT_SEL1_TICKET) == 1
+    assert ctx.get_option(D.DLG_OPT_SEL1_TICKET) == -1
     assert ctx.get_option(D.DLG_OPT_BOUNDS_STREAM) == 0
     assert ctx.get_option(D.DLG_OPT_HYP_SHARD) == -1
     assert ctx.get_option(D.DLG_OPT_COMM_TIMEOUT_MS) == 600000
