@@ -10,8 +10,9 @@
 #include <cstdint>
 
 // A launch that carries timing events on its own dispatch (hipExtLaunchKernelGGL) only when one
-// is asked for: an extended dispatch costs the stream a gap of ~5-6 us on each side even with
-// null events (rocprofv3 kernel trace), the plain launch none.
+// is asked for, else the plain launch.  (Round 6 suspected the extended dispatch of the ~5 us
+// gaps in front of k_prune_supers, k_score_tiles_ex, k_ustamp, k_fs_walk, k_fs_segfix and
+// k_sel1_morton; the kernel trace with plain launches shows the same gaps: not the cause.)
 #define DLG_LAUNCH_EV(kernel, grid, block, shmem, stream, ev0, ev1, ...)                      \
   do {                                                                                         \
     if ((ev0) != nullptr || (ev1) != nullptr)                                                  \
