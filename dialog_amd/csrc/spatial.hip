@@ -1121,20 +1121,22 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
         const uint32_t tag = (uint32_t)(slot0 + (t - t0)) << 12;
         const float tlim = prune_lim(margin, tb.w);
         if (stats && lane == 0) { atomicAdd(&s_st[2], 1ull); atomicAdd(&s_st[1], (unsigned long long)(le - lb)); }
+        const f32x2 tbx = {tb.x, tb.x}, tby = {tb.y, tb.y}, tbz = {tb.z, tb.z};
         auto test4 = [&](uint32_t wa, uint32_t wb, int ea) {
           const int j0 = (int)(wa & 0xFFFFu), j1 = (int)(wa >> 16);
           const int j2 = (int)(wb & 0xFFFFu), j3 = (int)(wb >> 16);
           const float4 c0 = s_cf[j0], c1 = s_cf[j1], c2 = s_cf[j2], c3 = s_cf[j3];
-          // (scalar FMAs: the same products and sums as the packed form, whose operand pairs cost
-          // 12 moves per call and whose v_pk_fma_f32 issues at half rate)
-          auto h = [&](const float4 q) {
-            return __builtin_fmaf(q.x, tb.x, __builtin_fmaf(q.y, tb.y, __builtin_fmaf(q.z, tb.z, q.w)));
-          };
+          const f32x2 ax2 = {c0.x, c1.x}, ay2 = {c0.y, c1.y}, az2 = {c0.z, c1.z}, aw2 = {c0.w, c1.w};
+          const f32x2 bx2 = {c2.x, c3.x}, by2 = {c2.y, c3.y}, bz2 = {c2.z, c3.z}, bw2 = {c2.w, c3.w};
+          const f32x2 ha = __builtin_elementwise_fma(ax2, tbx, __builtin_elementwise_fma(ay2, tby,
+                                                     __builtin_elementwise_fma(az2, tbz, aw2)));
+          const f32x2 hb = __builtin_elementwise_fma(bx2, tbx, __builtin_elementwise_fma(by2, tby,
+                                                     __builtin_elementwise_fma(bz2, tbz, bw2)));
           const int eb = ea + 2 * kWave;
-          const bool n0 = ea < le && fabsf(h(c0)) <= tlim;
-          const bool n1 = ea + 1 < le && fabsf(h(c1)) <= tlim;
-          const bool n2 = eb < le && fabsf(h(c2)) <= tlim;
-          const bool n3 = eb + 1 < le && fabsf(h(c3)) <= tlim;
+          const bool n0 = ea < le && fabsf(ha.x) <= tlim;
+          const bool n1 = ea + 1 < le && fabsf(ha.y) <= tlim;
+          const bool n2 = eb < le && fabsf(hb.x) <= tlim;
+          const bool n3 = eb + 1 < le && fabsf(hb.y) <= tlim;
           const uint64_t m0 = ballot(n0), m1 = ballot(n1), m2 = ballot(n2), m3 = ballot(n3);
           const int k0 = (int)__popcll(m0), k1 = k0 + (int)__popcll(m1), k2 = k1 + (int)__popcll(m2);
           if (n0) ring[(nq + lanes_below(m0)) & (kExRing - 1)] = (uint16_t)(tag | (uint32_t)j0);
