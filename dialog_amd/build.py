@@ -25,6 +25,8 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectori
             "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function",
             # MFMA results in VGPRs (the VALU consumes every element; AGPR copies cost 1 op each)
             "-mllvm", "-amdgpu-mfma-vgpr-form"]
+# (A/B builds only, tools/build_ab.sh: e.g. DLG_EXTRA_CXXFLAGS=-DDLG_WG_TRACE)
+CXXFLAGS += os.environ.get("DLG_EXTRA_CXXFLAGS", "").split()
 
 
 def hipcc() -> str:

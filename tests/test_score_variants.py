@@ -17,8 +17,9 @@ VARIANTS = (0, 1, 2)  # DLG_SCORE_EXACT (PCL op order), DLG_SCORE_BF16 (matrix c
 # A/B-only variants 11, 14 (1 / 4 planes per lane), 12 (packed f32 tests) and the claim variants
 # 15 (round 4's round-robin), 16 (list-length classes, no tail), 17 (tail, no classes), and
 # DLG_TILE_MFMA (2: f32 matrix-core groups of 16 planes + band re-decision; 18: the same with
-# every result re-decided, 19: a 64 u S band -- A/B checks of the band)
-TILE_SCORERS = (2, 18, 19, 1, 11, 12, 14, 15, 16, 17)
+# every result re-decided, 19: a 64 u S band -- A/B checks of the band), 21 (long lists split
+# into 1024-entry chunk items; the "wide" case's threshold puts most planes on every list)
+TILE_SCORERS = (2, 18, 19, 21, 1, 11, 12, 14, 15, 16, 17)
 
 
 def counts(ctx, cloud, D, v, thr):
@@ -44,6 +45,9 @@ def make(case):
         p[::97, 1] = np.nan
         p[5::1013, 2] = np.inf
         return p, 0.02
+    if case == "wide":
+        p, _, _ = plane_cloud(300_007, 6, sigma=0.01, seed=15)
+        return p, 0.3
     if case == "tiny":
         p, _, _ = plane_cloud(1_000, 3, sigma=0.01, seed=14)
         return (p * np.float32(1e-3)).astype(np.float32), 2e-5
@@ -51,7 +55,7 @@ def make(case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["noisy", "far", "nonfinite", "tiny"])
+@pytest.mark.parametrize("case", ["noisy", "far", "nonfinite", "wide", "tiny"])
 def test_score_variants_bit_identical(gpu_ctx, case):
     import dialog_amd as D
     p, thr = make(case)

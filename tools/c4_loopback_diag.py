@@ -1,6 +1,7 @@
 """C4's 100M-point cloud over 8 in-process loopback ranks (tests/test_fullsize_golden.py's
 sharded run), repeated, with context options given on the command line; one JSON line per run:
-every rank's outcome (ok + bits equal to the golden ones, or its error) and wall time.
+every rank's outcome (ok + bits equal to the golden ones, or its error) and wall time; with
+PROFILE=1 also every rank's phase split (score / select / PCL refit walk / rebase / repair ms).
 
     python tools/c4_loopback_diag.py pcl 3 FS_ONE_WALK=1 SEL1_TICKET=0 BOUNDS_STREAM=1
 
@@ -31,6 +32,7 @@ def sha(a):
 def main():
     mode, reps = sys.argv[1], int(sys.argv[2])
     opts = [(getattr(D, "DLG_OPT_" + o.split("=")[0]), int(o.split("=")[1])) for o in sys.argv[3:]]
+    prof = os.environ.get("PROFILE") == "1"
     w = DB["c4shape"]
     g = w["modes"][mode]
     p, _, _ = plane_cloud(w["n_points"], w["planes"], seed=w["seed"], shares=w["shares"])
@@ -47,6 +49,8 @@ def main():
             try:
                 for o, v in opts:
                     ctxs[r].set_option(o, v)
+                if prof:
+                    ctxs[r].set_profiling(True)
                 c = D.Cloud(ctxs[r], p[b[r]:b[r + 1]], id_base=b[r])
                 e = D.extract_planes(c, prm, max_planes=20, min_inliers=500, capacity=p.shape[0])
                 c.close()
@@ -55,6 +59,12 @@ def main():
                       and [sha(e["inliers"][offs[k]:offs[k + 1]]) for k in range(e["n_planes"])]
                       == g["inliers_sha256"])
                 res[r] = dict(rank=r, ok=bool(ok), t=round(time.monotonic() - t0, 2))
+                if prof:
+                    st = e["stats"]
+                    res[r]["ms"] = {k: round(st[k], 3) for k in (
+                        "score_ms", "select_ms", "refit_walk_ms", "refit_rebase_ms",
+                        "refit_repair_ms", "wall_ms")}
+                    res[r]["rounds"] = st["rounds"]
             except Exception as ex:
                 res[r] = dict(rank=r, ok=False, err=str(ex), t=round(time.monotonic() - t0, 2))
 

@@ -53,7 +53,7 @@ for s in "$@"; do
              python3 -u -m pytest ${arg//,/ } -m gpu -x -v --timeout 240 --timeout-method thread ;;
     gputests) run gputests 1100 python3 -u -m pytest tests -m gpu -x -v --durations=15 --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
-    ab) run ab 300 env PRUNE_STATS=1 python3 -u tools/score_ab.py ${arg//,/ } ;;
+    ab) run ab_$(echo "$arg" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-30) 300 env PRUNE_STATS=1 python3 -u tools/score_ab.py ${arg//,/ } ;;
     bench) run bench_$(echo "$arg" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40)_$(echo "$arg" | md5sum | cut -c1-6) 900 \
              python3 -u bench.py --steps 10 --warmup 3 ${arg//,/ } ;;
     benchfull) run benchfull 900 python3 -u bench.py ;;
