@@ -1977,7 +1977,6 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         if (value != DLG_TILE_EXACT && value != DLG_TILE_BF16 && value != DLG_TILE_MFMA &&
             value != kTileScorerExK1 && value != kTileScorerMfmaX && value != kTileScorerMfmaW &&
             value != kTileScorerExK4 && value != kTileScorerExPk &&
-            value != kTileScorerSplit &&
             !(value >= kTileScorerClaimR4 && value <= kTileScorerClaimTail))
           throw DlgError(DLG_ERR_INVALID, "DLG_OPT_PRUNE_TILE_SCORER: DLG_TILE_EXACT or DLG_TILE_BF16");
         o.tile_scorer = (int)value;

@@ -644,7 +644,6 @@ constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad 
                                // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
 constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
 constexpr int kStaticNum = 7, kStaticDen = 8;  // k_score_tiles_ex: items dealt before the tail
-constexpr int kItemBits = 26, kItemMask = (1 << kItemBits) - 1;  // split items: chunk << kItemBits
 constexpr int64_t kOrderMaxSupers = 65536;      // class-ordered claims up to this many super-tiles
 // NORMAL_PLANE slots: x[32] y[32] z[32] lim[32] + pad (bases 0, 132, 264, 396 dwords: banks 0,
 // 4, 8, 12, disjoint for b128)
@@ -800,7 +799,7 @@ __device__ __forceinline__ void mf_pass(int m, const uint16_t* ring, int head, c
   }
 #pragma unroll
   for (int g = 0; g < G; ++g)
-    if (g < ng && cnt[g]) atomicAdd(&s_cnt[jj[g] & 0xFFF], cnt[g]);
+    if (g < ng && cnt[g]) atomicAdd(&s_cnt[(jj[g] & 0xFFF) >> 1], cnt[g] << (16 * (jj[g] & 1)));
 }
 
 // NPM (SACMODEL_NORMAL_PLANE, K = 2): the pass evaluates PCL's prefilter b = (1 - w) d_euclid <
@@ -830,7 +829,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   constexpr int kChunk = 2;  // tiles per item
   constexpr int kSlotF = NPM ? kExSlotNp : kExSlotF;
   __shared__ float4 s_cf[kMaxHypPerLaunch];
-  __shared__ uint32_t s_cnt[kMaxHypPerLaunch];  // (32-bit: no cap on a workgroup's points)
+  __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves: <= 65535 points per workgroup
   __shared__ __attribute__((aligned(8))) uint16_t s_ring[BS / kWave][kExRing];
   __shared__ __attribute__((aligned(16))) float s_pt[BS / kWave][4 * kSlotF];
   __shared__ int s_own[NPM ? BS / kWave : 1][NPM ? kWave : 1];   // NPM: chunk owners
@@ -844,7 +843,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
   }
   if (threadIdx.x == 0) s_taken = 0;
-  for (int j = threadIdx.x; j < kMaxHypPerLaunch; j += BS) s_cnt[j] = 0u;
+  for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += BS) s_cnt[j] = 0u;
   if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
   __syncthreads();
   const int ntiles = (n + kTileP - 1) / kTileP;
@@ -869,42 +868,28 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     nx_st += o_cnt[b];
   }
   if (!order) nx_st = xcd ? (nsup - xw + 7) / 8 : nsup;
-  // order 2 (split items): a super-tile of list-length class 0 (>= 2048 near planes) gives 4 x ips
-  // items, class 1 (>= 1024) 2 x ips, one per kListCap-entry chunk of its list (the chunk in the
-  // item's bits kItemBits..): a long list is no longer one wave's serial work
-  const bool split = order == 2;
-  auto mult = [&](int q) -> int64_t { return split && q < 2 ? 4 >> q : 1; };
-  int64_t nx_it = nx_st * ips;  // (uniform: this XCD's items)
-  if (split) {
-    nx_it = 0;
-#pragma unroll
-    for (int b = 0; b < kPwBuckets; ++b) nx_it += o_cnt[b] * ips * mult(b);
-  }
   const int64_t gx = xcd ? (int64_t)(gridDim.x >> 3) : (int64_t)gridDim.x;  // this XCD's workgroups
   const int64_t bx = xcd ? (int64_t)(blockIdx.x >> 3) : (int64_t)blockIdx.x;
   // (tail 0: every item dealt round-robin, round 4's claim)
-  const int64_t n_static = tail ? (nx_it * kStaticNum / kStaticDen) / gx * gx : nx_it;
+  const int64_t n_static = tail ? (nx_st * ips * kStaticNum / kStaticDen) / gx * gx : nx_st * ips;
   // the XCD's l-th item (-1: the last super-tile's missing items; nitems: past the end)
   auto item_of = [&](int64_t l) -> int64_t {
+    int64_t i = l / ips;
+    int64_t st;
     if (order) {
-      int64_t r = l, per = ips;
       int b = kPwBuckets;
 #pragma unroll
       for (int q = 0; q < kPwBuckets; ++q)  // (unrolled: o_cnt stays in registers)
         if (b == kPwBuckets) {
-          const int64_t nq = o_cnt[q] * ips * mult(q);
-          if (r < nq) { b = q; per = ips * mult(q); }
-          else r -= nq;
+          if (i < o_cnt[q]) b = q;
+          else i -= o_cnt[q];
         }
       if (b == kPwBuckets) return nitems;
-      const int64_t st = ord_of(lp_n, nsup, xw, b)[r / per];
-      const int64_t w = r % per;  // (chunk-major: a chunk's items share its list slice in L2)
-      const int64_t itm = st * ips + w % ips;
-      return itm < nitems ? itm + ((w / ips) << kItemBits) : -1;
+      st = ord_of(lp_n, nsup, xw, b)[i];
+    } else {
+      st = xcd ? (int64_t)xw + 8 * i : i;
+      if (st >= nsup) return nitems;
     }
-    const int64_t i = l / ips;
-    const int64_t st = xcd ? (int64_t)xw + 8 * i : i;
-    if (st >= nsup) return nitems;
     const int64_t itm = st * ips + l % ips;
     return itm < nitems ? itm : -1;
   };
@@ -924,8 +909,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   };
   // lane l holds point l of an item (its two tiles); NaN past n.  NPM: and its prefilter limit
   // (-inf: never passes; a NaN w leaves the exact test NaN < thr, never an inlier)
-  auto fetch = [&](int itc, float& px, float& py, float& pz, float& pl) {
-    const int it = itc & kItemMask;
+  auto fetch = [&](int it, float& px, float& py, float& pz, float& pl) {
     const int64_t p = (int64_t)it * (kChunk * kTileP) + lane;
     px = py = pz = __builtin_nanf("");
     pl = -INFINITY;
@@ -1021,7 +1005,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
           const float4 nn = NRM[(int64_t)s_stile[wv][slot] * kTileP + pt];
           const double w = lambda * (1.0 - (double)nn.w);
           if (np_full(CN[jj], nn, w, (1.0 - w) * (double)de, thr))
-            atomicAdd(&s_cnt[jj], 1u);
+            atomicAdd(&s_cnt[jj >> 1], 1u << (16 * (jj & 1)));
         }
       }
       head += m;
@@ -1062,7 +1046,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int j = (int)(e[k] & 0xFFFu);
-      if (acc[k]) atomicAdd(&s_cnt[j], acc[k]);  // (pads count 0)
+      if (acc[k]) atomicAdd(&s_cnt[j >> 1], acc[k] << (16 * (j & 1)));  // (pads count 0)
     }
     head += m;
   };
@@ -1080,7 +1064,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   float px, py, pz, pl;
   fetch(it_next, px, py, pz, pl);
   for (int seq = 0;; ++seq) {
-    const int it = it_next & kItemMask, chunk = it_next >> kItemBits;
+    const int it = it_next;
     if (it >= nitems) break;
     it_next = claim();
     const int t0 = it * kChunk, t_end = min(ntiles, t0 + kChunk);
@@ -1106,9 +1090,8 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
       __builtin_amdgcn_wave_barrier();
     }
     fetch(it_next, px, py, pz, pl);  // the next item's points, in flight during this one
-    const int lb_end = split ? min(nlp, (chunk + 1) * kListCap) : nlp;
 #pragma unroll 1
-    for (int lb = chunk * kListCap; lb < lb_end; lb += kListCap) {
+    for (int lb = 0; lb < nlp; lb += kListCap) {
       const int le = min(nlp, lb + kListCap);
       uint32_t L[kListRegs];
 #pragma unroll
@@ -1165,7 +1148,7 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   if (nq > head) pass(nq - head);
   __syncthreads();
   for (int j = threadIdx.x; j < D; j += BS) {
-    const int c = (int)s_cnt[j];
+    const int c = (int)((s_cnt[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
     if (c) atomicAdd(&counts[j], c);
   }
   if (stats && threadIdx.x < 6) atomicAdd(&stats[threadIdx.x], s_st[threadIdx.x]);
@@ -1334,10 +1317,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   constexpr int kBS = 1024, kChunkTiles = 2;
   static_assert(kSuperTiles % kChunkTiles == 0, "an item stays inside one super-tile");
   const int64_t items = (sp_tiles(v.n) + kChunkTiles - 1) / kChunkTiles;
-  // (k_score_tiles_ex counts in 32-bit LDS words since round 6: the split items' launch drops
-  // the cap; the others keep round 5's grid)
-  const bool split = tile_scorer == kTileScorerSplit && !np;
-  const int blk_cap = split ? (1 << 30) : 65535 / (kChunkTiles * kTileP);
+  const int blk_cap = 65535 / (kChunkTiles * kTileP);
   int64_t g = std::max<int64_t>(
       1, std::max<int64_t>(std::min<int64_t>(num_cus, (items + kBS / kWave - 1) / (kBS / kWave)),
                            (items + blk_cap - 1) / blk_cap));
@@ -1361,7 +1341,7 @@ void launch_score_pruned(const SpatialView& v, const HypRec* hyps, int D, float 
   // launch 0.418 -> 0.409 ms, at C4's 100M points on one GPU (195k) it costs the prune launch 97
   // -> 187 us (the bucket appends' atomics) and the scoring 1465 -> 1610 us (r05j4-j7)
   const int order = ex && xcd && ns <= kOrderMaxSupers && tile_scorer != kTileScorerClaimR4 &&
-                            tile_scorer != kTileScorerClaimTail ? (split ? 2 : 1) : 0;
+                            tile_scorer != kTileScorerClaimTail ? 1 : 0;
   const int tail = claim_ab && tile_scorer != kTileScorerClaimTail ? 0 : 1;
   // (timing events, when given, ride the two dispatches themselves: no marker packets, so no
   // launch gaps around the scoring)

@@ -86,8 +86,6 @@ constexpr int kTileScorerMfmaW = 19;  // A/B check: the same with a band of 64 u
 constexpr int kTileScorerExK1 = 11, kTileScorerExK4 = 14;
 constexpr int kTileScorerExPk = 12;
 constexpr int kTileScorerClaimR4 = 15, kTileScorerClaimClass = 16, kTileScorerClaimTail = 17;  // A/B
-// A/B: the class order with long lists split into kListCap-entry chunk items, no per-workgroup cap
-constexpr int kTileScorerSplit = 21;
 // the pruned scorer's int32 buffer: a fixed header of kPwHeader words -- the item counters (one
 // per XCD, each on its own 128-byte line, kPruneWorkStride words apart), per XCD the counts of its
 // super-tiles in each of kPwBuckets list-length classes (k_prune_supers appends them,

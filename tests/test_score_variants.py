@@ -17,9 +17,9 @@ VARIANTS = (0, 1, 2)  # DLG_SCORE_EXACT (PCL op order), DLG_SCORE_BF16 (matrix c
 # A/B-only variants 11, 14 (1 / 4 planes per lane), 12 (packed f32 tests) and the claim variants
 # 15 (round 4's round-robin), 16 (list-length classes, no tail), 17 (tail, no classes), and
 # DLG_TILE_MFMA (2: f32 matrix-core groups of 16 planes + band re-decision; 18: the same with
-# every result re-decided, 19: a 64 u S band -- A/B checks of the band), 21 (long lists split
-# into 1024-entry chunk items; the "wide" case's threshold puts most planes on every list)
-TILE_SCORERS = (2, 18, 19, 21, 1, 11, 12, 14, 15, 16, 17)
+# every result re-decided, 19: a 64 u S band -- A/B checks of the band); the "wide" case's
+# threshold puts most planes on every super-tile's list (lists past the 1024-entry register chunk)
+TILE_SCORERS = (2, 18, 19, 1, 11, 12, 14, 15, 16, 17)
 
 
 def counts(ctx, cloud, D, v, thr):

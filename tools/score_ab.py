@@ -20,10 +20,10 @@ from dialog_amd.synth import SEED_BASE, plane_cloud  # noqa: E402
 
 NAMES = {0: "exact_p4", 1: "bf16_t8", 2: "pruned_ex", 3: "pruned_bf16", 5: "pruned_ex_k1",
          6: "pruned_ex_k4", 7: "pruned_ex_pk", 8: "pruned_mfma", 9: "pruned_ex_claim_r4",
-         10: "pruned_ex_claim_class", 11: "pruned_ex_claim_tail", 12: "pruned_ex_split"}
+         10: "pruned_ex_claim_class", 11: "pruned_ex_claim_tail"}
 # DLG_OPT_PRUNE_TILE_SCORER per pruned variant (2: DLG_TILE_EXACT, the default; 11, 12, 14: A/B
 # only)
-TILE_OPT = {2: 0, 3: 1, 5: 11, 6: 14, 7: 12, 8: 2, 9: 15, 10: 16, 11: 17, 12: 21}
+TILE_OPT = {2: 0, 3: 1, 5: 11, 6: 14, 7: 12, 8: 2, 9: 15, 10: 16, 11: 17}
 
 
 def main():
