@@ -393,7 +393,7 @@ def main():
         extras["incl_index_build"] = {
             "value": round(sum(o["stats"]["tests"] for o in outs) / len(outs) / sec / 1e9, 3),
             "unit": "G point-plane tests/s", "ms_per_step": round(sec * 1e3, 3),
-            "note": "each step rebuilds the Morton-ordered copy and its bounding spheres from "
+            "note": "each step rebuilds the Hilbert-ordered copy and its bounding spheres from "
                     "the device-resident cloud (dlg_cloud_drop_spatial + dlg_cloud_build_spatial), "
                     "then extracts; inputs resident in HBM"}
 
@@ -426,7 +426,7 @@ def main():
     avg_launch_ms = score_ms / max(launches, 1)
     ktests_per_s = per_rank_tests / (score_ms / 1e3) if score_ms > 0 else 0.0
     pruned = a.points >= 131072  # (the library builds the Morton copy for such clouds)
-    kname = ("k_prune_supers + k_score_tiles_ex (countWithinDistance over the Morton-ordered copy: "
+    kname = ("k_prune_supers + k_score_tiles_ex (countWithinDistance over the Hilbert-ordered copy: "
              "super-tile and tile bounding spheres rule out (tile, plane) pairs with no possible "
              "PCL inlier; the rest evaluated exactly in PCL's f32 op order, lanes as planes; "
              f"{a.hyps} hypotheses/launch)" if pruned else

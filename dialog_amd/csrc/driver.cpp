@@ -329,7 +329,7 @@ void build_spatial(dlg_ctx* c, dlg_cloud* cl) {
     HIPCHK(hipMemsetAsync(c->totals.p, 0, 4, c->stream));
     c->mxyz.ensure((size_t)std::max<int64_t>(n, 1));
     launch_morton_keys(cl->pristine.view(n), cl->amax[0], cl->amax[1], cl->amax[2], k0.p, i0.p,
-                       c->totals.p, c->mxyz.p, c->stream);
+                       c->totals.p, c->mxyz.p, c->stream, c->opt.spatial_curve == 1);
     HIPCHK(morton_sort(tmp.p, tb, k0.p, k1.p, i0.p, i1.p, n, c->stream));
     int32_t nonfinite = 0;
     HIPCHK(hipMemcpyAsync(&nonfinite, c->totals.p, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1963,6 +1963,10 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         o.sel1_ticket = (int)value;
         break;
       case DLG_OPT_BOUNDS_STREAM: o.bounds_stream = value != 0; break;
+      case DLG_OPT_SPATIAL_CURVE:
+        if (value < 0 || value > 1) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_SPATIAL_CURVE: 0 or 1");
+        o.spatial_curve = (int)value;
+        break;
       case DLG_OPT_FS_SEGMENTS:
         if (value < 1 || value > kFsSegMax) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_SEGMENTS: 1..16");
         o.fs_segments = (int)value;
@@ -2007,6 +2011,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_COMM_TIMEOUT_MS: *value = c->comm->timeout_ms; break;
     case DLG_OPT_SEL1_TICKET: *value = o.sel1_ticket; break;
     case DLG_OPT_BOUNDS_STREAM: *value = o.bounds_stream; break;
+    case DLG_OPT_SPATIAL_CURVE: *value = o.spatial_curve; break;
     case DLG_OPT_FS_ONE_WALK: *value = o.fs_protocol; break;
     case DLG_OPT_FS_SEGMENTS: *value = o.fs_segments; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;

@@ -191,6 +191,7 @@ struct PathOptions {
                            // 0 never, -1 while another context of this process shares the device
   bool bounds_stream = false;  // DLG_OPT_BOUNDS_STREAM: lean rounds' survivor sphere bounds on a
                                // second stream beside the list pass (event-ordered)
+  int spatial_curve = 1;  // DLG_OPT_SPATIAL_CURVE: 1 Hilbert, 0 Morton order of the spatial copy
 };
 
 struct dlg_ctx {

@@ -33,11 +33,38 @@ __device__ __forceinline__ uint32_t quant10(float v, float a) {
   return (uint32_t)fminf(fmaxf(t, 0.0f), 1023.0f);
 }
 
+// Hilbert index of the 10-bit cell (x, y, z) (Skilling's transpose form: undo the excess work of
+// each bit level's Gray-code reflections, Gray-decode, then interleave the three words as a
+// Morton key would).  Consecutive keys are face-adjacent cells, so a run of 32 points -- a tile --
+// stays in one connected patch of the curve: no Z-order jump across the cloud inside a tile.
+// (tools: the curve's unit steps and the tiles' sphere radii checked by a numpy model.)
+__device__ __forceinline__ uint32_t hilbert10(uint32_t x, uint32_t y, uint32_t z) {
+  uint32_t X0 = x, X1 = y, X2 = z;
+#pragma unroll
+  for (uint32_t Q = 1u << 9; Q > 1u; Q >>= 1) {
+    const uint32_t P = Q - 1u;
+    if (X0 & Q) X0 ^= P;
+    if (X1 & Q) X0 ^= P;
+    else { const uint32_t t = (X0 ^ X1) & P; X0 ^= t; X1 ^= t; }
+    if (X2 & Q) X0 ^= P;
+    else { const uint32_t t = (X0 ^ X2) & P; X0 ^= t; X2 ^= t; }
+  }
+  X1 ^= X0;
+  X2 ^= X1;
+  uint32_t t = 0u;
+#pragma unroll
+  for (uint32_t Q = 1u << 9; Q > 1u; Q >>= 1)
+    if (X2 & Q) t ^= Q - 1u;
+  X0 ^= t; X1 ^= t; X2 ^= t;
+  return (spread10(X0) << 2) | (spread10(X1) << 1) | spread10(X2);
+}
+
 // (also writes the points as (x, y, z, 0) records: k_gather_order and k_ucompact gather from
 // them, one 16-byte record per point instead of three scattered floats)
 __global__ void k_morton_keys(PointsView src, float ax, float ay, float az,
                               uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
-                              int32_t* __restrict__ n_nonfinite, float4* __restrict__ aos) {
+                              int32_t* __restrict__ n_nonfinite, float4* __restrict__ aos,
+                              int hilbert) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool nf = false;
   if (i < src.n) {
@@ -45,7 +72,8 @@ __global__ void k_morton_keys(PointsView src, float ax, float ay, float az,
     aos[i] = make_float4(x, y, z, 0.0f);
     uint32_t k = 0xFFFFFFFFu;
     if (isfinite(x) && isfinite(y) && isfinite(z))
-      k = spread10(quant10(x, ax)) | (spread10(quant10(y, ay)) << 1) | (spread10(quant10(z, az)) << 2);
+      k = hilbert ? hilbert10(quant10(x, ax), quant10(y, ay), quant10(z, az))
+                  : spread10(quant10(x, ax)) | (spread10(quant10(y, ay)) << 1) | (spread10(quant10(z, az)) << 2);
     else
       nf = true;
     keys[i] = k;
@@ -1220,10 +1248,11 @@ __global__ void k_curv_range(const float4* __restrict__ nrm, int64_t n, uint32_t
 }  // namespace
 
 void launch_morton_keys(PointsView src, float ax, float ay, float az, uint32_t* keys,
-                        int32_t* idx, int32_t* n_nonfinite, float4* aos, hipStream_t s) {
+                        int32_t* idx, int32_t* n_nonfinite, float4* aos, hipStream_t s,
+                        bool hilbert) {
   if (src.n <= 0) return;
   hipLaunchKernelGGL(k_morton_keys, dim3((unsigned)((src.n + 255) / 256)), dim3(256), 0, s, src,
-                     ax, ay, az, keys, idx, n_nonfinite, aos);
+                     ax, ay, az, keys, idx, n_nonfinite, aos, hilbert ? 1 : 0);
 }
 
 size_t morton_sort_temp_bytes(int64_t n) {

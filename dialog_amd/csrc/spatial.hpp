@@ -51,11 +51,12 @@ __device__ __forceinline__ bool sphere_near(float4 cf, float4 sp, float margin) 
   return fabsf(h) <= prune_lim(margin, sp.w);
 }
 
-// Morton keys over [-amax, amax] per axis; non-finite points get key 0xFFFFFFFF (sorted last)
-// and are counted into *n_nonfinite (never inliers of any plane: PCL's distance is NaN or inf);
-// aos[i] = (x, y, z, 0) of point i
+// Curve keys over [-amax, amax] per axis, 10 bits per axis: Hilbert (hilbert, the default) or
+// Morton; non-finite points get key 0xFFFFFFFF (sorted last) and are counted into *n_nonfinite
+// (never inliers of any plane: PCL's distance is NaN or inf); aos[i] = (x, y, z, 0) of point i
 void launch_morton_keys(PointsView src, float ax, float ay, float az, uint32_t* keys,
-                        int32_t* idx, int32_t* n_nonfinite, float4* aos, hipStream_t s);
+                        int32_t* idx, int32_t* n_nonfinite, float4* aos, hipStream_t s,
+                        bool hilbert = true);
 size_t morton_sort_temp_bytes(int64_t n);
 hipError_t morton_sort(void* tmp, size_t tmp_bytes, uint32_t* keys_in, uint32_t* keys_out,
                        int32_t* idx_in, int32_t* idx_out, int64_t n, hipStream_t s);

@@ -43,6 +43,7 @@ extern "C" {
  * the tile-scorer option's getter returns the value set.
  * 5: a failing rank aborts its group (peers return DLG_ERR_COMM); DLG_OPT_FAULT_INJECT,
  * DLG_OPT_SYNC_CHECK, DLG_OPT_COMM_TIMEOUT_MS, DLG_OPT_SEL1_TICKET, DLG_OPT_BOUNDS_STREAM;
+ * DLG_OPT_SPATIAL_CURVE (same ABI version: an added option);
  * DLG_OPT_HYP_SHARD defaults to -1 (automatic); dlg_shard_range */
 #define DLG_ABI_VERSION 5
 
@@ -503,8 +504,13 @@ enum {
                                while the launch has the device to itself): -1 (default) tickets
                                while another context of this process uses the same device, 1
                                always, 0 never */
-  DLG_OPT_BOUNDS_STREAM = 20 /* lean rounds: 1 = the survivors' sphere bounds on a second stream
+  DLG_OPT_BOUNDS_STREAM = 20, /* lean rounds: 1 = the survivors' sphere bounds on a second stream
                                beside the list pass (event-ordered both ways); 0 (default) */
+  DLG_OPT_SPATIAL_CURVE = 21 /* the spatial copy's point order (tiles of 32 consecutive points):
+                               1 (default) = Hilbert curve, 0 = Morton (Z-order, rounds 1-5).
+                               Same results either way; Hilbert tiles are more compact (no Z
+                               jumps inside a tile), so fewer (tile, plane) pairs pass the
+                               sphere tests.  Applies to clouds built after the change */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1, DLG_TILE_MFMA = 2 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };

@@ -144,6 +144,7 @@ def test_options_reported(gpu_ctx):
     ctx = D.Context(0)
     assert ctx.get_option(D.DLG_OPT_SEL1_TICKET) == -1
     assert ctx.get_option(D.DLG_OPT_BOUNDS_STREAM) == 0
+    assert ctx.get_option(D.DLG_OPT_SPATIAL_CURVE) == 1
     assert ctx.get_option(D.DLG_OPT_HYP_SHARD) == -1
     assert ctx.get_option(D.DLG_OPT_COMM_TIMEOUT_MS) == 600000
     ctx.set_option(D.DLG_OPT_COMM_TIMEOUT_MS, 1234)

@@ -246,7 +246,8 @@ def test_lean_list_indexed_cloud(gpu_ctx, optimize):
 def test_path_options_identical(gpu_ctx, seed):
     """Every execution-path option (dlg_ctx_set_option) gives the same planes and inliers: lean
     vs two-pass selects, speculative vs host pick, pruned vs exhaustive bf16 vs exact VALU
-    scoring -- each against the oracle's optimize-off extraction (the paths lean rounds take)."""
+    scoring, Hilbert vs Morton order of the spatial copy -- each against the oracle's optimize-off
+    extraction (the paths lean rounds take)."""
     rng = np.random.default_rng(900 + seed)
     p, _, _ = plane_cloud(int(rng.integers(20000, 80000)), int(rng.integers(2, 7)),
                           seed=seed + 300, outlier_frac=float(rng.uniform(0.05, 0.4)))
@@ -259,7 +260,8 @@ def test_path_options_identical(gpu_ctx, seed):
               {D.DLG_OPT_PRUNE: 0}, {D.DLG_OPT_PRUNE: 0, D.DLG_OPT_SCORE_KERNEL: D.DLG_SCORE_EXACT},
               {D.DLG_OPT_SELECT_TILE: 4096}, {D.DLG_OPT_SELECT_TILE: 8192},
               {D.DLG_OPT_SELECT_TILE: 16384},
-              {D.DLG_OPT_PRUNE_TILE_SCORER: D.DLG_TILE_BF16}]
+              {D.DLG_OPT_PRUNE_TILE_SCORER: D.DLG_TILE_BF16},
+              {D.DLG_OPT_SPATIAL_CURVE: 0}]  # (Morton-ordered copy; the default is Hilbert)
     for opts in combos:
         ctx = D.Context(0)
         try:
