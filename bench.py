@@ -22,8 +22,8 @@ with its PMC traffic, issue view and the work the pruning leaves (pruned_work). 
 the same JSON object: refit_fast (DLG_REFIT_FAST, an exact least-squares refit -- NOT PCL's
 arithmetic: its planes differ from PCL's), incl_index_build (the Morton copy + spheres rebuilt
 every step), secondary (C5).  cpu_baseline: the PCL-1.8 restatement (oracle) on the box's host
-cores (every CPU of the process's affinity mask for countWithinDistance; the box's 16-CPU share
-and a single-thread sample beside it), rank 0 at N = 1.
+cores (every CPU the process can use for countWithinDistance: its affinity mask capped by the
+cgroup CPU quota; the box's 16-CPU share and a single-thread sample beside it), rank 0 at N = 1.
 """
 from __future__ import annotations
 
@@ -569,9 +569,11 @@ def main():
         except OSError:
             pass
         # three legs of the oracle's segment() (countWithinDistance over OpenMP threads; integer
-        # sums: the same counts): every host CPU the process may run on (the headline cpu leg),
-        # the box's CPU share (--cpu-threads, 16 on the GPU box), and one thread (PCL 1.8's
-        # RANSAC is serial)
+        # sums: the same counts): every host CPU the process can use (the headline cpu leg: the
+        # affinity mask, capped by the cgroup's CPU quota -- on the GPU box 256 CPUs in the mask
+        # but a 16-CPU quota, where 256 threads ran 525 s, throttled), the box's CPU share
+        # (--cpu-threads, 16 on the GPU box; the same leg when the quota already is 16), and one
+        # thread (PCL 1.8's RANSAC is serial)
         try:
             affinity = len(os.sched_getaffinity(0))
         except AttributeError:
@@ -594,19 +596,21 @@ def main():
             dt = time.perf_counter() - t0
             return r["iterations"] * pts.shape[0] / dt / 1e9, dt
 
-        v_all, dt_all = seg_leg(affinity, a.hyps)
-        thr = max(1, min(a.cpu_threads, affinity))
-        v_share, dt_share = seg_leg(thr, a.hyps)
+        usable = affinity if quota is None else max(1, min(affinity, int(quota)))
+        v_all, dt_all = seg_leg(usable, a.hyps)
+        thr = max(1, min(a.cpu_threads, usable))
+        v_share, dt_share = (v_all, dt_all) if thr == usable else seg_leg(thr, a.hyps)
         v_one, dt_one = seg_leg(1, a.cpu_hyps)
         O.set_threads(1)
         cpu = {"value": round(v_all, 4),
-               "unit": "G point-plane tests/s", "cores": affinity, "kind": "port",
+               "unit": "G point-plane tests/s", "cores": usable, "kind": "port",
                "sample": f"one PCL SACSegmentation::segment (the first extraction round) on the "
                          f"same {pts.shape[0]}-pt cloud with {a.hyps} hypotheses + refit + select, "
-                         f"oracle/pcl_oracle.c with countWithinDistance over {affinity} OpenMP "
-                         f"threads (every CPU in the process's affinity mask; OpenMP static "
-                         f"schedule, threads placed by the OS over {numa} NUMA node(s); cgroup CPU "
-                         f"quota {quota if quota is not None else 'none'}), {dt_all:.1f} s",
+                         f"oracle/pcl_oracle.c with countWithinDistance over {usable} OpenMP "
+                         f"threads (every CPU the process can use: {affinity} in its affinity "
+                         f"mask, cgroup CPU quota {quota if quota is not None else 'none'}; OpenMP "
+                         f"static schedule, threads placed by the OS over {numa} NUMA node(s)), "
+                         f"{dt_all:.1f} s",
                "share": {"value": round(v_share, 4), "cores": thr,
                          "sample": f"the same segment() over {thr} threads (the GPU box's CPU "
                                    f"share per GPU), {dt_share:.1f} s"},

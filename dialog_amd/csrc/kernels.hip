@@ -661,7 +661,10 @@ __global__ __launch_bounds__(kPickBS) void k_pick_p1(PickArgs a) { pick_body<kPi
 // the publish by the nthr threads of one workgroup (k_publish, or the last tile of a fused
 // select); tot01: the select's own totals[0..1] when the caller has just computed them (the
 // global words may not be visible yet), else null
-__device__ __forceinline__ void publish_body(const PubArgs& a, const int32_t* tot01, int t, int nthr) {
+// (own01: totals[0..1] from t0 / t1 instead of a.totals -- two scalars, not an array: a
+// dynamically indexed local array would put the whole kernel on scratch)
+__device__ __forceinline__ void publish_body(const PubArgs& a, bool own01, int32_t t0, int32_t t1,
+                                             int t, int nthr) {
   // (the sticky look-back error word, read coherently at agent scope.  A predecessor tile whose
   // aggregate the last tile already summed can still give up after this publish: that failure
   // then surfaces at the next publish or at the extraction's end check, and the extraction throws
@@ -671,7 +674,7 @@ __device__ __forceinline__ void publish_body(const PubArgs& a, const int32_t* to
   if (t == 0)
     a.pub[kPubErr] = a.err ? __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   for (int i = t; i < a.ntot; i += nthr)
-    a.pub[kPubTot + i] = tot01 && i < 2 ? tot01[i] : a.totals[i];
+    a.pub[kPubTot + i] = own01 && i < 2 ? (i == 0 ? t0 : t1) : a.totals[i];
   for (int i = t; i < 4 * a.nsmall; i += nthr)
     a.pub[kPubSmall + i] = __float_as_int(reinterpret_cast<const float*>(a.small)[i]);
   for (int i = t; i < a.npick; i += nthr) a.pub[kPubPick + i] = a.pick[i];
@@ -683,7 +686,7 @@ __device__ __forceinline__ void publish_body(const PubArgs& a, const int32_t* to
 }
 
 __global__ __launch_bounds__(256) void k_publish(PubArgs a) {
-  publish_body(a, nullptr, threadIdx.x, 256);
+  publish_body(a, false, 0, 0, threadIdx.x, 256);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1037,8 +1040,7 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_morton(PointsView src, const flo
       totals[4] = (int32_t)(src.n - in);
     }
     if (pa.pub) {
-      const int32_t t01[2] = {in, (int32_t)(n_list - in)};
-      publish_body(pa, t01, threadIdx.x, kS1BS);
+      publish_body(pa, true, in, (int32_t)(n_list - in), threadIdx.x, kS1BS);
     }
   }
 }
