@@ -671,6 +671,7 @@ constexpr int kExRing = 1024;  // >= 64 K - 1 queued + 256 appended per list ste
 constexpr int kExSlotF = 100;  // floats per tile slot: x[32] y[32] z[32] + pad (slot bases 0,
                                // 100, 200, 300 dwords: banks 0, 36, 8, 44, disjoint for b128)
 constexpr uint32_t kExPad = 0x4000u;  // ring entry flag: padding (no plane)
+constexpr uint32_t kExNone = kMaxHypPerLaunch;  // list-register filler past a list's end
 constexpr int kStaticNum = 7, kStaticDen = 8;  // k_score_tiles_ex: items dealt before the tail
 constexpr int64_t kOrderMaxSupers = 65536;      // class-ordered claims up to this many super-tiles
 // NORMAL_PLANE slots: x[32] y[32] z[32] lim[32] + pad (bases 0, 132, 264, 396 dwords: banks 0,
@@ -856,7 +857,8 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
   constexpr int kPassN = MF ? kMfPass * kMfG : K * kWave;  // queued entries one pass takes
   constexpr int kChunk = 2;  // tiles per item
   constexpr int kSlotF = NPM ? kExSlotNp : kExSlotF;
-  __shared__ float4 s_cf[kMaxHypPerLaunch];
+  // (+1: plane kExNone, a NaN plane the list registers hold past the list's end -- never near)
+  __shared__ float4 s_cf[kMaxHypPerLaunch + 1];
   __shared__ uint32_t s_cnt[kMaxHypPerLaunch / 2];  // 16-bit halves: <= 65535 points per workgroup
   __shared__ __attribute__((aligned(8))) uint16_t s_ring[BS / kWave][kExRing];
   __shared__ __attribute__((aligned(16))) float s_pt[BS / kWave][4 * kSlotF];
@@ -870,7 +872,10 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
     const HypRec h = hyps[j];
     s_cf[j] = make_float4(h.a, h.b, h.c, h.d);
   }
-  if (threadIdx.x == 0) s_taken = 0;
+  if (threadIdx.x == 0) {
+    s_taken = 0;
+    s_cf[kExNone] = make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
+  }
   for (int j = threadIdx.x; j < kMaxHypPerLaunch / 2; j += BS) s_cnt[j] = 0u;
   if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
   __syncthreads();
@@ -1125,8 +1130,8 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
 #pragma unroll
       for (int k = 0; k < kListRegs; ++k) {
         const int e = lb + 2 * (lane + k * kWave);
-        L[k] = e < le ? lw[(lb >> 1) + lane + k * kWave] : 0u;
-        if (e + 1 >= le) L[k] &= 0xFFFFu;
+        L[k] = e < le ? lw[(lb >> 1) + lane + k * kWave] : (kExNone | kExNone << 16);
+        if (e + 1 >= le) L[k] = (L[k] & 0xFFFFu) | kExNone << 16;
       }
 #pragma unroll 1
       for (int t = t0; t < t_end; ++t) {
@@ -1145,11 +1150,9 @@ __global__ __launch_bounds__(BS) void k_score_tiles_ex(
                                                      __builtin_elementwise_fma(az2, tbz, aw2)));
           const f32x2 hb = __builtin_elementwise_fma(bx2, tbx, __builtin_elementwise_fma(by2, tby,
                                                      __builtin_elementwise_fma(bz2, tbz, bw2)));
-          const int eb = ea + 2 * kWave;
-          const bool n0 = ea < le && fabsf(ha.x) <= tlim;
-          const bool n1 = ea + 1 < le && fabsf(ha.y) <= tlim;
-          const bool n2 = eb < le && fabsf(hb.x) <= tlim;
-          const bool n3 = eb + 1 < le && fabsf(hb.y) <= tlim;
+          // (entries past the list's end are kExNone: a NaN plane, never near)
+          const bool n0 = fabsf(ha.x) <= tlim, n1 = fabsf(ha.y) <= tlim;
+          const bool n2 = fabsf(hb.x) <= tlim, n3 = fabsf(hb.y) <= tlim;
           const uint64_t m0 = ballot(n0), m1 = ballot(n1), m2 = ballot(n2), m3 = ballot(n3);
           const int k0 = (int)__popcll(m0), k1 = k0 + (int)__popcll(m1), k2 = k1 + (int)__popcll(m2);
           if (n0) ring[(nq + lanes_below(m0)) & (kExRing - 1)] = (uint16_t)(tag | (uint32_t)j0);

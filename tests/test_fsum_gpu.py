@@ -119,7 +119,7 @@ def test_device_sums_poisoned_tables(fs):
         ctx.close()
 
 
-@pytest.mark.parametrize("segments", [1, 2, 5, 16])
+@pytest.mark.parametrize("segments", [1, 2, 5, 8, 16])
 def test_device_sums_segments(fs, segments):
     """DLG_OPT_FS_SEGMENTS (one rank): each chain's windows in that many segments, walked at once
     from the refined guesses and joined in order by k_fs_segfix (a segment whose guess missed its
