@@ -819,7 +819,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
                         rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
                         walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol, &repairs,
-                        c->opt.fs_segments, walk_ev(4), walk_ev(5));
+                        c->opt.fs_segments, walk_ev(4), walk_ev(5), c->opt.fs_join);
       } else {
         c->inl_xyz.ensure(3 * (size_t)std::max<int64_t>(src.n, 1));
         stage_wait();
@@ -828,7 +828,7 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
         launch_fs_refit(c->inl_xyz.p, c->inl_xyz.p + 1, c->inl_xyz.p + 2, 3, c->totals.p, src.n,
                         c->fs_b, bc_dev, rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(),
                         walk_ev(0), walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol,
-                        &repairs, c->opt.fs_segments, walk_ev(4), walk_ev(5));
+                        &repairs, c->opt.fs_segments, walk_ev(4), walk_ev(5), c->opt.fs_join);
       }
       HIPCHK(hipGetLastError());
       if (xs) xs->refit_repairs += repairs;
@@ -1839,7 +1839,8 @@ dlg_status dlg_float_sums(dlg_ctx* c, const float* xyz, int64_t n, const float c
       HIPCHK(hipEventRecord(c->ev[0], c->stream));
       launch_fs_refit(dx.p, dx.p + 1, dx.p + 2, 3, dn.p, std::max<int64_t>(n, 1), b, dc.p,
                       dc.p + 1, dres.p, c->num_cus, c->stream, nullptr, nullptr, nullptr, nullptr,
-                      nullptr, 0, nullptr, c->opt.fs_segments);
+                      nullptr, 0, nullptr, c->opt.fs_segments, nullptr, nullptr,
+                      c->opt.fs_join);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev[1], c->stream));
       sync(c);
@@ -1967,6 +1968,7 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         if (value < 0 || value > 1) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_SPATIAL_CURVE: 0 or 1");
         o.spatial_curve = (int)value;
         break;
+      case DLG_OPT_FS_JOIN: o.fs_join = value != 0; break;
       case DLG_OPT_FS_SEGMENTS:
         if (value < 1 || value > kFsSegMax) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_SEGMENTS: 1..16");
         o.fs_segments = (int)value;
@@ -2012,6 +2014,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_SEL1_TICKET: *value = o.sel1_ticket; break;
     case DLG_OPT_BOUNDS_STREAM: *value = o.bounds_stream; break;
     case DLG_OPT_SPATIAL_CURVE: *value = o.spatial_curve; break;
+    case DLG_OPT_FS_JOIN: *value = o.fs_join; break;
     case DLG_OPT_FS_ONE_WALK: *value = o.fs_protocol; break;
     case DLG_OPT_FS_SEGMENTS: *value = o.fs_segments; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;

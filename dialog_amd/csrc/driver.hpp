@@ -192,6 +192,7 @@ struct PathOptions {
   bool bounds_stream = false;  // DLG_OPT_BOUNDS_STREAM: lean rounds' survivor sphere bounds on a
                                // second stream beside the list pass (event-ordered)
   int spatial_curve = 1;  // DLG_OPT_SPATIAL_CURVE: 1 Hilbert, 0 Morton order of the spatial copy
+  bool fs_join = true;    // DLG_OPT_FS_JOIN: segmented walk's joins by each chain's last walker
 };
 
 struct dlg_ctx {

@@ -1271,6 +1271,9 @@ __device__ bool fs_walk_span(const FsDev& d, int c, int64_t w_lo, int64_t w_hi, 
 // The last chain to finish runs the refit tail when asked.
 constexpr int kFwBS = kWave;
 constexpr int kFwGuess = 1, kFwRecord = 2;  // k_fs_walk's mode bits
+// segmented walk: the last of a chain's segment walkers to finish joins the chain's segments
+// itself (k_fs_segfix's body) instead of a separate k_fs_segfix launch
+constexpr int kFwJoin = 4;
 constexpr int kFwSegShift = 8;               // mode >> kFwSegShift: segments per chain (> 1)
 // segments a chain's NW windows are walked in (at most S, at least kFsSegWin windows each)
 __device__ __forceinline__ int fs_seg_count(int64_t NW, int S) {
@@ -1280,6 +1283,11 @@ __device__ __forceinline__ int fs_seg_count(int64_t NW, int S) {
 __device__ void fs_walk_finish(const FsDev& d, int c, float t, int lane, int64_t n,
                                const float4* __restrict__ cin, float4* __restrict__ cout,
                                int32_t* __restrict__ res);
+__device__ void fs_seg_join(const FsDev& d, int c, const float* __restrict__ start9, int S,
+                            const float4* __restrict__ cin, float4* __restrict__ cout,
+                            int32_t* __restrict__ res, int lane,
+                            __attribute__((address_space(3))) char* ring,
+                            __attribute__((address_space(3))) uint64_t* tl);
 __device__ __forceinline__ void fs_put_counters(const FsDev& d, int c, const FsWalkCounters& ct,
                                                 int64_t clk0, bool add) {
   int64_t* w = d.b.wst + 8 * c;
@@ -1346,6 +1354,20 @@ __global__ __launch_bounds__(kFwBS) void k_fs_walk(FsDev d, const float* __restr
       d.b.seg[(c * kFsSegMax + sg) * 2] = t0;
       d.b.seg[(c * kFsSegMax + sg) * 2 + 1] = t;
     }
+    if (!(mode & kFwJoin)) return;
+    // the chain's last segment to finish joins them (one wave per workgroup: the release fence
+    // waits for every lane's stores -- the segment's (start, end) and its recorded window
+    // entries -- before the arrival; the joiner's acquire fence drops its stale L1 lines)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    unsigned arrived = 0;
+    if (lane == 0)
+      arrived = __hip_atomic_fetch_add(d.b.ticket + 2 + c, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    arrived = __builtin_amdgcn_readfirstlane(arrived);
+    if (arrived != (unsigned)fs_seg_count(NW, S) - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane == 0) d.b.ticket[2 + c] = 0u;  // (zero again for the next launch)
+    fs_seg_join(d, c, start9, S, cin, cout, res, lane, ring, tl);
     return;
   }
   fs_walk_finish(d, c, t, lane, n, cin, cout, res);
@@ -1431,15 +1453,11 @@ __global__ void k_fs_guess2(const float* __restrict__ gath2, int rank, float* __
 // later segment whose recorded start equals the exact end of the one before was exact itself,
 // else it is walked again from that end until it meets its recorded walk (k_fs_repair's rule).
 // Then as k_fs_walk's end: sums, and the last chain to finish runs the refit tail.
-__global__ __launch_bounds__(kFwBS) void k_fs_segfix(FsDev d, const float* __restrict__ start9,
-                                                     int S, const float4* __restrict__ cin,
-                                                     float4* __restrict__ cout,
-                                                     int32_t* __restrict__ res) {
-  __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
-  __shared__ uint64_t tl_raw[kFtLdsWords];
-  auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
-  auto* tl = (__attribute__((address_space(3))) uint64_t*)tl_raw;
-  const int c = blockIdx.x, lane = threadIdx.x;
+__device__ void fs_seg_join(const FsDev& d, int c, const float* __restrict__ start9, int S,
+                            const float4* __restrict__ cin, float4* __restrict__ cout,
+                            int32_t* __restrict__ res, int lane,
+                            __attribute__((address_space(3))) char* ring,
+                            __attribute__((address_space(3))) uint64_t* tl) {
   const int64_t n = *d.n_dev;
   const int64_t NW = (fs_chunks(n) + kWave - 1) / kWave;
   const float* sg = d.b.seg + c * kFsSegMax * 2;
@@ -1458,6 +1476,18 @@ __global__ __launch_bounds__(kFwBS) void k_fs_segfix(FsDev d, const float* __res
     }
   }
   fs_walk_finish(d, c, t, lane, n, cin, cout, res);
+}
+
+// (DLG_OPT_FS_JOIN 0: the joins as their own launch, one wave per chain -- round 5's form)
+__global__ __launch_bounds__(kFwBS) void k_fs_segfix(FsDev d, const float* __restrict__ start9,
+                                                     int S, const float4* __restrict__ cin,
+                                                     float4* __restrict__ cout,
+                                                     int32_t* __restrict__ res) {
+  __shared__ __attribute__((aligned(16))) char ring_raw[2 * kFsSlotBytes];
+  __shared__ uint64_t tl_raw[kFtLdsWords];
+  auto* ring = (__attribute__((address_space(3))) char*)ring_raw;
+  auto* tl = (__attribute__((address_space(3))) uint64_t*)tl_raw;
+  fs_seg_join(d, (int)blockIdx.x, start9, S, cin, cout, res, (int)threadIdx.x, ring, tl);
 }
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -1517,7 +1547,8 @@ FsBuffers fs_carve(void* base, int64_t n_cap, int world) {
   p += align256(sizeof(uint2) * U * kFsChains * kFtW);
   b.wq = reinterpret_cast<uint2*>(p);
   p += align256(sizeof(uint2) * U * kFsChains);
-  b.ticket = reinterpret_cast<unsigned*>(p);  // [0]: k_fs_prep / k_fs_inc, [1]: k_fs_walk
+  b.ticket = reinterpret_cast<unsigned*>(p);  // [0]: k_fs_prep / k_fs_inc, [1]: k_fs_walk,
+                                              // [2 + c]: chain c's segments done (kFwJoin)
   return b;
 }
 
@@ -1541,7 +1572,7 @@ hipError_t fs_reset(const FsBuffers& b, hipStream_t s, bool poison) {
   }
   hipError_t e = hipMemsetAsync(b.wtab, 0, sizeof(uint2) * (size_t)nt, s);
   if (e == hipSuccess) e = hipMemsetAsync(b.wq, 0, sizeof(uint2) * (size_t)nq, s);
-  if (e == hipSuccess) e = hipMemsetAsync(b.ticket, 0, 2 * sizeof(unsigned), s);
+  if (e == hipSuccess) e = hipMemsetAsync(b.ticket, 0, (2 + kFsChains) * sizeof(unsigned), s);
   return e;
 }
 
@@ -1550,7 +1581,7 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      float4* cout, int32_t* res, int num_cus, hipStream_t s, Comm* comm,
                      hipEvent_t ev_walk0, hipEvent_t ev_walk1, hipEvent_t ev_rep0,
                      hipEvent_t ev_rep1, int protocol, int* repairs, int segments,
-                     hipEvent_t ev_mid0, hipEvent_t ev_mid1) {
+                     hipEvent_t ev_mid0, hipEvent_t ev_mid1, bool fused_join) {
   uint32_t gen = ++s_gen;
   if (gen == 0) gen = ++s_gen;  // (0 marks a dropped table entry)
   FsDev d{px, py, pz, stride, n_dev, b, gen};
@@ -1569,7 +1600,14 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
     hipLaunchKernelGGL(k_fs_l1, dim3(gl), dim3(kFlBS), 0, s, d);
     const int S = std::min(std::max(segments, 1), kFsSegMax);
     if (S > 1) {
-      // segmented: kFsChains x S walkers (+ the table builders), then the joins
+      // segmented: kFsChains x S walkers (+ the table builders), then the joins -- by each
+      // chain's last segment walker (fused_join), or as a launch of their own
+      if (fused_join) {
+        DLG_LAUNCH_EV(k_fs_walk, dim3(gw + kFsChains * (S - 1)), dim3(kFwBS), 0, s, ev_walk0,
+                              ev_walk1, d, (const float*)nullptr, S << kFwSegShift | kFwJoin, cin,
+                              cout, res);
+        return;
+      }
       DLG_LAUNCH_EV(k_fs_walk, dim3(gw + kFsChains * (S - 1)), dim3(kFwBS), 0, s, ev_walk0,
                             nullptr, d, (const float*)nullptr, S << kFwSegShift,
                             (const float4*)nullptr, (float4*)nullptr, (int32_t*)nullptr);

@@ -267,7 +267,8 @@ void launch_fs_refit(const float* px, const float* py, const float* pz, int stri
                      hipEvent_t ev_walk0 = nullptr, hipEvent_t ev_walk1 = nullptr,
                      hipEvent_t ev_rep0 = nullptr, hipEvent_t ev_rep1 = nullptr,
                      int protocol = 0, int* repairs = nullptr, int segments = 1,
-                     hipEvent_t ev_mid0 = nullptr, hipEvent_t ev_mid1 = nullptr);
+                     hipEvent_t ev_mid0 = nullptr, hipEvent_t ev_mid1 = nullptr,
+                     bool fused_join = true);
 
 // device fast refit: cout = refit_exact of the summed digits, or cin when optimize == 0 or fewer
 // than 4 inliers

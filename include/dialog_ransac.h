@@ -43,7 +43,7 @@ extern "C" {
  * the tile-scorer option's getter returns the value set.
  * 5: a failing rank aborts its group (peers return DLG_ERR_COMM); DLG_OPT_FAULT_INJECT,
  * DLG_OPT_SYNC_CHECK, DLG_OPT_COMM_TIMEOUT_MS, DLG_OPT_SEL1_TICKET, DLG_OPT_BOUNDS_STREAM;
- * DLG_OPT_SPATIAL_CURVE (same ABI version: an added option);
+ * DLG_OPT_SPATIAL_CURVE, DLG_OPT_FS_JOIN (same ABI version: added options);
  * DLG_OPT_HYP_SHARD defaults to -1 (automatic); dlg_shard_range */
 #define DLG_ABI_VERSION 5
 
@@ -506,11 +506,15 @@ enum {
                                always, 0 never */
   DLG_OPT_BOUNDS_STREAM = 20, /* lean rounds: 1 = the survivors' sphere bounds on a second stream
                                beside the list pass (event-ordered both ways); 0 (default) */
-  DLG_OPT_SPATIAL_CURVE = 21 /* the spatial copy's point order (tiles of 32 consecutive points):
+  DLG_OPT_SPATIAL_CURVE = 21, /* the spatial copy's point order (tiles of 32 consecutive points):
                                1 (default) = Hilbert curve, 0 = Morton (Z-order, rounds 1-5).
                                Same results either way; Hilbert tiles are more compact (no Z
                                jumps inside a tile), so fewer (tile, plane) pairs pass the
                                sphere tests.  Applies to clouds built after the change */
+  DLG_OPT_FS_JOIN = 22       /* one rank, PCL float refit, segmented walk: 1 (default) = the last
+                               of a chain's segment walkers to finish joins the chain's segments in
+                               the walk's own launch; 0 = the joins as a launch of their own
+                               (round 5).  Same sums either way */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1, DLG_TILE_MFMA = 2 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };

@@ -119,17 +119,22 @@ def test_device_sums_poisoned_tables(fs):
         ctx.close()
 
 
-@pytest.mark.parametrize("segments", [1, 2, 5, 8, 16])
-def test_device_sums_segments(fs, segments):
+@pytest.mark.parametrize("segments,join", [(1, 1), (2, 1), (4, 1), (5, 1), (8, 1), (16, 1),
+                                           (4, 0), (8, 0)])
+def test_device_sums_segments(fs, segments, join):
     """DLG_OPT_FS_SEGMENTS (one rank): each chain's windows in that many segments, walked at once
-    from the refined guesses and joined in order by k_fs_segfix (a segment whose guess missed its
-    exact start is walked again until it meets its recorded walk).  Every segmentation gives the
-    literal loop's sums: hovering and quantised sequences (the guesses miss) and C3's planes."""
+    from the refined guesses and joined in order (a segment whose guess missed its exact start is
+    walked again until it meets its recorded walk) -- by each chain's last segment walker in the
+    walk's launch (DLG_OPT_FS_JOIN 1, the default) or by k_fs_segfix (0).  Every segmentation
+    gives the literal loop's sums: hovering and quantised sequences (the guesses miss) and C3's
+    planes."""
     ctx = D.Context(0)
     try:
+        assert ctx.get_option(D.DLG_OPT_FS_JOIN) == 1
         ctx.set_option(D.DLG_OPT_FS_SEGMENTS, segments)
+        ctx.set_option(D.DLG_OPT_FS_JOIN, join)
         assert ctx.get_option(D.DLG_OPT_FS_SEGMENTS) == segments
-        rng = np.random.default_rng(500 + segments)
+        rng = np.random.default_rng(500 + segments + 100 * join)
         for kind in ("hover", "quant", "alternating", "mags", "drift"):
             for n in (4097, 70000, 600000):
                 xyz = np.ascontiguousarray(np.stack(gen(kind, n, rng), axis=1))
