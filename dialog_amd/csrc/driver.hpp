@@ -179,7 +179,7 @@ struct PathOptions {
                        // batch's hypotheses, the counts are allreduced (DLG_OPT_HYP_SHARD: 1 on,
                        // 0 off, -1 = on when every rank holds the same cloud, ids included)
   int fs_protocol = 0;  // several ranks: the PCL refit's protocol (DLG_OPT_FS_ONE_WALK, 0..2)
-  int fs_segments = 4;  // one rank: walkers per float chain (DLG_OPT_FS_SEGMENTS; round 5: 8)
+  int fs_segments = 8;  // one rank: walkers per float chain (DLG_OPT_FS_SEGMENTS)
   bool fs_poison = false;  // tests only: fill the float-sum walk's window tables with garbage
                            // entries stamped for the next launch before the clear (fs_reset)
   int fault_round = 0;     // tests only (DLG_OPT_FAULT_INJECT): > 0 = this rank throws in the

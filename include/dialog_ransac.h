@@ -482,7 +482,7 @@ enum {
                                parallel repair iterations and host checks instead of the
                                hand-over (tests and A/B only) */
   DLG_OPT_FS_SEGMENTS = 15, /* one rank, PCL float refit: walkers per float chain, 1..16 (default
-                               4; round 5: 8): the chain's windows in segments walked at once from the refined
+                               8): the chain's windows in segments walked at once from the refined
                                guesses, then joined in order (a segment whose guess was not its
                                exact start is walked again until it meets its recorded walk); 1 =
                                one walker per chain.  Same sums every way */
