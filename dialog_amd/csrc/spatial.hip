@@ -99,85 +99,12 @@ __global__ void k_gather_order(const float4* __restrict__ src, const int32_t* __
 // inflated by 2^-18 (covers the few roundings of the distance evaluation).  Super sphere: centre
 // = midpoint of the super box, radius = max over its tiles of |c_t - C| + r_t, inflated the same
 // way.
-// k_sphere_bounds2: one lane per tile.  A wave stages 64 tiles (2048
-// points, two super-tiles) in LDS with coalesced loads (padded rows: lane l reads row l without
-// bank conflicts), each lane reduces its tile's box and radius, then the 32 lanes of a super-tile
-// combine their spheres.  ~4x less VALU work than a half-wave per tile.
-constexpr int kSb2Pts = kWave * kTileP;  // points per wave (64 tiles)
-constexpr int kSb2Sup = kWave / kSuperTiles;  // super-tiles per wave
-__global__ __launch_bounds__(64) void k_sphere_bounds2(const float* __restrict__ X,
-                                                       const float* __restrict__ Y,
-                                                       const float* __restrict__ Z, int64_t n_arg,
-                                                       const int32_t* __restrict__ n_dev,
-                                                       float4* __restrict__ tiles,
-                                                       float4* __restrict__ supers) {
-  __shared__ float s_p[3][kSb2Pts + kSb2Pts / kTileP];  // row t: 33 floats
-  const int64_t n = n_dev ? (int64_t)*n_dev : n_arg;
-  const int lane = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kSb2Pts;
-  if (base >= n) return;
-  const int cnt = (int)min<int64_t>(kSb2Pts, n - base);
-  // all 96 loads in flight before the first LDS store (clamped, unconditional: a guarded load
-  // per point is a branch, and the compiler waits for each before the next)
-  constexpr int kPer = kSb2Pts / kWave;
-  float vx[kPer], vy[kPer], vz[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int64_t e = base + min(k * kWave + lane, cnt - 1);
-    vx[k] = X[e]; vy[k] = Y[e]; vz[k] = Z[e];
-  }
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = k * kWave + lane, r = i + i / kTileP;
-    s_p[0][r] = vx[k]; s_p[1][r] = vy[k]; s_p[2][r] = vz[k];
-  }
-  __syncthreads();
-  const int np = min(kTileP, cnt - lane * kTileP);  // this lane's tile size (<= 0: none)
-  const float* px = &s_p[0][lane * (kTileP + 1)];
-  const float* py = &s_p[1][lane * (kTileP + 1)];
-  const float* pz = &s_p[2][lane * (kTileP + 1)];
-  float x0 = INFINITY, y0 = INFINITY, z0 = INFINITY, x1 = -INFINITY, y1 = -INFINITY, z1 = -INFINITY;
-  for (int i = 0; i < np; ++i) {
-    const float x = px[i], y = py[i], z = pz[i];
-    x0 = fminf(x0, x); y0 = fminf(y0, y); z0 = fminf(z0, z);
-    x1 = fmaxf(x1, x); y1 = fmaxf(y1, y); z1 = fmaxf(z1, z);
-  }
-  const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), cz = 0.5f * (z0 + z1);
-  float d = 0.0f;
-  for (int i = 0; i < np; ++i) {
-    const float dx = px[i] - cx, dy = py[i] - cy, dz = pz[i] - cz;
-    d = fmaxf(d, sqrtf(dx * dx + dy * dy + dz * dz));
-  }
-  const float rt = d * (1.0f + 0x1p-18f) + 1e-30f;
-  const int64_t t = (int64_t)blockIdx.x * (kSb2Pts / kTileP) + lane;
-  if (np > 0) tiles[t] = make_float4(cx, cy, cz, rt);
-  // super-tile of each kSuperTiles lanes: box over its tiles, then max |c_t - C| + r_t
-  float bx0 = x0, by0 = y0, bz0 = z0, bx1 = x1, by1 = y1, bz1 = z1;
-#pragma unroll
-  for (int o = 1; o < kSuperTiles; o <<= 1) {
-    bx0 = fminf(bx0, __shfl_xor(bx0, o)); by0 = fminf(by0, __shfl_xor(by0, o));
-    bz0 = fminf(bz0, __shfl_xor(bz0, o));
-    bx1 = fmaxf(bx1, __shfl_xor(bx1, o)); by1 = fmaxf(by1, __shfl_xor(by1, o));
-    bz1 = fmaxf(bz1, __shfl_xor(bz1, o));
-  }
-  const float Cx = 0.5f * (bx0 + bx1), Cy = 0.5f * (by0 + by1), Cz = 0.5f * (bz0 + bz1);
-  float R = 0.0f;
-  if (np > 0) {
-    const float dx = cx - Cx, dy = cy - Cy, dz = cz - Cz;
-    R = sqrtf(dx * dx + dy * dy + dz * dz) + rt;
-  }
-#pragma unroll
-  for (int o = 1; o < kSuperTiles; o <<= 1) R = fmaxf(R, __shfl_xor(R, o));
-  const int sub = lane / kSuperTiles;
-  if ((lane % kSuperTiles) == 0 && sub * kSuperP < cnt)
-    supers[(int64_t)blockIdx.x * kSb2Sup + sub] = make_float4(Cx, Cy, Cz, R * (1.0f + 0x1p-18f) + 1e-30f);
-}
-
-// k_sphere_bounds3: the same spheres, two lanes per tile (lane l: tile l & 31, points
-// 16 (l >> 5) .. + 16), 32 tiles (two super-tiles) a wave: half the LDS staging of
-// k_sphere_bounds2 (12.4 KB a workgroup: 12 workgroups per CU instead of 6) and half the serial
-// work per lane.  min / max are exact in any order, so the tile boxes, centres and radii (max of
-// the same per-point distances) are bit for bit k_sphere_bounds2's.
+// k_sphere_bounds3: two lanes per tile (lane l: tile l & 31, points 16 (l >> 5) .. + 16), 32
+// tiles (two super-tiles) a wave staged in LDS with coalesced loads (padded rows: no bank
+// conflicts), the two halves' boxes and radii combined by one shuffle, then the 16 lanes of a
+// super-tile combine their spheres.  (Round 5's k_sphere_bounds2 took one lane per tile and 64
+// tiles a wave: 25 KB of LDS a workgroup, 6 workgroups per CU, 20.5 us per round at C3 against
+// 17.8 here; min / max are exact in any order, so the spheres are the same bit for bit.)
 constexpr int kSb3Tiles = 32;
 constexpr int kSb3Pts = kSb3Tiles * kTileP;  // points per wave (32 tiles)
 __global__ __launch_bounds__(64) void k_sphere_bounds3(const float* __restrict__ X,
