@@ -20,7 +20,7 @@ from ._lib import (DLG_OPT_LEAN_ROUNDS, DLG_OPT_PCL_REFIT_DEVICE, DLG_OPT_PRUNE,
                    DLG_OPT_PRUNE_STATS, DLG_OPT_SCORE_KERNEL, DLG_OPT_SELECT_TILE,
                    DLG_OPT_REGULATE_WAVE, DLG_OPT_SPEC_PICK, DLG_OPT_FS_POISON, DLG_OPT_HYP_SHARD, DLG_OPT_FS_ONE_WALK, DLG_OPT_FS_SEGMENTS,
                    DLG_OPT_FAULT_INJECT, DLG_OPT_SYNC_CHECK, DLG_OPT_COMM_TIMEOUT_MS, DLG_OPT_SEL1_TICKET,
-                   DLG_OPT_BOUNDS_STREAM, DLG_OPT_SPATIAL_CURVE, DLG_OPT_FS_JOIN, DLG_ERR_COMM, DLG_ERR_INTERNAL, DLG_SCORE_BF16,
+                   DLG_OPT_BOUNDS_STREAM, DLG_OPT_SPATIAL_CURVE, DLG_OPT_FS_JOIN, DLG_OPT_UNREFINED_LIST, DLG_ERR_COMM, DLG_ERR_INTERNAL, DLG_SCORE_BF16,
                    DLG_SCORE_EXACT, DLG_SCORE_PRUNED)
 
 __all__ = ["Context", "Cloud", "SACSegmentation", "extract_planes", "segment_cloud", "make_params",

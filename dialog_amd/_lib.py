@@ -59,6 +59,7 @@ DLG_OPT_SEL1_TICKET = 19
 DLG_OPT_BOUNDS_STREAM = 20
 DLG_OPT_SPATIAL_CURVE = 21
 DLG_OPT_FS_JOIN = 22
+DLG_OPT_UNREFINED_LIST = 23
 DLG_TILE_EXACT = 0
 DLG_TILE_BF16 = 1
 DLG_TILE_MFMA = 2

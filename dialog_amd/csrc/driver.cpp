@@ -793,29 +793,37 @@ SegOut segment_impl(dlg_ctx* c, dlg_cloud* cl, const dlg_sac_params& prm, bool c
       int32_t* fs_res = reinterpret_cast<int32_t*>(c->small.p + 8);
       int repairs = 0;
       if (lean) {
-        // inliers stamped into a bitmap over pristine indices from the Morton copy's near tiles,
-        // compacted in ascending pristine order = list order
+        // the unrefined plane's inliers' x, y, z in list order (= ascending pristine order):
+        // one pass over the active list (k_ulist), or (DLG_OPT_UNREFINED_LIST 0) stamped into a
+        // bitmap over pristine indices from the Morton copy's near tiles and compacted from it
         const int64_t nw = (cl->n_total + 31) / 32;
-        if (cl->ubits.cap < (size_t)nw + 16 || cl->ubits_dirty) {
-          // (new, or left stamped by an extraction that failed between the stamp and the
-          // compaction, which clears every word it reads)
-          cl->ubits.ensure((size_t)nw + 16);
-          HIPCHK(hipMemsetAsync(cl->ubits.p, 0, cl->ubits.cap * sizeof(uint32_t), c->stream));
-          cl->ubits_dirty = false;
-        }
-        ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n), ucompact_tiles(nw));
         c->fs_x.ensure((size_t)std::max<int64_t>(src.n, 1));
         c->fs_y.ensure((size_t)std::max<int64_t>(src.n, 1));
         c->fs_z.ensure((size_t)std::max<int64_t>(src.n, 1));
         c->fs_n.ensure(1);
-        const SpatialView sv = spatial_view(cl);
-        cl->ubits_dirty = true;
-        launch_ustamp(sp_cur_view(), sv.tiles, sv.supers, pmargin, bc_dev, mt, cl->ubits.p,
-                      c->stream);
-        launch_ucompact(cl->ubits.p, nw, cl->pristine.view(cl->n_total), c->sel1, c->fs_x.p,
-                        c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
-        HIPCHK(hipGetLastError());
-        cl->ubits_dirty = false;
+        if (c->opt.unrefined_list) {
+          ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n));
+          launch_ulist(lidx, src.n, cl->pristine.view(cl->n_total), bc_dev, mt, c->sel1,
+                       c->fs_x.p, c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
+          HIPCHK(hipGetLastError());
+        } else {
+          if (cl->ubits.cap < (size_t)nw + 16 || cl->ubits_dirty) {
+            // (new, or left stamped by an extraction that failed between the stamp and the
+            // compaction, which clears every word it reads)
+            cl->ubits.ensure((size_t)nw + 16);
+            HIPCHK(hipMemsetAsync(cl->ubits.p, 0, cl->ubits.cap * sizeof(uint32_t), c->stream));
+            cl->ubits_dirty = false;
+          }
+          ensure_sel1(c, std::max<int64_t>(src.n, cl->sp_n), ucompact_tiles(nw));
+          const SpatialView sv = spatial_view(cl);
+          cl->ubits_dirty = true;
+          launch_ustamp(sp_cur_view(), sv.tiles, sv.supers, pmargin, bc_dev, mt, cl->ubits.p,
+                        c->stream);
+          launch_ucompact(cl->ubits.p, nw, cl->pristine.view(cl->n_total), c->sel1, c->fs_x.p,
+                          c->fs_y.p, c->fs_z.p, c->fs_n.p, c->stream);
+          HIPCHK(hipGetLastError());
+          cl->ubits_dirty = false;
+        }
         launch_fs_refit(c->fs_x.p, c->fs_y.p, c->fs_z.p, 1, c->fs_n.p, src.n, c->fs_b, bc_dev,
                         rc_dev, fs_res, c->num_cus, c->stream, c->comm.get(), walk_ev(0),
                         walk_ev(1), walk_ev(2), walk_ev(3), c->opt.fs_protocol, &repairs,
@@ -1969,6 +1977,7 @@ dlg_status dlg_ctx_set_option(dlg_ctx* c, int option, int64_t value) {
         o.spatial_curve = (int)value;
         break;
       case DLG_OPT_FS_JOIN: o.fs_join = value != 0; break;
+      case DLG_OPT_UNREFINED_LIST: o.unrefined_list = value != 0; break;
       case DLG_OPT_FS_SEGMENTS:
         if (value < 1 || value > kFsSegMax) throw DlgError(DLG_ERR_INVALID, "DLG_OPT_FS_SEGMENTS: 1..16");
         o.fs_segments = (int)value;
@@ -2015,6 +2024,7 @@ dlg_status dlg_ctx_get_option(const dlg_ctx* c, int option, int64_t* value) {
     case DLG_OPT_BOUNDS_STREAM: *value = o.bounds_stream; break;
     case DLG_OPT_SPATIAL_CURVE: *value = o.spatial_curve; break;
     case DLG_OPT_FS_JOIN: *value = o.fs_join; break;
+    case DLG_OPT_UNREFINED_LIST: *value = o.unrefined_list; break;
     case DLG_OPT_FS_ONE_WALK: *value = o.fs_protocol; break;
     case DLG_OPT_FS_SEGMENTS: *value = o.fs_segments; break;
     case DLG_OPT_PRUNE_TILE_SCORER: *value = o.tile_scorer; break;

@@ -193,6 +193,7 @@ struct PathOptions {
                                // second stream beside the list pass (event-ordered)
   int spatial_curve = 1;  // DLG_OPT_SPATIAL_CURVE: 1 Hilbert, 0 Morton order of the spatial copy
   bool fs_join = true;    // DLG_OPT_FS_JOIN: segmented walk's joins by each chain's last walker
+  bool unrefined_list = true;  // DLG_OPT_UNREFINED_LIST: lean PCL refit's inliers by one list pass
 };
 
 struct dlg_ctx {

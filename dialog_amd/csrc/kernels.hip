@@ -1103,6 +1103,61 @@ __global__ __launch_bounds__(kS1BS) void k_sel1_list(const int32_t* __restrict__
   }
 }
 
+// k_ulist (PCL refit in lean rounds, DLG_OPT_UNREFINED_PASS 1): the unrefined plane's inliers in
+// list order straight from the list -- lane-strided list entries (16 a lane), their pristine
+// coordinates gathered by index (ascending: coalesced while the list is dense), the model test,
+// and the single-pass look-back compaction of the inliers' x, y, z (as k_sel1_list / k_ucompact);
+// the last tile writes the count to *n_out.  The same inliers, in the same order, as k_ustamp +
+// k_ucompact (the Morton copy holds the same coordinates and runs the same test; the list is the
+// active points' pristine indices ascending), in one pass instead of two and without the
+// bitmap's scattered gather.
+template <bool IDENT, bool NP, int kS1BS>
+__global__ __launch_bounds__(kS1BS) void k_ulist(const int32_t* __restrict__ lidx, int64_t n,
+                                                 PointsView pristine,
+                                                 const float4* __restrict__ cfp, ModelTest mt,
+                                                 Sel1State L, int ntiles, float* __restrict__ ox,
+                                                 float* __restrict__ oy, float* __restrict__ oz,
+                                                 int32_t* __restrict__ n_out) {
+  constexpr int kS1Slots = S1<kS1BS>::kSlots, kS1Tile = S1<kS1BS>::kTile;
+  __shared__ int s_cnt[kS1Slots], s_pre[kS1Slots], s_base[2];
+  const int tile = sel1_tile_of(L, s_base);
+  const float4 cf = *cfp;
+  const float4 cn = eigen_normalized3(cf.x, cf.y, cf.z, 0.0f);
+  const int w = threadIdx.x / kWave;
+  const int64_t base = (int64_t)tile * kS1Tile;
+  int32_t p[kS1It];
+  float x[kS1It], y[kS1It], z[kS1It];
+  uint64_t m[kS1It];
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = min<int64_t>(base + j * kS1BS + threadIdx.x, n - 1);
+    p[j] = IDENT ? (int32_t)e : lidx[e];
+  }
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    x[j] = pristine.x[p[j]]; y[j] = pristine.y[p[j]]; z[j] = pristine.z[p[j]];
+  }
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = base + j * kS1BS + threadIdx.x;
+    const bool in = e < n && model_in<NP>(pristine, p[j], cf, cn, mt, x[j], y[j], z[j]);
+    m[j] = ballot(in);
+    if ((threadIdx.x & (kWave - 1)) == 0) s_cnt[j * (kS1BS / kWave) + w] = __popcll(m[j]);
+  }
+  const int excl = sel1_scan<kS1BS>(L, tile, s_cnt, s_pre, s_base);
+  if (excl < 0) return;  // (look-back failed: *L.err is set)
+#pragma unroll
+  for (int j = 0; j < kS1It; ++j) {
+    const int64_t e = base + j * kS1BS + threadIdx.x;
+    if (e >= n) break;
+    if ((m[j] >> (threadIdx.x & (kWave - 1))) & 1ull) {
+      const int o = excl + s_pre[j * (kS1BS / kWave) + w] + lanes_below(m[j]);
+      ox[o] = x[j]; oy[o] = y[j]; oz[o] = z[j];
+    }
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) *n_out = excl + s_base[1];
+}
+
 __global__ void k_sel1_empty(int64_t n_list, int32_t* totals) {
   totals[0] = 0;
   totals[1] = (int32_t)n_list;
@@ -1522,6 +1577,22 @@ void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, flo
   // (NORMAL_PLANE: the model test reads the copy's normals, sp.nrm; margin = the NP prune margin)
   hipLaunchKernelGGL(mt.normal_plane ? k_ustamp<true> : k_ustamp<false>, dim3(g), dim3(kMoBS), 0, s,
                      sp, tiles, supers, margin, coef, mt, bits);
+}
+
+void launch_ulist(const int32_t* lidx, int64_t n, PointsView pristine, const float4* coef,
+                  const ModelTest& mt, Sel1State& L, float* ox, float* oy, float* oz,
+                  int32_t* n_out, hipStream_t s) {
+  constexpr int kBS = 1024;
+  const int nt = (int)((n + kBS * kS1It - 1) / (kBS * kS1It));
+  if (nt == 0) {
+    (void)hipMemsetAsync(n_out, 0, sizeof(int32_t), s);
+    return;
+  }
+  sel1_next(L, nt);
+  auto* k = lidx ? (mt.normal_plane ? k_ulist<false, true, kBS> : k_ulist<false, false, kBS>)
+                 : (mt.normal_plane ? k_ulist<true, true, kBS> : k_ulist<true, false, kBS>);
+  hipLaunchKernelGGL(k, dim3(nt), dim3(kBS), 0, s, lidx, n, pristine, coef, mt, L, nt, ox, oy, oz,
+                     n_out);
 }
 
 int ucompact_tiles(int64_t nwords) { return (int)((nwords + kUcBS * kUcWords - 1) / (kUcBS * kUcWords)); }

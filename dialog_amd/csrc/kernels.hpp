@@ -198,6 +198,11 @@ void launch_moments_sp(PointsView src, const float4* tiles, const float4* supers
 void launch_ustamp(PointsView sp, const float4* tiles, const float4* supers, float margin,
                    const float4* coef, const ModelTest& mt, uint32_t* bits, hipStream_t s);
 int ucompact_tiles(int64_t nwords);
+// the unrefined plane's inliers' x, y, z in list order in one list pass (lidx null: the pristine
+// list); count to *n_out (k_ulist)
+void launch_ulist(const int32_t* lidx, int64_t n, PointsView pristine, const float4* coef,
+                  const ModelTest& mt, Sel1State& L, float* ox, float* oy, float* oz,
+                  int32_t* n_out, hipStream_t s);
 void launch_ucompact(uint32_t* bits, int64_t nwords, PointsView pristine, Sel1State& L, float* ox,
                      float* oy, float* oz, int32_t* n_out, hipStream_t s);
 

@@ -43,7 +43,7 @@ extern "C" {
  * the tile-scorer option's getter returns the value set.
  * 5: a failing rank aborts its group (peers return DLG_ERR_COMM); DLG_OPT_FAULT_INJECT,
  * DLG_OPT_SYNC_CHECK, DLG_OPT_COMM_TIMEOUT_MS, DLG_OPT_SEL1_TICKET, DLG_OPT_BOUNDS_STREAM;
- * DLG_OPT_SPATIAL_CURVE, DLG_OPT_FS_JOIN (same ABI version: added options);
+ * DLG_OPT_SPATIAL_CURVE, DLG_OPT_FS_JOIN, DLG_OPT_UNREFINED_LIST (same ABI version: added options);
  * DLG_OPT_HYP_SHARD defaults to -1 (automatic); dlg_shard_range */
 #define DLG_ABI_VERSION 5
 
@@ -511,10 +511,15 @@ enum {
                                Same results either way; Hilbert tiles are more compact (no Z
                                jumps inside a tile), so fewer (tile, plane) pairs pass the
                                sphere tests.  Applies to clouds built after the change */
-  DLG_OPT_FS_JOIN = 22       /* one rank, PCL float refit, segmented walk: 1 (default) = the last
+  DLG_OPT_FS_JOIN = 22,      /* one rank, PCL float refit, segmented walk: 1 (default) = the last
                                of a chain's segment walkers to finish joins the chain's segments in
                                the walk's own launch; 0 = the joins as a launch of their own
                                (round 5).  Same sums either way */
+  DLG_OPT_UNREFINED_LIST = 23 /* lean rounds, PCL float refit: the unrefined plane's inliers in
+                               list order by 1 (default) = one pass over the active list (k_ulist:
+                               pristine coordinates gathered by index, look-back compaction); 0 =
+                               stamps from the Morton copy's near tiles into a bitmap + its
+                               compaction (rounds 3-5).  Same inliers either way */
 };
 enum { DLG_TILE_EXACT = 0, DLG_TILE_BF16 = 1, DLG_TILE_MFMA = 2 };
 enum { DLG_SCORE_EXACT = 0, DLG_SCORE_BF16 = 1, DLG_SCORE_PRUNED = 2 };

@@ -49,8 +49,11 @@ def check(e, ref, tag):
     assert np.array_equal(e["inliers"], ref["inliers"]), tag
 
 
+# (DLG_OPT_UNREFINED_LIST 0: the lean rounds' unrefined inliers from the Morton copy's stamps and
+# the bitmap compaction instead of the default list pass)
 OPTS = [dict(), {D.DLG_OPT_LEAN_ROUNDS: 0}, {D.DLG_OPT_PCL_REFIT_DEVICE: 0},
-        {D.DLG_OPT_PCL_REFIT_DEVICE: 2}, {D.DLG_OPT_PCL_REFIT_DEVICE: 3}]
+        {D.DLG_OPT_PCL_REFIT_DEVICE: 2}, {D.DLG_OPT_PCL_REFIT_DEVICE: 3},
+        {D.DLG_OPT_UNREFINED_LIST: 0}]
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -103,7 +106,8 @@ def test_extract_pcl_adversarial_sums(case):
     prm = D.make_params(thr, **kw)
     # (DLG_OPT_FS_POISON: the window tables hold garbage stamped for the next launch until the
     # clear after the scratch is laid out; results unchanged)
-    for opts in (dict(), {D.DLG_OPT_LEAN_ROUNDS: 0}, {D.DLG_OPT_FS_POISON: 1}):
+    for opts in (dict(), {D.DLG_OPT_LEAN_ROUNDS: 0}, {D.DLG_OPT_FS_POISON: 1},
+                 {D.DLG_OPT_UNREFINED_LIST: 0}):
         check(extract(p, prm, opts, 6, 200), ref, (case, opts))
 
 
