@@ -480,17 +480,21 @@ def main():
                      + 16.0 * sum_active + 16.0 * surv + 1.0 * inliers_local
                      + 5.0 * sum_active + 4.0 * surv + 8.0 * inliers_local
                      + 12.0 * surv + 0.5 * surv)
-        if a.refit == "pcl":
-            # PCL refit instead of the moments: the stamp pass visits the same near tiles (the
-            # 12 B per inlier above), the inlier bitmap over pristine indices is written and read
-            # once per round, and the float-sum passes leave nine 64-byte chunk records (9 B per
-            # inlier).  Each inlier's coordinates count once: k_ucompact's gather from the
-            # pristine records and the float-sum passes' re-reads of the compacted list
-            # (k_fs_prep, k_fs_inc, k_fs_l1) are implementation traffic, not algorithmic bytes.
-            # The chains' walk (k_fs_walk: sequential, latency-bound) is timed on its own and
-            # left out of this phase.
+        if a.refit == "pcl" and "UNREFINED_LIST=0" in a.opt:
+            # PCL refit instead of the moments, round 5's form: the stamp pass visits the same
+            # near tiles (the 12 B per inlier above), the inlier bitmap over pristine indices is
+            # written and read once per round, and the float-sum passes leave nine 64-byte chunk
+            # records (9 B per inlier).  The float-sum passes' re-reads of the compacted list
+            # (k_fs_prep, k_fs_inc, k_fs_l1) are implementation traffic not counted here; the
+            # chains' walk (k_fs_walk: sequential, latency-bound) is timed on its own and left out
+            # of this phase.
             sel_bytes += (2.0 * per_rank_points_total / 8.0 * rounds_per_step * a.steps
                           + 9.0 * inliers_local)
+        elif a.refit == "pcl":
+            # PCL refit, round 6 (k_ulist): the unrefined inliers from one pass over the list
+            # (4 B index + 12 B coordinates per active point, 12 B per inlier written) instead of
+            # the near-tile moments' 12 B per inlier above; the chunk records as before
+            sel_bytes += 16.0 * sum_active + 9.0 * inliers_local
     else:
         n_copies = 2 if pruned else 1
         sel_bytes = (12.0 * sum_active + n_copies * (28.0 * sum_active + 16.0 * (sum_active - inliers_local))
@@ -507,7 +511,8 @@ def main():
     impl_gbs = sel_bytes / (mb_ms / 1e3) / 1e9 if mb_ms > 0 else 0.0
     roofline["memory_bound_passes"] = {
         "phase": "%s + selectWithinDistance + compaction (%s)"
-                 % ("PCL float refit (inlier bitmap, compaction, exact float sums, eigen33)"
+                 % ("PCL float refit (the unrefined inliers in list order, exact float sums, "
+                    "eigen33)"
                     if a.refit == "pcl" else "refit moments",
                     "lean rounds: single-pass select of the Morton copy + the index list from "
                     "the inlier stamps" if lean else
